@@ -1,0 +1,207 @@
+/*
+ * orbslam2_amd.h — C-ABI of the MI355X (gfx950) ORB front end + local BA.
+ *
+ * This is the drop-in boundary for the hot path of tiantianxuabc/ORB_SLAM2_Refactored
+ * (SURVEY.md §8b).  Every entry point cites the reference interface it replaces.
+ * Plain pointers and sizes only; no torch / OpenCV / Eigen types cross it.
+ *
+ *   status codes: 0 = ok, < 0 = error (orb_last_error() has a thread-local message)
+ *   host pointers  : functions without the _device suffix take host memory and are
+ *                    synchronous (the reference's calling convention).
+ *   device pointers: *_device functions take HBM pointers and a hipStream_t (void*);
+ *                    they only enqueue work (no host sync) unless stated.
+ */
+#ifndef ORBSLAM2_AMD_H
+#define ORBSLAM2_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORB_OK          0
+#define ORB_EINVAL     -1   /* bad argument (the reference throws cv::Exception via CV_Assert) */
+#define ORB_EHIP       -2   /* HIP runtime error */
+#define ORB_ENOMEM     -3
+#define ORB_ECAP       -4   /* caller's output capacity too small */
+#define ORB_EINTERNAL  -5   /* a device-side capacity / consistency check failed */
+
+/* ------------------------------------------------------------------------------------------
+ * Extractor.  Replaces ORB_SLAM2::ORBextractor (include/ORBextractor.h:35-81).
+ * ---------------------------------------------------------------------------------------- */
+
+/* == ORBextractor::Parameters (include/ORBextractor.h:39-47, defaults src/ORBextractor.cc:830-833) */
+typedef struct orbx_params {
+    int32_t nfeatures;    /* 2000 */
+    float   scaleFactor;  /* 1.2f */
+    int32_t nlevels;      /* 8 */
+    int32_t iniThFAST;    /* 20 */
+    int32_t minThFAST;    /* 7 */
+} orbx_params;
+
+/* Byte-compatible with cv::KeyPoint (28 B): pt.x, pt.y, size, angle, response, octave, class_id. */
+typedef struct orbx_keypoint {
+    float   x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbx_keypoint;
+
+typedef struct orbx_extractor orbx_extractor;
+
+/* ORBextractor(const Parameters&) + Init() (src/ORBextractor.cc:695-741).  device = HIP ordinal. */
+int orbx_create(const orbx_params* params, int device, orbx_extractor** out);
+int orbx_destroy(orbx_extractor* h);
+
+/* GetLevels/GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
+ * GetInverseScaleSigmaSquares (src/ORBextractor.cc:822-827) plus the per-level feature quota
+ * (ComputeNumFeaturesPerScale, :472-487).  Each array has nlevels entries; any may be NULL. */
+int orbx_scale_tables(const orbx_extractor* h, float* scale, float* inv_scale, float* sigma2,
+                      float* inv_sigma2, int32_t* features_per_level);
+
+/* Upper bound on keypoints Extract can return for an image of rows x cols (per-level
+ * quadtree output <= max(quota, 4*roots) + 3). */
+int orbx_max_keypoints(const orbx_extractor* h, int rows, int cols, int32_t* cap);
+
+/* void ORBextractor::Extract(const cv::Mat& image, KeyPoints& keypoints, cv::Mat& descriptors)
+ * (include/ORBextractor.h:55, src/ORBextractor.cc:743-820).  Host memory, synchronous.
+ * img: CV_8U rows x cols, row stride `step` bytes.  kps: cap entries; desc: cap x 32 bytes.
+ * On return *n = number of keypoints.  Reference quirk kept: when the image yields no keypoint
+ * at all *n = 0 and kps/desc are NOT written (Extract returns before keypoints.clear(), :778-782).
+ * Returns ORB_ECAP (and *n = required count) if cap is too small. */
+int orbx_extract(orbx_extractor* h, const uint8_t* img, int rows, int cols, size_t step,
+                 orbx_keypoint* kps, uint8_t* desc, int cap, int* n);
+
+/* GetImagePyramid() (src/ORBextractor.cc:828): copy level `level` of the last extracted image
+ * (frame 0 of the last batch) to host memory dst (row stride dst_step; NULL dst = query only). */
+int orbx_pyramid_level(const orbx_extractor* h, int level, uint8_t* dst, size_t dst_step,
+                       int* rows, int* cols);
+
+/* Batched, HBM-resident Extract over n_frames independent frames of identical size.
+ * d_imgs: frame f at d_imgs + f*frame_stride, rows of `step` bytes.
+ * Outputs per frame f: d_kps[f*cap .. ], d_desc[(f*cap)*32 .. ], d_counts[f].
+ * Keypoint/descriptor order per frame is the reference's (level-major, quadtree list order).
+ * Enqueue only (no host sync).  cap must be >= orbx_max_keypoints(). */
+int orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int n_frames, int rows,
+                              int cols, size_t frame_stride, size_t step, orbx_keypoint* d_kps,
+                              uint8_t* d_desc, int32_t* d_counts, int cap, void* stream);
+
+/* Device pointer to the batch's pyramid (frame f, level s) for downstream consumers
+ * (ComputeStereoMatches reads GetImagePyramid(), ORBmatcher.cc:165-166). */
+int orbx_pyramid_device(const orbx_extractor* h, int frame, int level, const uint8_t** ptr,
+                        int* rows, int* cols, size_t* step);
+
+/* ------------------------------------------------------------------------------------------
+ * Matcher.  Replaces the Hamming kernels of ORB_SLAM2::ORBmatcher (src/ORBmatcher.cc).
+ * ---------------------------------------------------------------------------------------- */
+
+/* static int ORBmatcher::DescriptorDistance(const cv::Mat&, const cv::Mat&)
+ * (include/ORBmatcher.h:54, src/ORBmatcher.cc:1449-1457).  Two 32-byte rows. */
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Brute-force best / second-best Hamming search with the reference's loop semantics
+ * (SearchByBoW inner loop, src/ORBmatcher.cc:477-498): for each query row i of A scan B in
+ * ascending j; best starts at 256 / idx -1, strict '<' updates (lowest j wins ties,
+ * second = 2nd order statistic).  Device pointers, enqueue only. */
+int orbm_hamming_top2_device(const uint8_t* d_A, int nA, const uint8_t* d_B, int nB,
+                             int32_t* d_best_idx, int32_t* d_best, int32_t* d_second, void* stream);
+
+/* Batched pairs: pair p matches A_p (rows d_A + p*strideA*32, count d_nA[p]) against
+ * B_p (d_B + p*strideB*32, count d_nB[p]).  Outputs at p*strideA.  Also applies the
+ * acceptance test of :500 when d_match != NULL: match = best_idx if best <= th_low and
+ * (float)best < nnratio * (float)second, else -1. */
+int orbm_bf_match_batch_device(const uint8_t* d_A, const int32_t* d_nA, int strideA,
+                               const uint8_t* d_B, const int32_t* d_nB, int strideB, int n_pairs,
+                               float nnratio, int th_low, int32_t* d_best_idx, int32_t* d_best,
+                               int32_t* d_second, int32_t* d_match, void* stream);
+
+/* Host-memory convenience form of the two above (synchronous). */
+int orbm_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float nnratio, int th_low,
+                  int32_t* best_idx, int32_t* best, int32_t* second, int32_t* match);
+
+/* One keyframe's view for SearchForTriangulation (src/ORBmatcher.cc:768-866). */
+typedef struct orbm_tri_frame {
+    int32_t        n;           /* keyframe->N */
+    const float*   kp_xy;       /* keypointsUn pt, n x 2 */
+    const int32_t* octave;      /* keypointsUn octave, n */
+    const float*   uright;      /* n (< 0: mono) */
+    const uint8_t* has_mappoint;/* GetMapPoint(idx) != nullptr, n (0/1) */
+    const uint8_t* desc;        /* descriptorsL, n x 32 */
+    /* DBoW2 FeatureVector as CSR: node ids ascending, node k owns
+     * indices[node_off[k] .. node_off[k+1]) (ascending feature indices). */
+    int32_t        n_nodes;
+    const uint32_t* node_id;
+    const int32_t* node_off;
+    const int32_t* indices;
+} orbm_tri_frame;
+
+/* int ORBmatcher::SearchForTriangulation(const KeyFrame* kf1, const KeyFrame* kf2,
+ *   const cv::Mat& F12, std::vector<std::pair<size_t,size_t>>& matchIds, bool onlyStereo)
+ * (include/ORBmatcher.h:84-85).  F12 row-major 3x3 (cv::Mat1f); ep2 = projection of kf1's
+ * camera centre in kf2 (:772-773); scale2/sigma2: kf2 pyramid scaleFactors / sigmaSq.
+ * Host memory.  match12[idx1] = idx2 or -1 (pairs sorted by idx1 are the non-negative
+ * entries); *nmatches = count.  checkOrientation is false at the only caller
+ * (LocalMapping.cc:388), so it is not applied. */
+int orbm_search_for_triangulation(const orbm_tri_frame* kf1, const orbm_tri_frame* kf2,
+                                  const float* F12, const float* ep2, const float* scale2,
+                                  const float* sigma2, int n_levels, int only_stereo,
+                                  int32_t* match12, int32_t* nmatches);
+
+/* ------------------------------------------------------------------------------------------
+ * Local bundle adjustment.  Replaces Optimizer::LocalBundleAdjustment (include/Optimizer.h:47,
+ * src/Optimizer.cc:491-736) from the vertex/edge setup (:540-631) onwards: the caller
+ * gathers local / fixed keyframes and map points and flattens them in reference order.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct orbba_problem {
+    int32_t        n_poses;     /* local KFs then fixed KFs (vertex insertion order) */
+    const double*  pose_R;      /* n_poses x 9 row-major world->camera rotation (CameraPose R) */
+    const double*  pose_t;      /* n_poses x 3 */
+    const uint8_t* pose_fixed;  /* n_poses: KF id 0 or a fixed camera */
+    int32_t        n_points;
+    const double*  points;      /* n_points x 3 world position */
+    int32_t        n_edges;     /* observations, in reference insertion order */
+    const int32_t* edge_point;  /* n_edges */
+    const int32_t* edge_pose;   /* n_edges */
+    const double*  edge_obs;    /* n_edges x 3: u, v, ur (ur < 0 => mono edge, :595) */
+    const double*  edge_inv_sigma2; /* n_edges: pyramid.invSigmaSq[octave] */
+    const double*  edge_cam;    /* n_edges x 5: fx, fy, cx, cy, bf */
+} orbba_problem;
+
+typedef struct orbba_result {
+    double*   pose_R;       /* n_poses x 9 (optimised; fixed poses unchanged) */
+    double*   pose_t;       /* n_poses x 3 */
+    double*   pose_q;       /* n_poses x 4 (x,y,z,w), g2o SE3Quat rotation; may be NULL */
+    double*   points;       /* n_points x 3 */
+    uint8_t*  edge_outlier; /* n_edges: 1 = chi2 > 5.991/7.815 or depth <= 0 at the end (:686-699) */
+    double*   edge_chi2;    /* n_edges: final chi2 (may be NULL) */
+    int32_t   iterations[2];/* LM iterations run by optimize(5) and optimize(10) */
+    double    chi2[2];      /* active robust chi2 after each optimize */
+} orbba_result;
+
+/* stop_flag: polled like g2o's force-stop flag (sparse_optimizer.h:188); may be NULL. */
+int orbba_local_ba(const orbba_problem* prob, orbba_result* res, const volatile int32_t* stop_flag,
+                   int device);
+
+const char* orb_last_error(void);
+int orb_device_count(void);
+
+/* Stage timing with HIP events recorded on the launch stream around each stage
+ * (0 pyramid, 1 FAST cells, 2 quadtree, 3 describe).  enable != 0 starts recording; read
+ * synchronises, returns the summed milliseconds and launch count per stage, and resets. */
+#define ORBX_NSTAGES 4
+int orbx_profile_enable(orbx_extractor* h, int enable);
+int orbx_profile_read(orbx_extractor* h, double* ms, int32_t* launches);
+
+/* ------------------------------------------------------------------------------------------
+ * Diagnostics (used by the per-stage parity tests; synchronous, host memory).
+ * ---------------------------------------------------------------------------------------- */
+/* FAST candidates of (frame, level) of the last batch, in DetectFAST's push order (cell raster,
+ * row-major inside a cell): packed x | y << 12 | score << 24.  *n = count (cap-limited copy). */
+int orbx_debug_level_candidates(const orbx_extractor* h, int frame, int level, uint32_t* out, int cap, int* n);
+/* Quadtree output of (frame, level) of the last batch (list order, packed as above). */
+int orbx_debug_level_selected(const orbx_extractor* h, int frame, int level, uint32_t* out, int cap, int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBSLAM2_AMD_H */

@@ -1,0 +1,1271 @@
+/*
+ * orb_oracle.cpp — CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * ===========================================================================================
+ *  This file is the parity ORACLE.  Only tests/, __graft_entry__.smoke() and bench.py's
+ *  cpu_baseline leg may load it.  The product (orb_slam2_refactored_amd/) never links,
+ *  imports or calls it; the product fails loudly when its HIP library is missing.
+ * ===========================================================================================
+ *
+ * What it restates (file:line into /root/reference):
+ *   ORBextractor   src/ORBextractor.cc:67-828   (Init, ComputePyramid, DetectFAST,
+ *                  QuadTreeSuppression + QTreeNode::divide, IC_Angle, ComputeOrbDescriptor,
+ *                  Extract) — with std::list / std::sort from the real libstdc++, so the
+ *                  quadtree's list order and unstable-sort tie order are the library's own.
+ *   OpenCV 4.x generic CPU paths the extractor calls [ext, not vendored, version unpinned]:
+ *                  cv::resize INTER_LINEAR 8U (fixed point, SIMD vertical rounding),
+ *                  cv::FAST TYPE_9_16 + cornerScore<16> + 3x3 NMS, GaussianBlur 7x7 sigma 2
+ *                  bit-exact Q8 (error-diffused taps) REFLECT_101, cv::fastAtan2, cvRound.
+ *   ORBmatcher     src/ORBmatcher.cc:384-404 (CheckDistEpipolarLine), :477-507 (best /
+ *                  second-best loop), :768-866 (SearchForTriangulation), :1449-1457.
+ *   LocalBA        src/Optimizer.cc:491-736 and the vendored g2o it drives:
+ *                  core/optimization_algorithm_levenberg.cpp:61-189, core/sparse_optimizer.cpp
+ *                  (:206-264 active set, :354-435 optimize/update), core/block_solver.hpp
+ *                  (:353-486 Schur, :501-604 buildSystem / lambda), core/base_binary_edge.hpp
+ *                  :54-120, core/robust_kernel_impl.cpp:65-91, types/types_six_dof_expmap.{h,cpp},
+ *                  types/se3quat.h, types/types_sba.h — Eigen replaced by explicit fp64 code,
+ *                  SimplicialLDLT by a dense LDLT of the reduced camera system.
+ *
+ * Parity status: the reference has NO tests, fixtures or golden vectors for this path and
+ * cannot be built here (OpenCV / Eigen absent; a shim build is not allowed).  This oracle is
+ * therefore "parity unpinned" against a real OpenCV/g2o build; it is pinned only by the
+ * known-answer values derivable from the reference text (umax, quotas, pyramid sizes, Gaussian
+ * taps, pattern checksum — tests/test_oracle_kat.py) and by libstdc++ itself for the sort.
+ * Documented choices where the reference is ambiguous:
+ *   - cos/sin in ComputeOrbDescriptor (:107) resolve to ::cos(double) (no `using namespace std`
+ *     in the refactor) => a = (float)cos((double)angle).
+ *   - cv::resize vertical pass uses the universal-intrinsics rounding
+ *     ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2 for every column (the SIMD loop's formula).
+ *   - GaussianBlur taps are OpenCV 4.x's error-diffused Q8 [18,34,48,56,48,34,18].
+ *   - Compiled -ffp-contract=off: the reference is ISO C++14 (CMakeLists.txt:10-11), under
+ *     which GCC does not contract a*b+c.
+ */
+#include <algorithm>
+#include <array>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <list>
+#include <vector>
+
+#include "orbslam2_amd.h"
+
+namespace oracle {
+
+// ---------------------------------------------------------------------------------------------
+// OpenCV scalar primitives [ext]
+// ---------------------------------------------------------------------------------------------
+static inline int cv_round(double v) { return (int)std::lrint(v); }   // _mm_cvtsd_si32: half-even
+static inline int cv_round(float v) { return (int)std::lrintf(v); }   // _mm_cvtss_si32
+static inline int cv_floor(float v) { return (int)std::floor(v); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+static inline short sat_short_f(float v) {
+    int iv = cv_round(v);
+    return (short)(iv < -32768 ? -32768 : iv > 32767 ? 32767 : iv);
+}
+
+// cv::fastAtan2 (core/src/mathfuncs_core.simd.hpp, atan_f32): degrees in [0,360).
+static float fast_atan2(float y, float x) {
+    const float k = (float)(180 / M_PI);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    float ax = std::fabs(x), ay = std::fabs(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// Simple owning 8U image with a row stride.
+struct Img {
+    int rows = 0, cols = 0;
+    size_t step = 0;
+    std::vector<uint8_t> buf;
+    const uint8_t* data = nullptr;   // may alias external memory
+    void alloc(int r, int c) {
+        rows = r; cols = c; step = (size_t)c;
+        buf.assign((size_t)r * c, 0);
+        data = buf.data();
+    }
+    uint8_t* mut_row(int y) { return buf.data() + (size_t)y * step; }
+    const uint8_t* row(int y) const { return data + (size_t)y * step; }
+    uint8_t at(int y, int x) const { return data[(size_t)y * step + x]; }
+};
+
+// cv::resize(src, dst, Size(dw, dh)) with INTER_LINEAR on CV_8UC1 [ext].
+static void resize_linear(const Img& src, Img& dst, int dw, int dh) {
+    const int sw = src.cols, sh = src.rows;
+    dst.alloc(dh, dw);
+    const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    std::vector<int> xofs(dw);
+    std::vector<short> ialpha(2 * dw);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        xofs[dx] = sx;
+        ialpha[2 * dx] = sat_short_f((1.f - fx) * 2048);
+        ialpha[2 * dx + 1] = sat_short_f(fx * 2048);
+    }
+    std::vector<int> r0(dw), r1(dw);
+    auto hrow = [&](int sy, std::vector<int>& D) {
+        const uint8_t* S = src.row(sy);
+        int dx = 0;
+        for (; dx < xmax; dx++) D[dx] = S[xofs[dx]] * ialpha[2 * dx] + S[xofs[dx] + 1] * ialpha[2 * dx + 1];
+        for (; dx < dw; dx++) D[dx] = S[xofs[dx]] * 2048;
+    };
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor(fy);
+        fy -= sy;
+        const int b0 = sat_short_f((1.f - fy) * 2048), b1 = sat_short_f(fy * 2048);
+        auto clip = [&](int y) { return y < 0 ? 0 : (y >= sh ? sh - 1 : y); };
+        hrow(clip(sy), r0);
+        hrow(clip(sy + 1), r1);
+        uint8_t* D = dst.mut_row(dy);
+        for (int x = 0; x < dw; x++) {
+            const int s0 = std::min(r0[x] >> 4, 32767), s1 = std::min(r1[x] >> 4, 32767);
+            const int v = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
+            D[x] = sat_u8((v + 2) >> 2);
+        }
+    }
+}
+
+// cv::FAST(img, kps, threshold, nonmax=true), TYPE_9_16 [ext, features2d/src/fast.cpp].
+struct RawKp { float x, y, response; };
+
+static const int kCircle[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                                   {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+static int corner_score16(const uint8_t* p, const int* off, int threshold) {
+    const int N = 25;
+    int v = p[0];
+    short d[N];
+    for (int k = 0; k < N; k++) d[k] = (short)(v - p[off[k]]);
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = std::min((int)d[k + 1], (int)d[k + 2]);
+        a = std::min(a, (int)d[k + 3]);
+        if (a <= a0) continue;
+        a = std::min(a, (int)d[k + 4]);
+        a = std::min(a, (int)d[k + 5]);
+        a = std::min(a, (int)d[k + 6]);
+        a = std::min(a, (int)d[k + 7]);
+        a = std::min(a, (int)d[k + 8]);
+        a0 = std::max(a0, std::min(a, (int)d[k]));
+        a0 = std::max(a0, std::min(a, (int)d[k + 9]));
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = std::max((int)d[k + 1], (int)d[k + 2]);
+        b = std::max(b, (int)d[k + 3]);
+        b = std::max(b, (int)d[k + 4]);
+        b = std::max(b, (int)d[k + 5]);
+        if (b >= b0) continue;
+        b = std::max(b, (int)d[k + 6]);
+        b = std::max(b, (int)d[k + 7]);
+        b = std::max(b, (int)d[k + 8]);
+        b0 = std::min(b0, std::max(b, (int)d[k]));
+        b0 = std::min(b0, std::max(b, (int)d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+// FAST on the view rows [y0,y1) x cols [x0,x1) of `im`; keypoints in view coordinates.
+static void fast916(const Img& im, int x0, int y0, int x1, int y1, int threshold, std::vector<RawKp>& out) {
+    out.clear();
+    const int rows = y1 - y0, cols = x1 - x0;
+    const int step = (int)im.step;
+    int off[25];
+    for (int k = 0; k < 16; k++) off[k] = kCircle[k][0] + kCircle[k][1] * step;
+    for (int k = 16; k < 25; k++) off[k] = off[k - 16];
+    threshold = std::min(std::max(threshold, 0), 255);
+    uint8_t tab[512];
+    for (int i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+    if (rows < 7 || cols < 7) return;
+    std::vector<uint8_t> sbuf[3];
+    std::vector<int> cpos[3];
+    for (int b = 0; b < 3; b++) { sbuf[b].assign(cols, 0); cpos[b].clear(); }
+    for (int i = 3; i < rows - 2; i++) {
+        std::vector<uint8_t>& curr = sbuf[(i - 3) % 3];
+        std::vector<int>& cp = cpos[(i - 3) % 3];
+        std::fill(curr.begin(), curr.end(), 0);
+        cp.clear();
+        if (i < rows - 3) {
+            const uint8_t* ptr = im.row(y0 + i) + x0 + 3;
+            for (int j = 3; j < cols - 3; j++, ptr++) {
+                const int v = ptr[0];
+                const uint8_t* t = &tab[0] - v + 255;
+                int d = t[ptr[off[0]]] | t[ptr[off[8]]];
+                if (d == 0) continue;
+                d &= t[ptr[off[2]]] | t[ptr[off[10]]];
+                d &= t[ptr[off[4]]] | t[ptr[off[12]]];
+                d &= t[ptr[off[6]]] | t[ptr[off[14]]];
+                if (d == 0) continue;
+                d &= t[ptr[off[1]]] | t[ptr[off[9]]];
+                d &= t[ptr[off[3]]] | t[ptr[off[11]]];
+                d &= t[ptr[off[5]]] | t[ptr[off[13]]];
+                d &= t[ptr[off[7]]] | t[ptr[off[15]]];
+                if (d & 1) {
+                    int vt = v - threshold, count = 0;
+                    for (int k = 0; k < 25; k++) {
+                        if (ptr[off[k]] < vt) {
+                            if (++count > 8) {
+                                cp.push_back(j);
+                                curr[j] = (uint8_t)corner_score16(ptr, off, threshold);
+                                break;
+                            }
+                        } else count = 0;
+                    }
+                }
+                if (d & 2) {
+                    int vt = v + threshold, count = 0;
+                    for (int k = 0; k < 25; k++) {
+                        if (ptr[off[k]] > vt) {
+                            if (++count > 8) {
+                                cp.push_back(j);
+                                curr[j] = (uint8_t)corner_score16(ptr, off, threshold);
+                                break;
+                            }
+                        } else count = 0;
+                    }
+                }
+            }
+        }
+        if (i == 3) continue;
+        const std::vector<uint8_t>& prev = sbuf[(i - 4 + 3) % 3];
+        const std::vector<uint8_t>& pprev = sbuf[(i - 5 + 3) % 3];
+        const std::vector<int>& pc = cpos[(i - 4 + 3) % 3];
+        for (int j : pc) {
+            const int s = prev[j];
+            if (s > prev[j + 1] && s > prev[j - 1] && s > pprev[j - 1] && s > pprev[j] && s > pprev[j + 1] &&
+                s > curr[j - 1] && s > curr[j] && s > curr[j + 1])
+                out.push_back({(float)j, (float)(i - 1), (float)s});
+        }
+    }
+}
+
+// cv::GaussianBlur(src, dst, Size(7,7), 2, 2, BORDER_REFLECT_101), 8U bit-exact path [ext].
+static void gaussian_taps_q8(int taps[7]) {
+    // getGaussianKernelBitExact (n=7, sigma=2) then getGaussianKernelFixedPoint_ED(.., 8 bits).
+    const double sigma = 2.0, scale2 = -0.125 / (sigma * sigma);
+    double vals[3], sum = 0;
+    for (int i = 0, x = -6; i < 3; i++, x += 2) { vals[i] = std::exp((double)(x * x) * scale2); sum += vals[i]; }
+    sum = sum * 2 + 1.0;
+    const double mul = 1.0 / sum;
+    double err = 0;
+    int64_t s = 0;
+    for (int i = 0; i < 3; i++) {
+        double adj = vals[i] * mul * 256.0 + err;
+        int v = cv_round(adj);
+        err = adj - v;
+        taps[i] = taps[6 - i] = v;
+        s += v;
+    }
+    taps[3] = (int)(256 - 2 * s);
+}
+
+static inline int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+static void gaussian_blur(const Img& src, Img& dst) {
+    int k[7];
+    gaussian_taps_q8(k);
+    const int W = src.cols, H = src.rows;
+    dst.alloc(H, W);
+    std::vector<uint32_t> h((size_t)W * H);   // Q8 horizontal sums (ufixedpoint16, exact)
+    for (int y = 0; y < H; y++) {
+        const uint8_t* S = src.row(y);
+        for (int x = 0; x < W; x++) {
+            uint32_t acc = 0;
+            for (int t = 0; t < 7; t++) acc += (uint32_t)k[t] * S[reflect101(x + t - 3, W)];
+            h[(size_t)y * W + x] = acc;
+        }
+    }
+    for (int y = 0; y < H; y++) {
+        uint8_t* D = dst.mut_row(y);
+        for (int x = 0; x < W; x++) {
+            uint32_t acc = 0;   // ufixedpoint32, Q16
+            for (int t = 0; t < 7; t++) acc += (uint32_t)k[t] * h[(size_t)reflect101(y + t - 3, H) * W + x];
+            D[x] = sat_u8((int)((acc + (1u << 15)) >> 16));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ORBextractor (src/ORBextractor.cc)
+// ---------------------------------------------------------------------------------------------
+static const int kPattern[1024] = {
+#include "orb_pattern31.inc"
+};
+
+struct Kp {   // cv::KeyPoint fields used by the extractor
+    float x, y, size, angle, response;
+    int octave;
+};
+
+struct Params {
+    int nfeatures;
+    float scaleFactor;
+    int nlevels, iniThFAST, minThFAST;
+};
+
+struct Extractor {
+    Params p;
+    std::vector<int> quota, umax;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<Img> levels, blurred;
+
+    explicit Extractor(const Params& prm) : p(prm) { init(); }
+
+    // ORBextractor::Init (:697-741) + ComputeNumFeaturesPerScale (:472-487)
+    void init() {
+        umax.assign(16, 0);
+        const int vmax = (int)std::floor(15 * std::sqrt(2.) / 2 + 1);
+        const int vmin = (int)std::ceil(15 * std::sqrt(2.) / 2);
+        for (int v = 0; v <= vmax; ++v) umax[v] = cv_round(std::sqrt(15.0 * 15 - v * v));
+        for (int v = 15, v0 = 0; v >= vmin; --v) {
+            while (umax[v0] == umax[v0 + 1]) ++v0;
+            umax[v] = v0;
+            ++v0;
+        }
+        const int L = p.nlevels;
+        scale.resize(L); inv_scale.resize(L); sigma2.resize(L); inv_sigma2.resize(L);
+        float s = 1.f;
+        for (int l = 0; l < L; l++) {
+            scale[l] = s; inv_scale[l] = 1.f / s; sigma2[l] = s * s; inv_sigma2[l] = 1.f / (s * s);
+            s *= p.scaleFactor;
+        }
+        quota.resize(L);
+        const double factor = 1 / p.scaleFactor;   // int / float: float division, widened
+        double nf = p.nfeatures * (1 - factor) / (1 - std::pow(factor, L));
+        int sum = 0;
+        for (int l = 0; l < L - 1; l++) {
+            quota[l] = cv_round(nf);
+            sum += quota[l];
+            nf *= factor;
+        }
+        quota[L - 1] = std::max(p.nfeatures - sum, 0);
+    }
+
+    // ComputePyramid (:455-470)
+    void pyramid(const Img& image) {
+        levels.assign(p.nlevels, Img());
+        levels[0].alloc(image.rows, image.cols);
+        for (int y = 0; y < image.rows; y++) std::memcpy(levels[0].mut_row(y), image.row(y), image.cols);
+        for (int l = 1; l < p.nlevels; l++) {
+            const int h = cv_round(inv_scale[l] * image.rows);
+            const int w = cv_round(inv_scale[l] * image.cols);
+            resize_linear(levels[l - 1], levels[l], w, h);
+        }
+    }
+
+    // DetectFAST (:489-540); roi = inset by BORDER 16 (:755-760)
+    static void detect_fast(const Img& im, int rx, int ry, int rw, int rh, int thIni, int thMin, std::vector<Kp>& kps) {
+        kps.clear();
+        const int minx = rx, miny = ry, maxx = rx + rw, maxy = ry + rh;
+        const int gridw = rw / 30, gridh = rh / 30;
+        if (gridw <= 0 || gridh <= 0) return;   // reference divides by zero here (UB); we emit none
+        const int cellw = (int)std::ceil(1. * rw / gridw), cellh = (int)std::ceil(1. * rh / gridh);
+        std::vector<RawKp> cell;
+        for (int cy = 0, y0 = miny; cy < gridh && y0 + 6 < maxy; cy++, y0 += cellh) {
+            for (int cx = 0, x0 = minx; cx < gridw && x0 + 6 < maxx; cx++, x0 += cellw) {
+                const int y1 = std::min(y0 + cellh + 6, maxy), x1 = std::min(x0 + cellw + 6, maxx);
+                fast916(im, x0, y0, x1, y1, thIni, cell);
+                if (cell.empty()) fast916(im, x0, y0, x1, y1, thMin, cell);
+                for (const RawKp& r : cell) kps.push_back({r.x + x0, r.y + y0, 7.f, -1.f, r.response, 0});
+            }
+        }
+    }
+
+    // QTreeNode (:402-452)
+    struct Node {
+        std::vector<Kp> pts;
+        int tlx = 0, tly = 0, brx = 0, bry = 0;
+        std::list<Node>::iterator self;
+        bool divisible = true;
+        void split(std::array<Node, 4>& ch) const {
+            const int hx = (int)std::ceil(0.5 * (brx - tlx)), hy = (int)std::ceil(0.5 * (bry - tly));
+            const int xm = tlx + hx, ym = tly + hy;
+            ch[0].tlx = tlx; ch[0].tly = tly; ch[0].brx = xm;  ch[0].bry = ym;
+            ch[1].tlx = xm;  ch[1].tly = tly; ch[1].brx = brx; ch[1].bry = ym;
+            ch[2].tlx = tlx; ch[2].tly = ym;  ch[2].brx = xm;  ch[2].bry = bry;
+            ch[3].tlx = xm;  ch[3].tly = ym;  ch[3].brx = brx; ch[3].bry = bry;
+            for (const Kp& k : pts) {
+                const int q = k.x < xm ? (k.y < ym ? 0 : 2) : (k.y < ym ? 1 : 3);
+                ch[q].pts.push_back(k);
+            }
+            for (int i = 0; i < 4; i++) if (ch[i].pts.size() == 1) ch[i].divisible = false;
+        }
+    };
+
+    // QuadTreeSuppression (:542-693)
+    static void quadtree(const std::vector<Kp>& src, int rx, int ry, int rw, int rh, size_t nfeat, std::vector<Kp>& dst) {
+        std::vector<Kp> out;
+        if (src.empty() || rw <= 0 || rh <= 0) { dst.clear(); return; }
+        const int nroots = cv_round(1. * rw / rh);
+        const double hx = 1. * rw / nroots;
+        std::list<Node> nodes;
+        std::vector<Node*> roots(nroots);
+        for (int i = 0; i < nroots; i++) {
+            Node n;
+            n.tlx = (int)(rx + hx * i); n.tly = ry;
+            n.brx = (int)(rx + hx * (i + 1)); n.bry = ry + rh;
+            nodes.push_back(n);
+            roots[i] = &nodes.back();
+        }
+        for (const Kp& k : src) roots[(int)((k.x - rx) / hx)]->pts.push_back(k);
+        for (auto it = nodes.begin(); it != nodes.end();) {
+            if (it->pts.empty()) it = nodes.erase(it);
+            else { if (it->pts.size() == 1) it->divisible = false; ++it; }
+        }
+        struct Div { size_t size; const Node* node; };
+        std::vector<Div> divs;
+        auto push_children = [&](const std::array<Node, 4>& ch) {
+            for (const Node& c : ch) {
+                if (c.pts.empty()) continue;
+                nodes.push_front(c);
+                if (c.pts.size() > 1) {
+                    nodes.front().self = nodes.begin();
+                    divs.push_back({c.pts.size(), &nodes.front()});
+                }
+            }
+        };
+        bool done = false;
+        while (!done) {
+            size_t before = nodes.size();
+            divs.clear();
+            for (auto it = nodes.begin(); it != nodes.end();) {
+                if (!it->divisible) { ++it; continue; }
+                std::array<Node, 4> ch;
+                it->split(ch);
+                push_children(ch);
+                it = nodes.erase(it);
+            }
+            if (nodes.size() >= nfeat || nodes.size() == before) break;
+            if (nodes.size() + 3 * divs.size() > nfeat) {
+                while (!done) {
+                    before = nodes.size();
+                    std::vector<Div> prev = divs;
+                    divs.clear();
+                    std::sort(prev.begin(), prev.end(), [](const Div& a, const Div& b) { return a.size > b.size; });
+                    for (const Div& d : prev) {
+                        std::array<Node, 4> ch;
+                        d.node->split(ch);
+                        push_children(ch);
+                        nodes.erase(d.node->self);
+                        if (nodes.size() >= nfeat) break;
+                    }
+                    if (nodes.size() >= nfeat || nodes.size() == before) done = true;
+                }
+            }
+        }
+        for (const Node& n : nodes) {
+            const Kp* best = nullptr;
+            float maxr = 0.f;
+            for (const Kp& k : n.pts)
+                if (k.response > maxr) { maxr = k.response; best = &k; }
+            out.push_back(*best);
+        }
+        dst.swap(out);
+    }
+
+    // IC_Angle (:74-101)
+    float ic_angle(const Img& im, float px, float py) const {
+        int m01 = 0, m10 = 0;
+        const uint8_t* c = im.row(cv_round(py)) + cv_round(px);
+        for (int u = -15; u <= 15; ++u) m10 += u * c[u];
+        const int step = (int)im.step;
+        for (int v = 1; v <= 15; ++v) {
+            int vs = 0;
+            const int d = umax[v];
+            for (int u = -d; u <= d; ++u) {
+                const int vp = c[u + v * step], vm = c[u - v * step];
+                vs += vp - vm;
+                m10 += u * (vp + vm);
+            }
+            m01 += v * vs;
+        }
+        return fast_atan2((float)m01, (float)m10);
+    }
+
+    // ComputeOrbDescriptor (:103-140)
+    static void describe(const Kp& k, const Img& im, uint8_t* desc) {
+        const float factorPI = (float)(M_PI / 180.f);
+        const float angle = k.angle * factorPI;
+        const float a = (float)std::cos((double)angle), b = (float)std::sin((double)angle);
+        const uint8_t* c = im.row(cv_round(k.y)) + cv_round(k.x);
+        const int step = (int)im.step;
+        auto val = [&](int idx) {
+            const float x = (float)kPattern[2 * idx], y = (float)kPattern[2 * idx + 1];
+            return (int)c[cv_round(x * b + y * a) * step + cv_round(x * a - y * b)];
+        };
+        for (int i = 0; i < 32; i++) {
+            int byte = 0;
+            for (int j = 0; j < 8; j++) {
+                const int p = i * 16 + 2 * j;
+                byte |= (val(p) < val(p + 1)) << j;
+            }
+            desc[i] = (uint8_t)byte;
+        }
+    }
+
+    // Extract (:743-820).  Returns total; fills kps/desc (cap checked by caller).
+    std::vector<std::vector<Kp>> per_level;
+    int extract(const Img& image, std::vector<Kp>& kps, std::vector<uint8_t>& desc) {
+        const int L = p.nlevels;
+        per_level.assign(L, {});
+        pyramid(image);
+        int total = 0;
+        for (int l = 0; l < L; l++) {
+            const Img& im = levels[l];
+            const int rx = 16, ry = 16, rw = im.cols - 32, rh = im.rows - 32;
+            std::vector<Kp>& lk = per_level[l];
+            if (rw > 0 && rh > 0) {
+                detect_fast(im, rx, ry, rw, rh, p.iniThFAST, p.minThFAST, lk);
+                quadtree(lk, rx, ry, rw, rh, (size_t)quota[l], lk);
+            }
+            // else: level narrower/shorter than 2*BORDER.  The reference then runs FAST on the
+            // whole level (:497-500), skips the quadtree (:544-545) and IC_Angle reads up to 15 px
+            // outside the image (or divides by zero when the level is < 30 px): undefined
+            // behaviour.  Documented deviation: such a level contributes no keypoints.
+            for (Kp& k : lk) {
+                k.octave = l;
+                k.size = scale[l] * 31;
+                k.angle = ic_angle(im, k.x, k.y);
+            }
+            total += (int)lk.size();
+        }
+        if (total == 0) return 0;
+        desc.assign((size_t)total * 32, 0);
+        kps.clear();
+        blurred.assign(L, Img());
+        int off = 0;
+        for (int l = 0; l < L; l++) {
+            std::vector<Kp>& lk = per_level[l];
+            if (lk.empty()) continue;
+            gaussian_blur(levels[l], blurred[l]);
+            for (size_t i = 0; i < lk.size(); i++) describe(lk[i], blurred[l], &desc[(size_t)(off + i) * 32]);
+            off += (int)lk.size();
+            if (l > 0)
+                for (Kp& k : lk) { k.x *= scale[l]; k.y *= scale[l]; }
+            kps.insert(kps.end(), lk.begin(), lk.end());
+        }
+        return total;
+    }
+};
+
+static Params to_params(const orbx_params* p) {
+    return Params{p->nfeatures, p->scaleFactor, p->nlevels, p->iniThFAST, p->minThFAST};
+}
+static Img view(const uint8_t* img, int rows, int cols, size_t step) {
+    Img im;
+    im.rows = rows; im.cols = cols; im.step = step; im.data = img;
+    return im;
+}
+static void to_abi(const Kp& k, orbx_keypoint* o) {
+    o->x = k.x; o->y = k.y; o->size = k.size; o->angle = k.angle; o->response = k.response;
+    o->octave = k.octave; o->class_id = -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// ORBmatcher
+// ---------------------------------------------------------------------------------------------
+static int hamming(const uint8_t* a, const uint8_t* b) {   // :1449-1457
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        std::memcpy(&x, a + 4 * i, 4);
+        std::memcpy(&y, b + 4 * i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+// CheckDistEpipolarLine (:384-404)
+static bool epipolar_ok(float x1, float y1, float x2, float y2, const float* F, float sigma2) {
+    const float a = x1 * F[0] + y1 * F[3] + F[6];
+    const float b = x1 * F[1] + y1 * F[4] + F[7];
+    const float c = x1 * F[2] + y1 * F[5] + F[8];
+    const float num = a * x2 + b * y2 + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return dsqr < 3.84 * sigma2;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LocalBA: g2o Levenberg-Marquardt with Schur complement (fp64)
+// ---------------------------------------------------------------------------------------------
+struct Quat { double x, y, z, w; };
+
+static Quat quat_from_R(const double* m) {   // Eigen::Quaterniond(const Matrix3d&)
+    Quat q;
+    const double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        double s = std::sqrt(t + 1.0);
+        q.w = 0.5 * s;
+        s = 0.5 / s;
+        q.x = (m[7] - m[5]) * s;
+        q.y = (m[2] - m[6]) * s;
+        q.z = (m[3] - m[1]) * s;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[3 * i + i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = std::sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
+        double qv[3];
+        qv[i] = 0.5 * s;
+        s = 0.5 / s;
+        q.w = (m[3 * k + j] - m[3 * j + k]) * s;
+        qv[j] = (m[3 * j + i] + m[3 * i + j]) * s;
+        qv[k] = (m[3 * k + i] + m[3 * i + k]) * s;
+        q.x = qv[0]; q.y = qv[1]; q.z = qv[2];
+    }
+    return q;
+}
+static void quat_normalize_pos(Quat& q) {   // SE3Quat::normalizeRotation
+    if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
+    const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    if (n > 0) { q.x /= n; q.y /= n; q.z /= n; q.w /= n; }
+}
+static void quat_to_R(const Quat& q, double* R) {   // Eigen toRotationMatrix
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+static Quat quat_mul(const Quat& a, const Quat& b) {
+    return Quat{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+                a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+                a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x,
+                a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+static void quat_rotate(const Quat& q, const double* v, double* o) {   // Eigen _transformVector
+    double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    const double c[3] = {q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2], q.x * uv[1] - q.y * uv[0]};
+    for (int i = 0; i < 3; i++) o[i] = v[i] + q.w * uv[i] + c[i];
+}
+
+struct SE3 { Quat q; double t[3]; };
+
+static void se3_map(const SE3& T, const double* X, double* o) {
+    quat_rotate(T.q, X, o);
+    o[0] += T.t[0]; o[1] += T.t[1]; o[2] += T.t[2];
+}
+
+// SE3Quat::exp (se3quat.h:217-257) followed by operator* (:99-105)
+static SE3 se3_exp_mul(const double* upd, const SE3& T) {
+    const double w[3] = {upd[0], upd[1], upd[2]}, u[3] = {upd[3], upd[4], upd[5]};
+    const double theta = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const double O[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+    double O2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += O[3 * i + k] * O[3 * k + j];
+            O2[3 * i + j] = s;
+        }
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        const double s = std::sin(theta), c = std::cos(theta);
+        const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / std::pow(theta, 3);
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + a * O[i] + b * O2[i];
+        for (int i = 0; i < 9; i++) V[i] = (i % 4 == 0 ? 1.0 : 0.0) + b * O[i] + d * O2[i];
+    }
+    SE3 E;
+    E.q = quat_from_R(R);
+    quat_normalize_pos(E.q);
+    for (int i = 0; i < 3; i++) E.t[i] = V[3 * i] * u[0] + V[3 * i + 1] * u[1] + V[3 * i + 2] * u[2];
+    SE3 out;
+    double rt[3];
+    quat_rotate(E.q, T.t, rt);
+    for (int i = 0; i < 3; i++) out.t[i] = E.t[i] + rt[i];
+    out.q = quat_mul(E.q, T.q);
+    quat_normalize_pos(out.q);
+    return out;
+}
+
+struct BA {
+    // problem
+    int P, N, E;
+    std::vector<SE3> pose;
+    std::vector<uint8_t> fixed;
+    std::vector<double> X;   // N x 3
+    std::vector<int> ep, ek; // edge point, edge pose
+    std::vector<uint8_t> stereo;
+    std::vector<double> obs, info, cam;
+    // edge state
+    std::vector<int> level;
+    std::vector<uint8_t> robust;
+    std::vector<double> err;   // E x 3 (last computed)
+    // active set
+    std::vector<int> act_edges;
+    std::vector<int> hp, hl;   // Hessian index per pose / point (-1 inactive or fixed)
+    int np = 0, nl = 0;
+    const volatile int32_t* stop = nullptr;
+
+    bool terminate() const { return stop && *stop; }
+
+    double chi2(int e) const {
+        const int d = stereo[e] ? 3 : 2;
+        double s = 0;
+        for (int i = 0; i < d; i++) s += err[3 * e + i] * info[e] * err[3 * e + i];
+        return s;
+    }
+    void robustify(int e, double chi, double& r0, double& r1) const {
+        if (!robust[e]) { r0 = chi; r1 = 1.0; return; }
+        const double delta = stereo[e] ? std::sqrt(7.815) : std::sqrt(5.991);
+        const double dsqr = delta * delta;
+        if (chi <= dsqr) { r0 = chi; r1 = 1.0; }
+        else { const double s = std::sqrt(chi); r0 = 2 * s * delta - dsqr; r1 = delta / s; }
+    }
+    void compute_error(int e) {
+        double Xc[3];
+        se3_map(pose[ek[e]], &X[3 * ep[e]], Xc);
+        const double* c = &cam[5 * e];
+        const double* z = &obs[3 * e];
+        if (!stereo[e]) {
+            err[3 * e + 0] = z[0] - (Xc[0] / Xc[2] * c[0] + c[2]);
+            err[3 * e + 1] = z[1] - (Xc[1] / Xc[2] * c[1] + c[3]);
+            err[3 * e + 2] = 0;
+        } else {
+            const float invz = 1.0f / Xc[2];
+            const float bf = (float)c[4];
+            const double u = Xc[0] * invz * c[0] + c[2];
+            const double v = Xc[1] * invz * c[1] + c[3];
+            err[3 * e + 0] = z[0] - u;
+            err[3 * e + 1] = z[1] - v;
+            err[3 * e + 2] = z[2] - (u - (double)(bf * invz));
+        }
+    }
+    bool depth_positive(int e) const {
+        double Xc[3];
+        se3_map(pose[ek[e]], &X[3 * ep[e]], Xc);
+        return Xc[2] > 0.0;
+    }
+    double active_robust_chi2() const {
+        double s = 0;
+        for (int e : act_edges) { double r0, r1; robustify(e, chi2(e), r0, r1); s += r0; }
+        return s;
+    }
+    void compute_active_errors() { for (int e : act_edges) compute_error(e); }
+
+    // initializeOptimization(level) (sparse_optimizer.cpp:206-264, :166-190)
+    void init_level(int lvl) {
+        act_edges.clear();
+        std::vector<uint8_t> pa(P, 0), la(N, 0);
+        for (int e = 0; e < E; e++) {
+            if (level[e] != lvl) continue;   // points are never fixed: edge never all-fixed
+            act_edges.push_back(e);
+            pa[ek[e]] = 1; la[ep[e]] = 1;
+        }
+        hp.assign(P, -1); hl.assign(N, -1);
+        np = 0; nl = 0;
+        for (int i = 0; i < P; i++) if (pa[i] && !fixed[i]) hp[i] = np++;
+        for (int i = 0; i < N; i++) if (la[i]) hl[i] = nl++;
+    }
+
+    // system
+    std::vector<double> Hpp, Hll, Hpl, bp, bl;   // Hpp dense (6np)^2; Hll nl x 9; Hpl per edge 18; b
+    std::vector<double> x;                       // 6np + 3nl
+
+    // linearizeOplus + constructQuadraticForm (types_six_dof_expmap.cpp:103-139,188-234;
+    // base_binary_edge.hpp:54-120), then copyB.
+    void build_system() {
+        const int D = 6 * np;
+        Hpp.assign((size_t)D * D, 0); Hll.assign((size_t)nl * 9, 0);
+        Hpl.assign((size_t)E * 18, 0);
+        bp.assign(D, 0); bl.assign((size_t)nl * 3, 0);
+        for (int e : act_edges) {
+            const SE3& T = pose[ek[e]];
+            double Xc[3];
+            se3_map(T, &X[3 * ep[e]], Xc);
+            double R[9];
+            quat_to_R(T.q, R);
+            const double x = Xc[0], y = Xc[1], z = Xc[2], z2 = z * z;
+            const double* c = &cam[5 * e];
+            const double fx = c[0], fy = c[1], bf = c[4];
+            const int d = stereo[e] ? 3 : 2;
+            double A[3][3] = {{0}}, B[3][6] = {{0}};
+            if (!stereo[e]) {
+                const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+                for (int r = 0; r < 2; r++)
+                    for (int j = 0; j < 3; j++) {
+                        double s = 0;
+                        for (int k = 0; k < 3; k++) s += tmp[r][k] * R[3 * k + j];
+                        A[r][j] = -1. / z * s;
+                    }
+            } else {
+                for (int j = 0; j < 3; j++) {
+                    A[0][j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
+                    A[1][j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
+                    A[2][j] = A[0][j] - bf * R[6 + j] / z2;
+                }
+            }
+            B[0][0] = x * y / z2 * fx; B[0][1] = -(1 + (x * x / z2)) * fx; B[0][2] = y / z * fx;
+            B[0][3] = -1. / z * fx;    B[0][4] = 0;                        B[0][5] = x / z2 * fx;
+            B[1][0] = (1 + y * y / z2) * fy; B[1][1] = -x * y / z2 * fy; B[1][2] = -x / z * fy;
+            B[1][3] = 0;                     B[1][4] = -1. / z * fy;     B[1][5] = y / z2 * fy;
+            if (stereo[e]) {
+                B[2][0] = B[0][0] - bf * y / z2; B[2][1] = B[0][1] + bf * x / z2; B[2][2] = B[0][2];
+                B[2][3] = B[0][3];               B[2][4] = 0;                     B[2][5] = B[0][5] - bf / z2;
+            }
+            double r0, r1;
+            robustify(e, chi2(e), r0, r1);
+            const double w = r1 * info[e];   // weighted information (diagonal)
+            double om_r[3];
+            for (int r = 0; r < d; r++) om_r[r] = -info[e] * err[3 * e + r] * r1;
+            const int il = hl[ep[e]], ip = hp[ek[e]];
+            // point block (vertex 0 = point, never fixed)
+            for (int i = 0; i < 3; i++) {
+                double s = 0;
+                for (int r = 0; r < d; r++) s += A[r][i] * om_r[r];
+                bl[3 * il + i] += s;
+                for (int j = 0; j < 3; j++) {
+                    double h = 0;
+                    for (int r = 0; r < d; r++) h += A[r][i] * w * A[r][j];
+                    Hll[9 * il + 3 * i + j] += h;
+                }
+            }
+            if (ip >= 0) {
+                for (int i = 0; i < 6; i++) {
+                    double s = 0;
+                    for (int r = 0; r < d; r++) s += B[r][i] * om_r[r];
+                    bp[6 * ip + i] += s;
+                    for (int j = 0; j < 6; j++) {
+                        double h = 0;
+                        for (int r = 0; r < d; r++) h += B[r][i] * w * B[r][j];
+                        Hpp[(size_t)(6 * ip + i) * D + 6 * ip + j] += h;
+                    }
+                    for (int j = 0; j < 3; j++) {   // Hpl (pose i, point j) = B^T W A
+                        double h = 0;
+                        for (int r = 0; r < d; r++) h += B[r][i] * w * A[r][j];
+                        Hpl[18 * e + 3 * i + j] = h;
+                    }
+                }
+            }
+        }
+    }
+
+    double lambda_init() const {   // computeLambdaInit (levenberg.cpp:166-180), tau = 1e-5
+        const int D = 6 * np;
+        double m = 0;
+        for (int i = 0; i < D; i++) m = std::max(m, std::fabs(Hpp[(size_t)i * D + i]));
+        for (int l = 0; l < nl; l++)
+            for (int j = 0; j < 3; j++) m = std::max(m, std::fabs(Hll[9 * l + 4 * j]));
+        return 1e-5 * m;
+    }
+
+    static bool inv3(const double* m, double* o) {
+        const double c00 = m[4] * m[8] - m[5] * m[7], c01 = m[5] * m[6] - m[3] * m[8], c02 = m[3] * m[7] - m[4] * m[6];
+        const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+        if (det == 0) return false;
+        const double id = 1.0 / det;
+        o[0] = c00 * id; o[1] = (m[2] * m[7] - m[1] * m[8]) * id; o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+        o[3] = c01 * id; o[4] = (m[0] * m[8] - m[2] * m[6]) * id; o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+        o[6] = c02 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+        return true;
+    }
+
+    // BlockSolver::solve with lambda on the diagonals (block_solver.hpp:353-486, :563-604)
+    bool solve(double lambda) {
+        const int D = 6 * np;
+        x.assign((size_t)D + 3 * nl, 0);
+        std::vector<double> S = Hpp, bs = bp;
+        for (int i = 0; i < D; i++) S[(size_t)i * D + i] += lambda;
+        std::vector<double> Dinv((size_t)nl * 9), db((size_t)nl * 3);
+        // per point: its active edges with a free pose
+        std::vector<std::vector<int>> pe(nl);
+        for (int e : act_edges) if (hp[ek[e]] >= 0) pe[hl[ep[e]]].push_back(e);
+        for (int l = 0; l < nl; l++) {
+            double Dm[9];
+            for (int i = 0; i < 9; i++) Dm[i] = Hll[9 * l + i];
+            Dm[0] += lambda; Dm[4] += lambda; Dm[8] += lambda;
+            inv3(Dm, &Dinv[9 * l]);
+            for (int i = 0; i < 3; i++) {
+                double s = 0;
+                for (int j = 0; j < 3; j++) s += Dinv[9 * l + 3 * i + j] * bl[3 * l + j];
+                db[3 * l + i] = s;
+            }
+            for (int e1 : pe[l]) {
+                const int i1 = hp[ek[e1]];
+                double W[18];   // Hpl * Dinv (6x3)
+                for (int r = 0; r < 6; r++)
+                    for (int c = 0; c < 3; c++) {
+                        double s = 0;
+                        for (int k = 0; k < 3; k++) s += Hpl[18 * e1 + 3 * r + k] * Dinv[9 * l + 3 * k + c];
+                        W[3 * r + c] = s;
+                    }
+                for (int r = 0; r < 6; r++) {
+                    double s = 0;
+                    for (int k = 0; k < 3; k++) s += Hpl[18 * e1 + 3 * r + k] * db[3 * l + k];
+                    bs[6 * i1 + r] -= s;
+                }
+                for (int e2 : pe[l]) {
+                    const int i2 = hp[ek[e2]];
+                    for (int r = 0; r < 6; r++)
+                        for (int c = 0; c < 6; c++) {
+                            double s = 0;
+                            for (int k = 0; k < 3; k++) s += W[3 * r + k] * Hpl[18 * e2 + 3 * c + k];
+                            S[(size_t)(6 * i1 + r) * D + 6 * i2 + c] -= s;
+                        }
+                }
+            }
+        }
+        // dense LDL^T of the reduced camera system (stands in for SimplicialLDLT)
+        std::vector<double> L((size_t)D * D, 0), dd(D, 0);
+        for (int j = 0; j < D; j++) {
+            double v = S[(size_t)j * D + j];
+            for (int k = 0; k < j; k++) v -= L[(size_t)j * D + k] * L[(size_t)j * D + k] * dd[k];
+            if (v == 0 || !std::isfinite(v)) return false;
+            dd[j] = v;
+            L[(size_t)j * D + j] = 1;
+            for (int i = j + 1; i < D; i++) {
+                double s = S[(size_t)i * D + j];
+                for (int k = 0; k < j; k++) s -= L[(size_t)i * D + k] * L[(size_t)j * D + k] * dd[k];
+                L[(size_t)i * D + j] = s / v;
+            }
+        }
+        std::vector<double> yv(D);
+        for (int i = 0; i < D; i++) {
+            double s = bs[i];
+            for (int k = 0; k < i; k++) s -= L[(size_t)i * D + k] * yv[k];
+            yv[i] = s;
+        }
+        for (int i = 0; i < D; i++) yv[i] /= dd[i];
+        for (int i = D - 1; i >= 0; i--) {
+            double s = yv[i];
+            for (int k = i + 1; k < D; k++) s -= L[(size_t)k * D + i] * x[k];
+            x[i] = s;
+        }
+        // back-substitution for points: xl = Dinv (bl - Hpl^T xp)
+        for (int l = 0; l < nl; l++) {
+            double cl[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
+            for (int e : pe[l]) {
+                const int ip = hp[ek[e]];
+                for (int k = 0; k < 3; k++) {
+                    double s = 0;
+                    for (int r = 0; r < 6; r++) s += Hpl[18 * e + 3 * r + k] * x[6 * ip + r];
+                    cl[k] -= s;
+                }
+            }
+            for (int i = 0; i < 3; i++) {
+                double s = 0;
+                for (int j = 0; j < 3; j++) s += Dinv[9 * l + 3 * i + j] * cl[j];
+                x[(size_t)D + 3 * l + i] = s;
+            }
+        }
+        return true;
+    }
+
+    std::vector<SE3> saved_pose;
+    std::vector<double> saved_X;
+    void push() { saved_pose = pose; saved_X = X; }
+    void pop() { pose = saved_pose; X = saved_X; }
+    void update() {
+        const int D = 6 * np;
+        for (int i = 0; i < P; i++) if (hp[i] >= 0) pose[i] = se3_exp_mul(&x[6 * hp[i]], pose[i]);
+        for (int l = 0; l < N; l++)
+            if (hl[l] >= 0) for (int k = 0; k < 3; k++) X[3 * l + k] += x[(size_t)D + 3 * hl[l] + k];
+    }
+
+    // SparseOptimizer::optimize + OptimizationAlgorithmLevenberg::solve
+    int optimize(int iters, double& final_chi) {
+        double lambda = 0, ni = 2;
+        int nbad = 0, done_iters = 0;
+        final_chi = 0;
+        if (np + nl == 0 || act_edges.empty()) return 0;
+        for (int it = 0; it < iters && !terminate(); it++) {
+            compute_active_errors();
+            double cur = active_robust_chi2();
+            const double ini = cur;
+            build_system();
+            if (it == 0) { lambda = lambda_init(); ni = 2; nbad = 0; }
+            double rho = 0;
+            int q = 0;
+            do {
+                push();
+                const bool ok = solve(lambda);
+                update();
+                compute_active_errors();
+                double tmp = active_robust_chi2();
+                if (!ok) tmp = DBL_MAX;
+                rho = cur - tmp;
+                double scale = 0;
+                const int D = 6 * np;
+                for (int j = 0; j < D; j++) scale += x[j] * (lambda * x[j] + bp[j]);
+                for (int j = 0; j < 3 * nl; j++) scale += x[(size_t)D + j] * (lambda * x[(size_t)D + j] + bl[j]);
+                scale += 1e-3;
+                rho /= scale;
+                if (rho > 0 && std::isfinite(tmp)) {
+                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    alpha = std::min(alpha, 2. / 3.);
+                    lambda *= std::max(1. / 3., alpha);
+                    ni = 2;
+                    cur = tmp;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    pop();
+                }
+                q++;
+            } while (rho < 0 && q < 10 && !terminate());
+            done_iters++;
+            final_chi = cur;
+            if (q == 10 || rho == 0) break;
+            if ((ini - cur) * 1e3 < ini) nbad++; else nbad = 0;
+            if (nbad >= 3) break;
+        }
+        return done_iters;
+    }
+};
+
+}  // namespace oracle
+
+using namespace oracle;
+
+// =============================================================================================
+// C ABI for the tests (ctypes).  Prefix oracle_.
+// =============================================================================================
+extern "C" {
+
+int oracle_scale_tables(const orbx_params* prm, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                        int32_t* quota, int32_t* umax16) {
+    Extractor ex(to_params(prm));
+    for (int l = 0; l < prm->nlevels; l++) {
+        if (scale) scale[l] = ex.scale[l];
+        if (inv_scale) inv_scale[l] = ex.inv_scale[l];
+        if (sigma2) sigma2[l] = ex.sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = ex.inv_sigma2[l];
+        if (quota) quota[l] = ex.quota[l];
+    }
+    if (umax16) for (int v = 0; v < 16; v++) umax16[v] = ex.umax[v];
+    return 0;
+}
+
+void oracle_gaussian_taps(int32_t* taps7) {
+    int t[7];
+    gaussian_taps_q8(t);
+    for (int i = 0; i < 7; i++) taps7[i] = t[i];
+}
+
+float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+
+// Pyramid: level l written at out + offs[l] (tight rows); dims in w[l], h[l].
+int oracle_pyramid(const orbx_params* prm, const uint8_t* img, int rows, int cols, size_t step, uint8_t* out,
+                   int64_t* offs, int32_t* w, int32_t* h) {
+    Extractor ex(to_params(prm));
+    ex.pyramid(view(img, rows, cols, step));
+    int64_t o = 0;
+    for (int l = 0; l < prm->nlevels; l++) {
+        const Img& im = ex.levels[l];
+        w[l] = im.cols; h[l] = im.rows; offs[l] = o;
+        if (out) for (int y = 0; y < im.rows; y++) std::memcpy(out + o + (int64_t)y * im.cols, im.row(y), im.cols);
+        o += (int64_t)im.rows * im.cols;
+    }
+    return 0;
+}
+
+// DetectFAST on one level image (full-image ROI inset 16): xs/ys/resp up to cap, returns count.
+int oracle_detect_fast(const uint8_t* img, int rows, int cols, size_t step, int thIni, int thMin, float* xs, float* ys,
+                       float* resp, int cap) {
+    std::vector<Kp> k;
+    Img im = view(img, rows, cols, step);
+    if (cols - 32 > 0 && rows - 32 > 0) Extractor::detect_fast(im, 16, 16, cols - 32, rows - 32, thIni, thMin, k);
+    const int n = (int)k.size();
+    for (int i = 0; i < n && i < cap; i++) { xs[i] = k[i].x; ys[i] = k[i].y; resp[i] = k[i].response; }
+    return n;
+}
+
+// Literal cv::FAST on a whole image (for score-map unit tests).
+int oracle_fast_raw(const uint8_t* img, int rows, int cols, size_t step, int th, float* xs, float* ys, float* resp,
+                    int cap) {
+    std::vector<RawKp> k;
+    fast916(view(img, rows, cols, step), 0, 0, cols, rows, th, k);
+    const int n = (int)k.size();
+    for (int i = 0; i < n && i < cap; i++) { xs[i] = k[i].x; ys[i] = k[i].y; resp[i] = k[i].response; }
+    return n;
+}
+
+// QuadTreeSuppression over given keypoints (roi inset 16 of a rows x cols level).
+int oracle_quadtree(const float* xs, const float* ys, const float* resp, int n, int rows, int cols, int nfeat,
+                    float* oxs, float* oys, float* oresp, int cap) {
+    std::vector<Kp> src(n), dst;
+    for (int i = 0; i < n; i++) src[i] = {xs[i], ys[i], 7.f, -1.f, resp[i], 0};
+    Extractor::quadtree(src, 16, 16, cols - 32, rows - 32, (size_t)nfeat, dst);
+    const int m = (int)dst.size();
+    for (int i = 0; i < m && i < cap; i++) { oxs[i] = dst[i].x; oys[i] = dst[i].y; oresp[i] = dst[i].response; }
+    return m;
+}
+
+int oracle_gaussian_blur(const uint8_t* img, int rows, int cols, size_t step, uint8_t* out) {
+    Img d;
+    gaussian_blur(view(img, rows, cols, step), d);
+    std::memcpy(out, d.buf.data(), (size_t)rows * cols);
+    return 0;
+}
+
+int oracle_extract(const orbx_params* prm, const uint8_t* img, int rows, int cols, size_t step, orbx_keypoint* kps,
+                   uint8_t* desc, int cap, int32_t* n, int32_t* per_level) {
+    Extractor ex(to_params(prm));
+    std::vector<Kp> k;
+    std::vector<uint8_t> d;
+    const int total = ex.extract(view(img, rows, cols, step), k, d);
+    *n = total;
+    if (per_level)
+        for (int l = 0; l < prm->nlevels; l++) per_level[l] = (int32_t)ex.per_level[l].size();
+    if (total > cap) return ORB_ECAP;
+    for (int i = 0; i < total; i++) to_abi(k[i], &kps[i]);
+    if (total) std::memcpy(desc, d.data(), (size_t)total * 32);
+    return 0;
+}
+
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) { return hamming(a, b); }
+
+// Best / second-best scan (ORBmatcher.cc:477-498) + acceptance (:500).
+void oracle_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float nnratio, int th_low, int32_t* bidx,
+                     int32_t* best, int32_t* second, int32_t* match) {
+    for (int i = 0; i < nA; i++) {
+        int bd = 256, sd = 256, bi = -1;
+        for (int j = 0; j < nB; j++) {
+            const int d = hamming(A + 32 * (size_t)i, B + 32 * (size_t)j);
+            if (d < bd) { sd = bd; bd = d; bi = j; }
+            else if (d < sd) sd = d;
+        }
+        bidx[i] = bi; best[i] = bd; second[i] = sd;
+        if (match) match[i] = (bd <= th_low && bd < nnratio * sd) ? bi : -1;
+    }
+}
+
+// SearchForTriangulation (ORBmatcher.cc:768-866), checkOrientation = false.
+int oracle_search_for_triangulation(const orbm_tri_frame* f1, const orbm_tri_frame* f2, const float* F12,
+                                    const float* ep2, const float* scale2, const float* sigma2, int only_stereo,
+                                    int32_t* match12) {
+    const int TH_LOW = 50;
+    for (int i = 0; i < f1->n; i++) match12[i] = -1;
+    int nm = 0;
+    int a = 0, b = 0;
+    while (a < f1->n_nodes && b < f2->n_nodes) {   // FeatureVectorIterator (:406-450)
+        if (f1->node_id[a] == f2->node_id[b]) {
+            for (int u = f1->node_off[a]; u < f1->node_off[a + 1]; u++) {
+                const int i1 = f1->indices[u];
+                if (f1->has_mappoint[i1]) continue;
+                const bool st1 = f1->uright[i1] >= 0;
+                if (only_stereo && !st1) continue;
+                int bd = TH_LOW, bi = -1;
+                for (int v = f2->node_off[b]; v < f2->node_off[b + 1]; v++) {
+                    const int i2 = f2->indices[v];
+                    if (f2->has_mappoint[i2]) continue;
+                    const bool st2 = f2->uright[i2] >= 0;
+                    if (only_stereo && !st2) continue;
+                    const int d = hamming(f1->desc + 32 * (size_t)i1, f2->desc + 32 * (size_t)i2);
+                    if (d > TH_LOW || d > bd) continue;
+                    const float x2 = f2->kp_xy[2 * i2], y2 = f2->kp_xy[2 * i2 + 1];
+                    const int o2 = f2->octave[i2];
+                    if (!st1 && !st2) {
+                        const float dx = ep2[0] - x2, dy = ep2[1] - y2;
+                        if (dx * dx + dy * dy < 100 * scale2[o2]) continue;
+                    }
+                    if (epipolar_ok(f1->kp_xy[2 * i1], f1->kp_xy[2 * i1 + 1], x2, y2, F12, sigma2[o2])) {
+                        bi = i2; bd = d;
+                    }
+                }
+                if (bi >= 0) { match12[i1] = bi; nm++; }
+            }
+            a++; b++;
+        } else if (f1->node_id[a] < f2->node_id[b]) a++;
+        else b++;
+    }
+    return nm;
+}
+
+// Optimizer::LocalBundleAdjustment from the vertex/edge setup on (Optimizer.cc:540-735).
+int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile int32_t* stop) {
+    BA ba;
+    ba.P = pr->n_poses; ba.N = pr->n_points; ba.E = pr->n_edges;
+    ba.stop = stop;
+    ba.pose.resize(ba.P);
+    ba.fixed.assign(pr->pose_fixed, pr->pose_fixed + ba.P);
+    for (int i = 0; i < ba.P; i++) {   // ToSE3Quat: SE3Quat(R, t) -> Quaterniond(R), normalize
+        ba.pose[i].q = quat_from_R(pr->pose_R + 9 * i);
+        quat_normalize_pos(ba.pose[i].q);
+        for (int k = 0; k < 3; k++) ba.pose[i].t[k] = pr->pose_t[3 * i + k];
+    }
+    ba.X.assign(pr->points, pr->points + 3 * (size_t)ba.N);
+    ba.ep.assign(pr->edge_point, pr->edge_point + ba.E);
+    ba.ek.assign(pr->edge_pose, pr->edge_pose + ba.E);
+    ba.obs.assign(pr->edge_obs, pr->edge_obs + 3 * (size_t)ba.E);
+    ba.info.assign(pr->edge_inv_sigma2, pr->edge_inv_sigma2 + ba.E);
+    ba.cam.assign(pr->edge_cam, pr->edge_cam + 5 * (size_t)ba.E);
+    ba.stereo.resize(ba.E);
+    for (int e = 0; e < ba.E; e++) ba.stereo[e] = ba.obs[3 * e + 2] < 0 ? 0 : 1;
+    ba.level.assign(ba.E, 0);
+    ba.robust.assign(ba.E, 1);
+    ba.err.assign(3 * (size_t)ba.E, 0);
+    res->iterations[0] = res->iterations[1] = 0;
+    res->chi2[0] = res->chi2[1] = 0;
+    bool run = !(stop && *stop);
+    if (run) {
+        ba.init_level(0);
+        res->iterations[0] = ba.optimize(5, res->chi2[0]);
+        bool more = !(stop && *stop);
+        if (more) {
+            for (int e = 0; e < ba.E; e++) {
+                const double maxc = ba.stereo[e] ? 7.815 : 5.991;
+                if (ba.chi2(e) > maxc || !ba.depth_positive(e)) ba.level[e] = 1;
+                ba.robust[e] = 0;
+            }
+            ba.init_level(0);
+            res->iterations[1] = ba.optimize(10, res->chi2[1]);
+        }
+    }
+    for (int e = 0; e < ba.E; e++) {
+        const double maxc = ba.stereo[e] ? 7.815 : 5.991;
+        const double c = ba.chi2(e);
+        res->edge_outlier[e] = run ? (uint8_t)(c > maxc || !ba.depth_positive(e)) : 0;
+        if (res->edge_chi2) res->edge_chi2[e] = c;
+    }
+    for (int i = 0; i < ba.P; i++) {
+        quat_to_R(ba.pose[i].q, res->pose_R + 9 * i);
+        for (int k = 0; k < 3; k++) res->pose_t[3 * i + k] = ba.pose[i].t[k];
+        if (res->pose_q) {
+            res->pose_q[4 * i] = ba.pose[i].q.x; res->pose_q[4 * i + 1] = ba.pose[i].q.y;
+            res->pose_q[4 * i + 2] = ba.pose[i].q.z; res->pose_q[4 * i + 3] = ba.pose[i].q.w;
+        }
+    }
+    std::memcpy(res->points, ba.X.data(), sizeof(double) * 3 * ba.N);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,14 @@
+"""MI355X-native ORB-SLAM2 hot path: ORB front end + local bundle adjustment on gfx950.
+
+Host mirrors of the reference's interfaces (tiantianxuabc/ORB_SLAM2_Refactored):
+  ORBextractor        <- include/ORBextractor.h
+  ORBmatcher          <- include/ORBmatcher.h (Hamming kernels)
+  Optimizer.LocalBundleAdjustment <- include/Optimizer.h:47
+All compute runs in liborbslam2_amd.so (HIP kernels behind include/orbslam2_amd.h).
+"""
+from .extractor import ORBextractor, KP_DTYPE
+from .matcher import ORBmatcher
+from . import optimizer
+from .synth import synth_image, shifted_pair
+
+__all__ = ["ORBextractor", "ORBmatcher", "optimizer", "KP_DTYPE", "synth_image", "shifted_pair"]

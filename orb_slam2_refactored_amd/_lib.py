@@ -1,0 +1,116 @@
+"""Loader for liborbslam2_amd.so (the HIP kernels + C-ABI, include/orbslam2_amd.h).
+
+There is deliberately no CPU fallback: if the library is missing or cannot be loaded this module
+raises, and every op in the package fails loudly.
+"""
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("ORBSLAM2_AMD_LIB", PKG / "liborbslam2_amd.so"))
+
+
+class OrbxParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scaleFactor", C.c_float), ("nlevels", C.c_int32),
+                ("iniThFAST", C.c_int32), ("minThFAST", C.c_int32)]
+
+
+class TriFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kp_xy", C.c_void_p), ("octave", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mappoint", C.c_void_p), ("desc", C.c_void_p), ("n_nodes", C.c_int32),
+                ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("indices", C.c_void_p)]
+
+
+class BAProblem(C.Structure):
+    _fields_ = [("n_poses", C.c_int32), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
+                ("pose_fixed", C.c_void_p), ("n_points", C.c_int32), ("points", C.c_void_p),
+                ("n_edges", C.c_int32), ("edge_point", C.c_void_p), ("edge_pose", C.c_void_p),
+                ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p), ("edge_cam", C.c_void_p)]
+
+
+class BAResult(C.Structure):
+    _fields_ = [("pose_R", C.c_void_p), ("pose_t", C.c_void_p), ("pose_q", C.c_void_p),
+                ("points", C.c_void_p), ("edge_outlier", C.c_void_p), ("edge_chi2", C.c_void_p),
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2)]
+
+
+# cv::KeyPoint layout (28 bytes)
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+VP = C.c_void_p
+I32 = C.c_int32
+SZ = C.c_size_t
+
+# name -> (restype, argtypes); every symbol declared in include/orbslam2_amd.h
+SIGNATURES = {
+    "orbx_create": (C.c_int, [C.POINTER(OrbxParams), C.c_int, C.POINTER(VP)]),
+    "orbx_destroy": (C.c_int, [VP]),
+    "orbx_scale_tables": (C.c_int, [VP, VP, VP, VP, VP, VP]),
+    "orbx_max_keypoints": (C.c_int, [VP, C.c_int, C.c_int, C.POINTER(I32)]),
+    "orbx_extract": (C.c_int, [VP, VP, C.c_int, C.c_int, SZ, VP, VP, C.c_int, C.POINTER(C.c_int)]),
+    "orbx_pyramid_level": (C.c_int, [VP, C.c_int, VP, SZ, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "orbx_extract_batch_device": (C.c_int, [VP, VP, C.c_int, C.c_int, C.c_int, SZ, SZ, VP, VP, VP, C.c_int, VP]),
+    "orbx_pyramid_device": (C.c_int, [VP, C.c_int, C.c_int, C.POINTER(VP), C.POINTER(C.c_int),
+                                      C.POINTER(C.c_int), C.POINTER(SZ)]),
+    "orbm_descriptor_distance": (C.c_int, [VP, VP]),
+    "orbm_hamming_top2_device": (C.c_int, [VP, C.c_int, VP, C.c_int, VP, VP, VP, VP]),
+    "orbm_bf_match_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, C.c_int, C.c_int, C.c_float, C.c_int,
+                                             VP, VP, VP, VP, VP]),
+    "orbm_bf_match": (C.c_int, [VP, C.c_int, VP, C.c_int, C.c_float, C.c_int, VP, VP, VP, VP]),
+    "orbm_search_for_triangulation": (C.c_int, [C.POINTER(TriFrame), C.POINTER(TriFrame), VP, VP, VP, VP,
+                                                C.c_int, C.c_int, VP, C.POINTER(I32)]),
+    "orbba_local_ba": (C.c_int, [C.POINTER(BAProblem), C.POINTER(BAResult), VP, C.c_int]),
+    "orbx_profile_enable": (C.c_int, [VP, C.c_int]),
+    "orbx_profile_read": (C.c_int, [VP, VP, VP]),
+    "orbx_debug_level_candidates": (C.c_int, [VP, C.c_int, C.c_int, VP, C.c_int, C.POINTER(C.c_int)]),
+    "orbx_debug_level_selected": (C.c_int, [VP, C.c_int, C.c_int, VP, C.c_int, C.POINTER(C.c_int)]),
+    "orb_last_error": (C.c_char_p, []),
+    "orb_device_count": (C.c_int, []),
+}
+
+_lib = None
+
+
+class OrbError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the native library (raises if absent: no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise OrbError(f"{LIB_PATH} not found — build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        l = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().orb_last_error().decode(errors="replace")
+        raise OrbError(f"{what} failed with status {rc}: {msg}")
+    return rc
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(VP)
+
+
+def tptr(t):
+    """Device pointer of a torch tensor."""
+    return VP(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return VP(s.cuda_stream)

@@ -1,0 +1,945 @@
+// orbba.hip — Optimizer::LocalBundleAdjustment on gfx950.
+//
+// g2o's Levenberg-Marquardt over SE3Expmap poses and marginalised XYZ points, fp64 throughout:
+//   per LM iteration (OptimizationAlgorithmLevenberg::solve, levenberg.cpp:61-164)
+//     ba_error_kernel        computeActiveErrors + robust chi2 per edge   (one lane per edge)
+//     ba_linearize_kernel    linearizeOplus + constructQuadraticForm       (one lane per edge)
+//     ba_point_accum_kernel  Hll / b_l per point, edges in g2o order      (one lane per point)
+//     ba_pose_accum_kernel   Hpp / b_p per pose, fixed-order tree sums    (one workgroup per pose)
+//   per trial (do { ... } while (rho < 0 ...))
+//     ba_schur_point_kernel  D^-1 = (Hll+lI)^-1, W = Hpl D^-1, Hpl D^-1 b_l (lane per point)
+//     ba_schur_block_kernel  S(i1,i2) = Hpp+lI - sum W Hpl^T over shared points (WG per block)
+//     ba_schur_rhs_kernel    b_schur = b_p - sum Hpl D^-1 b_l              (WG per pose)
+//     ba_ldlt_kernel         dense LDL^T solve of the (6P)^2 reduced camera system in LDS
+//     ba_update_kernel       back-substitution, push, SE3 exp-update / point += (lane per vertex)
+//     ba_error_kernel        + deterministic reduction -> new chi2
+//     ba_decide_kernel       rho, lambda / nu update, accept or pop (restore)
+// Every reduction runs in a fixed order, so results are bit-reproducible run to run.  The LM
+// control scalars live on the device; the host reads one small status block per trial to decide
+// whether to run another (the reference's loop condition), and polls the stop flag like g2o.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace orbamd {
+
+struct BACtl {
+    double lambda, ni, cur, ini, tmp, scale, rho;
+    int ok2, accepted;
+    double maxdiag;
+};
+
+// ------------------------------------------------------------------ SE3 helpers (se3quat.h)
+struct Q4 { double x, y, z, w; };
+
+__device__ __forceinline__ Q4 q_from_R(const double* m) {   // Eigen::Quaterniond(Matrix3d)
+    Q4 q;
+    const double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        double s = sqrt(t + 1.0);
+        q.w = 0.5 * s;
+        s = 0.5 / s;
+        q.x = (m[7] - m[5]) * s;
+        q.y = (m[2] - m[6]) * s;
+        q.z = (m[3] - m[1]) * s;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[3 * i + i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
+        double qv[3];
+        qv[i] = 0.5 * s;
+        s = 0.5 / s;
+        q.w = (m[3 * k + j] - m[3 * j + k]) * s;
+        qv[j] = (m[3 * j + i] + m[3 * i + j]) * s;
+        qv[k] = (m[3 * k + i] + m[3 * i + k]) * s;
+        q.x = qv[0]; q.y = qv[1]; q.z = qv[2];
+    }
+    return q;
+}
+__device__ __forceinline__ void q_normalize_pos(Q4& q) {   // SE3Quat::normalizeRotation
+    if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
+    const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    if (n > 0) { q.x /= n; q.y /= n; q.z /= n; q.w /= n; }
+}
+__host__ __device__ __forceinline__ void q_to_R(const double* q4, double* R) {   // toRotationMatrix
+    const double x = q4[0], y = q4[1], z = q4[2], w = q4[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+__device__ __forceinline__ void q_rotate(const double* q4, const double* v, double* o) {   // Eigen q*v
+    const double qx = q4[0], qy = q4[1], qz = q4[2], qw = q4[3];
+    double uv[3] = {qy * v[2] - qz * v[1], qz * v[0] - qx * v[2], qx * v[1] - qy * v[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    const double c[3] = {qy * uv[2] - qz * uv[1], qz * uv[0] - qx * uv[2], qx * uv[1] - qy * uv[0]};
+    for (int i = 0; i < 3; i++) o[i] = v[i] + qw * uv[i] + c[i];
+}
+__device__ __forceinline__ void se3_map(const double* q4, const double* t3, const double* X, double* o) {
+    q_rotate(q4, X, o);
+    o[0] += t3[0]; o[1] += t3[1]; o[2] += t3[2];
+}
+// pose <- SE3Quat::exp(upd) * pose   (se3quat.h:217-257, :99-105)
+__device__ void se3_exp_update(const double* upd, double* q4, double* t3) {
+    const double w0 = upd[0], w1 = upd[1], w2 = upd[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += O[3 * i + k] * O[3 * k + j];
+            O2[3 * i + j] = s;
+        }
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        const double s = sin(theta), c = cos(theta);
+        const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / pow(theta, 3);
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + a * O[i] + b * O2[i];
+        for (int i = 0; i < 9; i++) V[i] = (i % 4 == 0 ? 1.0 : 0.0) + b * O[i] + d * O2[i];
+    }
+    Q4 E = q_from_R(R);
+    q_normalize_pos(E);
+    const double Eq[4] = {E.x, E.y, E.z, E.w};
+    double Et[3];
+    for (int i = 0; i < 3; i++) Et[i] = V[3 * i] * upd[3] + V[3 * i + 1] * upd[4] + V[3 * i + 2] * upd[5];
+    double rt[3];
+    q_rotate(Eq, t3, rt);
+    for (int i = 0; i < 3; i++) t3[i] = Et[i] + rt[i];
+    const double ax = E.x, ay = E.y, az = E.z, aw = E.w;
+    const double bx = q4[0], by = q4[1], bz = q4[2], bw = q4[3];
+    Q4 r{aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
+         aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz};
+    q_normalize_pos(r);
+    q4[0] = r.x; q4[1] = r.y; q4[2] = r.z; q4[3] = r.w;
+}
+
+// ------------------------------------------------------------------ problem on the device
+struct BADev {
+    int P, N, E;
+    double* q;      // P x 4
+    double* t;      // P x 3
+    double* q_sv;   // push/pop copies
+    double* t_sv;
+    double* X;      // N x 3
+    double* X_sv;
+    const uint8_t* fixed;
+    const int* ep;
+    const int* ek;
+    const uint8_t* stereo;
+    const double* obs;    // E x 3
+    const double* info;   // E
+    const double* cam;    // E x 5
+    uint8_t* robust;      // E
+    double* err;          // E x 3 (last computed error, g2o's _error)
+    // active structure
+    int Ea, np, nl, nblk;
+    const int* act;       // Ea: edge id per active slot (ascending edge id)
+    const int* hp;        // P: hessian index or -1
+    const int* hl;        // N: point index or -1
+    const int* pt_beg;    // nl+1: CSR of active slots per active point (slot order)
+    const int* pt_slot;
+    const int* pt_id;     // nl: point id of point index
+    const int* ps_beg;    // np+1: CSR of active slots per free pose
+    const int* ps_slot;
+    const int* ps_id;     // np: pose id
+    const int* blk_i1;    // nblk
+    const int* blk_i2;
+    const int* blk_beg;   // nblk+1: CSR of (slot1, slot2) pairs
+    const int2* blk_pair;
+    // per active slot products
+    double* J;            // Ea x 72: Hll(9) bl(3) Hpp(36) bp(6) Hpl(18, pose-major 6x3)
+    double* W;            // Ea x 24: W = Hpl Dinv (18) | Hpl Dinv b_l (6)
+    // per point / pose system
+    double* Hll;          // nl x 9
+    double* bl;           // nl x 3
+    double* Dinv;         // nl x 9
+    double* Hpp;          // np x 36
+    double* bp;           // np x 6
+    double* S;            // D x D reduced system
+    double* bs;           // D
+    double* x;            // D + 3 nl
+    double* rchi;         // Ea: robust chi2 per active slot
+    double* part;         // scale partials: nl + np
+    BACtl* ctl;
+};
+
+__device__ __forceinline__ double edge_chi2(const BADev& b, int e) {
+    const int d = b.stereo[e] ? 3 : 2;
+    double s = 0;
+    for (int i = 0; i < d; i++) s += b.err[3 * e + i] * b.info[e] * b.err[3 * e + i];
+    return s;
+}
+__device__ __forceinline__ void robustify(const BADev& b, int e, double chi, double& r0, double& r1) {
+    if (!b.robust[e]) { r0 = chi; r1 = 1.0; return; }
+    const double delta = b.stereo[e] ? sqrt(7.815) : sqrt(5.991);   // Optimizer.cc:44-47
+    const double dsqr = delta * delta;
+    if (chi <= dsqr) { r0 = chi; r1 = 1.0; }
+    else { const double s = sqrt(chi); r0 = 2 * s * delta - dsqr; r1 = delta / s; }   // robust_kernel_impl.cpp:78-91
+}
+
+// EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::computeError (types_six_dof_expmap.h:90-95,122-127)
+__global__ void ba_error_kernel(BADev b) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= b.Ea) return;
+    const int e = b.act[k];
+    const int pi = b.ek[e];
+    double Xc[3];
+    se3_map(b.q + 4 * pi, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
+    const double* c = b.cam + 5 * e;
+    const double* z = b.obs + 3 * e;
+    if (!b.stereo[e]) {
+        b.err[3 * e + 0] = z[0] - (Xc[0] / Xc[2] * c[0] + c[2]);
+        b.err[3 * e + 1] = z[1] - (Xc[1] / Xc[2] * c[1] + c[3]);
+        b.err[3 * e + 2] = 0;
+    } else {   // cam_project(..., bf): invz narrowed to float, bf*invz in float (.cpp:148-156)
+        const float invz = 1.0f / Xc[2];
+        const float bf = (float)c[4];
+        const double u = Xc[0] * invz * c[0] + c[2];
+        const double v = Xc[1] * invz * c[1] + c[3];
+        b.err[3 * e + 0] = z[0] - u;
+        b.err[3 * e + 1] = z[1] - v;
+        b.err[3 * e + 2] = z[2] - (u - (double)(bf * invz));
+    }
+    double r0, r1;
+    robustify(b, e, edge_chi2(b, e), r0, r1);
+    b.rchi[k] = r0;
+}
+
+// Deterministic single-workgroup sum (fixed strided order + fixed tree).
+__global__ __launch_bounds__(1024) void ba_sum_kernel(const double* v, int n, double* out) {
+    __shared__ double sh[1024];
+    double s = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += v[i];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = sh[0];
+}
+
+// linearizeOplus + constructQuadraticForm per active edge (types_six_dof_expmap.cpp:103-139,
+// 188-234; base_binary_edge.hpp:54-120)
+__global__ void ba_linearize_kernel(BADev b) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= b.Ea) return;
+    const int e = b.act[k];
+    const int pi = b.ek[e];
+    const double* q4 = b.q + 4 * pi;
+    double Xc[3], R[9];
+    se3_map(q4, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
+    q_to_R(q4, R);
+    const double x = Xc[0], y = Xc[1], z = Xc[2], z2 = z * z;
+    const double* c = b.cam + 5 * e;
+    const double fx = c[0], fy = c[1], bf = c[4];
+    const bool st = b.stereo[e];
+    const int d = st ? 3 : 2;
+    double A[3][3], B[3][6];
+    for (int r = 0; r < 3; r++) {
+        for (int j = 0; j < 3; j++) A[r][j] = 0;
+        for (int j = 0; j < 6; j++) B[r][j] = 0;
+    }
+    if (!st) {
+        const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+        for (int r = 0; r < 2; r++)
+            for (int j = 0; j < 3; j++) {
+                double s = 0;
+                for (int m = 0; m < 3; m++) s += tmp[r][m] * R[3 * m + j];
+                A[r][j] = -1. / z * s;
+            }
+    } else {
+        for (int j = 0; j < 3; j++) {
+            A[0][j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
+            A[1][j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
+            A[2][j] = A[0][j] - bf * R[6 + j] / z2;
+        }
+    }
+    B[0][0] = x * y / z2 * fx; B[0][1] = -(1 + (x * x / z2)) * fx; B[0][2] = y / z * fx;
+    B[0][3] = -1. / z * fx;    B[0][4] = 0;                        B[0][5] = x / z2 * fx;
+    B[1][0] = (1 + y * y / z2) * fy; B[1][1] = -x * y / z2 * fy; B[1][2] = -x / z * fy;
+    B[1][3] = 0;                     B[1][4] = -1. / z * fy;     B[1][5] = y / z2 * fy;
+    if (st) {
+        B[2][0] = B[0][0] - bf * y / z2; B[2][1] = B[0][1] + bf * x / z2; B[2][2] = B[0][2];
+        B[2][3] = B[0][3];               B[2][4] = 0;                     B[2][5] = B[0][5] - bf / z2;
+    }
+    double r0, r1;
+    robustify(b, e, edge_chi2(b, e), r0, r1);
+    const double w = r1 * b.info[e];
+    double om_r[3] = {0, 0, 0};
+    for (int r = 0; r < d; r++) om_r[r] = -b.info[e] * b.err[3 * e + r] * r1;
+    double* J = b.J + (long long)k * 72;
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int r = 0; r < d; r++) s += A[r][i] * om_r[r];
+        J[9 + i] = s;
+        for (int j = 0; j < 3; j++) {
+            double h = 0;
+            for (int r = 0; r < d; r++) h += A[r][i] * w * A[r][j];
+            J[3 * i + j] = h;
+        }
+    }
+    if (b.hp[pi] >= 0) {
+        for (int i = 0; i < 6; i++) {
+            double s = 0;
+            for (int r = 0; r < d; r++) s += B[r][i] * om_r[r];
+            J[48 + i] = s;
+            for (int j = 0; j < 6; j++) {
+                double h = 0;
+                for (int r = 0; r < d; r++) h += B[r][i] * w * B[r][j];
+                J[12 + 6 * i + j] = h;
+            }
+            for (int j = 0; j < 3; j++) {
+                double h = 0;
+                for (int r = 0; r < d; r++) h += B[r][i] * w * A[r][j];
+                J[54 + 3 * i + j] = h;
+            }
+        }
+    }
+}
+
+__global__ void ba_point_accum_kernel(BADev b) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= b.nl) return;
+    double H[9] = {0}, g[3] = {0};
+    for (int u = b.pt_beg[l]; u < b.pt_beg[l + 1]; u++) {
+        const double* J = b.J + (long long)b.pt_slot[u] * 72;
+        for (int i = 0; i < 9; i++) H[i] += J[i];
+        for (int i = 0; i < 3; i++) g[i] += J[9 + i];
+    }
+    for (int i = 0; i < 9; i++) b.Hll[9 * l + i] = H[i];
+    for (int i = 0; i < 3; i++) b.bl[3 * l + i] = g[i];
+}
+
+// One workgroup (256 threads) per free pose: 42 sums (Hpp 36 + b 6) in a fixed order.
+__global__ __launch_bounds__(256) void ba_pose_accum_kernel(BADev b) {
+    __shared__ double sh[6][42];
+    const int i = blockIdx.x;
+    const int g = threadIdx.x / 42, c = threadIdx.x % 42;   // 6 groups x 42 entries (252 threads)
+    const int beg = b.ps_beg[i], end = b.ps_beg[i + 1];
+    if (g < 6) {
+        double s = 0;
+        for (int u = beg + g; u < end; u += 6) s += b.J[(long long)b.ps_slot[u] * 72 + 12 + c];
+        sh[g][c] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 42) {
+        double s = 0;
+        for (int q = 0; q < 6; q++) s += sh[q][threadIdx.x];
+        if (threadIdx.x < 36) b.Hpp[36 * i + threadIdx.x] = s;
+        else b.bp[6 * i + threadIdx.x - 36] = s;
+    }
+}
+
+// computeLambdaInit (levenberg.cpp:166-180): tau * max |diag H| over active vertices.
+__global__ __launch_bounds__(256) void ba_lambda_init_kernel(BADev b) {
+    __shared__ double sh[256];
+    double m = 0;
+    for (int i = threadIdx.x; i < 6 * b.np; i += blockDim.x) m = fmax(m, fabs(b.Hpp[36 * (i / 6) + 7 * (i % 6)]));
+    for (int i = threadIdx.x; i < 3 * b.nl; i += blockDim.x) m = fmax(m, fabs(b.Hll[9 * (i / 3) + 4 * (i % 3)]));
+    sh[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        b.ctl->maxdiag = sh[0];
+        b.ctl->lambda = 1e-5 * sh[0];
+        b.ctl->ni = 2;
+    }
+}
+
+__device__ __forceinline__ bool inv3(const double* m, double* o) {
+    const double c00 = m[4] * m[8] - m[5] * m[7], c01 = m[5] * m[6] - m[3] * m[8], c02 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+    if (det == 0) return false;
+    const double id = 1.0 / det;
+    o[0] = c00 * id; o[1] = (m[2] * m[7] - m[1] * m[8]) * id; o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    o[3] = c01 * id; o[4] = (m[0] * m[8] - m[2] * m[6]) * id; o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    o[6] = c02 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+    return true;
+}
+
+// BlockSolver::solve, landmark part (block_solver.hpp:377-419)
+__global__ void ba_schur_point_kernel(BADev b) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= b.nl) return;
+    const double lam = b.ctl->lambda;
+    double D[9], Di[9];
+    for (int i = 0; i < 9; i++) D[i] = b.Hll[9 * l + i];
+    D[0] += lam; D[4] += lam; D[8] += lam;
+    inv3(D, Di);
+    for (int i = 0; i < 9; i++) b.Dinv[9 * l + i] = Di[i];
+    double db[3];
+    for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * b.bl[3 * l] + Di[3 * i + 1] * b.bl[3 * l + 1] + Di[3 * i + 2] * b.bl[3 * l + 2];
+    for (int u = b.pt_beg[l]; u < b.pt_beg[l + 1]; u++) {
+        const int k = b.pt_slot[u];
+        if (b.hp[b.ek[b.act[k]]] < 0) continue;
+        const double* Hpl = b.J + (long long)k * 72 + 54;
+        double* W = b.W + (long long)k * 24;
+        for (int r = 0; r < 6; r++) {
+            for (int c = 0; c < 3; c++)
+                W[3 * r + c] = Hpl[3 * r] * Di[c] + Hpl[3 * r + 1] * Di[3 + c] + Hpl[3 * r + 2] * Di[6 + c];
+            W[18 + r] = Hpl[3 * r] * db[0] + Hpl[3 * r + 1] * db[1] + Hpl[3 * r + 2] * db[2];
+        }
+    }
+}
+
+// Reduced camera system block (i1, i2): 36 entries x 7 partial groups, fixed-order combine.
+__global__ __launch_bounds__(256) void ba_schur_block_kernel(BADev b, int D) {
+    __shared__ double sh[7][36];
+    const int blk = blockIdx.x;
+    const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
+    const int g = threadIdx.x / 36, c = threadIdx.x % 36;
+    const int r = c / 6, cc = c % 6;
+    if (g < 7) {
+        double s = 0;
+        for (int u = b.blk_beg[blk] + g; u < b.blk_beg[blk + 1]; u += 7) {
+            const int2 pr = b.blk_pair[u];
+            const double* W = b.W + (long long)pr.x * 24 + 3 * r;
+            const double* H = b.J + (long long)pr.y * 72 + 54 + 3 * cc;
+            s += W[0] * H[0] + W[1] * H[1] + W[2] * H[2];
+        }
+        sh[g][c] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 36) {
+        double s = 0;
+        for (int q = 0; q < 7; q++) s += sh[q][threadIdx.x];
+        double v = -s;
+        if (i1 == i2) {
+            v += b.Hpp[36 * i1 + threadIdx.x];
+            if (r == cc) v += b.ctl->lambda;
+        }
+        b.S[(long long)(6 * i1 + r) * D + 6 * i2 + cc] = v;
+        if (i1 != i2) b.S[(long long)(6 * i2 + cc) * D + 6 * i1 + r] = v;
+    }
+}
+
+__global__ __launch_bounds__(64) void ba_schur_rhs_kernel(BADev b) {
+    const int i = blockIdx.x;
+    if (threadIdx.x >= 6) return;
+    double s = 0;
+    for (int u = b.ps_beg[i]; u < b.ps_beg[i + 1]; u++) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + threadIdx.x];
+    b.bs[6 * i + threadIdx.x] = b.bp[6 * i + threadIdx.x] - s;
+}
+
+// Dense LDL^T solve of S x = bs, S in LDS (right-looking; one workgroup).
+__global__ __launch_bounds__(1024) void ba_ldlt_kernel(BADev b, int D) {
+    extern __shared__ __attribute__((aligned(16))) double A[];
+    double* v = A + (size_t)D * D;
+    __shared__ int s_ok;
+    for (int i = threadIdx.x; i < D * D; i += blockDim.x) A[i] = b.S[i];
+    for (int i = threadIdx.x; i < D; i += blockDim.x) v[i] = b.bs[i];
+    if (threadIdx.x == 0) s_ok = 1;
+    __syncthreads();
+    for (int j = 0; j < D; j++) {
+        const double dj = A[j * D + j];
+        if (!(dj != 0 && isfinite(dj))) {
+            if (threadIdx.x == 0) s_ok = 0;
+            break;   // uniform: every thread read the same dj
+        }
+        for (int i = j + 1 + threadIdx.x; i < D; i += blockDim.x) A[i * D + j] /= dj;   // L(i,j)
+        __syncthreads();
+        const int m = D - j - 1;
+        for (int t = threadIdx.x; t < m * m; t += blockDim.x) {
+            const int i = j + 1 + t / m, k = j + 1 + t % m;
+            if (k <= i) A[i * D + k] -= A[i * D + j] * dj * A[k * D + j];
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    const int ok = s_ok;
+    if (ok) {
+        // L y = b (column sweep), y /= d, L^T x = y
+        for (int j = 0; j < D; j++) {
+            const double yj = v[j];
+            for (int i = j + 1 + threadIdx.x; i < D; i += blockDim.x) v[i] -= A[i * D + j] * yj;
+            __syncthreads();
+        }
+        for (int i = threadIdx.x; i < D; i += blockDim.x) v[i] /= A[i * D + i];
+        __syncthreads();
+        for (int j = D - 1; j >= 0; j--) {
+            const double xj = v[j];
+            for (int i = threadIdx.x; i < j; i += blockDim.x) v[i] -= A[j * D + i] * xj;
+            __syncthreads();
+        }
+        for (int i = threadIdx.x; i < D; i += blockDim.x) b.x[i] = v[i];
+    } else {
+        for (int i = threadIdx.x; i < D; i += blockDim.x) b.x[i] = 0;
+    }
+    if (threadIdx.x == 0) b.ctl->ok2 = ok;
+}
+
+// Back-substitution xl = Dinv (bl - Hpl^T xp), push(), oplus; scale partials x.(lambda x + b).
+__global__ void ba_update_kernel(BADev b, int D) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const double lam = b.ctl->lambda;
+    if (t < b.nl) {
+        const int l = t;
+        double cl[3] = {b.bl[3 * l], b.bl[3 * l + 1], b.bl[3 * l + 2]};
+        for (int u = b.pt_beg[l]; u < b.pt_beg[l + 1]; u++) {
+            const int k = b.pt_slot[u];
+            const int ip = b.hp[b.ek[b.act[k]]];
+            if (ip < 0) continue;
+            const double* Hpl = b.J + (long long)k * 72 + 54;
+            for (int c = 0; c < 3; c++) {
+                double s = 0;
+                for (int r = 0; r < 6; r++) s += Hpl[3 * r + c] * b.x[6 * ip + r];
+                cl[c] -= s;
+            }
+        }
+        const double* Di = b.Dinv + 9 * l;
+        const int id = b.pt_id[l];
+        double part = 0;
+        for (int i = 0; i < 3; i++) {
+            const double xi = Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1] + Di[3 * i + 2] * cl[2];
+            b.x[D + 3 * l + i] = xi;
+            b.X_sv[3 * id + i] = b.X[3 * id + i];
+            b.X[3 * id + i] += xi;
+            part += xi * (lam * xi + b.bl[3 * l + i]);
+        }
+        b.part[l] = part;
+    } else if (t < b.nl + b.np) {
+        const int i = t - b.nl;
+        const int id = b.ps_id[i];
+        double part = 0;
+        for (int j = 0; j < 6; j++) part += b.x[6 * i + j] * (lam * b.x[6 * i + j] + b.bp[6 * i + j]);
+        b.part[b.nl + i] = part;
+        for (int j = 0; j < 4; j++) b.q_sv[4 * id + j] = b.q[4 * id + j];
+        for (int j = 0; j < 3; j++) b.t_sv[3 * id + j] = b.t[3 * id + j];
+        se3_exp_update(b.x + 6 * i, b.q + 4 * id, b.t + 3 * id);
+    }
+}
+
+// levenberg.cpp:120-147 — the accept / reject decision (one thread).
+__global__ void ba_decide_kernel(BADev b) {
+    BACtl* c = b.ctl;
+    double tmp = c->tmp;
+    if (!c->ok2) tmp = 1.7976931348623157e308;   // std::numeric_limits<double>::max()
+    double rho = c->cur - tmp;
+    double scale = c->scale + 1e-3;
+    rho /= scale;
+    c->rho = rho;
+    if (rho > 0 && isfinite(tmp)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        c->lambda *= fmax(1. / 3., alpha);
+        c->ni = 2;
+        c->cur = tmp;
+        c->accepted = 1;
+    } else {
+        c->lambda *= c->ni;
+        c->ni *= 2;
+        c->accepted = 0;
+    }
+}
+
+// pop(): restore the pushed estimates when the step was rejected.
+__global__ void ba_restore_kernel(BADev b) {
+    if (b.ctl->accepted) return;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < b.nl) {
+        const int id = b.pt_id[t];
+        for (int i = 0; i < 3; i++) b.X[3 * id + i] = b.X_sv[3 * id + i];
+    } else if (t < b.nl + b.np) {
+        const int id = b.ps_id[t - b.nl];
+        for (int j = 0; j < 4; j++) b.q[4 * id + j] = b.q_sv[4 * id + j];
+        for (int j = 0; j < 3; j++) b.t[3 * id + j] = b.t_sv[3 * id + j];
+    }
+}
+
+// final outlier classification (Optimizer.cc:644-670, :686-699) + chi2 out
+__global__ void ba_classify_kernel(BADev b, uint8_t* outlier, double* chi2o, uint8_t* level, int set_level) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= b.E) return;
+    const double maxc = b.stereo[e] ? 7.815 : 5.991;
+    const double c = edge_chi2(b, e);
+    double Xc[3];
+    const int pi = b.ek[e];
+    se3_map(b.q + 4 * pi, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
+    const uint8_t bad = (c > maxc || !(Xc[2] > 0.0)) ? 1 : 0;
+    if (outlier) outlier[e] = bad;
+    if (chi2o) chi2o[e] = c;
+    if (set_level) {
+        if (bad) level[e] = 1;
+        b.robust[e] = 0;
+    }
+}
+
+}  // namespace orbamd
+
+using namespace orbamd;
+
+namespace {
+
+// Device-resident LocalBA workspace (one per thread: LocalMapping runs one LocalBA at a time).
+struct BAContext {
+    int device = -1;
+    hipStream_t st = nullptr;
+    DevBuf prob, state, structure, sys, ctlbuf;
+    BACtl* h_ctl = nullptr;   // pinned
+    ~BAContext() {
+        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
+        if (h_ctl) (void)hipHostFree(h_ctl);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+thread_local BAContext g_ba;
+
+struct Carve {
+    char* base;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t n) {
+        T* p = reinterpret_cast<T*>(base + off);
+        off += align_up(std::max<size_t>(n, 1) * sizeof(T), 256);
+        return p;
+    }
+};
+template <class T>
+size_t carve_size(size_t n) { return align_up(std::max<size_t>(n, 1) * sizeof(T), 256); }
+
+struct HostStructure {
+    std::vector<int> act, hp, hl, pt_beg, pt_slot, pt_id, ps_beg, ps_slot, ps_id, blk_i1, blk_i2, blk_beg;
+    std::vector<int2> blk_pair;
+    int np = 0, nl = 0;
+};
+
+// SparseOptimizer::initializeOptimization(level) (sparse_optimizer.cpp:206-264) and the
+// BlockSolver structure (block_solver.hpp:142-295): active edges / vertices, Hessian indices, and
+// the Schur fill pattern (pose pairs that share a point).
+void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
+                     const int* ek, HostStructure& s) {
+    const int E = (int)level.size();
+    std::vector<uint8_t> pa(P, 0), la(N, 0);
+    s.act.clear();
+    for (int e = 0; e < E; e++)
+        if (level[e] == 0) { s.act.push_back(e); pa[ek[e]] = 1; la[ep[e]] = 1; }
+    s.hp.assign(P, -1); s.hl.assign(N, -1);
+    s.ps_id.clear(); s.pt_id.clear();
+    s.np = 0; s.nl = 0;
+    for (int i = 0; i < P; i++) if (pa[i] && !fixed[i]) { s.hp[i] = s.np++; s.ps_id.push_back(i); }
+    for (int i = 0; i < N; i++) if (la[i]) { s.hl[i] = s.nl++; s.pt_id.push_back(i); }
+    const int Ea = (int)s.act.size();
+    s.pt_beg.assign(s.nl + 1, 0); s.ps_beg.assign(s.np + 1, 0);
+    for (int k = 0; k < Ea; k++) {
+        const int e = s.act[k];
+        s.pt_beg[s.hl[ep[e]] + 1]++;
+        if (s.hp[ek[e]] >= 0) s.ps_beg[s.hp[ek[e]] + 1]++;
+    }
+    for (int i = 0; i < s.nl; i++) s.pt_beg[i + 1] += s.pt_beg[i];
+    for (int i = 0; i < s.np; i++) s.ps_beg[i + 1] += s.ps_beg[i];
+    s.pt_slot.assign(Ea, 0); s.ps_slot.assign(s.ps_beg[s.np], 0);
+    std::vector<int> fp(s.pt_beg.begin(), s.pt_beg.end() - 1), fq(s.ps_beg.begin(), s.ps_beg.end() - 1);
+    for (int k = 0; k < Ea; k++) {
+        const int e = s.act[k];
+        s.pt_slot[fp[s.hl[ep[e]]]++] = k;
+        if (s.hp[ek[e]] >= 0) s.ps_slot[fq[s.hp[ek[e]]]++] = k;
+    }
+    // pose-pair blocks: (i1 <= i2), pairs (slot with pose i1, slot with pose i2) per shared point
+    const int np = s.np;
+    std::vector<std::vector<int2>> pairs((size_t)np * np);
+    std::vector<int> blk_index((size_t)np * np, -1);
+    for (int l = 0; l < s.nl; l++) {
+        std::vector<int> sl;
+        for (int u = s.pt_beg[l]; u < s.pt_beg[l + 1]; u++)
+            if (s.hp[ek[s.act[s.pt_slot[u]]]] >= 0) sl.push_back(s.pt_slot[u]);
+        for (int a : sl)
+            for (int c : sl) {
+                const int i1 = s.hp[ek[s.act[a]]], i2 = s.hp[ek[s.act[c]]];
+                if (i1 <= i2) pairs[(size_t)i1 * np + i2].push_back(make_int2(a, c));
+            }
+    }
+    s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0); s.blk_pair.clear();
+    for (int i1 = 0; i1 < np; i1++)
+        for (int i2 = i1; i2 < np; i2++) {
+            const auto& v = pairs[(size_t)i1 * np + i2];
+            if (v.empty() && i1 != i2) continue;
+            s.blk_i1.push_back(i1);
+            s.blk_i2.push_back(i2);
+            s.blk_pair.insert(s.blk_pair.end(), v.begin(), v.end());
+            s.blk_beg.push_back((int)s.blk_pair.size());
+        }
+}
+
+}  // namespace
+
+extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const volatile int32_t* stop_flag,
+                              int device) {
+    ORB_CHECK_ARG(pr && res, "null argument");
+    const int P = pr->n_poses, N = pr->n_points, E = pr->n_edges;
+    ORB_CHECK_ARG(P >= 0 && N >= 0 && E >= 0, "negative sizes");
+    ORB_CHECK_ARG(res->pose_R && res->pose_t && res->points && res->edge_outlier, "null result buffers");
+    for (int e = 0; e < E; e++)
+        ORB_CHECK_ARG(pr->edge_point[e] >= 0 && pr->edge_point[e] < N && pr->edge_pose[e] >= 0 &&
+                          pr->edge_pose[e] < P, "edge references a missing vertex");
+    BAContext& C = g_ba;
+    if (C.device != device) {
+        ORB_HIP_TRY(hipSetDevice(device));
+        if (C.st) (void)hipStreamDestroy(C.st);
+        ORB_HIP_TRY(hipStreamCreateWithFlags(&C.st, hipStreamNonBlocking));
+        if (!C.h_ctl) ORB_HIP_TRY(hipHostMalloc((void**)&C.h_ctl, sizeof(BACtl), hipHostMallocDefault));
+        C.device = device;
+    }
+    ORB_HIP_TRY(hipSetDevice(device));
+    hipStream_t st = C.st;
+    auto stopped = [&]() { return stop_flag && *stop_flag; };
+
+    // initial estimates: SE3Quat(R, t) -> Quaterniond(R) normalised (Optimizer.cc:145-150)
+    std::vector<double> q0(4 * (size_t)P);
+    for (int i = 0; i < P; i++) {
+        const double* m = pr->pose_R + 9 * i;
+        double x, y, z, w;
+        const double tr = m[0] + m[4] + m[8];
+        if (tr > 0) {
+            double s = std::sqrt(tr + 1.0);
+            w = 0.5 * s; s = 0.5 / s;
+            x = (m[7] - m[5]) * s; y = (m[2] - m[6]) * s; z = (m[3] - m[1]) * s;
+        } else {
+            int a = 0;
+            if (m[4] > m[0]) a = 1;
+            if (m[8] > m[3 * a + a]) a = 2;
+            const int bb = (a + 1) % 3, c = (bb + 1) % 3;
+            double s = std::sqrt(m[3 * a + a] - m[3 * bb + bb] - m[3 * c + c] + 1.0);
+            double qv[3];
+            qv[a] = 0.5 * s; s = 0.5 / s;
+            w = (m[3 * c + bb] - m[3 * bb + c]) * s;
+            qv[bb] = (m[3 * bb + a] + m[3 * a + bb]) * s;
+            qv[c] = (m[3 * c + a] + m[3 * a + c]) * s;
+            x = qv[0]; y = qv[1]; z = qv[2];
+        }
+        if (w < 0) { x = -x; y = -y; z = -z; w = -w; }
+        const double n = std::sqrt(x * x + y * y + z * z + w * w);
+        if (n > 0) { x /= n; y /= n; z /= n; w /= n; }
+        q0[4 * i] = x; q0[4 * i + 1] = y; q0[4 * i + 2] = z; q0[4 * i + 3] = w;
+    }
+    std::vector<uint8_t> stereo(E);
+    for (int e = 0; e < E; e++) stereo[e] = pr->edge_obs[3 * e + 2] < 0 ? 0 : 1;   // ur < 0 => mono (:595)
+
+    // ---- device problem + state
+    const size_t prob_bytes = carve_size<uint8_t>(P) + carve_size<int>(E) * 2 + carve_size<uint8_t>(E) +
+                              carve_size<double>(3 * (size_t)E) + carve_size<double>(E) + carve_size<double>(5 * (size_t)E);
+    const size_t state_bytes = carve_size<double>(4 * (size_t)P) * 2 + carve_size<double>(3 * (size_t)P) * 2 +
+                               carve_size<double>(3 * (size_t)N) * 2 + carve_size<uint8_t>(E) * 3 +
+                               carve_size<double>(3 * (size_t)E) + carve_size<double>(E);
+    int rc;
+    if ((rc = C.prob.reserve(prob_bytes))) return rc;
+    if ((rc = C.state.reserve(state_bytes))) return rc;
+    if ((rc = C.ctlbuf.reserve(sizeof(BACtl) + 64))) return rc;
+    Carve cp{C.prob.as<char>()}, cs{C.state.as<char>()};
+    BADev b;
+    std::memset(&b, 0, sizeof(b));
+    b.P = P; b.N = N; b.E = E;
+    uint8_t* d_fixed = cp.take<uint8_t>(P);
+    int* d_ep = cp.take<int>(E);
+    int* d_ek = cp.take<int>(E);
+    uint8_t* d_st = cp.take<uint8_t>(E);
+    double* d_obs = cp.take<double>(3 * (size_t)E);
+    double* d_info = cp.take<double>(E);
+    double* d_cam = cp.take<double>(5 * (size_t)E);
+    b.q = cs.take<double>(4 * (size_t)P); b.q_sv = cs.take<double>(4 * (size_t)P);
+    b.t = cs.take<double>(3 * (size_t)P); b.t_sv = cs.take<double>(3 * (size_t)P);
+    b.X = cs.take<double>(3 * (size_t)N); b.X_sv = cs.take<double>(3 * (size_t)N);
+    b.robust = cs.take<uint8_t>(E);
+    uint8_t* d_level = cs.take<uint8_t>(E);
+    uint8_t* d_outl = cs.take<uint8_t>(E);
+    b.err = cs.take<double>(3 * (size_t)E);
+    double* d_chi = cs.take<double>(E);
+    b.fixed = d_fixed; b.ep = d_ep; b.ek = d_ek; b.stereo = d_st; b.obs = d_obs; b.info = d_info; b.cam = d_cam;
+    b.ctl = C.ctlbuf.as<BACtl>();
+    if (P) {
+        ORB_HIP_TRY(hipMemcpyAsync(d_fixed, pr->pose_fixed, P, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemcpyAsync(b.q, q0.data(), 32 * (size_t)P, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemcpyAsync(b.t, pr->pose_t, 24 * (size_t)P, hipMemcpyHostToDevice, st));
+    }
+    if (N) ORB_HIP_TRY(hipMemcpyAsync(b.X, pr->points, 24 * (size_t)N, hipMemcpyHostToDevice, st));
+    if (E) {
+        ORB_HIP_TRY(hipMemcpyAsync(d_ep, pr->edge_point, 4 * (size_t)E, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemcpyAsync(d_ek, pr->edge_pose, 4 * (size_t)E, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemcpyAsync(d_st, stereo.data(), E, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemcpyAsync(d_obs, pr->edge_obs, 24 * (size_t)E, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemcpyAsync(d_info, pr->edge_inv_sigma2, 8 * (size_t)E, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemcpyAsync(d_cam, pr->edge_cam, 40 * (size_t)E, hipMemcpyHostToDevice, st));
+        ORB_HIP_TRY(hipMemsetAsync(b.robust, 1, E, st));
+        ORB_HIP_TRY(hipMemsetAsync(d_level, 0, E, st));
+        ORB_HIP_TRY(hipMemsetAsync(b.err, 0, 24 * (size_t)E, st));
+    }
+    res->iterations[0] = res->iterations[1] = 0;
+    res->chi2[0] = res->chi2[1] = 0;
+
+    std::vector<uint8_t> level(E, 0);
+    HostStructure hs;
+    // ------------------------------------------------------------------ one optimize(iters)
+    auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
+        build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs);
+        const int Ea = (int)hs.act.size(), np = hs.np, nl = hs.nl, D = 6 * np;
+        const int nblk = (int)hs.blk_i1.size();
+        *iters_out = 0;
+        *chi_out = 0;
+        if (Ea == 0 || np + nl == 0) return ORB_OK;
+        if ((size_t)D * D * 8 + (size_t)D * 8 > 150 * 1024) {
+            set_error("LocalBA: too many free keyframes for the in-LDS reduced-system solve (max 22)");
+            return ORB_EINVAL;
+        }
+        // structure upload
+        const size_t sbytes = carve_size<int>(Ea) + carve_size<int>(P) + carve_size<int>(N) + carve_size<int>(nl + 1) +
+                              carve_size<int>(Ea) + carve_size<int>(nl) + carve_size<int>(np + 1) +
+                              carve_size<int>(hs.ps_slot.size()) + carve_size<int>(np) + carve_size<int>(nblk) * 2 +
+                              carve_size<int>(nblk + 1) + carve_size<int2>(hs.blk_pair.size());
+        int rc2;
+        if ((rc2 = C.structure.reserve(sbytes))) return rc2;
+        Carve cr{C.structure.as<char>()};
+        auto up = [&](const void* src, size_t n, char* dst) -> int {
+            if (n) ORB_HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
+            return ORB_OK;
+        };
+        int* d_act = cr.take<int>(Ea);
+        int* d_hp = cr.take<int>(P);
+        int* d_hl = cr.take<int>(N);
+        int* d_ptb = cr.take<int>(nl + 1);
+        int* d_pts = cr.take<int>(Ea);
+        int* d_pti = cr.take<int>(nl);
+        int* d_psb = cr.take<int>(np + 1);
+        int* d_pss = cr.take<int>(hs.ps_slot.size());
+        int* d_psi = cr.take<int>(np);
+        int* d_b1 = cr.take<int>(nblk);
+        int* d_b2 = cr.take<int>(nblk);
+        int* d_bb = cr.take<int>(nblk + 1);
+        int2* d_bp = cr.take<int2>(hs.blk_pair.size());
+        if ((rc2 = up(hs.act.data(), 4 * (size_t)Ea, (char*)d_act))) return rc2;
+        if ((rc2 = up(hs.hp.data(), 4 * (size_t)P, (char*)d_hp))) return rc2;
+        if ((rc2 = up(hs.hl.data(), 4 * (size_t)N, (char*)d_hl))) return rc2;
+        if ((rc2 = up(hs.pt_beg.data(), 4 * (size_t)(nl + 1), (char*)d_ptb))) return rc2;
+        if ((rc2 = up(hs.pt_slot.data(), 4 * (size_t)Ea, (char*)d_pts))) return rc2;
+        if ((rc2 = up(hs.pt_id.data(), 4 * (size_t)nl, (char*)d_pti))) return rc2;
+        if ((rc2 = up(hs.ps_beg.data(), 4 * (size_t)(np + 1), (char*)d_psb))) return rc2;
+        if ((rc2 = up(hs.ps_slot.data(), 4 * hs.ps_slot.size(), (char*)d_pss))) return rc2;
+        if ((rc2 = up(hs.ps_id.data(), 4 * (size_t)np, (char*)d_psi))) return rc2;
+        if ((rc2 = up(hs.blk_i1.data(), 4 * (size_t)nblk, (char*)d_b1))) return rc2;
+        if ((rc2 = up(hs.blk_i2.data(), 4 * (size_t)nblk, (char*)d_b2))) return rc2;
+        if ((rc2 = up(hs.blk_beg.data(), 4 * (size_t)(nblk + 1), (char*)d_bb))) return rc2;
+        if ((rc2 = up(hs.blk_pair.data(), 8 * hs.blk_pair.size(), (char*)d_bp))) return rc2;
+        b.Ea = Ea; b.np = np; b.nl = nl; b.nblk = nblk;
+        b.act = d_act; b.hp = d_hp; b.hl = d_hl; b.pt_beg = d_ptb; b.pt_slot = d_pts; b.pt_id = d_pti;
+        b.ps_beg = d_psb; b.ps_slot = d_pss; b.ps_id = d_psi; b.blk_i1 = d_b1; b.blk_i2 = d_b2; b.blk_beg = d_bb;
+        b.blk_pair = d_bp;
+        // system buffers
+        const size_t ybytes = carve_size<double>(72 * (size_t)Ea) + carve_size<double>(24 * (size_t)Ea) +
+                              carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +
+                              carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
+                              carve_size<double>((size_t)D * D) + carve_size<double>(D) +
+                              carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(Ea) +
+                              carve_size<double>(nl + np) + 64;
+        if ((rc2 = C.sys.reserve(ybytes))) return rc2;
+        Carve cy{C.sys.as<char>()};
+        b.J = cy.take<double>(72 * (size_t)Ea);
+        b.W = cy.take<double>(24 * (size_t)Ea);
+        b.Hll = cy.take<double>(9 * (size_t)nl);
+        b.Dinv = cy.take<double>(9 * (size_t)nl);
+        b.bl = cy.take<double>(3 * (size_t)nl);
+        b.Hpp = cy.take<double>(36 * (size_t)np);
+        b.bp = cy.take<double>(6 * (size_t)np);
+        b.S = cy.take<double>((size_t)D * D);
+        b.bs = cy.take<double>(D);
+        b.x = cy.take<double>(D + 3 * (size_t)nl);
+        b.rchi = cy.take<double>(Ea);
+        b.part = cy.take<double>(nl + np);
+        ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
+        if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
+        const size_t ldlt_lds = ((size_t)D * D + D) * 8;
+        ORB_HIP_TRY(hipFuncSetAttribute((const void*)ba_ldlt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)std::max<size_t>(ldlt_lds, 1024)));
+        const dim3 ge((Ea + 255) / 256), gv((nl + np + 255) / 256), gp((nl + 255) / 256);
+        double* d_cur = &b.ctl->cur;
+        int nbad = 0;
+        for (int it = 0; it < iters && !stopped(); it++) {
+            hipLaunchKernelGGL(ba_error_kernel, ge, dim3(256), 0, st, b);
+            hipLaunchKernelGGL(ba_sum_kernel, dim3(1), dim3(1024), 0, st, (const double*)b.rchi, Ea, d_cur);
+            ORB_HIP_TRY(hipMemcpyAsync(&b.ctl->ini, d_cur, 8, hipMemcpyDeviceToDevice, st));
+            hipLaunchKernelGGL(ba_linearize_kernel, ge, dim3(256), 0, st, b);
+            if (nl) hipLaunchKernelGGL(ba_point_accum_kernel, gp, dim3(256), 0, st, b);
+            if (np) hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np), dim3(256), 0, st, b);
+            if (it == 0) hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
+            int q = 0;
+            double rho = 0;
+            do {
+                if (nl) hipLaunchKernelGGL(ba_schur_point_kernel, gp, dim3(256), 0, st, b);
+                if (np) {
+                    hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk), dim3(256), 0, st, b, D);
+                    hipLaunchKernelGGL(ba_schur_rhs_kernel, dim3(np), dim3(64), 0, st, b);
+                    hipLaunchKernelGGL(ba_ldlt_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
+                } else {
+                    ORB_HIP_TRY(hipMemsetAsync(&b.ctl->ok2, 0xff, 4, st));   // no poses: ok
+                }
+                hipLaunchKernelGGL(ba_update_kernel, gv, dim3(256), 0, st, b, D);
+                hipLaunchKernelGGL(ba_sum_kernel, dim3(1), dim3(1024), 0, st, (const double*)b.part, nl + np, &b.ctl->scale);
+                hipLaunchKernelGGL(ba_error_kernel, ge, dim3(256), 0, st, b);
+                hipLaunchKernelGGL(ba_sum_kernel, dim3(1), dim3(1024), 0, st, (const double*)b.rchi, Ea, &b.ctl->tmp);
+                hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(1), 0, st, b);
+                hipLaunchKernelGGL(ba_restore_kernel, gv, dim3(256), 0, st, b);
+                ORB_HIP_TRY(hipGetLastError());
+                ORB_HIP_TRY(hipMemcpyAsync(C.h_ctl, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost, st));
+                ORB_HIP_TRY(hipStreamSynchronize(st));
+                rho = C.h_ctl->rho;
+                q++;
+            } while (rho < 0 && q < 10 && !stopped());
+            (*iters_out)++;
+            *chi_out = C.h_ctl->cur;
+            if (q == 10 || rho == 0) break;   // Terminate
+            const double ini = C.h_ctl->ini, cur = C.h_ctl->cur;
+            if ((ini - cur) * 1e3 < ini) nbad++; else nbad = 0;
+            if (nbad >= 3) break;
+        }
+        return ORB_OK;
+    };
+
+    const bool run = !stopped();   // Optimizer.cc:633-634: stop before optimising => nothing done
+    if (run) {
+        if ((rc = optimize(5, &res->iterations[0], &res->chi2[0]))) return rc;
+        if (!stopped()) {
+            // tag outliers (level 1) and drop the robust kernels (:644-670)
+            if (E) {
+                hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, (uint8_t*)nullptr,
+                                   (double*)nullptr, d_level, 1);
+                ORB_HIP_TRY(hipMemcpyAsync(level.data(), d_level, E, hipMemcpyDeviceToHost, st));
+                ORB_HIP_TRY(hipStreamSynchronize(st));
+            }
+            if ((rc = optimize(10, &res->iterations[1], &res->chi2[1]))) return rc;
+        }
+    }
+    if (E) {
+        hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, d_outl, d_chi,
+                           (uint8_t*)nullptr, 0);
+        ORB_HIP_TRY(hipGetLastError());
+        ORB_HIP_TRY(hipMemcpyAsync(res->edge_outlier, d_outl, E, hipMemcpyDeviceToHost, st));
+        if (res->edge_chi2) ORB_HIP_TRY(hipMemcpyAsync(res->edge_chi2, d_chi, 8 * (size_t)E, hipMemcpyDeviceToHost, st));
+    }
+    std::vector<double> qh(4 * (size_t)P);
+    if (P) {
+        ORB_HIP_TRY(hipMemcpyAsync(qh.data(), b.q, 32 * (size_t)P, hipMemcpyDeviceToHost, st));
+        ORB_HIP_TRY(hipMemcpyAsync(res->pose_t, b.t, 24 * (size_t)P, hipMemcpyDeviceToHost, st));
+    }
+    if (N) ORB_HIP_TRY(hipMemcpyAsync(res->points, b.X, 24 * (size_t)N, hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipStreamSynchronize(st));
+    if (!run)
+        for (int e = 0; e < E; e++) res->edge_outlier[e] = 0;
+    for (int i = 0; i < P; i++) {
+        q_to_R(&qh[4 * i], res->pose_R + 9 * i);
+        if (res->pose_q) std::memcpy(res->pose_q + 4 * i, &qh[4 * i], 32);
+    }
+    return ORB_OK;
+}

@@ -1,0 +1,1365 @@
+// orbx.hip — ORBextractor::Extract as gfx950 HIP kernels.
+//
+// Pipeline for a batch of F frames of identical size (one launch per stage, all frames at once):
+//   1. pyramid_level_kernel  x (nlevels-1): cascaded cv::resize INTER_LINEAR 8U
+//                             (src/ORBextractor.cc:455-470).  Level 0 is the caller's image.
+//   2. fast_cells_kernel     : one workgroup per (frame, 30-px cell): crop -> LDS, FAST-9/16
+//                             corner score, cell-local 3x3 NMS at iniThFAST, retry at minThFAST
+//                             when the cell is empty (DetectFAST :489-540, cv::FAST [ext]).
+//   3. quadtree_kernel       : one workgroup per (frame, level): QuadTreeSuppression (:542-693)
+//                             with the reference's std::list order and libstdc++ introsort ties
+//                             (qt_sort.h); partitions run wave-parallel, list bookkeeping in LDS.
+//   4. describe_kernel       : one wave per kept keypoint: IC_Angle on the raw level (:74-101),
+//                             GaussianBlur 7x7 s2 Q8 REFLECT_101 of the 43x43 neighbourhood in
+//                             LDS (:799), rotated rBRIEF (:103-140) packed with wave ballots,
+//                             octave / size / scale written in the reference's output order.
+// Compiled with -ffp-contract=off so every float expression rounds like the reference's
+// ISO C++14 build (no FMA contraction).
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+#include "qt_sort.h"
+
+namespace orbamd {
+
+constexpr int MAX_LEVELS = 16;
+constexpr int MAX_ZONE = 64;            // max FAST detection-zone side (cellw <= 59 always)
+constexpr int MAX_CROP = MAX_ZONE + 6;
+constexpr int MAX_ROOTS = 32;
+constexpr int PATCH = 43;               // raw neighbourhood: +-21 (rBRIEF reach 18 + blur 3)
+constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
+
+__constant__ int c_pattern[1024] = {
+#include "orb_pattern31.inc"
+};
+__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+__constant__ int c_gauss[7] = {18, 34, 48, 56, 48, 34, 18};   // OpenCV 4.x bit-exact Q8 taps
+__constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+__constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+struct LevelDev {
+    int w, h, stride;
+    long long off;          // byte offset of this level in a frame's pyramid slab (l >= 1)
+    int rx, ry, rw, rh;     // ROI = level inset by BORDER 16 (:755-760)
+    int ncells, cell_base;
+    long long cand_base;    // offset of this level's candidate array in a frame's slab
+    int cand_cap;
+    int quota, out_cap, out_base;
+    int nroots;
+    double hx;
+    float scale, size;
+    long long xtab_off, ytab_off;   // resize coefficient tables (l >= 1)
+};
+
+struct Geom {
+    int nlevels;
+    int ncells_total;
+    long long pyr_frame_bytes;
+    long long slot_frame;     // candidate slots per frame (sum of per-cell capacities)
+    long long cand_frame;     // contiguous candidate entries per frame
+    int out_frame;            // selected keypoints per frame (sum of out_cap)
+    int nfeat_unused;
+    LevelDev lv[MAX_LEVELS];
+};
+
+struct CellDev {
+    int level;
+    int x0y0;     // x0 | y0 << 16 (crop origin, level coords)
+    int zwzh;     // detection zone width | height << 16
+    int slot;     // first slot (per-frame candidate-slot index)
+};
+
+// ------------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+__device__ __forceinline__ int popc64(unsigned long long m) { return __popcll(m); }
+
+__device__ __forceinline__ const uint8_t* level_base(const Geom& g, int l, int f, const uint8_t* in,
+                                                      long long in_fstride, int in_step, const uint8_t* pyr,
+                                                      int* step) {
+    if (l == 0) {
+        *step = in_step;
+        return in + (long long)f * in_fstride;
+    }
+    *step = g.lv[l].stride;
+    return pyr + (long long)f * g.pyr_frame_bytes + g.lv[l].off;
+}
+
+// Wave-inclusive scan of ints (64 lanes).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan for blockDim.x == 256 (4 waves). `tmp` >= 8 ints of LDS.
+__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const int inc = wave_incl_scan(v);
+    if (l == 63) tmp[w] = inc;
+    __syncthreads();
+    int base = 0, tot = 0;
+    const int nw = blockDim.x >> 6;
+    for (int i = 0; i < nw; i++) {
+        if (i < w) base += tmp[i];
+        tot += tmp[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// ------------------------------------------------------------------------------------------
+// 1. pyramid
+// ------------------------------------------------------------------------------------------
+// cv::resize INTER_LINEAR CV_8UC1 [ext]: horizontal 11-bit fixed point (exact int32), vertical
+// with the universal-intrinsics rounding ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2.
+// xtab[dx] = {sx0 | sx1 << 16, a0 | a1 << 16}; ytab[dy] = {sy0 | sy1 << 16, b0 | b1 << 16}.
+__global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const uint8_t* __restrict__ in,
+                                                            long long in_fstride, int in_step, uint8_t* pyr,
+                                                            const int2* __restrict__ xtab,
+                                                            const int2* __restrict__ ytab) {
+    const LevelDev& L = g.lv[l];
+    const int f = blockIdx.y;
+    int sstep;
+    const uint8_t* src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &sstep);
+    uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off;
+    const int2* xt = xtab + L.xtab_off;
+    const int2* yt = ytab + L.ytab_off;
+    const int total = L.w * L.h;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int dy = i / L.w, dx = i - dy * L.w;
+        const int2 xv = xt[dx], yv = yt[dy];
+        const int sx0 = xv.x & 0xffff, sx1 = xv.x >> 16, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
+        const int sy0 = yv.x & 0xffff, sy1 = yv.x >> 16, b0 = yv.y & 0xffff, b1 = yv.y >> 16;
+        const uint8_t* r0 = src + (long long)sy0 * sstep;
+        const uint8_t* r1 = src + (long long)sy1 * sstep;
+        const int h0 = r0[sx0] * a0 + r0[sx1] * a1;
+        const int h1 = r1[sx0] * a0 + r1[sx1] * a1;
+        const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
+        int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+        dst[(long long)dy * L.stride + dx] = (uint8_t)(v > 255 ? 255 : v);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 2. FAST per cell
+// ------------------------------------------------------------------------------------------
+// Corner strength M = max over the 16 nine-pixel arcs and both polarities of min |I_p - I_c|.
+// A pixel is a FAST-9 corner at threshold t iff M > t, and cornerScore<16> == M - 1 for every
+// detected corner (threshold-independent), so one M map serves both the iniThFAST pass and the
+// minThFAST retry of DetectFAST.
+__device__ __forceinline__ int corner_strength(const uint8_t* crop, int cw, int cx, int cy) {
+    const int v = crop[cy * cw + cx];
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - (int)crop[(cy + c_circle_dy[k]) * cw + cx + c_circle_dx[k]];
+    int lo2[16], hi2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        lo2[k] = min(d[k], d[(k + 1) & 15]);
+        hi2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int lo4[16], hi4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        lo4[k] = min(lo2[k], lo2[(k + 2) & 15]);
+        hi4[k] = max(hi2[k], hi2[(k + 2) & 15]);
+    }
+    int M = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int lo8 = min(lo4[k], lo4[(k + 4) & 15]);
+        const int hi8 = max(hi4[k], hi4[(k + 4) & 15]);
+        const int lo9 = min(lo8, d[(k + 8) & 15]);
+        const int hi9 = max(hi8, d[(k + 8) & 15]);
+        M = max(M, max(lo9, -hi9));
+    }
+    return M;
+}
+
+// Cheap necessary test for "corner at threshold t": some 9-run of bright or dark pixels.
+__device__ __forceinline__ bool is_corner_t(const uint8_t* crop, int cw, int cx, int cy, int t) {
+    const int v = crop[cy * cw + cx];
+    unsigned br = 0, dk = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int p = crop[(cy + c_circle_dy[k]) * cw + cx + c_circle_dx[k]];
+        br |= (unsigned)(p > v + t) << k;
+        dk |= (unsigned)(p < v - t) << k;
+    }
+    auto run9 = [](unsigned m) {
+        unsigned x = m | (m << 16);
+        unsigned a = x & (x >> 1);
+        unsigned b = a & (a >> 2);
+        unsigned c = b & (b >> 4);
+        return (c & (x >> 8) & 0xffffu) != 0;
+    };
+    return run9(br) || run9(dk);
+}
+
+__global__ __launch_bounds__(256) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
+                                                         const uint8_t* __restrict__ in, long long in_fstride,
+                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
+                                                         int th_min, uint32_t* __restrict__ slots,
+                                                         int* __restrict__ cell_cnt, uint32_t* fault) {
+    __shared__ uint8_t crop[MAX_CROP * MAX_CROP];
+    __shared__ uint8_t Mz[MAX_ZONE * MAX_ZONE];
+    __shared__ short list[MAX_ZONE * MAX_ZONE];
+    __shared__ int s_nlist, s_nkp, s_wave[8];
+
+    const CellDev cell = cells[blockIdx.x];
+    const int f = blockIdx.y;
+    const int x0 = cell.x0y0 & 0xffff, y0 = cell.x0y0 >> 16;
+    const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
+    const int cw = zw + 6, ch = zh + 6;
+    int step;
+    const uint8_t* img = level_base(g, cell.level, f, in, in_fstride, in_step, pyr, &step);
+
+    if (threadIdx.x == 0) { s_nlist = 0; s_nkp = 0; }
+    for (int i = threadIdx.x; i < cw * ch; i += blockDim.x) {
+        const int r = i / cw, c = i - r * cw;
+        crop[i] = img[(long long)(y0 + r) * step + x0 + c];
+    }
+    const int nz = zw * zh;
+    for (int i = threadIdx.x; i < nz; i += blockDim.x) Mz[i] = 0;
+    __syncthreads();
+
+    // candidates at the lower of the two thresholds, compacted into `list`
+    const int tlo = min(th_ini, th_min);
+    for (int base = 0; base < nz; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        bool c = false;
+        if (i < nz) {
+            const int zy = i / zw, zx = i - zy * zw;
+            c = is_corner_t(crop, cw, zx + 3, zy + 3, tlo);
+        }
+        const unsigned long long m = __ballot(c);
+        int wbase = 0;
+        if (lane_id() == 0 && m) wbase = atomicAdd(&s_nlist, popc64(m));
+        wbase = __shfl(wbase, 0, 64);
+        if (c) list[wbase + popc64(m & lanemask_lt())] = (short)i;
+    }
+    __syncthreads();
+    const int nl = s_nlist;
+    for (int j = threadIdx.x; j < nl; j += blockDim.x) {
+        const int i = list[j];
+        const int zy = i / zw, zx = i - zy * zw;
+        Mz[i] = (uint8_t)min(corner_strength(crop, cw, zx + 3, zy + 3), 255);
+    }
+    __syncthreads();
+
+    // cell-local NMS: neighbours outside the detection zone count as score 0
+    auto is_kp = [&](int i, int t) -> bool {
+        const int m = Mz[i];
+        if (m <= t) return false;
+        const int zy = i / zw, zx = i - zy * zw;
+#pragma unroll
+        for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+            for (int dx = -1; dx <= 1; dx++) {
+                if (!dx && !dy) continue;
+                const int yy = zy + dy, xx = zx + dx;
+                if (yy < 0 || yy >= zh || xx < 0 || xx >= zw) continue;
+                const int q = Mz[yy * zw + xx];
+                if (q > t && q >= m) return false;
+            }
+        return true;
+    };
+    int mine = 0;
+    for (int j = threadIdx.x; j < nl; j += blockDim.x) mine += is_kp(list[j], th_ini);
+    if (mine) atomicAdd(&s_nkp, mine);
+    __syncthreads();
+    const int t = s_nkp > 0 ? th_ini : th_min;
+
+    // emit in row-major order (FAST emits row by row, x ascending)
+    uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
+    const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
+    int running = 0;
+    for (int base = 0; base < nz; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool k = i < nz && is_kp(i, t);
+        const unsigned long long m = __ballot(k);
+        const int w = threadIdx.x >> 6;
+        if (lane_id() == 0) s_wave[w] = popc64(m);
+        __syncthreads();
+        int before = running, tot = 0;
+        for (int q = 0; q < (int)(blockDim.x >> 6); q++) {
+            if (q < w) before += s_wave[q];
+            tot += s_wave[q];
+        }
+        if (k) {
+            const int r = before + popc64(m & lanemask_lt());
+            const int zy = i / zw, zx = i - zy * zw;
+            const uint32_t x = (uint32_t)(x0 + 3 + zx), y = (uint32_t)(y0 + 3 + zy);
+            if (r < cap) out[r] = x | (y << 12) | ((uint32_t)(Mz[i] - 1) << 24);
+        }
+        running += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (running > cap) atomicOr(fault, FAULT_CELL_CAP);
+        cell_cnt[(long long)f * g.ncells_total + blockIdx.x] = min(running, cap);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. quadtree
+// ------------------------------------------------------------------------------------------
+struct QtNode {
+    short tlx, tly, brx, bry;
+    int beg, cnt;
+};
+
+__device__ __forceinline__ int kp_x(uint32_t k) { return (int)(k & 0xfff); }
+__device__ __forceinline__ int kp_y(uint32_t k) { return (int)((k >> 12) & 0xfff); }
+__device__ __forceinline__ int kp_s(uint32_t k) { return (int)(k >> 24); }
+
+// QTreeNode::divide (:404-452): children TL/BR and the stable 4-way split of the node's points.
+__device__ __forceinline__ void qt_child_geom(const QtNode& n, int c, QtNode& ch) {
+    const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;   // TL.x + RoundUp(0.5*(BR.x-TL.x)), d >= 0
+    const int ym = n.tly + (n.bry - n.tly + 1) / 2;
+    ch.tlx = (short)((c & 1) ? xm : n.tlx);
+    ch.brx = (short)((c & 1) ? n.brx : xm);
+    ch.tly = (short)((c & 2) ? ym : n.tly);
+    ch.bry = (short)((c & 2) ? n.bry : ym);
+}
+
+// One wave splits one node: counts per child (returned) and stable scatter into T.
+__device__ int4 qt_wave_split(const QtNode& n, const uint32_t* __restrict__ P, uint32_t* __restrict__ T) {
+    const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
+    const int ym = n.tly + (n.bry - n.tly + 1) / 2;
+    int c[4] = {0, 0, 0, 0};
+    for (int b = 0; b < n.cnt; b += 64) {
+        const int j = b + lane_id();
+        int q = -1;
+        if (j < n.cnt) {
+            const uint32_t k = P[n.beg + j];
+            q = kp_x(k) < xm ? (kp_y(k) < ym ? 0 : 2) : (kp_y(k) < ym ? 1 : 3);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) c[qq] += popc64(__ballot(q == qq));
+    }
+    int o[4] = {n.beg, n.beg + c[0], n.beg + c[0] + c[1], n.beg + c[0] + c[1] + c[2]};
+    for (int b = 0; b < n.cnt; b += 64) {
+        const int j = b + lane_id();
+        int q = -1;
+        uint32_t k = 0;
+        if (j < n.cnt) {
+            k = P[n.beg + j];
+            q = kp_x(k) < xm ? (kp_y(k) < ym ? 0 : 2) : (kp_y(k) < ym ? 1 : 3);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const unsigned long long m = __ballot(q == qq);
+            if (q == qq) T[o[qq] + popc64(m & lanemask_lt())] = k;
+            o[qq] += popc64(m);
+        }
+    }
+    return make_int4(c[0], c[1], c[2], c[3]);
+}
+
+__device__ __forceinline__ int ne4(int4 c) { return (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0); }
+__device__ __forceinline__ int dv4(int4 c) { return (c.x > 1) + (c.y > 1) + (c.z > 1) + (c.w > 1); }
+__device__ __forceinline__ int c4(int4 c, int i) { return i == 0 ? c.x : i == 1 ? c.y : i == 2 ? c.z : c.w; }
+
+// Appends item `j`'s children into the new list (group position `gpos`, children in push_front
+// order c3..c0) and its divisible children into `divs` at `dpos` (child order c0..c3).
+__device__ __forceinline__ void qt_emit_children(const QtNode& parent, int4 cc, int gpos, int dpos, QtNode* nb,
+                                                 QtItem* divs, int NC) {
+    int pos = gpos;
+    for (int c = 3; c >= 0; c--) {
+        const int n = c4(cc, c);
+        if (n <= 0) continue;
+        QtNode ch;
+        qt_child_geom(parent, c, ch);
+        int off = 0;
+        for (int q = 0; q < c; q++) off += c4(cc, q);
+        ch.beg = parent.beg + off;
+        ch.cnt = n;
+        if (pos < NC) nb[pos] = ch;
+        pos++;
+    }
+    // positions: child c sits at gpos + #{nonempty c' > c}
+    int d = dpos;
+    for (int c = 0; c < 4; c++) {
+        const int n = c4(cc, c);
+        if (n <= 1) continue;
+        int above = 0;
+        for (int q = c + 1; q < 4; q++) above += c4(cc, q) > 0;
+        if (d < NC) divs[d] = QtItem{n, gpos + above};
+        d++;
+    }
+}
+
+__global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
+                                                       const uint32_t* __restrict__ slots, const CellDev* cells,
+                                                       uint32_t* __restrict__ Pbuf, uint32_t* __restrict__ Tbuf,
+                                                       uint32_t* __restrict__ sel, int* __restrict__ sel_cnt, int NC,
+                                                       uint32_t* fault) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    QtNode* na = reinterpret_cast<QtNode*>(smem);
+    QtNode* nb = na + NC;
+    int4* cc = reinterpret_cast<int4*>(nb + NC);
+    QtItem* divs = reinterpret_cast<QtItem*>(cc + NC);
+    QtItem* prev = divs + NC;
+    int* ia = reinterpret_cast<int*>(prev + NC);    // per-node scratch (flags / positions)
+    int* ib = ia + NC;
+    __shared__ int tmp[16];
+    __shared__ int s_n, s_ndiv, s_state, s_proc, s_fail;
+    __shared__ int rc[MAX_ROOTS];
+
+    const int l = blockIdx.x, f = blockIdx.y;
+    const LevelDev& L = g.lv[l];
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int* scnt = sel_cnt + f * g.nlevels + l;
+    if (L.rw <= 0 || L.rh <= 0 || L.ncells == 0) {
+        if (threadIdx.x == 0) *scnt = 0;
+        return;
+    }
+    uint32_t* P = Pbuf + (long long)f * g.cand_frame + L.cand_base;
+    uint32_t* T = Tbuf + (long long)f * g.cand_frame + L.cand_base;
+    const int* ccell = cell_cnt + (long long)f * g.ncells_total + L.cell_base;
+    const uint32_t* fslots = slots + (long long)f * g.slot_frame;
+
+    // ---- gather candidates in cell raster order (DetectFAST push_back order)
+    int carry = 0;
+    for (int b = 0; b < L.ncells; b += blockDim.x) {
+        const int i = b + threadIdx.x;
+        const int v = i < L.ncells ? ccell[i] : 0;
+        int tot;
+        const int ex = block_excl_scan(v, tmp, &tot);
+        if (i < L.ncells) {
+            const uint32_t* s = fslots + cells[L.cell_base + i].slot;
+            for (int j = 0; j < v; j++) P[carry + ex + j] = s[j];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    const int n_src = carry;
+    if (n_src == 0) {
+        if (threadIdx.x == 0) *scnt = 0;
+        return;
+    }
+    __syncthreads();
+
+    // ---- root nodes (:547-579): stable partition by root id
+    const int R = L.nroots;
+    if (threadIdx.x < MAX_ROOTS) rc[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_fail = 0;
+    __syncthreads();
+    auto root_of = [&](uint32_t k) -> int {
+        const float dx = (float)kp_x(k) - (float)L.rx;   // keypoint.pt.x - roi.x (float)
+        return (int)((double)dx / L.hx);
+    };
+    if (w == 0) {
+        int counts[MAX_ROOTS];
+        for (int r = 0; r < R; r++) counts[r] = 0;
+        for (int b = 0; b < n_src; b += 64) {
+            const int j = b + lane_id();
+            const int r = j < n_src ? root_of(P[j]) : -1;
+            if (j < n_src && (r < 0 || r >= R)) atomicOr(fault, FAULT_QT_ROOT);
+            for (int q = 0; q < R; q++) counts[q] += popc64(__ballot(r == q));
+        }
+        int o[MAX_ROOTS];
+        int acc = 0;
+        for (int q = 0; q < R; q++) { o[q] = acc; acc += counts[q]; }
+        if (lane_id() == 0) for (int q = 0; q < R; q++) rc[q] = counts[q];
+        for (int b = 0; b < n_src; b += 64) {
+            const int j = b + lane_id();
+            const uint32_t k = j < n_src ? P[j] : 0;
+            const int r = j < n_src ? root_of(k) : -1;
+            for (int q = 0; q < R; q++) {
+                const unsigned long long m = __ballot(r == q);
+                if (r == q) T[o[q] + popc64(m & lanemask_lt())] = k;
+                o[q] += popc64(m);
+            }
+        }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n_src; j += blockDim.x) P[j] = T[j];
+    if (threadIdx.x == 0) {
+        int n = 0, acc = 0;
+        for (int q = 0; q < R; q++) {
+            if (rc[q] > 0) {
+                QtNode r;
+                r.tlx = (short)(int)(L.rx + L.hx * q);
+                r.tly = (short)L.ry;
+                r.brx = (short)(int)(L.rx + L.hx * (q + 1));
+                r.bry = (short)(L.ry + L.rh);
+                r.beg = acc;
+                r.cnt = rc[q];
+                na[n++] = r;
+            }
+            acc += rc[q];
+        }
+        s_n = n;
+        s_state = 0;   // 0 = phase 1, 1 = phase 2, 2 = finished
+        s_ndiv = 0;
+    }
+    __syncthreads();
+
+    const int nfeat = L.quota;
+    // ---- main loop
+    while (true) {
+        const int n = s_n;
+        const int state = s_state;
+        if (state == 2) break;
+        if (state == 0) {
+            // Phase 1 pass (:588-630): split every divisible node in list order.
+            // D positions via compaction
+            int kdiv = 0, nnd = 0;
+            for (int b = 0; b < n; b += blockDim.x) {
+                const int i = b + threadIdx.x;
+                const int dvf = (i < n && na[i].cnt > 1) ? 1 : 0;
+                int tot;
+                const int ex = block_excl_scan(dvf, tmp, &tot);
+                if (i < n) {
+                    if (dvf) ia[kdiv + ex] = i;               // D: divisible, processing order
+                    else ib[i] = nnd + (i - b - ex);          // rank among non-divisible
+                }
+                nnd += min((int)blockDim.x, n - b) - tot;
+                kdiv += tot;
+            }
+            __syncthreads();
+            for (int j = w; j < kdiv; j += nw) {
+                const int4 c = qt_wave_split(na[ia[j]], P, T);
+                if (lane_id() == 0) cc[j] = c;
+            }
+            __syncthreads();
+            // group positions: reverse processing order; divisibles: forward order
+            int ne_carry = 0, dv_carry = 0, ne_total = 0;
+            // total ne first
+            {
+                int part = 0;
+                for (int j = threadIdx.x; j < kdiv; j += blockDim.x) part += ne4(cc[j]);
+                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+                if (lane_id() == 0) tmp[8 + w] = part;
+                __syncthreads();
+                for (int q = 0; q < nw; q++) ne_total += tmp[8 + q];
+                __syncthreads();
+            }
+            for (int b = 0; b < kdiv; b += blockDim.x) {
+                const int j = b + threadIdx.x;
+                const int4 c = j < kdiv ? cc[j] : make_int4(0, 0, 0, 0);
+                int t1, t2;
+                const int ex_ne = block_excl_scan(ne4(c), tmp, &t1);
+                const int ex_dv = block_excl_scan(dv4(c), tmp, &t2);
+                if (j < kdiv) {
+                    const int incl = ne_carry + ex_ne + ne4(c);
+                    const int gpos = ne_total - incl;   // sum of ne over items after j
+                    qt_emit_children(na[ia[j]], c, gpos, dv_carry + ex_dv, nb, divs, NC);
+                }
+                ne_carry += t1;
+                dv_carry += t2;
+            }
+            const int n_new = ne_total + nnd;
+            for (int i = threadIdx.x; i < n; i += blockDim.x)
+                if (na[i].cnt <= 1 && ne_total + ib[i] < NC) nb[ne_total + ib[i]] = na[i];
+            // commit the splits T -> P
+            for (int j = w; j < kdiv; j += nw) {
+                const QtNode& p = na[ia[j]];
+                for (int q = lane_id(); q < p.cnt; q += 64) P[p.beg + q] = T[p.beg + q];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                if (n_new > NC) { s_fail = 1; atomicOr(fault, FAULT_QT_NODES); }
+                s_n = min(n_new, NC);
+                s_ndiv = dv_carry;
+                if (n_new >= nfeat || n_new == n || s_fail) s_state = 2;
+                else if (n_new + 3 * dv_carry > nfeat) s_state = 1;
+            }
+            __syncthreads();
+            QtNode* t = na; na = nb; nb = t;
+        } else {
+            // Phase 2 round (:632-672): split the previous round's divisible nodes, largest
+            // first (std::sort, emulated), stopping as soon as the list reaches nfeat.
+            const int m = s_ndiv;
+            if (threadIdx.x == 0) {
+                for (int j = 0; j < m; j++) prev[j] = divs[j];
+                qt_sort(prev, prev + m);
+            }
+            __syncthreads();
+            for (int j = w; j < m; j += nw) {
+                const int4 c = qt_wave_split(na[prev[j].node], P, T);
+                if (lane_id() == 0) cc[j] = c;
+            }
+            for (int i = threadIdx.x; i < n; i += blockDim.x) ia[i] = 0;   // erased flags
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int count = n, proc = m;
+                for (int j = 0; j < m; j++) {
+                    count += ne4(cc[j]) - 1;
+                    if (count >= nfeat) { proc = j + 1; break; }
+                }
+                s_proc = proc;
+            }
+            __syncthreads();
+            const int proc = s_proc;
+            for (int j = threadIdx.x; j < proc; j += blockDim.x) ia[prev[j].node] = 1;
+            __syncthreads();
+            int ne_total = 0;
+            {
+                int part = 0;
+                for (int j = threadIdx.x; j < proc; j += blockDim.x) part += ne4(cc[j]);
+                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+                if (lane_id() == 0) tmp[8 + w] = part;
+                __syncthreads();
+                for (int q = 0; q < nw; q++) ne_total += tmp[8 + q];
+                __syncthreads();
+            }
+            int ne_carry = 0, dv_carry = 0;
+            for (int b = 0; b < proc; b += blockDim.x) {
+                const int j = b + threadIdx.x;
+                const int4 c = j < proc ? cc[j] : make_int4(0, 0, 0, 0);
+                int t1, t2;
+                const int ex_ne = block_excl_scan(ne4(c), tmp, &t1);
+                const int ex_dv = block_excl_scan(dv4(c), tmp, &t2);
+                if (j < proc) {
+                    const int gpos = ne_total - (ne_carry + ex_ne + ne4(c));
+                    qt_emit_children(na[prev[j].node], c, gpos, dv_carry + ex_dv, nb, divs, NC);
+                }
+                ne_carry += t1;
+                dv_carry += t2;
+            }
+            // survivors keep their order after the new groups
+            int surv = 0;
+            for (int b = 0; b < n; b += blockDim.x) {
+                const int i = b + threadIdx.x;
+                const int keep = (i < n && !ia[i]) ? 1 : 0;
+                int tot;
+                const int ex = block_excl_scan(keep, tmp, &tot);
+                if (keep && ne_total + surv + ex < NC) nb[ne_total + surv + ex] = na[i];
+                surv += tot;
+            }
+            for (int j = w; j < proc; j += nw) {
+                const QtNode& p = na[prev[j].node];
+                for (int q = lane_id(); q < p.cnt; q += 64) P[p.beg + q] = T[p.beg + q];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int n_new = ne_total + surv;
+                if (n_new > NC) { s_fail = 1; atomicOr(fault, FAULT_QT_NODES); }
+                s_n = min(n_new, NC);
+                s_ndiv = dv_carry;
+                if (n_new >= nfeat || n_new == n || s_fail) s_state = 2;
+            }
+            __syncthreads();
+            QtNode* t = na; na = nb; nb = t;
+        }
+    }
+
+    // ---- retain the best point per node (:677-692): strict '>' => first maximum wins
+    const int n = s_n;
+    uint32_t* out = sel + (long long)f * g.out_frame + L.out_base;
+    if (n > L.out_cap && threadIdx.x == 0) atomicOr(fault, FAULT_OUT_CAP);
+    for (int i = w; i < n && i < L.out_cap; i += nw) {
+        const QtNode& nd = na[i];
+        int bs = -1, bj = 0x7fffffff;
+        for (int j = lane_id(); j < nd.cnt; j += 64) {
+            const int s = kp_s(P[nd.beg + j]);
+            if (s > bs) { bs = s; bj = j; }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const int os = __shfl_xor(bs, o, 64), oj = __shfl_xor(bj, o, 64);
+            if (os > bs || (os == bs && oj < bj)) { bs = os; bj = oj; }
+        }
+        if (lane_id() == 0) out[i] = P[nd.beg + bj];
+    }
+    if (threadIdx.x == 0) *scnt = min(n, L.out_cap);
+}
+
+// ------------------------------------------------------------------------------------------
+// 4. orientation + descriptor
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float fast_atan2_dev(float y, float x) {
+    const float k = (float)(180 / M_PI);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+__global__ __launch_bounds__(256) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
+                                                       int in_step, const uint8_t* __restrict__ pyr,
+                                                       const uint32_t* __restrict__ sel,
+                                                       const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
+                                                       uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
+                                                       int cap) {
+    __shared__ uint8_t raw[4][PATCH * PATCH + 15];
+    __shared__ uint16_t hb[4][PATCH * HBLUR_W];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int f = blockIdx.y;
+    const int s = blockIdx.x * 4 + w;
+    const int* cnt = sel_cnt + f * g.nlevels;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int tot = 0;
+        for (int q = 0; q < g.nlevels; q++) tot += cnt[q];
+        counts[f] = tot;
+    }
+    int l = 0;
+    if (s < g.out_frame)
+        while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_base) l++;
+    const LevelDev& L = g.lv[l];
+    const int i = s - L.out_base;
+    int oidx = i;
+    for (int q = 0; q < l; q++) oidx += cnt[q];
+    const bool valid = s < g.out_frame && i < cnt[l] && oidx < cap;   // wave-uniform
+
+    uint32_t k = 0;
+    if (valid) k = sel[(long long)f * g.out_frame + s];
+    const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
+    int step;
+    const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
+    uint8_t* R = raw[w];
+    if (valid)
+        for (int q = lane; q < PATCH * PATCH; q += 64) {
+            const int r = q / PATCH, c = q - r * PATCH;
+            const int yy = reflect101(ky - 21 + r, L.h), xx = reflect101(kx - 21 + c, L.w);
+            R[q] = img[(long long)yy * step + xx];
+        }
+    __syncthreads();
+
+    // IC_Angle on the unblurred level, patch centre (21, 21)
+    int m10 = 0, m01 = 0;
+    for (int q = lane; q < 31; q += 64) m10 += (q - 15) * R[21 * PATCH + 6 + q];
+    for (int q = lane; q < 15 * 31; q += 64) {
+        const int v = q / 31 + 1, u = q % 31 - 15;
+        if (u < -c_umax[v] || u > c_umax[v]) continue;
+        const int vp = R[(21 + v) * PATCH + 21 + u], vm = R[(21 - v) * PATCH + 21 + u];
+        m01 += v * (vp - vm);
+        m10 += u * (vp + vm);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        m10 += __shfl_xor(m10, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
+    const float angle = fast_atan2_dev((float)m01, (float)m10);
+
+    // horizontal Q8 blur of rows 0..42, columns kx-18..kx+18
+    uint16_t* H = hb[w];
+    for (int q = lane; q < PATCH * HBLUR_W; q += 64) {
+        const int r = q / HBLUR_W, c = q - r * HBLUR_W;
+        const uint8_t* rr = R + r * PATCH + c;
+        int acc = 0;
+#pragma unroll
+        for (int t = 0; t < 7; t++) acc += c_gauss[t] * rr[t];
+        H[q] = (uint16_t)acc;
+    }
+    __syncthreads();
+    if (!valid) return;
+
+    const float factorPI = (float)(M_PI / 180.f);
+    const float ang = angle * factorPI;
+    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+    auto sample = [&](int idx) -> int {
+        const float x = (float)c_pattern[2 * idx], y = (float)c_pattern[2 * idx + 1];
+        const int dy = (int)rintf(x * b + y * a);
+        const int dx = (int)rintf(x * a - y * b);
+        const uint16_t* col = H + (21 + dy - 3) * HBLUR_W + 18 + dx;
+        unsigned acc = 0;
+#pragma unroll
+        for (int t = 0; t < 7; t++) acc += (unsigned)c_gauss[t] * col[t * HBLUR_W];
+        return (int)((acc + (1u << 15)) >> 16);
+    };
+    unsigned long long words[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int p = r * 64 + lane;
+        const bool bit = sample(2 * p) < sample(2 * p + 1);
+        words[r] = __ballot(bit);
+    }
+    const long long o = (long long)f * cap + oidx;
+    if (lane < 4) {
+        unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = wv;
+    }
+    if (lane == 0) {
+        orbx_keypoint kp;
+        kp.x = l > 0 ? (float)kx * L.scale : (float)kx;
+        kp.y = l > 0 ? (float)ky * L.scale : (float)ky;
+        kp.size = L.size;
+        kp.angle = angle;
+        kp.response = (float)score;
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[o] = kp;
+    }
+}
+
+}  // namespace orbamd
+
+// ==============================================================================================
+// Host side: extractor object and C-ABI
+// ==============================================================================================
+using namespace orbamd;
+
+struct orbx_extractor {
+    orbx_params p;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> quota;
+    std::mutex mu;   // one instance is not re-entrant (as the reference's mutable members)
+
+    // geometry for the current image size
+    int g_rows = -1, g_cols = -1;
+    Geom geom;
+    std::vector<CellDev> cells;
+    int NC = 0;
+    size_t qt_lds = 0;
+    DevBuf d_cells, d_xtab, d_ytab;
+
+    // workspace for up to ws_frames frames
+    int ws_frames = 0;
+    DevBuf d_pyr, d_slots, d_cellcnt, d_P, d_T, d_sel, d_selcnt, d_fault;
+    // single-frame host API buffers
+    DevBuf d_img, d_kps, d_desc, d_counts;
+    // stage profiling (events on the launch stream)
+    bool prof = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[4];
+    std::vector<hipEvent_t> ev_pool;
+    // last batch (for GetImagePyramid)
+    const uint8_t* last_in = nullptr;
+    long long last_fstride = 0;
+    size_t last_step = 0;
+    int last_frames = 0;
+};
+
+static int cv_round_d(double v) { return (int)std::lrint(v); }
+static int cv_round_f(float v) { return (int)std::lrintf(v); }
+
+static void compute_tables(orbx_extractor* h) {
+    const orbx_params& p = h->p;
+    const int L = p.nlevels;
+    h->scale.resize(L); h->inv_scale.resize(L); h->sigma2.resize(L); h->inv_sigma2.resize(L);
+    h->quota.resize(L);
+    float s = 1.f;
+    for (int l = 0; l < L; l++) {   // ORBextractor::Init (:728-737)
+        h->scale[l] = s;
+        h->inv_scale[l] = 1.f / s;
+        h->sigma2[l] = s * s;
+        h->inv_sigma2[l] = 1.f / (s * s);
+        s *= p.scaleFactor;
+    }
+    const double factor = 1 / p.scaleFactor;   // ComputeNumFeaturesPerScale (:472-487)
+    double nf = p.nfeatures * (1 - factor) / (1 - std::pow(factor, L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; l++) {
+        h->quota[l] = cv_round_d(nf);
+        sum += h->quota[l];
+        nf *= factor;
+    }
+    h->quota[L - 1] = std::max(p.nfeatures - sum, 0);
+}
+
+// Level sizes, resize tables, FAST cell grid, buffer layout for a rows x cols input.
+static int setup_geometry(orbx_extractor* h, int rows, int cols) {
+    if (h->g_rows == rows && h->g_cols == cols) return ORB_OK;
+    const int Lc = h->p.nlevels;
+    Geom g;
+    std::memset(&g, 0, sizeof(g));
+    g.nlevels = Lc;
+    std::vector<int2> xtab, ytab;
+    std::vector<CellDev> cells;
+    long long pyr_off = 0, slot = 0, cand = 0;
+    int out = 0, NC = 64;
+    int prev_w = cols, prev_h = rows;
+    for (int l = 0; l < Lc; l++) {
+        LevelDev& L = g.lv[l];
+        if (l == 0) {
+            L.w = cols; L.h = rows; L.stride = cols; L.off = -1;
+        } else {
+            L.h = cv_round_f(h->inv_scale[l] * rows);
+            L.w = cv_round_f(h->inv_scale[l] * cols);
+            if (L.w <= 0 || L.h <= 0) {
+                set_error("pyramid level collapses to zero size");
+                return ORB_EINVAL;
+            }
+            L.stride = (int)align_up(L.w, 16);
+            L.off = pyr_off;
+            pyr_off += (long long)align_up((size_t)L.stride * L.h, 256);
+            // cv::resize tables (same arithmetic as the oracle / OpenCV)
+            const int sw = prev_w, sh = prev_h, dw = L.w, dh = L.h;
+            const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+            L.xtab_off = (long long)xtab.size();
+            L.ytab_off = (long long)ytab.size();
+            int xmax = dw;
+            std::vector<int> sxs(dw), a0s(dw), a1s(dw);
+            for (int dx = 0; dx < dw; dx++) {
+                float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                int sx = (int)std::floor(fx);
+                fx -= sx;
+                if (sx < 0) { fx = 0; sx = 0; }
+                if (sx + 1 >= sw) {
+                    xmax = std::min(xmax, dx);
+                    if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+                }
+                sxs[dx] = sx;
+                a0s[dx] = std::min(std::max(cv_round_f((1.f - fx) * 2048), -32768), 32767);
+                a1s[dx] = std::min(std::max(cv_round_f(fx * 2048), -32768), 32767);
+            }
+            for (int dx = 0; dx < dw; dx++) {
+                int sx0 = sxs[dx], sx1 = std::min(sxs[dx] + 1, sw - 1), a0 = a0s[dx], a1 = a1s[dx];
+                if (dx >= xmax) { sx1 = sx0; a0 = 2048; a1 = 0; }
+                xtab.push_back(make_int2(sx0 | (sx1 << 16), (a0 & 0xffff) | (a1 << 16)));
+            }
+            for (int dy = 0; dy < dh; dy++) {
+                float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                int sy = (int)std::floor(fy);
+                fy -= sy;
+                const int b0 = std::min(std::max(cv_round_f((1.f - fy) * 2048), -32768), 32767);
+                const int b1 = std::min(std::max(cv_round_f(fy * 2048), -32768), 32767);
+                auto clip = [&](int y) { return y < 0 ? 0 : (y >= sh ? sh - 1 : y); };
+                ytab.push_back(make_int2(clip(sy) | (clip(sy + 1) << 16), (b0 & 0xffff) | (b1 << 16)));
+            }
+        }
+        if (L.w >= 4096 || L.h >= 4096) {
+            set_error("image dimensions must be < 4096");
+            return ORB_EINVAL;
+        }
+        prev_w = L.w; prev_h = L.h;
+        L.rx = 16; L.ry = 16; L.rw = L.w - 32; L.rh = L.h - 32;
+        L.scale = h->scale[l];
+        L.size = h->scale[l] * 31;
+        L.quota = h->quota[l];
+        L.cell_base = (int)cells.size();
+        L.ncells = 0;
+        L.cand_base = cand;
+        L.cand_cap = 0;
+        L.nroots = 0;
+        L.out_base = out;
+        L.out_cap = 0;
+        if (L.rw > 0 && L.rh > 0) {
+            const int gridw = L.rw / 30, gridh = L.rh / 30;
+            if (gridw > 0 && gridh > 0) {
+                const int cellw = (int)std::ceil(1. * L.rw / gridw), cellh = (int)std::ceil(1. * L.rh / gridh);
+                const int maxx = L.rx + L.rw, maxy = L.ry + L.rh;
+                for (int cy = 0, y0 = L.ry; cy < gridh && y0 + 6 < maxy; cy++, y0 += cellh)
+                    for (int cx = 0, x0 = L.rx; cx < gridw && x0 + 6 < maxx; cx++, x0 += cellw) {
+                        const int y1 = std::min(y0 + cellh + 6, maxy), x1 = std::min(x0 + cellw + 6, maxx);
+                        const int zw = x1 - x0 - 6, zh = y1 - y0 - 6;
+                        if (zw > MAX_ZONE || zh > MAX_ZONE) {
+                            set_error("FAST cell larger than supported zone");
+                            return ORB_EINVAL;
+                        }
+                        CellDev c;
+                        c.level = l;
+                        c.x0y0 = x0 | (y0 << 16);
+                        c.zwzh = zw | (zh << 16);
+                        c.slot = (int)slot;
+                        const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
+                        slot += cap;
+                        L.cand_cap += cap;
+                        cells.push_back(c);
+                        L.ncells++;
+                    }
+                L.nroots = cv_round_d(1. * L.rw / L.rh);
+                if (L.nroots <= 0 || L.nroots > MAX_ROOTS) {
+                    set_error("unsupported aspect ratio (quadtree root count)");
+                    return ORB_EINVAL;
+                }
+                L.hx = 1. * L.rw / L.nroots;
+                L.out_cap = std::max(L.quota + 3, 4 * L.nroots) + 1;
+                NC = std::max(NC, L.out_cap + 8);
+            }
+        }
+        cand += L.cand_cap;
+        out += L.out_cap;
+    }
+    g.ncells_total = (int)cells.size();
+    g.pyr_frame_bytes = std::max<long long>(pyr_off, 256);
+    g.slot_frame = std::max<long long>(slot, 1);
+    g.cand_frame = std::max<long long>(cand, 1);
+    g.out_frame = std::max(out, 1);
+    NC = (int)align_up(NC, 64);
+    const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int));
+    if (lds > 60 * 1024) {
+        set_error("nfeatures too large for the quadtree LDS budget");
+        return ORB_EINVAL;
+    }
+    int rc;
+    if ((rc = h->d_cells.reserve(std::max<size_t>(1, cells.size()) * sizeof(CellDev)))) return rc;
+    if ((rc = h->d_xtab.reserve(std::max<size_t>(1, xtab.size()) * sizeof(int2)))) return rc;
+    if ((rc = h->d_ytab.reserve(std::max<size_t>(1, ytab.size()) * sizeof(int2)))) return rc;
+    if (!cells.empty())
+        ORB_HIP_TRY(hipMemcpy(h->d_cells.ptr, cells.data(), cells.size() * sizeof(CellDev), hipMemcpyHostToDevice));
+    if (!xtab.empty())
+        ORB_HIP_TRY(hipMemcpy(h->d_xtab.ptr, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice));
+    if (!ytab.empty())
+        ORB_HIP_TRY(hipMemcpy(h->d_ytab.ptr, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice));
+    h->geom = g;
+    h->cells = cells;
+    h->NC = NC;
+    h->qt_lds = lds;
+    h->g_rows = rows;
+    h->g_cols = cols;
+    h->ws_frames = 0;   // force workspace re-layout
+    return ORB_OK;
+}
+
+static int reserve_workspace(orbx_extractor* h, int frames) {
+    if (frames <= h->ws_frames) return ORB_OK;
+    const Geom& g = h->geom;
+    int rc;
+    if ((rc = h->d_pyr.reserve((size_t)frames * g.pyr_frame_bytes))) return rc;
+    if ((rc = h->d_slots.reserve((size_t)frames * g.slot_frame * 4))) return rc;
+    if ((rc = h->d_cellcnt.reserve((size_t)frames * std::max(1, g.ncells_total) * 4))) return rc;
+    if ((rc = h->d_P.reserve((size_t)frames * g.cand_frame * 4))) return rc;
+    if ((rc = h->d_T.reserve((size_t)frames * g.cand_frame * 4))) return rc;
+    if ((rc = h->d_sel.reserve((size_t)frames * g.out_frame * 4))) return rc;
+    if ((rc = h->d_selcnt.reserve((size_t)frames * g.nlevels * 4))) return rc;
+    if ((rc = h->d_fault.reserve(16))) return rc;
+    ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));
+    h->ws_frames = frames;
+    return ORB_OK;
+}
+
+static hipEvent_t prof_event(orbx_extractor* h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct StageMark {
+    orbx_extractor* h;
+    hipStream_t st;
+    int stage;
+    hipEvent_t a = nullptr;
+    StageMark(orbx_extractor* h_, hipStream_t s, int k) : h(h_), st(s), stage(k) {
+        if (h->prof) {
+            a = prof_event(h);
+            (void)hipEventRecord(a, st);
+        }
+    }
+    ~StageMark() {
+        if (h->prof) {
+            hipEvent_t b = prof_event(h);
+            (void)hipEventRecord(b, st);
+            h->prof_ev[stage].push_back({a, b});
+        }
+    }
+};
+
+static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long long fstride, int step,
+                        orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st) {
+    const Geom& g = h->geom;
+    uint8_t* pyr = h->d_pyr.as<uint8_t>();
+    {
+    StageMark m0(h, st, 0);
+    for (int l = 1; l < g.nlevels; l++) {
+        const int total = g.lv[l].w * g.lv[l].h;
+        dim3 grid((unsigned)std::min(1024, (total + 255) / 256), (unsigned)F);
+        hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
+                           h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
+    }
+    }
+    uint32_t* fault = h->d_fault.as<uint32_t>();
+    if (g.ncells_total > 0) {
+        StageMark m1(h, st, 1);
+        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)g.ncells_total, (unsigned)F), dim3(256), 0, st, g,
+                           h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST, h->p.minThFAST,
+                           h->d_slots.as<uint32_t>(), h->d_cellcnt.as<int>(), fault);
+    }
+    {
+    StageMark m2(h, st, 2);
+    hipLaunchKernelGGL(quadtree_kernel, dim3((unsigned)g.nlevels, (unsigned)F), dim3(256), h->qt_lds, st, g,
+                       h->d_cellcnt.as<int>(), h->d_slots.as<uint32_t>(), h->d_cells.as<CellDev>(),
+                       h->d_P.as<uint32_t>(), h->d_T.as<uint32_t>(), h->d_sel.as<uint32_t>(), h->d_selcnt.as<int>(),
+                       h->NC, fault);
+    }
+    {
+    StageMark m3(h, st, 3);
+    hipLaunchKernelGGL(describe_kernel, dim3((unsigned)((g.out_frame + 3) / 4), (unsigned)F), dim3(256), 0, st, g,
+                       d_imgs, fstride, step, pyr, h->d_sel.as<uint32_t>(), h->d_selcnt.as<int>(), d_kps, d_desc,
+                       d_counts, cap);
+    }
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+static int check_fault(orbx_extractor* h) {
+    uint32_t f = 0;
+    ORB_HIP_TRY(hipMemcpy(&f, h->d_fault.ptr, 4, hipMemcpyDeviceToHost));
+    if (f) {
+        ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 4));
+        set_error("device capacity check failed (fault mask " + std::to_string(f) + ")");
+        return ORB_EINTERNAL;
+    }
+    return ORB_OK;
+}
+
+extern "C" {
+
+int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
+    ORB_CHECK_ARG(params && out, "null argument");
+    ORB_CHECK_ARG(params->nlevels >= 1 && params->nlevels <= MAX_LEVELS, "nlevels must be in [1,16]");
+    ORB_CHECK_ARG(params->nfeatures >= 0 && params->scaleFactor > 1.0f, "bad nfeatures / scaleFactor");
+    int ndev = 0;
+    ORB_HIP_TRY(hipGetDeviceCount(&ndev));
+    ORB_CHECK_ARG(device >= 0 && device < ndev, "no such HIP device");
+    ORB_HIP_TRY(hipSetDevice(device));
+    orbx_extractor* h = new orbx_extractor();
+    h->p = *params;
+    h->device = device;
+    compute_tables(h);
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete h;
+        set_error(std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        return ORB_EHIP;
+    }
+    *out = h;
+    return ORB_OK;
+}
+
+int orbx_destroy(orbx_extractor* h) {
+    if (!h) return ORB_OK;
+    (void)hipSetDevice(h->device);
+    DevBuf* bufs[] = {&h->d_cells, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
+                      &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
+                      &h->d_counts};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& v : h->prof_ev)
+        for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return ORB_OK;
+}
+
+int orbx_scale_tables(const orbx_extractor* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                      int32_t* features_per_level) {
+    ORB_CHECK_ARG(h, "null extractor");
+    for (int l = 0; l < h->p.nlevels; l++) {
+        if (scale) scale[l] = h->scale[l];
+        if (inv_scale) inv_scale[l] = h->inv_scale[l];
+        if (sigma2) sigma2[l] = h->sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = h->inv_sigma2[l];
+        if (features_per_level) features_per_level[l] = h->quota[l];
+    }
+    return ORB_OK;
+}
+
+int orbx_max_keypoints(const orbx_extractor* hc, int rows, int cols, int32_t* cap) {
+    ORB_CHECK_ARG(hc && cap && rows > 0 && cols > 0, "bad argument");
+    orbx_extractor* h = const_cast<orbx_extractor*>(hc);
+    std::lock_guard<std::mutex> lk(h->mu);
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    int rc = setup_geometry(h, rows, cols);
+    if (rc) return rc;
+    int c = 0;
+    for (int l = 0; l < h->geom.nlevels; l++) c += h->geom.lv[l].out_cap;
+    *cap = c;
+    return ORB_OK;
+}
+
+int orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int n_frames, int rows, int cols,
+                              size_t frame_stride, size_t step, orbx_keypoint* d_kps, uint8_t* d_desc,
+                              int32_t* d_counts, int cap, void* stream) {
+    ORB_CHECK_ARG(h && d_imgs && d_kps && d_desc && d_counts, "null argument");
+    ORB_CHECK_ARG(n_frames > 0 && n_frames <= 65535 && rows > 0 && cols > 0, "bad batch shape");
+    ORB_CHECK_ARG(step >= (size_t)cols && step < (1u << 31), "bad row step");
+    std::lock_guard<std::mutex> lk(h->mu);
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    int rc = setup_geometry(h, rows, cols);
+    if (rc) return rc;
+    int need = 0;
+    for (int l = 0; l < h->geom.nlevels; l++) need += h->geom.lv[l].out_cap;
+    if (cap < need) {
+        set_error("cap < orbx_max_keypoints()");
+        return ORB_ECAP;
+    }
+    if ((rc = reserve_workspace(h, n_frames))) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    h->last_in = d_imgs;
+    h->last_fstride = (long long)frame_stride;
+    h->last_step = step;
+    h->last_frames = n_frames;
+    return launch_batch(h, d_imgs, n_frames, (long long)frame_stride, (int)step, d_kps, d_desc, d_counts, cap, st);
+}
+
+int orbx_extract(orbx_extractor* h, const uint8_t* img, int rows, int cols, size_t step, orbx_keypoint* kps,
+                 uint8_t* desc, int cap, int* n) {
+    ORB_CHECK_ARG(h && img && n, "null argument");
+    ORB_CHECK_ARG(rows > 0 && cols > 0 && step >= (size_t)cols, "image must be a non-empty CV_8U matrix");
+    std::lock_guard<std::mutex> lk(h->mu);
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    int rc = setup_geometry(h, rows, cols);
+    if (rc) return rc;
+    int kcap = 0;
+    for (int l = 0; l < h->geom.nlevels; l++) kcap += h->geom.lv[l].out_cap;
+    if ((rc = reserve_workspace(h, 1))) return rc;
+    if ((rc = h->d_img.reserve((size_t)rows * cols))) return rc;
+    if ((rc = h->d_kps.reserve((size_t)kcap * sizeof(orbx_keypoint)))) return rc;
+    if ((rc = h->d_desc.reserve((size_t)kcap * 32))) return rc;
+    if ((rc = h->d_counts.reserve(16))) return rc;
+    hipStream_t st = h->stream;
+    ORB_HIP_TRY(hipMemcpy2DAsync(h->d_img.ptr, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+    h->last_in = h->d_img.as<uint8_t>();
+    h->last_fstride = (long long)rows * cols;
+    h->last_step = cols;
+    h->last_frames = 1;
+    rc = launch_batch(h, h->d_img.as<uint8_t>(), 1, (long long)rows * cols, cols, h->d_kps.as<orbx_keypoint>(),
+                      h->d_desc.as<uint8_t>(), h->d_counts.as<int32_t>(), kcap, st);
+    if (rc) return rc;
+    int32_t total = 0;
+    ORB_HIP_TRY(hipMemcpyAsync(&total, h->d_counts.ptr, 4, hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = check_fault(h))) return rc;
+    *n = total;
+    if (total == 0) return ORB_OK;   // reference: keypoints left untouched (:778-782)
+    if (total > cap) {
+        set_error("output capacity too small");
+        return ORB_ECAP;
+    }
+    ORB_CHECK_ARG(kps && desc, "null output");
+    ORB_HIP_TRY(hipMemcpyAsync(kps, h->d_kps.ptr, (size_t)total * sizeof(orbx_keypoint), hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipMemcpyAsync(desc, h->d_desc.ptr, (size_t)total * 32, hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipStreamSynchronize(st));
+    return ORB_OK;
+}
+
+int orbx_pyramid_device(const orbx_extractor* h, int frame, int level, const uint8_t** ptr, int* rows, int* cols,
+                        size_t* step) {
+    ORB_CHECK_ARG(h && ptr && h->last_in, "no extraction has run");
+    ORB_CHECK_ARG(frame >= 0 && frame < h->last_frames && level >= 0 && level < h->geom.nlevels, "bad index");
+    const LevelDev& L = h->geom.lv[level];
+    if (level == 0) {
+        *ptr = h->last_in + (long long)frame * h->last_fstride;
+        if (step) *step = h->last_step;
+    } else {
+        *ptr = h->d_pyr.as<uint8_t>() + (long long)frame * h->geom.pyr_frame_bytes + L.off;
+        if (step) *step = (size_t)L.stride;
+    }
+    if (rows) *rows = L.h;
+    if (cols) *cols = L.w;
+    return ORB_OK;
+}
+
+int orbx_pyramid_level(const orbx_extractor* h, int level, uint8_t* dst, size_t dst_step, int* rows, int* cols) {
+    const uint8_t* p = nullptr;
+    int r = 0, c = 0;
+    size_t st = 0;
+    int rc = orbx_pyramid_device(h, 0, level, &p, &r, &c, &st);
+    if (rc) return rc;
+    if (rows) *rows = r;
+    if (cols) *cols = c;
+    if (!dst) return ORB_OK;
+    ORB_CHECK_ARG(dst_step >= (size_t)c, "dst_step too small");
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    ORB_HIP_TRY(hipStreamSynchronize(h->stream));
+    ORB_HIP_TRY(hipMemcpy2D(dst, dst_step, p, st, c, r, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbx_debug_level_candidates(const orbx_extractor* h, int frame, int level, uint32_t* out, int cap, int* n) {
+    ORB_CHECK_ARG(h && n && h->last_frames > 0, "no extraction has run");
+    ORB_CHECK_ARG(frame >= 0 && frame < h->last_frames && level >= 0 && level < h->geom.nlevels, "bad index");
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    ORB_HIP_TRY(hipDeviceSynchronize());
+    const Geom& g = h->geom;
+    const LevelDev& L = g.lv[level];
+    std::vector<int> cnt(std::max(1, L.ncells));
+    if (L.ncells)
+        ORB_HIP_TRY(hipMemcpy(cnt.data(), h->d_cellcnt.as<int>() + (long long)frame * g.ncells_total + L.cell_base,
+                              4 * (size_t)L.ncells, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> slots((size_t)g.slot_frame);
+    ORB_HIP_TRY(hipMemcpy(slots.data(), h->d_slots.as<uint32_t>() + (long long)frame * g.slot_frame,
+                          4 * (size_t)g.slot_frame, hipMemcpyDeviceToHost));
+    int m = 0;
+    for (int c = 0; c < L.ncells; c++) {
+        const CellDev& cd = h->cells[L.cell_base + c];
+        for (int j = 0; j < cnt[c]; j++) {
+            if (out && m < cap) out[m] = slots[cd.slot + j];
+            m++;
+        }
+    }
+    *n = m;
+    return ORB_OK;
+}
+
+int orbx_debug_level_selected(const orbx_extractor* h, int frame, int level, uint32_t* out, int cap, int* n) {
+    ORB_CHECK_ARG(h && n && h->last_frames > 0, "no extraction has run");
+    ORB_CHECK_ARG(frame >= 0 && frame < h->last_frames && level >= 0 && level < h->geom.nlevels, "bad index");
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    ORB_HIP_TRY(hipDeviceSynchronize());
+    const Geom& g = h->geom;
+    int c = 0;
+    ORB_HIP_TRY(hipMemcpy(&c, h->d_selcnt.as<int>() + frame * g.nlevels + level, 4, hipMemcpyDeviceToHost));
+    *n = c;
+    if (out && c > 0)
+        ORB_HIP_TRY(hipMemcpy(out, h->d_sel.as<uint32_t>() + (long long)frame * g.out_frame + g.lv[level].out_base,
+                              4 * (size_t)std::min(c, cap), hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbx_profile_enable(orbx_extractor* h, int enable) {
+    ORB_CHECK_ARG(h, "null extractor");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->prof = enable != 0;
+    return ORB_OK;
+}
+
+int orbx_profile_read(orbx_extractor* h, double* ms, int32_t* launches) {
+    ORB_CHECK_ARG(h, "null extractor");
+    std::lock_guard<std::mutex> lk(h->mu);
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    for (int k = 0; k < 4; k++) {
+        double tot = 0;
+        for (auto& pr : h->prof_ev[k]) {
+            ORB_HIP_TRY(hipEventSynchronize(pr.second));
+            float t = 0;
+            ORB_HIP_TRY(hipEventElapsedTime(&t, pr.first, pr.second));
+            tot += t;
+            h->ev_pool.push_back(pr.first);
+            h->ev_pool.push_back(pr.second);
+        }
+        if (ms) ms[k] = tot;
+        if (launches) launches[k] = (int32_t)h->prof_ev[k].size();
+        h->prof_ev[k].clear();
+    }
+    return ORB_OK;
+}
+
+}  // extern "C"

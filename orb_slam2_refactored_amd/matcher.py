@@ -1,0 +1,80 @@
+"""ORBmatcher mirror for the Hamming hot loops (include/ORBmatcher.h, src/ORBmatcher.cc)."""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import TriFrame, check, lib, ptr, stream_ptr, tptr
+
+TH_HIGH = 100   # src/ORBmatcher.cc:41
+TH_LOW = 50     # src/ORBmatcher.cc:42
+HISTO_LENGTH = 30
+
+
+class ORBmatcher:
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True):
+        self.fNNRatio_ = float(nnratio)
+        self.checkOrientation_ = bool(checkOri)
+
+    @staticmethod
+    def DescriptorDistance(a, b) -> int:
+        """static int DescriptorDistance(const cv::Mat&, const cv::Mat&) (src/ORBmatcher.cc:1449-1457)."""
+        a = np.ascontiguousarray(a, np.uint8).reshape(32)
+        b = np.ascontiguousarray(b, np.uint8).reshape(32)
+        return lib().orbm_descriptor_distance(ptr(a), ptr(b))
+
+    def MatchBruteForce(self, descA, descB, th_low: int = TH_LOW):
+        """Best / second-best search of every row of A over all rows of B with the reference loop
+        semantics (src/ORBmatcher.cc:477-507).  Returns (best_idx, best, second, match)."""
+        A = np.ascontiguousarray(descA, np.uint8).reshape(-1, 32)
+        B = np.ascontiguousarray(descB, np.uint8).reshape(-1, 32)
+        nA = len(A)
+        bi, bd, sd, m = (np.zeros(nA, np.int32) for _ in range(4))
+        check(lib().orbm_bf_match(ptr(A), nA, ptr(B), len(B), C.c_float(self.fNNRatio_), th_low, ptr(bi), ptr(bd),
+                                  ptr(sd), ptr(m)), "orbm_bf_match")
+        return bi, bd, sd, m
+
+    def match_batch_device(self, descA, nA, descB, nB, th_low: int = TH_LOW, out=None, stream=None):
+        """Batched pairs on the GPU: descA [P, capA, 32], nA [P] int32, descB [P, capB, 32], nB [P].
+        Returns int32 tensor [4, P, capA] = (best_idx, best, second, match)."""
+        import torch
+        P, capA = descA.shape[0], descA.shape[1]
+        if out is None:
+            out = torch.empty((4, P, capA), dtype=torch.int32, device=descA.device)
+        check(lib().orbm_bf_match_batch_device(tptr(descA), tptr(nA), capA, tptr(descB), tptr(nB), descB.shape[1], P,
+                                               C.c_float(self.fNNRatio_), th_low, tptr(out[0]), tptr(out[1]),
+                                               tptr(out[2]), tptr(out[3]), stream_ptr(stream)),
+              "orbm_bf_match_batch_device")
+        return out
+
+    def SearchForTriangulation(self, kf1, kf2, F12, onlyStereo: bool = False):
+        """int SearchForTriangulation(kf1, kf2, F12, matchIds, onlyStereo) (src/ORBmatcher.cc:768-866).
+
+        kf1/kf2: dicts with keys xy [N,2] f32, octave [N], uright [N], has_mappoint [N] bool,
+        desc [N,32] u8, fv = (node_ids ascending, offsets, indices) (DBoW2 FeatureVector as CSR),
+        scale_factors [L], sigma2 [L] (kf2's pyramid), ep2 = projection of kf1's centre in kf2
+        (computed by the caller, :772-773).  Returns the (idx1, idx2) pairs sorted by idx1."""
+        keep = []
+
+        def k(a, dt):
+            a = np.ascontiguousarray(a, dt)
+            keep.append(a)
+            return ptr(a)
+
+        def frame(kf):
+            ids, off, idx = kf["fv"]
+            return TriFrame(len(kf["xy"]), k(kf["xy"], np.float32), k(kf["octave"], np.int32),
+                            k(kf["uright"], np.float32), k(kf["has_mappoint"], np.uint8), k(kf["desc"], np.uint8),
+                            len(ids), k(ids, np.uint32), k(off, np.int32), k(idx, np.int32))
+
+        f1, f2 = frame(kf1), frame(kf2)
+        n1 = f1.n
+        out = np.zeros(max(n1, 1), np.int32)
+        nm = C.c_int32(0)
+        L = len(kf2["scale_factors"])
+        check(lib().orbm_search_for_triangulation(C.byref(f1), C.byref(f2), k(F12, np.float32), k(kf2["ep2"], np.float32),
+                                                  k(kf2["scale_factors"], np.float32), k(kf2["sigma2"], np.float32),
+                                                  L, int(onlyStereo), ptr(out), C.byref(nm)),
+              "orbm_search_for_triangulation")
+        out = out[:n1]
+        idx1 = np.nonzero(out >= 0)[0]
+        return [(int(i), int(out[i])) for i in idx1], out

@@ -1,0 +1,124 @@
+"""Seeded synthetic inputs.  No datasets are available offline.
+
+G(seed, W, H): background 128, 300 filled axis-aligned rectangles with uniform random
+corners and uniform gray level 0..255 painted in order, plus i.i.d. integer noise U{-6..6},
+clipped to u8.  Rectangle corners give FAST corners at every pyramid level.
+"""
+import numpy as np
+
+
+def synth_image(seed: int, width: int, height: int, n_rects: int = 300) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    img = np.full((height, width), 128, np.int16)
+    xs = np.sort(rng.integers(0, width, size=(n_rects, 2)), axis=1)
+    ys = np.sort(rng.integers(0, height, size=(n_rects, 2)), axis=1)
+    gray = rng.integers(0, 256, size=n_rects)
+    for (x0, x1), (y0, y1), g in zip(xs, ys, gray):
+        img[y0:y1 + 1, x0:x1 + 1] = g
+    img += rng.integers(-6, 7, size=(height, width)).astype(np.int16)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def shifted_pair(seed: int, width: int, height: int, dx: int = 3, dy: int = 2):
+    """C2 pair: A = G(seed), B = A shifted by (dx, dy) with edge replicate + fresh noise."""
+    a = synth_image(seed, width, height)
+    base = np.pad(a.astype(np.int16), ((dy, 0), (dx, 0)), mode="edge")[:height, :width]
+    rng = np.random.default_rng(seed + 1000)
+    b = np.clip(base + rng.integers(-3, 4, size=(height, width)), 0, 255).astype(np.uint8)
+    return a, b
+
+
+# KITTI 00-02 intrinsics (Examples/Stereo/KITTI00-02.yaml:8-25)
+KITTI = dict(fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, bf=386.1448, width=1241, height=376)
+
+
+def _rot_y(deg):
+    a = np.deg2rad(deg)
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def _small_rot(rng, sigma_deg):
+    w = rng.normal(0, np.deg2rad(sigma_deg), 3)
+    th = np.linalg.norm(w)
+    if th < 1e-12:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def make_ba_problem(seed: int = 0, n_kf: int = 20, n_pts: int = 3000, n_fixed: int = 2, stereo_frac: float = 0.2,
+                    outlier_frac: float = 0.03, cam=KITTI):
+    """C4: a LocalBundleAdjustment problem in the flattened orbba_problem layout.
+
+    n_kf local keyframes moving forward along +z (0.5 m apart, 0.5 deg yaw per KF); KF 0 is the
+    fixed gauge (`localKF->id == 0`, Optimizer.cc:551) and `n_fixed` extra fixed cameras observe
+    some points (the fixedCameras set, :524-537).  Each point is seen by a run of K ~ U{2..6}
+    keyframes; 20 % of observations are stereo (ur >= 0), octaves U{0..7} with pixel noise
+    N(0, 1.2^oct) and invSigma2 = 1/1.2^(2 oct); 3 % outliers get +-U(15,40) px.  Initial poses
+    are perturbed by 0.2 deg / 2 cm and points by 2 % of depth.
+    """
+    rng = np.random.default_rng(seed)
+    P = n_kf + n_fixed
+    R_true, t_true, C = [], [], []
+    for k in range(P):
+        kk = k if k < n_kf else -(k - n_kf + 1)   # fixed cameras behind KF 0
+        Rwc = _rot_y(0.5 * kk)
+        c = np.array([0.02 * np.sin(kk), 0.0, 0.5 * kk])
+        Rcw = Rwc.T
+        R_true.append(Rcw)
+        t_true.append(-Rcw @ c)
+        C.append(c)
+    fixed = np.zeros(P, np.uint8)
+    fixed[0] = 1
+    fixed[n_kf:] = 1
+    pts, ep, ek, obs, info, camv = [], [], [], [], [], []
+    for p in range(n_pts):
+        K = int(rng.integers(2, 7))
+        s = int(rng.integers(-n_fixed, n_kf - K + 1))
+        kfs = [(k if k >= 0 else n_kf + (-k - 1)) for k in range(s, s + K)]
+        zc = max(C[k][2] for k in kfs)
+        X = np.array([rng.uniform(-15, 15), rng.uniform(-3, 3), zc + rng.uniform(5, 40)])
+        pid = len(pts)
+        pts.append(X)
+        for k in kfs:
+            Xc = R_true[k] @ X + t_true[k]
+            u = cam["fx"] * Xc[0] / Xc[2] + cam["cx"]
+            v = cam["fy"] * Xc[1] / Xc[2] + cam["cy"]
+            octv = int(rng.integers(0, 8))
+            sig = 1.2 ** octv
+            u += rng.normal(0, sig)
+            v += rng.normal(0, sig)
+            ur = -1.0
+            if rng.random() < stereo_frac:
+                ur = u - cam["bf"] / Xc[2] + rng.normal(0, sig)
+            if rng.random() < outlier_frac:
+                u += rng.choice([-1, 1]) * rng.uniform(15, 40)
+                v += rng.choice([-1, 1]) * rng.uniform(15, 40)
+                if ur >= 0:
+                    ur = u - cam["bf"] / Xc[2]
+            ep.append(pid)
+            ek.append(k)
+            # measurements are floats in the reference (cv::KeyPoint pt, uright)
+            obs.append([np.float32(u), np.float32(v), np.float32(ur) if ur >= 0 else -1.0])
+            info.append(np.float32(1.0 / (sig * sig)))
+            camv.append([np.float32(cam[k2]) for k2 in ("fx", "fy", "cx", "cy", "bf")])
+    pose_R = np.zeros((P, 9))
+    pose_t = np.zeros((P, 3))
+    for k in range(P):
+        R, t = R_true[k], t_true[k]
+        if not fixed[k]:
+            R = _small_rot(rng, 0.2) @ R
+            t = t + rng.normal(0, 0.02, 3)
+        pose_R[k] = R.reshape(-1)
+        pose_t[k] = t
+    pts = np.array(pts)
+    depth = np.abs(pts[:, 2] - np.mean([c[2] for c in C]))
+    pts0 = pts + rng.normal(0, 1, pts.shape) * (0.02 * depth)[:, None]
+    return dict(pose_R=pose_R.astype(np.float32).astype(np.float64), pose_t=pose_t.astype(np.float32).astype(np.float64),
+                pose_fixed=fixed, points=pts0.astype(np.float32).astype(np.float64),
+                edge_point=np.array(ep, np.int32), edge_pose=np.array(ek, np.int32),
+                edge_obs=np.array(obs, np.float64), edge_inv_sigma2=np.array(info, np.float64),
+                edge_cam=np.array(camv, np.float64), gt_R=np.array([r.reshape(-1) for r in R_true]),
+                gt_t=np.array(t_true), gt_points=pts)

@@ -1,0 +1,215 @@
+"""ctypes binding of the CPU oracle (oracle/orb_oracle.cpp).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this module.
+"""
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_SO = ORACLE_DIR / "_build" / "liborb_oracle.so"
+
+
+class OrbxParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scaleFactor", C.c_float), ("nlevels", C.c_int32),
+                ("iniThFAST", C.c_int32), ("minThFAST", C.c_int32)]
+
+
+class Keypoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class TriFrame(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kp_xy", C.c_void_p), ("octave", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mappoint", C.c_void_p), ("desc", C.c_void_p), ("n_nodes", C.c_int32),
+                ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("indices", C.c_void_p)]
+
+
+class BAProblem(C.Structure):
+    _fields_ = [("n_poses", C.c_int32), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
+                ("pose_fixed", C.c_void_p), ("n_points", C.c_int32), ("points", C.c_void_p),
+                ("n_edges", C.c_int32), ("edge_point", C.c_void_p), ("edge_pose", C.c_void_p),
+                ("edge_obs", C.c_void_p), ("edge_inv_sigma2", C.c_void_p), ("edge_cam", C.c_void_p)]
+
+
+class BAResult(C.Structure):
+    _fields_ = [("pose_R", C.c_void_p), ("pose_t", C.c_void_p), ("pose_q", C.c_void_p),
+                ("points", C.c_void_p), ("edge_outlier", C.c_void_p), ("edge_chi2", C.c_void_p),
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not ORACLE_SO.exists() and (ORACLE_DIR / "orb_oracle.cpp").exists():
+            build()
+        _lib = C.CDLL(str(ORACLE_SO))
+        _lib.oracle_fast_atan2.restype = C.c_float
+        _lib.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def params(nfeatures=2000, scale=1.2, nlevels=8, ini=20, mn=7):
+    return OrbxParams(nfeatures, scale, nlevels, ini, mn)
+
+
+def scale_tables(p):
+    L = p.nlevels
+    s, i, s2, is2 = (np.zeros(L, np.float32) for _ in range(4))
+    q = np.zeros(L, np.int32)
+    um = np.zeros(16, np.int32)
+    lib().oracle_scale_tables(C.byref(p), ptr(s), ptr(i), ptr(s2), ptr(is2), ptr(q), ptr(um))
+    return dict(scale=s, inv_scale=i, sigma2=s2, inv_sigma2=is2, quota=q, umax=um)
+
+
+def gaussian_taps():
+    t = np.zeros(7, np.int32)
+    lib().oracle_gaussian_taps(ptr(t))
+    return t
+
+
+def pyramid(p, img):
+    img = np.ascontiguousarray(img)
+    L = p.nlevels
+    offs = np.zeros(L, np.int64)
+    w = np.zeros(L, np.int32)
+    h = np.zeros(L, np.int32)
+    lib().oracle_pyramid(C.byref(p), ptr(img), img.shape[0], img.shape[1], C.c_size_t(img.shape[1]), None,
+                         ptr(offs), ptr(w), ptr(h))
+    total = int((w.astype(np.int64) * h).sum())
+    out = np.zeros(total, np.uint8)
+    lib().oracle_pyramid(C.byref(p), ptr(img), img.shape[0], img.shape[1], C.c_size_t(img.shape[1]), ptr(out),
+                         ptr(offs), ptr(w), ptr(h))
+    return [out[offs[l]:offs[l] + w[l] * h[l]].reshape(h[l], w[l]) for l in range(L)]
+
+
+def _kp_out(fn, *args, cap=1 << 20):
+    xs, ys, rs = (np.zeros(cap, np.float32) for _ in range(3))
+    n = fn(*args, ptr(xs), ptr(ys), ptr(rs), cap)
+    assert n <= cap
+    return np.stack([xs[:n], ys[:n], rs[:n]], axis=1)
+
+
+def detect_fast(level_img, ini=20, mn=7):
+    im = np.ascontiguousarray(level_img)
+    return _kp_out(lib().oracle_detect_fast, ptr(im), im.shape[0], im.shape[1], C.c_size_t(im.shape[1]), ini, mn)
+
+
+def fast_raw(img, th):
+    im = np.ascontiguousarray(img)
+    return _kp_out(lib().oracle_fast_raw, ptr(im), im.shape[0], im.shape[1], C.c_size_t(im.shape[1]), th)
+
+
+def quadtree(kps, rows, cols, nfeat):
+    kps = np.ascontiguousarray(kps, np.float32)
+    xs, ys, rs = (np.ascontiguousarray(kps[:, i]) for i in range(3))
+    cap = max(len(kps), 1) + 8
+    ox, oy, orr = (np.zeros(cap, np.float32) for _ in range(3))
+    n = lib().oracle_quadtree(ptr(xs), ptr(ys), ptr(rs), len(kps), rows, cols, nfeat, ptr(ox), ptr(oy), ptr(orr), cap)
+    return np.stack([ox[:n], oy[:n], orr[:n]], axis=1)
+
+
+def gaussian_blur(img):
+    im = np.ascontiguousarray(img)
+    out = np.zeros_like(im)
+    lib().oracle_gaussian_blur(ptr(im), im.shape[0], im.shape[1], C.c_size_t(im.shape[1]), ptr(out))
+    return out
+
+
+def extract(p, img, cap=8192):
+    img = np.ascontiguousarray(img)
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int32(0)
+    per = np.zeros(p.nlevels, np.int32)
+    rc = lib().oracle_extract(C.byref(p), ptr(img), img.shape[0], img.shape[1], C.c_size_t(img.shape[1]), ptr(kps),
+                              ptr(desc), cap, C.byref(n), ptr(per))
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy(), per
+
+
+def bf_match(A, B, nnratio=0.6, th_low=50):
+    A = np.ascontiguousarray(A, np.uint8)
+    B = np.ascontiguousarray(B, np.uint8)
+    nA = len(A)
+    bi, bd, sd, m = (np.zeros(nA, np.int32) for _ in range(4))
+    lib().oracle_bf_match(ptr(A), nA, ptr(B), len(B), C.c_float(nnratio), th_low, ptr(bi), ptr(bd), ptr(sd), ptr(m))
+    return bi, bd, sd, m
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().oracle_descriptor_distance(ptr(a), ptr(b))
+
+
+class _Keep:
+    """Holds numpy arrays alive while a ctypes struct points into them."""
+
+    def __init__(self):
+        self.arrs = []
+
+    def __call__(self, a, dtype):
+        a = np.ascontiguousarray(a, dtype)
+        self.arrs.append(a)
+        return ptr(a)
+
+
+def tri_frame(keep, xy, octave, uright, has_mp, desc, node_ids, node_off, indices):
+    return TriFrame(len(xy), keep(xy, np.float32), keep(octave, np.int32), keep(uright, np.float32),
+                    keep(has_mp, np.uint8), keep(desc, np.uint8), len(node_ids), keep(node_ids, np.uint32),
+                    keep(node_off, np.int32), keep(indices, np.int32))
+
+
+def search_for_triangulation(f1, f2, F12, ep2, scale2, sigma2, only_stereo=False):
+    keep = _Keep()
+    out = np.zeros(f1.n, np.int32)
+    n = lib().oracle_search_for_triangulation(C.byref(f1), C.byref(f2), keep(F12, np.float32), keep(ep2, np.float32),
+                                              keep(scale2, np.float32), keep(sigma2, np.float32), int(only_stereo),
+                                              ptr(out))
+    return out, n
+
+
+def ba_problem(keep, prob):
+    return BAProblem(len(prob["pose_R"]), keep(prob["pose_R"], np.float64), keep(prob["pose_t"], np.float64),
+                     keep(prob["pose_fixed"], np.uint8), len(prob["points"]), keep(prob["points"], np.float64),
+                     len(prob["edge_point"]), keep(prob["edge_point"], np.int32), keep(prob["edge_pose"], np.int32),
+                     keep(prob["edge_obs"], np.float64), keep(prob["edge_inv_sigma2"], np.float64),
+                     keep(prob["edge_cam"], np.float64))
+
+
+def local_ba(prob, stop=None):
+    keep = _Keep()
+    pr = ba_problem(keep, prob)
+    P, N, E = pr.n_poses, pr.n_points, pr.n_edges
+    out = dict(pose_R=np.zeros((P, 9)), pose_t=np.zeros((P, 3)), pose_q=np.zeros((P, 4)),
+               points=np.zeros((N, 3)), edge_outlier=np.zeros(E, np.uint8), edge_chi2=np.zeros(E))
+    res = BAResult(ptr(out["pose_R"]), ptr(out["pose_t"]), ptr(out["pose_q"]), ptr(out["points"]),
+                   ptr(out["edge_outlier"]), ptr(out["edge_chi2"]))
+    sf = None
+    if stop is not None:
+        sf = C.byref(C.c_int32(int(stop)))
+    lib().oracle_local_ba(C.byref(pr), C.byref(res), sf)
+    out["iterations"] = tuple(res.iterations)
+    out["chi2"] = tuple(res.chi2)
+    return out

@@ -1,0 +1,92 @@
+"""GPU parity of the Hamming matchers against the oracle (exact integers / indices)."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from orb_slam2_refactored_amd import ORBmatcher
+from tri_case import make_case, oracle_run
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def rand_desc(rng, n, p=0.5):
+    bits = (rng.random((n, 256)) < p).astype(np.uint8)
+    return np.packbits(bits, axis=1, bitorder="little")
+
+
+@pytest.mark.parametrize("nA,nB", [(1, 1), (300, 1), (257, 513), (2000, 2000), (1000, 0), (0, 10), (64, 255)])
+def test_bf_match_random(oracle, nA, nB):
+    rng = np.random.default_rng(nA * 7 + nB)
+    A = rand_desc(rng, nA)
+    B = rand_desc(rng, nB)
+    if nB > 10:
+        B[7] = B[3]
+        A[: min(nA, 5)] = B[3] ^ np.uint8(1)   # ties on best
+    m = ORBmatcher()
+    got = m.MatchBruteForce(A, B)
+    exp = oracle.bf_match(A, B)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+
+
+def test_bf_match_near_duplicates(oracle):
+    rng = np.random.default_rng(3)
+    B = rand_desc(rng, 900, 0.5)
+    A = B[rng.integers(0, 900, 700)].copy()
+    flip = (rng.random(A.shape) < 0.02)
+    A ^= (flip * rng.integers(1, 256, A.shape)).astype(np.uint8)
+    got = ORBmatcher().MatchBruteForce(A, B)
+    exp = oracle.bf_match(A, B)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    assert (got[3] >= 0).sum() > 100
+
+
+def test_bf_match_all_256():
+    A = np.zeros((3, 32), np.uint8)
+    B = np.full((4, 32), 255, np.uint8)
+    bi, bd, sd, m = ORBmatcher().MatchBruteForce(A, B)
+    assert bi.tolist() == [-1] * 3 and bd.tolist() == [256] * 3 and sd.tolist() == [256] * 3 and m.tolist() == [-1] * 3
+
+
+def test_bf_match_golden():
+    g = np.load(GOLDEN / "bf_match_c1.npz")
+    bi, bd, sd, m = ORBmatcher().MatchBruteForce(g["A"], g["B"])
+    assert np.array_equal(bi, g["best_idx"]) and np.array_equal(bd, g["best"])
+    assert np.array_equal(sd, g["second"]) and np.array_equal(m, g["match"])
+
+
+def test_descriptor_distance(oracle):
+    rng = np.random.default_rng(1)
+    A = rand_desc(rng, 20)
+    for i in range(19):
+        assert ORBmatcher.DescriptorDistance(A[i], A[i + 1]) == oracle.descriptor_distance(A[i], A[i + 1])
+
+
+def test_batch_device(oracle):
+    import torch
+    rng = np.random.default_rng(5)
+    P, cap = 6, 700
+    nA = rng.integers(0, cap, P).astype(np.int32)
+    nB = rng.integers(0, cap, P).astype(np.int32)
+    A = np.stack([rand_desc(rng, cap) for _ in range(P)])
+    B = np.stack([rand_desc(rng, cap) for _ in range(P)])
+    out = ORBmatcher().match_batch_device(torch.from_numpy(A).cuda(), torch.from_numpy(nA).cuda(),
+                                          torch.from_numpy(B).cuda(), torch.from_numpy(nB).cuda())
+    out = out.cpu().numpy()
+    for p in range(P):
+        exp = oracle.bf_match(A[p, :nA[p]], B[p, :nB[p]])
+        for k in range(4):
+            assert np.array_equal(out[k, p, :nA[p]], exp[k])
+
+
+@pytest.mark.parametrize("seed,stereo,single", [(0, False, False), (1, True, False), (2, False, True), (3, False, False)])
+def test_search_for_triangulation(oracle, seed, stereo, single):
+    kf1, kf2, F = make_case(seed, n1=1500, n2=1600, n_nodes=9, only_single_node=single)
+    pairs, got = ORBmatcher(0.6, False).SearchForTriangulation(kf1, kf2, F, stereo)
+    exp, n = oracle_run(oracle, kf1, kf2, F, stereo)
+    assert np.array_equal(got, exp)
+    assert len(pairs) == n and n > 0
+    assert [p[0] for p in pairs] == sorted(p[0] for p in pairs)
