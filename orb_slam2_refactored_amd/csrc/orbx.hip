@@ -1009,10 +1009,13 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.out_frame = std::max(out, 1);
     NC = (int)align_up(NC, 64);
     const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int));
-    if (lds > 60 * 1024) {
-        set_error("nfeatures too large for the quadtree LDS budget");
+    if (lds > 156 * 1024) {   // gfx950: 160 KiB LDS per workgroup
+        set_error("nfeatures too large for the quadtree LDS budget (per-level quota <= ~2100)");
         return ORB_EINVAL;
     }
+    if (lds > 48 * 1024)
+        ORB_HIP_TRY(hipFuncSetAttribute((const void*)quadtree_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds));
     int rc;
     if ((rc = h->d_cells.reserve(std::max<size_t>(1, cells.size()) * sizeof(CellDev)))) return rc;
     if ((rc = h->d_xtab.reserve(std::max<size_t>(1, xtab.size()) * sizeof(int2)))) return rc;
