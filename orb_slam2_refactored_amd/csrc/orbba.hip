@@ -429,19 +429,31 @@ __global__ __launch_bounds__(256) void ba_schur_block_kernel(BADev b, int D) {
     }
 }
 
-__global__ __launch_bounds__(64) void ba_schur_rhs_kernel(BADev b) {
+// b_schur = b_p - sum over the pose's edges of Hpl D^-1 b_l: 6 entries x 42 partial groups.
+__global__ __launch_bounds__(256) void ba_schur_rhs_kernel(BADev b) {
+    __shared__ double sh[42][6];
     const int i = blockIdx.x;
-    if (threadIdx.x >= 6) return;
-    double s = 0;
-    for (int u = b.ps_beg[i]; u < b.ps_beg[i + 1]; u++) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + threadIdx.x];
-    b.bs[6 * i + threadIdx.x] = b.bp[6 * i + threadIdx.x] - s;
+    const int g = threadIdx.x / 6, c = threadIdx.x % 6;
+    if (g < 42) {
+        double s = 0;
+        for (int u = b.ps_beg[i] + g; u < b.ps_beg[i + 1]; u += 42) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + c];
+        sh[g][c] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        double s = 0;
+        for (int q = 0; q < 42; q++) s += sh[q][threadIdx.x];
+        b.bs[6 * i + threadIdx.x] = b.bp[6 * i + threadIdx.x] - s;
+    }
 }
 
-// Dense LDL^T solve of S x = bs, S in LDS (right-looking; one workgroup).
+// Dense LDL^T solve of S x = bs with S in LDS (right-looking, one workgroup of 32x32 threads;
+// stands in for g2o's SimplicialLDLT, linear_solver_eigen.h:94-124).
 __global__ __launch_bounds__(1024) void ba_ldlt_kernel(BADev b, int D) {
     extern __shared__ __attribute__((aligned(16))) double A[];
     double* v = A + (size_t)D * D;
     __shared__ int s_ok;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     for (int i = threadIdx.x; i < D * D; i += blockDim.x) A[i] = b.S[i];
     for (int i = threadIdx.x; i < D; i += blockDim.x) v[i] = b.bs[i];
     if (threadIdx.x == 0) s_ok = 1;
@@ -452,13 +464,15 @@ __global__ __launch_bounds__(1024) void ba_ldlt_kernel(BADev b, int D) {
             if (threadIdx.x == 0) s_ok = 0;
             break;   // uniform: every thread read the same dj
         }
-        for (int i = j + 1 + threadIdx.x; i < D; i += blockDim.x) A[i * D + j] /= dj;   // L(i,j)
-        __syncthreads();
-        const int m = D - j - 1;
-        for (int t = threadIdx.x; t < m * m; t += blockDim.x) {
-            const int i = j + 1 + t / m, k = j + 1 + t % m;
-            if (k <= i) A[i * D + k] -= A[i * D + j] * dj * A[k * D + j];
+        // trailing update of the lower triangle, using column j before it is scaled:
+        // A(i,k) -= A(i,j) * A(k,j) / dj  for j < k <= i
+        const double inv = 1.0 / dj;
+        for (int i = j + 1 + ty; i < D; i += 32) {
+            const double aij = A[i * D + j] * inv;
+            for (int k = j + 1 + tx; k <= i; k += 32) A[i * D + k] -= aij * A[k * D + j];
         }
+        __syncthreads();
+        for (int i = j + 1 + threadIdx.x; i < D; i += blockDim.x) A[i * D + j] *= inv;   // L(i,j)
         __syncthreads();
     }
     __syncthreads();
@@ -880,7 +894,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 if (nl) hipLaunchKernelGGL(ba_schur_point_kernel, gp, dim3(256), 0, st, b);
                 if (np) {
                     hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk), dim3(256), 0, st, b, D);
-                    hipLaunchKernelGGL(ba_schur_rhs_kernel, dim3(np), dim3(64), 0, st, b);
+                    hipLaunchKernelGGL(ba_schur_rhs_kernel, dim3(np), dim3(256), 0, st, b);
                     hipLaunchKernelGGL(ba_ldlt_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
                 } else {
                     ORB_HIP_TRY(hipMemsetAsync(&b.ctl->ok2, 0xff, 4, st));   // no poses: ok

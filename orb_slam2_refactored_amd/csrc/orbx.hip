@@ -39,8 +39,9 @@ __constant__ int c_pattern[1024] = {
 };
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 __constant__ int c_gauss[7] = {18, 34, 48, 56, 48, 34, 18};   // OpenCV 4.x bit-exact Q8 taps
-__constant__ int c_circle_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-__constant__ int c_circle_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+// FAST circle (cv::FAST makeOffsets, pattern 16): compile-time so LDS reads use immediate offsets
+constexpr int c_circle_dx_h[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+constexpr int c_circle_dy_h[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
 struct LevelDev {
     int w, h, stride;
@@ -133,26 +134,38 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
                                                             long long in_fstride, int in_step, uint8_t* pyr,
                                                             const int2* __restrict__ xtab,
                                                             const int2* __restrict__ ytab) {
+    // block = 64 x 4 threads, each thread 4 consecutive output pixels of one row (dword store)
     const LevelDev& L = g.lv[l];
-    const int f = blockIdx.y;
+    const int f = blockIdx.z;
+    const int dx0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (dy >= L.h || dx0 >= L.w) return;
     int sstep;
     const uint8_t* src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &sstep);
-    uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off;
+    uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off + (long long)dy * L.stride;
     const int2* xt = xtab + L.xtab_off;
-    const int2* yt = ytab + L.ytab_off;
-    const int total = L.w * L.h;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const int dy = i / L.w, dx = i - dy * L.w;
-        const int2 xv = xt[dx], yv = yt[dy];
-        const int sx0 = xv.x & 0xffff, sx1 = xv.x >> 16, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
-        const int sy0 = yv.x & 0xffff, sy1 = yv.x >> 16, b0 = yv.y & 0xffff, b1 = yv.y >> 16;
-        const uint8_t* r0 = src + (long long)sy0 * sstep;
-        const uint8_t* r1 = src + (long long)sy1 * sstep;
-        const int h0 = r0[sx0] * a0 + r0[sx1] * a1;
-        const int h1 = r1[sx0] * a0 + r1[sx1] * a1;
-        const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
-        int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
-        dst[(long long)dy * L.stride + dx] = (uint8_t)(v > 255 ? 255 : v);
+    const int2 yv = ytab[L.ytab_off + dy];
+    const int sy0 = yv.x & 0xffff, sy1 = yv.x >> 16, b0 = yv.y & 0xffff, b1 = yv.y >> 16;
+    const uint8_t* r0 = src + (long long)sy0 * sstep;
+    const uint8_t* r1 = src + (long long)sy1 * sstep;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int dx = dx0 + k;
+        if (dx < L.w) {
+            const int2 xv = xt[dx];
+            const int sx0 = xv.x & 0xffff, sx1 = xv.x >> 16, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
+            const int h0 = r0[sx0] * a0 + r0[sx1] * a1;
+            const int h1 = r1[sx0] * a0 + r1[sx1] * a1;
+            const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
+            const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+            packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
+        }
+    }
+    if (dx0 + 3 < L.w) {
+        *reinterpret_cast<uint32_t*>(dst + dx0) = packed;   // stride % 16 == 0, dx0 % 4 == 0
+    } else {
+        for (int k = 0; dx0 + k < L.w; k++) dst[dx0 + k] = (uint8_t)(packed >> (8 * k));
     }
 }
 
@@ -163,11 +176,14 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
 // A pixel is a FAST-9 corner at threshold t iff M > t, and cornerScore<16> == M - 1 for every
 // detected corner (threshold-independent), so one M map serves both the iniThFAST pass and the
 // minThFAST retry of DetectFAST.
-__device__ __forceinline__ int corner_strength(const uint8_t* crop, int cw, int cx, int cy) {
-    const int v = crop[cy * cw + cx];
+constexpr int CS = 72;   // LDS crop row stride (bytes)
+constexpr int ZS = 64;   // LDS zone row stride
+
+__device__ __forceinline__ int corner_strength(const uint8_t* c) {   // c -> centre pixel in LDS
+    const int v = c[0];
     int d[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)crop[(cy + c_circle_dy[k]) * cw + cx + c_circle_dx[k]];
+    for (int k = 0; k < 16; k++) d[k] = v - (int)c[c_circle_dy_h[k] * CS + c_circle_dx_h[k]];
     int lo2[16], hi2[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -192,13 +208,13 @@ __device__ __forceinline__ int corner_strength(const uint8_t* crop, int cw, int 
     return M;
 }
 
-// Cheap necessary test for "corner at threshold t": some 9-run of bright or dark pixels.
-__device__ __forceinline__ bool is_corner_t(const uint8_t* crop, int cw, int cx, int cy, int t) {
-    const int v = crop[cy * cw + cx];
+// Cheap exact test for "corner at threshold t": a 9-run of bright or of dark circle pixels.
+__device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t) {
+    const int v = c[0];
     unsigned br = 0, dk = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int p = crop[(cy + c_circle_dy[k]) * cw + cx + c_circle_dx[k]];
+        const int p = c[c_circle_dy_h[k] * CS + c_circle_dx_h[k]];
         br |= (unsigned)(p > v + t) << k;
         dk |= (unsigned)(p < v - t) << k;
     }
@@ -206,60 +222,62 @@ __device__ __forceinline__ bool is_corner_t(const uint8_t* crop, int cw, int cx,
         unsigned x = m | (m << 16);
         unsigned a = x & (x >> 1);
         unsigned b = a & (a >> 2);
-        unsigned c = b & (b >> 4);
-        return (c & (x >> 8) & 0xffffu) != 0;
+        unsigned c2 = b & (b >> 4);
+        return (c2 & (x >> 8) & 0xffffu) != 0;
     };
     return run9(br) || run9(dk);
 }
 
+// One workgroup per (cell, frame).  Threads tile the detection zone 32x8 (zone width <= 32) or
+// 64x4, so a block-wide scan over threadIdx order is row-major order — FAST's emission order.
 __global__ __launch_bounds__(256) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                          const uint8_t* __restrict__ in, long long in_fstride,
                                                          int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                          int th_min, uint32_t* __restrict__ slots,
                                                          int* __restrict__ cell_cnt, uint32_t* fault) {
-    __shared__ uint8_t crop[MAX_CROP * MAX_CROP];
-    __shared__ uint8_t Mz[MAX_ZONE * MAX_ZONE];
+    __shared__ __attribute__((aligned(16))) uint8_t crop[MAX_CROP * CS];
+    __shared__ __attribute__((aligned(16))) uint8_t Mz[MAX_ZONE * ZS];
     __shared__ short list[MAX_ZONE * MAX_ZONE];
-    __shared__ int s_nlist, s_nkp, s_wave[8];
+    __shared__ int tmp[8];
+    __shared__ int s_nkp;
 
     const CellDev cell = cells[blockIdx.x];
     const int f = blockIdx.y;
     const int x0 = cell.x0y0 & 0xffff, y0 = cell.x0y0 >> 16;
     const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
     const int cw = zw + 6, ch = zh + 6;
+    const bool wide = zw > 32;
+    const int lxs = wide ? 6 : 5;                 // log2 of the tile width
+    const int lx = 1 << lxs, ly = 256 >> lxs;
+    const int tx = threadIdx.x & (lx - 1), ty = threadIdx.x >> lxs;
     int step;
     const uint8_t* img = level_base(g, cell.level, f, in, in_fstride, in_step, pyr, &step);
 
-    if (threadIdx.x == 0) { s_nlist = 0; s_nkp = 0; }
-    for (int i = threadIdx.x; i < cw * ch; i += blockDim.x) {
-        const int r = i / cw, c = i - r * cw;
-        crop[i] = img[(long long)(y0 + r) * step + x0 + c];
+    if (threadIdx.x == 0) s_nkp = 0;
+    for (int r = ty; r < ch; r += ly) {
+        const uint8_t* row = img + (long long)(y0 + r) * step + x0;
+        for (int c = tx; c < cw; c += lx) crop[r * CS + c] = row[c];
     }
-    const int nz = zw * zh;
-    for (int i = threadIdx.x; i < nz; i += blockDim.x) Mz[i] = 0;
+    for (int r = ty; r < zh; r += ly)
+        for (int c = tx; c < zw; c += lx) Mz[r * ZS + c] = 0;
     __syncthreads();
 
-    // candidates at the lower of the two thresholds, compacted into `list`
+    // candidates at the lower threshold, compacted in row-major order
     const int tlo = min(th_ini, th_min);
-    for (int base = 0; base < nz; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        bool c = false;
-        if (i < nz) {
-            const int zy = i / zw, zx = i - zy * zw;
-            c = is_corner_t(crop, cw, zx + 3, zy + 3, tlo);
-        }
-        const unsigned long long m = __ballot(c);
-        int wbase = 0;
-        if (lane_id() == 0 && m) wbase = atomicAdd(&s_nlist, popc64(m));
-        wbase = __shfl(wbase, 0, 64);
-        if (c) list[wbase + popc64(m & lanemask_lt())] = (short)i;
+    int nl = 0;
+    for (int yb = 0; yb < zh; yb += ly) {
+        const int y = yb + ty;
+        const bool c = y < zh && tx < zw && is_corner_t(&crop[(y + 3) * CS + tx + 3], tlo);
+        int tot;
+        const int ex = block_excl_scan(c ? 1 : 0, tmp, &tot);
+        if (c) list[nl + ex] = (short)(y * ZS + tx);
+        nl += tot;
     }
     __syncthreads();
-    const int nl = s_nlist;
     for (int j = threadIdx.x; j < nl; j += blockDim.x) {
         const int i = list[j];
-        const int zy = i / zw, zx = i - zy * zw;
-        Mz[i] = (uint8_t)min(corner_strength(crop, cw, zx + 3, zy + 3), 255);
+        const int y = i >> 6, x = i & 63;
+        Mz[i] = (uint8_t)min(corner_strength(&crop[(y + 3) * CS + x + 3]), 255);
     }
     __syncthreads();
 
@@ -267,7 +285,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(Geom g, const CellDev* 
     auto is_kp = [&](int i, int t) -> bool {
         const int m = Mz[i];
         if (m <= t) return false;
-        const int zy = i / zw, zx = i - zy * zw;
+        const int zy = i >> 6, zx = i & 63;
 #pragma unroll
         for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
@@ -275,7 +293,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(Geom g, const CellDev* 
                 if (!dx && !dy) continue;
                 const int yy = zy + dy, xx = zx + dx;
                 if (yy < 0 || yy >= zh || xx < 0 || xx >= zw) continue;
-                const int q = Mz[yy * zw + xx];
+                const int q = Mz[yy * ZS + xx];
                 if (q > t && q >= m) return false;
             }
         return true;
@@ -286,30 +304,20 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(Geom g, const CellDev* 
     __syncthreads();
     const int t = s_nkp > 0 ? th_ini : th_min;
 
-    // emit in row-major order (FAST emits row by row, x ascending)
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
     const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
     int running = 0;
-    for (int base = 0; base < nz; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const bool k = i < nz && is_kp(i, t);
-        const unsigned long long m = __ballot(k);
-        const int w = threadIdx.x >> 6;
-        if (lane_id() == 0) s_wave[w] = popc64(m);
-        __syncthreads();
-        int before = running, tot = 0;
-        for (int q = 0; q < (int)(blockDim.x >> 6); q++) {
-            if (q < w) before += s_wave[q];
-            tot += s_wave[q];
-        }
-        if (k) {
-            const int r = before + popc64(m & lanemask_lt());
-            const int zy = i / zw, zx = i - zy * zw;
-            const uint32_t x = (uint32_t)(x0 + 3 + zx), y = (uint32_t)(y0 + 3 + zy);
-            if (r < cap) out[r] = x | (y << 12) | ((uint32_t)(Mz[i] - 1) << 24);
+    for (int jb = 0; jb < nl; jb += blockDim.x) {
+        const int j = jb + threadIdx.x;
+        const int i = j < nl ? list[j] : 0;
+        const bool k = j < nl && is_kp(i, t);
+        int tot;
+        const int r = running + block_excl_scan(k ? 1 : 0, tmp, &tot);
+        if (k && r < cap) {
+            const uint32_t x = (uint32_t)(x0 + 3 + (i & 63)), y = (uint32_t)(y0 + 3 + (i >> 6));
+            out[r] = x | (y << 12) | ((uint32_t)(Mz[i] - 1) << 24);
         }
         running += tot;
-        __syncthreads();
     }
     if (threadIdx.x == 0) {
         if (running > cap) atomicOr(fault, FAULT_CELL_CAP);
@@ -715,53 +723,56 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return i;
 }
 
-__global__ __launch_bounds__(256) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
-                                                       int in_step, const uint8_t* __restrict__ pyr,
-                                                       const uint32_t* __restrict__ sel,
-                                                       const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
-                                                       uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                       int cap) {
-    __shared__ uint8_t raw[4][PATCH * PATCH + 15];
-    __shared__ uint16_t hb[4][PATCH * HBLUR_W];
-    const int w = threadIdx.x >> 6, lane = lane_id();
+constexpr int RS = 44;   // LDS raw-patch row stride
+
+// One workgroup = one wavefront = one kept keypoint.
+__global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
+                                                      int in_step, const uint8_t* __restrict__ pyr,
+                                                      const uint32_t* __restrict__ sel,
+                                                      const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
+                                                      uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
+                                                      int cap) {
+    __shared__ __attribute__((aligned(16))) uint8_t R[PATCH * RS];
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[PATCH * HBLUR_W];
+    const int lane = threadIdx.x;
     const int f = blockIdx.y;
-    const int s = blockIdx.x * 4 + w;
+    const int s = blockIdx.x;
     const int* cnt = sel_cnt + f * g.nlevels;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (s == 0 && lane == 0) {
         int tot = 0;
         for (int q = 0; q < g.nlevels; q++) tot += cnt[q];
         counts[f] = tot;
     }
     int l = 0;
-    if (s < g.out_frame)
-        while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_base) l++;
+    while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_base) l++;
     const LevelDev& L = g.lv[l];
     const int i = s - L.out_base;
+    if (i >= cnt[l]) return;
     int oidx = i;
     for (int q = 0; q < l; q++) oidx += cnt[q];
-    const bool valid = s < g.out_frame && i < cnt[l] && oidx < cap;   // wave-uniform
+    if (oidx >= cap) return;
 
-    uint32_t k = 0;
-    if (valid) k = sel[(long long)f * g.out_frame + s];
+    const uint32_t k = sel[(long long)f * g.out_frame + s];
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
     int step;
     const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
-    uint8_t* R = raw[w];
-    if (valid)
-        for (int q = lane; q < PATCH * PATCH; q += 64) {
-            const int r = q / PATCH, c = q - r * PATCH;
-            const int yy = reflect101(ky - 21 + r, L.h), xx = reflect101(kx - 21 + c, L.w);
-            R[q] = img[(long long)yy * step + xx];
+    // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101)
+    if (lane < PATCH) {
+        const int xx = reflect101(kx - 21 + lane, L.w);
+        for (int r = 0; r < PATCH; r++) {
+            const int yy = reflect101(ky - 21 + r, L.h);
+            R[r * RS + lane] = img[(long long)yy * step + xx];
         }
+    }
     __syncthreads();
 
     // IC_Angle on the unblurred level, patch centre (21, 21)
     int m10 = 0, m01 = 0;
-    for (int q = lane; q < 31; q += 64) m10 += (q - 15) * R[21 * PATCH + 6 + q];
+    if (lane < 31) m10 = (lane - 15) * R[21 * RS + 6 + lane];
     for (int q = lane; q < 15 * 31; q += 64) {
-        const int v = q / 31 + 1, u = q % 31 - 15;
+        const int v = q / 31 + 1, u = q - (v - 1) * 31 - 15;
         if (u < -c_umax[v] || u > c_umax[v]) continue;
-        const int vp = R[(21 + v) * PATCH + 21 + u], vm = R[(21 - v) * PATCH + 21 + u];
+        const int vp = R[(21 + v) * RS + 21 + u], vm = R[(21 - v) * RS + 21 + u];
         m01 += v * (vp - vm);
         m10 += u * (vp + vm);
     }
@@ -771,18 +782,17 @@ __global__ __launch_bounds__(256) void describe_kernel(Geom g, const uint8_t* __
     }
     const float angle = fast_atan2_dev((float)m01, (float)m10);
 
-    // horizontal Q8 blur of rows 0..42, columns kx-18..kx+18
-    uint16_t* H = hb[w];
-    for (int q = lane; q < PATCH * HBLUR_W; q += 64) {
-        const int r = q / HBLUR_W, c = q - r * HBLUR_W;
-        const uint8_t* rr = R + r * PATCH + c;
-        int acc = 0;
+    // horizontal Q8 blur, one row per lane (sliding window in registers); taps are symmetric
+    if (lane < PATCH) {
+        int v[PATCH];
 #pragma unroll
-        for (int t = 0; t < 7; t++) acc += c_gauss[t] * rr[t];
-        H[q] = (uint16_t)acc;
+        for (int c = 0; c < PATCH; c++) v[c] = R[lane * RS + c];
+#pragma unroll
+        for (int c = 0; c < HBLUR_W; c++)
+            Hb[lane * HBLUR_W + c] =
+                (uint16_t)(18 * (v[c] + v[c + 6]) + 34 * (v[c + 1] + v[c + 5]) + 48 * (v[c + 2] + v[c + 4]) + 56 * v[c + 3]);
     }
     __syncthreads();
-    if (!valid) return;
 
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
@@ -791,34 +801,34 @@ __global__ __launch_bounds__(256) void describe_kernel(Geom g, const uint8_t* __
         const float x = (float)c_pattern[2 * idx], y = (float)c_pattern[2 * idx + 1];
         const int dy = (int)rintf(x * b + y * a);
         const int dx = (int)rintf(x * a - y * b);
-        const uint16_t* col = H + (21 + dy - 3) * HBLUR_W + 18 + dx;
-        unsigned acc = 0;
-#pragma unroll
-        for (int t = 0; t < 7; t++) acc += (unsigned)c_gauss[t] * col[t * HBLUR_W];
+        const uint16_t* col = Hb + (18 + dy) * HBLUR_W + 18 + dx;
+        const unsigned acc = 18u * (col[0] + col[6 * HBLUR_W]) + 34u * (col[HBLUR_W] + col[5 * HBLUR_W]) +
+                             48u * (col[2 * HBLUR_W] + col[4 * HBLUR_W]) + 56u * col[3 * HBLUR_W];
         return (int)((acc + (1u << 15)) >> 16);
     };
     unsigned long long words[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int p = r * 64 + lane;
-        const bool bit = sample(2 * p) < sample(2 * p + 1);
-        words[r] = __ballot(bit);
+        words[r] = __ballot(sample(2 * p) < sample(2 * p + 1));
     }
     const long long o = (long long)f * cap + oidx;
     if (lane < 4) {
-        unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
         reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = wv;
     }
-    if (lane == 0) {
-        orbx_keypoint kp;
-        kp.x = l > 0 ? (float)kx * L.scale : (float)kx;
-        kp.y = l > 0 ? (float)ky * L.scale : (float)ky;
-        kp.size = L.size;
-        kp.angle = angle;
-        kp.response = (float)score;
-        kp.octave = l;
-        kp.class_id = -1;
-        kps[o] = kp;
+    if (lane < 7) {
+        float fv;
+        switch (lane) {
+            case 0: fv = l > 0 ? (float)kx * L.scale : (float)kx; break;
+            case 1: fv = l > 0 ? (float)ky * L.scale : (float)ky; break;
+            case 2: fv = L.size; break;
+            case 3: fv = angle; break;
+            case 4: fv = (float)score; break;
+            case 5: fv = __int_as_float(l); break;
+            default: fv = __int_as_float(-1); break;
+        }
+        reinterpret_cast<float*>(kps + o)[lane] = fv;
     }
 }
 
@@ -1091,8 +1101,7 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
     {
     StageMark m0(h, st, 0);
     for (int l = 1; l < g.nlevels; l++) {
-        const int total = g.lv[l].w * g.lv[l].h;
-        dim3 grid((unsigned)std::min(1024, (total + 255) / 256), (unsigned)F);
+        dim3 grid((unsigned)((g.lv[l].w + 255) / 256), (unsigned)((g.lv[l].h + 3) / 4), (unsigned)F);
         hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
                            h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
     }
@@ -1113,7 +1122,7 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
     }
     {
     StageMark m3(h, st, 3);
-    hipLaunchKernelGGL(describe_kernel, dim3((unsigned)((g.out_frame + 3) / 4), (unsigned)F), dim3(256), 0, st, g,
+    hipLaunchKernelGGL(describe_kernel, dim3((unsigned)g.out_frame, (unsigned)F), dim3(64), 0, st, g,
                        d_imgs, fstride, step, pyr, h->d_sel.as<uint32_t>(), h->d_selcnt.as<int>(), d_kps, d_desc,
                        d_counts, cap);
     }

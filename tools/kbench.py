@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Kernel-level driver for profiling: runs the batched extractor (+ matcher) `--iters` times on
+`--frames` synthetic 1280x720 frames resident in HBM, prints per-stage HIP-event times."""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--match", action="store_true")
+    a = ap.parse_args()
+    import torch
+    from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
+    from orb_slam2_refactored_amd.synth import synth_image
+    pool = np.stack([synth_image(i, a.width, a.height) for i in range(min(16, a.frames))])
+    frames = torch.from_numpy(np.concatenate([pool[i % len(pool)][None] for i in range(a.frames)])).cuda()
+    ex = ORBextractor(ORBextractor.Parameters(nfeatures=a.nfeatures))
+    kps, desc, cnt = ex.extract_batch_device(frames)
+    m = ORBmatcher(0.6, False)
+    prev = torch.tensor([(i - 1) % a.frames for i in range(a.frames)], device="cuda")
+    torch.cuda.synchronize()
+    ex.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        ex.extract_batch_device(frames, kps, desc, cnt)
+        if a.match:
+            m.match_batch_device(desc, cnt, desc.index_select(0, prev), cnt.index_select(0, prev))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = ex.profile_read()
+    print({k: round(v[0] / a.iters, 4) for k, v in st.items()}, f"wall/iter {1e3 * dt / a.iters:.3f} ms",
+          f"fps {a.frames * a.iters / dt:.0f}")
+
+
+if __name__ == "__main__":
+    main()
