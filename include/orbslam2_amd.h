@@ -198,6 +198,9 @@ int orbx_profile_read(orbx_extractor* h, double* ms, int32_t* launches);
 /* FAST candidates of (frame, level) of the last batch, in DetectFAST's push order (cell raster,
  * row-major inside a cell): packed x | y << 12 | score << 24.  *n = count (cap-limited copy). */
 int orbx_debug_level_candidates(const orbx_extractor* h, int frame, int level, uint32_t* out, int cap, int* n);
+/* Runs the quadtree's on-device std::sort emulation (one wavefront) on `sizes`: perm[k] = index of
+ * the element that std::sort(size-descending, src/ORBextractor.cc:642-643) puts at position k. */
+int orbx_debug_qt_sort(const int32_t* sizes, int n, int32_t* perm);
 /* Quadtree output of (frame, level) of the last batch (list order, packed as above). */
 int orbx_debug_level_selected(const orbx_extractor* h, int frame, int level, uint32_t* out, int cap, int* n);
 

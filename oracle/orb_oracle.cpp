@@ -1268,4 +1268,14 @@ int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile i
     return 0;
 }
 
+// std::sort of QuadTreeSuppression's DivisibleNode vector (src/ORBextractor.cc:635-643), real
+// libstdc++: perm[k] = input index placed at position k.
+void oracle_std_sort_sizes(const int32_t* sizes, int n, int32_t* perm) {
+    struct DivisibleNode { size_t size; const int32_t* ptr; };
+    std::vector<DivisibleNode> v(n);
+    for (int i = 0; i < n; i++) v[i] = {(size_t)sizes[i], sizes + i};
+    std::sort(v.begin(), v.end(), [](const DivisibleNode& a, const DivisibleNode& b) { return a.size > b.size; });
+    for (int i = 0; i < n; i++) perm[i] = (int32_t)(v[i].ptr - sizes);
+}
+
 }  // extern "C"

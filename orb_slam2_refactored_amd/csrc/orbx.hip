@@ -228,64 +228,122 @@ __device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t) {
     return run9(br) || run9(dk);
 }
 
-// One workgroup per (cell, frame).  Threads tile the detection zone 32x8 (zone width <= 32) or
-// 64x4, so a block-wide scan over threadIdx order is row-major order — FAST's emission order.
-__global__ __launch_bounds__(256) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
-                                                         const uint8_t* __restrict__ in, long long in_fstride,
-                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
-                                                         int th_min, uint32_t* __restrict__ slots,
-                                                         int* __restrict__ cell_cnt, uint32_t* fault) {
+// Necessary condition for a 9-arc at threshold t: two circle-adjacent compass points (circle
+// positions 0/4/8/12) both brighter than v+t or both darker than v-t.
+__device__ __forceinline__ bool compass_test(const uint8_t* c, int t) {
+    const int v = c[0];
+    const int p0 = c[3 * CS], p4 = c[3], p8 = c[-3 * CS], p12 = c[-3];
+    const bool b0 = p0 > v + t, b4 = p4 > v + t, b8 = p8 > v + t, b12 = p12 > v + t;
+    const bool d0 = p0 < v - t, d4 = p4 < v - t, d8 = p8 < v - t, d12 = p12 < v - t;
+    return (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
+}
+
+// One wavefront per (cell, frame).  Lanes tile the detection zone as 2 rows x 32 columns (zone
+// width <= 32) or 1 row x 64, so lane order inside a chunk is row-major — FAST's emission order —
+// and every prefix is a ballot + popcount (no workgroup barriers).
+//   1. crop (zone + 3-px apron) -> LDS with aligned dword loads
+//   2. compass pre-test; passers queue in LDS and get the full 9-arc test + corner strength M
+//      densely, 64 at a time; M is stored in a zone map (0 = no corner at min(ini, min) threshold)
+//   3. one pass over the zone: cell-local 3x3 NMS at iniThFAST and at minThFAST, ballots kept
+//   4. emit the iniThFAST set, or the minThFAST set when it is empty (DetectFAST :527-530)
+__global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
+                                                        const uint8_t* __restrict__ in, long long in_fstride,
+                                                        int in_step, const uint8_t* __restrict__ pyr, int th_ini,
+                                                        int th_min, uint32_t* __restrict__ slots,
+                                                        int* __restrict__ cell_cnt, uint32_t* fault) {
     __shared__ __attribute__((aligned(16))) uint8_t crop[MAX_CROP * CS];
     __shared__ __attribute__((aligned(16))) uint8_t Mz[MAX_ZONE * ZS];
-    __shared__ short list[MAX_ZONE * MAX_ZONE];
-    __shared__ int tmp[8];
-    __shared__ int s_nkp;
+    __shared__ unsigned long long bal[2][MAX_ZONE];
+    __shared__ short queue[128];
 
+    const int lane = threadIdx.x;
     const CellDev cell = cells[blockIdx.x];
     const int f = blockIdx.y;
     const int x0 = cell.x0y0 & 0xffff, y0 = cell.x0y0 >> 16;
     const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
     const int cw = zw + 6, ch = zh + 6;
-    const bool wide = zw > 32;
-    const int lxs = wide ? 6 : 5;                 // log2 of the tile width
-    const int lx = 1 << lxs, ly = 256 >> lxs;
-    const int tx = threadIdx.x & (lx - 1), ty = threadIdx.x >> lxs;
     int step;
     const uint8_t* img = level_base(g, cell.level, f, in, in_fstride, in_step, pyr, &step);
 
-    if (threadIdx.x == 0) s_nkp = 0;
-    for (int r = ty; r < ch; r += ly) {
-        const uint8_t* row = img + (long long)(y0 + r) * step + x0;
-        for (int c = tx; c < cw; c += lx) crop[r * CS + c] = row[c];
+    // 1. crop: lanes = 16 dwords x 4 rows; dword-aligned global loads issued together (kept in
+    //    registers), then bytes scattered into LDS
+    {
+        const int j = lane & 15, rr = lane >> 4;
+        constexpr int NR = (MAX_CROP + 3) / 4;   // row iterations (4 rows each)
+        uint32_t w[NR][2];
+        int offr[NR];
+#pragma unroll
+        for (int it = 0; it < NR; it++) {
+            const int r = rr + 4 * it;
+            w[it][0] = w[it][1] = 0;
+            offr[it] = 0;
+            if (r < ch) {
+                const uintptr_t addr = reinterpret_cast<uintptr_t>(img + (long long)(y0 + r) * step + x0);
+                const int off = (int)(addr & 3);
+                const uint32_t* a0 = reinterpret_cast<const uint32_t*>(addr - off);
+                const int nd = (off + cw + 3) >> 2;
+                offr[it] = off;
+                if (j < nd) w[it][0] = a0[j];
+                if (j + 16 < nd) w[it][1] = a0[j + 16];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < NR; it++) {
+            const int r = rr + 4 * it;
+            if (r >= ch) continue;
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int c = 4 * (j + 16 * h) + q - offr[it];
+                    if (c >= 0 && c < cw) crop[r * CS + c] = (uint8_t)(w[it][h] >> (8 * q));
+                }
+        }
+        for (int i = lane; i < zh * (ZS / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
     }
-    for (int r = ty; r < zh; r += ly)
-        for (int c = tx; c < zw; c += lx) Mz[r * ZS + c] = 0;
     __syncthreads();
 
-    // candidates at the lower threshold, compacted in row-major order
+    const bool narrow = zw <= 32;
+    const int rows_per = narrow ? 2 : 1;
+    const int lx = narrow ? (lane & 31) : lane;
+    const int ly = narrow ? (lane >> 5) : 0;
     const int tlo = min(th_ini, th_min);
-    int nl = 0;
-    for (int yb = 0; yb < zh; yb += ly) {
-        const int y = yb + ty;
-        const bool c = y < zh && tx < zw && is_corner_t(&crop[(y + 3) * CS + tx + 3], tlo);
-        int tot;
-        const int ex = block_excl_scan(c ? 1 : 0, tmp, &tot);
-        if (c) list[nl + ex] = (short)(y * ZS + tx);
-        nl += tot;
+    const unsigned long long lt = lanemask_lt();
+
+    // 2. compass pre-test -> queue -> dense full test
+    int qn = 0;   // wave-uniform queue length
+    auto drain = [&](int n) {
+        const int i = lane < n ? queue[lane] : -1;
+        int m = 0;
+        if (i >= 0) {
+            const uint8_t* c = &crop[((i >> 6) + 3) * CS + (i & 63) + 3];
+            if (is_corner_t(c, tlo)) m = min(corner_strength(c), 255);
+        }
+        if (m > 0) Mz[i] = (uint8_t)m;
+    };
+    for (int yb = 0; yb < zh; yb += rows_per) {
+        const int y = yb + ly;
+        const bool pass = y < zh && lx < zw && compass_test(&crop[(y + 3) * CS + lx + 3], tlo);
+        const unsigned long long bm = __ballot(pass);
+        if (pass) queue[qn + popc64(bm & lt)] = (short)(y * ZS + lx);
+        qn += popc64(bm);
+        __syncthreads();
+        if (qn >= 64) {
+            drain(64);
+            __syncthreads();
+            const short tail = lane + 64 < qn ? queue[lane + 64] : 0;
+            __syncthreads();
+            if (lane + 64 < qn) queue[lane] = tail;
+            qn -= 64;
+            __syncthreads();
+        }
     }
-    __syncthreads();
-    for (int j = threadIdx.x; j < nl; j += blockDim.x) {
-        const int i = list[j];
-        const int y = i >> 6, x = i & 63;
-        Mz[i] = (uint8_t)min(corner_strength(&crop[(y + 3) * CS + x + 3]), 255);
-    }
+    if (qn > 0) drain(qn);
     __syncthreads();
 
-    // cell-local NMS: neighbours outside the detection zone count as score 0
-    auto is_kp = [&](int i, int t) -> bool {
-        const int m = Mz[i];
+    // 3. NMS at both thresholds (neighbours outside the detection zone count as score 0)
+    auto nms = [&](int zy, int zx, int m, int t) -> bool {
         if (m <= t) return false;
-        const int zy = i >> 6, zx = i & 63;
 #pragma unroll
         for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
@@ -298,30 +356,45 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(Geom g, const CellDev* 
             }
         return true;
     };
-    int mine = 0;
-    for (int j = threadIdx.x; j < nl; j += blockDim.x) mine += is_kp(list[j], th_ini);
-    if (mine) atomicAdd(&s_nkp, mine);
+    int n_ini = 0, n_min = 0, chunk = 0;
+    for (int yb = 0; yb < zh; yb += rows_per, chunk++) {
+        const int y = yb + ly;
+        const bool in_zone = y < zh && lx < zw;
+        const int m = in_zone ? Mz[y * ZS + lx] : 0;
+        bool ki = false, km = false;
+        if (m > 0) {
+            ki = nms(y, lx, m, th_ini);
+            km = nms(y, lx, m, th_min);
+        }
+        const unsigned long long bi = __ballot(ki), bmn = __ballot(km);
+        if (lane == 0) { bal[0][chunk] = bi; bal[1][chunk] = bmn; }
+        n_ini += popc64(bi);
+        n_min += popc64(bmn);
+    }
     __syncthreads();
-    const int t = s_nkp > 0 ? th_ini : th_min;
 
+    // 4. emission in row-major order
+    const int which = n_ini > 0 ? 0 : 1;
+    const int total = which == 0 ? n_ini : n_min;
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
     const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
     int running = 0;
-    for (int jb = 0; jb < nl; jb += blockDim.x) {
-        const int j = jb + threadIdx.x;
-        const int i = j < nl ? list[j] : 0;
-        const bool k = j < nl && is_kp(i, t);
-        int tot;
-        const int r = running + block_excl_scan(k ? 1 : 0, tmp, &tot);
-        if (k && r < cap) {
-            const uint32_t x = (uint32_t)(x0 + 3 + (i & 63)), y = (uint32_t)(y0 + 3 + (i >> 6));
-            out[r] = x | (y << 12) | ((uint32_t)(Mz[i] - 1) << 24);
+    chunk = 0;
+    for (int yb = 0; yb < zh; yb += rows_per, chunk++) {
+        const unsigned long long bm = bal[which][chunk];
+        if (bm & (1ull << lane)) {
+            const int r = running + popc64(bm & lt);
+            const int y = yb + ly;
+            if (r < cap) {
+                const uint32_t x = (uint32_t)(x0 + 3 + lx), yy = (uint32_t)(y0 + 3 + y);
+                out[r] = x | (yy << 12) | ((uint32_t)(Mz[y * ZS + lx] - 1) << 24);
+            }
         }
-        running += tot;
+        running += popc64(bm);
     }
-    if (threadIdx.x == 0) {
-        if (running > cap) atomicOr(fault, FAULT_CELL_CAP);
-        cell_cnt[(long long)f * g.ncells_total + blockIdx.x] = min(running, cap);
+    if (lane == 0) {
+        if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
+        cell_cnt[(long long)f * g.ncells_total + blockIdx.x] = min(total, cap);
     }
 }
 
@@ -414,6 +487,102 @@ __device__ __forceinline__ void qt_emit_children(const QtNode& parent, int4 cc, 
     }
 }
 
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// std::sort(a, a+n, size-descending) on one wavefront: qt_sort_parallel_form() (qt_sort.h) with
+// each Hoare partition computed from ballot-compacted stopper lists.  Scratch: Ls, Rs, seg_lo,
+// seg_len (n ints each), tmp (n items), stk (>= 192 ints).  All lanes of the wave must call it.
+__device__ void qt_sort_wave(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, int* seg_len, QtItem* tmp, int* stk) {
+    const int lane = lane_id();
+    const unsigned long long lt = lanemask_lt();
+    if (n <= 0) return;
+    int sp = 0;
+    if (lane == 0) { stk[0] = 0; stk[1] = n; stk[2] = 2 * qt_lg(n); }
+    sp = 1;
+    wave_lds_sync();
+    while (sp > 0) {
+        --sp;
+        const int lo = stk[3 * sp], hi = stk[3 * sp + 1];
+        int depth = stk[3 * sp + 2];
+        wave_lds_sync();
+        if (hi - lo > 16) {
+            if (depth == 0) {
+                if (lane == 0) qt_heap_sort(a + lo, a + hi);
+                for (int i = lo + lane; i < hi; i += 64) { seg_lo[i] = lo; seg_len[i] = -1; }
+                wave_lds_sync();
+                continue;
+            }
+            --depth;
+            const int mid = lo + (hi - lo) / 2;
+            if (lane == 0) qt_median_to_first(a + lo, a + lo + 1, a + mid, a + hi - 1);
+            wave_lds_sync();
+            const int p = a[lo].size;
+            int nl = 0, nr = 0;
+            for (int base = lo + 1; base < hi; base += 64) {
+                const int i = base + lane;
+                const bool f = i < hi && a[i].size <= p;
+                const unsigned long long m = __ballot(f);
+                if (f) Ls[nl + popc64(m & lt)] = i;
+                nl += popc64(m);
+            }
+            for (int base = hi - 1; base >= lo; base -= 64) {
+                const int j = base - lane;
+                const bool f = j >= lo && a[j].size >= p;
+                const unsigned long long m = __ballot(f);
+                if (f) Rs[nr + popc64(m & lt)] = j;
+                nr += popc64(m);
+            }
+            wave_lds_sync();
+            const int mn = min(nl, nr);
+            int K = 0;
+            for (int kb = 0; kb < mn; kb += 64) {
+                const int k = kb + lane;
+                const unsigned long long m = __ballot(k < mn && Ls[k] < Rs[k]);
+                K += popc64(m);
+                if (m != ~0ull) break;   // the predicate holds on a prefix of k
+            }
+            for (int k = lane; k < K; k += 64) {
+                const int li = Ls[k], ri = Rs[k];
+                const QtItem x = a[li], y = a[ri];
+                a[li] = y;
+                a[ri] = x;
+            }
+            wave_lds_sync();
+            int cut;
+            if (K == 0) cut = Ls[0];
+            else {
+                const int c1 = K < nl ? Ls[K] : hi;
+                const int c2 = Rs[K - 1];
+                cut = c1 < c2 ? c1 : c2;
+            }
+            if (lane == 0) {
+                stk[3 * sp] = lo; stk[3 * sp + 1] = cut; stk[3 * sp + 2] = depth;
+                stk[3 * sp + 3] = cut; stk[3 * sp + 4] = hi; stk[3 * sp + 5] = depth;
+            }
+            sp += 2;
+            wave_lds_sync();
+            continue;
+        }
+        for (int i = lo + lane; i < hi; i += 64) { seg_lo[i] = lo; seg_len[i] = hi - lo; }
+        wave_lds_sync();
+    }
+    // final insertion pass == stable sort inside each final segment
+    for (int i = lane; i < n; i += 64) {
+        const QtItem v = a[i];
+        if (seg_len[i] < 0) { tmp[i] = v; continue; }
+        const int lo = seg_lo[i], hi = lo + seg_len[i];
+        int r = 0;
+        for (int j = lo; j < hi; j++) {
+            const int sj = a[j].size;
+            r += (sj > v.size) || (sj == v.size && j < i);
+        }
+        tmp[lo + r] = v;
+    }
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) a[i] = tmp[i];
+    wave_lds_sync();
+}
+
 __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
                                                        const uint32_t* __restrict__ slots, const CellDev* cells,
                                                        uint32_t* __restrict__ Pbuf, uint32_t* __restrict__ Tbuf,
@@ -429,6 +598,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     int* ib = ia + NC;
     __shared__ int tmp[16];
     __shared__ int s_n, s_ndiv, s_state, s_proc, s_fail;
+    __shared__ int stk[3 * 64];
     __shared__ int rc[MAX_ROOTS];
 
     const int l = blockIdx.x, f = blockIdx.y;
@@ -444,16 +614,22 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     const int* ccell = cell_cnt + (long long)f * g.ncells_total + L.cell_base;
     const uint32_t* fslots = slots + (long long)f * g.slot_frame;
 
-    // ---- gather candidates in cell raster order (DetectFAST push_back order)
+    // ---- gather candidates in cell raster order (DetectFAST push_back order): per-cell offsets by a
+    //      block scan, then one wave per cell copies its points (coalesced)
     int carry = 0;
     for (int b = 0; b < L.ncells; b += blockDim.x) {
         const int i = b + threadIdx.x;
         const int v = i < L.ncells ? ccell[i] : 0;
         int tot;
         const int ex = block_excl_scan(v, tmp, &tot);
-        if (i < L.ncells) {
-            const uint32_t* s = fslots + cells[L.cell_base + i].slot;
-            for (int j = 0; j < v; j++) P[carry + ex + j] = s[j];
+        if (i < L.ncells) ia[i - b] = carry + ex;     // chunk-local offsets
+        __syncthreads();
+        const int nc = min((int)blockDim.x, L.ncells - b);
+        for (int c = w; c < nc; c += nw) {
+            const int n = ccell[b + c];
+            const uint32_t* src = fslots + cells[L.cell_base + b + c].slot;
+            uint32_t* dst = P + ia[c];
+            for (int j = lane_id(); j < n; j += 64) dst[j] = src[j];
         }
         carry += tot;
         __syncthreads();
@@ -597,9 +773,11 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             // Phase 2 round (:632-672): split the previous round's divisible nodes, largest
             // first (std::sort, emulated), stopping as soon as the list reaches nfeat.
             const int m = s_ndiv;
-            if (threadIdx.x == 0) {
-                for (int j = 0; j < m; j++) prev[j] = divs[j];
-                qt_sort(prev, prev + m);
+            for (int j = threadIdx.x; j < m; j += blockDim.x) prev[j] = divs[j];
+            __syncthreads();
+            if (w == 0) {
+                int* seg = reinterpret_cast<int*>(cc);   // cc is free until the splits below
+                qt_sort_wave(prev, m, ia, ib, seg, seg + NC, divs, stk);
             }
             __syncthreads();
             for (int j = w; j < m; j += nw) {
@@ -607,14 +785,19 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                 if (lane_id() == 0) cc[j] = c;
             }
             for (int i = threadIdx.x; i < n; i += blockDim.x) ia[i] = 0;   // erased flags
+            if (threadIdx.x == 0) s_proc = m;
             __syncthreads();
-            if (threadIdx.x == 0) {
-                int count = n, proc = m;
-                for (int j = 0; j < m; j++) {
-                    count += ne4(cc[j]) - 1;
-                    if (count >= nfeat) { proc = j + 1; break; }
+            // first sorted item whose split brings the list to nfeat (:666-667), by prefix sums
+            {
+                int carry2 = 0;
+                for (int b = 0; b < m; b += blockDim.x) {
+                    const int j = b + threadIdx.x;
+                    const int d = j < m ? ne4(cc[j]) - 1 : 0;
+                    int tot;
+                    const int ex = block_excl_scan(d, tmp, &tot);
+                    if (j < m && n + carry2 + ex + d >= nfeat) atomicMin(&s_proc, j + 1);
+                    carry2 += tot;
                 }
-                s_proc = proc;
             }
             __syncthreads();
             const int proc = s_proc;
@@ -756,13 +939,15 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
     int step;
     const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
-    // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101)
+    // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101):
+    // lane = column, all 43 row loads issued before the LDS stores
     if (lane < PATCH) {
         const int xx = reflect101(kx - 21 + lane, L.w);
-        for (int r = 0; r < PATCH; r++) {
-            const int yy = reflect101(ky - 21 + r, L.h);
-            R[r * RS + lane] = img[(long long)yy * step + xx];
-        }
+        uint8_t v[PATCH];
+#pragma unroll
+        for (int r = 0; r < PATCH; r++) v[r] = img[(long long)reflect101(ky - 21 + r, L.h) * step + xx];
+#pragma unroll
+        for (int r = 0; r < PATCH; r++) R[r * RS + lane] = v[r];
     }
     __syncthreads();
 
@@ -830,6 +1015,12 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         }
         reinterpret_cast<float*>(kps + o)[lane] = fv;
     }
+}
+
+__global__ __launch_bounds__(64) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
+    __shared__ int stk[3 * 64];
+    qt_sort_wave(items, n, scratch, scratch + n, scratch + 2 * n, scratch + 3 * n,
+                 reinterpret_cast<QtItem*>(scratch + 4 * n), stk);
 }
 
 }  // namespace orbamd
@@ -1017,7 +1208,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.slot_frame = std::max<long long>(slot, 1);
     g.cand_frame = std::max<long long>(cand, 1);
     g.out_frame = std::max(out, 1);
-    NC = (int)align_up(NC, 64);
+    NC = (int)align_up(std::max(NC, 256), 64);   // >= blockDim: the gather reuses the node scratch
     const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int));
     if (lds > 156 * 1024) {   // gfx950: 160 KiB LDS per workgroup
         set_error("nfeatures too large for the quadtree LDS budget (per-level quota <= ~2100)");
@@ -1109,7 +1300,7 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
     uint32_t* fault = h->d_fault.as<uint32_t>();
     if (g.ncells_total > 0) {
         StageMark m1(h, st, 1);
-        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)g.ncells_total, (unsigned)F), dim3(256), 0, st, g,
+        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)g.ncells_total, (unsigned)F), dim3(64), 0, st, g,
                            h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST, h->p.minThFAST,
                            h->d_slots.as<uint32_t>(), h->d_cellcnt.as<int>(), fault);
     }
@@ -1371,6 +1562,26 @@ int orbx_profile_read(orbx_extractor* h, double* ms, int32_t* launches) {
         if (launches) launches[k] = (int32_t)h->prof_ev[k].size();
         h->prof_ev[k].clear();
     }
+    return ORB_OK;
+}
+
+int orbx_debug_qt_sort(const int32_t* sizes, int n, int32_t* perm) {
+    ORB_CHECK_ARG(n >= 0 && (n == 0 || (sizes && perm)), "bad argument");
+    if (n == 0) return ORB_OK;
+    std::vector<QtItem> h(n);
+    for (int i = 0; i < n; i++) h[i] = QtItem{sizes[i], i};
+    DevBuf d;
+    int rc;
+    if ((rc = d.reserve((size_t)n * sizeof(QtItem) + (size_t)n * 6 * sizeof(int) + 64))) return rc;
+    QtItem* items = d.as<QtItem>();
+    int* scratch = reinterpret_cast<int*>(items + n);
+    ORB_HIP_TRY(hipMemcpy(items, h.data(), n * sizeof(QtItem), hipMemcpyHostToDevice));
+    // the kernel keeps items in global memory (same code path as LDS: generic pointers)
+    hipLaunchKernelGGL(qt_sort_test_kernel, dim3(1), dim3(64), 0, 0, items, n, scratch);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpy(h.data(), items, n * sizeof(QtItem), hipMemcpyDeviceToHost));
+    d.release();
+    for (int i = 0; i < n; i++) perm[i] = h[i].node;
     return ORB_OK;
 }
 

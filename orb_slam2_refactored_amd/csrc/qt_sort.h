@@ -188,4 +188,74 @@ QT_HD void qt_sort(QtItem* first, QtItem* last) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Data-parallel formulation of the same sort (what the quadtree kernel runs on a wavefront).
+//
+//  * __unguarded_partition(first+1, last, pivot=first) with p = pivot.size: let Ls = ascending
+//    positions in [first+1, last) with size <= p (left-scan stops) and Rs = descending positions
+//    in [first, last) with size >= p (right-scan stops), both in the array as it stands before
+//    the partition.  The k-th swap exchanges Ls[k] and Rs[k] for every k with Ls[k] < Rs[k]
+//    (a prefix of k, K of them), and the returned cut is Ls[0] when K == 0, otherwise
+//    min(Ls[K], Rs[K-1]).  (Positions strictly between the k-th stops are untouched by earlier
+//    swaps, so each scan's next stop is the next original stopper or the nearest swapped slot.)
+//  * __final_insertion_sort is a stable insertion sort, and introsort_loop leaves the array as a
+//    sequence of final segments (<= 16 elements, or heap-sorted) with every element of a segment
+//    >= every element of any later segment; so the insertion pass is a stable sort inside each
+//    final segment.
+// qt_sort_parallel_form() is the sequential statement of that formulation, checked against
+// std::sort by tests/native/qt_sort_check.cpp.
+// ------------------------------------------------------------------------------------------
+QT_HD int qt_partition_parallel_form(QtItem* a, int lo, int hi, int* Ls, int* Rs) {
+    const int p = a[lo].size;
+    int nl = 0, nr = 0;
+    for (int i = lo + 1; i < hi; i++)
+        if (a[i].size <= p) Ls[nl++] = i;
+    for (int j = hi - 1; j >= lo; j--)
+        if (a[j].size >= p) Rs[nr++] = j;
+    int K = 0;
+    while (K < nl && K < nr && Ls[K] < Rs[K]) K++;
+    for (int k = 0; k < K; k++) qt_swap(&a[Ls[k]], &a[Rs[k]]);
+    if (K == 0) return Ls[0];
+    const int c1 = K < nl ? Ls[K] : hi;
+    return c1 < Rs[K - 1] ? c1 : Rs[K - 1];
+}
+
+// seg_lo[i] / seg_len[i]: final segment of position i (seg_len < 0: heap-sorted segment).
+QT_HD void qt_sort_parallel_form(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, int* seg_len, QtItem* tmp) {
+    if (n <= 0) return;
+    struct Frame { int lo, hi, depth; };
+    Frame stack[64];
+    int sp = 0;
+    stack[sp++] = Frame{0, n, 2 * qt_lg(n)};
+    while (sp > 0) {
+        Frame f = stack[--sp];
+        int lo = f.lo, hi = f.hi, depth = f.depth;
+        if (hi - lo > 16) {
+            if (depth == 0) {
+                qt_heap_sort(a + lo, a + hi);
+                for (int i = lo; i < hi; i++) { seg_lo[i] = lo; seg_len[i] = -1; }
+                continue;
+            }
+            --depth;
+            const int mid = lo + (hi - lo) / 2;
+            qt_median_to_first(a + lo, a + lo + 1, a + mid, a + hi - 1);
+            const int cut = qt_partition_parallel_form(a, lo, hi, Ls, Rs);
+            stack[sp++] = Frame{lo, cut, depth};
+            stack[sp++] = Frame{cut, hi, depth};
+            continue;
+        }
+        for (int i = lo; i < hi; i++) { seg_lo[i] = lo; seg_len[i] = hi - lo; }
+    }
+    // stable sort inside each final segment (descending size)
+    for (int i = 0; i < n; i++) {
+        if (seg_len[i] < 0) { tmp[i] = a[i]; continue; }
+        const int lo = seg_lo[i], hi = lo + seg_len[i];
+        int r = 0;
+        for (int j = lo; j < hi; j++)
+            r += (a[j].size > a[i].size) || (a[j].size == a[i].size && j < i);
+        tmp[lo + r] = a[i];
+    }
+    for (int i = 0; i < n; i++) a[i] = tmp[i];
+}
+
 }  // namespace orbamd

@@ -29,10 +29,18 @@ int main(int argc, char** argv) {
             for (int i = 0; i < n; i++) emu[i] = {(int)ref[i].size, (int)(ref[i].ptr - tags)};
         }
         std::sort(ref.begin(), ref.end(), [](const DivisibleNode& a, const DivisibleNode& b) { return a.size > b.size; });
+        std::vector<orbamd::QtItem> par = emu;
         orbamd::qt_sort(emu.data(), emu.data() + n);
+        std::vector<int> Ls(n + 1), Rs(n + 1), sl(n + 1), sn(n + 1);
+        std::vector<orbamd::QtItem> tmp(n + 1);
+        orbamd::qt_sort_parallel_form(par.data(), n, Ls.data(), Rs.data(), sl.data(), sn.data(), tmp.data());
         for (int i = 0; i < n; i++) {
             if ((int)(ref[i].ptr - tags) != emu[i].node || (int)ref[i].size != emu[i].size) {
                 printf("MISMATCH case %d n %d at %d\n", c, n, i);
+                return 1;
+            }
+            if (par[i].node != emu[i].node) {
+                printf("PARALLEL-FORM MISMATCH case %d n %d at %d\n", c, n, i);
                 return 1;
             }
         }

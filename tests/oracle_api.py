@@ -213,3 +213,10 @@ def local_ba(prob, stop=None):
     out["iterations"] = tuple(res.iterations)
     out["chi2"] = tuple(res.chi2)
     return out
+
+
+def std_sort_perm(sizes):
+    sizes = np.ascontiguousarray(sizes, np.int32)
+    perm = np.zeros(len(sizes), np.int32)
+    lib().oracle_std_sort_sizes(ptr(sizes), len(sizes), ptr(perm))
+    return perm

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes: per kernel, the mean per-dispatch value of each counter."""
+import csv
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def main(d):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in sorted(Path(d).rglob("run_counter_collection.csv")):
+        per = defaultdict(lambda: defaultdict(float))
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"].split("(")[0].replace("orbamd::", "")
+            per[(name, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        for (name, _), cs in per.items():
+            for c, v in cs.items():
+                acc[name][c].append(v)
+    for name, cs in sorted(acc.items()):
+        print(name)
+        for c, vs in sorted(cs.items()):
+            print(f"   {c:24s} {sum(vs) / len(vs):16.1f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
