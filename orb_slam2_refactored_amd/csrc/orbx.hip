@@ -487,6 +487,19 @@ __device__ __forceinline__ void qt_emit_children(const QtNode& parent, int4 cc, 
     }
 }
 
+#ifdef ORB_QT_STAMPS
+__device__ unsigned long long g_qt_stamps[64];
+#define QT_STAMP(k)                                                                                \
+    do {                                                                                           \
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && (k) < 64)                    \
+            g_qt_stamps[(k)] = __builtin_amdgcn_s_memtime();                                       \
+    } while (0)
+#else
+#define QT_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // std::sort(a, a+n, size-descending) on one wavefront: qt_sort_parallel_form() (qt_sort.h) with
@@ -587,7 +600,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                                                        const uint32_t* __restrict__ slots, const CellDev* cells,
                                                        uint32_t* __restrict__ Pbuf, uint32_t* __restrict__ Tbuf,
                                                        uint32_t* __restrict__ sel, int* __restrict__ sel_cnt, int NC,
-                                                       uint32_t* fault) {
+                                                       int PTC, uint32_t* fault) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     QtNode* na = reinterpret_cast<QtNode*>(smem);
     QtNode* nb = na + NC;
@@ -596,12 +609,14 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     QtItem* prev = divs + NC;
     int* ia = reinterpret_cast<int*>(prev + NC);    // per-node scratch (flags / positions)
     int* ib = ia + NC;
+    uint32_t* lds_P = reinterpret_cast<uint32_t*>(ib + NC);   // candidate arrays when they fit
+    uint32_t* lds_T = lds_P + PTC;
     __shared__ int tmp[16];
     __shared__ int s_n, s_ndiv, s_state, s_proc, s_fail;
     __shared__ int stk[3 * 64];
     __shared__ int rc[MAX_ROOTS];
 
-    const int l = blockIdx.x, f = blockIdx.y;
+    const int f = blockIdx.x, l = blockIdx.y;   // level-major grid: level-0 trees start first
     const LevelDev& L = g.lv[l];
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     int* scnt = sel_cnt + f * g.nlevels + l;
@@ -611,30 +626,47 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     }
     uint32_t* P = Pbuf + (long long)f * g.cand_frame + L.cand_base;
     uint32_t* T = Tbuf + (long long)f * g.cand_frame + L.cand_base;
+    uint32_t* gP = P;
     const int* ccell = cell_cnt + (long long)f * g.ncells_total + L.cell_base;
     const uint32_t* fslots = slots + (long long)f * g.slot_frame;
 
-    // ---- gather candidates in cell raster order (DetectFAST push_back order): per-cell offsets by a
-    //      block scan, then one wave per cell copies its points (coalesced)
+    QT_STAMP(0);
+    // ---- gather candidates in cell raster order (DetectFAST push_back order).  Pass 1: total count;
+    //      the arrays live in LDS when they fit.  Pass 2: one lane per cell copies its points.
+    int n_total = 0;
+    {
+        int part = 0;
+        for (int i = threadIdx.x; i < L.ncells; i += blockDim.x) part += ccell[i];
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        if (lane_id() == 0) tmp[8 + w] = part;
+        __syncthreads();
+        for (int q = 0; q < nw; q++) n_total += tmp[8 + q];
+        __syncthreads();
+    }
+    if (n_total <= PTC) { P = lds_P; T = lds_T; }
     int carry = 0;
     for (int b = 0; b < L.ncells; b += blockDim.x) {
         const int i = b + threadIdx.x;
         const int v = i < L.ncells ? ccell[i] : 0;
         int tot;
         const int ex = block_excl_scan(v, tmp, &tot);
-        if (i < L.ncells) ia[i - b] = carry + ex;     // chunk-local offsets
-        __syncthreads();
-        const int nc = min((int)blockDim.x, L.ncells - b);
-        for (int c = w; c < nc; c += nw) {
-            const int n = ccell[b + c];
-            const uint32_t* src = fslots + cells[L.cell_base + b + c].slot;
-            uint32_t* dst = P + ia[c];
-            for (int j = lane_id(); j < n; j += 64) dst[j] = src[j];
+        if (v > 0) {
+            const uint32_t* __restrict__ src = fslots + cells[L.cell_base + i].slot;
+            uint32_t* dst = P + carry + ex;
+            for (int j0 = 0; j0 < v; j0 += 8) {
+                uint32_t r[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) r[q] = j0 + q < v ? src[j0 + q] : 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (j0 + q < v) dst[j0 + q] = r[q];
+            }
         }
         carry += tot;
-        __syncthreads();
     }
+    __syncthreads();
     const int n_src = carry;
+    QT_STAMP(1);
     if (n_src == 0) {
         if (threadIdx.x == 0) *scnt = 0;
         return;
@@ -698,10 +730,21 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     __syncthreads();
 
     const int nfeat = L.quota;
+    QT_STAMP(2);
+    int iter_no = 0;
+    (void)iter_no;
+    (void)gP;
     // ---- main loop
     while (true) {
         const int n = s_n;
         const int state = s_state;
+        QT_STAMP(3 + 2 * iter_no);
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+#ifdef ORB_QT_STAMPS
+            if (4 + 2 * iter_no < 60) g_qt_stamps[4 + 2 * iter_no] = ((unsigned long long)state << 32) | (unsigned)n;
+#endif
+        }
+        iter_no++;
         if (state == 2) break;
         if (state == 0) {
             // Phase 1 pass (:588-630): split every divisible node in list order.
@@ -854,24 +897,27 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
         }
     }
 
-    // ---- retain the best point per node (:677-692): strict '>' => first maximum wins
+    // ---- retain the best point per node (:677-692): strict '>' => first maximum wins.  One lane
+    //      per node (nodes are small at this point).
     const int n = s_n;
     uint32_t* out = sel + (long long)f * g.out_frame + L.out_base;
     if (n > L.out_cap && threadIdx.x == 0) atomicOr(fault, FAULT_OUT_CAP);
-    for (int i = w; i < n && i < L.out_cap; i += nw) {
-        const QtNode& nd = na[i];
-        int bs = -1, bj = 0x7fffffff;
-        for (int j = lane_id(); j < nd.cnt; j += 64) {
-            const int s = kp_s(P[nd.beg + j]);
-            if (s > bs) { bs = s; bj = j; }
+    for (int i = threadIdx.x; i < n && i < L.out_cap; i += blockDim.x) {
+        const QtNode nd = na[i];
+        int bs = -1;
+        uint32_t best = 0;
+        for (int j0 = 0; j0 < nd.cnt; j0 += 4) {
+            uint32_t r[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) r[q] = j0 + q < nd.cnt ? P[nd.beg + j0 + q] : 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (j0 + q < nd.cnt && kp_s(r[q]) > bs) { bs = kp_s(r[q]); best = r[q]; }
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            const int os = __shfl_xor(bs, o, 64), oj = __shfl_xor(bj, o, 64);
-            if (os > bs || (os == bs && oj < bj)) { bs = os; bj = oj; }
-        }
-        if (lane_id() == 0) out[i] = P[nd.beg + bj];
+        out[i] = best;
     }
     if (threadIdx.x == 0) *scnt = min(n, L.out_cap);
+    QT_STAMP(63);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1042,7 +1088,7 @@ struct orbx_extractor {
     int g_rows = -1, g_cols = -1;
     Geom geom;
     std::vector<CellDev> cells;
-    int NC = 0;
+    int NC = 0, PTC = 0;
     size_t qt_lds = 0;
     DevBuf d_cells, d_xtab, d_ytab;
 
@@ -1209,7 +1255,9 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.cand_frame = std::max<long long>(cand, 1);
     g.out_frame = std::max(out, 1);
     NC = (int)align_up(std::max(NC, 256), 64);   // >= blockDim: the gather reuses the node scratch
-    const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int));
+    const int PTC = 4096;   // candidate points kept in LDS (P and T) when a level has at most this many
+    const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int)) +
+                       (size_t)PTC * 8;
     if (lds > 156 * 1024) {   // gfx950: 160 KiB LDS per workgroup
         set_error("nfeatures too large for the quadtree LDS budget (per-level quota <= ~2100)");
         return ORB_EINVAL;
@@ -1230,6 +1278,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     h->geom = g;
     h->cells = cells;
     h->NC = NC;
+    h->PTC = PTC;
     h->qt_lds = lds;
     h->g_rows = rows;
     h->g_cols = cols;
@@ -1306,10 +1355,10 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
     }
     {
     StageMark m2(h, st, 2);
-    hipLaunchKernelGGL(quadtree_kernel, dim3((unsigned)g.nlevels, (unsigned)F), dim3(256), h->qt_lds, st, g,
+    hipLaunchKernelGGL(quadtree_kernel, dim3((unsigned)F, (unsigned)g.nlevels), dim3(256), h->qt_lds, st, g,
                        h->d_cellcnt.as<int>(), h->d_slots.as<uint32_t>(), h->d_cells.as<CellDev>(),
                        h->d_P.as<uint32_t>(), h->d_T.as<uint32_t>(), h->d_sel.as<uint32_t>(), h->d_selcnt.as<int>(),
-                       h->NC, fault);
+                       h->NC, h->PTC, fault);
     }
     {
     StageMark m3(h, st, 3);
@@ -1583,6 +1632,18 @@ int orbx_debug_qt_sort(const int32_t* sizes, int n, int32_t* perm) {
     d.release();
     for (int i = 0; i < n; i++) perm[i] = h[i].node;
     return ORB_OK;
+}
+
+int orbx_debug_qt_stamps(unsigned long long* out) {
+#ifdef ORB_QT_STAMPS
+    ORB_HIP_TRY(hipDeviceSynchronize());
+    ORB_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), 64 * 8));
+    return ORB_OK;
+#else
+    (void)out;
+    set_error("built without ORB_QT_STAMPS");
+    return ORB_EINVAL;
+#endif
 }
 
 }  // extern "C"

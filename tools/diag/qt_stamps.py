@@ -1,0 +1,37 @@
+"""Diagnostic: quadtree phase stamps of (frame 0, level 0) with the ORB_QT_STAMPS build."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+os.environ["ORBSLAM2_AMD_LIB"] = str(ROOT / "tools" / "diag" / "liborbslam2_amd_stamps.so")
+sys.path.insert(0, str(ROOT))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from orb_slam2_refactored_amd import ORBextractor  # noqa: E402
+from orb_slam2_refactored_amd._lib import lib  # noqa: E402
+from orb_slam2_refactored_amd.synth import synth_image  # noqa: E402
+
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+frames = torch.from_numpy(np.stack([synth_image(i % 16, 1280, 720) for i in range(F)])).cuda()
+ex = ORBextractor(ORBextractor.Parameters(nfeatures=2000))
+for _ in range(3):
+    ex.extract_batch_device(frames)
+torch.cuda.synchronize()
+buf = (C.c_ulonglong * 64)()
+lib().orbx_debug_qt_stamps.argtypes = [C.c_void_p]
+assert lib().orbx_debug_qt_stamps(C.cast(buf, C.c_void_p)) == 0
+v = list(buf)
+t0 = v[0]
+print("gather", v[1] - t0, "roots", v[2] - v[1])
+i = 0
+prev = v[2]
+while 3 + 2 * i < 63 and v[3 + 2 * i] > 0 and 4 + 2 * i < 64:
+    st = v[4 + 2 * i]
+    print(f"iter {i}: state {st >> 32} n {st & 0xffffffff} t {v[3 + 2 * i] - t0} (+{v[3 + 2 * i] - prev})")
+    prev = v[3 + 2 * i]
+    if (st >> 32) == 2:
+        break
+    i += 1
+print("end", v[63] - t0, "(+", v[63] - prev, ")   [s_memtime ticks]")
