@@ -96,6 +96,9 @@ __device__ __forceinline__ const uint8_t* level_base(const Geom& g, int l, int f
     return pyr + (long long)f * g.pyr_frame_bytes + g.lv[l].off;
 }
 
+// Orders this wavefront's LDS accesses across lanes (LDS ops of one wave complete in order).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // Wave-inclusive scan of ints (64 lanes).
 __device__ __forceinline__ int wave_incl_scan(int v) {
     const int l = lane_id();
@@ -179,11 +182,11 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
 constexpr int CS = 72;   // LDS crop row stride (bytes)
 constexpr int ZS = 64;   // LDS zone row stride
 
-__device__ __forceinline__ int corner_strength(const uint8_t* c) {   // c -> centre pixel in LDS
+__device__ __forceinline__ int corner_strength(const uint8_t* c, int cs) {   // c -> centre pixel in LDS
     const int v = c[0];
     int d[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)c[c_circle_dy_h[k] * CS + c_circle_dx_h[k]];
+    for (int k = 0; k < 16; k++) d[k] = v - (int)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]];
     int lo2[16], hi2[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -209,12 +212,12 @@ __device__ __forceinline__ int corner_strength(const uint8_t* c) {   // c -> cen
 }
 
 // Cheap exact test for "corner at threshold t": a 9-run of bright or of dark circle pixels.
-__device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t) {
+__device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t, int cs) {
     const int v = c[0];
     unsigned br = 0, dk = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int p = c[c_circle_dy_h[k] * CS + c_circle_dx_h[k]];
+        const int p = c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]];
         br |= (unsigned)(p > v + t) << k;
         dk |= (unsigned)(p < v - t) << k;
     }
@@ -228,35 +231,60 @@ __device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t) {
     return run9(br) || run9(dk);
 }
 
-// Necessary condition for a 9-arc at threshold t: two circle-adjacent compass points (circle
-// positions 0/4/8/12) both brighter than v+t or both darker than v-t.
-__device__ __forceinline__ bool compass_test(const uint8_t* c, int t) {
-    const int v = c[0];
-    const int p0 = c[3 * CS], p4 = c[3], p8 = c[-3 * CS], p12 = c[-3];
-    const bool b0 = p0 > v + t, b4 = p4 > v + t, b8 = p8 > v + t, b12 = p12 > v + t;
-    const bool d0 = p0 < v - t, d4 = p4 < v - t, d8 = p8 < v - t, d12 = p12 < v - t;
-    return (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
+// Necessary condition for a 9-arc at threshold t, on 4 horizontally adjacent pixels at once: two
+// circle-adjacent compass points (positions 0/4/8/12) both brighter than v+t, or both darker than
+// v-t.  With packed u16 lanes: bright <=> max over the 4 adjacent pairs of min(pa, pb) > v + t,
+// dark <=> min over the pairs of max(pa, pb) < v - t (no clamping needed: p <= 255).
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ us2 lo_pair(uint32_t w) {   // bytes 0,1 -> u16 lanes
+    const uint32_t r = __builtin_amdgcn_perm(0u, w, 0x0c010c00u);
+    return *reinterpret_cast<const us2*>(&r);
+}
+__device__ __forceinline__ us2 hi_pair(uint32_t w) {   // bytes 2,3 -> u16 lanes
+    const uint32_t r = __builtin_amdgcn_perm(0u, w, 0x0c030c02u);
+    return *reinterpret_cast<const us2*>(&r);
+}
+__device__ __forceinline__ uint32_t compass2(us2 v, us2 n, us2 e, us2 s, us2 wv, us2 t) {
+    const us2 bmax = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_elementwise_min(n, e), __builtin_elementwise_min(e, s)),
+                                               __builtin_elementwise_max(__builtin_elementwise_min(s, wv), __builtin_elementwise_min(wv, n)));
+    const us2 dmin = __builtin_elementwise_min(__builtin_elementwise_min(__builtin_elementwise_max(n, e), __builtin_elementwise_max(e, s)),
+                                               __builtin_elementwise_min(__builtin_elementwise_max(s, wv), __builtin_elementwise_max(wv, n)));
+    const us2 hi = v + t;
+    const us2 lo = __builtin_elementwise_sub_sat(v, t);
+    const us2 f = __builtin_elementwise_sub_sat(bmax, hi) | __builtin_elementwise_sub_sat(lo, dmin);
+    return (f.x ? 1u : 0u) | (f.y ? 2u : 0u);
 }
 
-// One wavefront per (cell, frame).  Lanes tile the detection zone as 2 rows x 32 columns (zone
-// width <= 32) or 1 row x 64, so lane order inside a chunk is row-major — FAST's emission order —
-// and every prefix is a ballot + popcount (no workgroup barriers).
-//   1. crop (zone + 3-px apron) -> LDS with aligned dword loads
-//   2. compass pre-test; passers queue in LDS and get the full 9-arc test + corner strength M
-//      densely, 64 at a time; M is stored in a zone map (0 = no corner at min(ini, min) threshold)
-//   3. one pass over the zone: cell-local 3x3 NMS at iniThFAST and at minThFAST, ballots kept
-//   4. emit the iniThFAST set, or the minThFAST set when it is empty (DetectFAST :527-530)
+// One wavefront per (cell, frame).  LDS (sized per launch from the largest cell): the crop
+// (zone + 3-px apron, stored one byte right so zone column 0 is dword aligned), a zone map of
+// corner strengths, a queue of pre-test passers and the ordered list of corners.
+//   1. crop -> LDS with aligned dword loads issued together
+//   2. compass pre-test, 4 pixels per lane, passers queued in row-major order
+//   3. queued pixels get the full 9-arc test at min(ini, min) densely, 64 at a time; corners are
+//      appended in row-major order
+//   4. corner strength M (cornerScore + 1) for the corner list; NMS at iniThFAST and minThFAST
+//      over the list (3x3, cell-local: neighbours outside the zone count as 0)
+//   5. emit the iniThFAST set, or the minThFAST set when it is empty (DetectFAST :527-530)
+struct FastLds {
+    int CS, ZS, crop_bytes, mz_bytes, qcap, ccap;
+};
+
 __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
-                                                        int* __restrict__ cell_cnt, uint32_t* fault) {
-    __shared__ __attribute__((aligned(16))) uint8_t crop[MAX_CROP * CS];
-    __shared__ __attribute__((aligned(16))) uint8_t Mz[MAX_ZONE * ZS];
-    __shared__ unsigned long long bal[2][MAX_ZONE];
-    __shared__ short queue[128];
+                                                        int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
+    uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
+    uint8_t* Mz = fsm + fl.crop_bytes;
+    short* queue = reinterpret_cast<short*>(Mz + fl.mz_bytes);
+    short* clist = queue + fl.qcap;
+    unsigned long long* bal = reinterpret_cast<unsigned long long*>(clist + fl.ccap);
+    const int CSd = fl.CS, ZSd = fl.ZS;
 
     const int lane = threadIdx.x;
+    const unsigned long long lt = lanemask_lt();
     const CellDev cell = cells[blockIdx.x];
     const int f = blockIdx.y;
     const int x0 = cell.x0y0 & 0xffff, y0 = cell.x0y0 >> 16;
@@ -265,11 +293,10 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     int step;
     const uint8_t* img = level_base(g, cell.level, f, in, in_fstride, in_step, pyr, &step);
 
-    // 1. crop: lanes = 16 dwords x 4 rows; dword-aligned global loads issued together (kept in
-    //    registers), then bytes scattered into LDS
+    // 1. crop
     {
         const int j = lane & 15, rr = lane >> 4;
-        constexpr int NR = (MAX_CROP + 3) / 4;   // row iterations (4 rows each)
+        constexpr int NR = (MAX_CROP + 3) / 4;
         uint32_t w[NR][2];
         int offr[NR];
 #pragma unroll
@@ -296,52 +323,78 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int c = 4 * (j + 16 * h) + q - offr[it];
-                    if (c >= 0 && c < cw) crop[r * CS + c] = (uint8_t)(w[it][h] >> (8 * q));
+                    if (c >= 0 && c < cw) crop[r * CSd + 1 + c] = (uint8_t)(w[it][h] >> (8 * q));
                 }
         }
-        for (int i = lane; i < zh * (ZS / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
+        for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
     }
     __syncthreads();
 
-    const bool narrow = zw <= 32;
-    const int rows_per = narrow ? 2 : 1;
-    const int lx = narrow ? (lane & 31) : lane;
-    const int ly = narrow ? (lane >> 5) : 0;
     const int tlo = min(th_ini, th_min);
-    const unsigned long long lt = lanemask_lt();
+    const us2 t2 = {(unsigned short)tlo, (unsigned short)tlo};
+    // lanes: QR quads per row (8 or 16), 64/QR rows per chunk
+    const int qsh = zw <= 32 ? 3 : 4;
+    const int QR = 1 << qsh, RPC = 64 >> qsh;
+    const int qx = (lane & (QR - 1)) * 4, qy = lane >> qsh;
 
-    // 2. compass pre-test -> queue -> dense full test
-    int qn = 0;   // wave-uniform queue length
+    int qn = 0, nc = 0;
     auto drain = [&](int n) {
         const int i = lane < n ? queue[lane] : -1;
-        int m = 0;
-        if (i >= 0) {
-            const uint8_t* c = &crop[((i >> 6) + 3) * CS + (i & 63) + 3];
-            if (is_corner_t(c, tlo)) m = min(corner_strength(c), 255);
-        }
-        if (m > 0) Mz[i] = (uint8_t)m;
+        bool c = false;
+        if (i >= 0) c = is_corner_t(&crop[((i / ZSd) + 3) * CSd + 1 + (i % ZSd) + 3], tlo, CSd);
+        const unsigned long long bm = __ballot(c);
+        if (c) clist[nc + popc64(bm & lt)] = (short)i;
+        nc += popc64(bm);
     };
-    for (int yb = 0; yb < zh; yb += rows_per) {
-        const int y = yb + ly;
-        const bool pass = y < zh && lx < zw && compass_test(&crop[(y + 3) * CS + lx + 3], tlo);
-        const unsigned long long bm = __ballot(pass);
-        if (pass) queue[qn + popc64(bm & lt)] = (short)(y * ZS + lx);
-        qn += popc64(bm);
-        __syncthreads();
-        if (qn >= 64) {
+    for (int yb = 0; yb < zh; yb += RPC) {
+        const int y = yb + qy;
+        uint32_t mask = 0;
+        if (y < zh && qx < zw) {
+            const uint8_t* rowc = crop + (y + 3) * CSd + 4;   // zone (y, 0) = crop (y+3, 3) at byte 4
+            const uint32_t wv = *reinterpret_cast<const uint32_t*>(rowc + qx);
+            const uint32_t wl = *reinterpret_cast<const uint32_t*>(rowc + qx - 4);
+            const uint32_t wr = *reinterpret_cast<const uint32_t*>(rowc + qx + 4);
+            const uint32_t wn = *reinterpret_cast<const uint32_t*>(rowc + 3 * CSd + qx);   // (0,+3)
+            const uint32_t ws = *reinterpret_cast<const uint32_t*>(rowc - 3 * CSd + qx);   // (0,-3)
+            const uint32_t we = __builtin_amdgcn_alignbyte(wr, wv, 3);   // (+3, 0): bytes qx+3..qx+6
+            const uint32_t ww = __builtin_amdgcn_alignbyte(wv, wl, 1);   // (-3, 0): bytes qx-3..qx
+            mask = compass2(lo_pair(wv), lo_pair(wn), lo_pair(we), lo_pair(ws), lo_pair(ww), t2) |
+                   (compass2(hi_pair(wv), hi_pair(wn), hi_pair(we), hi_pair(ws), hi_pair(ww), t2) << 2);
+            const int valid = min(4, zw - qx);
+            mask &= (1u << valid) - 1u;
+        }
+        // ordered compaction of up to 4 passers per lane
+        const int cnt = __popc(mask);
+        const int incl = wave_incl_scan(cnt);
+        int pos = qn + incl - cnt;
+        for (int k = 0; k < 4; k++)
+            if (mask & (1u << k)) queue[pos++] = (short)(y * ZSd + qx + k);
+        qn += __shfl(incl, 63, 64);
+        wave_lds_sync();
+        while (qn >= 64) {
             drain(64);
-            __syncthreads();
-            const short tail = lane + 64 < qn ? queue[lane + 64] : 0;
-            __syncthreads();
-            if (lane + 64 < qn) queue[lane] = tail;
+            wave_lds_sync();
+            short tail[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) tail[k] = lane + 64 * (k + 1) < qn ? queue[lane + 64 * (k + 1)] : 0;
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (lane + 64 * (k + 1) < qn) queue[lane + 64 * k] = tail[k];
             qn -= 64;
-            __syncthreads();
+            wave_lds_sync();
         }
     }
     if (qn > 0) drain(qn);
-    __syncthreads();
+    wave_lds_sync();
 
-    // 3. NMS at both thresholds (neighbours outside the detection zone count as score 0)
+    // corner strengths into the zone map
+    for (int j = lane; j < nc; j += 64) {
+        const int i = clist[j];
+        Mz[i] = (uint8_t)min(corner_strength(&crop[((i / ZSd) + 3) * CSd + 1 + (i % ZSd) + 3], CSd), 255);
+    }
+    wave_lds_sync();
+
     auto nms = [&](int zy, int zx, int m, int t) -> bool {
         if (m <= t) return false;
 #pragma unroll
@@ -351,43 +404,41 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
                 if (!dx && !dy) continue;
                 const int yy = zy + dy, xx = zx + dx;
                 if (yy < 0 || yy >= zh || xx < 0 || xx >= zw) continue;
-                const int q = Mz[yy * ZS + xx];
+                const int q = Mz[yy * ZSd + xx];
                 if (q > t && q >= m) return false;
             }
         return true;
     };
-    int n_ini = 0, n_min = 0, chunk = 0;
-    for (int yb = 0; yb < zh; yb += rows_per, chunk++) {
-        const int y = yb + ly;
-        const bool in_zone = y < zh && lx < zw;
-        const int m = in_zone ? Mz[y * ZS + lx] : 0;
+    int n_ini = 0, n_min = 0;
+    for (int jb = 0, ch2 = 0; jb < nc; jb += 64, ch2++) {
+        const int j = jb + lane;
         bool ki = false, km = false;
-        if (m > 0) {
-            ki = nms(y, lx, m, th_ini);
-            km = nms(y, lx, m, th_min);
+        if (j < nc) {
+            const int i = clist[j];
+            const int zy = i / ZSd, zx = i % ZSd, m = Mz[i];
+            ki = nms(zy, zx, m, th_ini);
+            km = nms(zy, zx, m, th_min);
         }
         const unsigned long long bi = __ballot(ki), bmn = __ballot(km);
-        if (lane == 0) { bal[0][chunk] = bi; bal[1][chunk] = bmn; }
+        if (lane == 0) { bal[2 * ch2] = bi; bal[2 * ch2 + 1] = bmn; }
         n_ini += popc64(bi);
         n_min += popc64(bmn);
     }
-    __syncthreads();
+    wave_lds_sync();
 
-    // 4. emission in row-major order
     const int which = n_ini > 0 ? 0 : 1;
     const int total = which == 0 ? n_ini : n_min;
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
     const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
     int running = 0;
-    chunk = 0;
-    for (int yb = 0; yb < zh; yb += rows_per, chunk++) {
-        const unsigned long long bm = bal[which][chunk];
+    for (int jb = 0, ch2 = 0; jb < nc; jb += 64, ch2++) {
+        const unsigned long long bm = bal[2 * ch2 + which];
         if (bm & (1ull << lane)) {
             const int r = running + popc64(bm & lt);
-            const int y = yb + ly;
+            const int i = clist[jb + lane];
             if (r < cap) {
-                const uint32_t x = (uint32_t)(x0 + 3 + lx), yy = (uint32_t)(y0 + 3 + y);
-                out[r] = x | (yy << 12) | ((uint32_t)(Mz[y * ZS + lx] - 1) << 24);
+                const uint32_t x = (uint32_t)(x0 + 3 + i % ZSd), yy = (uint32_t)(y0 + 3 + i / ZSd);
+                out[r] = x | (yy << 12) | ((uint32_t)(Mz[i] - 1) << 24);
             }
         }
         running += popc64(bm);
@@ -500,7 +551,6 @@ __device__ unsigned long long g_qt_stamps[64];
     } while (0)
 #endif
 
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // std::sort(a, a+n, size-descending) on one wavefront: qt_sort_parallel_form() (qt_sort.h) with
 // each Hoare partition computed from ballot-compacted stopper lists.  Scratch: Ls, Rs, seg_lo,
@@ -1090,6 +1140,8 @@ struct orbx_extractor {
     std::vector<CellDev> cells;
     int NC = 0, PTC = 0;
     size_t qt_lds = 0;
+    FastLds fl;
+    size_t fast_lds = 0;
     DevBuf d_cells, d_xtab, d_ytab;
 
     // workspace for up to ws_frames frames
@@ -1277,6 +1329,20 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         ORB_HIP_TRY(hipMemcpy(h->d_ytab.ptr, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice));
     h->geom = g;
     h->cells = cells;
+    {
+        int mzw = 1, mzh = 1;
+        for (const CellDev& c : cells) { mzw = std::max(mzw, c.zwzh & 0xffff); mzh = std::max(mzh, c.zwzh >> 16); }
+        FastLds fl;
+        fl.CS = (int)align_up(mzw + 6 + 8, 4);         // +1 shift, +4 dword over-read each side
+        fl.ZS = (int)align_up(mzw, 4);
+        fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6), 16);
+        fl.mz_bytes = (int)align_up((size_t)fl.ZS * mzh, 16);
+        fl.qcap = 64 + 4 * 64;
+        fl.ccap = (int)align_up((size_t)mzw * mzh, 8);
+        const int nbal = (fl.ccap + 63) / 64;
+        h->fast_lds = (size_t)fl.crop_bytes + fl.mz_bytes + 2 * (size_t)(fl.qcap + fl.ccap) + 16 * (size_t)nbal;
+        h->fl = fl;
+    }
     h->NC = NC;
     h->PTC = PTC;
     h->qt_lds = lds;
@@ -1349,9 +1415,9 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
     uint32_t* fault = h->d_fault.as<uint32_t>();
     if (g.ncells_total > 0) {
         StageMark m1(h, st, 1);
-        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)g.ncells_total, (unsigned)F), dim3(64), 0, st, g,
-                           h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST, h->p.minThFAST,
-                           h->d_slots.as<uint32_t>(), h->d_cellcnt.as<int>(), fault);
+        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)g.ncells_total, (unsigned)F), dim3(64), h->fast_lds, st,
+                           g, h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
+                           h->p.minThFAST, h->d_slots.as<uint32_t>(), h->d_cellcnt.as<int>(), fault, h->fl);
     }
     {
     StageMark m2(h, st, 2);
