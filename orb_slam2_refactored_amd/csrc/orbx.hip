@@ -133,43 +133,74 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
 // cv::resize INTER_LINEAR CV_8UC1 [ext]: horizontal 11-bit fixed point (exact int32), vertical
 // with the universal-intrinsics rounding ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2.
 // xtab[dx] = {sx0 | sx1 << 16, a0 | a1 << 16}; ytab[dy] = {sy0 | sy1 << 16, b0 | b1 << 16}.
+// One workgroup = a 64 x 16 tile of level l (256 threads, 4 output pixels each).  The source
+// rectangle of level l-1 it needs is staged in LDS with dword loads; coefficients come from the
+// per-level tables.
+constexpr int PYR_TW = 64, PYR_TH = 16;
+constexpr int PYR_SW = 128, PYR_SH = 48;   // LDS source tile capacity (scale factor <= ~1.9)
+
 __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const uint8_t* __restrict__ in,
                                                             long long in_fstride, int in_step, uint8_t* pyr,
                                                             const int2* __restrict__ xtab,
                                                             const int2* __restrict__ ytab) {
-    // block = 64 x 4 threads, each thread 4 consecutive output pixels of one row (dword store)
+    __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW];
+    __shared__ int2 xs_t[PYR_TW], ys_t[PYR_TH];
     const LevelDev& L = g.lv[l];
+    const LevelDev& Ls = g.lv[l - 1];
     const int f = blockIdx.z;
-    const int dx0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (dy >= L.h || dx0 >= L.w) return;
+    const int tx0 = blockIdx.x * PYR_TW, ty0 = blockIdx.y * PYR_TH;
+    const int tw = min(PYR_TW, L.w - tx0), th = min(PYR_TH, L.h - ty0);
     int sstep;
     const uint8_t* src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &sstep);
-    uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off + (long long)dy * L.stride;
     const int2* xt = xtab + L.xtab_off;
-    const int2 yv = ytab[L.ytab_off + dy];
-    const int sy0 = yv.x & 0xffff, sy1 = yv.x >> 16, b0 = yv.y & 0xffff, b1 = yv.y >> 16;
-    const uint8_t* r0 = src + (long long)sy0 * sstep;
-    const uint8_t* r1 = src + (long long)sy1 * sstep;
+    const int2* yt = ytab + L.ytab_off;
+    if ((int)threadIdx.x < tw) xs_t[threadIdx.x] = xt[tx0 + threadIdx.x];
+    if ((int)threadIdx.x < th) ys_t[threadIdx.x] = yt[ty0 + threadIdx.x];
+    // source rectangle: monotone tables -> first / last entries bound it
+    const int sx_lo = xt[tx0].x & 0xffff, sx_hi = xt[tx0 + tw - 1].x >> 16;
+    const int sy_lo = yt[ty0].x & 0xffff, sy_hi = yt[ty0 + th - 1].x >> 16;
+    const int xa = sx_lo & ~3;
+    const int nd = (sx_hi - xa + 4) >> 2;   // dwords per source row
+    const int nr = sy_hi - sy_lo + 1;
+    const int sw = Ls.w;
+    for (int i = threadIdx.x; i < nd * nr; i += blockDim.x) {
+        const int r = i / nd, d = i - r * nd;
+        const uint8_t* rowp = src + (long long)(sy_lo + r) * sstep;
+        const int x = xa + 4 * d;
+        uint32_t v;
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(rowp + x);
+        if (x + 3 < sw && (addr & 3) == 0) {
+            v = *reinterpret_cast<const uint32_t*>(rowp + x);
+        } else {
+            v = 0;
+            for (int q = 0; q < 4; q++)
+                if (x + q < sw) v |= (uint32_t)rowp[x + q] << (8 * q);
+        }
+        *reinterpret_cast<uint32_t*>(&S[r * PYR_SW + 4 * d]) = v;
+    }
+    __syncthreads();
+    const int ty = threadIdx.x >> 4, q0 = (threadIdx.x & 15) * 4;
+    if (ty >= th || q0 >= tw) return;
+    const int2 yv = ys_t[ty];
+    const int r0 = ((yv.x & 0xffff) - sy_lo) * PYR_SW - xa, r1 = ((yv.x >> 16) - sy_lo) * PYR_SW - xa;
+    const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
     uint32_t packed = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int dx = dx0 + k;
-        if (dx < L.w) {
-            const int2 xv = xt[dx];
+        if (q0 + k < tw) {
+            const int2 xv = xs_t[q0 + k];
             const int sx0 = xv.x & 0xffff, sx1 = xv.x >> 16, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
-            const int h0 = r0[sx0] * a0 + r0[sx1] * a1;
-            const int h1 = r1[sx0] * a0 + r1[sx1] * a1;
+            const int h0 = S[r0 + sx0] * a0 + S[r0 + sx1] * a1;
+            const int h1 = S[r1 + sx0] * a0 + S[r1 + sx1] * a1;
             const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
             const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
             packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
         }
     }
-    if (dx0 + 3 < L.w) {
-        *reinterpret_cast<uint32_t*>(dst + dx0) = packed;   // stride % 16 == 0, dx0 % 4 == 0
-    } else {
-        for (int k = 0; dx0 + k < L.w; k++) dst[dx0 + k] = (uint8_t)(packed >> (8 * k));
-    }
+    uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off + (long long)(ty0 + ty) * L.stride + tx0 + q0;
+    if (q0 + 3 < tw) *reinterpret_cast<uint32_t*>(dst) = packed;   // stride % 16 == 0, tx0+q0 % 4 == 0
+    else
+        for (int k = 0; q0 + k < tw; k++) dst[k] = (uint8_t)(packed >> (8 * k));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -179,8 +210,6 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
 // A pixel is a FAST-9 corner at threshold t iff M > t, and cornerScore<16> == M - 1 for every
 // detected corner (threshold-independent), so one M map serves both the iniThFAST pass and the
 // minThFAST retry of DetectFAST.
-constexpr int CS = 72;   // LDS crop row stride (bytes)
-constexpr int ZS = 64;   // LDS zone row stride
 
 __device__ __forceinline__ int corner_strength(const uint8_t* c, int cs) {   // c -> centre pixel in LDS
     const int v = c[0];
@@ -1248,6 +1277,13 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
                 ytab.push_back(make_int2(clip(sy) | (clip(sy + 1) << 16), (b0 & 0xffff) | (b1 << 16)));
             }
         }
+        if (l > 0) {   // the pyramid kernel's LDS source tile must hold a 64x16 output tile's footprint
+            const double sc = (double)prev_w / L.w, scy = (double)prev_h / L.h;
+            if (sc * (PYR_TW - 1) + 2 + 4 > PYR_SW || scy * (PYR_TH - 1) + 3 > PYR_SH) {
+                set_error("scaleFactor too large for the pyramid tile (max ~1.9)");
+                return ORB_EINVAL;
+            }
+        }
         if (L.w >= 4096 || L.h >= 4096) {
             set_error("image dimensions must be < 4096");
             return ORB_EINVAL;
@@ -1407,7 +1443,8 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
     {
     StageMark m0(h, st, 0);
     for (int l = 1; l < g.nlevels; l++) {
-        dim3 grid((unsigned)((g.lv[l].w + 255) / 256), (unsigned)((g.lv[l].h + 3) / 4), (unsigned)F);
+        dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
+                  (unsigned)F);
         hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
                            h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
     }
