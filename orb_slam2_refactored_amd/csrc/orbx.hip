@@ -29,7 +29,6 @@ namespace orbamd {
 
 constexpr int MAX_LEVELS = 16;
 constexpr int MAX_ZONE = 64;            // max FAST detection-zone side (cellw <= 59 always)
-constexpr int MAX_CROP = MAX_ZONE + 6;
 constexpr int MAX_ROOTS = 32;
 constexpr int PATCH = 43;               // raw neighbourhood: +-21 (rBRIEF reach 18 + blur 3)
 constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
@@ -322,38 +321,45 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     int step;
     const uint8_t* img = level_base(g, cell.level, f, in, in_fstride, in_step, pyr, &step);
 
-    // 1. crop
+    // 1. crop: LDS dword m of a crop row holds crop cols 4m-1 .. 4m+2 (col c at byte c+1), built from
+    //    two aligned global dwords with v_alignbyte; all loads of a lane are issued together.
     {
-        const int j = lane & 15, rr = lane >> 4;
-        constexpr int NR = (MAX_CROP + 3) / 4;
-        uint32_t w[NR][2];
-        int offr[NR];
+        const int m = lane & 15, rr = lane >> 4;
+        const int ndl = (cw + 1 + 3) >> 2;   // LDS dwords per crop row (<= 18)
+        constexpr int NB = 5;                // row iterations per batch (20 rows)
+        for (int rb = 0; rb < ch; rb += 4 * NB) {
+            uint32_t lo[NB][2], hi[NB][2];
+            int sh[NB];
 #pragma unroll
-        for (int it = 0; it < NR; it++) {
-            const int r = rr + 4 * it;
-            w[it][0] = w[it][1] = 0;
-            offr[it] = 0;
-            if (r < ch) {
-                const uintptr_t addr = reinterpret_cast<uintptr_t>(img + (long long)(y0 + r) * step + x0);
-                const int off = (int)(addr & 3);
-                const uint32_t* a0 = reinterpret_cast<const uint32_t*>(addr - off);
-                const int nd = (off + cw + 3) >> 2;
-                offr[it] = off;
-                if (j < nd) w[it][0] = a0[j];
-                if (j + 16 < nd) w[it][1] = a0[j + 16];
-            }
-        }
+            for (int it = 0; it < NB; it++) {
+                const int r = rb + rr + 4 * it;
+                sh[it] = 0;
 #pragma unroll
-        for (int it = 0; it < NR; it++) {
-            const int r = rr + 4 * it;
-            if (r >= ch) continue;
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int c = 4 * (j + 16 * h) + q - offr[it];
-                    if (c >= 0 && c < cw) crop[r * CSd + 1 + c] = (uint8_t)(w[it][h] >> (8 * q));
+                for (int h = 0; h < 2; h++) {
+                    lo[it][h] = hi[it][h] = 0;
+                    const int mm = m + 16 * h;
+                    if (r < ch && mm < ndl) {
+                        const uintptr_t addr = reinterpret_cast<uintptr_t>(img + (long long)(y0 + r) * step + x0);
+                        const int e = (int)(addr & 3) - 1;   // global byte of crop col -1, relative to addr & ~3
+                        const uint32_t* a0 = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+                        const int k = mm + (e < 0 ? -1 : 0);
+                        lo[it][h] = a0[k];
+                        hi[it][h] = a0[k + 1];
+                        sh[it] = e & 3;
+                    }
                 }
+            }
+#pragma unroll
+            for (int it = 0; it < NB; it++) {
+                const int r = rb + rr + 4 * it;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int mm = m + 16 * h;
+                    if (r < ch && mm < ndl)
+                        reinterpret_cast<uint32_t*>(crop + r * CSd)[mm] =
+                            __builtin_amdgcn_alignbyte(hi[it][h], lo[it][h], sh[it]);
+                }
+            }
         }
         for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
     }
@@ -370,7 +376,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     auto drain = [&](int n) {
         const int i = lane < n ? queue[lane] : -1;
         bool c = false;
-        if (i >= 0) c = is_corner_t(&crop[((i / ZSd) + 3) * CSd + 1 + (i % ZSd) + 3], tlo, CSd);
+        if (i >= 0) c = is_corner_t(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], tlo, CSd);
         const unsigned long long bm = __ballot(c);
         if (c) clist[nc + popc64(bm & lt)] = (short)i;
         nc += popc64(bm);
@@ -397,7 +403,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
         const int incl = wave_incl_scan(cnt);
         int pos = qn + incl - cnt;
         for (int k = 0; k < 4; k++)
-            if (mask & (1u << k)) queue[pos++] = (short)(y * ZSd + qx + k);
+            if (mask & (1u << k)) queue[pos++] = (short)((y << 8) | (qx + k));
         qn += __shfl(incl, 63, 64);
         wave_lds_sync();
         while (qn >= 64) {
@@ -420,7 +426,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     // corner strengths into the zone map
     for (int j = lane; j < nc; j += 64) {
         const int i = clist[j];
-        Mz[i] = (uint8_t)min(corner_strength(&crop[((i / ZSd) + 3) * CSd + 1 + (i % ZSd) + 3], CSd), 255);
+        Mz[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(corner_strength(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd), 255);
     }
     wave_lds_sync();
 
@@ -444,7 +450,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
         bool ki = false, km = false;
         if (j < nc) {
             const int i = clist[j];
-            const int zy = i / ZSd, zx = i % ZSd, m = Mz[i];
+            const int zy = i >> 8, zx = i & 255, m = Mz[zy * ZSd + zx];
             ki = nms(zy, zx, m, th_ini);
             km = nms(zy, zx, m, th_min);
         }
@@ -466,8 +472,9 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
             const int r = running + popc64(bm & lt);
             const int i = clist[jb + lane];
             if (r < cap) {
-                const uint32_t x = (uint32_t)(x0 + 3 + i % ZSd), yy = (uint32_t)(y0 + 3 + i / ZSd);
-                out[r] = x | (yy << 12) | ((uint32_t)(Mz[i] - 1) << 24);
+                const int zy = i >> 8, zx = i & 255;
+                const uint32_t x = (uint32_t)(x0 + 3 + zx), yy = (uint32_t)(y0 + 3 + zy);
+                out[r] = x | (yy << 12) | ((uint32_t)(Mz[zy * ZSd + zx] - 1) << 24);
             }
         }
         running += popc64(bm);
@@ -1370,6 +1377,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         for (const CellDev& c : cells) { mzw = std::max(mzw, c.zwzh & 0xffff); mzh = std::max(mzh, c.zwzh >> 16); }
         FastLds fl;
         fl.CS = (int)align_up(mzw + 6 + 8, 4);         // +1 shift, +4 dword over-read each side
+        if (fl.CS < 4 * ((mzw + 6 + 1 + 3) / 4)) fl.CS = 4 * ((mzw + 6 + 1 + 3) / 4);
         fl.ZS = (int)align_up(mzw, 4);
         fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * mzh, 16);
