@@ -118,7 +118,7 @@ def main():
     kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
     desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
     counts = torch.empty((B,), dtype=torch.int32, device=dev)
-    prev_idx = torch.tensor([(i - 1) % B for i in range(B)], device=dev)
+    prev_idx = torch.tensor([(i - 1) % B for i in range(B)], dtype=torch.int32, device=dev)
     match_out = torch.empty((4, B, cap), dtype=torch.int32, device=dev)
     if world > 1:
         g_kps = torch.empty((world * B, cap, 7), dtype=torch.int32, device=dev)
@@ -128,9 +128,7 @@ def main():
 
     def step():
         ex.extract_batch_device(frames, kps, desc, counts, stream=stream)
-        descB = desc.index_select(0, prev_idx)
-        nB = counts.index_select(0, prev_idx)
-        m.match_batch_device(desc, counts, descB, nB, out=match_out, stream=stream)
+        m.match_batch_device(desc, counts, desc, counts, out=match_out, stream=stream, pair_b=prev_idx)
         if world > 1:
             dist.all_gather_into_tensor(g_counts, counts)
             dist.all_gather_into_tensor(g_kps, kps)

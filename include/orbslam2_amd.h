@@ -107,13 +107,15 @@ int orbm_hamming_top2_device(const uint8_t* d_A, int nA, const uint8_t* d_B, int
                              int32_t* d_best_idx, int32_t* d_best, int32_t* d_second, void* stream);
 
 /* Batched pairs: pair p matches A_p (rows d_A + p*strideA*32, count d_nA[p]) against
- * B_p (d_B + p*strideB*32, count d_nB[p]).  Outputs at p*strideA.  Also applies the
- * acceptance test of :500 when d_match != NULL: match = best_idx if best <= th_low and
- * (float)best < nnratio * (float)second, else -1. */
+ * B_q (d_B + q*strideB*32, count d_nB[q]) with q = d_pair_b ? d_pair_b[p] : p (so a batch of
+ * frames can be matched against its own predecessors without a copy).  Outputs at p*strideA.
+ * Also applies the acceptance test of :500 when d_match != NULL: match = best_idx if
+ * best <= th_low and (float)best < nnratio * (float)second, else -1. */
 int orbm_bf_match_batch_device(const uint8_t* d_A, const int32_t* d_nA, int strideA,
-                               const uint8_t* d_B, const int32_t* d_nB, int strideB, int n_pairs,
-                               float nnratio, int th_low, int32_t* d_best_idx, int32_t* d_best,
-                               int32_t* d_second, int32_t* d_match, void* stream);
+                               const uint8_t* d_B, const int32_t* d_nB, int strideB,
+                               const int32_t* d_pair_b, int n_pairs, float nnratio, int th_low,
+                               int32_t* d_best_idx, int32_t* d_best, int32_t* d_second,
+                               int32_t* d_match, void* stream);
 
 /* Host-memory convenience form of the two above (synchronous). */
 int orbm_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float nnratio, int th_low,

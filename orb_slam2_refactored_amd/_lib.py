@@ -58,7 +58,7 @@ SIGNATURES = {
                                       C.POINTER(C.c_int), C.POINTER(SZ)]),
     "orbm_descriptor_distance": (C.c_int, [VP, VP]),
     "orbm_hamming_top2_device": (C.c_int, [VP, C.c_int, VP, C.c_int, VP, VP, VP, VP]),
-    "orbm_bf_match_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, C.c_int, C.c_int, C.c_float, C.c_int,
+    "orbm_bf_match_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, C.c_int, VP, C.c_int, C.c_float, C.c_int,
                                              VP, VP, VP, VP, VP]),
     "orbm_bf_match": (C.c_int, [VP, C.c_int, VP, C.c_int, C.c_float, C.c_int, VP, VP, VP, VP]),
     "orbm_search_for_triangulation": (C.c_int, [C.POINTER(TriFrame), C.POINTER(TriFrame), VP, VP, VP, VP,

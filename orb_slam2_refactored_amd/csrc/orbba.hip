@@ -1,18 +1,18 @@
 // orbba.hip — Optimizer::LocalBundleAdjustment on gfx950.
 //
-// g2o's Levenberg-Marquardt over SE3Expmap poses and marginalised XYZ points, fp64 throughout:
+// g2o's Levenberg-Marquardt over SE3Expmap poses and marginalised XYZ points, fp64 throughout.
+// Points own their edges (CSR); a point is served by a group of 8 lanes (one edge per lane,
+// fixed-order shuffle reductions), so per-point work spreads over ~N/8 wavefronts.
 //   per LM iteration (OptimizationAlgorithmLevenberg::solve, levenberg.cpp:61-164)
-//     ba_error_kernel        computeActiveErrors + robust chi2 per edge   (one lane per edge)
-//     ba_linearize_kernel    linearizeOplus + constructQuadraticForm       (one lane per edge)
-//     ba_point_accum_kernel  Hll / b_l per point, edges in g2o order      (one lane per point)
-//     ba_pose_accum_kernel   Hpp / b_p per pose, fixed-order tree sums    (one workgroup per pose)
+//     ba_iter_kernel         computeActiveErrors + robust chi2 + linearizeOplus +
+//                            constructQuadraticForm; Hll / b_l per point, per-edge pose parts
+//     ba_pose_accum_kernel   Hpp / b_p per free pose (fixed-order sums); extra block: chi2 total
 //   per trial (do { ... } while (rho < 0 ...))
-//     ba_schur_point_kernel  D^-1 = (Hll+lI)^-1, W = Hpl D^-1, Hpl D^-1 b_l (lane per point)
-//     ba_schur_block_kernel  S(i1,i2) = Hpp+lI - sum W Hpl^T over shared points (WG per block)
-//     ba_schur_rhs_kernel    b_schur = b_p - sum Hpl D^-1 b_l              (WG per pose)
-//     ba_ldlt_kernel         dense LDL^T solve of the (6P)^2 reduced camera system in LDS
-//     ba_update_kernel       back-substitution, push, SE3 exp-update / point += (lane per vertex)
-//     ba_error_kernel        + deterministic reduction -> new chi2
+//     ba_schur_point_kernel  D^-1 = (Hll + lambda I)^-1, W = Hpl D^-1, Hpl D^-1 b_l
+//     ba_schur_block_kernel  S(i1,i2) = Hpp + lambda I - sum W Hpl^T; b_schur on diagonal blocks
+//     ba_solve_kernel        blocked LDL^T of the (6P)^2 reduced camera system in LDS, triangular
+//                            solves, push + SE3 exp-update of the free poses
+//     ba_point_update_kernel back-substitution, push, point +=, errors + robust chi2 of its edges
 //     ba_decide_kernel       rho, lambda / nu update, accept or pop (restore)
 // Every reduction runs in a fixed order, so results are bit-reproducible run to run.  The LM
 // control scalars live on the device; the host reads one small status block per trial to decide
@@ -190,13 +190,8 @@ __device__ __forceinline__ void robustify(const BADev& b, int e, double chi, dou
 }
 
 // EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::computeError (types_six_dof_expmap.h:90-95,122-127)
-__global__ void ba_error_kernel(BADev b) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= b.Ea) return;
-    const int e = b.act[k];
-    const int pi = b.ek[e];
-    double Xc[3];
-    se3_map(b.q + 4 * pi, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
+// for edge e with camera-frame point Xc; stores g2o's _error and returns the robust chi2 term.
+__device__ __forceinline__ double edge_error(const BADev& b, int e, const double* Xc) {
     const double* c = b.cam + 5 * e;
     const double* z = b.obs + 3 * e;
     if (!b.stereo[e]) {
@@ -214,12 +209,119 @@ __global__ void ba_error_kernel(BADev b) {
     }
     double r0, r1;
     robustify(b, e, edge_chi2(b, e), r0, r1);
-    b.rchi[k] = r0;
+    return r0;
+}
+
+// fixed-order sum over the 8-lane group of a point
+__device__ __forceinline__ double grp_sum(double v) {
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    return v;
+}
+
+constexpr int GRP = 8;   // lanes per point
+
+// Per LM iteration: errors + robust chi2 (computeActiveErrors / activeRobustChi2), linearizeOplus
+// and constructQuadraticForm of every active edge (types_six_dof_expmap.cpp:103-139,188-234;
+// base_binary_edge.hpp:54-120), Hll / b_l summed per point, pose parts stored per edge.
+__global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = t / GRP, sub = t % GRP;
+    const bool live = l < b.nl;
+    double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, chi = 0;
+    if (live) {
+        for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
+            const int k = b.pt_slot[u];
+            const int e = b.act[k];
+            const int pi = b.ek[e];
+            const double* q4 = b.q + 4 * pi;
+            double Xc[3], R[9];
+            se3_map(q4, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
+            chi += edge_error(b, e, Xc);
+            q_to_R(q4, R);
+            const double x = Xc[0], y = Xc[1], z = Xc[2], z2 = z * z;
+            const double* c = b.cam + 5 * e;
+            const double fx = c[0], fy = c[1], bf = c[4];
+            const bool st = b.stereo[e];
+            const int d = st ? 3 : 2;
+            double A[3][3], Bm[3][6];
+            for (int r = 0; r < 3; r++) {
+                for (int j = 0; j < 3; j++) A[r][j] = 0;
+                for (int j = 0; j < 6; j++) Bm[r][j] = 0;
+            }
+            if (!st) {
+                const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+                for (int r = 0; r < 2; r++)
+                    for (int j = 0; j < 3; j++) {
+                        double s = 0;
+                        for (int m = 0; m < 3; m++) s += tmp[r][m] * R[3 * m + j];
+                        A[r][j] = -1. / z * s;
+                    }
+            } else {
+                for (int j = 0; j < 3; j++) {
+                    A[0][j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
+                    A[1][j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
+                    A[2][j] = A[0][j] - bf * R[6 + j] / z2;
+                }
+            }
+            Bm[0][0] = x * y / z2 * fx; Bm[0][1] = -(1 + (x * x / z2)) * fx; Bm[0][2] = y / z * fx;
+            Bm[0][3] = -1. / z * fx;    Bm[0][4] = 0;                        Bm[0][5] = x / z2 * fx;
+            Bm[1][0] = (1 + y * y / z2) * fy; Bm[1][1] = -x * y / z2 * fy; Bm[1][2] = -x / z * fy;
+            Bm[1][3] = 0;                     Bm[1][4] = -1. / z * fy;     Bm[1][5] = y / z2 * fy;
+            if (st) {
+                Bm[2][0] = Bm[0][0] - bf * y / z2; Bm[2][1] = Bm[0][1] + bf * x / z2; Bm[2][2] = Bm[0][2];
+                Bm[2][3] = Bm[0][3];               Bm[2][4] = 0;                      Bm[2][5] = Bm[0][5] - bf / z2;
+            }
+            double r0, r1;
+            robustify(b, e, edge_chi2(b, e), r0, r1);
+            const double w = r1 * b.info[e];
+            double om_r[3] = {0, 0, 0};
+            for (int r = 0; r < d; r++) om_r[r] = -b.info[e] * b.err[3 * e + r] * r1;
+            for (int i = 0; i < 3; i++) {
+                double s = 0;
+                for (int r = 0; r < d; r++) s += A[r][i] * om_r[r];
+                g[i] += s;
+                for (int j = 0; j < 3; j++) {
+                    double h = 0;
+                    for (int r = 0; r < d; r++) h += A[r][i] * w * A[r][j];
+                    H[3 * i + j] += h;
+                }
+            }
+            if (b.hp[pi] >= 0) {
+                double* J = b.J + (long long)k * 72;
+                for (int i = 0; i < 6; i++) {
+                    double s = 0;
+                    for (int r = 0; r < d; r++) s += Bm[r][i] * om_r[r];
+                    J[48 + i] = s;
+                    for (int j = 0; j < 6; j++) {
+                        double h = 0;
+                        for (int r = 0; r < d; r++) h += Bm[r][i] * w * Bm[r][j];
+                        J[12 + 6 * i + j] = h;
+                    }
+                    for (int j = 0; j < 3; j++) {
+                        double h = 0;
+                        for (int r = 0; r < d; r++) h += Bm[r][i] * w * A[r][j];
+                        J[54 + 3 * i + j] = h;
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) H[i] = grp_sum(H[i]);
+#pragma unroll
+    for (int i = 0; i < 3; i++) g[i] = grp_sum(g[i]);
+    chi = grp_sum(chi);
+    if (live && sub == 0) {
+        for (int i = 0; i < 9; i++) b.Hll[9 * l + i] = H[i];
+        for (int i = 0; i < 3; i++) b.bl[3 * l + i] = g[i];
+        b.rchi[l] = chi;
+    }
 }
 
 // Deterministic single-workgroup sum (fixed strided order + fixed tree).
-__global__ __launch_bounds__(1024) void ba_sum_kernel(const double* v, int n, double* out) {
-    __shared__ double sh[1024];
+__device__ double block_sum_1024(const double* v, int n, double* sh) {
     double s = 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) s += v[i];
     sh[threadIdx.x] = s;
@@ -228,116 +330,43 @@ __global__ __launch_bounds__(1024) void ba_sum_kernel(const double* v, int n, do
         if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = sh[0];
+    const double r = sh[0];
+    __syncthreads();
+    return r;
 }
 
-// linearizeOplus + constructQuadraticForm per active edge (types_six_dof_expmap.cpp:103-139,
-// 188-234; base_binary_edge.hpp:54-120)
-__global__ void ba_linearize_kernel(BADev b) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= b.Ea) return;
-    const int e = b.act[k];
-    const int pi = b.ek[e];
-    const double* q4 = b.q + 4 * pi;
-    double Xc[3], R[9];
-    se3_map(q4, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
-    q_to_R(q4, R);
-    const double x = Xc[0], y = Xc[1], z = Xc[2], z2 = z * z;
-    const double* c = b.cam + 5 * e;
-    const double fx = c[0], fy = c[1], bf = c[4];
-    const bool st = b.stereo[e];
-    const int d = st ? 3 : 2;
-    double A[3][3], B[3][6];
-    for (int r = 0; r < 3; r++) {
-        for (int j = 0; j < 3; j++) A[r][j] = 0;
-        for (int j = 0; j < 6; j++) B[r][j] = 0;
-    }
-    if (!st) {
-        const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
-        for (int r = 0; r < 2; r++)
-            for (int j = 0; j < 3; j++) {
-                double s = 0;
-                for (int m = 0; m < 3; m++) s += tmp[r][m] * R[3 * m + j];
-                A[r][j] = -1. / z * s;
-            }
-    } else {
-        for (int j = 0; j < 3; j++) {
-            A[0][j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
-            A[1][j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
-            A[2][j] = A[0][j] - bf * R[6 + j] / z2;
-        }
-    }
-    B[0][0] = x * y / z2 * fx; B[0][1] = -(1 + (x * x / z2)) * fx; B[0][2] = y / z * fx;
-    B[0][3] = -1. / z * fx;    B[0][4] = 0;                        B[0][5] = x / z2 * fx;
-    B[1][0] = (1 + y * y / z2) * fy; B[1][1] = -x * y / z2 * fy; B[1][2] = -x / z * fy;
-    B[1][3] = 0;                     B[1][4] = -1. / z * fy;     B[1][5] = y / z2 * fy;
-    if (st) {
-        B[2][0] = B[0][0] - bf * y / z2; B[2][1] = B[0][1] + bf * x / z2; B[2][2] = B[0][2];
-        B[2][3] = B[0][3];               B[2][4] = 0;                     B[2][5] = B[0][5] - bf / z2;
-    }
-    double r0, r1;
-    robustify(b, e, edge_chi2(b, e), r0, r1);
-    const double w = r1 * b.info[e];
-    double om_r[3] = {0, 0, 0};
-    for (int r = 0; r < d; r++) om_r[r] = -b.info[e] * b.err[3 * e + r] * r1;
-    double* J = b.J + (long long)k * 72;
-    for (int i = 0; i < 3; i++) {
-        double s = 0;
-        for (int r = 0; r < d; r++) s += A[r][i] * om_r[r];
-        J[9 + i] = s;
-        for (int j = 0; j < 3; j++) {
-            double h = 0;
-            for (int r = 0; r < d; r++) h += A[r][i] * w * A[r][j];
-            J[3 * i + j] = h;
-        }
-    }
-    if (b.hp[pi] >= 0) {
-        for (int i = 0; i < 6; i++) {
-            double s = 0;
-            for (int r = 0; r < d; r++) s += B[r][i] * om_r[r];
-            J[48 + i] = s;
-            for (int j = 0; j < 6; j++) {
-                double h = 0;
-                for (int r = 0; r < d; r++) h += B[r][i] * w * B[r][j];
-                J[12 + 6 * i + j] = h;
-            }
-            for (int j = 0; j < 3; j++) {
-                double h = 0;
-                for (int r = 0; r < d; r++) h += B[r][i] * w * A[r][j];
-                J[54 + 3 * i + j] = h;
-            }
-        }
-    }
-}
-
-__global__ void ba_point_accum_kernel(BADev b) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= b.nl) return;
-    double H[9] = {0}, g[3] = {0};
-    for (int u = b.pt_beg[l]; u < b.pt_beg[l + 1]; u++) {
-        const double* J = b.J + (long long)b.pt_slot[u] * 72;
-        for (int i = 0; i < 9; i++) H[i] += J[i];
-        for (int i = 0; i < 3; i++) g[i] += J[9 + i];
-    }
-    for (int i = 0; i < 9; i++) b.Hll[9 * l + i] = H[i];
-    for (int i = 0; i < 3; i++) b.bl[3 * l + i] = g[i];
-}
-
-// One workgroup (256 threads) per free pose: 42 sums (Hpp 36 + b 6) in a fixed order.
-__global__ __launch_bounds__(256) void ba_pose_accum_kernel(BADev b) {
-    __shared__ double sh[6][42];
+// One workgroup (1008 threads) per free pose: 42 sums (Hpp 36 + b 6), 24 partial groups with
+// four interleaved accumulators each, combined in a fixed order.  Block np: chi2 total.
+constexpr int PA_G = 24;
+__global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b, int set_ini) {
+    __shared__ double sh[1024];
     const int i = blockIdx.x;
-    const int g = threadIdx.x / 42, c = threadIdx.x % 42;   // 6 groups x 42 entries (252 threads)
+    if (i == b.np) {
+        const double c = block_sum_1024(b.rchi, b.nl, sh);
+        if (threadIdx.x == 0) {
+            b.ctl->cur = c;
+            if (set_ini) b.ctl->ini = c;
+        }
+        return;
+    }
+    const int g = threadIdx.x / 42, c = threadIdx.x % 42;
     const int beg = b.ps_beg[i], end = b.ps_beg[i + 1];
-    if (g < 6) {
-        double s = 0;
-        for (int u = beg + g; u < end; u += 6) s += b.J[(long long)b.ps_slot[u] * 72 + 12 + c];
-        sh[g][c] = s;
+    if (g < PA_G) {
+        double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        int u = beg + g;
+        for (; u + 3 * PA_G < end; u += 4 * PA_G) {
+            s0 += b.J[(long long)b.ps_slot[u] * 72 + 12 + c];
+            s1 += b.J[(long long)b.ps_slot[u + PA_G] * 72 + 12 + c];
+            s2 += b.J[(long long)b.ps_slot[u + 2 * PA_G] * 72 + 12 + c];
+            s3 += b.J[(long long)b.ps_slot[u + 3 * PA_G] * 72 + 12 + c];
+        }
+        for (; u < end; u += PA_G) s0 += b.J[(long long)b.ps_slot[u] * 72 + 12 + c];
+        sh[g * 42 + c] = (s0 + s1) + (s2 + s3);
     }
     __syncthreads();
     if (threadIdx.x < 42) {
         double s = 0;
-        for (int q = 0; q < 6; q++) s += sh[q][threadIdx.x];
+        for (int q = 0; q < PA_G; q++) s += sh[q * 42 + threadIdx.x];
         if (threadIdx.x < 36) b.Hpp[36 * i + threadIdx.x] = s;
         else b.bp[6 * i + threadIdx.x - 36] = s;
     }
@@ -373,19 +402,22 @@ __device__ __forceinline__ bool inv3(const double* m, double* o) {
     return true;
 }
 
-// BlockSolver::solve, landmark part (block_solver.hpp:377-419)
-__global__ void ba_schur_point_kernel(BADev b) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+// BlockSolver::solve, landmark part (block_solver.hpp:377-419): every lane of a point's group
+// forms D^-1 (same values), each lane handles its edges' W = Hpl D^-1 and Hpl D^-1 b_l.
+__global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = t / GRP, sub = t % GRP;
     if (l >= b.nl) return;
     const double lam = b.ctl->lambda;
     double D[9], Di[9];
     for (int i = 0; i < 9; i++) D[i] = b.Hll[9 * l + i];
     D[0] += lam; D[4] += lam; D[8] += lam;
     inv3(D, Di);
-    for (int i = 0; i < 9; i++) b.Dinv[9 * l + i] = Di[i];
+    if (sub == 0)
+        for (int i = 0; i < 9; i++) b.Dinv[9 * l + i] = Di[i];
     double db[3];
     for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * b.bl[3 * l] + Di[3 * i + 1] * b.bl[3 * l + 1] + Di[3 * i + 2] * b.bl[3 * l + 2];
-    for (int u = b.pt_beg[l]; u < b.pt_beg[l + 1]; u++) {
+    for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
         const int k = b.pt_slot[u];
         if (b.hp[b.ek[b.act[k]]] < 0) continue;
         const double* Hpl = b.J + (long long)k * 72 + 54;
@@ -398,27 +430,40 @@ __global__ void ba_schur_point_kernel(BADev b) {
     }
 }
 
-// Reduced camera system block (i1, i2): 36 entries x 7 partial groups, fixed-order combine.
-__global__ __launch_bounds__(256) void ba_schur_block_kernel(BADev b, int D) {
-    __shared__ double sh[7][36];
+// Reduced camera system block (i1, i2): 36 entries x 28 partial groups (two accumulators each),
+// fixed-order combine.  Diagonal blocks also form b_schur = b_p - sum Hpl D^-1 b_l.
+constexpr int SB_G = 28;
+__global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D) {
+    __shared__ double sh[1024];
     const int blk = blockIdx.x;
     const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
     const int g = threadIdx.x / 36, c = threadIdx.x % 36;
     const int r = c / 6, cc = c % 6;
-    if (g < 7) {
-        double s = 0;
-        for (int u = b.blk_beg[blk] + g; u < b.blk_beg[blk + 1]; u += 7) {
-            const int2 pr = b.blk_pair[u];
-            const double* W = b.W + (long long)pr.x * 24 + 3 * r;
-            const double* H = b.J + (long long)pr.y * 72 + 54 + 3 * cc;
-            s += W[0] * H[0] + W[1] * H[1] + W[2] * H[2];
+    if (g < SB_G) {
+        double s0 = 0, s1 = 0;
+        const int end = b.blk_beg[blk + 1];
+        int u = b.blk_beg[blk] + g;
+        for (; u + SB_G < end; u += 2 * SB_G) {
+            const int2 p0 = b.blk_pair[u], p1 = b.blk_pair[u + SB_G];
+            const double* W0 = b.W + (long long)p0.x * 24 + 3 * r;
+            const double* H0 = b.J + (long long)p0.y * 72 + 54 + 3 * cc;
+            const double* W1 = b.W + (long long)p1.x * 24 + 3 * r;
+            const double* H1 = b.J + (long long)p1.y * 72 + 54 + 3 * cc;
+            s0 += W0[0] * H0[0] + W0[1] * H0[1] + W0[2] * H0[2];
+            s1 += W1[0] * H1[0] + W1[1] * H1[1] + W1[2] * H1[2];
         }
-        sh[g][c] = s;
+        if (u < end) {
+            const int2 p0 = b.blk_pair[u];
+            const double* W0 = b.W + (long long)p0.x * 24 + 3 * r;
+            const double* H0 = b.J + (long long)p0.y * 72 + 54 + 3 * cc;
+            s0 += W0[0] * H0[0] + W0[1] * H0[1] + W0[2] * H0[2];
+        }
+        sh[g * 36 + c] = s0 + s1;
     }
     __syncthreads();
     if (threadIdx.x < 36) {
         double s = 0;
-        for (int q = 0; q < 7; q++) s += sh[q][threadIdx.x];
+        for (int q = 0; q < SB_G; q++) s += sh[q * 36 + threadIdx.x];
         double v = -s;
         if (i1 == i2) {
             v += b.Hpp[36 * i1 + threadIdx.x];
@@ -427,108 +472,152 @@ __global__ __launch_bounds__(256) void ba_schur_block_kernel(BADev b, int D) {
         b.S[(long long)(6 * i1 + r) * D + 6 * i2 + cc] = v;
         if (i1 != i2) b.S[(long long)(6 * i2 + cc) * D + 6 * i1 + r] = v;
     }
-}
-
-// b_schur = b_p - sum over the pose's edges of Hpl D^-1 b_l: 6 entries x 42 partial groups.
-__global__ __launch_bounds__(256) void ba_schur_rhs_kernel(BADev b) {
-    __shared__ double sh[42][6];
-    const int i = blockIdx.x;
-    const int g = threadIdx.x / 6, c = threadIdx.x % 6;
-    if (g < 42) {
-        double s = 0;
-        for (int u = b.ps_beg[i] + g; u < b.ps_beg[i + 1]; u += 42) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + c];
-        sh[g][c] = s;
-    }
+    if (i1 != i2) return;
+    __syncthreads();
+    // b_schur for pose i1: 6 entries x 168 partial groups
+    const int g2 = threadIdx.x / 6, c2 = threadIdx.x % 6;
+    double s = 0;
+    if (g2 < 168)
+        for (int u = b.ps_beg[i1] + g2; u < b.ps_beg[i1 + 1]; u += 168) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + c2];
+    sh[threadIdx.x] = g2 < 168 ? s : 0.0;
     __syncthreads();
     if (threadIdx.x < 6) {
-        double s = 0;
-        for (int q = 0; q < 42; q++) s += sh[q][threadIdx.x];
-        b.bs[6 * i + threadIdx.x] = b.bp[6 * i + threadIdx.x] - s;
+        double tot = 0;
+        for (int q = 0; q < 168; q++) tot += sh[q * 6 + threadIdx.x];
+        b.bs[6 * i1 + threadIdx.x] = b.bp[6 * i1 + threadIdx.x] - tot;
     }
 }
 
-// Dense LDL^T solve of S x = bs with S in LDS (right-looking, one workgroup of 32x32 threads;
-// stands in for g2o's SimplicialLDLT, linear_solver_eigen.h:94-124).
-__global__ __launch_bounds__(1024) void ba_ldlt_kernel(BADev b, int D) {
+__device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Reduced camera system solve + pose update.  Blocked LDL^T by 6x6 pose blocks in LDS
+// (right-looking: diagonal block in registers, panel, trailing lower-triangle update; three
+// barriers per block column), triangular solves on wavefront 0 with the right-hand side in
+// registers, then push() + SE3Quat::exp(dx) * pose for every free pose (+ its scale term).
+// Stands in for g2o's SimplicialLDLT (linear_solver_eigen.h:94-124): same factorisation up to
+// rounding order.  D <= 132 (22 free keyframes).
+__global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     extern __shared__ __attribute__((aligned(16))) double A[];
-    double* v = A + (size_t)D * D;
+    __shared__ double dblk[6];
     __shared__ int s_ok;
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-    for (int i = threadIdx.x; i < D * D; i += blockDim.x) A[i] = b.S[i];
-    for (int i = threadIdx.x; i < D; i += blockDim.x) v[i] = b.bs[i];
+    const int NB = D / 6;
+    {
+        const double2* S2 = reinterpret_cast<const double2*>(b.S);
+        double2* A2 = reinterpret_cast<double2*>(A);
+        const int n2 = (D * D) / 2;   // D is even
+        for (int i0 = threadIdx.x; i0 < n2; i0 += 4 * blockDim.x) {
+            double2 r[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) r[q] = i0 + q * (int)blockDim.x < n2 ? S2[i0 + q * blockDim.x] : make_double2(0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (i0 + q * (int)blockDim.x < n2) A2[i0 + q * blockDim.x] = r[q];
+        }
+    }
     if (threadIdx.x == 0) s_ok = 1;
     __syncthreads();
-    for (int j = 0; j < D; j++) {
-        const double dj = A[j * D + j];
-        if (!(dj != 0 && isfinite(dj))) {
-            if (threadIdx.x == 0) s_ok = 0;
-            break;   // uniform: every thread read the same dj
-        }
-        // trailing update of the lower triangle, using column j before it is scaled:
-        // A(i,k) -= A(i,j) * A(k,j) / dj  for j < k <= i
-        const double inv = 1.0 / dj;
-        for (int i = j + 1 + ty; i < D; i += 32) {
-            const double aij = A[i * D + j] * inv;
-            for (int k = j + 1 + tx; k <= i; k += 32) A[i * D + k] -= aij * A[k * D + j];
+    for (int J = 0; J < NB; J++) {
+        const int j0 = 6 * J;
+        if (threadIdx.x == 0) {   // (1) diagonal block, in registers
+            double a[6][6];
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int k = 0; k < 6; k++) a[i][k] = k <= i ? A[(j0 + i) * D + j0 + k] : 0.0;
+            double d[6];
+            int ok = 1;
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                double dj = a[j][j];
+#pragma unroll
+                for (int k = 0; k < j; k++) dj -= a[j][k] * a[j][k] * d[k];
+                ok &= (dj != 0 && isfinite(dj)) ? 1 : 0;
+                d[j] = dj;
+#pragma unroll
+                for (int i = j + 1; i < 6; i++) {
+                    double sum = a[i][j];
+#pragma unroll
+                    for (int k = 0; k < j; k++) sum -= a[i][k] * a[j][k] * d[k];
+                    a[i][j] = sum / dj;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+#pragma unroll
+                for (int k = 0; k < i; k++) A[(j0 + i) * D + j0 + k] = a[i][k];
+                A[(j0 + i) * D + j0 + i] = d[i];
+                dblk[i] = d[i];
+            }
+            if (!ok) s_ok = 0;
         }
         __syncthreads();
-        for (int i = j + 1 + threadIdx.x; i < D; i += blockDim.x) A[i * D + j] *= inv;   // L(i,j)
-        __syncthreads();
-    }
-    __syncthreads();
-    const int ok = s_ok;
-    if (ok) {
-        // L y = b (column sweep), y /= d, L^T x = y
-        for (int j = 0; j < D; j++) {
-            const double yj = v[j];
-            for (int i = j + 1 + threadIdx.x; i < D; i += blockDim.x) v[i] -= A[i * D + j] * yj;
-            __syncthreads();
+        if (!s_ok) break;
+        // (2) panel: rows below solve  L_IJ D_J L_JJ^T = A_IJ  (one row per thread)
+        for (int i = j0 + 6 + threadIdx.x; i < D; i += blockDim.x) {
+            double x[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                double sum = A[i * D + j0 + j];
+#pragma unroll
+                for (int k = 0; k < j; k++) sum -= x[k] * dblk[k] * A[(j0 + j) * D + j0 + k];
+                x[j] = sum / dblk[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 6; j++) A[i * D + j0 + j] = x[j];
         }
-        for (int i = threadIdx.x; i < D; i += blockDim.x) v[i] /= A[i * D + i];
         __syncthreads();
-        for (int j = D - 1; j >= 0; j--) {
-            const double xj = v[j];
-            for (int i = threadIdx.x; i < j; i += blockDim.x) v[i] -= A[j * D + i] * xj;
-            __syncthreads();
-        }
-        for (int i = threadIdx.x; i < D; i += blockDim.x) b.x[i] = v[i];
-    } else {
-        for (int i = threadIdx.x; i < D; i += blockDim.x) b.x[i] = 0;
-    }
-    if (threadIdx.x == 0) b.ctl->ok2 = ok;
-}
-
-// Back-substitution xl = Dinv (bl - Hpl^T xp), push(), oplus; scale partials x.(lambda x + b).
-__global__ void ba_update_kernel(BADev b, int D) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const double lam = b.ctl->lambda;
-    if (t < b.nl) {
-        const int l = t;
-        double cl[3] = {b.bl[3 * l], b.bl[3 * l + 1], b.bl[3 * l + 2]};
-        for (int u = b.pt_beg[l]; u < b.pt_beg[l + 1]; u++) {
-            const int k = b.pt_slot[u];
-            const int ip = b.hp[b.ek[b.act[k]]];
-            if (ip < 0) continue;
-            const double* Hpl = b.J + (long long)k * 72 + 54;
-            for (int c = 0; c < 3; c++) {
-                double s = 0;
-                for (int r = 0; r < 6; r++) s += Hpl[3 * r + c] * b.x[6 * ip + r];
-                cl[c] -= s;
+        // (3) trailing update of the lower triangle: A_ik -= sum_j (L_ij d_j) L_kj, j in block J
+        {
+            const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+            for (int i = j0 + 6 + ty; i < D; i += 16) {
+                double li[6];
+#pragma unroll
+                for (int j = 0; j < 6; j++) li[j] = A[i * D + j0 + j] * dblk[j];
+                for (int k = j0 + 6 + tx; k <= i; k += 16) {
+                    const double* lk = A + k * D + j0;
+                    A[i * D + k] -= li[0] * lk[0] + li[1] * lk[1] + li[2] * lk[2] + li[3] * lk[3] + li[4] * lk[4] +
+                                    li[5] * lk[5];
+                }
             }
         }
-        const double* Di = b.Dinv + 9 * l;
-        const int id = b.pt_id[l];
-        double part = 0;
-        for (int i = 0; i < 3; i++) {
-            const double xi = Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1] + Di[3 * i + 2] * cl[2];
-            b.x[D + 3 * l + i] = xi;
-            b.X_sv[3 * id + i] = b.X[3 * id + i];
-            b.X[3 * id + i] += xi;
-            part += xi * (lam * xi + b.bl[3 * l + i]);
+        __syncthreads();
+    }
+    const int ok = s_ok;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        // right-hand side in registers: lane holds rows lane and lane + 64
+        double v0 = lane < D ? b.bs[lane] : 0.0, v1 = lane + 64 < D ? b.bs[lane + 64] : 0.0;
+        if (ok) {
+            for (int j = 0; j < D; j++) {   // L y = b
+                const double yj = j < 64 ? readlane_d(v0, j) : readlane_d(v1, j - 64);
+                if (lane > j && lane < D) v0 -= A[lane * D + j] * yj;
+                if (lane + 64 > j && lane + 64 < D) v1 -= A[(lane + 64) * D + j] * yj;
+            }
+            if (lane < D) v0 /= A[lane * D + lane];
+            if (lane + 64 < D) v1 /= A[(lane + 64) * D + lane + 64];
+            for (int j = D - 1; j >= 0; j--) {   // L^T x = y
+                const double xj = j < 64 ? readlane_d(v0, j) : readlane_d(v1, j - 64);
+                if (lane < j) v0 -= A[j * D + lane] * xj;
+                if (lane + 64 < j) v1 -= A[j * D + lane + 64] * xj;
+            }
+        } else {
+            v0 = v1 = 0;
         }
-        b.part[l] = part;
-    } else if (t < b.nl + b.np) {
-        const int i = t - b.nl;
+        if (lane < D) b.x[lane] = v0;
+        if (lane + 64 < D) b.x[lane + 64] = v1;
+        if (lane == 0) b.ctl->ok2 = ok;
+    }
+    __syncthreads();
+    // push() + oplus for the free poses, scale terms x.(lambda x + b)
+    const double lam = b.ctl->lambda;
+    for (int i = threadIdx.x; i < b.np; i += blockDim.x) {
         const int id = b.ps_id[i];
         double part = 0;
         for (int j = 0; j < 6; j++) part += b.x[6 * i + j] * (lam * b.x[6 * i + j] + b.bp[6 * i + j]);
@@ -539,40 +628,105 @@ __global__ void ba_update_kernel(BADev b, int D) {
     }
 }
 
-// levenberg.cpp:120-147 — the accept / reject decision (one thread).
-__global__ void ba_decide_kernel(BADev b) {
-    BACtl* c = b.ctl;
-    double tmp = c->tmp;
-    if (!c->ok2) tmp = 1.7976931348623157e308;   // std::numeric_limits<double>::max()
-    double rho = c->cur - tmp;
-    double scale = c->scale + 1e-3;
-    rho /= scale;
-    c->rho = rho;
-    if (rho > 0 && isfinite(tmp)) {
-        double alpha = 1. - pow((2 * rho - 1), 3);
-        alpha = fmin(alpha, 2. / 3.);
-        c->lambda *= fmax(1. / 3., alpha);
-        c->ni = 2;
-        c->cur = tmp;
-        c->accepted = 1;
-    } else {
-        c->lambda *= c->ni;
-        c->ni *= 2;
-        c->accepted = 0;
+// Back-substitution xl = Dinv (bl - Hpl^T xp), push(), point +=, scale term, then the errors and
+// robust chi2 of the point's edges at the new estimate (computeActiveErrors after update()).
+__global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = t / GRP, sub = t % GRP;
+    const bool live = l < b.nl;
+    double cl[3] = {0, 0, 0};
+    if (live)
+        for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
+            const int k = b.pt_slot[u];
+            const int ip = b.hp[b.ek[b.act[k]]];
+            if (ip < 0) continue;
+            const double* Hpl = b.J + (long long)k * 72 + 54;
+            for (int c = 0; c < 3; c++) {
+                double s = 0;
+                for (int r = 0; r < 6; r++) s += Hpl[3 * r + c] * b.x[6 * ip + r];
+                cl[c] += s;
+            }
+        }
+    for (int c = 0; c < 3; c++) cl[c] = grp_sum(cl[c]);
+    if (!live) return;
+    const double lam = b.ctl->lambda;
+    double bl[3], xl[3];
+    for (int c = 0; c < 3; c++) bl[c] = b.bl[3 * l + c];
+    const double* Di = b.Dinv + 9 * l;
+    for (int c = 0; c < 3; c++) cl[c] = bl[c] - cl[c];
+    const int id = b.pt_id[l];
+    double Xn[3];
+    double part = 0;
+    for (int i = 0; i < 3; i++) {
+        xl[i] = Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1] + Di[3 * i + 2] * cl[2];
+        Xn[i] = b.X[3 * id + i] + xl[i];
+        part += xl[i] * (lam * xl[i] + bl[i]);
     }
+    // every lane of the group read X before lane 0 overwrites it below (same wavefront, in order)
+    __builtin_amdgcn_wave_barrier();
+    if (sub == 0) {
+        for (int i = 0; i < 3; i++) {
+            b.x[D + 3 * l + i] = xl[i];
+            b.X_sv[3 * id + i] = b.X[3 * id + i];
+            b.X[3 * id + i] = Xn[i];
+        }
+        b.part[l] = part;
+    }
+    double chi = 0;
+    for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
+        const int e = b.act[b.pt_slot[u]];
+        const int pi = b.ek[e];
+        double Xc[3];
+        se3_map(b.q + 4 * pi, b.t + 3 * pi, Xn, Xc);
+        chi += edge_error(b, e, Xc);
+    }
+    // group partial (lanes of a group are contiguous; sum in fixed order via shuffles)
+    chi += __shfl_xor(chi, 1, 64);
+    chi += __shfl_xor(chi, 2, 64);
+    chi += __shfl_xor(chi, 4, 64);
+    if (sub == 0) b.rchi[l] = chi;
 }
 
-// pop(): restore the pushed estimates when the step was rejected.
-__global__ void ba_restore_kernel(BADev b) {
-    if (b.ctl->accepted) return;
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < b.nl) {
-        const int id = b.pt_id[t];
-        for (int i = 0; i < 3; i++) b.X[3 * id + i] = b.X_sv[3 * id + i];
-    } else if (t < b.nl + b.np) {
-        const int id = b.ps_id[t - b.nl];
-        for (int j = 0; j < 4; j++) b.q[4 * id + j] = b.q_sv[4 * id + j];
-        for (int j = 0; j < 3; j++) b.t[3 * id + j] = b.t_sv[3 * id + j];
+// levenberg.cpp:120-147 — sums, accept / reject, lambda / nu update, pop() on reject.
+__global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b) {
+    __shared__ double sh[1024];
+    __shared__ int s_acc;
+    const double tmp_sum = block_sum_1024(b.rchi, b.nl, sh);
+    const double scale_sum = block_sum_1024(b.part, b.nl + b.np, sh);
+    BACtl* c = b.ctl;
+    if (threadIdx.x == 0) {
+        c->tmp = tmp_sum;
+        c->scale = scale_sum;
+        double tmp = tmp_sum;
+        if (!c->ok2) tmp = 1.7976931348623157e308;   // std::numeric_limits<double>::max()
+        double rho = c->cur - tmp;
+        rho /= (scale_sum + 1e-3);
+        c->rho = rho;
+        if (rho > 0 && isfinite(tmp)) {
+            double alpha = 1. - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2. / 3.);
+            c->lambda *= fmax(1. / 3., alpha);
+            c->ni = 2;
+            c->cur = tmp;
+            c->accepted = 1;
+        } else {
+            c->lambda *= c->ni;
+            c->ni *= 2;
+            c->accepted = 0;
+        }
+        s_acc = c->accepted;
+    }
+    __syncthreads();
+    if (s_acc) return;
+    for (int t = threadIdx.x; t < b.nl + b.np; t += blockDim.x) {
+        if (t < b.nl) {
+            const int id = b.pt_id[t];
+            for (int i = 0; i < 3; i++) b.X[3 * id + i] = b.X_sv[3 * id + i];
+        } else {
+            const int id = b.ps_id[t - b.nl];
+            for (int j = 0; j < 4; j++) b.q[4 * id + j] = b.q_sv[4 * id + j];
+            for (int j = 0; j < 3; j++) b.t[3 * id + j] = b.t_sv[3 * id + j];
+        }
     }
 }
 
@@ -805,8 +959,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         *iters_out = 0;
         *chi_out = 0;
         if (Ea == 0 || np + nl == 0) return ORB_OK;
-        if ((size_t)D * D * 8 + (size_t)D * 8 > 150 * 1024) {
-            set_error("LocalBA: too many free keyframes for the in-LDS reduced-system solve (max 22)");
+        if (D > 128 || (size_t)D * D * 8 > 150 * 1024) {
+            set_error("LocalBA: too many free keyframes for the in-LDS reduced-system solve (max 21)");
             return ORB_EINVAL;
         }
         // structure upload
@@ -856,7 +1010,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                               carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +
                               carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
                               carve_size<double>((size_t)D * D) + carve_size<double>(D) +
-                              carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(Ea) +
+                              carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
                               carve_size<double>(nl + np) + 64;
         if ((rc2 = C.sys.reserve(ybytes))) return rc2;
         Carve cy{C.sys.as<char>()};
@@ -870,41 +1024,27 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.S = cy.take<double>((size_t)D * D);
         b.bs = cy.take<double>(D);
         b.x = cy.take<double>(D + 3 * (size_t)nl);
-        b.rchi = cy.take<double>(Ea);
+        b.rchi = cy.take<double>(std::max(Ea, nl));
         b.part = cy.take<double>(nl + np);
         ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
-        const size_t ldlt_lds = ((size_t)D * D + D) * 8;
-        ORB_HIP_TRY(hipFuncSetAttribute((const void*)ba_ldlt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        const size_t ldlt_lds = std::max<size_t>((size_t)D * D * 8, 16);
+        ORB_HIP_TRY(hipFuncSetAttribute((const void*)ba_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)std::max<size_t>(ldlt_lds, 1024)));
-        const dim3 ge((Ea + 255) / 256), gv((nl + np + 255) / 256), gp((nl + 255) / 256);
-        double* d_cur = &b.ctl->cur;
+        const dim3 gg((nl * 8 + 63) / 64);   // 8 lanes per point
         int nbad = 0;
         for (int it = 0; it < iters && !stopped(); it++) {
-            hipLaunchKernelGGL(ba_error_kernel, ge, dim3(256), 0, st, b);
-            hipLaunchKernelGGL(ba_sum_kernel, dim3(1), dim3(1024), 0, st, (const double*)b.rchi, Ea, d_cur);
-            ORB_HIP_TRY(hipMemcpyAsync(&b.ctl->ini, d_cur, 8, hipMemcpyDeviceToDevice, st));
-            hipLaunchKernelGGL(ba_linearize_kernel, ge, dim3(256), 0, st, b);
-            if (nl) hipLaunchKernelGGL(ba_point_accum_kernel, gp, dim3(256), 0, st, b);
-            if (np) hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np), dim3(256), 0, st, b);
+            hipLaunchKernelGGL(ba_iter_kernel, gg, dim3(64), 0, st, b);
+            hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b, 1);
             if (it == 0) hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
             int q = 0;
             double rho = 0;
             do {
-                if (nl) hipLaunchKernelGGL(ba_schur_point_kernel, gp, dim3(256), 0, st, b);
-                if (np) {
-                    hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk), dim3(256), 0, st, b, D);
-                    hipLaunchKernelGGL(ba_schur_rhs_kernel, dim3(np), dim3(256), 0, st, b);
-                    hipLaunchKernelGGL(ba_ldlt_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
-                } else {
-                    ORB_HIP_TRY(hipMemsetAsync(&b.ctl->ok2, 0xff, 4, st));   // no poses: ok
-                }
-                hipLaunchKernelGGL(ba_update_kernel, gv, dim3(256), 0, st, b, D);
-                hipLaunchKernelGGL(ba_sum_kernel, dim3(1), dim3(1024), 0, st, (const double*)b.part, nl + np, &b.ctl->scale);
-                hipLaunchKernelGGL(ba_error_kernel, ge, dim3(256), 0, st, b);
-                hipLaunchKernelGGL(ba_sum_kernel, dim3(1), dim3(1024), 0, st, (const double*)b.rchi, Ea, &b.ctl->tmp);
-                hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(1), 0, st, b);
-                hipLaunchKernelGGL(ba_restore_kernel, gv, dim3(256), 0, st, b);
+                hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
+                if (np) hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk), dim3(1024), 0, st, b, D);
+                hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
+                hipLaunchKernelGGL(ba_point_update_kernel, gg, dim3(64), 0, st, b, D);
+                hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(1024), 0, st, b);
                 ORB_HIP_TRY(hipGetLastError());
                 ORB_HIP_TRY(hipMemcpyAsync(C.h_ctl, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost, st));
                 ORB_HIP_TRY(hipStreamSynchronize(st));

@@ -17,20 +17,37 @@ namespace orbamd {
 
 constexpr int TILE = 256;
 
+__device__ __forceinline__ int hamming32(uint4 a0, uint4 a1, uint4 b0, uint4 b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__device__ __forceinline__ void top2_update(int d, int j, int& bd, int& sd, int& bi) {
+    if (d < bd) {
+        sd = bd;
+        bd = d;
+        bi = j;
+    } else if (d < sd) {
+        sd = d;
+    }
+}
+
 __global__ __launch_bounds__(256) void hamming_top2_kernel(const uint8_t* __restrict__ A, const int32_t* __restrict__ nA_arr,
                                                            int nA_fixed, int strideA, const uint8_t* __restrict__ B,
                                                            const int32_t* __restrict__ nB_arr, int nB_fixed, int strideB,
-                                                           float nnratio, int th_low, int32_t* __restrict__ best_idx,
+                                                           const int32_t* __restrict__ pair_b, float nnratio,
+                                                           int th_low, int32_t* __restrict__ best_idx,
                                                            int32_t* __restrict__ best, int32_t* __restrict__ second,
                                                            int32_t* __restrict__ match) {
     __shared__ uint4 tile[TILE * 2];
     const int p = blockIdx.y;
+    const int q = pair_b ? pair_b[p] : p;
     const int nA = nA_arr ? nA_arr[p] : nA_fixed;
-    const int nB = nB_arr ? nB_arr[p] : nB_fixed;
+    const int nB = nB_arr ? nB_arr[q] : nB_fixed;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if ((int)(blockIdx.x * blockDim.x) >= nA) return;   // block-uniform
     const uint8_t* Ap = A + (long long)p * strideA * 32;
-    const uint8_t* Bp = B + (long long)p * strideB * 32;
+    const uint8_t* Bp = B + (long long)q * strideB * 32;
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
     if (i < nA) {
         q0 = reinterpret_cast<const uint4*>(Ap)[2 * i];
@@ -43,18 +60,18 @@ __global__ __launch_bounds__(256) void hamming_top2_kernel(const uint8_t* __rest
         for (int r = threadIdx.x; r < 2 * nt; r += blockDim.x)
             tile[r] = reinterpret_cast<const uint4*>(Bp)[2 * t0 + r];
         __syncthreads();
-        for (int j = 0; j < nt; j++) {
-            const uint4 b0 = tile[2 * j], b1 = tile[2 * j + 1];
-            const int d = __popc(q0.x ^ b0.x) + __popc(q0.y ^ b0.y) + __popc(q0.z ^ b0.z) + __popc(q0.w ^ b0.w) +
-                          __popc(q1.x ^ b1.x) + __popc(q1.y ^ b1.y) + __popc(q1.z ^ b1.z) + __popc(q1.w ^ b1.w);
-            if (d < bd) {
-                sd = bd;
-                bd = d;
-                bi = t0 + j;
-            } else if (d < sd) {
-                sd = d;
-            }
+        int j = 0;
+        for (; j + 4 <= nt; j += 4) {   // four candidates per step: LDS reads issued together
+            const uint4 b00 = tile[2 * j], b01 = tile[2 * j + 1], b10 = tile[2 * j + 2], b11 = tile[2 * j + 3];
+            const uint4 b20 = tile[2 * j + 4], b21 = tile[2 * j + 5], b30 = tile[2 * j + 6], b31 = tile[2 * j + 7];
+            const int d0 = hamming32(q0, q1, b00, b01), d1 = hamming32(q0, q1, b10, b11);
+            const int d2 = hamming32(q0, q1, b20, b21), d3 = hamming32(q0, q1, b30, b31);
+            top2_update(d0, t0 + j, bd, sd, bi);
+            top2_update(d1, t0 + j + 1, bd, sd, bi);
+            top2_update(d2, t0 + j + 2, bd, sd, bi);
+            top2_update(d3, t0 + j + 3, bd, sd, bi);
         }
+        for (; j < nt; j++) top2_update(hamming32(q0, q1, tile[2 * j], tile[2 * j + 1]), t0 + j, bd, sd, bi);
     }
     if (i < nA) {
         const long long o = (long long)p * strideA + i;
@@ -147,22 +164,22 @@ int orbm_hamming_top2_device(const uint8_t* d_A, int nA, const uint8_t* d_B, int
     ORB_CHECK_ARG(nA >= 0 && nB >= 0 && (nA == 0 || d_A) && (nB == 0 || d_B), "bad matcher arguments");
     if (nA == 0) return ORB_OK;
     hipLaunchKernelGGL(hamming_top2_kernel, dim3((unsigned)((nA + 255) / 256), 1), dim3(256), 0, (hipStream_t)stream,
-                       d_A, (const int32_t*)nullptr, nA, nA, d_B, (const int32_t*)nullptr, nB, nB, 0.6f, 50, d_best_idx,
-                       d_best, d_second, (int32_t*)nullptr);
+                       d_A, (const int32_t*)nullptr, nA, nA, d_B, (const int32_t*)nullptr, nB, nB,
+                       (const int32_t*)nullptr, 0.6f, 50, d_best_idx, d_best, d_second, (int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
 
 int orbm_bf_match_batch_device(const uint8_t* d_A, const int32_t* d_nA, int strideA, const uint8_t* d_B,
-                               const int32_t* d_nB, int strideB, int n_pairs, float nnratio, int th_low,
-                               int32_t* d_best_idx, int32_t* d_best, int32_t* d_second, int32_t* d_match,
-                               void* stream) {
+                               const int32_t* d_nB, int strideB, const int32_t* d_pair_b, int n_pairs, float nnratio,
+                               int th_low, int32_t* d_best_idx, int32_t* d_best, int32_t* d_second,
+                               int32_t* d_match, void* stream) {
     ORB_CHECK_ARG(d_A && d_B && d_nA && d_nB && n_pairs >= 0 && strideA > 0 && strideB > 0, "bad matcher arguments");
     if (n_pairs == 0) return ORB_OK;
     ORB_CHECK_ARG(n_pairs <= 65535, "too many pairs in one launch");
     hipLaunchKernelGGL(hamming_top2_kernel, dim3((unsigned)((strideA + 255) / 256), (unsigned)n_pairs), dim3(256), 0,
-                       (hipStream_t)stream, d_A, d_nA, 0, strideA, d_B, d_nB, 0, strideB, nnratio, th_low, d_best_idx,
-                       d_best, d_second, d_match);
+                       (hipStream_t)stream, d_A, d_nA, 0, strideA, d_B, d_nB, 0, strideB, d_pair_b, nnratio, th_low,
+                       d_best_idx, d_best, d_second, d_match);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
@@ -182,7 +199,7 @@ int orbm_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float nnra
     if (nB) ORB_HIP_TRY(hipMemcpy(s.b.ptr, B, (size_t)nB * 32, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(hamming_top2_kernel, dim3((unsigned)((nA + 255) / 256), 1), dim3(256), 0, (hipStream_t)0,
                        s.a.as<uint8_t>(), (const int32_t*)nullptr, nA, nA, s.b.as<uint8_t>(), (const int32_t*)nullptr,
-                       nB, nB, nnratio, th_low, o, o + nA, o + 2 * nA, o + 3 * nA);
+                       nB, nB, (const int32_t*)nullptr, nnratio, th_low, o, o + nA, o + 2 * nA, o + 3 * nA);
     ORB_HIP_TRY(hipGetLastError());
     std::vector<int32_t> h((size_t)nA * 4);
     ORB_HIP_TRY(hipMemcpy(h.data(), o, (size_t)nA * 16, hipMemcpyDeviceToHost));

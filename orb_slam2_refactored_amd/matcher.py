@@ -33,15 +33,17 @@ class ORBmatcher:
                                   ptr(sd), ptr(m)), "orbm_bf_match")
         return bi, bd, sd, m
 
-    def match_batch_device(self, descA, nA, descB, nB, th_low: int = TH_LOW, out=None, stream=None):
-        """Batched pairs on the GPU: descA [P, capA, 32], nA [P] int32, descB [P, capB, 32], nB [P].
+    def match_batch_device(self, descA, nA, descB, nB, th_low: int = TH_LOW, out=None, stream=None, pair_b=None):
+        """Batched pairs on the GPU: descA [P, capA, 32], nA [P] int32, descB [Q, capB, 32], nB [Q];
+        pair p uses B frame pair_b[p] (int32 [P] tensor) or p when pair_b is None.
         Returns int32 tensor [4, P, capA] = (best_idx, best, second, match)."""
         import torch
         P, capA = descA.shape[0], descA.shape[1]
         if out is None:
             out = torch.empty((4, P, capA), dtype=torch.int32, device=descA.device)
-        check(lib().orbm_bf_match_batch_device(tptr(descA), tptr(nA), capA, tptr(descB), tptr(nB), descB.shape[1], P,
-                                               C.c_float(self.fNNRatio_), th_low, tptr(out[0]), tptr(out[1]),
+        pb = tptr(pair_b) if pair_b is not None else None
+        check(lib().orbm_bf_match_batch_device(tptr(descA), tptr(nA), capA, tptr(descB), tptr(nB), descB.shape[1], pb,
+                                               P, C.c_float(self.fNNRatio_), th_low, tptr(out[0]), tptr(out[1]),
                                                tptr(out[2]), tptr(out[3]), stream_ptr(stream)),
               "orbm_bf_match_batch_device")
         return out

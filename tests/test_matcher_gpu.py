@@ -80,6 +80,15 @@ def test_batch_device(oracle):
         exp = oracle.bf_match(A[p, :nA[p]], B[p, :nB[p]])
         for k in range(4):
             assert np.array_equal(out[k, p, :nA[p]], exp[k])
+    # pair -> B-frame indirection (match each frame against its predecessor without a copy)
+    pb = np.array([(p - 1) % P for p in range(P)], np.int32)
+    out = ORBmatcher().match_batch_device(torch.from_numpy(A).cuda(), torch.from_numpy(nA).cuda(),
+                                          torch.from_numpy(B).cuda(), torch.from_numpy(nB).cuda(),
+                                          pair_b=torch.from_numpy(pb).cuda()).cpu().numpy()
+    for p in range(P):
+        exp = oracle.bf_match(A[p, :nA[p]], B[pb[p], :nB[pb[p]]])
+        for k in range(4):
+            assert np.array_equal(out[k, p, :nA[p]], exp[k])
 
 
 @pytest.mark.parametrize("seed,stereo,single", [(0, False, False), (1, True, False), (2, False, True), (3, False, False)])

@@ -29,14 +29,14 @@ def main():
     ex = ORBextractor(ORBextractor.Parameters(nfeatures=a.nfeatures))
     kps, desc, cnt = ex.extract_batch_device(frames)
     m = ORBmatcher(0.6, False)
-    prev = torch.tensor([(i - 1) % a.frames for i in range(a.frames)], device="cuda")
+    prev = torch.tensor([(i - 1) % a.frames for i in range(a.frames)], dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     ex.profile(True)
     t0 = time.perf_counter()
     for _ in range(a.iters):
         ex.extract_batch_device(frames, kps, desc, cnt)
         if a.match:
-            m.match_batch_device(desc, cnt, desc.index_select(0, prev), cnt.index_select(0, prev))
+            m.match_batch_device(desc, cnt, desc, cnt, pair_b=prev)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st = ex.profile_read()
