@@ -1,0 +1,172 @@
+// orbslam2_amd.hpp — C++ drop-in classes over the C-ABI (include/orbslam2_amd.h).
+//
+// They keep the reference's class / method shapes so Tracking and LocalMapping call them
+// unchanged:
+//   ORB_SLAM2_AMD::ORBextractor   <- ORB_SLAM2::ORBextractor   (include/ORBextractor.h:35-81)
+//   ORB_SLAM2_AMD::ORBmatcher     <- ORB_SLAM2::ORBmatcher Hamming kernels (include/ORBmatcher.h)
+//   ORB_SLAM2_AMD::LocalBundleAdjustment <- Optimizer::LocalBundleAdjustment (include/Optimizer.h:47)
+// Plain-type overloads are always available; when OpenCV is on the include path the
+// cv::Mat / cv::KeyPoint overloads with the reference's exact signatures are added.
+// A non-zero C status is turned into an exception, as the reference's CV_Assert does.
+#ifndef ORBSLAM2_AMD_HPP
+#define ORBSLAM2_AMD_HPP
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "orbslam2_amd.h"
+
+#if defined(__has_include)
+#if __has_include(<opencv2/core.hpp>)
+#include <opencv2/core.hpp>
+#define ORBSLAM2_AMD_HAVE_OPENCV 1
+#endif
+#endif
+
+namespace ORB_SLAM2_AMD {
+
+inline void check(int rc, const char* what) {
+    if (rc != ORB_OK) throw std::runtime_error(std::string(what) + ": " + orb_last_error());
+}
+
+class ORBextractor {
+public:
+    struct Parameters {   // include/ORBextractor.h:39-47
+        int nfeatures;
+        float scaleFactor;
+        int nlevels;
+        int iniThFAST;
+        int minThFAST;
+        Parameters(int nfeatures = 2000, float scaleFactor = 1.2f, int nlevels = 8, int iniThFAST = 20,
+                   int minThFAST = 7)
+            : nfeatures(nfeatures), scaleFactor(scaleFactor), nlevels(nlevels), iniThFAST(iniThFAST),
+              minThFAST(minThFAST) {}
+    };
+
+    explicit ORBextractor(const Parameters& p, int device = 0) : param_(p) {
+        orbx_params c{p.nfeatures, p.scaleFactor, p.nlevels, p.iniThFAST, p.minThFAST};
+        check(orbx_create(&c, device, &h_), "orbx_create");
+        const int L = p.nlevels;
+        scale_.resize(L); inv_.resize(L); s2_.resize(L); is2_.resize(L);
+        check(orbx_scale_tables(h_, scale_.data(), inv_.data(), s2_.data(), is2_.data(), nullptr), "orbx_scale_tables");
+    }
+    ~ORBextractor() { orbx_destroy(h_); }
+    ORBextractor(const ORBextractor&) = delete;
+    ORBextractor& operator=(const ORBextractor&) = delete;
+
+    // Extract on a raw CV_8U image.  Returns false (outputs untouched) when no keypoint exists —
+    // the reference's early return (src/ORBextractor.cc:778-782).
+    bool Extract(const uint8_t* img, int rows, int cols, size_t step, std::vector<orbx_keypoint>& keypoints,
+                 std::vector<uint8_t>& descriptors) {
+        int32_t cap = 0;
+        check(orbx_max_keypoints(h_, rows, cols, &cap), "orbx_max_keypoints");
+        kbuf_.resize(cap);
+        dbuf_.resize((size_t)cap * 32);
+        int n = 0;
+        check(orbx_extract(h_, img, rows, cols, step, kbuf_.data(), dbuf_.data(), cap, &n), "orbx_extract");
+        if (n == 0) {
+            descriptors.clear();
+            return false;
+        }
+        keypoints.assign(kbuf_.begin(), kbuf_.begin() + n);
+        descriptors.assign(dbuf_.begin(), dbuf_.begin() + (size_t)n * 32);
+        return true;
+    }
+
+#ifdef ORBSLAM2_AMD_HAVE_OPENCV
+    // void Extract(const cv::Mat& image, KeyPoints& keypoints, cv::Mat& descriptors)
+    void Extract(const cv::Mat& image, std::vector<cv::KeyPoint>& keypoints, cv::Mat& descriptors) {
+        CV_Assert(image.type() == CV_8U);
+        std::vector<orbx_keypoint> k;
+        std::vector<uint8_t> d;
+        if (!Extract(image.data, image.rows, image.cols, image.step, k, d)) {
+            descriptors.release();   // keypoints left untouched, as the reference
+            return;
+        }
+        keypoints.resize(k.size());
+        for (size_t i = 0; i < k.size(); i++)
+            keypoints[i] = cv::KeyPoint(k[i].x, k[i].y, k[i].size, k[i].angle, k[i].response, k[i].octave,
+                                        k[i].class_id);
+        descriptors.create((int)k.size(), 32, CV_8U);
+        std::copy(d.begin(), d.end(), descriptors.data);
+    }
+#endif
+
+    int GetLevels() const { return param_.nlevels; }
+    float GetScaleFactor() const { return param_.scaleFactor; }
+    const std::vector<float>& GetScaleFactors() const { return scale_; }
+    const std::vector<float>& GetInverseScaleFactors() const { return inv_; }
+    const std::vector<float>& GetScaleSigmaSquares() const { return s2_; }
+    const std::vector<float>& GetInverseScaleSigmaSquares() const { return is2_; }
+
+    // GetImagePyramid(): level s of the last image, copied to host memory.
+    std::vector<uint8_t> GetImagePyramidLevel(int s, int* rows, int* cols) const {
+        check(orbx_pyramid_level(h_, s, nullptr, 0, rows, cols), "orbx_pyramid_level");
+        std::vector<uint8_t> out((size_t)(*rows) * (*cols));
+        check(orbx_pyramid_level(h_, s, out.data(), (size_t)(*cols), rows, cols), "orbx_pyramid_level");
+        return out;
+    }
+
+    orbx_extractor* handle() const { return h_; }
+
+private:
+    Parameters param_;
+    orbx_extractor* h_ = nullptr;
+    std::vector<float> scale_, inv_, s2_, is2_;
+    std::vector<orbx_keypoint> kbuf_;
+    std::vector<uint8_t> dbuf_;
+};
+
+class ORBmatcher {
+public:
+    explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true) : nnratio_(nnratio), checkOri_(checkOri) {}
+
+    // static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b) on 32-byte rows
+    static int DescriptorDistance(const uint8_t* a, const uint8_t* b) { return orbm_descriptor_distance(a, b); }
+
+    // Brute-force best / second-best + ratio test over all rows (reference loop semantics).
+    void MatchBruteForce(const uint8_t* A, int nA, const uint8_t* B, int nB, std::vector<int>& match,
+                         int th_low = 50) const {
+        std::vector<int32_t> bi(nA), bd(nA), sd(nA), m(nA);
+        check(orbm_bf_match(A, nA, B, nB, nnratio_, th_low, bi.data(), bd.data(), sd.data(), m.data()), "orbm_bf_match");
+        match.assign(m.begin(), m.end());
+    }
+
+    // int SearchForTriangulation(kf1, kf2, F12, matchIds, onlyStereo) on flattened keyframes.
+    int SearchForTriangulation(const orbm_tri_frame& kf1, const orbm_tri_frame& kf2, const float F12[9],
+                               const float ep2[2], const std::vector<float>& scale2, const std::vector<float>& sigma2,
+                               std::vector<std::pair<size_t, size_t>>& matchIds, bool onlyStereo) const {
+        std::vector<int32_t> m12(kf1.n);
+        int32_t n = 0;
+        check(orbm_search_for_triangulation(&kf1, &kf2, F12, ep2, scale2.data(), sigma2.data(), (int)scale2.size(),
+                                            onlyStereo ? 1 : 0, m12.data(), &n),
+              "orbm_search_for_triangulation");
+        matchIds.clear();
+        matchIds.reserve(n);
+        for (int i = 0; i < kf1.n; i++)
+            if (m12[i] >= 0) matchIds.emplace_back((size_t)i, (size_t)m12[i]);
+        return n;
+    }
+
+    float nnratio() const { return nnratio_; }
+    bool checkOrientation() const { return checkOri_; }
+
+private:
+    float nnratio_;
+    bool checkOri_;
+};
+
+// Optimizer::LocalBundleAdjustment from the flattened graph (Optimizer.cc:540-631): the caller
+// gathers local / fixed keyframes and local map points exactly as :493-537, calls this, then
+// erases the outlier observations and writes poses / points back under the map mutex (:677-735).
+inline void LocalBundleAdjustment(const orbba_problem& problem, orbba_result& result, const volatile int32_t* stopFlag,
+                                  int device = 0) {
+    check(orbba_local_ba(&problem, &result, stopFlag, device), "orbba_local_ba");
+}
+
+}  // namespace ORB_SLAM2_AMD
+
+#endif  // ORBSLAM2_AMD_HPP

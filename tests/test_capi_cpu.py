@@ -48,3 +48,16 @@ def test_package_does_not_import_oracle():
     for p in (ROOT / "orb_slam2_refactored_amd" / "csrc").glob("*"):
         if p.suffix in (".hip", ".h", ".cpp"):
             assert "orb_oracle" not in p.read_text(), p
+
+
+def test_cpp_wrapper_compiles_and_links(tmp_path):
+    """include/orbslam2_amd.hpp (the C++ drop-in classes) compiles and links against the library."""
+    src = ROOT / "tests" / "native" / "cpp_wrapper_use.cpp"
+    obj = tmp_path / "w.o"
+    subprocess.run(["g++", "-std=c++14", "-c", f"-I{ROOT / 'include'}", str(src), "-o", str(obj)], check=True)
+    if LIB.exists():
+        main = tmp_path / "main.cpp"
+        main.write_text("int use_wrapper(); int main() { return use_wrapper() >= 0 ? 0 : 1; }\n")
+        exe = tmp_path / "w"
+        subprocess.run(["g++", str(main), str(obj), "-o", str(exe), f"-L{LIB.parent}", "-lorbslam2_amd",
+                        f"-Wl,-rpath,{LIB.parent}"], check=True)
