@@ -105,37 +105,41 @@ def main():
 
     from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
     from orb_slam2_refactored_amd.synth import synth_image
+    from orb_slam2_refactored_amd.shard import SlotExchange, Slots, shard_range
 
     W, H, B = args.width, args.height, args.frames
-    # synthetic frames (seeded, distinct per rank); generate a pool and tile it
+    # synthetic frames: this rank's shard of world*B global frames (seed = global frame index);
+    # a pool of 16 distinct images is tiled over the batch
+    g0, _ = shard_range(world * B, world, rank)
     pool = min(B, 16)
-    base = np.stack([synth_image(rank * 100003 + i, W, H) for i in range(pool)])
+    base = np.stack([synth_image(g0 + i, W, H) for i in range(pool)])
     frames_np = np.concatenate([base[i % pool][None] for i in range(B)])
     frames = torch.from_numpy(frames_np).to(dev)
     ex = ORBextractor(ORBextractor.Parameters(nfeatures=args.nfeatures), device=local)
     m = ORBmatcher(0.6, False)
     cap = ex.max_keypoints(H, W)
-    kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
-    desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-    counts = torch.empty((B,), dtype=torch.int32, device=dev)
     prev_idx = torch.tensor([(i - 1) % B for i in range(B)], dtype=torch.int32, device=dev)
     match_out = torch.empty((4, B, cap), dtype=torch.int32, device=dev)
-    if world > 1:
-        g_kps = torch.empty((world * B, cap, 7), dtype=torch.int32, device=dev)
-        g_desc = torch.empty((world * B, cap, 32), dtype=torch.uint8, device=dev)
-        g_counts = torch.empty((world * B,), dtype=torch.int32, device=dev)
+    # world > 1: double-buffered async all-gather of every rank's slots (shard.SlotExchange);
+    # step k's collectives overlap step k+1's kernels.
+    xchg = SlotExchange(B, cap, dev) if world > 1 else None
+    single = Slots.empty(B, cap, dev)
     stream = torch.cuda.current_stream()
+    last = [single]
 
     def step():
-        ex.extract_batch_device(frames, kps, desc, counts, stream=stream)
-        m.match_batch_device(desc, counts, desc, counts, out=match_out, stream=stream, pair_b=prev_idx)
-        if world > 1:
-            dist.all_gather_into_tensor(g_counts, counts)
-            dist.all_gather_into_tensor(g_kps, kps)
-            dist.all_gather_into_tensor(g_desc, desc)
+        local = xchg.acquire() if xchg else single
+        ex.extract_batch_device(frames, local.kps, local.desc, local.counts, stream=stream)
+        m.match_batch_device(local.desc, local.counts, local.desc, local.counts, out=match_out, stream=stream,
+                             pair_b=prev_idx)
+        if xchg:
+            xchg.publish()
+        last[0] = local
 
     for _ in range(args.warmup):
         step()
+    if xchg:
+        xchg.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -146,6 +150,8 @@ def main():
     ev0.record(stream)
     for _ in range(args.steps):
         step()
+    if xchg:
+        xchg.drain()
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -159,7 +165,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    n_kp = float(counts.float().mean().item())
+    n_kp = float(last[0].counts.float().mean().item())
     matches = int((match_out[3] >= 0).sum().item())
     total_frames = world * B * args.steps
     value = total_frames / elapsed

@@ -1,0 +1,119 @@
+"""N>1 path on CPU: frame sharding and the double-buffered slot all-gather over `gloo`, world_size 2
+(the same SlotExchange that bench.py runs over RCCL).  The gathered buffer must equal the
+concatenation of every rank's slots byte for byte."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from orb_slam2_refactored_amd.shard import SlotExchange, Slots, shard_range, unpack  # noqa: E402
+
+FRAMES, CAP, STEPS = 3, 40, 5
+
+
+def fake_slots(global_frame0: int, step: int) -> Slots:
+    """Deterministic stand-in for one rank's extraction output (ragged counts, incl. 0 and CAP)."""
+    s = Slots.empty(FRAMES, CAP, "cpu")
+    for f in range(FRAMES):
+        g = global_frame0 + f
+        gen = torch.Generator().manual_seed(1000 * step + g)
+        s.kps[f] = torch.randint(-2**31, 2**31 - 1, (CAP, 7), generator=gen, dtype=torch.int64).to(torch.int32)
+        s.desc[f] = torch.randint(0, 256, (CAP, 32), generator=gen, dtype=torch.int64).to(torch.uint8)
+        s.counts[f] = [0, CAP, (7 * g + step) % CAP][(g + step) % 3]
+    return s
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, errq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        start, count = shard_range(world * FRAMES, world, rank)
+        assert count == FRAMES
+        ex = SlotExchange(FRAMES, CAP, "cpu")
+        for step in range(STEPS):
+            local = ex.acquire()
+            src = fake_slots(start, step)
+            local.kps.copy_(src.kps)
+            local.desc.copy_(src.desc)
+            local.counts.copy_(src.counts)
+            i = ex.publish()
+        ex.drain()
+        # the last published set holds step STEPS-1 from every rank, in rank order
+        g = ex.gathered(i)
+        for r in range(world):
+            r0, _ = shard_range(world * FRAMES, world, r)
+            want = fake_slots(r0, STEPS - 1)
+            sl = slice(r * FRAMES, (r + 1) * FRAMES)
+            assert torch.equal(g.kps[sl], want.kps)
+            assert torch.equal(g.desc[sl], want.desc)
+            assert torch.equal(g.counts[sl], want.counts)
+        # and the other set holds step STEPS-2
+        g2 = ex.gathered(1 - i)
+        for r in range(world):
+            r0, _ = shard_range(world * FRAMES, world, r)
+            assert torch.equal(g2.desc[r * FRAMES:(r + 1) * FRAMES], fake_slots(r0, STEPS - 2).desc)
+        per_frame = unpack(g)
+        assert len(per_frame) == world * FRAMES
+        assert [int(k.shape[0]) for k, _ in per_frame] == g.counts.tolist()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # pragma: no cover - reported by the parent
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+@pytest.mark.parametrize("world", [2])
+def test_slot_exchange_gloo(world):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_shard_range_partitions():
+    for n in range(0, 40):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                s, c = shard_range(n, world, r)
+                seen.extend(range(s, s + c))
+            assert seen == list(range(n))
+    with pytest.raises(ValueError):
+        shard_range(4, 2, 2)
+
+
+def test_single_process_exchange_is_copy():
+    ex = SlotExchange(FRAMES, CAP, "cpu")
+    local = ex.acquire()
+    src = fake_slots(0, 0)
+    local.kps.copy_(src.kps)
+    local.desc.copy_(src.desc)
+    local.counts.copy_(src.counts)
+    i = ex.publish()
+    ex.drain()
+    assert torch.equal(ex.gathered(i).desc, src.desc)
+    assert torch.equal(ex.gathered(i).counts, src.counts)
