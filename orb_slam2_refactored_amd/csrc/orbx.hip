@@ -96,6 +96,15 @@ __device__ __forceinline__ const uint8_t* level_base(const Geom& g, int l, int f
 }
 
 // Orders this wavefront's LDS accesses across lanes (LDS ops of one wave complete in order).
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs (linear id % 8), each
+// with its own 4 MiB L2.  Remap so XCD x runs one contiguous 1/8 of the logical blocks: neighbouring
+// cells / tiles / keypoints of a frame then share that XCD's L2 for their overlapping rows instead
+// of fetching the same 128-B lines from the fabric on several XCDs.  Bijective for any nb.
+__device__ __forceinline__ int xcd_swizzle(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Wave-inclusive scan of ints (64 lanes).
@@ -146,8 +155,10 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
     __shared__ int2 xs_t[PYR_TW], ys_t[PYR_TH];
     const LevelDev& L = g.lv[l];
     const LevelDev& Ls = g.lv[l - 1];
-    const int f = blockIdx.z;
-    const int tx0 = blockIdx.x * PYR_TW, ty0 = blockIdx.y * PYR_TH;
+    const int gx = gridDim.x, gxy = gridDim.x * gridDim.y;
+    const int lb = xcd_swizzle(blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z, gxy * gridDim.z);
+    const int f = lb / gxy;
+    const int tx0 = (lb % gx) * PYR_TW, ty0 = ((lb % gxy) / gx) * PYR_TH;
     const int tw = min(PYR_TW, L.w - tx0), th = min(PYR_TH, L.h - ty0);
     int sstep;
     const uint8_t* src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &sstep);
@@ -298,6 +309,18 @@ struct FastLds {
     int CS, ZS, crop_bytes, mz_bytes, qcap, ccap;
 };
 
+#ifdef ORB_FAST_STAMPS
+// diagnostic build: phase stamps of every 64th logical wave (8 words each)
+#define FAST_NSAMP 8192
+__device__ unsigned long long g_fast_stamps[FAST_NSAMP * 8];
+#define FAST_STAMP(k, v)                                                                               \
+    do {                                                                                             \
+        if (lane == 0 && (lb & 63) == 0 && (lb >> 6) < FAST_NSAMP) g_fast_stamps[(lb >> 6) * 8 + (k)] = (v); \
+    } while (0)
+#else
+#define FAST_STAMP(k, v) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
@@ -313,8 +336,11 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
 
     const int lane = threadIdx.x;
     const unsigned long long lt = lanemask_lt();
-    const CellDev cell = cells[blockIdx.x];
-    const int f = blockIdx.y;
+    const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    FAST_STAMP(0, __builtin_amdgcn_s_memtime());
+    const int ci = lb % gridDim.x;
+    const CellDev cell = cells[ci];
+    const int f = lb / gridDim.x;
     const int x0 = cell.x0y0 & 0xffff, y0 = cell.x0y0 >> 16;
     const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
     const int cw = zw + 6, ch = zh + 6;
@@ -364,6 +390,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
         for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
     }
     __syncthreads();
+    FAST_STAMP(1, __builtin_amdgcn_s_memtime());
 
     const int tlo = min(th_ini, th_min);
     const us2 t2 = {(unsigned short)tlo, (unsigned short)tlo};
@@ -422,6 +449,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     }
     if (qn > 0) drain(qn);
     wave_lds_sync();
+    FAST_STAMP(2, __builtin_amdgcn_s_memtime());
 
     // corner strengths into the zone map
     for (int j = lane; j < nc; j += 64) {
@@ -429,6 +457,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
         Mz[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(corner_strength(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd), 255);
     }
     wave_lds_sync();
+    FAST_STAMP(3, __builtin_amdgcn_s_memtime());
 
     auto nms = [&](int zy, int zx, int m, int t) -> bool {
         if (m <= t) return false;
@@ -461,6 +490,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     }
     wave_lds_sync();
 
+    FAST_STAMP(4, __builtin_amdgcn_s_memtime());
     const int which = n_ini > 0 ? 0 : 1;
     const int total = which == 0 ? n_ini : n_min;
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
@@ -481,8 +511,11 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     }
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
-        cell_cnt[(long long)f * g.ncells_total + blockIdx.x] = min(total, cap);
+        cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap);
     }
+    FAST_STAMP(5, __builtin_amdgcn_s_memtime());
+    FAST_STAMP(6, ((unsigned long long)cell.level << 48) | ((unsigned long long)nc << 16) | (unsigned)total);
+    FAST_STAMP(7, ((unsigned long long)f << 32) | (unsigned)ci);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1050,8 +1083,9 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     __shared__ __attribute__((aligned(16))) uint8_t R[PATCH * RS];
     __shared__ __attribute__((aligned(16))) uint16_t Hb[PATCH * HBLUR_W];
     const int lane = threadIdx.x;
-    const int f = blockIdx.y;
-    const int s = blockIdx.x;
+    const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int f = lb / gridDim.x;
+    const int s = lb % gridDim.x;
     const int* cnt = sel_cnt + f * g.nlevels;
     if (s == 0 && lane == 0) {
         int tot = 0;
@@ -1743,6 +1777,19 @@ int orbx_debug_qt_sort(const int32_t* sizes, int n, int32_t* perm) {
     d.release();
     for (int i = 0; i < n; i++) perm[i] = h[i].node;
     return ORB_OK;
+}
+
+int orbx_debug_fast_stamps(unsigned long long* out, int n_words) {
+#ifdef ORB_FAST_STAMPS
+    ORB_CHECK_ARG(out && n_words > 0 && n_words <= FAST_NSAMP * 8, "bad stamp buffer");
+    ORB_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_stamps), (size_t)n_words * 8));
+    return ORB_OK;
+#else
+    (void)out;
+    (void)n_words;
+    set_error("built without ORB_FAST_STAMPS");
+    return ORB_EINVAL;
+#endif
 }
 
 int orbx_debug_qt_stamps(unsigned long long* out) {
