@@ -321,11 +321,81 @@ __device__ unsigned long long g_fast_stamps[FAST_NSAMP * 8];
 #define FAST_STAMP(k, v) do {} while (0)
 #endif
 
-__global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
+// Crop staging.  LDS dword mm of crop row r holds crop cols 4mm-1 .. 4mm+2 (col c at byte c+1), i.e.
+// the 4 image bytes starting at q = (y0+r)*step + x0 - 1 + 4mm, built with v_alignbyte from the two
+// dword-aligned image words around q.  The (row, dword) pairs are walked flat over the wave's 64
+// lanes; the first CROP_PF*64 of them are loaded into registers one cell ahead (the loads of cell
+// i+1 are in flight while cell i is processed), the rest (cells wider or taller than ~40 px) are
+// loaded and stored synchronously.
+constexpr int CROP_PF = 8;
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+struct CropWalk {
+    int row, mm, dr, dm, ndl;
+    __device__ __forceinline__ CropWalk(int lane, int ndl_) : ndl(ndl_) {
+        row = lane / ndl;
+        mm = lane - row * ndl;
+        dr = 64 / ndl;
+        dm = 64 - dr * ndl;
+    }
+    __device__ __forceinline__ void next() {
+        row += dr;
+        mm += dm;
+        if (mm >= ndl) { mm -= ndl; row++; }
+    }
+};
+
+struct CropSrc {
+    const uint8_t* img;   // level base of the frame (wave-uniform)
+    int step, x0, y0, ch, ndl;
+    __device__ __forceinline__ int q(const CropWalk& w) const { return (y0 + w.row) * step + x0 - 1 + 4 * w.mm; }
+    __device__ __forceinline__ int mis(int q) const {
+        return (int)(((uint32_t)reinterpret_cast<uintptr_t>(img) + (uint32_t)q) & 3u);
+    }
+    __device__ __forceinline__ u32x2a4 load(int q) const {
+        return *reinterpret_cast<const u32x2a4*>(img + (q - mis(q)));
+    }
+};
+
+__device__ __forceinline__ void crop_prefetch(const CropSrc& c, int lane, u32x2a4 (&v)[CROP_PF]) {
+    CropWalk w(lane, c.ndl);
+#pragma unroll
+    for (int it = 0; it < CROP_PF; it++) {   // unconditional (row clamped): straight-line loads
+        CropWalk wc = w;
+        wc.row = min(w.row, c.ch - 1);
+        v[it] = c.load(c.q(wc));
+        w.next();
+    }
+}
+
+__device__ __forceinline__ void crop_commit(const CropSrc& c, int lane, const u32x2a4 (&v)[CROP_PF], uint8_t* crop,
+                                            int CSd) {
+    CropWalk w(lane, c.ndl);
+#pragma unroll
+    for (int it = 0; it < CROP_PF; it++) {
+        if (w.row < c.ch) {
+            const int q = c.q(w);
+            reinterpret_cast<uint32_t*>(crop + w.row * CSd)[w.mm] = __builtin_amdgcn_alignbyte(v[it].y, v[it].x, c.mis(q));
+        }
+        w.next();
+    }
+    while (w.row < c.ch) {   // rare: crops larger than CROP_PF*64 dwords
+        const int q = c.q(w);
+        const u32x2a4 t = c.load(q);
+        reinterpret_cast<uint32_t*>(crop + w.row * CSd)[w.mm] = __builtin_amdgcn_alignbyte(t.y, t.x, c.mis(q));
+        w.next();
+    }
+}
+
+// One wavefront processes `cpw` consecutive (frame, cell) items of the XCD-swizzled order; item
+// i = f * ncells + cell.  LDS (sized per launch from the largest cell): the crop (zone + 3-px
+// apron), a zone map of corner strengths, a queue of pre-test passers and the ordered corner list.
+__global__ __launch_bounds__(64, 5) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
-                                                        int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl) {
+                                                        int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
+                                                        int n_items, int cpw) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -336,61 +406,43 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
 
     const int lane = threadIdx.x;
     const unsigned long long lt = lanemask_lt();
-    const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int lb = xcd_swizzle(blockIdx.x, gridDim.x);
     FAST_STAMP(0, __builtin_amdgcn_s_memtime());
-    const int ci = lb % gridDim.x;
-    const CellDev cell = cells[ci];
-    const int f = lb / gridDim.x;
-    const int x0 = cell.x0y0 & 0xffff, y0 = cell.x0y0 >> 16;
-    const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
-    const int cw = zw + 6, ch = zh + 6;
-    int step;
-    const uint8_t* img = level_base(g, cell.level, f, in, in_fstride, in_step, pyr, &step);
+    const int i_beg = lb * cpw, i_end = min(i_beg + cpw, n_items);
+    const int ncells = g.ncells_total;
 
-    // 1. crop: LDS dword m of a crop row holds crop cols 4m-1 .. 4m+2 (col c at byte c+1), built from
-    //    two aligned global dwords with v_alignbyte; all loads of a lane are issued together.
-    {
-        const int m = lane & 15, rr = lane >> 4;
-        const int ndl = (cw + 1 + 3) >> 2;   // LDS dwords per crop row (<= 18)
-        constexpr int NB = 5;                // row iterations per batch (20 rows)
-        for (int rb = 0; rb < ch; rb += 4 * NB) {
-            uint32_t lo[NB][2], hi[NB][2];
-            int sh[NB];
-#pragma unroll
-            for (int it = 0; it < NB; it++) {
-                const int r = rb + rr + 4 * it;
-                sh[it] = 0;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    lo[it][h] = hi[it][h] = 0;
-                    const int mm = m + 16 * h;
-                    if (r < ch && mm < ndl) {
-                        const uintptr_t addr = reinterpret_cast<uintptr_t>(img + (long long)(y0 + r) * step + x0);
-                        const int e = (int)(addr & 3) - 1;   // global byte of crop col -1, relative to addr & ~3
-                        const uint32_t* a0 = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
-                        const int k = mm + (e < 0 ? -1 : 0);
-                        lo[it][h] = a0[k];
-                        hi[it][h] = a0[k + 1];
-                        sh[it] = e & 3;
-                    }
-                }
-            }
-#pragma unroll
-            for (int it = 0; it < NB; it++) {
-                const int r = rb + rr + 4 * it;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int mm = m + 16 * h;
-                    if (r < ch && mm < ndl)
-                        reinterpret_cast<uint32_t*>(crop + r * CSd)[mm] =
-                            __builtin_amdgcn_alignbyte(hi[it][h], lo[it][h], sh[it]);
-                }
-            }
-        }
-        for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
+    auto source = [&](int item, CellDev& cd, int& f, int& ci) {
+        f = item / ncells;
+        ci = item - f * ncells;
+        cd = cells[ci];
+        CropSrc c;
+        c.img = level_base(g, cd.level, f, in, in_fstride, in_step, pyr, &c.step);
+        c.x0 = cd.x0y0 & 0xffff;
+        c.y0 = cd.x0y0 >> 16;
+        c.ch = (cd.zwzh >> 16) + 6;
+        c.ndl = ((cd.zwzh & 0xffff) + 6 + 1 + 3) >> 2;   // LDS dwords per crop row
+        return c;
+    };
+    CellDev cell;
+    int f, ci;
+    CropSrc src = source(i_beg, cell, f, ci);
+    u32x2a4 pre[CROP_PF];
+    crop_prefetch(src, lane, pre);
+
+    for (int item = i_beg; item < i_end; item++) {
+    const int x0 = src.x0, y0 = src.y0;
+    const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
+    crop_commit(src, lane, pre, crop, CSd);
+    for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
+    wave_lds_sync();
+    if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
+    CellDev ncell;
+    int nf = f, nci = ci;
+    CropSrc nsrc = src;
+    if (item + 1 < i_end) {
+        nsrc = source(item + 1, ncell, nf, nci);
+        crop_prefetch(nsrc, lane, pre);
     }
-    __syncthreads();
-    FAST_STAMP(1, __builtin_amdgcn_s_memtime());
 
     const int tlo = min(th_ini, th_min);
     const us2 t2 = {(unsigned short)tlo, (unsigned short)tlo};
@@ -449,7 +501,6 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     }
     if (qn > 0) drain(qn);
     wave_lds_sync();
-    FAST_STAMP(2, __builtin_amdgcn_s_memtime());
 
     // corner strengths into the zone map
     for (int j = lane; j < nc; j += 64) {
@@ -457,7 +508,6 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
         Mz[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(corner_strength(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd), 255);
     }
     wave_lds_sync();
-    FAST_STAMP(3, __builtin_amdgcn_s_memtime());
 
     auto nms = [&](int zy, int zx, int m, int t) -> bool {
         if (m <= t) return false;
@@ -490,7 +540,6 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
     }
     wave_lds_sync();
 
-    FAST_STAMP(4, __builtin_amdgcn_s_memtime());
     const int which = n_ini > 0 ? 0 : 1;
     const int total = which == 0 ? n_ini : n_min;
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
@@ -513,9 +562,18 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const CellDev* _
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
         cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap);
     }
+    if (item == i_beg) {
+        FAST_STAMP(2, __builtin_amdgcn_s_memtime());
+        FAST_STAMP(6, ((unsigned long long)cell.level << 48) | ((unsigned long long)nc << 16) | (unsigned)total);
+    }
+    wave_lds_sync();
+    cell = ncell;
+    f = nf;
+    ci = nci;
+    src = nsrc;
+    }   // items
     FAST_STAMP(5, __builtin_amdgcn_s_memtime());
-    FAST_STAMP(6, ((unsigned long long)cell.level << 48) | ((unsigned long long)nc << 16) | (unsigned)total);
-    FAST_STAMP(7, ((unsigned long long)f << 32) | (unsigned)ci);
+    FAST_STAMP(7, (unsigned long long)(i_end - i_beg));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1212,6 +1270,10 @@ struct orbx_extractor {
     size_t qt_lds = 0;
     FastLds fl;
     size_t fast_lds = 0;
+    int fast_cpw = 4;   // FAST cells per wavefront (crop loads pipelined one cell ahead)
+    int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
+    std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
+    hipEvent_t fork_ev = nullptr;
     DevBuf d_cells, d_xtab, d_ytab;
 
     // workspace for up to ws_frames frames
@@ -1458,6 +1520,8 @@ static hipEvent_t prof_event(orbx_extractor* h) {
     return e;
 }
 
+constexpr int ORBX_MIN_SUB_FRAMES = 16;
+
 struct StageMark {
     orbx_extractor* h;
     hipStream_t st;
@@ -1478,10 +1542,23 @@ struct StageMark {
     }
 };
 
-static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long long fstride, int step,
-                        orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st) {
+// All four stages for frames [f0, f0 + F) of the workspace, enqueued on st.  Every kernel indexes
+// its per-frame buffers from the frame index within the launch, so a chunk is launched with base
+// pointers advanced by f0 frames.
+static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F, long long fstride, int step,
+                         orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st) {
     const Geom& g = h->geom;
-    uint8_t* pyr = h->d_pyr.as<uint8_t>();
+    uint8_t* pyr = h->d_pyr.as<uint8_t>() + (long long)f0 * g.pyr_frame_bytes;
+    d_imgs += (long long)f0 * fstride;
+    d_kps += (long long)f0 * cap;
+    d_desc += (long long)f0 * cap * 32;
+    d_counts += f0;
+    uint32_t* slots = h->d_slots.as<uint32_t>() + (long long)f0 * g.slot_frame;
+    int* cellcnt = h->d_cellcnt.as<int>() + (long long)f0 * g.ncells_total;
+    uint32_t* Pb = h->d_P.as<uint32_t>() + (long long)f0 * g.cand_frame;
+    uint32_t* Tb = h->d_T.as<uint32_t>() + (long long)f0 * g.cand_frame;
+    uint32_t* sel = h->d_sel.as<uint32_t>() + (long long)f0 * g.out_frame;
+    int* selcnt = h->d_selcnt.as<int>() + (long long)f0 * g.nlevels;
     {
     StageMark m0(h, st, 0);
     for (int l = 1; l < g.nlevels; l++) {
@@ -1494,22 +1571,53 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
     uint32_t* fault = h->d_fault.as<uint32_t>();
     if (g.ncells_total > 0) {
         StageMark m1(h, st, 1);
-        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)g.ncells_total, (unsigned)F), dim3(64), h->fast_lds, st,
+        const int n_items = g.ncells_total * F;
+        const int cpw = h->fast_cpw;
+        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)((n_items + cpw - 1) / cpw)), dim3(64), h->fast_lds, st,
                            g, h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
-                           h->p.minThFAST, h->d_slots.as<uint32_t>(), h->d_cellcnt.as<int>(), fault, h->fl);
+                           h->p.minThFAST, slots, cellcnt, fault, h->fl,
+                           n_items, cpw);
     }
     {
     StageMark m2(h, st, 2);
     hipLaunchKernelGGL(quadtree_kernel, dim3((unsigned)F, (unsigned)g.nlevels), dim3(256), h->qt_lds, st, g,
-                       h->d_cellcnt.as<int>(), h->d_slots.as<uint32_t>(), h->d_cells.as<CellDev>(),
-                       h->d_P.as<uint32_t>(), h->d_T.as<uint32_t>(), h->d_sel.as<uint32_t>(), h->d_selcnt.as<int>(),
-                       h->NC, h->PTC, fault);
+                       cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault);
     }
     {
     StageMark m3(h, st, 3);
     hipLaunchKernelGGL(describe_kernel, dim3((unsigned)g.out_frame, (unsigned)F), dim3(64), 0, st, g,
-                       d_imgs, fstride, step, pyr, h->d_sel.as<uint32_t>(), h->d_selcnt.as<int>(), d_kps, d_desc,
-                       d_counts, cap);
+                       d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
+    }
+}
+
+// Frames are split into sub-batches on the handle's side streams (fork/join with events on st) so
+// that one sub-batch's latency-bound stages (the short pyramid levels, the quadtree's level-0 tail)
+// overlap another's FAST / describe work.
+static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long long fstride, int step,
+                        orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st) {
+    int nsub = std::min(h->nsub, F / ORBX_MIN_SUB_FRAMES);
+    if (nsub <= 1) {
+        launch_chunk(h, 0, d_imgs, F, fstride, step, d_kps, d_desc, d_counts, cap, st);
+        ORB_HIP_TRY(hipGetLastError());
+        return ORB_OK;
+    }
+    while ((int)h->sub.size() < nsub) {
+        hipStream_t s2;
+        ORB_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        hipEvent_t e;
+        ORB_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        h->sub.push_back({s2, e});
+    }
+    if (!h->fork_ev) ORB_HIP_TRY(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+    ORB_HIP_TRY(hipEventRecord(h->fork_ev, st));
+    int f0 = 0;
+    for (int i = 0; i < nsub; i++) {
+        const int Fi = F / nsub + (i < F % nsub ? 1 : 0);
+        ORB_HIP_TRY(hipStreamWaitEvent(h->sub[i].first, h->fork_ev, 0));
+        launch_chunk(h, f0, d_imgs, Fi, fstride, step, d_kps, d_desc, d_counts, cap, h->sub[i].first);
+        ORB_HIP_TRY(hipEventRecord(h->sub[i].second, h->sub[i].first));
+        ORB_HIP_TRY(hipStreamWaitEvent(st, h->sub[i].second, 0));
+        f0 += Fi;
     }
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
@@ -1539,6 +1647,8 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     orbx_extractor* h = new orbx_extractor();
     h->p = *params;
     h->device = device;
+    if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
+    if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     compute_tables(h);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1561,6 +1671,8 @@ int orbx_destroy(orbx_extractor* h) {
         for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    for (auto& se : h->sub) { (void)hipStreamDestroy(se.first); (void)hipEventDestroy(se.second); }
+    if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
     delete h;
     return ORB_OK;
 }

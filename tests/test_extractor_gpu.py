@@ -140,3 +140,25 @@ def test_batch_device_matches_single(oracle):
         n = int(cnt[i])
         kps = ORBextractor.kps_to_numpy(kps_all[i, :n])
         assert_same_kps(kps, okps, desc_all[i, :n], odesc)
+
+
+@pytest.mark.parametrize("nsub,cpw", [(1, 1), (2, 4), (3, 3)])
+def test_batch_sub_streams_and_cells_per_wave(monkeypatch, nsub, cpw):
+    """Sub-batches on side streams (ORBX_NSUB) and the FAST cells-per-wave pipelining
+    (ORBX_FAST_CPW) must not change a bit of the output; 50 frames -> ragged chunks."""
+    import torch
+    frames = np.stack([synth_image(100 + (i % 7), 320, 240) for i in range(50)])
+    t = torch.from_numpy(frames).cuda()
+    ref = make(500).extract_batch_device(t)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("ORBX_NSUB", str(nsub))
+    monkeypatch.setenv("ORBX_FAST_CPW", str(cpw))
+    out = make(500).extract_batch_device(t)
+    torch.cuda.synchronize()
+    cnt = ref[2].cpu().numpy()
+    assert np.array_equal(cnt, out[2].cpu().numpy())
+    k0, k1 = ref[0].cpu().numpy(), out[0].cpu().numpy()
+    d0, d1 = ref[1].cpu().numpy(), out[1].cpu().numpy()
+    for i, n in enumerate(cnt):
+        assert np.array_equal(k0[i, :n], k1[i, :n]), i
+        assert np.array_equal(d0[i, :n], d1[i, :n]), i

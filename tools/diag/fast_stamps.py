@@ -1,5 +1,4 @@
-"""Diagnostic: per-phase s_memtime stamps of sampled FAST waves (ORB_FAST_STAMPS build).
-Phases: 0 start, 1 crop in LDS, 2 compass + full tests, 3 strengths, 4 NMS, 5 end."""
+"""Diagnostic: s_memtime stamps of sampled FAST waves (ORB_FAST_STAMPS build): 0 wave start, 1 first\ncrop in LDS, 2 first item done, 5 wave end; 6 first item level/corners; 7 items in the wave."""
 import ctypes as C
 import os
 import sys
@@ -27,22 +26,16 @@ fn.argtypes = [C.c_void_p, C.c_int]
 assert fn(C.cast(buf, C.c_void_p), N * 8) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(N, 8).astype(np.int64)
 a = a[a[:, 5] > 0]
-t = a[:, :6] - a[:, :1].min()
+t = a[:, :6] - a[:, :1]
 lvl = (a[:, 6] >> 48) & 0xffff
 nc = (a[:, 6] >> 16) & 0xffffffff
-span = t[:, 5].max() - t[:, 0].min()
-print(f"sampled waves {len(a)}, kernel span {span} ticks, mean wave life {np.mean(t[:, 5] - t[:, 0]):.0f}")
-names = ["crop", "compass+full", "strength", "nms", "emit"]
+nit = a[:, 7]
+print(f"sampled waves {len(a)}, items/wave {nit.mean():.2f}, mean wave life {t[:, 5].mean():.0f} ticks")
+print(f"first crop (unhidden load) {t[:, 1].mean():.0f}, first item body {np.mean(t[:, 2] - t[:, 1]):.0f}")
+m = nit > 1
+if m.any():
+    print(f"later items: {np.mean((t[m, 5] - t[m, 2]) / (nit[m] - 1)):.0f} ticks per item (crop prefetched)")
 for L in range(int(lvl.max()) + 1):
-    m = lvl == L
-    if not m.any():
-        continue
-    d = np.diff(t[m], axis=1).mean(axis=0)
-    print(f"level {L}: n {m.sum():5d} corners {nc[m].mean():6.1f} " + " ".join(f"{k} {v:7.0f}" for k, v in zip(names, d)))
-d = np.diff(t, axis=1).mean(axis=0)
-print("all     : " + " ".join(f"{k} {v:7.0f}" for k, v in zip(names, d)))
-# concurrency: waves alive over time
-ts = np.sort(t[:, 0]); te = np.sort(t[:, 5])
-grid = np.linspace(0, span, 20)
-alive = [(np.searchsorted(ts, x) - np.searchsorted(te, x)) * 64 for x in grid]
-print("est. waves alive over kernel (x64 sampling):", [int(v) for v in alive])
+    k = lvl == L
+    if k.any():
+        print(f"level {L}: n {k.sum():5d} corners {nc[k].mean():6.1f} crop {t[k, 1].mean():7.0f} body {np.mean(t[k, 2] - t[k, 1]):7.0f}")
