@@ -497,123 +497,212 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// Reduced camera system solve + pose update.  Blocked LDL^T by 6x6 pose blocks in LDS
-// (right-looking: diagonal block in registers, panel, trailing lower-triangle update; three
-// barriers per block column), triangular solves on wavefront 0 with the right-hand side in
-// registers, then push() + SE3Quat::exp(dx) * pose for every free pose (+ its scale term).
-// Stands in for g2o's SimplicialLDLT (linear_solver_eigen.h:94-124): same factorisation up to
-// rounding order.  D <= 132 (22 free keyframes).
-__global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
-    extern __shared__ __attribute__((aligned(16))) double A[];
-    __shared__ double dblk[6];
-    __shared__ int s_ok;
-    const int NB = D / 6;
-    {
-        const double2* S2 = reinterpret_cast<const double2*>(b.S);
-        double2* A2 = reinterpret_cast<double2*>(A);
-        const int n2 = (D * D) / 2;   // D is even
-        for (int i0 = threadIdx.x; i0 < n2; i0 += 4 * blockDim.x) {
-            double2 r[4];
+// Reduced camera system solve + pose update: right-looking blocked LDL^T of the (6P)^2 system in
+// LDS, padded with identity to Dp = 16*ceil(D/16) so every block is a full 16 columns (the padded
+// unknowns solve to 0).  Row stride Dp+1 (odd) keeps column walks bank-conflict free.  The forward
+// substitution is carried along; back substitution is blocked.  Per block J:
+//   (1) wavefront 0: LDL^T of the 16x16 diagonal block in registers (lane i owns row i, pivot rows
+//       broadcast with v_readlane, branch-free), z_J, and Linv_JJ = L_JJ^-1 (kept in the unused upper
+//       triangle of the block: Linv[j][k] at (k, j));
+//   (2) panel, one thread per row: U_iJ = A_iJ Linv_JJ^T (= L_iJ D_J) as independent dot products;
+//       y_i -= L_iJ z_J;
+//   (3) trailing A_ik -= U_iJ D_J^-1 U_kJ^T on the lower triangle: thread (ty, tx) of a 16x16 grid
+//       owns rows R0+ty+16a, columns R0+tx+16c (c <= a), so a wavefront walks 16 consecutive rows.
+constexpr int SB = 16;
+
+#ifdef ORB_BA_STAMPS
+__device__ unsigned long long g_ba_stamps[64];
+#define BA_STAMP(k)                                                                              \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && (k) < 64) g_ba_stamps[(k)] = __builtin_amdgcn_s_memtime();       \
+    } while (0)
+#else
+#define BA_STAMP(k) do {} while (0)
+#endif
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__host__ __device__ constexpr int solve_dp(int D) { return (D + SB - 1) / SB * SB; }
+__host__ __device__ constexpr size_t solve_lds_doubles(int D) {
+    return (size_t)solve_dp(D) * (solve_dp(D) + 1) + 2 * (size_t)solve_dp(D);
+}
+
+__device__ __forceinline__ double rcp_d(double d) {   // 1/d to ~1 ulp: v_rcp_f64 + two Newton steps
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
+// A_ik -= sum_j U_ij dinv_j U_kj for the NBK x NBK lower block-triangle below block J.
+template <int NBK>
+__device__ __forceinline__ void trailing_update(double* A, const double* dinv, int ld, int J0, int R0, int tid) {
+    const int ty = tid >> 4, tx = tid & 15;
+    double acc[NBK][NBK];
 #pragma unroll
-            for (int q = 0; q < 4; q++) r[q] = i0 + q * (int)blockDim.x < n2 ? S2[i0 + q * blockDim.x] : make_double2(0, 0);
+    for (int a = 0; a < NBK; a++)
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (i0 + q * (int)blockDim.x < n2) A2[i0 + q * blockDim.x] = r[q];
+        for (int c = 0; c < NBK; c++) acc[a][c] = 0;
+    const double* wrow = A + (R0 + ty) * ld + J0;
+    const double* lrow = A + (R0 + tx) * ld + J0;
+#pragma unroll 4
+    for (int j = 0; j < SB; j++) {
+        const double dj = dinv[J0 + j];
+        double wi[NBK], lk[NBK];
+#pragma unroll
+        for (int a = 0; a < NBK; a++) {
+            wi[a] = wrow[SB * a * ld + j];
+            lk[a] = lrow[SB * a * ld + j] * dj;
         }
+#pragma unroll
+        for (int a = 0; a < NBK; a++)
+#pragma unroll
+            for (int c = 0; c <= a; c++) acc[a][c] = fma(wi[a], lk[c], acc[a][c]);
     }
-    if (threadIdx.x == 0) s_ok = 1;
+#pragma unroll
+    for (int a = 0; a < NBK; a++)
+#pragma unroll
+        for (int c = 0; c <= a; c++) A[(R0 + ty + SB * a) * ld + R0 + tx + SB * c] -= acc[a][c];
+}
+
+__global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
+    extern __shared__ __attribute__((aligned(16))) double A[];   // Dp x ld
+    const int Dp = solve_dp(D), ld = Dp + 1;
+    double* y = A + (size_t)Dp * ld;   // rhs -> z -> D^-1 z -> x
+    double* dinv = y + Dp;
+    __shared__ double part[256];
+    __shared__ int s_ok;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int e = tid; e < Dp * Dp; e += blockDim.x) {
+        const int r = e / Dp, c = e - r * Dp;
+        A[r * ld + c] = (r < D && c < D) ? b.S[r * D + c] : (r == c ? 1.0 : 0.0);
+    }
+    for (int i = tid; i < Dp; i += blockDim.x) y[i] = i < D ? b.bs[i] : 0.0;
+    if (tid == 0) s_ok = 1;
     __syncthreads();
-    for (int J = 0; J < NB; J++) {
-        const int j0 = 6 * J;
-        if (threadIdx.x == 0) {   // (1) diagonal block, in registers
-            double a[6][6];
+    BA_STAMP(0);
+    for (int J0 = 0; J0 < Dp; J0 += SB) {
+        const int R0 = J0 + SB;
+        if (wv == 0) {   // (1) diagonal block
+            const int i = lane & (SB - 1);
+            double r[SB];
 #pragma unroll
-            for (int i = 0; i < 6; i++)
+            for (int k = 0; k < SB; k++) r[k] = A[(J0 + max(i, k)) * ld + J0 + min(i, k)];
+            double yi = y[J0 + i];
+            bool ok = true;
 #pragma unroll
-                for (int k = 0; k < 6; k++) a[i][k] = k <= i ? A[(j0 + i) * D + j0 + k] : 0.0;
-            double d[6];
-            int ok = 1;
+            for (int j = 0; j < SB; j++) {
+                const double dj = readlane_d(r[j], j);
+                ok = ok && dj != 0 && isfinite(dj);
+                const double l = i > j ? r[j] * rcp_d(dj) : 0.0;
+                const double yj = readlane_d(yi, j);
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                double dj = a[j][j];
-#pragma unroll
-                for (int k = 0; k < j; k++) dj -= a[j][k] * a[j][k] * d[k];
-                ok &= (dj != 0 && isfinite(dj)) ? 1 : 0;
-                d[j] = dj;
-#pragma unroll
-                for (int i = j + 1; i < 6; i++) {
-                    double sum = a[i][j];
-#pragma unroll
-                    for (int k = 0; k < j; k++) sum -= a[i][k] * a[j][k] * d[k];
-                    a[i][j] = sum / dj;
-                }
+                for (int k = j + 1; k < SB; k++) r[k] = fma(-l, readlane_d(r[k], j), r[k]);
+                yi = fma(-l, yj, yi);
+                r[j] = i > j ? l : r[j];
             }
+            double di = r[0];
 #pragma unroll
-            for (int i = 0; i < 6; i++) {
+            for (int k = 1; k < SB; k++) di = k == i ? r[k] : di;
+            if (lane < SB) {
 #pragma unroll
-                for (int k = 0; k < i; k++) A[(j0 + i) * D + j0 + k] = a[i][k];
-                A[(j0 + i) * D + j0 + i] = d[i];
-                dblk[i] = d[i];
+                for (int k = 0; k < SB - 1; k++)
+                    if (k < i) A[(J0 + i) * ld + J0 + k] = r[k];
+                dinv[J0 + i] = rcp_d(di);
+                y[J0 + i] = yi;
             }
-            if (!ok) s_ok = 0;
+            if (lane == 0 && !ok) s_ok = 0;
+            wave_lds_sync();
+            BA_STAMP(44 + J0 / SB);
+            // Linv column c = lane: x_c = 1, x_j = -sum_{m<j} L_jm x_m (x_m = 0 for m < c)
+            const int c = i;
+            double x[SB];
+#pragma unroll
+            for (int j = 0; j < SB; j++) {
+                double sum = 0;
+#pragma unroll
+                for (int m = 0; m < j; m++) sum = fma(A[(J0 + j) * ld + J0 + m], x[m], sum);
+                x[j] = j < c ? 0.0 : (j == c ? 1.0 : -sum);
+            }
+            if (lane < SB) {
+#pragma unroll
+                for (int j = 1; j < SB; j++)
+                    if (j > c) A[(J0 + c) * ld + J0 + j] = x[j];
+            }
         }
         __syncthreads();
+        BA_STAMP(1 + 3 * (J0 / SB));
         if (!s_ok) break;
-        // (2) panel: rows below solve  L_IJ D_J L_JJ^T = A_IJ  (one row per thread)
-        for (int i = j0 + 6 + threadIdx.x; i < D; i += blockDim.x) {
-            double x[6];
+        // (2) panel, one thread per row below the block
+        for (int i = R0 + tid; i < Dp; i += blockDim.x) {
+            double a[SB];
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                double sum = A[i * D + j0 + j];
+            for (int k = 0; k < SB; k++) a[k] = A[i * ld + J0 + k];
+            double ysum = 0;
 #pragma unroll
-                for (int k = 0; k < j; k++) sum -= x[k] * dblk[k] * A[(j0 + j) * D + j0 + k];
-                x[j] = sum / dblk[j];
+            for (int j = 0; j < SB; j++) {
+                double v = a[j];
+#pragma unroll
+                for (int k = 0; k < j; k++) v = fma(A[(J0 + k) * ld + J0 + j], a[k], v);
+                ysum = fma(v * dinv[J0 + j], y[J0 + j], ysum);
+                A[i * ld + J0 + j] = v;
             }
-#pragma unroll
-            for (int j = 0; j < 6; j++) A[i * D + j0 + j] = x[j];
+            y[i] -= ysum;
         }
         __syncthreads();
-        // (3) trailing update of the lower triangle: A_ik -= sum_j (L_ij d_j) L_kj, j in block J
-        {
-            const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
-            for (int i = j0 + 6 + ty; i < D; i += 16) {
-                double li[6];
-#pragma unroll
-                for (int j = 0; j < 6; j++) li[j] = A[i * D + j0 + j] * dblk[j];
-                for (int k = j0 + 6 + tx; k <= i; k += 16) {
-                    const double* lk = A + k * D + j0;
-                    A[i * D + k] -= li[0] * lk[0] + li[1] * lk[1] + li[2] * lk[2] + li[3] * lk[3] + li[4] * lk[4] +
-                                    li[5] * lk[5];
-                }
-            }
+        BA_STAMP(2 + 3 * (J0 / SB));
+        // (3) trailing update of the lower triangle (row-block count as a template parameter so the
+        //     j loop is straight-line code with all loads of an iteration in flight together)
+        switch ((Dp - R0) / SB) {
+            case 1: trailing_update<1>(A, dinv, ld, J0, R0, tid); break;
+            case 2: trailing_update<2>(A, dinv, ld, J0, R0, tid); break;
+            case 3: trailing_update<3>(A, dinv, ld, J0, R0, tid); break;
+            case 4: trailing_update<4>(A, dinv, ld, J0, R0, tid); break;
+            case 5: trailing_update<5>(A, dinv, ld, J0, R0, tid); break;
+            case 6: trailing_update<6>(A, dinv, ld, J0, R0, tid); break;
+            case 7: trailing_update<7>(A, dinv, ld, J0, R0, tid); break;
+            default: break;
         }
         __syncthreads();
+        BA_STAMP(3 + 3 * (J0 / SB));
     }
     const int ok = s_ok;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        // right-hand side in registers: lane holds rows lane and lane + 64
-        double v0 = lane < D ? b.bs[lane] : 0.0, v1 = lane + 64 < D ? b.bs[lane + 64] : 0.0;
-        if (ok) {
-            for (int j = 0; j < D; j++) {   // L y = b
-                const double yj = j < 64 ? readlane_d(v0, j) : readlane_d(v1, j - 64);
-                if (lane > j && lane < D) v0 -= A[lane * D + j] * yj;
-                if (lane + 64 > j && lane + 64 < D) v1 -= A[(lane + 64) * D + j] * yj;
+    if (ok) {
+        for (int i = tid; i < Dp; i += blockDim.x) y[i] *= dinv[i];   // D^-1 z
+        __syncthreads();
+        // back substitution, last block first: t_J = z'_J - (U_IJ D_J^-1)^T x_I, x_J = Linv_JJ^T t_J
+        for (int J0 = Dp - SB; J0 >= 0; J0 -= SB) {
+            const int R0 = J0 + SB;
+            {
+                const int c = tid & 15, g = tid >> 4;
+                double sum = 0;
+                for (int i = R0 + g; i < Dp; i += 16) sum = fma(A[i * ld + J0 + c], y[i], sum);
+                part[tid] = sum;
             }
-            if (lane < D) v0 /= A[lane * D + lane];
-            if (lane + 64 < D) v1 /= A[(lane + 64) * D + lane + 64];
-            for (int j = D - 1; j >= 0; j--) {   // L^T x = y
-                const double xj = j < 64 ? readlane_d(v0, j) : readlane_d(v1, j - 64);
-                if (lane < j) v0 -= A[j * D + lane] * xj;
-                if (lane + 64 < j) v1 -= A[j * D + lane + 64] * xj;
+            __syncthreads();
+            if (wv == 0) {
+                const int c = lane & (SB - 1);
+                double tot = 0;
+#pragma unroll
+                for (int g = 0; g < 16; g++) tot += part[g * 16 + c];
+                const double tc = y[J0 + c] - tot * dinv[J0 + c];
+                double xc = tc;   // Linv unit diagonal
+#pragma unroll
+                for (int j = 1; j < SB; j++) {
+                    const double tj = readlane_d(tc, j);
+                    const double lv = A[(J0 + min(c, j)) * ld + J0 + j];   // Linv[j][c] for j > c
+                    xc = j > c ? fma(lv, tj, xc) : xc;
+                }
+                wave_lds_sync();
+                if (lane < SB) y[J0 + c] = xc;
             }
-        } else {
-            v0 = v1 = 0;
+            __syncthreads();
         }
-        if (lane < D) b.x[lane] = v0;
-        if (lane + 64 < D) b.x[lane + 64] = v1;
-        if (lane == 0) b.ctl->ok2 = ok;
     }
+    BA_STAMP(40);
+    for (int i = tid; i < D; i += blockDim.x) b.x[i] = ok ? y[i] : 0.0;
+    if (tid == 0) b.ctl->ok2 = ok;
     __syncthreads();
     // push() + oplus for the free poses, scale terms x.(lambda x + b)
     const double lam = b.ctl->lambda;
@@ -959,7 +1048,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         *iters_out = 0;
         *chi_out = 0;
         if (Ea == 0 || np + nl == 0) return ORB_OK;
-        if (D > 128 || (size_t)D * D * 8 > 150 * 1024) {
+        if (D > 128 || solve_lds_doubles(D) * 8 + 4096 > 160 * 1024) {
             set_error("LocalBA: too many free keyframes for the in-LDS reduced-system solve (max 21)");
             return ORB_EINVAL;
         }
@@ -1028,7 +1117,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.part = cy.take<double>(nl + np);
         ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
-        const size_t ldlt_lds = std::max<size_t>((size_t)D * D * 8, 16);
+        const size_t ldlt_lds = std::max<size_t>(solve_lds_doubles(D) * 8, 16);
         ORB_HIP_TRY(hipFuncSetAttribute((const void*)ba_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)std::max<size_t>(ldlt_lds, 1024)));
         const dim3 gg((nl * 8 + 63) / 64);   // 8 lanes per point
@@ -1096,4 +1185,16 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (res->pose_q) std::memcpy(res->pose_q + 4 * i, &qh[4 * i], 32);
     }
     return ORB_OK;
+}
+
+extern "C" int orbba_debug_stamps(unsigned long long* out) {
+#ifdef ORB_BA_STAMPS
+    ORB_HIP_TRY(hipDeviceSynchronize());
+    ORB_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ba_stamps), 64 * 8));
+    return ORB_OK;
+#else
+    (void)out;
+    set_error("built without ORB_BA_STAMPS");
+    return ORB_EINVAL;
+#endif
 }

@@ -1,0 +1,31 @@
+"""Diagnostic: phase stamps of the LocalBA solve kernel (ORB_BA_STAMPS build), last launch."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+os.environ["ORBSLAM2_AMD_LIB"] = str(ROOT / "tools" / "diag" / "liborbslam2_amd_bastamps.so")
+sys.path.insert(0, str(ROOT))
+from orb_slam2_refactored_amd._lib import lib  # noqa: E402
+from orb_slam2_refactored_amd.optimizer import LocalBundleAdjustment  # noqa: E402
+from orb_slam2_refactored_amd.synth import make_ba_problem  # noqa: E402
+
+pr = make_ba_problem(0)
+for _ in range(3):
+    LocalBundleAdjustment(pr)
+buf = (C.c_ulonglong * 64)()
+f = lib().orbba_debug_stamps
+f.argtypes = [C.c_void_p]
+assert f(C.cast(buf, C.c_void_p)) == 0
+v = list(buf)
+t0 = v[0]
+prev = t0
+for blk in range(13):
+    a, b_, c = v[1 + 3 * blk], v[2 + 3 * blk], v[3 + 3 * blk]
+    if a == 0:
+        break
+    f = v[44 + blk]
+    print(f"block {blk}: diag {a - prev:6d} (factor {f - prev:6d}, Linv {a - f:6d}) panel {b_ - a:6d} trailing {c - b_:6d}")
+    prev = c
+print(f"back-substitution {v[40] - prev}, total {v[40] - t0} ticks")
