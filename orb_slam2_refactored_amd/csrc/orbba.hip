@@ -30,7 +30,18 @@ struct BACtl {
     double lambda, ni, cur, ini, tmp, scale, rho;
     int ok2, accepted;
     double maxdiag;
+    // LM loop state, advanced on the device by ba_decide_kernel (g2o SparseOptimizer::optimize +
+    // OptimizationAlgorithmLevenberg::solve): iteration, trial within it, nBad, flags
+    int it, q, nbad, done, need_lin, iters_max, iters_done, pad;
+    double chi_out;
 };
+
+// Every kernel of an LM step returns at once when the loop has finished (steps are enqueued ahead
+// of the host learning that); the linearisation kernels also skip on a retry trial.
+#define BA_RETURN_IF_DONE(b) \
+    do {                     \
+        if ((b).ctl->done) return; \
+    } while (0)
 
 // ------------------------------------------------------------------ SE3 helpers (se3quat.h)
 struct Q4 { double x, y, z, w; };
@@ -226,6 +237,7 @@ constexpr int GRP = 8;   // lanes per point
 // and constructQuadraticForm of every active edge (types_six_dof_expmap.cpp:103-139,188-234;
 // base_binary_edge.hpp:54-120), Hll / b_l summed per point, pose parts stored per edge.
 __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
+    if (b.ctl->done || !b.ctl->need_lin) return;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = t / GRP, sub = t % GRP;
     const bool live = l < b.nl;
@@ -339,6 +351,7 @@ __device__ double block_sum_1024(const double* v, int n, double* sh) {
 // four interleaved accumulators each, combined in a fixed order.  Block np: chi2 total.
 constexpr int PA_G = 24;
 __global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b, int set_ini) {
+    if (b.ctl->done || !b.ctl->need_lin) return;
     __shared__ double sh[1024];
     const int i = blockIdx.x;
     if (i == b.np) {
@@ -374,6 +387,7 @@ __global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b, int set_in
 
 // computeLambdaInit (levenberg.cpp:166-180): tau * max |diag H| over active vertices.
 __global__ __launch_bounds__(256) void ba_lambda_init_kernel(BADev b) {
+    if (b.ctl->done || !b.ctl->need_lin || b.ctl->it != 0) return;
     __shared__ double sh[256];
     double m = 0;
     for (int i = threadIdx.x; i < 6 * b.np; i += blockDim.x) m = fmax(m, fabs(b.Hpp[36 * (i / 6) + 7 * (i % 6)]));
@@ -405,6 +419,7 @@ __device__ __forceinline__ bool inv3(const double* m, double* o) {
 // BlockSolver::solve, landmark part (block_solver.hpp:377-419): every lane of a point's group
 // forms D^-1 (same values), each lane handles its edges' W = Hpl D^-1 and Hpl D^-1 b_l.
 __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
+    BA_RETURN_IF_DONE(b);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = t / GRP, sub = t % GRP;
     if (l >= b.nl) return;
@@ -434,6 +449,7 @@ __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
 // fixed-order combine.  Diagonal blocks also form b_schur = b_p - sum Hpl D^-1 b_l.
 constexpr int SB_G = 28;
 __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D) {
+    BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
     const int blk = blockIdx.x;
     const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
@@ -496,6 +512,21 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     const int hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+template <int J>
+__device__ __forceinline__ double row_bcast_t(double v);
+// j must fold to a constant after unrolling (it does inside the fully unrolled loops below)
+__device__ __forceinline__ double row_bcast_d(double v, int j) {
+    switch (j) {
+        case 0: return row_bcast_t<0>(v);   case 1: return row_bcast_t<1>(v);
+        case 2: return row_bcast_t<2>(v);   case 3: return row_bcast_t<3>(v);
+        case 4: return row_bcast_t<4>(v);   case 5: return row_bcast_t<5>(v);
+        case 6: return row_bcast_t<6>(v);   case 7: return row_bcast_t<7>(v);
+        case 8: return row_bcast_t<8>(v);   case 9: return row_bcast_t<9>(v);
+        case 10: return row_bcast_t<10>(v); case 11: return row_bcast_t<11>(v);
+        case 12: return row_bcast_t<12>(v); case 13: return row_bcast_t<13>(v);
+        case 14: return row_bcast_t<14>(v); default: return row_bcast_t<15>(v);
+    }
+}
 
 // Reduced camera system solve + pose update: right-looking blocked LDL^T of the (6P)^2 system in
 // LDS, padded with identity to Dp = 16*ceil(D/16) so every block is a full 16 columns (the padded
@@ -522,9 +553,20 @@ __device__ unsigned long long g_ba_stamps[64];
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// Value of lane J of each 16-lane row (DPP row_newbcast), for a double.
+template <int J>
+__device__ __forceinline__ double row_bcast_t(double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffff), 0x150 + J, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x150 + J, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __host__ __device__ constexpr int solve_dp(int D) { return (D + SB - 1) / SB * SB; }
 __host__ __device__ constexpr size_t solve_lds_doubles(int D) {
-    return (size_t)solve_dp(D) * (solve_dp(D) + 1) + 2 * (size_t)solve_dp(D);
+    return (size_t)solve_dp(D) * (solve_dp(D) + 1) + 3 * (size_t)solve_dp(D);
 }
 
 __device__ __forceinline__ double rcp_d(double d) {   // 1/d to ~1 ulp: v_rcp_f64 + two Newton steps
@@ -566,140 +608,226 @@ __device__ __forceinline__ void trailing_update(double* A, const double* dinv, i
         for (int c = 0; c <= a; c++) A[(R0 + ty + SB * a) * ld + R0 + tx + SB * c] -= acc[a][c];
 }
 
+// (1) of the solve, split over two wavefronts that run concurrently:
+//   solve_diag_factor (wavefront 0): LDL^T of diagonal block J0 in registers (lane i owns row i, pivot
+//     rows broadcast with DPP row_newbcast; every 16-lane row holds the same copy) and the forward
+//     substitution z_J.  After pivot step m it stores column m of L and raises flag[0] = m + 1.
+//   solve_diag_inverse (wavefront 1): Linv_JJ = L_JJ^-1 column by column (lane c), right-looking, each
+//     step m as soon as column m of L is out; then v_J = Linv^T D^-1 z_J for the panel's rhs update.
+//     Linv[j][k] is kept at (k, j), the block's unused upper triangle.
+__device__ __forceinline__ int lds_flag_read(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
+
+__device__ __forceinline__ bool solve_diag_factor(double* A, double* y, double* dinv, int ld, int J0, int lane,
+                                                  int* flag, int nreal) {
+    const int i = lane & (SB - 1);
+    double r[SB];
+#pragma unroll
+    for (int k = 0; k < SB; k++) r[k] = A[(J0 + max(i, k)) * ld + J0 + min(i, k)];
+    double yi = y[J0 + i];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < SB; j++) {
+        if (j < nreal) {   // past nreal: identity padding, nothing left to eliminate (uniform)
+            const double dj = row_bcast_d(r[j], j);
+            ok = ok && dj != 0 && isfinite(dj);
+            const double l = i > j ? r[j] * rcp_d(dj) : 0.0;
+            if (lane < SB && i > j) A[(J0 + i) * ld + J0 + j] = l;   // column j of L
+            const double yj = row_bcast_d(yi, j);
+#pragma unroll
+            for (int k = j + 1; k < SB; k++) r[k] = fma(-l, row_bcast_d(r[k], j), r[k]);
+            yi = fma(-l, yj, yi);
+            r[j] = i > j ? l : r[j];
+        }
+        if (j < SB - 1) {   // a wavefront's LDS operations execute in order: no wait needed here
+            asm volatile("" ::: "memory");
+            if (lane == 0) __atomic_store_n(flag, j + 1, __ATOMIC_RELAXED);
+        }
+    }
+    double di = r[0];
+#pragma unroll
+    for (int k = 1; k < SB; k++) di = k == i ? r[k] : di;
+    if (lane < SB) {
+        dinv[J0 + i] = rcp_d(di);
+        y[J0 + i] = yi;
+    }
+    wave_lds_sync();
+    if (lane == 0) __atomic_store_n(flag, SB, __ATOMIC_RELAXED);   // dinv, z_J out as well
+    return ok;
+}
+
+__device__ __forceinline__ void solve_diag_inverse(double* A, const double* y, const double* dinv, double* vz,
+                                                   int ld, int J0, int lane, const int* flag, int nreal) {
+    const int c = lane & (SB - 1);
+    double x[SB];
+#pragma unroll
+    for (int m = 0; m < SB; m++) x[m] = 0;
+#pragma unroll
+    for (int m = 0; m < SB - 1; m++) {
+        const double xm = m < c ? 0.0 : (m == c ? 1.0 : -x[m]);
+        x[m] = xm;
+        if (m < nreal) {   // padded columns of L are zero
+            while (lds_flag_read(flag) < m + 1) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int j = m + 1; j < SB; j++) x[j] = fma(A[(J0 + j) * ld + J0 + m], xm, x[j]);
+        }
+    }
+    x[SB - 1] = (SB - 1) < c ? 0.0 : ((SB - 1) == c ? 1.0 : -x[SB - 1]);
+    while (lds_flag_read(flag) < SB) __builtin_amdgcn_s_sleep(1);
+    double v = 0;   // v_c = sum_{j>=c} Linv[j][c] dinv_j z_j
+#pragma unroll
+    for (int j = 0; j < SB; j++) v = fma(x[j], dinv[J0 + j] * y[J0 + j], v);
+    if (lane < SB) {
+#pragma unroll
+        for (int j = 1; j < SB; j++)
+            if (j > c) A[(J0 + c) * ld + J0 + j] = x[j];
+        vz[J0 + c] = v;
+    }
+}
+
+// One 16x16 tile of the trailing update: A[i0.., k0..] -= U_I D_J^-1 U_K^T (v_mfma_f64_16x16x4).
+__device__ __forceinline__ void solve_trailing_tile(double* A, int ld, int J0, int i0, int k0, int col, int kq,
+                                                    const double (&dk)[4]) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) {
+        av[s2] = A[(i0 + col) * ld + J0 + 4 * s2 + kq];
+        bv[s2] = A[(k0 + col) * ld + J0 + 4 * s2 + kq] * dk[s2];
+    }
+    d4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], bv[s2], acc, 0, 0, 0);
+    const double u[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int r2 = 0; r2 < 4; r2++) A[(i0 + kq + 4 * r2) * ld + k0 + col] -= u[r2];
+}
+
+// Schedule per block J (one barrier each after the panel and after the trailing step):
+//   panel J (all waves) | wavefront 0: trailing tile (J+1, J+1), then the diagonal block J+1
+//   (lookahead), while wavefronts 1-3 update every other trailing tile.
+// Back substitution runs on wavefront 0 alone: x_J = Linv_JJ^T t_J, then t_c -= sum_i L_ic x_i for
+// all earlier columns c (right-looking), block by block from the last.
 __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
+    BA_RETURN_IF_DONE(b);
     extern __shared__ __attribute__((aligned(16))) double A[];   // Dp x ld
     const int Dp = solve_dp(D), ld = Dp + 1;
     double* y = A + (size_t)Dp * ld;   // rhs -> z -> D^-1 z -> x
     double* dinv = y + Dp;
-    __shared__ double part[256];
+    double* vz = dinv + Dp;
     __shared__ int s_ok;
+    __shared__ int s_flag;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int col = lane & 15, kq = lane >> 4;
     for (int e = tid; e < Dp * Dp; e += blockDim.x) {
         const int r = e / Dp, c = e - r * Dp;
         A[r * ld + c] = (r < D && c < D) ? b.S[r * D + c] : (r == c ? 1.0 : 0.0);
     }
     for (int i = tid; i < Dp; i += blockDim.x) y[i] = i < D ? b.bs[i] : 0.0;
-    if (tid == 0) s_ok = 1;
+    if (tid == 0) {
+        s_ok = 1;
+        s_flag = 0;
+    }
     __syncthreads();
     BA_STAMP(0);
-    for (int J0 = 0; J0 < Dp; J0 += SB) {
+    if (wv == 0) {
+        if (!solve_diag_factor(A, y, dinv, ld, 0, lane, &s_flag, D) && lane == 0) s_ok = 0;
+    } else if (wv == 1) {
+        solve_diag_inverse(A, y, dinv, vz, ld, 0, lane, &s_flag, D);
+    }
+    __syncthreads();
+    for (int J0 = 0; J0 < Dp && s_ok; J0 += SB) {
         const int R0 = J0 + SB;
-        if (wv == 0) {   // (1) diagonal block
-            const int i = lane & (SB - 1);
-            double r[SB];
-#pragma unroll
-            for (int k = 0; k < SB; k++) r[k] = A[(J0 + max(i, k)) * ld + J0 + min(i, k)];
-            double yi = y[J0 + i];
-            bool ok = true;
-#pragma unroll
-            for (int j = 0; j < SB; j++) {
-                const double dj = readlane_d(r[j], j);
-                ok = ok && dj != 0 && isfinite(dj);
-                const double l = i > j ? r[j] * rcp_d(dj) : 0.0;
-                const double yj = readlane_d(yi, j);
-#pragma unroll
-                for (int k = j + 1; k < SB; k++) r[k] = fma(-l, readlane_d(r[k], j), r[k]);
-                yi = fma(-l, yj, yi);
-                r[j] = i > j ? l : r[j];
-            }
-            double di = r[0];
-#pragma unroll
-            for (int k = 1; k < SB; k++) di = k == i ? r[k] : di;
-            if (lane < SB) {
-#pragma unroll
-                for (int k = 0; k < SB - 1; k++)
-                    if (k < i) A[(J0 + i) * ld + J0 + k] = r[k];
-                dinv[J0 + i] = rcp_d(di);
-                y[J0 + i] = yi;
-            }
-            if (lane == 0 && !ok) s_ok = 0;
-            wave_lds_sync();
-            BA_STAMP(44 + J0 / SB);
-            // Linv column c = lane: x_c = 1, x_j = -sum_{m<j} L_jm x_m (x_m = 0 for m < c)
-            const int c = i;
-            double x[SB];
-#pragma unroll
-            for (int j = 0; j < SB; j++) {
-                double sum = 0;
-#pragma unroll
-                for (int m = 0; m < j; m++) sum = fma(A[(J0 + j) * ld + J0 + m], x[m], sum);
-                x[j] = j < c ? 0.0 : (j == c ? 1.0 : -sum);
-            }
-            if (lane < SB) {
-#pragma unroll
-                for (int j = 1; j < SB; j++)
-                    if (j > c) A[(J0 + c) * ld + J0 + j] = x[j];
-            }
-        }
-        __syncthreads();
+        const int nbk = (Dp - R0) / SB;
         BA_STAMP(1 + 3 * (J0 / SB));
-        if (!s_ok) break;
-        // (2) panel, one thread per row below the block
-        for (int i = R0 + tid; i < Dp; i += blockDim.x) {
-            double a[SB];
+        if (nbk == 0) break;
+        if (tid == 0) s_flag = 0;   // read by wavefront 1 only after the panel's barrier
+        // (2) panel U_I = A_IJ Linv^T per 16-row tile (MFMA); rhs y_i -= A_iJ v with v = Linv^T D^-1 z_J
+        if (wv < nbk) {
+            double binv[4], bvz[4];
 #pragma unroll
-            for (int k = 0; k < SB; k++) a[k] = A[i * ld + J0 + k];
-            double ysum = 0;
-#pragma unroll
-            for (int j = 0; j < SB; j++) {
-                double v = a[j];
-#pragma unroll
-                for (int k = 0; k < j; k++) v = fma(A[(J0 + k) * ld + J0 + j], a[k], v);
-                ysum = fma(v * dinv[J0 + j], y[J0 + j], ysum);
-                A[i * ld + J0 + j] = v;
+            for (int s2 = 0; s2 < 4; s2++) {
+                const int k = 4 * s2 + kq;
+                const double v = A[(J0 + min(k, col)) * ld + J0 + max(k, col)];
+                binv[s2] = col > k ? v : (col == k ? 1.0 : 0.0);
             }
-            y[i] -= ysum;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++) bvz[s2] = col == 0 ? vz[J0 + 4 * s2 + kq] : 0.0;   // B = [v | 0]
+            for (int t = wv; t < nbk; t += 4) {
+                const int i0 = R0 + SB * t;
+                double av[4];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) av[s2] = A[(i0 + col) * ld + J0 + 4 * s2 + kq];
+                d4 acc = {0, 0, 0, 0}, accy = {0, 0, 0, 0};
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) {
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], binv[s2], acc, 0, 0, 0);
+                    accy = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], bvz[s2], accy, 0, 0, 0);
+                }
+                const double u[4] = {acc.x, acc.y, acc.z, acc.w};
+                const double uy[4] = {accy.x, accy.y, accy.z, accy.w};
+#pragma unroll
+                for (int r2 = 0; r2 < 4; r2++) {
+                    const int row = i0 + kq + 4 * r2;
+                    A[row * ld + J0 + col] = u[r2];
+                    if (col == 0) y[row] -= uy[r2];
+                }
+            }
         }
         __syncthreads();
         BA_STAMP(2 + 3 * (J0 / SB));
-        // (3) trailing update of the lower triangle (row-block count as a template parameter so the
-        //     j loop is straight-line code with all loads of an iteration in flight together)
-        switch ((Dp - R0) / SB) {
-            case 1: trailing_update<1>(A, dinv, ld, J0, R0, tid); break;
-            case 2: trailing_update<2>(A, dinv, ld, J0, R0, tid); break;
-            case 3: trailing_update<3>(A, dinv, ld, J0, R0, tid); break;
-            case 4: trailing_update<4>(A, dinv, ld, J0, R0, tid); break;
-            case 5: trailing_update<5>(A, dinv, ld, J0, R0, tid); break;
-            case 6: trailing_update<6>(A, dinv, ld, J0, R0, tid); break;
-            case 7: trailing_update<7>(A, dinv, ld, J0, R0, tid); break;
-            default: break;
+        // (3) trailing update with lookahead
+        {
+            double dk[4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++) dk[s2] = dinv[J0 + 4 * s2 + kq];
+            if (wv == 0) {
+                solve_trailing_tile(A, ld, J0, R0, R0, col, kq, dk);
+                wave_lds_sync();
+                if (!solve_diag_factor(A, y, dinv, ld, R0, lane, &s_flag, D - R0) && lane == 0) s_ok = 0;
+            } else if (wv == 1) {
+                solve_diag_inverse(A, y, dinv, vz, ld, R0, lane, &s_flag, D - R0);
+            } else {
+                const int ntile = nbk * (nbk + 1) / 2;
+                for (int t = wv - 1; t < ntile; t += 2) {   // tile 0 = (J+1, J+1) belongs to wavefront 0
+                    int I = 0;
+                    while ((I + 1) * (I + 2) / 2 <= t) I++;
+                    const int K = t - I * (I + 1) / 2;
+                    solve_trailing_tile(A, ld, J0, R0 + SB * I, R0 + SB * K, col, kq, dk);
+                }
+            }
         }
         __syncthreads();
         BA_STAMP(3 + 3 * (J0 / SB));
     }
     const int ok = s_ok;
-    if (ok) {
-        for (int i = tid; i < Dp; i += blockDim.x) y[i] *= dinv[i];   // D^-1 z
-        __syncthreads();
-        // back substitution, last block first: t_J = z'_J - (U_IJ D_J^-1)^T x_I, x_J = Linv_JJ^T t_J
+    if (ok && wv == 0) {
+        for (int i = lane; i < Dp; i += 64) y[i] *= dinv[i];   // t = D^-1 z
+        wave_lds_sync();
         for (int J0 = Dp - SB; J0 >= 0; J0 -= SB) {
-            const int R0 = J0 + SB;
-            {
-                const int c = tid & 15, g = tid >> 4;
-                double sum = 0;
-                for (int i = R0 + g; i < Dp; i += 16) sum = fma(A[i * ld + J0 + c], y[i], sum);
-                part[tid] = sum;
-            }
-            __syncthreads();
-            if (wv == 0) {
-                const int c = lane & (SB - 1);
-                double tot = 0;
+            // x_J = Linv_JJ^T t_J: x_c = t_c + sum_{j>c} Linv[j][c] t_j (four partial sums)
+            double xp[4] = {y[J0 + col], 0, 0, 0};
 #pragma unroll
-                for (int g = 0; g < 16; g++) tot += part[g * 16 + c];
-                const double tc = y[J0 + c] - tot * dinv[J0 + c];
-                double xc = tc;   // Linv unit diagonal
-#pragma unroll
-                for (int j = 1; j < SB; j++) {
-                    const double tj = readlane_d(tc, j);
-                    const double lv = A[(J0 + min(c, j)) * ld + J0 + j];   // Linv[j][c] for j > c
-                    xc = j > c ? fma(lv, tj, xc) : xc;
-                }
-                wave_lds_sync();
-                if (lane < SB) y[J0 + c] = xc;
+            for (int j = 1; j < SB; j++) {
+                const double lv = A[(J0 + min(col, j)) * ld + J0 + j];   // Linv[j][col] for j > col
+                xp[j & 3] = j > col ? fma(lv, y[J0 + j], xp[j & 3]) : xp[j & 3];
             }
-            __syncthreads();
+            const double xc = (xp[0] + xp[1]) + (xp[2] + xp[3]);
+            wave_lds_sync();
+            if (lane < SB) y[J0 + col] = xc;
+            wave_lds_sync();
+            // t_c -= sum_{i in J} L_ic x_i, L_ic = U_ic dinv_c, for all earlier columns c < J0
+            double xj[SB];
+#pragma unroll
+            for (int k = 0; k < SB; k++) xj[k] = y[J0 + k];
+            for (int c = lane; c < J0; c += 64) {
+                double sp[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < SB; k++) sp[k & 3] = fma(A[(J0 + k) * ld + c], xj[k], sp[k & 3]);
+                y[c] = fma(-((sp[0] + sp[1]) + (sp[2] + sp[3])), dinv[c], y[c]);
+            }
+            wave_lds_sync();
         }
     }
+    __syncthreads();
     BA_STAMP(40);
     for (int i = tid; i < D; i += blockDim.x) b.x[i] = ok ? y[i] : 0.0;
     if (tid == 0) b.ctl->ok2 = ok;
@@ -720,6 +848,7 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
 // Back-substitution xl = Dinv (bl - Hpl^T xp), push(), point +=, scale term, then the errors and
 // robust chi2 of the point's edges at the new estimate (computeActiveErrors after update()).
 __global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D) {
+    BA_RETURN_IF_DONE(b);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = t / GRP, sub = t % GRP;
     const bool live = l < b.nl;
@@ -777,7 +906,8 @@ __global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D) {
 }
 
 // levenberg.cpp:120-147 — sums, accept / reject, lambda / nu update, pop() on reject.
-__global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b) {
+__global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b, BACtl* host_snap) {
+    BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
     __shared__ int s_acc;
     const double tmp_sum = block_sum_1024(b.rchi, b.nl, sh);
@@ -804,6 +934,31 @@ __global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b) {
             c->accepted = 0;
         }
         s_acc = c->accepted;
+        // trial / iteration bookkeeping (host loop of levenberg solve + SparseOptimizer::optimize;
+        // the force-stop flag is applied by the host between steps)
+        c->q += 1;
+        if (rho < 0 && c->q < 10) {
+            c->need_lin = 0;   // retry with the new lambda
+        } else {
+            c->iters_done += 1;
+            c->chi_out = c->cur;
+            bool term = c->q == 10 || rho == 0;
+            if (!term) {
+                if ((c->ini - c->cur) * 1e3 < c->ini) c->nbad++;
+                else c->nbad = 0;
+                term = c->nbad >= 3;
+            }
+            c->it += 1;
+            if (c->it >= c->iters_max) term = true;
+            if (term) c->done = 1;
+            else {
+                c->need_lin = 1;
+                c->q = 0;
+            }
+        }
+        // control snapshot straight into pinned host memory (no copy on the stream)
+        *host_snap = *c;
+        __threadfence_system();
     }
     __syncthreads();
     if (s_acc) return;
@@ -820,6 +975,21 @@ __global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b) {
 }
 
 // final outlier classification (Optimizer.cc:644-670, :686-699) + chi2 out
+__global__ void ba_ctl_start_kernel(BADev b, int iters) {
+    BACtl* c = b.ctl;
+    c->it = 0;
+    c->q = 0;
+    c->nbad = 0;
+    c->done = iters <= 0 ? 1 : 0;
+    c->need_lin = 1;
+    c->iters_max = iters;
+    c->iters_done = 0;
+    c->chi_out = 0;
+    c->rho = 0;
+}
+
+__global__ void ba_ctl_stop_kernel(BADev b) { b.ctl->done = 1; }
+
 __global__ void ba_classify_kernel(BADev b, uint8_t* outlier, double* chi2o, uint8_t* level, int set_level) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= b.E) return;
@@ -843,13 +1013,39 @@ using namespace orbamd;
 
 namespace {
 
+// Grow-only pinned host buffer.  Only grown when no copy from it is in flight.
+struct PinnedBuf {
+    char* ptr = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return ORB_OK;
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+        const size_t c = align_up(bytes + bytes / 4, 1 << 16);
+        ORB_HIP_TRY(hipHostMalloc((void**)&ptr, c, hipHostMallocDefault));
+        cap = c;
+        return ORB_OK;
+    }
+    ~PinnedBuf() {
+        if (ptr) (void)hipHostFree(ptr);
+    }
+};
+
 // Device-resident LocalBA workspace (one per thread: LocalMapping runs one LocalBA at a time).
 struct BAContext {
     int device = -1;
     hipStream_t st = nullptr;
     DevBuf prob, state, structure, sys, ctlbuf;
     BACtl* h_ctl = nullptr;   // pinned
+    BACtl* h_ring = nullptr;  // pinned, device-mapped control snapshots, one per step in flight
+    BACtl* d_ring = nullptr;
+    hipEvent_t ring_ev[2] = {nullptr, nullptr};
+    PinnedBuf h_prob, h_struct, h_res;   // pinned staging images (one copy each way)
     ~BAContext() {
+        if (h_ring) (void)hipHostFree(h_ring);
+        for (hipEvent_t e : ring_ev)
+            if (e) (void)hipEventDestroy(e);
         prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (st) (void)hipStreamDestroy(st);
@@ -950,6 +1146,12 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (C.st) (void)hipStreamDestroy(C.st);
         ORB_HIP_TRY(hipStreamCreateWithFlags(&C.st, hipStreamNonBlocking));
         if (!C.h_ctl) ORB_HIP_TRY(hipHostMalloc((void**)&C.h_ctl, sizeof(BACtl), hipHostMallocDefault));
+        if (!C.h_ring) {
+            ORB_HIP_TRY(hipHostMalloc((void**)&C.h_ring, 2 * sizeof(BACtl), hipHostMallocMapped));
+            ORB_HIP_TRY(hipHostGetDevicePointer((void**)&C.d_ring, C.h_ring, 0));
+        }
+        for (hipEvent_t& e : C.ring_ev)
+            if (!e) ORB_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         C.device = device;
     }
     ORB_HIP_TRY(hipSetDevice(device));
@@ -984,20 +1186,25 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (n > 0) { x /= n; y /= n; z /= n; w /= n; }
         q0[4 * i] = x; q0[4 * i + 1] = y; q0[4 * i + 2] = z; q0[4 * i + 3] = w;
     }
-    std::vector<uint8_t> stereo(E);
-    for (int e = 0; e < E; e++) stereo[e] = pr->edge_obs[3 * e + 2] < 0 ? 0 : 1;   // ur < 0 => mono (:595)
 
-    // ---- device problem + state
-    const size_t prob_bytes = carve_size<uint8_t>(P) + carve_size<int>(E) * 2 + carve_size<uint8_t>(E) +
-                              carve_size<double>(3 * (size_t)E) + carve_size<double>(E) + carve_size<double>(5 * (size_t)E);
-    const size_t state_bytes = carve_size<double>(4 * (size_t)P) * 2 + carve_size<double>(3 * (size_t)P) * 2 +
-                               carve_size<double>(3 * (size_t)N) * 2 + carve_size<uint8_t>(E) * 3 +
+    // ---- device problem + state.  Everything the host provides is laid out in one region, built
+    // in pinned staging with the same offsets and uploaded with a single copy.
+    const size_t up_bytes = carve_size<uint8_t>(P) + carve_size<int>(E) * 2 + carve_size<uint8_t>(E) +
+                            carve_size<double>(3 * (size_t)E) + carve_size<double>(E) +
+                            carve_size<double>(5 * (size_t)E) + carve_size<double>(4 * (size_t)P) +
+                            carve_size<double>(3 * (size_t)P) + carve_size<double>(3 * (size_t)N);
+    const size_t state_bytes = carve_size<double>(4 * (size_t)P) + carve_size<double>(3 * (size_t)P) +
+                               carve_size<double>(3 * (size_t)N) + carve_size<uint8_t>(E) * 3 +
                                carve_size<double>(3 * (size_t)E) + carve_size<double>(E);
+    const size_t res_bytes = carve_size<double>(4 * (size_t)P) + carve_size<double>(3 * (size_t)P) +
+                             carve_size<double>(3 * (size_t)N) + carve_size<uint8_t>(E) + carve_size<double>(E);
     int rc;
-    if ((rc = C.prob.reserve(prob_bytes))) return rc;
+    if ((rc = C.prob.reserve(up_bytes))) return rc;
     if ((rc = C.state.reserve(state_bytes))) return rc;
     if ((rc = C.ctlbuf.reserve(sizeof(BACtl) + 64))) return rc;
-    Carve cp{C.prob.as<char>()}, cs{C.state.as<char>()};
+    if ((rc = C.h_prob.ensure(up_bytes))) return rc;
+    if ((rc = C.h_res.ensure(res_bytes))) return rc;
+    Carve cp{C.prob.as<char>()}, hp{C.h_prob.ptr}, cs{C.state.as<char>()};
     BADev b;
     std::memset(&b, 0, sizeof(b));
     b.P = P; b.N = N; b.E = E;
@@ -1008,9 +1215,25 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     double* d_obs = cp.take<double>(3 * (size_t)E);
     double* d_info = cp.take<double>(E);
     double* d_cam = cp.take<double>(5 * (size_t)E);
-    b.q = cs.take<double>(4 * (size_t)P); b.q_sv = cs.take<double>(4 * (size_t)P);
-    b.t = cs.take<double>(3 * (size_t)P); b.t_sv = cs.take<double>(3 * (size_t)P);
-    b.X = cs.take<double>(3 * (size_t)N); b.X_sv = cs.take<double>(3 * (size_t)N);
+    b.q = cp.take<double>(4 * (size_t)P);
+    b.t = cp.take<double>(3 * (size_t)P);
+    b.X = cp.take<double>(3 * (size_t)N);
+    {
+        std::memcpy(hp.take<uint8_t>(P), pr->pose_fixed, P);
+        std::memcpy(hp.take<int>(E), pr->edge_point, 4 * (size_t)E);
+        std::memcpy(hp.take<int>(E), pr->edge_pose, 4 * (size_t)E);
+        uint8_t* hst = hp.take<uint8_t>(E);
+        for (int e = 0; e < E; e++) hst[e] = pr->edge_obs[3 * e + 2] < 0 ? 0 : 1;   // ur < 0 => mono (:595)
+        std::memcpy(hp.take<double>(3 * (size_t)E), pr->edge_obs, 24 * (size_t)E);
+        std::memcpy(hp.take<double>(E), pr->edge_inv_sigma2, 8 * (size_t)E);
+        std::memcpy(hp.take<double>(5 * (size_t)E), pr->edge_cam, 40 * (size_t)E);
+        std::memcpy(hp.take<double>(4 * (size_t)P), q0.data(), 32 * (size_t)P);
+        std::memcpy(hp.take<double>(3 * (size_t)P), pr->pose_t, 24 * (size_t)P);
+        std::memcpy(hp.take<double>(3 * (size_t)N), pr->points, 24 * (size_t)N);
+    }
+    b.q_sv = cs.take<double>(4 * (size_t)P);
+    b.t_sv = cs.take<double>(3 * (size_t)P);
+    b.X_sv = cs.take<double>(3 * (size_t)N);
     b.robust = cs.take<uint8_t>(E);
     uint8_t* d_level = cs.take<uint8_t>(E);
     uint8_t* d_outl = cs.take<uint8_t>(E);
@@ -1018,19 +1241,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     double* d_chi = cs.take<double>(E);
     b.fixed = d_fixed; b.ep = d_ep; b.ek = d_ek; b.stereo = d_st; b.obs = d_obs; b.info = d_info; b.cam = d_cam;
     b.ctl = C.ctlbuf.as<BACtl>();
-    if (P) {
-        ORB_HIP_TRY(hipMemcpyAsync(d_fixed, pr->pose_fixed, P, hipMemcpyHostToDevice, st));
-        ORB_HIP_TRY(hipMemcpyAsync(b.q, q0.data(), 32 * (size_t)P, hipMemcpyHostToDevice, st));
-        ORB_HIP_TRY(hipMemcpyAsync(b.t, pr->pose_t, 24 * (size_t)P, hipMemcpyHostToDevice, st));
-    }
-    if (N) ORB_HIP_TRY(hipMemcpyAsync(b.X, pr->points, 24 * (size_t)N, hipMemcpyHostToDevice, st));
+    ORB_HIP_TRY(hipMemcpyAsync(C.prob.ptr, C.h_prob.ptr, cp.off, hipMemcpyHostToDevice, st));
     if (E) {
-        ORB_HIP_TRY(hipMemcpyAsync(d_ep, pr->edge_point, 4 * (size_t)E, hipMemcpyHostToDevice, st));
-        ORB_HIP_TRY(hipMemcpyAsync(d_ek, pr->edge_pose, 4 * (size_t)E, hipMemcpyHostToDevice, st));
-        ORB_HIP_TRY(hipMemcpyAsync(d_st, stereo.data(), E, hipMemcpyHostToDevice, st));
-        ORB_HIP_TRY(hipMemcpyAsync(d_obs, pr->edge_obs, 24 * (size_t)E, hipMemcpyHostToDevice, st));
-        ORB_HIP_TRY(hipMemcpyAsync(d_info, pr->edge_inv_sigma2, 8 * (size_t)E, hipMemcpyHostToDevice, st));
-        ORB_HIP_TRY(hipMemcpyAsync(d_cam, pr->edge_cam, 40 * (size_t)E, hipMemcpyHostToDevice, st));
         ORB_HIP_TRY(hipMemsetAsync(b.robust, 1, E, st));
         ORB_HIP_TRY(hipMemsetAsync(d_level, 0, E, st));
         ORB_HIP_TRY(hipMemsetAsync(b.err, 0, 24 * (size_t)E, st));
@@ -1059,10 +1271,10 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                               carve_size<int>(nblk + 1) + carve_size<int2>(hs.blk_pair.size());
         int rc2;
         if ((rc2 = C.structure.reserve(sbytes))) return rc2;
-        Carve cr{C.structure.as<char>()};
-        auto up = [&](const void* src, size_t n, char* dst) -> int {
-            if (n) ORB_HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
-            return ORB_OK;
+        if ((rc2 = C.h_struct.ensure(sbytes))) return rc2;   // previous optimize() has synchronised
+        Carve cr{C.structure.as<char>()}, hr{C.h_struct.ptr};
+        auto put = [&](const void* src, size_t n, char* hdst) {
+            if (n) std::memcpy(hdst, src, n);
         };
         int* d_act = cr.take<int>(Ea);
         int* d_hp = cr.take<int>(P);
@@ -1077,19 +1289,20 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         int* d_b2 = cr.take<int>(nblk);
         int* d_bb = cr.take<int>(nblk + 1);
         int2* d_bp = cr.take<int2>(hs.blk_pair.size());
-        if ((rc2 = up(hs.act.data(), 4 * (size_t)Ea, (char*)d_act))) return rc2;
-        if ((rc2 = up(hs.hp.data(), 4 * (size_t)P, (char*)d_hp))) return rc2;
-        if ((rc2 = up(hs.hl.data(), 4 * (size_t)N, (char*)d_hl))) return rc2;
-        if ((rc2 = up(hs.pt_beg.data(), 4 * (size_t)(nl + 1), (char*)d_ptb))) return rc2;
-        if ((rc2 = up(hs.pt_slot.data(), 4 * (size_t)Ea, (char*)d_pts))) return rc2;
-        if ((rc2 = up(hs.pt_id.data(), 4 * (size_t)nl, (char*)d_pti))) return rc2;
-        if ((rc2 = up(hs.ps_beg.data(), 4 * (size_t)(np + 1), (char*)d_psb))) return rc2;
-        if ((rc2 = up(hs.ps_slot.data(), 4 * hs.ps_slot.size(), (char*)d_pss))) return rc2;
-        if ((rc2 = up(hs.ps_id.data(), 4 * (size_t)np, (char*)d_psi))) return rc2;
-        if ((rc2 = up(hs.blk_i1.data(), 4 * (size_t)nblk, (char*)d_b1))) return rc2;
-        if ((rc2 = up(hs.blk_i2.data(), 4 * (size_t)nblk, (char*)d_b2))) return rc2;
-        if ((rc2 = up(hs.blk_beg.data(), 4 * (size_t)(nblk + 1), (char*)d_bb))) return rc2;
-        if ((rc2 = up(hs.blk_pair.data(), 8 * hs.blk_pair.size(), (char*)d_bp))) return rc2;
+        put(hs.act.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
+        put(hs.hp.data(), 4 * (size_t)P, (char*)hr.take<int>(P));
+        put(hs.hl.data(), 4 * (size_t)N, (char*)hr.take<int>(N));
+        put(hs.pt_beg.data(), 4 * (size_t)(nl + 1), (char*)hr.take<int>(nl + 1));
+        put(hs.pt_slot.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
+        put(hs.pt_id.data(), 4 * (size_t)nl, (char*)hr.take<int>(nl));
+        put(hs.ps_beg.data(), 4 * (size_t)(np + 1), (char*)hr.take<int>(np + 1));
+        put(hs.ps_slot.data(), 4 * hs.ps_slot.size(), (char*)hr.take<int>(hs.ps_slot.size()));
+        put(hs.ps_id.data(), 4 * (size_t)np, (char*)hr.take<int>(np));
+        put(hs.blk_i1.data(), 4 * (size_t)nblk, (char*)hr.take<int>(nblk));
+        put(hs.blk_i2.data(), 4 * (size_t)nblk, (char*)hr.take<int>(nblk));
+        put(hs.blk_beg.data(), 4 * (size_t)(nblk + 1), (char*)hr.take<int>(nblk + 1));
+        put(hs.blk_pair.data(), 8 * hs.blk_pair.size(), (char*)hr.take<int2>(hs.blk_pair.size()));
+        ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, cr.off, hipMemcpyHostToDevice, st));
         b.Ea = Ea; b.np = np; b.nl = nl; b.nblk = nblk;
         b.act = d_act; b.hp = d_hp; b.hl = d_hl; b.pt_beg = d_ptb; b.pt_slot = d_pts; b.pt_id = d_pti;
         b.ps_beg = d_psb; b.ps_slot = d_pss; b.ps_id = d_psi; b.blk_i1 = d_b1; b.blk_i2 = d_b2; b.blk_beg = d_bb;
@@ -1121,32 +1334,45 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         ORB_HIP_TRY(hipFuncSetAttribute((const void*)ba_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)std::max<size_t>(ldlt_lds, 1024)));
         const dim3 gg((nl * 8 + 63) / 64);   // 8 lanes per point
-        int nbad = 0;
-        for (int it = 0; it < iters && !stopped(); it++) {
-            hipLaunchKernelGGL(ba_iter_kernel, gg, dim3(64), 0, st, b);
-            hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b, 1);
-            if (it == 0) hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
-            int q = 0;
-            double rho = 0;
-            do {
+        // The LM loop runs on the device (ba_decide_kernel advances it); the host keeps LOOKAHEAD
+        // steps enqueued and reads each step's control snapshot from a pinned ring, so no trial
+        // waits for a host round trip.  Steps enqueued past the end return immediately.
+        hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, iters);
+        constexpr int LOOKAHEAD = 2;
+        const int max_steps = iters * 10;
+        int enq = 0, seen = 0;
+        bool fin = false, stop_sent = false;
+        BACtl last{};
+        while (!fin) {
+            while (enq < max_steps && enq - seen < LOOKAHEAD) {
+                hipLaunchKernelGGL(ba_iter_kernel, gg, dim3(64), 0, st, b);
+                hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b, 1);
+                if (enq == 0) hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
                 hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
                 if (np) hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk), dim3(1024), 0, st, b, D);
                 hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
                 hipLaunchKernelGGL(ba_point_update_kernel, gg, dim3(64), 0, st, b, D);
-                hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(1024), 0, st, b);
+                const int slot = enq % LOOKAHEAD;
+                hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(1024), 0, st, b, C.d_ring + slot);
                 ORB_HIP_TRY(hipGetLastError());
-                ORB_HIP_TRY(hipMemcpyAsync(C.h_ctl, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost, st));
-                ORB_HIP_TRY(hipStreamSynchronize(st));
-                rho = C.h_ctl->rho;
-                q++;
-            } while (rho < 0 && q < 10 && !stopped());
-            (*iters_out)++;
-            *chi_out = C.h_ctl->cur;
-            if (q == 10 || rho == 0) break;   // Terminate
-            const double ini = C.h_ctl->ini, cur = C.h_ctl->cur;
-            if ((ini - cur) * 1e3 < ini) nbad++; else nbad = 0;
-            if (nbad >= 3) break;
+                ORB_HIP_TRY(hipEventRecord(C.ring_ev[slot], st));
+                enq++;
+            }
+            if (seen == enq) break;
+            const int slot = seen % LOOKAHEAD;
+            ORB_HIP_TRY(hipEventSynchronize(C.ring_ev[slot]));
+            last = C.h_ring[slot];
+            seen++;
+            fin = last.done != 0;
+            if (!fin && stopped() && !stop_sent) {   // force stop: end the loop after the steps in flight
+                hipLaunchKernelGGL(ba_ctl_stop_kernel, dim3(1), dim3(1), 0, st, b);
+                stop_sent = true;
+            }
         }
+        ORB_HIP_TRY(hipStreamSynchronize(st));
+        ORB_HIP_TRY(hipMemcpy(&last, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost));
+        *iters_out = last.iters_done;
+        *chi_out = last.chi_out;
         return ORB_OK;
     };
 
@@ -1168,21 +1394,31 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, d_outl, d_chi,
                            (uint8_t*)nullptr, 0);
         ORB_HIP_TRY(hipGetLastError());
-        ORB_HIP_TRY(hipMemcpyAsync(res->edge_outlier, d_outl, E, hipMemcpyDeviceToHost, st));
-        if (res->edge_chi2) ORB_HIP_TRY(hipMemcpyAsync(res->edge_chi2, d_chi, 8 * (size_t)E, hipMemcpyDeviceToHost, st));
     }
-    std::vector<double> qh(4 * (size_t)P);
+    Carve hres{C.h_res.ptr};
+    double* hq = hres.take<double>(4 * (size_t)P);
+    double* ht = hres.take<double>(3 * (size_t)P);
+    double* hX = hres.take<double>(3 * (size_t)N);
+    uint8_t* ho = hres.take<uint8_t>(E);
+    double* hc = hres.take<double>(E);
     if (P) {
-        ORB_HIP_TRY(hipMemcpyAsync(qh.data(), b.q, 32 * (size_t)P, hipMemcpyDeviceToHost, st));
-        ORB_HIP_TRY(hipMemcpyAsync(res->pose_t, b.t, 24 * (size_t)P, hipMemcpyDeviceToHost, st));
+        ORB_HIP_TRY(hipMemcpyAsync(hq, b.q, 32 * (size_t)P, hipMemcpyDeviceToHost, st));
+        ORB_HIP_TRY(hipMemcpyAsync(ht, b.t, 24 * (size_t)P, hipMemcpyDeviceToHost, st));
     }
-    if (N) ORB_HIP_TRY(hipMemcpyAsync(res->points, b.X, 24 * (size_t)N, hipMemcpyDeviceToHost, st));
+    if (N) ORB_HIP_TRY(hipMemcpyAsync(hX, b.X, 24 * (size_t)N, hipMemcpyDeviceToHost, st));
+    if (E) {
+        ORB_HIP_TRY(hipMemcpyAsync(ho, d_outl, E, hipMemcpyDeviceToHost, st));
+        if (res->edge_chi2) ORB_HIP_TRY(hipMemcpyAsync(hc, d_chi, 8 * (size_t)E, hipMemcpyDeviceToHost, st));
+    }
     ORB_HIP_TRY(hipStreamSynchronize(st));
-    if (!run)
-        for (int e = 0; e < E; e++) res->edge_outlier[e] = 0;
+    std::memcpy(res->pose_t, ht, 24 * (size_t)P);
+    std::memcpy(res->points, hX, 24 * (size_t)N);
+    if (run) std::memcpy(res->edge_outlier, ho, E);
+    else std::memset(res->edge_outlier, 0, E);
+    if (res->edge_chi2) std::memcpy(res->edge_chi2, hc, 8 * (size_t)E);
     for (int i = 0; i < P; i++) {
-        q_to_R(&qh[4 * i], res->pose_R + 9 * i);
-        if (res->pose_q) std::memcpy(res->pose_q + 4 * i, &qh[4 * i], 32);
+        q_to_R(&hq[4 * i], res->pose_R + 9 * i);
+        if (res->pose_q) std::memcpy(res->pose_q + 4 * i, &hq[4 * i], 32);
     }
     return ORB_OK;
 }

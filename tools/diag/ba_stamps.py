@@ -21,11 +21,18 @@ assert f(C.cast(buf, C.c_void_p)) == 0
 v = list(buf)
 t0 = v[0]
 prev = t0
-for blk in range(13):
+last = t0
+for blk in range(16):
     a, b_, c = v[1 + 3 * blk], v[2 + 3 * blk], v[3 + 3 * blk]
-    if a == 0:
+    if a == 0 or a < t0:
         break
-    f = v[44 + blk]
-    print(f"block {blk}: diag {a - prev:6d} (factor {f - prev:6d}, Linv {a - f:6d}) panel {b_ - a:6d} trailing {c - b_:6d}")
-    prev = c
-print(f"back-substitution {v[40] - prev}, total {v[40] - t0} ticks")
+    line = f"block {blk}: diag-wait {a - prev:6d}"
+    if b_ >= a:
+        line += f" panel {b_ - a:6d}"
+        last = b_
+    if c >= b_ >= a:
+        line += f" lookahead(trailing+diag) {c - b_:6d}"
+        last = c
+    print(line)
+    prev = last
+print(f"back-substitution {v[40] - last}, total {v[40] - t0} ticks")
