@@ -45,6 +45,30 @@ def algorithmic_bytes(W, H, n_kp, nlevels=8):
     return P + (P - W * H) + 60 * n_kp, P
 
 
+STAGE_KERNEL = {"pyramid": "pyramid_level_kernel", "fast_cells": "fast_cells_kernel", "quadtree": "quadtree_kernel",
+                "describe": "describe_kernel"}
+
+
+def measured_traffic(stage, launches_per_step, frames, W, H, nfeat):
+    """HBM bytes per launch of `stage` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (profiles/*_traffic.json, tools/gpu_traffic.sh), corrected by the calibration measured in the same
+    run (FETCH_SIZE counts half the bytes of streaming reads on gfx950; WRITE_SIZE exact).  Only
+    reported when the profiled workload is this one; otherwise None."""
+    files = sorted(ROOT.glob("profiles/*_traffic.json"))
+    if not files or (frames, W, H, nfeat) != (128, 1280, 720, 2000):
+        return None
+    t = json.loads(files[-1].read_text())
+    k = t["kernels_per_dispatch"].get(STAGE_KERNEL.get(stage, ""))
+    if not k or k.get("fetch_bytes") is None:
+        return None
+    cal = t["calibration"]
+    fetch = k["fetch_bytes"] / cal.get("fetch_ratio_8B", 0.5)
+    write = (k.get("write_bytes") or 0.0) / cal.get("write_ratio_4B", 1.0)
+    # the profile averages over dispatches; a stage with several launches per step (pyramid: one
+    # per level) is reported per average launch, like `achieved`
+    return fetch + write
+
+
 def cpu_baseline(frames_np, nfeat, budget_s=12.0):
     """Oracle (single-threaded C++ restatement) extract + match on a bounded sample."""
     sys.path.insert(0, str(ROOT / "tests"))
@@ -180,6 +204,7 @@ def main():
         "describe": 60 * n_kp,      # keypoint + descriptor writes (neighbourhood reads are L2 re-reads)
     }
     dom = max(stages, key=lambda k: stages[k][0])
+    traffic = measured_traffic(dom, stages[dom][1] / max(args.steps, 1), B, W, H, args.nfeatures)
     dom_ms, dom_launches = stages[dom]
     per_launch_ms = dom_ms / max(dom_launches, 1)
     frames_per_launch = B
@@ -207,7 +232,7 @@ def main():
                    "nfeatures": args.nfeatures, "parallelism": f"frames sharded over {world} GPU(s)"
                    + (", RCCL all-gather of descriptor slots" if world > 1 else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": per_launch_ms,
                      "stage_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
                      "pipeline_algorithmic_GBs": pipeline_gbs, "pipeline_bytes_per_frame": bytes_frame},

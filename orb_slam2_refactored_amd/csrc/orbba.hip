@@ -252,38 +252,40 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
             se3_map(q4, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
             chi += edge_error(b, e, Xc);
             q_to_R(q4, R);
-            const double x = Xc[0], y = Xc[1], z = Xc[2], z2 = z * z;
+            // Jacobians with one reciprocal of z (g2o divides by z / z^2 in every term; the
+            // difference is rounding-level, within the LocalBA tolerance)
+            const double x = Xc[0], y = Xc[1], z = Xc[2];
+            const double iz = 1.0 / z, iz2 = iz * iz;
             const double* c = b.cam + 5 * e;
             const double fx = c[0], fy = c[1], bf = c[4];
             const bool st = b.stereo[e];
             const int d = st ? 3 : 2;
             double A[3][3], Bm[3][6];
-            for (int r = 0; r < 3; r++) {
-                for (int j = 0; j < 3; j++) A[r][j] = 0;
-                for (int j = 0; j < 6; j++) Bm[r][j] = 0;
-            }
             if (!st) {
-                const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+                const double tmp[2][3] = {{fx, 0, -x * iz * fx}, {0, fy, -y * iz * fy}};
                 for (int r = 0; r < 2; r++)
                     for (int j = 0; j < 3; j++) {
                         double s = 0;
                         for (int m = 0; m < 3; m++) s += tmp[r][m] * R[3 * m + j];
-                        A[r][j] = -1. / z * s;
+                        A[r][j] = -iz * s;
                     }
+                for (int j = 0; j < 3; j++) A[2][j] = 0;
             } else {
                 for (int j = 0; j < 3; j++) {
-                    A[0][j] = -fx * R[j] / z + fx * x * R[6 + j] / z2;
-                    A[1][j] = -fy * R[3 + j] / z + fy * y * R[6 + j] / z2;
-                    A[2][j] = A[0][j] - bf * R[6 + j] / z2;
+                    A[0][j] = -fx * R[j] * iz + fx * x * R[6 + j] * iz2;
+                    A[1][j] = -fy * R[3 + j] * iz + fy * y * R[6 + j] * iz2;
+                    A[2][j] = A[0][j] - bf * R[6 + j] * iz2;
                 }
             }
-            Bm[0][0] = x * y / z2 * fx; Bm[0][1] = -(1 + (x * x / z2)) * fx; Bm[0][2] = y / z * fx;
-            Bm[0][3] = -1. / z * fx;    Bm[0][4] = 0;                        Bm[0][5] = x / z2 * fx;
-            Bm[1][0] = (1 + y * y / z2) * fy; Bm[1][1] = -x * y / z2 * fy; Bm[1][2] = -x / z * fy;
-            Bm[1][3] = 0;                     Bm[1][4] = -1. / z * fy;     Bm[1][5] = y / z2 * fy;
+            Bm[0][0] = x * y * iz2 * fx; Bm[0][1] = -(1 + (x * x * iz2)) * fx; Bm[0][2] = y * iz * fx;
+            Bm[0][3] = -iz * fx;         Bm[0][4] = 0;                         Bm[0][5] = x * iz2 * fx;
+            Bm[1][0] = (1 + y * y * iz2) * fy; Bm[1][1] = -x * y * iz2 * fy; Bm[1][2] = -x * iz * fy;
+            Bm[1][3] = 0;                      Bm[1][4] = -iz * fy;          Bm[1][5] = y * iz2 * fy;
             if (st) {
-                Bm[2][0] = Bm[0][0] - bf * y / z2; Bm[2][1] = Bm[0][1] + bf * x / z2; Bm[2][2] = Bm[0][2];
-                Bm[2][3] = Bm[0][3];               Bm[2][4] = 0;                      Bm[2][5] = Bm[0][5] - bf / z2;
+                Bm[2][0] = Bm[0][0] - bf * y * iz2; Bm[2][1] = Bm[0][1] + bf * x * iz2; Bm[2][2] = Bm[0][2];
+                Bm[2][3] = Bm[0][3];                Bm[2][4] = 0;                       Bm[2][5] = Bm[0][5] - bf * iz2;
+            } else {
+                for (int j = 0; j < 6; j++) Bm[2][j] = 0;
             }
             double r0, r1;
             robustify(b, e, edge_chi2(b, e), r0, r1);
@@ -557,11 +559,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 // Value of lane J of each 16-lane row (DPP row_newbcast), for a double.
 template <int J>
-__device__ __forceinline__ double row_bcast_t(double v) {
-    const long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffff), 0x150 + J, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x150 + J, 0xf, 0xf, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+__device__ __forceinline__ double row_bcast_t(double v) {   // one v_mov_b64_dpp row_newbcast:J
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, false);
 }
 
 __host__ __device__ constexpr int solve_dp(int D) { return (D + SB - 1) / SB * SB; }
@@ -717,9 +716,38 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     __shared__ int s_flag;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int col = lane & 15, kq = lane >> 4;
-    for (int e = tid; e < Dp * Dp; e += blockDim.x) {
-        const int r = e / Dp, c = e - r * Dp;
-        A[r * ld + c] = (r < D && c < D) ? b.S[r * D + c] : (r == c ? 1.0 : 0.0);
+    BA_STAMP(41);
+    // pose state for the update at the end, loaded now so its latency hides behind the solve
+    double q_pre[4] = {0, 0, 0, 0}, t_pre[3] = {0, 0, 0}, bp_pre[6] = {0, 0, 0, 0, 0, 0};
+    if (tid < b.np) {
+        const int id = b.ps_id[tid];
+        for (int j = 0; j < 4; j++) q_pre[j] = b.q[4 * id + j];
+        for (int j = 0; j < 3; j++) t_pre[j] = b.t[3 * id + j];
+        for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
+    }
+    // S -> LDS (padded with identity): wavefront w takes rows w, w+4, ...; 8 rows (16 loads per lane)
+    // in flight per batch
+    for (int r0 = wv; r0 < Dp; r0 += 32) {
+        double v[8][2];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int r = r0 + 4 * q;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int c = lane + 64 * h;
+                const double sv = b.S[min(r, D - 1) * D + min(c, D - 1)];   // unconditional: no branch
+                v[q][h] = (r < D && c < D) ? sv : (r == c ? 1.0 : 0.0);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int r = r0 + 4 * q;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int c = lane + 64 * h;
+                if (r < Dp && c < Dp) A[r * ld + c] = v[q][h];
+            }
+        }
     }
     for (int i = tid; i < Dp; i += blockDim.x) y[i] = i < D ? b.bs[i] : 0.0;
     if (tid == 0) {
@@ -808,7 +836,7 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
 #pragma unroll
             for (int j = 1; j < SB; j++) {
                 const double lv = A[(J0 + min(col, j)) * ld + J0 + j];   // Linv[j][col] for j > col
-                xp[j & 3] = j > col ? fma(lv, y[J0 + j], xp[j & 3]) : xp[j & 3];
+                xp[j & 3] = fma(j > col ? lv : 0.0, y[J0 + j], xp[j & 3]);   // select, not a branch
             }
             const double xc = (xp[0] + xp[1]) + (xp[2] + xp[3]);
             wave_lds_sync();
@@ -834,15 +862,22 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     __syncthreads();
     // push() + oplus for the free poses, scale terms x.(lambda x + b)
     const double lam = b.ctl->lambda;
-    for (int i = threadIdx.x; i < b.np; i += blockDim.x) {
+    if (tid < b.np) {   // np <= 21 < blockDim
+        const int i = tid;
         const int id = b.ps_id[i];
-        double part = 0;
-        for (int j = 0; j < 6; j++) part += b.x[6 * i + j] * (lam * b.x[6 * i + j] + b.bp[6 * i + j]);
+        double xi[6], part = 0;
+        for (int j = 0; j < 6; j++) {
+            xi[j] = ok ? y[6 * i + j] : 0.0;
+            part += xi[j] * (lam * xi[j] + bp_pre[j]);
+        }
         b.part[b.nl + i] = part;
-        for (int j = 0; j < 4; j++) b.q_sv[4 * id + j] = b.q[4 * id + j];
-        for (int j = 0; j < 3; j++) b.t_sv[3 * id + j] = b.t[3 * id + j];
-        se3_exp_update(b.x + 6 * i, b.q + 4 * id, b.t + 3 * id);
+        for (int j = 0; j < 4; j++) b.q_sv[4 * id + j] = q_pre[j];
+        for (int j = 0; j < 3; j++) b.t_sv[3 * id + j] = t_pre[j];
+        se3_exp_update(xi, q_pre, t_pre);
+        for (int j = 0; j < 4; j++) b.q[4 * id + j] = q_pre[j];
+        for (int j = 0; j < 3; j++) b.t[3 * id + j] = t_pre[j];
     }
+    BA_STAMP(42);
 }
 
 // Back-substitution xl = Dinv (bl - Hpl^T xp), push(), point +=, scale term, then the errors and

@@ -35,4 +35,4 @@ for blk in range(16):
         last = c
     print(line)
     prev = last
-print(f"back-substitution {v[40] - last}, total {v[40] - t0} ticks")
+print(f"back-substitution {v[40] - last}, total {v[40] - t0} ticks; load S {v[0] - v[41]}, pose update tail {v[42] - v[40]}")
