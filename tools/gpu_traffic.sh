@@ -14,4 +14,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc $c -d $OUT/kb_$c -o run -- \
       python3 tools/kbench.py --iters 2 > $OUT/kb_$c.log 2>&1 || { echo "kbench $c failed"; tail -5 $OUT/kb_$c.log; exit 1; }
 done
-python3 tools/pmc_traffic.py $OUT profiles/${TAG}_traffic.json
+python3 tools/pmc_traffic.py $OUT $OUT/${TAG}_traffic.json   # copy into profiles/ afterwards
