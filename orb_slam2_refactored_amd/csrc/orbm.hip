@@ -1,9 +1,9 @@
 // orbm.hip — ORBmatcher Hamming kernels for gfx950.
 //
-//  * hamming_top2_kernel: brute-force best / second-best over all pairs with the reference's
-//    scan semantics (SearchByBoW inner loop, src/ORBmatcher.cc:477-498): one query per lane,
-//    query row in VGPRs, candidate rows staged through LDS in 256-row tiles and read as
-//    wave-wide broadcasts; distance = 8 x v_bcnt(v_xor) (DescriptorDistance, :1449-1457).
+//  * hamming_top2_mfma_kernel: brute-force best / second-best over all pairs with the reference's
+//    scan semantics (SearchByBoW inner loop, src/ORBmatcher.cc:477-498) as an int8 MFMA
+//    contraction: Hamming = |a| + |b| - 2<a, b> on 0/1-expanded bits (DescriptorDistance,
+//    :1449-1457), exact in int32; running top-2 kept as packed (distance, index) keys.
 //  * triangulation_kernel: SearchForTriangulation (:768-866) — per query, the last candidate
 //    with the minimum distance <= TH_LOW that passes the epipole and epipolar gates
 //    (CheckDistEpipolarLine :384-404).  `matched2` is never set by the reference (§0.5), so
@@ -15,71 +15,146 @@
 
 namespace orbamd {
 
-constexpr int TILE = 256;
+// ---------------------------------------------------------------------------------------------
+// Brute-force top-2 on the matrix cores.  For 0/1 bit vectors, Hamming(a, b) = |a| + |b| -
+// 2<a, b>, and <a, b> over the 256 bits is an exact int32 dot product of bytes: bits are expanded
+// to 0/1 bytes in registers and fed to v_mfma_i32_16x16x64_i8 (4 k-steps per 256 bits).  Any k
+// permutation applied identically to the A and B fragments leaves the dot product unchanged, so
+// lane l (group g = l >> 4) simply takes descriptor bytes 8g..8g+7 and k-step s their bits
+// 16s..16s+15.  Per (row, column) the lane forms key = d << 16 | j; the running best key is the
+// minimum (lowest j on equal d, as the reference's strict-< scan) and the running second key the
+// second order statistic.  Keys with d >= 256 (d == 256 and the padding columns) never displace a
+// real candidate and are mapped back to (256, -1) at the end, which is the reference's
+// bestDist = 256 / bestIdx = -1 initialisation.
+typedef int i4v __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int hamming32(uint4 a0, uint4 a1, uint4 b0, uint4 b1) {
-    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
-           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+__device__ __forceinline__ i4v expand16(uint32_t b) {   // bit k of b -> byte k (0 / 1)
+    i4v r;
+    r.x = (int)(((b & 0xfu) * 0x00204081u) & 0x01010101u);
+    r.y = (int)((((b >> 4) & 0xfu) * 0x00204081u) & 0x01010101u);
+    r.z = (int)((((b >> 8) & 0xfu) * 0x00204081u) & 0x01010101u);
+    r.w = (int)((((b >> 12) & 0xfu) * 0x00204081u) & 0x01010101u);
+    return r;
 }
 
-__device__ __forceinline__ void top2_update(int d, int j, int& bd, int& sd, int& bi) {
-    if (d < bd) {
-        sd = bd;
-        bd = d;
-        bi = j;
-    } else if (d < sd) {
-        sd = d;
-    }
+__device__ __forceinline__ uint32_t chunk16(uint2 v, int s) {
+    return ((s < 2 ? v.x : v.y) >> (16 * (s & 1))) & 0xffffu;
 }
 
-__global__ __launch_bounds__(256) void hamming_top2_kernel(const uint8_t* __restrict__ A, const int32_t* __restrict__ nA_arr,
-                                                           int nA_fixed, int strideA, const uint8_t* __restrict__ B,
-                                                           const int32_t* __restrict__ nB_arr, int nB_fixed, int strideB,
-                                                           const int32_t* __restrict__ pair_b, float nnratio,
-                                                           int th_low, int32_t* __restrict__ best_idx,
-                                                           int32_t* __restrict__ best, int32_t* __restrict__ second,
-                                                           int32_t* __restrict__ match) {
-    __shared__ uint4 tile[TILE * 2];
+__device__ __forceinline__ int popc_row(const uint8_t* r) {
+    const uint4 a = reinterpret_cast<const uint4*>(r)[0], b = reinterpret_cast<const uint4*>(r)[1];
+    return __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) + __popc(b.z) +
+           __popc(b.w);
+}
+
+constexpr int MM_RT = 4;                 // 16-row tiles per wavefront
+constexpr int MM_ROWS = 4 * 64 * MM_RT / 4;   // 256 query rows per workgroup
+
+__global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
+    const uint8_t* __restrict__ A, const int32_t* __restrict__ nA_arr, int nA_fixed, int strideA,
+    const uint8_t* __restrict__ B, const int32_t* __restrict__ nB_arr, int nB_fixed, int strideB,
+    const int32_t* __restrict__ pair_b, float nnratio, int th_low, int32_t* __restrict__ best_idx,
+    int32_t* __restrict__ best, int32_t* __restrict__ second, int32_t* __restrict__ match) {
+    extern __shared__ int mm_sm[];   // pa[MM_ROWS] | pb[nB padded to 16]
+    int* s_pa = mm_sm;
+    int* s_pb = mm_sm + MM_ROWS;
     const int p = blockIdx.y;
     const int q = pair_b ? pair_b[p] : p;
     const int nA = nA_arr ? nA_arr[p] : nA_fixed;
     const int nB = nB_arr ? nB_arr[q] : nB_fixed;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if ((int)(blockIdx.x * blockDim.x) >= nA) return;   // block-uniform
+    const int row_base = blockIdx.x * MM_ROWS;
+    if (row_base >= nA) return;   // block-uniform
     const uint8_t* Ap = A + (long long)p * strideA * 32;
     const uint8_t* Bp = B + (long long)q * strideB * 32;
-    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-    if (i < nA) {
-        q0 = reinterpret_cast<const uint4*>(Ap)[2 * i];
-        q1 = reinterpret_cast<const uint4*>(Ap)[2 * i + 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    const int nBt = (nB + 15) & ~15;
+    for (int j = tid; j < nBt; j += blockDim.x) s_pb[j] = j < nB ? popc_row(Bp + (long long)j * 32) : 256;
+    {
+        const int row = row_base + tid;
+        s_pa[tid] = row < nA ? popc_row(Ap + (long long)row * 32) : 0;
     }
-    int bd = 256, sd = 256, bi = -1;
-    for (int t0 = 0; t0 < nB; t0 += TILE) {
-        const int nt = min(TILE, nB - t0);
-        __syncthreads();
-        for (int r = threadIdx.x; r < 2 * nt; r += blockDim.x)
-            tile[r] = reinterpret_cast<const uint4*>(Bp)[2 * t0 + r];
-        __syncthreads();
-        int j = 0;
-        for (; j + 4 <= nt; j += 4) {   // four candidates per step: LDS reads issued together
-            const uint4 b00 = tile[2 * j], b01 = tile[2 * j + 1], b10 = tile[2 * j + 2], b11 = tile[2 * j + 3];
-            const uint4 b20 = tile[2 * j + 4], b21 = tile[2 * j + 5], b30 = tile[2 * j + 6], b31 = tile[2 * j + 7];
-            const int d0 = hamming32(q0, q1, b00, b01), d1 = hamming32(q0, q1, b10, b11);
-            const int d2 = hamming32(q0, q1, b20, b21), d3 = hamming32(q0, q1, b30, b31);
-            top2_update(d0, t0 + j, bd, sd, bi);
-            top2_update(d1, t0 + j + 1, bd, sd, bi);
-            top2_update(d2, t0 + j + 2, bd, sd, bi);
-            top2_update(d3, t0 + j + 3, bd, sd, bi);
+    // A fragments: tile rt rows row_base + 64w + 16rt + c16, bytes 8g..8g+7
+    i4v af[MM_RT][4];
+#pragma unroll
+    for (int rt = 0; rt < MM_RT; rt++) {
+        const int row = min(row_base + 64 * w + 16 * rt + c16, nA - 1);
+        const uint2 v = *reinterpret_cast<const uint2*>(Ap + (long long)row * 32 + 8 * g);
+#pragma unroll
+        for (int s2 = 0; s2 < 4; s2++) af[rt][s2] = expand16(chunk16(v, s2));
+    }
+    __syncthreads();
+    uint32_t pa16[MM_RT][4];
+#pragma unroll
+    for (int rt = 0; rt < MM_RT; rt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) pa16[rt][r] = (uint32_t)s_pa[64 * w + 16 * rt + 4 * g + r] << 16;
+    uint32_t bk[MM_RT][4], sk[MM_RT][4];
+#pragma unroll
+    for (int rt = 0; rt < MM_RT; rt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) bk[rt][r] = sk[rt][r] = 0xffffffffu;
+    // column tiles of 16, B loads one tile ahead
+    uint2 bnext = make_uint2(0, 0);
+    if (c16 < nB) bnext = *reinterpret_cast<const uint2*>(Bp + (long long)c16 * 32 + 8 * g);
+    for (int j0 = 0; j0 < nB; j0 += 16) {
+        const uint2 bcur = bnext;
+        const int jn = j0 + 16 + c16;
+        if (jn < nB) bnext = *reinterpret_cast<const uint2*>(Bp + (long long)jn * 32 + 8 * g);
+        const int j = j0 + c16;
+        const uint2 bv = j < nB ? bcur : make_uint2(0, 0);
+        const uint32_t cj = ((uint32_t)s_pb[j] << 16) | (uint32_t)j;
+        i4v bf[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; s2++) bf[s2] = expand16(chunk16(bv, s2));
+#pragma unroll
+        for (int rt = 0; rt < MM_RT; rt++) {
+            i4v acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[rt][s2], bf[s2], acc, 0, 0, 0);
+            const int dot[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const uint32_t key = pa16[rt][r] + cj - ((uint32_t)dot[r] << 17);   // (pa + pb - 2 dot) << 16 | j
+                const uint32_t hi = max(bk[rt][r], key);
+                bk[rt][r] = min(bk[rt][r], key);
+                sk[rt][r] = min(sk[rt][r], hi);
+            }
         }
-        for (; j < nt; j++) top2_update(hamming32(q0, q1, tile[2 * j], tile[2 * j + 1]), t0 + j, bd, sd, bi);
     }
-    if (i < nA) {
-        const long long o = (long long)p * strideA + i;
-        if (best_idx) best_idx[o] = bi;
-        if (best) best[o] = bd;
-        if (second) second[o] = sd;
-        if (match) match[o] = (bd <= th_low && (float)bd < nnratio * (float)sd) ? bi : -1;
-    }
+    // merge the 16 column classes of each row (lanes with the same g)
+#pragma unroll
+    for (int rt = 0; rt < MM_RT; rt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            uint32_t b1 = bk[rt][r], s1 = sk[rt][r];
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) {
+                const uint32_t b2 = (uint32_t)__shfl_xor((int)b1, m, 64), s2v = (uint32_t)__shfl_xor((int)s1, m, 64);
+                s1 = min(min(s1, s2v), max(b1, b2));
+                b1 = min(b1, b2);
+            }
+            const int row = row_base + 64 * w + 16 * rt + 4 * g + r;
+            if (c16 == 0 && row < nA) {
+                const int bd = b1 >> 16 >= 256 ? 256 : (int)(b1 >> 16);
+                const int bi = b1 >> 16 >= 256 ? -1 : (int)(b1 & 0xffffu);
+                const int sd = s1 >> 16 >= 256 ? 256 : (int)(s1 >> 16);
+                const long long o = (long long)p * strideA + row;
+                if (best_idx) best_idx[o] = bi;
+                if (best) best[o] = bd;
+                if (second) second[o] = sd;
+                if (match) match[o] = (bd <= th_low && (float)bd < nnratio * (float)sd) ? bi : -1;
+            }
+        }
+}
+
+static void launch_top2(const uint8_t* A, const int32_t* nA_arr, int nA_fixed, int strideA, const uint8_t* B,
+                        const int32_t* nB_arr, int nB_fixed, int strideB, const int32_t* pair_b, int n_pairs,
+                        float nnratio, int th_low, int32_t* bi, int32_t* bd, int32_t* sd, int32_t* mt,
+                        hipStream_t st) {
+    const size_t lds = (size_t)(MM_ROWS + ((strideB + 15) & ~15) + 16) * sizeof(int);
+    hipLaunchKernelGGL(hamming_top2_mfma_kernel, dim3((unsigned)((strideA + MM_ROWS - 1) / MM_ROWS), (unsigned)n_pairs),
+                       dim3(256), lds, st, A, nA_arr, nA_fixed, strideA, B, nB_arr, nB_fixed, strideB, pair_b,
+                       nnratio, th_low, bi, bd, sd, mt);
 }
 
 struct TriQuery {
@@ -163,9 +238,8 @@ int orbm_hamming_top2_device(const uint8_t* d_A, int nA, const uint8_t* d_B, int
                              int32_t* d_best, int32_t* d_second, void* stream) {
     ORB_CHECK_ARG(nA >= 0 && nB >= 0 && (nA == 0 || d_A) && (nB == 0 || d_B), "bad matcher arguments");
     if (nA == 0) return ORB_OK;
-    hipLaunchKernelGGL(hamming_top2_kernel, dim3((unsigned)((nA + 255) / 256), 1), dim3(256), 0, (hipStream_t)stream,
-                       d_A, (const int32_t*)nullptr, nA, nA, d_B, (const int32_t*)nullptr, nB, nB,
-                       (const int32_t*)nullptr, 0.6f, 50, d_best_idx, d_best, d_second, (int32_t*)nullptr);
+    launch_top2(d_A, nullptr, nA, nA, d_B, nullptr, nB, std::max(nB, 1), nullptr, 1, 0.6f, 50, d_best_idx, d_best,
+                d_second, nullptr, (hipStream_t)stream);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
@@ -177,9 +251,8 @@ int orbm_bf_match_batch_device(const uint8_t* d_A, const int32_t* d_nA, int stri
     ORB_CHECK_ARG(d_A && d_B && d_nA && d_nB && n_pairs >= 0 && strideA > 0 && strideB > 0, "bad matcher arguments");
     if (n_pairs == 0) return ORB_OK;
     ORB_CHECK_ARG(n_pairs <= 65535, "too many pairs in one launch");
-    hipLaunchKernelGGL(hamming_top2_kernel, dim3((unsigned)((strideA + 255) / 256), (unsigned)n_pairs), dim3(256), 0,
-                       (hipStream_t)stream, d_A, d_nA, 0, strideA, d_B, d_nB, 0, strideB, d_pair_b, nnratio, th_low,
-                       d_best_idx, d_best, d_second, d_match);
+    launch_top2(d_A, d_nA, 0, strideA, d_B, d_nB, 0, strideB, d_pair_b, n_pairs, nnratio, th_low, d_best_idx, d_best,
+                d_second, d_match, (hipStream_t)stream);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
@@ -197,9 +270,8 @@ int orbm_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float nnra
     int32_t* o = s.o1.as<int32_t>();
     ORB_HIP_TRY(hipMemcpy(s.a.ptr, A, (size_t)nA * 32, hipMemcpyHostToDevice));
     if (nB) ORB_HIP_TRY(hipMemcpy(s.b.ptr, B, (size_t)nB * 32, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(hamming_top2_kernel, dim3((unsigned)((nA + 255) / 256), 1), dim3(256), 0, (hipStream_t)0,
-                       s.a.as<uint8_t>(), (const int32_t*)nullptr, nA, nA, s.b.as<uint8_t>(), (const int32_t*)nullptr,
-                       nB, nB, (const int32_t*)nullptr, nnratio, th_low, o, o + nA, o + 2 * nA, o + 3 * nA);
+    launch_top2(s.a.as<uint8_t>(), nullptr, nA, nA, s.b.as<uint8_t>(), nullptr, nB, std::max(nB, 1), nullptr, 1, nnratio,
+                th_low, o, o + nA, o + 2 * nA, o + 3 * nA, (hipStream_t)0);
     ORB_HIP_TRY(hipGetLastError());
     std::vector<int32_t> h((size_t)nA * 4);
     ORB_HIP_TRY(hipMemcpy(h.data(), o, (size_t)nA * 16, hipMemcpyDeviceToHost));

@@ -144,8 +144,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
 // One workgroup = a 64 x 16 tile of level l (256 threads, 4 output pixels each).  The source
 // rectangle of level l-1 it needs is staged in LDS with dword loads; coefficients come from the
 // per-level tables.
-constexpr int PYR_TW = 64, PYR_TH = 16;
-constexpr int PYR_SW = 128, PYR_SH = 48;   // LDS source tile capacity (scale factor <= ~1.9)
+constexpr int PYR_TW = 64, PYR_TH = 64;
+constexpr int PYR_SW = 144, PYR_SH = 128;   // LDS source tile capacity (scale factor <= ~1.9)
 
 __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const uint8_t* __restrict__ in,
                                                             long long in_fstride, int in_step, uint8_t* pyr,
@@ -164,53 +164,85 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
     const uint8_t* src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &sstep);
     const int2* xt = xtab + L.xtab_off;
     const int2* yt = ytab + L.ytab_off;
+    // coefficient tables -> LDS (independent of the image loads below)
     if ((int)threadIdx.x < tw) xs_t[threadIdx.x] = xt[tx0 + threadIdx.x];
-    if ((int)threadIdx.x < th) ys_t[threadIdx.x] = yt[ty0 + threadIdx.x];
-    // source rectangle: monotone tables -> first / last entries bound it
-    const int sx_lo = xt[tx0].x & 0xffff, sx_hi = xt[tx0 + tw - 1].x >> 16;
-    const int sy_lo = yt[ty0].x & 0xffff, sy_hi = yt[ty0 + th - 1].x >> 16;
+    if ((int)threadIdx.x >= 64 && (int)threadIdx.x - 64 < th) ys_t[threadIdx.x - 64] = yt[ty0 + threadIdx.x - 64];
+    // conservative source rectangle from the scale (a superset of the tables' taps; no table
+    // round trip before the image loads)
+    const int sw = Ls.w, sh = Ls.h;
+    const double scx = (double)sw / L.w, scy = (double)sh / L.h;
+    const int sx_lo = max(0, (int)floor((tx0 + 0.5) * scx - 0.5) - 2);
+    const int sx_hi = min(sw - 1, (int)floor((tx0 + tw - 0.5) * scx - 0.5) + 2);
+    const int sy_lo = max(0, (int)floor((ty0 + 0.5) * scy - 0.5) - 2);
+    const int sy_hi = min(sh - 1, (int)floor((ty0 + th - 0.5) * scy - 0.5) + 2);
     const int xa = sx_lo & ~3;
     const int nd = (sx_hi - xa + 4) >> 2;   // dwords per source row
     const int nr = sy_hi - sy_lo + 1;
-    const int sw = Ls.w;
-    for (int i = threadIdx.x; i < nd * nr; i += blockDim.x) {
-        const int r = i / nd, d = i - r * nd;
-        const uint8_t* rowp = src + (long long)(sy_lo + r) * sstep;
-        const int x = xa + 4 * d;
-        uint32_t v;
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(rowp + x);
-        if (x + 3 < sw && (addr & 3) == 0) {
-            v = *reinterpret_cast<const uint32_t*>(rowp + x);
-        } else {
-            v = 0;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)sstep) & 3) == 0;
+    if (aligned) {
+        // flat (row, dword) walk; all of a thread's loads in flight before the LDS stores
+        constexpr int NL = (PYR_SW / 4) * PYR_SH / 256;
+        const int dr = 256 / nd, dm = 256 - dr * nd;
+        int r = threadIdx.x / nd, d = threadIdx.x - (threadIdx.x / nd) * nd;
+        uint32_t v[NL];
+        int rr[NL], dd[NL];
+#pragma unroll
+        for (int k = 0; k < NL; k++) {
+            rr[k] = r;
+            dd[k] = d;
+            const int rc = min(r, nr - 1);
+            const int xd = min(xa + 4 * d, (sw - 1) & ~3);   // in-row dword (row stride >= align4(w))
+            v[k] = *reinterpret_cast<const uint32_t*>(src + (long long)(sy_lo + rc) * sstep + xd);
+            r += dr;
+            d += dm;
+            if (d >= nd) { d -= nd; r++; }
+        }
+#pragma unroll
+        for (int k = 0; k < NL; k++)
+            if (rr[k] < nr) *reinterpret_cast<uint32_t*>(&S[rr[k] * PYR_SW + 4 * dd[k]]) = v[k];
+    } else {   // unaligned caller image (level 0 with an odd base / step): byte loads
+        for (int i = threadIdx.x; i < nd * nr; i += blockDim.x) {
+            const int r = i / nd, d = i - r * nd;
+            const uint8_t* rowp = src + (long long)(sy_lo + r) * sstep;
+            const int x = xa + 4 * d;
+            uint32_t v = 0;
             for (int q = 0; q < 4; q++)
                 if (x + q < sw) v |= (uint32_t)rowp[x + q] << (8 * q);
+            *reinterpret_cast<uint32_t*>(&S[r * PYR_SW + 4 * d]) = v;
         }
-        *reinterpret_cast<uint32_t*>(&S[r * PYR_SW + 4 * d]) = v;
     }
     __syncthreads();
-    const int ty = threadIdx.x >> 4, q0 = (threadIdx.x & 15) * 4;
-    if (ty >= th || q0 >= tw) return;
-    const int2 yv = ys_t[ty];
-    const int r0 = ((yv.x & 0xffff) - sy_lo) * PYR_SW - xa, r1 = ((yv.x >> 16) - sy_lo) * PYR_SW - xa;
-    const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
-    uint32_t packed = 0;
+    // 16 threads per 64-px output row segment (4 px each), 16 rows per pass
+    const int q0 = (threadIdx.x & 15) * 4;
+    if (q0 >= tw) return;
+    int sxo[4], a0v[4], a1v[4], sxo1[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        if (q0 + k < tw) {
-            const int2 xv = xs_t[q0 + k];
-            const int sx0 = xv.x & 0xffff, sx1 = xv.x >> 16, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
-            const int h0 = S[r0 + sx0] * a0 + S[r0 + sx1] * a1;
-            const int h1 = S[r1 + sx0] * a0 + S[r1 + sx1] * a1;
+        const int2 xv = xs_t[min(q0 + k, tw - 1)];
+        sxo[k] = (xv.x & 0xffff) - xa;
+        sxo1[k] = (xv.x >> 16) - xa;
+        a0v[k] = xv.y & 0xffff;
+        a1v[k] = xv.y >> 16;
+    }
+    uint8_t* dbase = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + q0;
+    for (int ty = threadIdx.x >> 4; ty < th; ty += 16) {
+        const int2 yv = ys_t[ty];
+        const int r0 = ((yv.x & 0xffff) - sy_lo) * PYR_SW, r1 = ((yv.x >> 16) - sy_lo) * PYR_SW;
+        const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int h0 = S[r0 + sxo[k]] * a0v[k] + S[r0 + sxo1[k]] * a1v[k];
+            const int h1 = S[r1 + sxo[k]] * a0v[k] + S[r1 + sxo1[k]] * a1v[k];
             const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
             const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
             packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
         }
+        uint8_t* dst = dbase + (long long)(ty0 + ty) * L.stride;
+        if (q0 + 3 < tw) *reinterpret_cast<uint32_t*>(dst) = packed;   // stride % 16 == 0, tx0+q0 % 4 == 0
+        else
+            for (int k = 0; q0 + k < tw; k++) dst[k] = (uint8_t)(packed >> (8 * k));
     }
-    uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off + (long long)(ty0 + ty) * L.stride + tx0 + q0;
-    if (q0 + 3 < tw) *reinterpret_cast<uint32_t*>(dst) = packed;   // stride % 16 == 0, tx0+q0 % 4 == 0
-    else
-        for (int k = 0; q0 + k < tw; k++) dst[k] = (uint8_t)(packed >> (8 * k));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1382,7 +1414,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         }
         if (l > 0) {   // the pyramid kernel's LDS source tile must hold a 64x16 output tile's footprint
             const double sc = (double)prev_w / L.w, scy = (double)prev_h / L.h;
-            if (sc * (PYR_TW - 1) + 2 + 4 > PYR_SW || scy * (PYR_TH - 1) + 3 > PYR_SH) {
+            if (sc * PYR_TW + 12 > PYR_SW || scy * PYR_TH + 6 > PYR_SH) {   // conservative rectangle + margins
                 set_error("scaleFactor too large for the pyramid tile (max ~1.9)");
                 return ORB_EINVAL;
             }
