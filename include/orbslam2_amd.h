@@ -81,7 +81,8 @@ int orbx_pyramid_level(const orbx_extractor* h, int level, uint8_t* dst, size_t 
  * d_imgs: frame f at d_imgs + f*frame_stride, rows of `step` bytes.
  * Outputs per frame f: d_kps[f*cap .. ], d_desc[(f*cap)*32 .. ], d_counts[f].
  * Keypoint/descriptor order per frame is the reference's (level-major, quadtree list order).
- * Enqueue only (no host sync).  cap must be >= orbx_max_keypoints(). */
+ * Enqueue only (no host sync) on `stream` (a hipStream_t; NULL = the default stream, ordered like
+ * any other HIP work on it).  cap must be >= orbx_max_keypoints(). */
 int orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int n_frames, int rows,
                               int cols, size_t frame_stride, size_t step, orbx_keypoint* d_kps,
                               uint8_t* d_desc, int32_t* d_counts, int cap, void* stream);

@@ -1752,7 +1752,7 @@ int orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int n_fr
         return ORB_ECAP;
     }
     if ((rc = reserve_workspace(h, n_frames))) return rc;
-    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the default stream, like every HIP API
     h->last_in = d_imgs;
     h->last_fstride = (long long)frame_stride;
     h->last_step = step;
