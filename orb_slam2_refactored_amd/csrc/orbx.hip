@@ -32,6 +32,7 @@ constexpr int MAX_ZONE = 64;            // max FAST detection-zone side (cellw <
 constexpr int MAX_ROOTS = 32;
 constexpr int PATCH = 43;               // raw neighbourhood: +-21 (rBRIEF reach 18 + blur 3)
 constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
+constexpr int HBS = HBLUR_W;            // LDS row stride of the blurred rows (u16)
 
 __constant__ int c_pattern[1024] = {
 #include "orb_pattern31.inc"
@@ -1164,6 +1165,12 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 constexpr int RS = 44;   // LDS raw-patch row stride
 
 // One workgroup = one wavefront = one kept keypoint.
+constexpr int DESC_KPW = 1;                               // keypoints per wavefront
+constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords per raw-patch row (RS = 4 * 11)
+constexpr int PATCH_LD = (PATCH * PATCH_DW + 63) / 64;    // dword loads per lane for a whole patch
+
+// One wavefront per DESC_KPW consecutive output keypoints of a frame (output order = level-major
+// list order); waves past the frame's total exit at once.
 __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
                                                       int in_step, const uint8_t* __restrict__ pyr,
                                                       const uint32_t* __restrict__ sel,
@@ -1171,33 +1178,52 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                                                       uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
                                                       int cap) {
     __shared__ __attribute__((aligned(16))) uint8_t R[PATCH * RS];
-    __shared__ __attribute__((aligned(16))) uint16_t Hb[PATCH * HBLUR_W];
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[PATCH * HBS];
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
-    const int s = lb % gridDim.x;
+    const int wslot = lb % gridDim.x;
     const int* cnt = sel_cnt + f * g.nlevels;
-    if (s == 0 && lane == 0) {
-        int tot = 0;
-        for (int q = 0; q < g.nlevels; q++) tot += cnt[q];
-        counts[f] = tot;
+    int total = 0;
+    for (int q = 0; q < g.nlevels; q++) total += cnt[q];
+    if (wslot == 0 && lane == 0) counts[f] = total;
+    for (int kk = 0; kk < DESC_KPW; kk++) {
+    const int oidx = wslot * DESC_KPW + kk;
+    if (oidx >= total || oidx >= cap) break;
+    int l = 0, lbase = 0;
+    while (l + 1 < g.nlevels && oidx >= lbase + cnt[l]) {
+        lbase += cnt[l];
+        l++;
     }
-    int l = 0;
-    while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_base) l++;
     const LevelDev& L = g.lv[l];
-    const int i = s - L.out_base;
-    if (i >= cnt[l]) return;
-    int oidx = i;
-    for (int q = 0; q < l; q++) oidx += cnt[q];
-    if (oidx >= cap) return;
+    const int s = L.out_base + (oidx - lbase);
 
     const uint32_t k = sel[(long long)f * g.out_frame + s];
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
     int step;
     const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
-    // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101):
-    // lane = column, all 43 row loads issued before the LDS stores
-    if (lane < PATCH) {
+    // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101)
+    if (kx >= 21 && ky >= 21 && kx + 21 + 8 < L.w && ky + 21 < L.h) {
+        // interior: aligned dword pairs realigned with v_alignbyte, all loads in flight together
+        const uint8_t* base = img + (long long)(ky - 21) * step + (kx - 21);
+        uint32_t lo[PATCH_LD], hi[PATCH_LD];
+        int off[PATCH_LD], sh[PATCH_LD];
+#pragma unroll
+        for (int t = 0; t < PATCH_LD; t++) {
+            const int it = min(lane + 64 * t, PATCH * PATCH_DW - 1);
+            const int r = it / PATCH_DW, d = it - r * PATCH_DW;
+            const uint8_t* pbyte = base + (long long)r * step + 4 * d;
+            const int m = (int)(reinterpret_cast<uintptr_t>(pbyte) & 3);
+            const uint32_t* pw = reinterpret_cast<const uint32_t*>(pbyte - m);
+            lo[t] = pw[0];
+            hi[t] = pw[1];
+            sh[t] = m;
+            off[t] = lane + 64 * t < PATCH * PATCH_DW ? r * RS + 4 * d : -1;
+        }
+#pragma unroll
+        for (int t = 0; t < PATCH_LD; t++)
+            if (off[t] >= 0) *reinterpret_cast<uint32_t*>(&R[off[t]]) = __builtin_amdgcn_alignbyte(hi[t], lo[t], sh[t]);
+    } else if (lane < PATCH) {
         const int xx = reflect101(kx - 21 + lane, L.w);
         uint8_t v[PATCH];
 #pragma unroll
@@ -1225,12 +1251,16 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 
     // horizontal Q8 blur, one row per lane (sliding window in registers); taps are symmetric
     if (lane < PATCH) {
-        int v[PATCH];
+        int v[PATCH_DW * 4];
 #pragma unroll
-        for (int c = 0; c < PATCH; c++) v[c] = R[lane * RS + c];
+        for (int d = 0; d < PATCH_DW; d++) {   // dword reads of the row, bytes unpacked in registers
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(&R[lane * RS + 4 * d]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) v[4 * d + q] = (int)((w >> (8 * q)) & 0xffu);
+        }
 #pragma unroll
         for (int c = 0; c < HBLUR_W; c++)
-            Hb[lane * HBLUR_W + c] =
+            Hb[lane * HBS + c] =
                 (uint16_t)(18 * (v[c] + v[c + 6]) + 34 * (v[c + 1] + v[c + 5]) + 48 * (v[c + 2] + v[c + 4]) + 56 * v[c + 3]);
     }
     __syncthreads();
@@ -1242,9 +1272,9 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         const float x = (float)c_pattern[2 * idx], y = (float)c_pattern[2 * idx + 1];
         const int dy = (int)rintf(x * b + y * a);
         const int dx = (int)rintf(x * a - y * b);
-        const uint16_t* col = Hb + (18 + dy) * HBLUR_W + 18 + dx;
-        const unsigned acc = 18u * (col[0] + col[6 * HBLUR_W]) + 34u * (col[HBLUR_W] + col[5 * HBLUR_W]) +
-                             48u * (col[2 * HBLUR_W] + col[4 * HBLUR_W]) + 56u * col[3 * HBLUR_W];
+        const uint16_t* col = Hb + (18 + dy) * HBS + 18 + dx;
+        const unsigned acc = 18u * (col[0] + col[6 * HBS]) + 34u * (col[HBS] + col[5 * HBS]) +
+                             48u * (col[2 * HBS] + col[4 * HBS]) + 56u * col[3 * HBS];
         return (int)((acc + (1u << 15)) >> 16);
     };
     unsigned long long words[4];
@@ -1271,6 +1301,8 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         }
         reinterpret_cast<float*>(kps + o)[lane] = fv;
     }
+    __syncthreads();   // R / Hb are rewritten by the next keypoint
+    }   // keypoints of this wavefront
 }
 
 __global__ __launch_bounds__(64) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
@@ -1617,7 +1649,8 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     }
     {
     StageMark m3(h, st, 3);
-    hipLaunchKernelGGL(describe_kernel, dim3((unsigned)g.out_frame, (unsigned)F), dim3(64), 0, st, g,
+    hipLaunchKernelGGL(describe_kernel, dim3((unsigned)((g.out_frame + DESC_KPW - 1) / DESC_KPW), (unsigned)F), dim3(64),
+                       0, st, g,
                        d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
     }
 }
