@@ -665,6 +665,39 @@ __device__ int4 qt_wave_split(const QtNode& n, const uint32_t* __restrict__ P, u
     return make_int4(c[0], c[1], c[2], c[3]);
 }
 
+// Child counts of one node by a single thread (phase 2 only needs the counts of every divisible
+// node to find where to stop; only the processed prefix is then split for real).
+__device__ __forceinline__ int4 qt_thread_count(const QtNode& n, const uint32_t* __restrict__ P) {
+    const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
+    const int ym = n.tly + (n.bry - n.tly + 1) / 2;
+    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (int j = 0; j < n.cnt; j++) {
+        const uint32_t k = P[n.beg + j];
+        const bool r = kp_x(k) >= xm, d = kp_y(k) >= ym;
+        c0 += !r && !d;
+        c1 += r && !d;
+        c2 += !r && d;
+        c3 += r && d;
+    }
+    return make_int4(c0, c1, c2, c3);
+}
+
+// Stable 4-way scatter of one small node by a single thread, child counts known.
+__device__ __forceinline__ void qt_thread_split(const QtNode& n, int4 cnt, const uint32_t* __restrict__ P,
+                                                uint32_t* __restrict__ T) {
+    const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
+    const int ym = n.tly + (n.bry - n.tly + 1) / 2;
+    int o0 = n.beg, o1 = o0 + cnt.x, o2 = o1 + cnt.y, o3 = o2 + cnt.z;
+    for (int j = 0; j < n.cnt; j++) {
+        const uint32_t k = P[n.beg + j];
+        const bool r = kp_x(k) >= xm, d = kp_y(k) >= ym;
+        const int dst = d ? (r ? o3++ : o2++) : (r ? o1++ : o0++);
+        T[dst] = k;
+    }
+}
+
+constexpr int QT_THREAD_SPLIT_MAX = 48;   // nodes up to this many points are split by one thread
+
 __device__ __forceinline__ int ne4(int4 c) { return (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0); }
 __device__ __forceinline__ int dv4(int4 c) { return (c.x > 1) + (c.y > 1) + (c.z > 1) + (c.w > 1); }
 __device__ __forceinline__ int c4(int4 c, int i) { return i == 0 ? c.x : i == 1 ? c.y : i == 2 ? c.z : c.w; }
@@ -700,6 +733,7 @@ __device__ __forceinline__ void qt_emit_children(const QtNode& parent, int4 cc, 
 
 #ifdef ORB_QT_STAMPS
 __device__ unsigned long long g_qt_stamps[64];
+__device__ unsigned long long g_qt_wg[4096 * 2];   // per (frame, level) WG: start, end
 #define QT_STAMP(k)                                                                                \
     do {                                                                                           \
         if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && (k) < 64)                    \
@@ -712,23 +746,37 @@ __device__ unsigned long long g_qt_stamps[64];
 #endif
 
 
-// std::sort(a, a+n, size-descending) on one wavefront: qt_sort_parallel_form() (qt_sort.h) with
-// each Hoare partition computed from ballot-compacted stopper lists.  Scratch: Ls, Rs, seg_lo,
-// seg_len (n ints each), tmp (n items), stk (>= 192 ints).  All lanes of the wave must call it.
-__device__ void qt_sort_wave(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, int* seg_len, QtItem* tmp, int* stk) {
-    const int lane = lane_id();
+// std::sort(a, a+n, size-descending) as qt_sort_parallel_form() (qt_sort.h): each Hoare partition
+// computed from ballot-compacted stopper lists by one wavefront.  Segments of one recursion round are disjoint
+// and a partition (or the depth-0 heap sort) only moves items inside its own segment, so the
+// rounds run one after another and a round's segments in parallel, one wavefront each; the
+// result is identical to the sequential order.  All threads of the block must call it.
+// Scratch: Ls, Rs, seg_lo, seg_len (n ints each), tmp (n items), lists (6 * list_cap ints),
+// s_cnt (2 shared ints).  list_cap >= n / 17 + 1.
+__device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, int* seg_len, QtItem* tmp,
+                              int* lists, int list_cap, int* s_cnt) {
+    const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const unsigned long long lt = lanemask_lt();
     if (n <= 0) return;
-    int sp = 0;
-    if (lane == 0) { stk[0] = 0; stk[1] = n; stk[2] = 2 * qt_lg(n); }
-    sp = 1;
-    wave_lds_sync();
-    while (sp > 0) {
-        --sp;
-        const int lo = stk[3 * sp], hi = stk[3 * sp + 1];
-        int depth = stk[3 * sp + 2];
-        wave_lds_sync();
-        if (hi - lo > 16) {
+    int* cur = lists;
+    int* nxt = lists + 3 * list_cap;
+    if (threadIdx.x == 0) {
+        s_cnt[0] = 0;
+        s_cnt[1] = 0;
+        if (n > 16) {
+            cur[0] = 0; cur[1] = n; cur[2] = 2 * qt_lg(n);
+            s_cnt[0] = 1;
+        }
+    }
+    if (n <= 16)
+        for (int i = threadIdx.x; i < n; i += blockDim.x) { seg_lo[i] = 0; seg_len[i] = n; }
+    __syncthreads();
+    while (true) {
+        const int nc = s_cnt[0];
+        if (nc == 0) break;
+        for (int si = w; si < nc; si += nw) {
+            const int lo = cur[3 * si], hi = cur[3 * si + 1];
+            int depth = cur[3 * si + 2];
             if (depth == 0) {
                 if (lane == 0) qt_heap_sort(a + lo, a + hi);
                 for (int i = lo + lane; i < hi; i += 64) { seg_lo[i] = lo; seg_len[i] = -1; }
@@ -739,20 +787,20 @@ __device__ void qt_sort_wave(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, in
             const int mid = lo + (hi - lo) / 2;
             if (lane == 0) qt_median_to_first(a + lo, a + lo + 1, a + mid, a + hi - 1);
             wave_lds_sync();
-            const int p = a[lo].size;
+            const int pv = a[lo].size;
             int nl = 0, nr = 0;
             for (int base = lo + 1; base < hi; base += 64) {
                 const int i = base + lane;
-                const bool f = i < hi && a[i].size <= p;
+                const bool f = i < hi && a[i].size <= pv;
                 const unsigned long long m = __ballot(f);
-                if (f) Ls[nl + popc64(m & lt)] = i;
+                if (f) Ls[lo + nl + popc64(m & lt)] = i;
                 nl += popc64(m);
             }
             for (int base = hi - 1; base >= lo; base -= 64) {
                 const int j = base - lane;
-                const bool f = j >= lo && a[j].size >= p;
+                const bool f = j >= lo && a[j].size >= pv;
                 const unsigned long long m = __ballot(f);
-                if (f) Rs[nr + popc64(m & lt)] = j;
+                if (f) Rs[lo + nr + popc64(m & lt)] = j;
                 nr += popc64(m);
             }
             wave_lds_sync();
@@ -760,37 +808,49 @@ __device__ void qt_sort_wave(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, in
             int K = 0;
             for (int kb = 0; kb < mn; kb += 64) {
                 const int k = kb + lane;
-                const unsigned long long m = __ballot(k < mn && Ls[k] < Rs[k]);
+                const unsigned long long m = __ballot(k < mn && Ls[lo + k] < Rs[lo + k]);
                 K += popc64(m);
                 if (m != ~0ull) break;   // the predicate holds on a prefix of k
             }
             for (int k = lane; k < K; k += 64) {
-                const int li = Ls[k], ri = Rs[k];
+                const int li = Ls[lo + k], ri = Rs[lo + k];
                 const QtItem x = a[li], y = a[ri];
                 a[li] = y;
                 a[ri] = x;
             }
             wave_lds_sync();
             int cut;
-            if (K == 0) cut = Ls[0];
+            if (K == 0) cut = Ls[lo];
             else {
-                const int c1 = K < nl ? Ls[K] : hi;
-                const int c2 = Rs[K - 1];
+                const int c1 = K < nl ? Ls[lo + K] : hi;
+                const int c2 = Rs[lo + K - 1];
                 cut = c1 < c2 ? c1 : c2;
             }
-            if (lane == 0) {
-                stk[3 * sp] = lo; stk[3 * sp + 1] = cut; stk[3 * sp + 2] = depth;
-                stk[3 * sp + 3] = cut; stk[3 * sp + 4] = hi; stk[3 * sp + 5] = depth;
+            // children: > 16 go to the next round, the rest are final segments now
+            const int clo[2] = {lo, cut}, chi[2] = {cut, hi};
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                if (chi[c] - clo[c] > 16) {
+                    if (lane == 0) {
+                        const int idx = atomicAdd(&s_cnt[1], 1);
+                        nxt[3 * idx] = clo[c]; nxt[3 * idx + 1] = chi[c]; nxt[3 * idx + 2] = depth;
+                    }
+                } else {
+                    for (int i = clo[c] + lane; i < chi[c]; i += 64) { seg_lo[i] = clo[c]; seg_len[i] = chi[c] - clo[c]; }
+                }
             }
-            sp += 2;
             wave_lds_sync();
-            continue;
         }
-        for (int i = lo + lane; i < hi; i += 64) { seg_lo[i] = lo; seg_len[i] = hi - lo; }
-        wave_lds_sync();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_cnt[0] = s_cnt[1];
+            s_cnt[1] = 0;
+        }
+        int* t = cur; cur = nxt; nxt = t;
+        __syncthreads();
     }
     // final insertion pass == stable sort inside each final segment
-    for (int i = lane; i < n; i += 64) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const QtItem v = a[i];
         if (seg_len[i] < 0) { tmp[i] = v; continue; }
         const int lo = seg_lo[i], hi = lo + seg_len[i];
@@ -801,9 +861,9 @@ __device__ void qt_sort_wave(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, in
         }
         tmp[lo + r] = v;
     }
-    wave_lds_sync();
-    for (int i = lane; i < n; i += 64) a[i] = tmp[i];
-    wave_lds_sync();
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = tmp[i];
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
@@ -823,7 +883,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     uint32_t* lds_T = lds_P + PTC;
     __shared__ int tmp[16];
     __shared__ int s_n, s_ndiv, s_state, s_proc, s_fail;
-    __shared__ int stk[3 * 64];
+    __shared__ int s_sortcnt[2];
     __shared__ int rc[MAX_ROOTS];
 
     const int f = blockIdx.x, l = blockIdx.y;   // level-major grid: level-0 trees start first
@@ -841,6 +901,11 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     const uint32_t* fslots = slots + (long long)f * g.slot_frame;
 
     QT_STAMP(0);
+    int p2_round = 0;
+    (void)p2_round;
+#ifdef ORB_QT_STAMPS
+    const unsigned long long qt_t0 = __builtin_amdgcn_s_memtime();
+#endif
     // ---- gather candidates in cell raster order (DetectFAST push_back order).  Pass 1: total count;
     //      the arrays live in LDS when they fit.  Pass 2: one lane per cell copies its points.
     int n_total = 0;
@@ -892,23 +957,64 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
         const float dx = (float)kp_x(k) - (float)L.rx;   // keypoint.pt.x - roi.x (float)
         return (int)((double)dx / L.hx);
     };
-    if (w == 0) {
+    // every wave partitions a contiguous quarter (root ids kept in registers between the passes);
+    // quarter q's base offset per root = that root's count over quarters < q -> stable overall
+    __shared__ int s_rcnt[4][MAX_ROOTS];
+    constexpr int QT_RPL = 32;   // points per lane held in registers (fallback loop past that)
+    const int qlen = (n_src + nw - 1) / nw;
+    const int q0 = min(n_src, w * qlen), q1 = min(n_src, q0 + qlen);
+    int rid[QT_RPL];
+    {
         int counts[MAX_ROOTS];
         for (int r = 0; r < R; r++) counts[r] = 0;
-        for (int b = 0; b < n_src; b += 64) {
-            const int j = b + lane_id();
-            const int r = j < n_src ? root_of(P[j]) : -1;
-            if (j < n_src && (r < 0 || r >= R)) atomicOr(fault, FAULT_QT_ROOT);
+#pragma unroll
+        for (int t = 0; t < QT_RPL; t++) {
+            const int j = q0 + 64 * t + lane_id();
+            int r = -1;
+            if (j < q1) {
+                r = root_of(P[j]);
+                if (r < 0 || r >= R) atomicOr(fault, FAULT_QT_ROOT);
+            }
+            rid[t] = r;
             for (int q = 0; q < R; q++) counts[q] += popc64(__ballot(r == q));
         }
+        for (int b = q0 + 64 * QT_RPL; b < q1; b += 64) {   // quarters longer than 64*QT_RPL points
+            const int j = b + lane_id();
+            const int r = j < q1 ? root_of(P[j]) : -1;
+            for (int q = 0; q < R; q++) counts[q] += popc64(__ballot(r == q));
+        }
+        if (lane_id() == 0)
+            for (int q = 0; q < R; q++) s_rcnt[w][q] = counts[q];
+    }
+    __syncthreads();
+    {
         int o[MAX_ROOTS];
         int acc = 0;
-        for (int q = 0; q < R; q++) { o[q] = acc; acc += counts[q]; }
-        if (lane_id() == 0) for (int q = 0; q < R; q++) rc[q] = counts[q];
-        for (int b = 0; b < n_src; b += 64) {
+        for (int q = 0; q < R; q++) {
+            int before = 0, tot = 0;
+            for (int v = 0; v < nw; v++) {
+                tot += s_rcnt[v][q];
+                if (v < w) before += s_rcnt[v][q];
+            }
+            o[q] = acc + before;
+            acc += tot;
+            if (threadIdx.x == 0) rc[q] = tot;
+        }
+#pragma unroll
+        for (int t = 0; t < QT_RPL; t++) {
+            const int j = q0 + 64 * t + lane_id();
+            const uint32_t k = j < q1 ? P[j] : 0;
+            const int r = rid[t];
+            for (int q = 0; q < R; q++) {
+                const unsigned long long m = __ballot(r == q);
+                if (r == q) T[o[q] + popc64(m & lanemask_lt())] = k;
+                o[q] += popc64(m);
+            }
+        }
+        for (int b = q0 + 64 * QT_RPL; b < q1; b += 64) {
             const int j = b + lane_id();
-            const uint32_t k = j < n_src ? P[j] : 0;
-            const int r = j < n_src ? root_of(k) : -1;
+            const uint32_t k = j < q1 ? P[j] : 0;
+            const int r = j < q1 ? root_of(k) : -1;
             for (int q = 0; q < R; q++) {
                 const unsigned long long m = __ballot(r == q);
                 if (r == q) T[o[q] + popc64(m & lanemask_lt())] = k;
@@ -1028,15 +1134,13 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             const int m = s_ndiv;
             for (int j = threadIdx.x; j < m; j += blockDim.x) prev[j] = divs[j];
             __syncthreads();
-            if (w == 0) {
-                int* seg = reinterpret_cast<int*>(cc);   // cc is free until the splits below
-                qt_sort_wave(prev, m, ia, ib, seg, seg + NC, divs, stk);
+            QT_STAMP(40 + 4 * min(p2_round, 5));
+            {
+                int* seg = reinterpret_cast<int*>(cc);   // cc (4 NC ints) is free until the splits below
+                qt_sort_block(prev, m, ia, ib, seg, seg + NC, divs, seg + 2 * NC, NC / 3, s_sortcnt);
             }
-            __syncthreads();
-            for (int j = w; j < m; j += nw) {
-                const int4 c = qt_wave_split(na[prev[j].node], P, T);
-                if (lane_id() == 0) cc[j] = c;
-            }
+            QT_STAMP(41 + 4 * min(p2_round, 5));
+            for (int j = threadIdx.x; j < m; j += blockDim.x) cc[j] = qt_thread_count(na[prev[j].node], P);
             for (int i = threadIdx.x; i < n; i += blockDim.x) ia[i] = 0;   // erased flags
             if (threadIdx.x == 0) s_proc = m;
             __syncthreads();
@@ -1054,7 +1158,13 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             }
             __syncthreads();
             const int proc = s_proc;
+            QT_STAMP(42 + 4 * min(p2_round, 5));
             for (int j = threadIdx.x; j < proc; j += blockDim.x) ia[prev[j].node] = 1;
+            // split the processed prefix only: small nodes one thread each, large ones one wave each
+            for (int j = threadIdx.x; j < proc; j += blockDim.x)
+                if (na[prev[j].node].cnt <= QT_THREAD_SPLIT_MAX) qt_thread_split(na[prev[j].node], cc[j], P, T);
+            for (int j = w; j < proc; j += nw)
+                if (na[prev[j].node].cnt > QT_THREAD_SPLIT_MAX) (void)qt_wave_split(na[prev[j].node], P, T);
             __syncthreads();
             int ne_total = 0;
             {
@@ -1103,6 +1213,8 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                 if (n_new >= nfeat || n_new == n || s_fail) s_state = 2;
             }
             __syncthreads();
+            QT_STAMP(43 + 4 * min(p2_round, 5));
+            p2_round++;
             QtNode* t = na; na = nb; nb = t;
         }
     }
@@ -1128,6 +1240,12 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     }
     if (threadIdx.x == 0) *scnt = min(n, L.out_cap);
     QT_STAMP(63);
+#ifdef ORB_QT_STAMPS
+    if (threadIdx.x == 0 && f * g.nlevels + l < 4096) {
+        g_qt_wg[2 * (f * g.nlevels + l)] = qt_t0;
+        g_qt_wg[2 * (f * g.nlevels + l) + 1] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1305,10 +1423,10 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     }   // keypoints of this wavefront
 }
 
-__global__ __launch_bounds__(64) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
-    __shared__ int stk[3 * 64];
-    qt_sort_wave(items, n, scratch, scratch + n, scratch + 2 * n, scratch + 3 * n,
-                 reinterpret_cast<QtItem*>(scratch + 4 * n), stk);
+__global__ __launch_bounds__(256) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
+    __shared__ int s_cnt[2];
+    qt_sort_block(items, n, scratch, scratch + n, scratch + 2 * n, scratch + 3 * n,
+                  reinterpret_cast<QtItem*>(scratch + 4 * n), scratch + 6 * n, n / 3 + 2, s_cnt);
 }
 
 }  // namespace orbamd
@@ -1943,12 +2061,12 @@ int orbx_debug_qt_sort(const int32_t* sizes, int n, int32_t* perm) {
     for (int i = 0; i < n; i++) h[i] = QtItem{sizes[i], i};
     DevBuf d;
     int rc;
-    if ((rc = d.reserve((size_t)n * sizeof(QtItem) + (size_t)n * 6 * sizeof(int) + 64))) return rc;
+    if ((rc = d.reserve((size_t)n * sizeof(QtItem) + ((size_t)n * 8 + 16) * sizeof(int) + 64))) return rc;
     QtItem* items = d.as<QtItem>();
     int* scratch = reinterpret_cast<int*>(items + n);
     ORB_HIP_TRY(hipMemcpy(items, h.data(), n * sizeof(QtItem), hipMemcpyHostToDevice));
     // the kernel keeps items in global memory (same code path as LDS: generic pointers)
-    hipLaunchKernelGGL(qt_sort_test_kernel, dim3(1), dim3(64), 0, 0, items, n, scratch);
+    hipLaunchKernelGGL(qt_sort_test_kernel, dim3(1), dim3(256), 0, 0, items, n, scratch);
     ORB_HIP_TRY(hipGetLastError());
     ORB_HIP_TRY(hipMemcpy(h.data(), items, n * sizeof(QtItem), hipMemcpyDeviceToHost));
     d.release();
@@ -1973,6 +2091,7 @@ int orbx_debug_qt_stamps(unsigned long long* out) {
 #ifdef ORB_QT_STAMPS
     ORB_HIP_TRY(hipDeviceSynchronize());
     ORB_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), 64 * 8));
+    ORB_HIP_TRY(hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_qt_wg), 4096 * 2 * 8));
     return ORB_OK;
 #else
     (void)out;

@@ -19,7 +19,7 @@ ex = ORBextractor(ORBextractor.Parameters(nfeatures=2000))
 for _ in range(3):
     ex.extract_batch_device(frames)
 torch.cuda.synchronize()
-buf = (C.c_ulonglong * 64)()
+buf = (C.c_ulonglong * (64 + 8192))()
 lib().orbx_debug_qt_stamps.argtypes = [C.c_void_p]
 assert lib().orbx_debug_qt_stamps(C.cast(buf, C.c_void_p)) == 0
 v = list(buf)
@@ -35,3 +35,13 @@ while 3 + 2 * i < 63 and v[3 + 2 * i] > 0 and 4 + 2 * i < 64:
         break
     i += 1
 print("end", v[63] - t0, "(+", v[63] - prev, ")   [s_memtime ticks]")
+
+wg = np.array(list(buf)[64:64 + 2 * F * 8], dtype=np.int64).reshape(F, 8, 2)
+dur = wg[:, :, 1] - wg[:, :, 0]
+for l in range(8):
+    print(f"level {l}: WG ticks mean {dur[:, l].mean():8.0f} max {dur[:, l].max():8.0f}")
+
+for r in range(3):
+    a = list(buf)[40 + 4 * r:44 + 4 * r]
+    if a[0] and a[3] > a[0]:
+        print(f"phase-2 round {r}: sort {a[1] - a[0]} counts+stop {a[2] - a[1]} split+emit {a[3] - a[2]}")
