@@ -423,7 +423,7 @@ __device__ __forceinline__ void crop_commit(const CropSrc& c, int lane, const u3
 // One wavefront processes `cpw` consecutive (frame, cell) items of the XCD-swizzled order; item
 // i = f * ncells + cell.  LDS (sized per launch from the largest cell): the crop (zone + 3-px
 // apron), a zone map of corner strengths, a queue of pre-test passers and the ordered corner list.
-__global__ __launch_bounds__(64, 5) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
+__global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
@@ -456,26 +456,20 @@ __global__ __launch_bounds__(64, 5) void fast_cells_kernel(Geom g, const CellDev
         c.ndl = ((cd.zwzh & 0xffff) + 6 + 1 + 3) >> 2;   // LDS dwords per crop row
         return c;
     };
+    for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
     int f, ci;
-    CropSrc src = source(i_beg, cell, f, ci);
-    u32x2a4 pre[CROP_PF];
-    crop_prefetch(src, lane, pre);
-
-    for (int item = i_beg; item < i_end; item++) {
+    const CropSrc src = source(item, cell, f, ci);
     const int x0 = src.x0, y0 = src.y0;
     const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
-    crop_commit(src, lane, pre, crop, CSd);
+    {
+        u32x2a4 pre[CROP_PF];
+        crop_prefetch(src, lane, pre);   // all of the lane's loads in flight, then the LDS stores
+        crop_commit(src, lane, pre, crop, CSd);
+    }
     for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
     wave_lds_sync();
     if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
-    CellDev ncell;
-    int nf = f, nci = ci;
-    CropSrc nsrc = src;
-    if (item + 1 < i_end) {
-        nsrc = source(item + 1, ncell, nf, nci);
-        crop_prefetch(nsrc, lane, pre);
-    }
 
     const int tlo = min(th_ini, th_min);
     const us2 t2 = {(unsigned short)tlo, (unsigned short)tlo};
@@ -600,10 +594,6 @@ __global__ __launch_bounds__(64, 5) void fast_cells_kernel(Geom g, const CellDev
         FAST_STAMP(6, ((unsigned long long)cell.level << 48) | ((unsigned long long)nc << 16) | (unsigned)total);
     }
     wave_lds_sync();
-    cell = ncell;
-    f = nf;
-    ci = nci;
-    src = nsrc;
     }   // items
     FAST_STAMP(5, __builtin_amdgcn_s_memtime());
     FAST_STAMP(7, (unsigned long long)(i_end - i_beg));
@@ -1452,7 +1442,7 @@ struct orbx_extractor {
     size_t qt_lds = 0;
     FastLds fl;
     size_t fast_lds = 0;
-    int fast_cpw = 4;   // FAST cells per wavefront (crop loads pipelined one cell ahead)
+    int fast_cpw = 1;   // FAST cells per wavefront
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
