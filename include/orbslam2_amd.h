@@ -150,6 +150,40 @@ int orbm_search_for_triangulation(const orbm_tri_frame* kf1, const orbm_tri_fram
                                   const float* sigma2, int n_levels, int only_stereo,
                                   int32_t* match12, int32_t* nmatches);
 
+/* Stereo matching.  Replaces ComputeStereoMatches (src/ORBmatcher.cc:72-247, PatchDistance
+ * :60-68; called from Frame construction for stereo input, System.cc:458-461): per left keypoint the
+ * best right keypoint in the row band (+-2*scale[octave_R] rows), octave +-1 and disparity
+ * [0, bf/baseline], Hamming < (TH_HIGH+TH_LOW)/2; then 11x11 SAD over +-5 px on the unblurred
+ * level of the left octave, parabola refinement, and the median-distance outlier filter.
+ * Outputs uright[i] / depth[i] (-1 = no match), one per left keypoint.
+ * A view is one frame: its keypoints (level-0 coordinates, cv::KeyPoint layout), descriptors and
+ * unblurred pyramid levels (GetImagePyramid()). */
+typedef struct orbm_stereo_view {
+    int32_t n;
+    const orbx_keypoint* kps;
+    const uint8_t* desc;                 /* n x 32 */
+    int32_t n_levels;
+    const uint8_t* const* level;         /* n_levels level images */
+    const int32_t* level_rows;
+    const int32_t* level_cols;
+    const int32_t* level_step;           /* bytes per row */
+} orbm_stereo_view;
+
+int orbm_compute_stereo_matches(const orbm_stereo_view* left, const orbm_stereo_view* right,
+                                const float* scale_factors, const float* inv_scale_factors, float bf,
+                                float baseline, float* uright, float* depth);
+
+/* Batched device version on the frames of two extractors' last batches (left frame f with right
+ * frame f; both extractors with the same Parameters and image size).  Keypoints / descriptors /
+ * counts are those batches' outputs.  d_uright / d_depth: n_frames * cap floats, slot f*cap + i.
+ * Enqueue only, on `stream` (NULL = default stream). */
+int orbx_stereo_matches_batch_device(orbx_extractor* left, orbx_extractor* right, int n_frames,
+                                     const orbx_keypoint* d_kps_l, const uint8_t* d_desc_l,
+                                     const int32_t* d_counts_l, const orbx_keypoint* d_kps_r,
+                                     const uint8_t* d_desc_r, const int32_t* d_counts_r, int cap,
+                                     float bf, float baseline, float* d_uright, float* d_depth,
+                                     void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Local bundle adjustment.  Replaces Optimizer::LocalBundleAdjustment (include/Optimizer.h:47,
  * src/Optimizer.cc:491-736) from the vertex/edge setup (:540-631) onwards: the caller

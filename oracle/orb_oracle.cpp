@@ -16,7 +16,8 @@
  *                  cv::resize INTER_LINEAR 8U (fixed point, SIMD vertical rounding),
  *                  cv::FAST TYPE_9_16 + cornerScore<16> + 3x3 NMS, GaussianBlur 7x7 sigma 2
  *                  bit-exact Q8 (error-diffused taps) REFLECT_101, cv::fastAtan2, cvRound.
- *   ORBmatcher     src/ORBmatcher.cc:384-404 (CheckDistEpipolarLine), :477-507 (best /
+ *   ORBmatcher     src/ORBmatcher.cc:60-247 (PatchDistance, ComputeStereoMatches),
+ *                  :384-404 (CheckDistEpipolarLine), :477-507 (best /
  *                  second-best loop), :768-866 (SearchForTriangulation), :1449-1457.
  *   LocalBA        src/Optimizer.cc:491-736 and the vendored g2o it drives:
  *                  core/optimization_algorithm_levenberg.cpp:61-189, core/sparse_optimizer.cpp
@@ -46,6 +47,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <list>
 #include <vector>
 
@@ -1211,6 +1213,101 @@ int oracle_search_for_triangulation(const orbm_tri_frame* f1, const orbm_tri_fra
 }
 
 // Optimizer::LocalBundleAdjustment from the vertex/edge setup on (Optimizer.cc:540-735).
+// ComputeStereoMatches (src/ORBmatcher.cc:72-247) with PatchDistance (:60-68).  Rounding helpers as
+// the reference's Round / RoundUp / RoundDn (:50-52): std::round (half away from zero), ceil, floor.
+// The empty-match case reads distIndices[0] in the reference (undefined); here it leaves all
+// results as computed.
+int oracle_compute_stereo_matches(const orbm_stereo_view* L, const orbm_stereo_view* R, const float* scaleFactors,
+                                  const float* invScaleFactors, float bf, float baseline, float* uright,
+                                  float* depth) {
+    const int TH_HIGH = 100, TH_LOW = 50, PR = 5, PS = 11, SR = 5;
+    const int nL = L->n, nR = R->n;
+    for (int i = 0; i < nL; i++) { uright[i] = -1.f; depth[i] = -1.f; }
+    auto px = [](const orbm_stereo_view* v, int lvl, int y, int x) -> int {
+        return v->level[lvl][(size_t)y * v->level_step[lvl] + x];
+    };
+    // row table (:86-100): right keypoint indices per image row, ascending
+    const int nrows = L->level_rows[0];
+    std::vector<std::vector<int>> rowIndices(nrows);
+    for (int iR = 0; iR < nR; iR++) {
+        const orbx_keypoint& k = R->kps[iR];
+        const float r = 2.f * scaleFactors[k.octave];
+        const int miny = (int)std::floor(k.y - r), maxy = (int)std::ceil(k.y + r);
+        for (int y = miny; y <= maxy; y++)
+            if (y >= 0 && y < nrows) rowIndices[y].push_back(iR);
+    }
+    const float minZ = baseline, mind = 0, maxd = bf / minZ;
+    const int TH_ORB_DIST = (TH_HIGH + TH_LOW) / 2;
+    const float eps = 0.01f;
+    std::vector<std::pair<int, int>> distIndices;
+    int distances[2 * SR + 1];
+    for (int iL = 0; iL < nL; iL++) {
+        const orbx_keypoint& kL = L->kps[iL];
+        const int octaveL = kL.octave;
+        const float vL = kL.y, uL = kL.x;
+        const int row = (int)vL;
+        if (row < 0 || row >= nrows) continue;
+        const std::vector<int>& cand = rowIndices[row];
+        if (cand.empty()) continue;
+        const float minu = uL - maxd, maxu = uL - mind;
+        if (maxu < 0) continue;
+        int bestHam = TH_HIGH, bestIdxR = 0;
+        for (int iR : cand) {
+            const orbx_keypoint& kR = R->kps[iR];
+            if (kR.octave < octaveL - 1 || kR.octave > octaveL + 1) continue;
+            const float uR = kR.x;
+            if (uR >= minu && uR <= maxu) {
+                const int d = hamming(L->desc + 32 * (size_t)iL, R->desc + 32 * (size_t)iR);
+                if (d < bestHam) { bestHam = d; bestIdxR = iR; }
+            }
+        }
+        if (!(bestHam < TH_ORB_DIST)) continue;
+        // sub-pixel correlation on the left octave's level (:170-236)
+        const float sf = invScaleFactors[octaveL];
+        const int suL = (int)std::round(sf * kL.x);
+        const int svL = (int)std::round(sf * kL.y);
+        const int suR = (int)std::round(sf * R->kps[bestIdxR].x);
+        const int colsR = R->level_cols[octaveL];
+        if (suR + SR - PR < 0 || suR + SR + PR + 1 >= colsR) continue;
+        int bestSad = INT32_MAX, bestdx = 0;
+        for (int dx = -SR; dx <= SR; dx++) {
+            const int sub = px(L, octaveL, svL, suL) - px(R, octaveL, svL, suR + dx);
+            int sum = 0;
+            for (int y = 0; y < PS; y++)
+                for (int x = 0; x < PS; x++)
+                    sum += std::abs(px(L, octaveL, svL - PR + y, suL - PR + x) -
+                                    px(R, octaveL, svL - PR + y, suR + dx - PR + x) - sub);
+            if (sum < bestSad) { bestSad = sum; bestdx = dx; }
+            distances[SR + dx] = sum;
+        }
+        if (bestdx == -SR || bestdx == SR) continue;
+        const int d1 = distances[SR + bestdx - 1], d2 = distances[SR + bestdx], d3 = distances[SR + bestdx + 1];
+        const float deltaR = (d1 - d3) / (2.f * (d1 + d3 - 2.f * d2));
+        if (deltaR < -1 || deltaR > 1) continue;
+        float bestuR = scaleFactors[octaveL] * (suR + bestdx + deltaR);
+        float disparity = uL - bestuR;
+        if (disparity >= mind && disparity < maxd) {
+            if (disparity <= 0) { disparity = eps; bestuR = uL - eps; }
+            depth[iL] = bf / disparity;
+            uright[iL] = bestuR;
+            distIndices.push_back(std::make_pair(bestSad, iL));
+        }
+    }
+    if (distIndices.empty()) return 0;
+    std::sort(distIndices.begin(), distIndices.end(), std::greater<std::pair<int, int>>());
+    const int m = std::max((int)distIndices.size() / 2 - 1, 0);
+    const int median = distIndices[m].first;
+    const float thDist = 1.5f * 1.4f * median;
+    int n = 0;
+    for (const auto& v : distIndices) {
+        if (v.first < thDist) break;
+        uright[v.second] = -1;
+        depth[v.second] = -1;
+    }
+    for (int i = 0; i < nL; i++) n += uright[i] >= 0;
+    return n;
+}
+
 int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile int32_t* stop) {
     BA ba;
     ba.P = pr->n_poses; ba.N = pr->n_points; ba.E = pr->n_edges;

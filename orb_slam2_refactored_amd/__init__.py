@@ -7,8 +7,8 @@ Host mirrors of the reference's interfaces (tiantianxuabc/ORB_SLAM2_Refactored):
 All compute runs in liborbslam2_amd.so (HIP kernels behind include/orbslam2_amd.h).
 """
 from .extractor import ORBextractor, KP_DTYPE
-from .matcher import ORBmatcher
+from .matcher import ORBmatcher, ComputeStereoMatches
 from . import optimizer
-from .synth import synth_image, shifted_pair
+from .synth import synth_image, shifted_pair, stereo_pair
 
-__all__ = ["ORBextractor", "ORBmatcher", "optimizer", "KP_DTYPE", "synth_image", "shifted_pair"]
+__all__ = ["ORBextractor", "ORBmatcher", "ComputeStereoMatches", "optimizer", "KP_DTYPE", "synth_image", "shifted_pair", "stereo_pair"]

@@ -24,6 +24,12 @@ class TriFrame(C.Structure):
                 ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("indices", C.c_void_p)]
 
 
+class StereoView(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("n_levels", C.c_int32),
+                ("level", C.c_void_p), ("level_rows", C.c_void_p), ("level_cols", C.c_void_p),
+                ("level_step", C.c_void_p)]
+
+
 class BAProblem(C.Structure):
     _fields_ = [("n_poses", C.c_int32), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
                 ("pose_fixed", C.c_void_p), ("n_points", C.c_int32), ("points", C.c_void_p),
@@ -63,6 +69,10 @@ SIGNATURES = {
     "orbm_bf_match": (C.c_int, [VP, C.c_int, VP, C.c_int, C.c_float, C.c_int, VP, VP, VP, VP]),
     "orbm_search_for_triangulation": (C.c_int, [C.POINTER(TriFrame), C.POINTER(TriFrame), VP, VP, VP, VP,
                                                 C.c_int, C.c_int, VP, C.POINTER(I32)]),
+    "orbm_compute_stereo_matches": (C.c_int, [C.POINTER(StereoView), C.POINTER(StereoView), VP, VP, C.c_float,
+                                              C.c_float, VP, VP]),
+    "orbx_stereo_matches_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, VP, VP, VP, C.c_int, C.c_float,
+                                                   C.c_float, VP, VP, VP]),
     "orbba_local_ba": (C.c_int, [C.POINTER(BAProblem), C.POINTER(BAResult), VP, C.c_int]),
     "orbx_profile_enable": (C.c_int, [VP, C.c_int]),
     "orbx_profile_read": (C.c_int, [VP, VP, VP]),

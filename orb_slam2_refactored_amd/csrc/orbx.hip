@@ -24,6 +24,7 @@
 
 #include "common.h"
 #include "qt_sort.h"
+#include "stereo.h"
 
 namespace orbamd {
 
@@ -1453,6 +1454,7 @@ struct orbx_extractor {
     DevBuf d_pyr, d_slots, d_cellcnt, d_P, d_T, d_sel, d_selcnt, d_fault;
     // single-frame host API buffers
     DevBuf d_img, d_kps, d_desc, d_counts;
+    DevBuf d_stereo_sad;   // stereo scratch (orbx_stereo_matches_batch_device)
     // stage profiling (events on the launch stream)
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[4];
@@ -1838,7 +1840,7 @@ int orbx_destroy(orbx_extractor* h) {
     (void)hipSetDevice(h->device);
     DevBuf* bufs[] = {&h->d_cells, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
-                      &h->d_counts};
+                      &h->d_counts, &h->d_stereo_sad};
     for (DevBuf* b : bufs) b->release();
     for (auto& v : h->prof_ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -2062,6 +2064,56 @@ int orbx_debug_qt_sort(const int32_t* sizes, int n, int32_t* perm) {
     d.release();
     for (int i = 0; i < n; i++) perm[i] = h[i].node;
     return ORB_OK;
+}
+
+static void stereo_side(const orbx_extractor* h, StereoSide& s) {
+    std::memset(&s, 0, sizeof(s));
+    const Geom& g = h->geom;
+    s.nlevels = g.nlevels;
+    s.lvl0 = h->last_in;
+    s.fstride0 = h->last_fstride;
+    s.step0 = (int)h->last_step;
+    s.pyr = h->d_pyr.as<uint8_t>();
+    s.pyr_frame = g.pyr_frame_bytes;
+    for (int l = 0; l < g.nlevels; l++) {
+        s.off[l] = g.lv[l].off;
+        s.stride[l] = g.lv[l].stride;
+        s.rows[l] = g.lv[l].h;
+        s.cols[l] = g.lv[l].w;
+    }
+}
+
+int orbx_stereo_matches_batch_device(orbx_extractor* left, orbx_extractor* right, int n_frames,
+                                     const orbx_keypoint* d_kps_l, const uint8_t* d_desc_l,
+                                     const int32_t* d_counts_l, const orbx_keypoint* d_kps_r,
+                                     const uint8_t* d_desc_r, const int32_t* d_counts_r, int cap, float bf,
+                                     float baseline, float* d_uright, float* d_depth, void* stream) {
+    ORB_CHECK_ARG(left && right && d_kps_l && d_desc_l && d_counts_l && d_kps_r && d_desc_r && d_counts_r && d_uright &&
+                      d_depth, "null argument");
+    ORB_CHECK_ARG(n_frames > 0 && cap > 0, "bad sizes");
+    ORB_CHECK_ARG(left->last_in && right->last_in && left->last_frames >= n_frames && right->last_frames >= n_frames,
+                  "both extractors need a batch of >= n_frames frames first");
+    ORB_CHECK_ARG(left->g_rows == right->g_rows && left->g_cols == right->g_cols &&
+                      left->p.nlevels == right->p.nlevels && left->p.scaleFactor == right->p.scaleFactor,
+                  "left / right extractors differ in image size or pyramid parameters");
+    ORB_CHECK_ARG(left->p.nlevels <= ST_MAX_LEVELS, "too many levels");
+    std::lock_guard<std::mutex> lk(left->mu);
+    ORB_HIP_TRY(hipSetDevice(left->device));
+    int rc;
+    if ((rc = left->d_stereo_sad.reserve((size_t)n_frames * cap * sizeof(int32_t)))) return rc;
+    StereoSide L, R;
+    stereo_side(left, L);
+    stereo_side(right, R);
+    StereoParams sp;
+    std::memset(&sp, 0, sizeof(sp));
+    for (int l = 0; l < left->p.nlevels; l++) {
+        sp.scale[l] = left->scale[l];
+        sp.inv_scale[l] = left->inv_scale[l];
+    }
+    sp.bf = bf;
+    sp.baseline = baseline;
+    return launch_stereo(L, R, sp, n_frames, d_kps_l, d_desc_l, d_counts_l, 0, d_kps_r, d_desc_r, d_counts_r, 0, cap,
+                         d_uright, d_depth, left->d_stereo_sad.as<int32_t>(), (hipStream_t)stream);
 }
 
 int orbx_debug_fast_stamps(unsigned long long* out, int n_words) {

@@ -80,3 +80,55 @@ class ORBmatcher:
         out = out[:n1]
         idx1 = np.nonzero(out >= 0)[0]
         return [(int(i), int(out[i])) for i in idx1], out
+
+
+def _stereo_view(kps, desc, pyramid):
+    from ._lib import KP_DTYPE, StereoView
+    kps = np.ascontiguousarray(kps)
+    if kps.dtype != KP_DTYPE:
+        kps = kps.view(KP_DTYPE).reshape(-1)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    levels = [np.ascontiguousarray(im, np.uint8) for im in pyramid]
+    ptrs = (C.c_void_p * len(levels))(*[im.ctypes.data for im in levels])
+    rows = np.array([im.shape[0] for im in levels], np.int32)
+    cols = np.array([im.shape[1] for im in levels], np.int32)
+    step = np.array([im.strides[0] for im in levels], np.int32)
+    v = StereoView(len(kps), kps.ctypes.data, desc.ctypes.data, len(levels), C.cast(ptrs, C.c_void_p),
+                   rows.ctypes.data, cols.ctypes.data, step.ctypes.data)
+    return v, (kps, desc, levels, ptrs, rows, cols, step)
+
+
+def ComputeStereoMatches(keypointsL, descriptorsL, pyramidL, keypointsR, descriptorsR, pyramidR, scaleFactors,
+                         invScaleFactors, bf: float, baseline: float):
+    """ComputeStereoMatches (src/ORBmatcher.cc:72-247): keypoints as KP_DTYPE arrays (level-0
+    coordinates), descriptors [N,32] u8, pyramids = lists of unblurred level images
+    (ORBextractor.GetImagePyramid()).  Returns (uright, depth), float32 [N_left], -1 = no match."""
+    vl, keep_l = _stereo_view(keypointsL, descriptorsL, pyramidL)
+    vr, keep_r = _stereo_view(keypointsR, descriptorsR, pyramidR)
+    n = vl.n
+    ur = np.full(n, -1, np.float32)
+    dp = np.full(n, -1, np.float32)
+    s = np.ascontiguousarray(scaleFactors, np.float32)
+    inv = np.ascontiguousarray(invScaleFactors, np.float32)
+    check(lib().orbm_compute_stereo_matches(C.byref(vl), C.byref(vr), ptr(s), ptr(inv), C.c_float(bf),
+                                            C.c_float(baseline), ptr(ur), ptr(dp)), "orbm_compute_stereo_matches")
+    return ur, dp
+
+
+def stereo_matches_batch_device(extractor_l, extractor_r, outs_l, outs_r, bf: float, baseline: float, out=None,
+                                stream=None):
+    """Batched ComputeStereoMatches on the frames of two extractors' last batches.  outs_l / outs_r are
+    the (kps, desc, counts) tensors those extract_batch_device calls returned.  Returns float32
+    tensors (uright, depth) of shape [F, cap]."""
+    import torch
+    kl, dl, cl = outs_l
+    kr, dr, cr = outs_r
+    F, cap = kl.shape[0], kl.shape[1]
+    if out is None:
+        out = (torch.empty((F, cap), dtype=torch.float32, device=kl.device),
+               torch.empty((F, cap), dtype=torch.float32, device=kl.device))
+    check(lib().orbx_stereo_matches_batch_device(extractor_l._h, extractor_r._h, F, tptr(kl), tptr(dl), tptr(cl),
+                                                 tptr(kr), tptr(dr), tptr(cr), cap, C.c_float(bf),
+                                                 C.c_float(baseline), tptr(out[0]), tptr(out[1]), stream_ptr(stream)),
+          "orbx_stereo_matches_batch_device")
+    return out

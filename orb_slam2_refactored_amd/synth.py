@@ -122,3 +122,24 @@ def make_ba_problem(seed: int = 0, n_kf: int = 20, n_pts: int = 3000, n_fixed: i
                 edge_obs=np.array(obs, np.float64), edge_inv_sigma2=np.array(info, np.float64),
                 edge_cam=np.array(camv, np.float64), gt_R=np.array([r.reshape(-1) for r in R_true]),
                 gt_t=np.array(t_true), gt_points=pts)
+
+
+STEREO_Z = (5.0, 7.0, 10.0, 14.0, 20.0, 28.0, 40.0, 56.0)   # SURVEY.md §8d C3 band depths (m)
+
+
+def stereo_pair(seed: int, width: int = 1242, height: int = 375, bf: float = KITTI["bf"]):
+    """C3 pair: L = G(seed, W, H); R = L warped by 8 vertical bands at depths STEREO_Z with disparity
+    round(bf / Z) (R[y, x] = L[y, x + d]); pixels with no source (x + d >= W) are noise-filled; fresh
+    noise U{-3..3} on R.  Returns (L, R, band_depth_of_right_column)."""
+    L = synth_image(seed, width, height)
+    rng = np.random.default_rng(seed + 2000)
+    R = np.empty_like(L, dtype=np.int16)
+    zcol = np.empty(width, np.float32)
+    edges = np.linspace(0, width, len(STEREO_Z) + 1).astype(int)
+    for b, z in enumerate(STEREO_Z):
+        d = int(round(bf / z))
+        for x in range(edges[b], edges[b + 1]):
+            zcol[x] = z
+            R[:, x] = L[:, x + d] if x + d < width else rng.integers(0, 256, size=height)
+    R += rng.integers(-3, 4, size=R.shape).astype(np.int16)
+    return L, np.clip(R, 0, 255).astype(np.uint8), zcol

@@ -220,3 +220,34 @@ def std_sort_perm(sizes):
     perm = np.zeros(len(sizes), np.int32)
     lib().oracle_std_sort_sizes(ptr(sizes), len(sizes), ptr(perm))
     return perm
+
+
+class StereoView(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("n_levels", C.c_int32),
+                ("level", C.c_void_p), ("level_rows", C.c_void_p), ("level_cols", C.c_void_p),
+                ("level_step", C.c_void_p)]
+
+
+def _stereo_view(keep, kps, desc, pyramid):
+    kps = np.ascontiguousarray(kps)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    levels = [np.ascontiguousarray(im, np.uint8) for im in pyramid]
+    ptrs = (C.c_void_p * len(levels))(*[im.ctypes.data for im in levels])
+    rows = np.array([im.shape[0] for im in levels], np.int32)
+    cols = np.array([im.shape[1] for im in levels], np.int32)
+    step = np.array([im.strides[0] for im in levels], np.int32)
+    keep.arrs += [kps, desc, levels, ptrs, rows, cols, step]
+    return StereoView(len(kps), kps.ctypes.data, desc.ctypes.data, len(levels), C.cast(ptrs, C.c_void_p),
+                      rows.ctypes.data, cols.ctypes.data, step.ctypes.data)
+
+
+def compute_stereo_matches(kpsL, descL, pyrL, kpsR, descR, pyrR, scale, inv_scale, bf, baseline):
+    """ComputeStereoMatches oracle (src/ORBmatcher.cc:72-247) -> (uright, depth)."""
+    keep = _Keep()
+    vl = _stereo_view(keep, kpsL, descL, pyrL)
+    vr = _stereo_view(keep, kpsR, descR, pyrR)
+    ur = np.zeros(vl.n, np.float32)
+    dp = np.zeros(vl.n, np.float32)
+    lib().oracle_compute_stereo_matches(C.byref(vl), C.byref(vr), keep(scale, np.float32), keep(inv_scale, np.float32),
+                                        C.c_float(bf), C.c_float(baseline), ptr(ur), ptr(dp))
+    return ur, dp
