@@ -103,6 +103,41 @@ def cpu_ba_baseline(prob, budget_s=6.0):
     return {"iters_per_s": iters / dt, "ms_per_call": 1e3 * dt / calls, "calls": calls, "cores": 1, "kind": "port"}
 
 
+def stereo_leg(dev, local, pairs=64, steps=5):
+    """configs[2]-shaped secondary measurement: 1242x375 stereo pairs (8 depth bands), both sides
+    extracted in one batch each, then ComputeStereoMatches per pair on the on-device pyramids."""
+    import torch
+    from orb_slam2_refactored_amd import ORBextractor
+    from orb_slam2_refactored_amd.matcher import stereo_matches_batch_device
+    from orb_slam2_refactored_amd.synth import KITTI, stereo_pair
+    pool = [stereo_pair(7000 + i) for i in range(8)]
+    Ls = torch.from_numpy(np.stack([pool[i % 8][0] for i in range(pairs)])).to(dev)
+    Rs = torch.from_numpy(np.stack([pool[i % 8][1] for i in range(pairs)])).to(dev)
+    exl = ORBextractor(ORBextractor.Parameters(2000), device=local)
+    exr = ORBextractor(ORBextractor.Parameters(2000), device=local)
+    bf, base = KITTI["bf"], KITTI["bf"] / KITTI["fx"]
+    outl = exl.extract_batch_device(Ls)
+    outr = exr.extract_batch_device(Rs)
+    out = stereo_matches_batch_device(exl, exr, outl, outr, bf, base)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        exl.extract_batch_device(Ls, *outl)
+        exr.extract_batch_device(Rs, *outr)
+        stereo_matches_batch_device(exl, exr, outl, outr, bf, base, out=out)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        stereo_matches_batch_device(exl, exr, outl, outr, bf, base, out=out)
+    torch.cuda.synchronize()
+    dts = (time.perf_counter() - t1) / steps
+    matched = float((out[1] > 0).sum().item()) / pairs
+    return {"workload": "C3-shaped: 1242x375 stereo pairs, 2000 features, extract L+R + ComputeStereoMatches",
+            "pairs_per_step": pairs, "pairs_per_s": pairs / dt, "stereo_match_ms_per_step": 1e3 * dts,
+            "matched_per_pair": matched}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,6 +149,7 @@ def main():
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ba", action="store_true")
+    ap.add_argument("--no-stereo", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -258,6 +294,9 @@ def main():
                              "edges": int(len(prob["edge_point"]))}
         if world == 1 and not args.no_cpu_baseline:
             result["localba"]["cpu_baseline"] = cpu_ba_baseline(prob)
+
+    if rank == 0 and not args.no_stereo:
+        result["stereo"] = stereo_leg(dev, local)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(frames_np[:4], args.nfeatures)

@@ -159,6 +159,39 @@ private:
     bool checkOri_;
 };
 
+// void ComputeStereoMatches(keypointsL, descriptorsL, pyramidL, keypointsR, descriptorsR, pyramidR,
+//                           scaleFactors, invScaleFactors, camera, uright, depth)  (src/ORBmatcher.cc:72-247)
+// on raw arrays: keypoints in cv::KeyPoint layout, 32-byte descriptors, pyramid level pointers.
+struct PyramidView {
+    std::vector<const uint8_t*> level;
+    std::vector<int32_t> rows, cols, step;
+};
+
+inline void ComputeStereoMatches(const std::vector<orbx_keypoint>& keypointsL, const uint8_t* descriptorsL,
+                                 const PyramidView& pyramidL, const std::vector<orbx_keypoint>& keypointsR,
+                                 const uint8_t* descriptorsR, const PyramidView& pyramidR,
+                                 const std::vector<float>& scaleFactors, const std::vector<float>& invScaleFactors,
+                                 float bf, float baseline, std::vector<float>& uright, std::vector<float>& depth) {
+    auto view = [](const std::vector<orbx_keypoint>& k, const uint8_t* d, const PyramidView& p) {
+        orbm_stereo_view v;
+        v.n = (int32_t)k.size();
+        v.kps = k.data();
+        v.desc = d;
+        v.n_levels = (int32_t)p.level.size();
+        v.level = p.level.data();
+        v.level_rows = p.rows.data();
+        v.level_cols = p.cols.data();
+        v.level_step = p.step.data();
+        return v;
+    };
+    const orbm_stereo_view l = view(keypointsL, descriptorsL, pyramidL), r = view(keypointsR, descriptorsR, pyramidR);
+    uright.assign(keypointsL.size(), -1.f);
+    depth.assign(keypointsL.size(), -1.f);
+    check(orbm_compute_stereo_matches(&l, &r, scaleFactors.data(), invScaleFactors.data(), bf, baseline, uright.data(),
+                                      depth.data()),
+          "orbm_compute_stereo_matches");
+}
+
 // Optimizer::LocalBundleAdjustment from the flattened graph (Optimizer.cc:540-631): the caller
 // gathers local / fixed keyframes and local map points exactly as :493-537, calls this, then
 // erases the outlier observations and writes poses / points back under the map mutex (:677-735).

@@ -8,3 +8,10 @@ int use_wrapper() {
     uint8_t a[32] = {0}, b[32] = {1};
     return ORB_SLAM2_AMD::ORBmatcher::DescriptorDistance(a, b) + (m.checkOrientation() ? 1 : 0);
 }
+
+void use_stereo(const std::vector<orbx_keypoint>& kl, const uint8_t* dl, const std::vector<orbx_keypoint>& kr,
+                const uint8_t* dr, const ORB_SLAM2_AMD::PyramidView& pl, const ORB_SLAM2_AMD::PyramidView& pr,
+                const std::vector<float>& s, const std::vector<float>& inv) {
+    std::vector<float> ur, depth;
+    ORB_SLAM2_AMD::ComputeStereoMatches(kl, dl, pl, kr, dr, pr, s, inv, 386.1448f, 0.537f, ur, depth);
+}
