@@ -138,6 +138,40 @@ def stereo_leg(dev, local, pairs=64, steps=5):
             "matched_per_pair": matched}
 
 
+def pose_leg(dev, frames=256, edges=1000, steps=10, cpu=True):
+    """§8f row 3: batched PoseOptimization (Optimizer.cc:345-489), frames x edges map-point matches
+    (KITTI-tracking sized), inputs resident in HBM, one launch per step; CPU oracle beside it."""
+    import torch
+    from orb_slam2_refactored_amd.optimizer import pose_optimization_device
+    from orb_slam2_refactored_amd.synth import make_pose_batch
+    b = make_pose_batch(12, n_frames=frames, n_edges=edges)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items() if not k.startswith("gt_")}
+    out = pose_optimization_device(d)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        pose_optimization_device(d, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    r = {"workload": f"{frames} frames x {edges} edges (40 % stereo, 10 % outliers), 4 x optimize(10), fp64",
+         "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms,
+         "mean_inliers": float(out["n_inliers"].double().mean().item())}
+    if cpu:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_api as O
+        sub = make_pose_batch(13, n_frames=16, n_edges=edges)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 4.0 or n < 16:
+            O.pose_optimization(sub)
+            n += 16
+        r["cpu_baseline"] = {"frames_per_s": n / (time.perf_counter() - t0), "cores": 1, "kind": "port",
+                             "sample": f"16-frame batches of {edges} edges, oracle/orb_oracle.cpp, 1 thread"}
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,6 +184,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ba", action="store_true")
     ap.add_argument("--no-stereo", action="store_true")
+    ap.add_argument("--no-pose", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -297,6 +332,9 @@ def main():
 
     if rank == 0 and not args.no_stereo:
         result["stereo"] = stereo_leg(dev, local)
+
+    if rank == 0 and not args.no_pose:
+        result["pose_opt"] = pose_leg(dev, cpu=world == 1 and not args.no_cpu_baseline)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(frames_np[:4], args.nfeatures)

@@ -219,6 +219,42 @@ typedef struct orbba_result {
 int orbba_local_ba(const orbba_problem* prob, orbba_result* res, const volatile int32_t* stop_flag,
                    int device);
 
+/* ------------------------------------------------------------------------------------------
+ * Motion-only bundle adjustment.  Replaces Optimizer::PoseOptimization (include/Optimizer.h:49,
+ * src/Optimizer.cc:345-489) for a batch of frames: one SE3 vertex per frame, one unary
+ * EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose per matched map point
+ * (types_six_dof_expmap.h:143-202), 4 rounds of optimize(10) with chi2 outlier
+ * classification (5.991 mono / 7.815 stereo), Huber kernels dropped after round 2, and a
+ * single round when a frame has fewer than 10 edges.  The caller flattens, per frame, the
+ * keypoints that have a map point in keypoint order (Optimizer.cc:364-410).
+ * ---------------------------------------------------------------------------------------- */
+#define ORBBA_POSE_MAX_EDGES 16384   /* edges per frame */
+
+typedef struct orbba_pose_batch {
+    int32_t        n_frames;
+    const int32_t* edge_begin;  /* n_frames + 1: frame f owns edges [edge_begin[f], edge_begin[f+1]) */
+    const double*  pose_R;      /* n_frames x 9 row-major Tcw rotation (frame->pose) */
+    const double*  pose_t;      /* n_frames x 3 */
+    const double*  cam;         /* n_frames x 5: fx, fy, cx, cy, bf (frame->camera) */
+    const double*  xw;          /* E x 3: the map point's GetWorldPos() */
+    const double*  obs;         /* E x 3: keypointsUn[i].pt.x, .y, uright[i] (ur < 0: monocular, :376) */
+    const double*  inv_sigma2;  /* E: pyramid.invSigmaSq[keypointsUn[i].octave] */
+} orbba_pose_batch;
+
+typedef struct orbba_pose_result {
+    double*  pose_R;     /* n_frames x 9 (frame->SetPose; input pose copied when < 3 edges) */
+    double*  pose_t;     /* n_frames x 3 */
+    int32_t* n_inliers;  /* n_frames: PoseOptimization's return value (nedges - noutliers, 0 if < 3);
+                          * -1 from the device entry when a frame exceeds ORBBA_POSE_MAX_EDGES */
+    uint8_t* outlier;    /* E: frame->outlier[i] after the last round */
+} orbba_pose_result;
+
+/* Host buffers; synchronous.  ORB_EINVAL if a frame has more than ORBBA_POSE_MAX_EDGES edges. */
+int orbba_pose_optimization(const orbba_pose_batch* in, orbba_pose_result* out, int device);
+/* Device buffers (every pointer in both structs); enqueue only, on `stream` (NULL = default
+ * stream).  One workgroup per frame. */
+int orbba_pose_optimization_device(const orbba_pose_batch* in, orbba_pose_result* out, void* stream);
+
 const char* orb_last_error(void);
 int orb_device_count(void);
 

@@ -26,6 +26,9 @@
  *                  :54-120, core/robust_kernel_impl.cpp:65-91, types/types_six_dof_expmap.{h,cpp},
  *                  types/se3quat.h, types/types_sba.h — Eigen replaced by explicit fp64 code,
  *                  SimplicialLDLT by a dense LDLT of the reduced camera system.
+ *   PoseOpt        src/Optimizer.cc:345-489 (4 x optimize(10) with chi2 classification) over
+ *                  the unary edges of types_six_dof_expmap.h:143-202 / .cpp:266-364 and
+ *                  solvers/linear_solver_dense.h:65-113 (Eigen LDLT -> unpivoted fp64 LDL^T).
  *
  * Parity status: the reference has NO tests, fixtures or golden vectors for this path and
  * cannot be built here (OpenCV / Eigen absent; a shim build is not allowed).  This oracle is
@@ -1053,6 +1056,177 @@ struct BA {
     }
 };
 
+// ---------------------------------------------------------------------------------------------
+// PoseOptimization: one SE3 vertex, unary edges (types_six_dof_expmap.h:143-202,
+// types_six_dof_expmap.cpp:266-364), LinearSolverDense under OptimizationAlgorithmLevenberg.
+// ---------------------------------------------------------------------------------------------
+struct PoseOpt {
+    int E = 0;
+    const double *xw = nullptr, *obs = nullptr, *info = nullptr;
+    double fx = 0, fy = 0, cx = 0, cy = 0, bf = 0;
+    std::vector<uint8_t> stereo, level;
+    bool robust = true;
+    std::vector<double> err;   // E x 3, the edge's _error as last computed
+    SE3 pose;
+    std::vector<int> act;
+
+    void compute_error(int e) {   // computeError (types_six_dof_expmap.h:153-158, :184-189)
+        double Xc[3];
+        se3_map(pose, &xw[3 * e], Xc);
+        const double* z = &obs[3 * e];
+        if (!stereo[e]) {         // cam_project (.cpp:290-296)
+            err[3 * e + 0] = z[0] - (Xc[0] / Xc[2] * fx + cx);
+            err[3 * e + 1] = z[1] - (Xc[1] / Xc[2] * fy + cy);
+            err[3 * e + 2] = 0;
+        } else {                  // (.cpp:299-306): invz narrowed to float, bf stays double
+            const float invz = 1.0f / Xc[2];
+            const double u = Xc[0] * invz * fx + cx;
+            const double v = Xc[1] * invz * fy + cy;
+            err[3 * e + 0] = z[0] - u;
+            err[3 * e + 1] = z[1] - v;
+            err[3 * e + 2] = z[2] - (u - bf * invz);
+        }
+    }
+    double chi2(int e) const {   // BaseEdge::chi2: e . (Omega e), Omega = invSigma2 * I
+        double s = 0;
+        for (int i = 0; i < (stereo[e] ? 3 : 2); i++) s += err[3 * e + i] * (info[e] * err[3 * e + i]);
+        return s;
+    }
+    void robustify(int e, double c, double& r0, double& r1) const {   // RobustKernelHuber
+        if (!robust) { r0 = c; r1 = 1.0; return; }
+        const double delta = stereo[e] ? std::sqrt(7.815) : std::sqrt(5.991), dsqr = delta * delta;
+        if (c <= dsqr) { r0 = c; r1 = 1.0; }
+        else { const double s = std::sqrt(c); r0 = 2 * s * delta - dsqr; r1 = delta / s; }
+    }
+    double active_robust_chi2() const {
+        double s = 0;
+        for (int e : act) { double r0, r1; robustify(e, chi2(e), r0, r1); s += r0; }
+        return s;
+    }
+    void compute_active_errors() { for (int e : act) compute_error(e); }
+
+    double H[36], b[6], x[6];
+    // linearizeOplus (.cpp:266-288, :335-364) + BaseUnaryEdge::constructQuadraticForm
+    void build_system() {
+        std::memset(H, 0, sizeof(H));
+        std::memset(b, 0, sizeof(b));
+        for (int e : act) {
+            double Xc[3];
+            se3_map(pose, &xw[3 * e], Xc);
+            const double X = Xc[0], Y = Xc[1], invz = 1.0 / Xc[2], invz2 = invz * invz;
+            double J[3][6] = {{0}};
+            J[0][0] = X * Y * invz2 * fx; J[0][1] = -(1 + (X * X * invz2)) * fx; J[0][2] = Y * invz * fx;
+            J[0][3] = -invz * fx;         J[0][4] = 0;                            J[0][5] = X * invz2 * fx;
+            J[1][0] = (1 + Y * Y * invz2) * fy; J[1][1] = -X * Y * invz2 * fy; J[1][2] = -X * invz * fy;
+            J[1][3] = 0;                        J[1][4] = -invz * fy;          J[1][5] = Y * invz2 * fy;
+            const int d = stereo[e] ? 3 : 2;
+            if (d == 3) {
+                J[2][0] = J[0][0] - bf * Y * invz2; J[2][1] = J[0][1] + bf * X * invz2; J[2][2] = J[0][2];
+                J[2][3] = J[0][3];                  J[2][4] = 0;                         J[2][5] = J[0][5] - bf * invz2;
+            }
+            double r0, r1;
+            robustify(e, chi2(e), r0, r1);
+            const double w = r1 * info[e];
+            for (int i = 0; i < 6; i++) {
+                double s = 0;
+                for (int r = 0; r < d; r++) s += J[r][i] * (info[e] * err[3 * e + r]);
+                b[i] -= r1 * s;
+                for (int j = 0; j < 6; j++) {
+                    double h = 0;
+                    for (int r = 0; r < d; r++) h += J[r][i] * w * J[r][j];
+                    H[6 * i + j] += h;
+                }
+            }
+        }
+    }
+    // LinearSolverDense::solve (linear_solver_dense.h:65-113): Eigen LDLT, rejected unless
+    // positive (semi)definite.  Unpivoted here; H + lambda*I is SPD whenever it is accepted.
+    bool solve(double lambda) {
+        double A[36], L[36] = {0}, dd[6];
+        std::memcpy(A, H, sizeof(A));
+        for (int i = 0; i < 6; i++) A[7 * i] += lambda;
+        for (int j = 0; j < 6; j++) {
+            double v = A[7 * j];
+            for (int k = 0; k < j; k++) v -= L[6 * j + k] * L[6 * j + k] * dd[k];
+            if (!(v >= 0) || !std::isfinite(v)) return false;
+            dd[j] = v;
+            L[7 * j] = 1;
+            for (int i = j + 1; i < 6; i++) {
+                double s = A[6 * i + j];
+                for (int k = 0; k < j; k++) s -= L[6 * i + k] * L[6 * j + k] * dd[k];
+                L[6 * i + j] = v != 0 ? s / v : 0;
+            }
+        }
+        double y[6];
+        for (int i = 0; i < 6; i++) {
+            double s = b[i];
+            for (int k = 0; k < i; k++) s -= L[6 * i + k] * y[k];
+            y[i] = s;
+        }
+        for (int i = 0; i < 6; i++) y[i] = dd[i] != 0 ? y[i] / dd[i] : 0;
+        for (int i = 5; i >= 0; i--) {
+            double s = y[i];
+            for (int k = i + 1; k < 6; k++) s -= L[6 * k + i] * x[k];
+            x[i] = s;
+        }
+        return true;
+    }
+    // SparseOptimizer::optimize (sparse_optimizer.cpp:354-419) around
+    // OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:60-163).
+    int optimize(int iters) {
+        if (act.empty()) return -1;   // "0 vertices to optimize"
+        double lambda = 0, ni = 2;
+        int nbad = 0, done = 0;
+        for (int it = 0; it < iters; it++) {
+            compute_active_errors();
+            double cur = active_robust_chi2();
+            const double ini = cur;
+            build_system();
+            if (it == 0) {   // computeLambdaInit (:166-180), tau 1e-5
+                double m = 0;
+                for (int j = 0; j < 6; j++) m = std::max(m, std::fabs(H[7 * j]));
+                lambda = 1e-5 * m; ni = 2; nbad = 0;
+            }
+            double rho = 0;
+            int q = 0;
+            do {
+                const SE3 saved = pose;
+                const bool ok = solve(lambda);
+                if (!ok) std::memset(x, 0, sizeof(x));   // x left unspecified by a failed solve
+                pose = se3_exp_mul(x, pose);             // VertexSE3Expmap::oplusImpl
+                compute_active_errors();
+                double tmp = active_robust_chi2();
+                if (!ok) tmp = DBL_MAX;
+                rho = cur - tmp;
+                double scale = 1e-3;   // computeScale (:182-190) + 1e-3
+                {
+                    double s = 0;
+                    for (int j = 0; j < 6; j++) s += x[j] * (lambda * x[j] + b[j]);
+                    scale += s;
+                }
+                rho /= scale;
+                if (rho > 0 && std::isfinite(tmp)) {
+                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    alpha = std::min(alpha, 2. / 3.);
+                    lambda *= std::max(1. / 3., alpha);
+                    ni = 2;
+                    cur = tmp;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    pose = saved;
+                }
+                q++;
+            } while (rho < 0 && q < 10);
+            done++;
+            if (q == 10 || rho == 0) break;
+            if ((ini - cur) * 1e3 < ini) nbad++; else nbad = 0;
+            if (nbad >= 3) break;
+        }
+        return done;
+    }
+};
+
 }  // namespace oracle
 
 using namespace oracle;
@@ -1362,6 +1536,58 @@ int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile i
         }
     }
     std::memcpy(res->points, ba.X.data(), sizeof(double) * 3 * ba.N);
+    return 0;
+}
+
+// Optimizer::PoseOptimization (src/Optimizer.cc:345-489), frame by frame.
+int oracle_pose_optimization(const orbba_pose_batch* in, orbba_pose_result* out) {
+    const double maxChi2[2] = {5.991, 7.815};   // CHI2_MONO, CHI2_STEREO (:44-45)
+    for (int f = 0; f < in->n_frames; f++) {
+        const int e0 = in->edge_begin[f], E = in->edge_begin[f + 1] - e0;
+        for (int e = 0; e < E; e++) out->outlier[e0 + e] = 0;   // frame->outlier[i] = false (:370)
+        const double* R0 = in->pose_R + 9 * (size_t)f;
+        const double* t0 = in->pose_t + 3 * (size_t)f;
+        if (E < 3) {   // (:412-414) return 0, pose untouched
+            std::memcpy(out->pose_R + 9 * (size_t)f, R0, 9 * sizeof(double));
+            std::memcpy(out->pose_t + 3 * (size_t)f, t0, 3 * sizeof(double));
+            out->n_inliers[f] = 0;
+            continue;
+        }
+        PoseOpt po;
+        po.E = E;
+        po.xw = in->xw + 3 * (size_t)e0; po.obs = in->obs + 3 * (size_t)e0; po.info = in->inv_sigma2 + e0;
+        const double* c = in->cam + 5 * (size_t)f;
+        po.fx = c[0]; po.fy = c[1]; po.cx = c[2]; po.cy = c[3]; po.bf = c[4];
+        po.stereo.resize(E);
+        for (int e = 0; e < E; e++) po.stereo[e] = po.obs[3 * e + 2] < 0 ? 0 : 1;
+        po.level.assign(E, 0);
+        po.err.assign(3 * (size_t)E, 0);
+        SE3 init;   // ToSE3Quat(frame->pose)
+        init.q = quat_from_R(R0);
+        quat_normalize_pos(init.q);
+        for (int k = 0; k < 3; k++) init.t[k] = t0[k];
+        int noutliers = 0;
+        for (int k = 0; k < 4; k++) {   // (:422-484)
+            po.pose = init;
+            po.act.clear();   // initializeOptimization(0)
+            for (int e = 0; e < E; e++) if (po.level[e] == 0) po.act.push_back(e);
+            po.optimize(10);
+            noutliers = 0;
+            for (int e = 0; e < E; e++) {
+                if (out->outlier[e0 + e]) po.compute_error(e);
+                if (po.chi2(e) > maxChi2[po.stereo[e]]) {
+                    out->outlier[e0 + e] = 1; po.level[e] = 1; noutliers++;
+                } else {
+                    out->outlier[e0 + e] = 0; po.level[e] = 0;
+                }
+            }
+            if (k == 2) po.robust = false;   // setRobustKernel(0)
+            if (E < 10) break;               // optimizer.edges().size() < 10
+        }
+        quat_to_R(po.pose.q, out->pose_R + 9 * (size_t)f);
+        for (int k = 0; k < 3; k++) out->pose_t[3 * (size_t)f + k] = po.pose.t[k];
+        out->n_inliers[f] = E - noutliers;
+    }
     return 0;
 }
 

@@ -43,6 +43,15 @@ class BAResult(C.Structure):
                 ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2)]
 
 
+class PoseBatch(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("edge_begin", C.c_void_p), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
+                ("cam", C.c_void_p), ("xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
+
+
+class PoseResult(C.Structure):
+    _fields_ = [("pose_R", C.c_void_p), ("pose_t", C.c_void_p), ("n_inliers", C.c_void_p), ("outlier", C.c_void_p)]
+
+
 # cv::KeyPoint layout (28 bytes)
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -74,6 +83,8 @@ SIGNATURES = {
     "orbx_stereo_matches_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, VP, VP, VP, C.c_int, C.c_float,
                                                    C.c_float, VP, VP, VP]),
     "orbba_local_ba": (C.c_int, [C.POINTER(BAProblem), C.POINTER(BAResult), VP, C.c_int]),
+    "orbba_pose_optimization": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), C.c_int]),
+    "orbba_pose_optimization_device": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), VP]),
     "orbx_profile_enable": (C.c_int, [VP, C.c_int]),
     "orbx_profile_read": (C.c_int, [VP, VP, VP]),
     "orbx_debug_level_candidates": (C.c_int, [VP, C.c_int, C.c_int, VP, C.c_int, C.POINTER(C.c_int)]),

@@ -1,4 +1,5 @@
-"""Optimizer::LocalBundleAdjustment mirror (include/Optimizer.h:47) over the gfx950 C-ABI.
+"""Optimizer::LocalBundleAdjustment / PoseOptimization mirrors (include/Optimizer.h:47-49) over the
+gfx950 C-ABI.
 
 The reference's graph gathering (local KFs by covisibility, local MPs, fixed KFs; Optimizer.cc:493-537)
 operates on ORB-SLAM's pointer graph; callers flatten that into a `problem` dict (see
@@ -9,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import BAProblem, BAResult, check, lib, ptr
+from ._lib import BAProblem, BAResult, PoseBatch, PoseResult, check, lib, ptr, stream_ptr, tptr
 
 
 def LocalBundleAdjustment(problem: dict, stop_flag=None, device: int = 0) -> dict:
@@ -38,4 +39,56 @@ def LocalBundleAdjustment(problem: dict, stop_flag=None, device: int = 0) -> dic
     check(lib().orbba_local_ba(C.byref(pr), C.byref(res), sf, device), "orbba_local_ba")
     out["iterations"] = tuple(res.iterations)
     out["chi2"] = tuple(res.chi2)
+    return out
+
+
+def _pose_arrays(batch: dict):
+    keep = []
+
+    def k(a, dt):
+        a = np.ascontiguousarray(a, dt)
+        keep.append(a)
+        return ptr(a)
+
+    n = len(batch["edge_begin"]) - 1
+    pb = PoseBatch(n, k(batch["edge_begin"], np.int32), k(batch["pose_R"], np.float64), k(batch["pose_t"], np.float64),
+                   k(batch["cam"], np.float64), k(batch["xw"], np.float64), k(batch["obs"], np.float64),
+                   k(batch["inv_sigma2"], np.float64))
+    return pb, keep
+
+
+def PoseOptimization(batch: dict, device: int = 0) -> dict:
+    """int Optimizer::PoseOptimization(Frame*) (include/Optimizer.h:49, src/Optimizer.cc:345-489) over a
+    batch of frames.  `batch` holds, per frame f, the edges [edge_begin[f], edge_begin[f+1]) of the
+    keypoints that have a map point, in keypoint order: xw (E,3) map point positions, obs (E,3)
+    = (u, v, ur) with ur < 0 for monocular, inv_sigma2 (E,), plus pose_R (F,9) / pose_t (F,3) = frame->pose
+    and cam (F,5) = fx, fy, cx, cy, bf.  Returns pose_R / pose_t (the frame->SetPose argument),
+    n_inliers (the return value) and outlier (E,) = frame->outlier."""
+    pb, keep = _pose_arrays(batch)
+    n, E = pb.n_frames, int(batch["edge_begin"][-1]) if len(batch["edge_begin"]) else 0
+    out = dict(pose_R=np.zeros((n, 9)), pose_t=np.zeros((n, 3)), n_inliers=np.zeros(n, np.int32),
+               outlier=np.zeros(E, np.uint8))
+    res = PoseResult(ptr(out["pose_R"]), ptr(out["pose_t"]), ptr(out["n_inliers"]), ptr(out["outlier"]))
+    check(lib().orbba_pose_optimization(C.byref(pb), C.byref(res), device), "orbba_pose_optimization")
+    return out
+
+
+def pose_optimization_device(batch: dict, out: dict | None = None, stream=None) -> dict:
+    """Device form: `batch` values are torch tensors on the GPU (int32 edge_begin, float64 others);
+    enqueues one launch on `stream` (default: torch's current stream) and returns the output tensors."""
+    import torch
+    eb = batch["edge_begin"]
+    n = eb.numel() - 1
+    E = batch["inv_sigma2"].numel()
+    dev = eb.device
+    if out is None:
+        out = dict(pose_R=torch.empty((n, 9), dtype=torch.float64, device=dev),
+                   pose_t=torch.empty((n, 3), dtype=torch.float64, device=dev),
+                   n_inliers=torch.empty(n, dtype=torch.int32, device=dev),
+                   outlier=torch.empty(max(E, 1), dtype=torch.uint8, device=dev))
+    pb = PoseBatch(n, tptr(eb), tptr(batch["pose_R"]), tptr(batch["pose_t"]), tptr(batch["cam"]), tptr(batch["xw"]),
+                   tptr(batch["obs"]), tptr(batch["inv_sigma2"]))
+    res = PoseResult(tptr(out["pose_R"]), tptr(out["pose_t"]), tptr(out["n_inliers"]), tptr(out["outlier"]))
+    check(lib().orbba_pose_optimization_device(C.byref(pb), C.byref(res), stream_ptr(stream)),
+          "orbba_pose_optimization_device")
     return out

@@ -143,3 +143,63 @@ def stereo_pair(seed: int, width: int = 1242, height: int = 375, bf: float = KIT
             R[:, x] = L[:, x + d] if x + d < width else rng.integers(0, 256, size=height)
     R += rng.integers(-3, 4, size=R.shape).astype(np.int16)
     return L, np.clip(R, 0, 255).astype(np.uint8), zcol
+
+
+def make_pose_batch(seed: int = 0, n_frames: int = 8, n_edges=600, stereo_frac: float = 0.4,
+                    outlier_frac: float = 0.1, rot_deg: float = 0.5, trans_m: float = 0.1, cam=KITTI):
+    """C5: a batch of PoseOptimization problems in the orbba_pose_batch layout.
+
+    Per frame: a random camera pose (yaw U(-180,180) deg, position U(-50,50) m in x/z), map points
+    back-projected from uniform pixels at depth U(3, 60) m, octaves U{0..7} with pixel noise
+    N(0, 1.2^oct) and invSigma2 = 1/1.2^(2 oct) (float, like Frame::pyramid.invSigmaSq);
+    `stereo_frac` of the observations carry ur = u - bf/z + noise; `outlier_frac` are moved by
+    +-U(10, 60) px.  The initial pose (the motion-model prediction) is the true pose perturbed by
+    N(0, rot_deg) rotation and N(0, trans_m) translation.  Measurements, map points and
+    intrinsics are rounded to float32, as the reference stores them.  n_edges: int or per-frame list.
+    """
+    rng = np.random.default_rng(seed)
+    counts = [int(n_edges)] * n_frames if np.isscalar(n_edges) else [int(n) for n in n_edges]
+    assert len(counts) == n_frames
+    eb = np.zeros(n_frames + 1, np.int32)
+    eb[1:] = np.cumsum(counts)
+    camv = np.array([cam[k] for k in ("fx", "fy", "cx", "cy", "bf")], np.float32).astype(np.float64)
+    fx, fy, cx, cy, bf = camv
+    pose_R, pose_t, gt_R, gt_t = [], [], [], []
+    xw, obs, info = [], [], []
+    for f, n in enumerate(counts):
+        Rcw = _rot_y(rng.uniform(-180, 180)) @ _small_rot(rng, 3.0)
+        C = np.array([rng.uniform(-50, 50), rng.uniform(-2, 2), rng.uniform(-50, 50)])
+        tcw = -Rcw @ C
+        gt_R.append(Rcw.reshape(-1))
+        gt_t.append(tcw)
+        u = rng.uniform(0, cam["width"], n)
+        v = rng.uniform(0, cam["height"], n)
+        z = rng.uniform(3, 60, n)
+        Xc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+        Xw = (Xc - tcw) @ Rcw   # Rcw^T (Xc - t)
+        octv = rng.integers(0, 8, n)
+        sig = 1.2 ** octv
+        uo = u + rng.normal(0, 1, n) * sig
+        vo = v + rng.normal(0, 1, n) * sig
+        st = rng.random(n) < stereo_frac
+        ur = np.where(st, u - bf / z + rng.normal(0, 1, n) * sig, -1.0)
+        out = rng.random(n) < outlier_frac
+        du = rng.choice([-1, 1], n) * rng.uniform(10, 60, n)
+        dv = rng.choice([-1, 1], n) * rng.uniform(10, 60, n)
+        uo = np.where(out, uo + du, uo)
+        vo = np.where(out, vo + dv, vo)
+        ur = np.where(out & st, ur + du, ur)
+        o = np.stack([uo, vo, ur], 1).astype(np.float32).astype(np.float64)
+        o[~st, 2] = -1.0
+        obs.append(o)
+        xw.append(Xw.astype(np.float32).astype(np.float64))
+        info.append((1.0 / (sig * sig)).astype(np.float32).astype(np.float64))
+        R0 = _small_rot(rng, rot_deg) @ Rcw
+        t0 = tcw + rng.normal(0, trans_m, 3)
+        pose_R.append(R0.astype(np.float32).astype(np.float64).reshape(-1))
+        pose_t.append(t0.astype(np.float32).astype(np.float64))
+    cat = (lambda a, w: np.concatenate(a).reshape(-1, w) if sum(counts) else np.zeros((0, w)))
+    return dict(edge_begin=eb, pose_R=np.array(pose_R).reshape(n_frames, 9), pose_t=np.array(pose_t).reshape(n_frames, 3),
+                cam=np.tile(camv, (n_frames, 1)), xw=cat(xw, 3), obs=cat(obs, 3),
+                inv_sigma2=np.concatenate(info) if sum(counts) else np.zeros(0),
+                gt_R=np.array(gt_R).reshape(n_frames, 9), gt_t=np.array(gt_t).reshape(n_frames, 3))

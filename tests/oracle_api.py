@@ -215,6 +215,30 @@ def local_ba(prob, stop=None):
     return out
 
 
+class PoseBatch(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("edge_begin", C.c_void_p), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
+                ("cam", C.c_void_p), ("xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
+
+
+class PoseResult(C.Structure):
+    _fields_ = [("pose_R", C.c_void_p), ("pose_t", C.c_void_p), ("n_inliers", C.c_void_p), ("outlier", C.c_void_p)]
+
+
+def pose_optimization(batch):
+    """Optimizer::PoseOptimization (src/Optimizer.cc:345-489) per frame of a make_pose_batch dict."""
+    keep = _Keep()
+    n = len(batch["edge_begin"]) - 1
+    E = int(batch["edge_begin"][-1])
+    pb = PoseBatch(n, keep(batch["edge_begin"], np.int32), keep(batch["pose_R"], np.float64),
+                   keep(batch["pose_t"], np.float64), keep(batch["cam"], np.float64), keep(batch["xw"], np.float64),
+                   keep(batch["obs"], np.float64), keep(batch["inv_sigma2"], np.float64))
+    out = dict(pose_R=np.zeros((n, 9)), pose_t=np.zeros((n, 3)), n_inliers=np.zeros(n, np.int32),
+               outlier=np.zeros(E, np.uint8))
+    res = PoseResult(ptr(out["pose_R"]), ptr(out["pose_t"]), ptr(out["n_inliers"]), ptr(out["outlier"]))
+    lib().oracle_pose_optimization(C.byref(pb), C.byref(res))
+    return out
+
+
 def std_sort_perm(sizes):
     sizes = np.ascontiguousarray(sizes, np.int32)
     perm = np.zeros(len(sizes), np.int32)

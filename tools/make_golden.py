@@ -17,13 +17,26 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
 import oracle_api as O  # noqa: E402
-from orb_slam2_refactored_amd.synth import make_ba_problem, synth_image  # noqa: E402
+from orb_slam2_refactored_amd.synth import make_ba_problem, make_pose_batch, synth_image  # noqa: E402
 
 OUT = ROOT / "tests" / "golden"
 
 
-def main():
+def pose_opt():
+    # PoseOptimization: ragged batch incl. the < 3 / < 10 edge cases
+    b = make_pose_batch(6, n_frames=6, n_edges=[0, 2, 7, 60, 300, 900])
+    r = O.pose_optimization(b)
+    keep = {k: v for k, v in b.items() if not k.startswith("gt_")}
+    np.savez_compressed(OUT / "pose_opt_small.npz", **keep, out_pose_R=r["pose_R"], out_pose_t=r["pose_t"],
+                        out_n_inliers=r["n_inliers"], out_outlier=r["outlier"])
+
+
+def main(only=None):
     OUT.mkdir(parents=True, exist_ok=True)
+    if only == "pose":
+        pose_opt()
+        return
+    pose_opt()
     for seed in range(4):
         img = synth_image(seed, 640, 480)
         kps, desc, per = O.extract(O.params(1000), img)
@@ -46,4 +59,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)   # "pose": only the PoseOptimization fixture
