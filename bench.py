@@ -138,7 +138,7 @@ def stereo_leg(dev, local, pairs=64, steps=5):
             "matched_per_pair": matched}
 
 
-def pose_leg(dev, frames=256, edges=1000, steps=10, cpu=True):
+def pose_leg(dev, frames=1024, edges=1000, steps=10, cpu=True):
     """§8f row 3: batched PoseOptimization (Optimizer.cc:345-489), frames x edges map-point matches
     (KITTI-tracking sized), inputs resident in HBM, one launch per step; CPU oracle beside it."""
     import torch

@@ -274,6 +274,10 @@ int orbx_debug_level_candidates(const orbx_extractor* h, int frame, int level, u
 /* Runs the quadtree's on-device std::sort emulation (one wavefront) on `sizes`: perm[k] = index of
  * the element that std::sort(size-descending, src/ORBextractor.cc:642-643) puts at position k. */
 int orbx_debug_qt_sort(const int32_t* sizes, int n, int32_t* perm);
+/* PoseOptimization's cross-lane sums on one wavefront: in = 64 lanes x 32 doubles (lane-major);
+ * scatter[l] = wave total of value l >> 1 (reduce-scatter butterfly), sum[l] = wave total of
+ * in[*][0] (all-reduce).  Checks the permlane / DPP lane mapping against a host sum. */
+int orbba_debug_po_wave(const double* in, double* scatter, double* sum);
 /* Quadtree output of (frame, level) of the last batch (list order, packed as above). */
 int orbx_debug_level_selected(const orbx_extractor* h, int frame, int level, uint32_t* out, int cap, int* n);
 

@@ -89,6 +89,7 @@ SIGNATURES = {
     "orbx_profile_read": (C.c_int, [VP, VP, VP]),
     "orbx_debug_level_candidates": (C.c_int, [VP, C.c_int, C.c_int, VP, C.c_int, C.POINTER(C.c_int)]),
     "orbx_debug_qt_sort": (C.c_int, [VP, C.c_int, VP]),
+    "orbba_debug_po_wave": (C.c_int, [VP, VP, VP]),
     "orbx_debug_level_selected": (C.c_int, [VP, C.c_int, C.c_int, VP, C.c_int, C.POINTER(C.c_int)]),
     "orb_last_error": (C.c_char_p, []),
     "orb_device_count": (C.c_int, []),

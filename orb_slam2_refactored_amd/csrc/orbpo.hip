@@ -6,15 +6,17 @@
 // linear solver, 4 rounds of optimize(10) with chi2 outlier classification in between.
 //
 // One 256-lane workgroup owns one frame for the whole optimisation (a single launch per batch):
-//   - edges are strided over the lanes (lane i owns edges i, i+256, ...; at most 64 each, so a
-//     lane's outlier / level flags live in one 64-bit register mask);
+//   - the frame's first PO_LDS_EDGES edges are staged once into LDS (structure of arrays, fp64);
+//     lane i owns edges i, i+256, ... (at most 64, so a lane's outlier / level flags are one
+//     register mask);
 //   - a pass over the active edges computes computeError + robust chi2 (and, for the
 //     linearisation pass, the Jacobian and the 21 + 6 entries of H and b), reduced across the
-//     wavefront by a reduce-scatter butterfly (32 values -> one per lane pair, 31 shuffles) and
-//     across the 4 wavefronts through LDS in a fixed order;
-//   - every lane then reads the same totals and runs the LM control, the 6x6 LDL^T solve and the
-//     SE3 exp update redundantly — identical inputs, identical results, so the pose stays in
-//     registers and no lane has to broadcast it.
+//     wavefront by a reduce-scatter butterfly built from v_permlane32_swap / v_permlane16_swap
+//     and DPP moves (VALU only, no LDS round trips), then across the 4 wavefronts through LDS
+//     in a fixed order, and broadcast back to every lane with v_readlane;
+//   - every lane then runs the LM control, the packed 6x6 LDL^T solve and the SE3 exp update
+//     redundantly on wave-uniform values — identical inputs, identical results, so the pose stays
+//     in registers and no lane has to broadcast it.
 // fp64 throughout, like the reference.  Sums run in a fixed order: results are bit-reproducible.
 #include <algorithm>
 #include <cfloat>
@@ -26,9 +28,38 @@
 
 namespace orbamd {
 
+#ifndef PO_THREADS_OVERRIDE
 constexpr int PO_THREADS = 256;
+#else
+constexpr int PO_THREADS = PO_THREADS_OVERRIDE;
+#endif
 constexpr int PO_WAVES = PO_THREADS / 64;
+#ifndef PO_LDS_EDGES_OVERRIDE
+constexpr int PO_LDS_EDGES = 1024;   // staged edges per frame: 7 doubles each = 56 KiB (2 frames per CU)
+#else
+constexpr int PO_LDS_EDGES = PO_LDS_EDGES_OVERRIDE;
+#endif
+constexpr size_t PO_LDS_BYTES = (size_t)7 * PO_LDS_EDGES * sizeof(double);
 static_assert(ORBBA_POSE_MAX_EDGES <= PO_THREADS * 64, "outlier mask is one u64 per lane");
+
+#ifdef ORB_PO_STAMPS
+// Diagnostic build only (tools/diag/po_stamps.py): cycles per phase summed over block 0, lane 0.
+//   0 linearize pass, 1 28-value reduction, 2 6x6 solve, 3 exp update, 4 chi pass + reduction,
+//   5 classification, 6 LM iterations, 7 trials
+__device__ unsigned long long g_po_stamps[8];
+#define PO_T0() unsigned long long _po_t = __builtin_amdgcn_s_memtime()
+#define PO_ACC(k)                                                                               \
+    do {                                                                                        \
+        const unsigned long long _n = __builtin_amdgcn_s_memtime();                             \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_po_stamps[(k)] += _n - _po_t;                \
+        _po_t = _n;                                                                             \
+    } while (0)
+#define PO_CNT(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_po_stamps[(k)] += 1; } while (0)
+#else
+#define PO_T0() do {} while (0)
+#define PO_ACC(k) do {} while (0)
+#define PO_CNT(k) do {} while (0)
+#endif
 
 struct PoArgs {
     int n_frames;
@@ -44,13 +75,27 @@ struct PoEdge {   // one observation as loaded by a pass
     bool stereo;
 };
 
-__device__ __forceinline__ void po_load(const PoArgs& a, int e, PoEdge& d) {
-    const double* x = a.xw + 3 * (size_t)e;
-    const double* o = a.obs + 3 * (size_t)e;
-    d.X[0] = x[0]; d.X[1] = x[1]; d.X[2] = x[2];
-    d.z[0] = o[0]; d.z[1] = o[1]; d.z[2] = o[2];
-    d.info = a.isig2[e];
-    d.stereo = !(o[2] < 0);   // ur < 0: monocular edge (Optimizer.cc:376)
+// Edge store of one frame: the first nl edges in LDS (SoA), the rest read from HBM.
+struct PoEdges {
+    const double* lds;   // 7 arrays of PO_LDS_EDGES: X0 X1 X2 u v ur info
+    const double *xw, *obs, *isig2;   // frame-relative global arrays
+    int nl;
+};
+
+__device__ __forceinline__ void po_load(const PoEdges& s, int e, PoEdge& d) {
+    if (e < s.nl) {
+        const double* L = s.lds + e;
+        d.X[0] = L[0]; d.X[1] = L[PO_LDS_EDGES]; d.X[2] = L[2 * PO_LDS_EDGES];
+        d.z[0] = L[3 * PO_LDS_EDGES]; d.z[1] = L[4 * PO_LDS_EDGES]; d.z[2] = L[5 * PO_LDS_EDGES];
+        d.info = L[6 * PO_LDS_EDGES];
+    } else {
+        const double* x = s.xw + 3 * (size_t)e;
+        const double* o = s.obs + 3 * (size_t)e;
+        d.X[0] = x[0]; d.X[1] = x[1]; d.X[2] = x[2];
+        d.z[0] = o[0]; d.z[1] = o[1]; d.z[2] = o[2];
+        d.info = s.isig2[e];
+    }
+    d.stereo = !(d.z[2] < 0);   // ur < 0: monocular edge (Optimizer.cc:376)
 }
 
 struct PoCam { double fx, fy, cx, cy, bf; };
@@ -84,62 +129,134 @@ __device__ __forceinline__ void po_robustify(bool robust, bool stereo, double c,
     else { const double s = sqrt(c); r0 = 2 * s * delta - dsqr; r1 = delta / s; }
 }
 
-// Wavefront reduce-scatter of 32 doubles: on return lane l holds the wave total of value l >> 1.
-template <int H>
-__device__ __forceinline__ void po_scatter_step(double (&v)[32], int lane) {
-    const bool hi = (lane & (2 * H)) != 0;
+// ---------------------------------------------------------------- cross-lane sums (VALU only)
+template <int CTRL>
+__device__ __forceinline__ double po_dpp(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, CTRL, 0xf, 0xf, false);
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int DPP_ROR4 = 0x124, DPP_ROR8 = 0x128, DPP_ROR12 = 0x12C;
+
+union PoD2 { double d; int i[2]; };
+
+// (a, b) -> (a', b'): lanes 32..63 of a swapped with lanes 0..31 of b (v_permlane32_swap), or odd
+// rows of a with even rows of b (v_permlane16_swap) when ROW16.
+template <bool ROW16>
+__device__ __forceinline__ void po_swap(double& a, double& b) {
+    PoD2 x{a}, y{b};
 #pragma unroll
-    for (int i = 0; i < H; i++) {
-        const double send = hi ? v[i] : v[i + H];
-        const double keep = hi ? v[i + H] : v[i];
-        v[i] = keep + __shfl_xor(send, 2 * H);
+    for (int h = 0; h < 2; h++) {
+        if constexpr (ROW16) {
+            auto r = __builtin_amdgcn_permlane16_swap(x.i[h], y.i[h], false, false);
+            x.i[h] = r[0]; y.i[h] = r[1];
+        } else {
+            auto r = __builtin_amdgcn_permlane32_swap(x.i[h], y.i[h], false, false);
+            x.i[h] = r[0]; y.i[h] = r[1];
+        }
+    }
+    a = x.d; b = y.d;
+}
+
+// Partner value across lane bit M (M = 4, 8 via DPP row rotates, 1, 2 via quad perms).
+template <int M>
+__device__ __forceinline__ double po_xor(double v, int lane) {
+    if constexpr (M == 1) return po_dpp<DPP_QUAD_XOR1>(v);
+    else if constexpr (M == 2) return po_dpp<DPP_QUAD_XOR2>(v);
+    else if constexpr (M == 8) return po_dpp<DPP_ROR8>(v);
+    else {
+        static_assert(M == 4, "");
+        // row_ror:N delivers lane (l - N) mod 16: l + 4 is ror 12, l - 4 is ror 4
+        const double up = po_dpp<DPP_ROR12>(v), dn = po_dpp<DPP_ROR4>(v);
+        return (lane & 4) ? dn : up;
     }
 }
+
+// One butterfly step over H value pairs: a lane keeps index i (bit clear) or i + H (bit set)
+// and adds its partner's copy of it.
+template <int H>
+__device__ __forceinline__ void po_scatter_step(double (&v)[32], int lane) {
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+        if constexpr (H == 16) {          // across lane bit 5
+            double a = v[i], b = v[i + H];
+            po_swap<false>(a, b);
+            v[i] = a + b;
+        } else if constexpr (H == 8) {    // across lane bit 4
+            double a = v[i], b = v[i + H];
+            po_swap<true>(a, b);
+            v[i] = a + b;
+        } else {                          // across lane bit log2(2H): DPP
+            const bool hi = (lane & (2 * H)) != 0;
+            const double send = hi ? v[i] : v[i + H];
+            const double keep = hi ? v[i + H] : v[i];
+            v[i] = keep + po_xor<2 * H>(send, lane);
+        }
+    }
+}
+
+// Wavefront reduce-scatter of 32 doubles: on return lane l holds the wave total of value l >> 1.
 __device__ __forceinline__ double po_wave_scatter32(double (&v)[32], int lane) {
     po_scatter_step<16>(v, lane);
     po_scatter_step<8>(v, lane);
     po_scatter_step<4>(v, lane);
     po_scatter_step<2>(v, lane);
     po_scatter_step<1>(v, lane);
-    return v[0] + __shfl_xor(v[0], 1);
+    return v[0] + po_xor<1>(v[0], lane);
 }
 
-__device__ __forceinline__ double po_wave_sum(double v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+// Wavefront all-reduce of one double (every lane gets the same bits: each step adds the same two
+// operands, a + b == b + a).
+__device__ __forceinline__ double po_wave_sum(double v, int lane) {
+    v += po_xor<1>(v, lane);
+    v += po_xor<2>(v, lane);
+    v += po_xor<4>(v, lane);
+    v += po_xor<8>(v, lane);
+    { double a = v, b = v; po_swap<true>(a, b); v = a + b; }
+    { double a = v, b = v; po_swap<false>(a, b); v = a + b; }
     return v;
 }
 
-// One LDS reduction slot set; reductions alternate between the two so a single barrier each
-// suffices (slot p is rewritten only two reductions later, after every lane passed the
-// barrier of the reduction in between).
+__device__ __forceinline__ double po_readlane(double v, int l) {
+    PoD2 x{v};
+    x.i[0] = __builtin_amdgcn_readlane(x.i[0], l);
+    x.i[1] = __builtin_amdgcn_readlane(x.i[1], l);
+    return x.d;
+}
+
+// LDS partials: the 28-value system has its own slot (read again by every trial of the
+// iteration); the 1-value sums alternate between two slots so one barrier each suffices.
 struct PoRed {
-    double s[2][PO_WAVES][32];
+    double sys[PO_WAVES][32];
+    double one[2][PO_WAVES];
 };
 
-__device__ __forceinline__ void po_block_sum28(double (&acc)[32], double (&tot)[28], PoRed& R, int& par) {
+// H (packed upper, 21) | b (6) | robust chi2 (1), summed over the block, wave-uniform in every lane.
+struct PoSys { double v[28]; };
+
+__device__ __forceinline__ void po_block_sum28(double (&acc)[32], PoSys& out, PoRed& R) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const double r = po_wave_scatter32(acc, lane);
-    if ((lane & 1) == 0) R.s[par][w][lane >> 1] = r;
+    if ((lane & 1) == 0) R.sys[w][lane >> 1] = r;
     __syncthreads();
+    double s = 0;
+    if (lane < 28) {
+        s = R.sys[0][lane];
 #pragma unroll
-    for (int j = 0; j < 28; j++) {
-        double s = R.s[par][0][j];
-#pragma unroll
-        for (int k = 1; k < PO_WAVES; k++) s += R.s[par][k][j];
-        tot[j] = s;
+        for (int k = 1; k < PO_WAVES; k++) s += R.sys[k][lane];
     }
-    par ^= 1;
+#pragma unroll
+    for (int j = 0; j < 28; j++) out.v[j] = po_readlane(s, j);
 }
 
 __device__ __forceinline__ double po_block_sum1(double v, PoRed& R, int& par) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    v = po_wave_sum(v);
-    if (lane == 0) R.s[par][w][0] = v;
+    v = po_wave_sum(v, lane);
+    if (lane == 0) R.one[par][w] = v;
     __syncthreads();
-    double s = R.s[par][0][0];
+    double s = R.one[par][0];
 #pragma unroll
-    for (int k = 1; k < PO_WAVES; k++) s += R.s[par][k][0];
+    for (int k = 1; k < PO_WAVES; k++) s += R.one[par][k];
     par ^= 1;
     return s;
 }
@@ -147,7 +264,7 @@ __device__ __forceinline__ double po_block_sum1(double v, PoRed& R, int& par) {
 // Linearisation pass: robust chi2 total (acc[27]), H upper triangle (acc[0..20], row-major),
 // b (acc[21..26]) over the active edges, at pose (q, t).  linearizeOplus (.cpp:266-288,
 // :335-364) and BaseUnaryEdge::constructQuadraticForm with weightedOmega = rho' * Omega.
-__device__ __forceinline__ void po_linearize(const PoArgs& a, int e0, int E, uint64_t outl, const PoCam& c,
+__device__ __forceinline__ void po_linearize(const PoEdges& S, int E, uint64_t outl, const PoCam& c,
                                              const double* q, const double* t, bool robust, double (&acc)[32]) {
 #pragma unroll
     for (int j = 0; j < 32; j++) acc[j] = 0;
@@ -155,7 +272,7 @@ __device__ __forceinline__ void po_linearize(const PoArgs& a, int e0, int E, uin
     for (int e = threadIdx.x; e < E; e += PO_THREADS, i++) {
         if ((outl >> i) & 1) continue;
         PoEdge d;
-        po_load(a, e0 + e, d);
+        po_load(S, e, d);
         double Xc[3], err[3];
         const double chi = po_error(d, c, q, t, Xc, err);
         double r0, r1;
@@ -188,14 +305,14 @@ __device__ __forceinline__ void po_linearize(const PoArgs& a, int e0, int E, uin
 }
 
 // Trial pass: robust chi2 of the active edges at (q, t) (computeActiveErrors + activeRobustChi2).
-__device__ __forceinline__ double po_chi_pass(const PoArgs& a, int e0, int E, uint64_t outl, const PoCam& c,
+__device__ __forceinline__ double po_chi_pass(const PoEdges& S, int E, uint64_t outl, const PoCam& c,
                                               const double* q, const double* t, bool robust) {
     double s = 0;
     int i = 0;
     for (int e = threadIdx.x; e < E; e += PO_THREADS, i++) {
         if ((outl >> i) & 1) continue;
         PoEdge d;
-        po_load(a, e0 + e, d);
+        po_load(S, e, d);
         double Xc[3], err[3];
         double r0, r1;
         po_robustify(robust, d.stereo, po_error(d, c, q, t, Xc, err), r0, r1);
@@ -204,53 +321,49 @@ __device__ __forceinline__ double po_chi_pass(const PoArgs& a, int e0, int E, ui
     return s;
 }
 
+// Packed upper-triangle index of (r, c), r <= c.
+__host__ __device__ constexpr int pk(int r, int c) { return r * 6 - r * (r - 1) / 2 + (c - r); }
+
 // LinearSolverDense (linear_solver_dense.h:65-113): LDL^T of H + lambda I, rejected unless
-// positive semi-definite.  Same operation order as the oracle.
-__device__ __forceinline__ bool po_solve(const double (&tot)[28], double lambda, double (&x)[6]) {
-    double A[36], L[36], dd[6];
-    {
-        int k = 0;
+// positive semi-definite.  In place on the packed triangle (L(i,j) overwrites H(j,i), D the
+// diagonal); same operation order as the oracle.
+__device__ __forceinline__ bool po_solve(const PoSys& S, double lambda, double (&x)[6]) {
+    double A[21];
 #pragma unroll
-        for (int r = 0; r < 6; r++)
+    for (int k = 0; k < 21; k++) A[k] = S.v[k];
 #pragma unroll
-            for (int cc = r; cc < 6; cc++, k++) { A[6 * r + cc] = tot[k]; A[6 * cc + r] = tot[k]; }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) A[7 * i] += lambda;
-#pragma unroll
-    for (int i = 0; i < 36; i++) L[i] = 0;
+    for (int i = 0; i < 6; i++) A[pk(i, i)] += lambda;
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < 6; j++) {
-        double v = A[7 * j];
+        double v = A[pk(j, j)];
 #pragma unroll
-        for (int k = 0; k < j; k++) v -= L[6 * j + k] * L[6 * j + k] * dd[k];
+        for (int k = 0; k < j; k++) v -= A[pk(k, j)] * A[pk(k, j)] * A[pk(k, k)];
         ok = ok && (v >= 0) && isfinite(v);
-        dd[j] = v;
-        L[7 * j] = 1;
+        A[pk(j, j)] = v;
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
-            double s = A[6 * i + j];
+            double s = A[pk(j, i)];
 #pragma unroll
-            for (int k = 0; k < j; k++) s -= L[6 * i + k] * L[6 * j + k] * dd[k];
-            L[6 * i + j] = v != 0 ? s / v : 0;
+            for (int k = 0; k < j; k++) s -= A[pk(k, i)] * A[pk(k, j)] * A[pk(k, k)];
+            A[pk(j, i)] = v != 0 ? s / v : 0;
         }
     }
     double y[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-        double s = tot[21 + i];
+        double s = S.v[21 + i];
 #pragma unroll
-        for (int k = 0; k < i; k++) s -= L[6 * i + k] * y[k];
+        for (int k = 0; k < i; k++) s -= A[pk(k, i)] * y[k];
         y[i] = s;
     }
 #pragma unroll
-    for (int i = 0; i < 6; i++) y[i] = dd[i] != 0 ? y[i] / dd[i] : 0;
+    for (int i = 0; i < 6; i++) y[i] = A[pk(i, i)] != 0 ? y[i] / A[pk(i, i)] : 0;
 #pragma unroll
     for (int i = 5; i >= 0; i--) {
         double s = y[i];
 #pragma unroll
-        for (int k = i + 1; k < 6; k++) s -= L[6 * k + i] * x[k];
+        for (int k = i + 1; k < 6; k++) s -= A[pk(i, k)] * x[k];
         x[i] = s;
     }
     if (!ok)
@@ -260,6 +373,7 @@ __device__ __forceinline__ bool po_solve(const double (&tot)[28], double lambda,
 }
 
 __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
+    extern __shared__ double po_lds[];
     __shared__ PoRed red;
     const int f = blockIdx.x;
     const int e0 = a.edge_begin[f], E = a.edge_begin[f + 1] - e0;
@@ -272,6 +386,15 @@ __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
         for (int e = threadIdx.x; e < E; e += PO_THREADS) a.outlier[e0 + e] = 0;
         return;
     }
+    const PoEdges S{po_lds, a.xw + 3 * (size_t)e0, a.obs + 3 * (size_t)e0, a.isig2 + e0, min(E, PO_LDS_EDGES)};
+    for (int e = threadIdx.x; e < S.nl; e += PO_THREADS) {   // stage: SoA X0 X1 X2 u v ur info
+#pragma unroll
+        for (int k = 0; k < 3; k++) po_lds[k * PO_LDS_EDGES + e] = S.xw[3 * e + k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) po_lds[(3 + k) * PO_LDS_EDGES + e] = S.obs[3 * e + k];
+        po_lds[6 * PO_LDS_EDGES + e] = S.isig2[e];
+    }
+    __syncthreads();
     const double* cp = a.cam + 5 * (size_t)f;
     const PoCam c{cp[0], cp[1], cp[2], cp[3], cp[4]};
     double q0[4], tt0[3];   // ToSE3Quat(frame->pose)
@@ -288,6 +411,7 @@ __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
     uint64_t outl = 0;                 // this lane's edges at level 1 (frame->outlier)
     int noutliers = 0, par = 0;
     bool robust = true;
+    PO_T0();
     const int rounds = E < 10 ? 1 : 4;   // optimizer.edges().size() < 10 -> break after round 0
     for (int k = 0; k < rounds; k++) {   // Optimizer.cc:422-484
 #pragma unroll
@@ -298,20 +422,26 @@ __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
             double lambda = 0, ni = 2;
             int nbad = 0;
             for (int it = 0; it < 10; it++) {
-                double acc[32], tot[28];
-                po_linearize(a, e0, E, outl, c, q, t, robust, acc);
-                po_block_sum28(acc, tot, red, par);
+                PoSys sys;
+                {
+                    double acc[32];
+                    PO_CNT(6);
+                    PO_ACC(5);
+                    po_linearize(S, E, outl, c, q, t, robust, acc);
+                    PO_ACC(0);
+                    po_block_sum28(acc, sys, red);
+                    PO_ACC(1);
+                }
 #pragma unroll
                 for (int i = 0; i < 4; i++) qe[i] = q[i];
 #pragma unroll
                 for (int i = 0; i < 3; i++) te[i] = t[i];
-                double cur = tot[27];
+                double cur = sys.v[27];
                 const double ini = cur;
                 if (it == 0) {   // computeLambdaInit (levenberg.cpp:166-180), tau = 1e-5
-                    const int dg[6] = {0, 6, 11, 15, 18, 20};
                     double m = 0;
 #pragma unroll
-                    for (int j = 0; j < 6; j++) m = fmax(m, fabs(tot[dg[j]]));
+                    for (int j = 0; j < 6; j++) m = fmax(m, fabs(sys.v[pk(j, j)]));
                     lambda = 1e-5 * m; ni = 2; nbad = 0;
                 }
                 double rho = 0;
@@ -322,21 +452,27 @@ __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
                     for (int i = 0; i < 4; i++) sq[i] = q[i];
 #pragma unroll
                     for (int i = 0; i < 3; i++) st[i] = t[i];
-                    const bool ok = po_solve(tot, lambda, x);
+                    PO_CNT(7);
+                    PO_ACC(5);
+                    const bool ok = po_solve(sys, lambda, x);
+                    PO_ACC(2);
                     se3_exp_update(x, q, t);   // VertexSE3Expmap::oplusImpl
-                    double tmp = po_block_sum1(po_chi_pass(a, e0, E, outl, c, q, t, robust), red, par);
+                    PO_ACC(3);
+                    double tmp = po_block_sum1(po_chi_pass(S, E, outl, c, q, t, robust), red, par);
+                    PO_ACC(4);
 #pragma unroll
                     for (int i = 0; i < 4; i++) qe[i] = q[i];
 #pragma unroll
                     for (int i = 0; i < 3; i++) te[i] = t[i];
                     if (!ok) tmp = DBL_MAX;
                     rho = cur - tmp;
-                    double s = 0;   // computeScale (levenberg.cpp:182-190)
+                    double sc = 0;   // computeScale (levenberg.cpp:182-190)
 #pragma unroll
-                    for (int j = 0; j < 6; j++) s += x[j] * (lambda * x[j] + tot[21 + j]);
-                    rho /= s + 1e-3;
+                    for (int j = 0; j < 6; j++) sc += x[j] * (lambda * x[j] + sys.v[21 + j]);
+                    rho /= sc + 1e-3;
                     if (rho > 0 && isfinite(tmp)) {
-                        double alpha = 1. - pow((2 * rho - 1), 3);
+                        const double u = 2 * rho - 1;   // pow(2 rho - 1, 3) in g2o
+                        double alpha = 1. - u * u * u;
                         alpha = fmin(alpha, 2. / 3.);
                         lambda *= fmax(1. / 3., alpha);
                         ni = 2;
@@ -363,7 +499,7 @@ __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
         for (int e = threadIdx.x; e < E; e += PO_THREADS, i++) {
             const bool was = (outl >> i) & 1;
             PoEdge d;
-            po_load(a, e0 + e, d);
+            po_load(S, e, d);
             double Xc[3], err[3];
             const double chi = was ? po_error(d, c, q, t, Xc, err) : po_error(d, c, qe, te, Xc, err);
             const bool out = chi > (d.stereo ? 7.815 : 5.991);
@@ -372,6 +508,7 @@ __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
         }
         outl = nout_mask;
         noutliers = (int)po_block_sum1((double)cnt, red, par);
+        PO_ACC(5);
         if (k == 2) robust = false;   // setRobustKernel(0)
     }
     double Rf[9];
@@ -385,8 +522,54 @@ __global__ __launch_bounds__(PO_THREADS) void pose_opt_kernel(PoArgs a) {
 
 static int launch_pose_opt(const PoArgs& a, hipStream_t st) {
     if (a.n_frames == 0) return ORB_OK;
-    hipLaunchKernelGGL(pose_opt_kernel, dim3(a.n_frames), dim3(PO_THREADS), 0, st, a);
+    static bool attr = [] {
+        return hipFuncSetAttribute((const void*)pose_opt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)PO_LDS_BYTES) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(pose_opt_kernel, dim3(a.n_frames), dim3(PO_THREADS), PO_LDS_BYTES, st, a);
     ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+extern "C" int orbba_debug_po_stamps(unsigned long long* out) {
+#ifdef ORB_PO_STAMPS
+    ORB_HIP_TRY(hipDeviceSynchronize());
+    ORB_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_po_stamps), sizeof(g_po_stamps)));
+    const unsigned long long z[8] = {0};
+    ORB_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_po_stamps), z, sizeof(z)));
+    return ORB_OK;
+#else
+    (void)out;
+    set_error("built without ORB_PO_STAMPS");
+    return ORB_EINVAL;
+#endif
+}
+
+// Diagnostic: the wavefront primitives on one wave.  in: 64 lanes x 32 values (lane-major);
+// scatter[l] = po_wave_scatter32 result of lane l; sum[l] = po_wave_sum of in[l][0].
+__global__ void po_wave_test_kernel(const double* in, double* scatter, double* sum) {
+    const int lane = threadIdx.x;
+    double v[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) v[j] = in[32 * lane + j];
+    const double s = po_wave_sum(v[0], lane);
+    scatter[lane] = po_wave_scatter32(v, lane);
+    sum[lane] = s;
+}
+
+extern "C" int orbba_debug_po_wave(const double* in, double* scatter, double* sum) {
+    ORB_CHECK_ARG(in && scatter && sum, "null argument");
+    DevBuf b;
+    int rc;
+    if ((rc = b.reserve((64 * 32 + 128) * sizeof(double)))) return rc;
+    double* d = b.as<double>();
+    ORB_HIP_TRY(hipMemcpy(d, in, 64 * 32 * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(po_wave_test_kernel, dim3(1), dim3(64), 0, nullptr, d, d + 2048, d + 2112);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpy(scatter, d + 2048, 64 * sizeof(double), hipMemcpyDeviceToHost));
+    ORB_HIP_TRY(hipMemcpy(sum, d + 2112, 64 * sizeof(double), hipMemcpyDeviceToHost));
+    b.release();
     return ORB_OK;
 }
 

@@ -46,7 +46,10 @@ __device__ __forceinline__ Q4 q_from_R(const double* m) {   // Eigen::Quaternion
 __device__ __forceinline__ void q_normalize_pos(Q4& q) {   // SE3Quat::normalizeRotation
     if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
     const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
-    if (n > 0) { q.x /= n; q.y /= n; q.z /= n; q.w /= n; }
+    if (n > 0) {   // one division, four multiplies (Eigen divides each: <= 1 ulp apart)
+        const double in = 1.0 / n;
+        q.x *= in; q.y *= in; q.z *= in; q.w *= in;
+    }
 }
 __host__ __device__ __forceinline__ void q_to_R(const double* q4, double* R) {   // toRotationMatrix
     const double x = q4[0], y = q4[1], z = q4[2], w = q4[3];
@@ -86,8 +89,10 @@ __device__ void se3_exp_update(const double* upd, double* q4, double* t3) {
         for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
         for (int i = 0; i < 9; i++) V[i] = R[i];
     } else {
-        const double s = sin(theta), c = cos(theta);
-        const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / pow(theta, 3);
+        double s, c;   // one sincos
+        sincos(theta, &s, &c);
+        const double it = 1.0 / theta;   // one division for a, b, d (<= 2 ulp from the reference's)
+        const double a = s * it, b = (1 - c) * (it * it), d = (theta - s) * (it * it * it);
         for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + a * O[i] + b * O2[i];
         for (int i = 0; i < 9; i++) V[i] = (i % 4 == 0 ? 1.0 : 0.0) + b * O[i] + d * O2[i];
     }

@@ -17,6 +17,20 @@ GOLDEN = Path(__file__).resolve().parent / "golden"
 TOL = 1e-6
 
 
+def test_wave_primitives_lane_mapping():
+    """permlane32/16 swaps + DPP rotates/quad perms must pair each lane with lane ^ m."""
+    import ctypes as C
+    from orb_slam2_refactored_amd._lib import check, lib, ptr
+    rng = np.random.default_rng(0)
+    # integers (exact in fp64 whatever the summation order)
+    x = rng.integers(-2**20, 2**20, size=(64, 32)).astype(np.float64)
+    sc, sm = np.zeros(64), np.zeros(64)
+    check(lib().orbba_debug_po_wave(ptr(x), ptr(sc), ptr(sm)), "orbba_debug_po_wave")
+    tot = x.sum(axis=0)
+    assert np.array_equal(sc, tot[np.arange(64) >> 1])
+    assert np.array_equal(sm, np.full(64, tot[0]))
+
+
 def compare(g, o):
     assert np.array_equal(g["n_inliers"], o["n_inliers"])
     assert np.array_equal(g["outlier"], o["outlier"])
