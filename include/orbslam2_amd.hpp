@@ -5,12 +5,14 @@
 //   ORB_SLAM2_AMD::ORBextractor   <- ORB_SLAM2::ORBextractor   (include/ORBextractor.h:35-81)
 //   ORB_SLAM2_AMD::ORBmatcher     <- ORB_SLAM2::ORBmatcher Hamming kernels (include/ORBmatcher.h)
 //   ORB_SLAM2_AMD::LocalBundleAdjustment <- Optimizer::LocalBundleAdjustment (include/Optimizer.h:47)
+//   ORB_SLAM2_AMD::PoseOptimization      <- Optimizer::PoseOptimization (include/Optimizer.h:49)
 // Plain-type overloads are always available; when OpenCV is on the include path the
 // cv::Mat / cv::KeyPoint overloads with the reference's exact signatures are added.
 // A non-zero C status is turned into an exception, as the reference's CV_Assert does.
 #ifndef ORBSLAM2_AMD_HPP
 #define ORBSLAM2_AMD_HPP
 
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -198,6 +200,52 @@ inline void ComputeStereoMatches(const std::vector<orbx_keypoint>& keypointsL, c
 inline void LocalBundleAdjustment(const orbba_problem& problem, orbba_result& result, const volatile int32_t* stopFlag,
                                   int device = 0) {
     check(orbba_local_ba(&problem, &result, stopFlag, device), "orbba_local_ba");
+}
+
+// int Optimizer::PoseOptimization(Frame*) (include/Optimizer.h:49, src/Optimizer.cc:345-489) over a
+// batch of frames.  One PoseFrame per frame holds the keypoints that have a map point, in keypoint
+// order (:364-410); R / t are frame->pose on entry and the SetPose argument on return, `outlier`
+// receives frame->outlier for those keypoints.  Returns each frame's inlier count.
+struct PoseFrame {
+    double R[9], t[3];
+    double fx, fy, cx, cy, bf;
+    std::vector<double> xw;         // 3 per edge: MapPoint::GetWorldPos()
+    std::vector<double> obs;        // 3 per edge: keypointsUn[i].pt.x, .y, uright[i] (< 0: monocular)
+    std::vector<double> invSigma2;  // 1 per edge: pyramid.invSigmaSq[keypointsUn[i].octave]
+    std::vector<uint8_t> outlier;   // out
+};
+
+inline std::vector<int> PoseOptimization(std::vector<PoseFrame>& frames, int device = 0) {
+    const size_t F = frames.size();
+    std::vector<int32_t> eb(F + 1, 0);
+    for (size_t f = 0; f < F; f++) eb[f + 1] = eb[f] + (int32_t)frames[f].invSigma2.size();
+    const size_t E = (size_t)eb[F];
+    std::vector<double> R(9 * F), t(3 * F), cam(5 * F), xw(3 * E), obs(3 * E), is2(E);
+    for (size_t f = 0; f < F; f++) {
+        const PoseFrame& p = frames[f];
+        std::copy(p.R, p.R + 9, R.begin() + 9 * f);
+        std::copy(p.t, p.t + 3, t.begin() + 3 * f);
+        const double c[5] = {p.fx, p.fy, p.cx, p.cy, p.bf};
+        std::copy(c, c + 5, cam.begin() + 5 * f);
+        std::copy(p.xw.begin(), p.xw.end(), xw.begin() + 3 * (size_t)eb[f]);
+        std::copy(p.obs.begin(), p.obs.end(), obs.begin() + 3 * (size_t)eb[f]);
+        std::copy(p.invSigma2.begin(), p.invSigma2.end(), is2.begin() + eb[f]);
+    }
+    std::vector<double> oR(9 * F), ot(3 * F);
+    std::vector<int32_t> ninl(F);
+    std::vector<uint8_t> outl(E);
+    const orbba_pose_batch in{(int32_t)F, eb.data(), R.data(), t.data(), cam.data(), xw.data(), obs.data(), is2.data()};
+    orbba_pose_result out{oR.data(), ot.data(), ninl.data(), outl.data()};
+    check(orbba_pose_optimization(&in, &out, device), "orbba_pose_optimization");
+    std::vector<int> result(F);
+    for (size_t f = 0; f < F; f++) {
+        PoseFrame& p = frames[f];
+        std::copy(oR.begin() + 9 * f, oR.begin() + 9 * f + 9, p.R);
+        std::copy(ot.begin() + 3 * f, ot.begin() + 3 * f + 3, p.t);
+        p.outlier.assign(outl.begin() + eb[f], outl.begin() + eb[f + 1]);
+        result[f] = ninl[f];
+    }
+    return result;
 }
 
 }  // namespace ORB_SLAM2_AMD
