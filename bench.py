@@ -172,6 +172,41 @@ def pose_leg(dev, frames=1024, edges=1000, steps=10, cpu=True):
     return r
 
 
+def projection_leg(dev, frames=256, steps=10, cpu=True):
+    """§8f row 2: batched SearchByProjection + FeaturesGrid (ORBmatcher.cc:315-382, Frame.cc:71-145):
+    per frame 2000 keypoints and 1500 local map points (th 1, nnratio 0.8), inputs in HBM."""
+    import torch
+    from orb_slam2_refactored_amd.matcher import search_by_projection_device
+    from orb_slam2_refactored_amd.synth import make_proj_batch, tile_proj_batch
+    base = make_proj_batch(21, n_frames=16, n_kp=2000, n_mp=1500)
+    b = tile_proj_batch(base, frames // 16)
+    d = {k: (torch.from_numpy(np.ascontiguousarray(v)).to(dev) if isinstance(v, np.ndarray) and k != "scale_factors"
+             else v) for k, v in b.items()}
+    km, nm = search_by_projection_device(d)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        search_by_projection_device(d, km, nm)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    r = {"workload": f"{frames} frames x (2000 keypoints, 1500 map points), th 1, grid + score + claim walk",
+         "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms,
+         "mean_matches": float(nm.double().mean().item())}
+    if cpu:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_api as O
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 3.0 or n < 16:
+            O.search_by_projection(base)
+            n += 16
+        r["cpu_baseline"] = {"frames_per_s": n / (time.perf_counter() - t0), "cores": 1, "kind": "port",
+                             "sample": "16-frame batches, oracle/orb_oracle.cpp, 1 thread"}
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -185,6 +220,7 @@ def main():
     ap.add_argument("--no-ba", action="store_true")
     ap.add_argument("--no-stereo", action="store_true")
     ap.add_argument("--no-pose", action="store_true")
+    ap.add_argument("--no-projection", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -332,6 +368,9 @@ def main():
 
     if rank == 0 and not args.no_stereo:
         result["stereo"] = stereo_leg(dev, local)
+
+    if rank == 0 and not args.no_projection:
+        result["search_by_projection"] = projection_leg(dev, cpu=world == 1 and not args.no_cpu_baseline)
 
     if rank == 0 and not args.no_pose:
         result["pose_opt"] = pose_leg(dev, cpu=world == 1 and not args.no_cpu_baseline)

@@ -185,6 +185,50 @@ int orbx_stereo_matches_batch_device(orbx_extractor* left, orbx_extractor* right
                                      void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Local-map search.  Replaces ORBmatcher::SearchByProjection(Frame&, const std::vector<MapPoint*>&,
+ * float th) (include/ORBmatcher.h:58, src/ORBmatcher.cc:315-382) together with the frame's
+ * FeaturesGrid (include/Frame.h:62-80; AssignFeatures / GetFeaturesInArea, src/Frame.cc:71-145),
+ * batched over frames.  Per frame f: keypoints [kp_begin[f], kp_begin[f+1]) (keypointsUn order)
+ * and the local map points [mp_begin[f], mp_begin[f+1]) (vector order) with the fields
+ * IsInFrustum filled (Tracking.cc:554-605).
+ * ---------------------------------------------------------------------------------------- */
+#define ORBM_GRID_COLS 64
+#define ORBM_GRID_ROWS 48
+#define ORBM_PROJ_MAX_KP 8192   /* keypoints per frame */
+
+typedef struct orbm_proj_batch {
+    int32_t        n_frames;
+    int32_t        total_kp, total_mp;   /* kp_begin[n_frames], mp_begin[n_frames] (workspace sizing) */
+    const int32_t* kp_begin;     /* n_frames + 1 */
+    const float*   kp_xy;        /* keypointsUn pt, total_kp x 2 */
+    const int32_t* kp_octave;    /* keypointsUn octave */
+    const float*   kp_uright;    /* uright */
+    const uint8_t* kp_desc;      /* descriptors, total_kp x 32 */
+    const uint8_t* kp_claimed;   /* mappoints[i] && mappoints[i]->Observations() > 0 on entry (NULL: none) */
+    const float*   bounds;       /* n_frames x 4: imageBounds minx, maxx, miny, maxy */
+    const int32_t* mp_begin;     /* n_frames + 1 */
+    const uint8_t* mp_valid;     /* trackInView && !isBad() (:320) */
+    const float*   mp_proj;      /* total_mp x 3: trackProjX, trackProjY, trackProjXR */
+    const float*   mp_view_cos;  /* trackViewCos */
+    const int32_t* mp_level;     /* trackScaleLevel (0 .. n_levels-1) */
+    const uint8_t* mp_desc;      /* GetDescriptor(), total_mp x 32 */
+    const uint8_t* mp_has_obs;   /* Observations() > 0 (a keypoint it claims is then skipped, :339) */
+    int32_t        n_levels;
+    const float*   scale_factors;/* n_levels (frame.pyramid.scaleFactors), host memory in both entries */
+    float          th;           /* SearchLocalPoints: 1, 3 (RGB-D) or 5 after relocalisation (Tracking.cc:1246) */
+    float          nnratio;      /* ORBmatcher(0.8f) in SearchLocalPoints (Tracking.cc:646) */
+} orbm_proj_batch;
+
+/* kp_match[k]: frame-relative index of the map point the call assigned to keypoint k (the last
+ * assignment of frame.mappoints[bestIdx] = mappoint, :376), -1 when the call assigned none.
+ * n_matches[f]: SearchByProjection's return value; -1 (device entry) when a frame has more than
+ * ORBM_PROJ_MAX_KP keypoints.  Host entry: every pointer is host memory, synchronous. */
+int orbm_search_by_projection(const orbm_proj_batch* b, int32_t* kp_match, int32_t* n_matches, int device);
+/* Device entry: every array in HBM except scale_factors; enqueue only on `stream`. */
+int orbm_search_by_projection_device(const orbm_proj_batch* b, int32_t* kp_match, int32_t* n_matches,
+                                     void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Local bundle adjustment.  Replaces Optimizer::LocalBundleAdjustment (include/Optimizer.h:47,
  * src/Optimizer.cc:491-736) from the vertex/edge setup (:540-631) onwards: the caller
  * gathers local / fixed keyframes and map points and flattens them in reference order.

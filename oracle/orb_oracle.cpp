@@ -26,6 +26,8 @@
  *                  :54-120, core/robust_kernel_impl.cpp:65-91, types/types_six_dof_expmap.{h,cpp},
  *                  types/se3quat.h, types/types_sba.h — Eigen replaced by explicit fp64 code,
  *                  SimplicialLDLT by a dense LDLT of the reduced camera system.
+ *   Grid/Project   src/Frame.cc:32-34,71-145 (FeaturesGrid), src/ORBmatcher.cc:53,315-382
+ *                  (SearchByProjection(Frame&, const std::vector<MapPoint*>&, float)).
  *   PoseOpt        src/Optimizer.cc:345-489 (4 x optimize(10) with chi2 classification) over
  *                  the unary edges of types_six_dof_expmap.h:143-202 / .cpp:266-364 and
  *                  solvers/linear_solver_dense.h:65-113 (Eigen LDLT -> unpivoted fp64 LDL^T).
@@ -51,6 +53,7 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <list>
 #include <vector>
 
@@ -1057,6 +1060,55 @@ struct BA {
 };
 
 // ---------------------------------------------------------------------------------------------
+// FeaturesGrid (src/Frame.cc:32-34 rounding, :71-145) and SearchByProjection (ORBmatcher.cc:315-382)
+// ---------------------------------------------------------------------------------------------
+struct FeaturesGrid {
+    static const int ROWS = 48, COLS = 64;
+    float invW = 0, invH = 0, minx = 0, miny = 0;
+    int nlevels = 0, n = 0;
+    const float* xy = nullptr;
+    const int32_t* oct = nullptr;
+    std::vector<size_t> grid[COLS][ROWS];
+
+    static int Round(float v) { return static_cast<int>(std::round(v)); }
+    static int RoundUp(float v) { return static_cast<int>(std::ceil(v)); }
+    static int RoundDn(float v) { return static_cast<int>(std::floor(v)); }
+
+    void assign(const float* kxy, const int32_t* koct, int nk, const float* bounds, int nl) {   // :71-100
+        invW = COLS / (bounds[1] - bounds[0]);   // ImageBounds::Width() = maxx - minx (:41-44)
+        invH = ROWS / (bounds[3] - bounds[2]);
+        minx = bounds[0]; miny = bounds[2];
+        xy = kxy; oct = koct; n = nk; nlevels = nl;
+        for (int i = 0; i < n; i++) {
+            const int cx = Round(invW * (xy[2 * i] - minx));
+            const int cy = Round(invH * (xy[2 * i + 1] - miny));
+            if (cx < 0 || cx >= COLS || cy < 0 || cy >= ROWS) continue;
+            grid[cx][cy].push_back(i);
+        }
+    }
+    std::vector<size_t> in_area(float x, float y, float r, int minLevel, int maxLevel) const {   // :102-145
+        std::vector<size_t> indices;
+        const int mincx = std::max(RoundDn(invW * (x - r - minx)), 0);
+        const int maxcx = std::min(RoundUp(invW * (x + r - minx)), COLS - 1);
+        const int mincy = std::max(RoundDn(invH * (y - r - miny)), 0);
+        const int maxcy = std::min(RoundUp(invH * (y + r - miny)), ROWS - 1);
+        if (mincx >= COLS || maxcx < 0 || mincy >= ROWS || maxcy < 0) return indices;
+        const bool checkLevels = (minLevel > 0) || (maxLevel >= 0);
+        if (maxLevel < 0) maxLevel = nlevels;
+        for (int cx = mincx; cx <= maxcx; cx++)
+            for (int cy = mincy; cy <= maxcy; cy++)
+                for (size_t idx : grid[cx][cy]) {
+                    const int level = oct[idx];
+                    if (checkLevels && (level < minLevel || level > maxLevel)) continue;
+                    const float distx = xy[2 * idx] - x;
+                    const float disty = xy[2 * idx + 1] - y;
+                    if (std::fabs(distx) < r && std::fabs(disty) < r) indices.push_back(idx);
+                }
+        return indices;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
 // PoseOptimization: one SE3 vertex, unary edges (types_six_dof_expmap.h:143-202,
 // types_six_dof_expmap.cpp:266-364), LinearSolverDense under OptimizationAlgorithmLevenberg.
 // ---------------------------------------------------------------------------------------------
@@ -1536,6 +1588,86 @@ int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile i
         }
     }
     std::memcpy(res->points, ba.X.data(), sizeof(double) * 3 * ba.N);
+    return 0;
+}
+
+// FeaturesGrid::AssignFeatures as CSR: cell c = cx * 48 + cy owns idx[cell_start[c] .. cell_start[c+1]).
+int oracle_features_grid(const float* xy, const int32_t* octave, int n, const float* bounds, int32_t* cell_start,
+                         int32_t* idx) {
+    std::unique_ptr<FeaturesGrid> g(new FeaturesGrid);
+    g->assign(xy, octave, n, bounds, 8);
+    int k = 0;
+    for (int cx = 0; cx < FeaturesGrid::COLS; cx++)
+        for (int cy = 0; cy < FeaturesGrid::ROWS; cy++) {
+            cell_start[cx * FeaturesGrid::ROWS + cy] = k;
+            for (size_t i : g->grid[cx][cy]) idx[k++] = (int32_t)i;
+        }
+    cell_start[FeaturesGrid::COLS * FeaturesGrid::ROWS] = k;
+    return k;
+}
+
+// FeaturesGrid::GetFeaturesInArea for one query; returns the count (out: up to cap indices, in order).
+int oracle_features_in_area(const float* xy, const int32_t* octave, int n, const float* bounds, int nlevels,
+                            float x, float y, float r, int minLevel, int maxLevel, int32_t* out, int cap) {
+    std::unique_ptr<FeaturesGrid> g(new FeaturesGrid);
+    g->assign(xy, octave, n, bounds, nlevels);
+    const std::vector<size_t> v = g->in_area(x, y, r, minLevel, maxLevel);
+    for (size_t i = 0; i < v.size() && (int)i < cap; i++) out[i] = (int32_t)v[i];
+    return (int)v.size();
+}
+
+// ORBmatcher::SearchByProjection(Frame&, const std::vector<MapPoint*>&, float th) (:315-382) per frame.
+// frame.mappoints is modelled by `owner` (claimed keypoints, :339) and kp_match (assignments).
+int oracle_search_by_projection(const orbm_proj_batch* b, int32_t* kp_match, int32_t* n_matches) {
+    const int TH_HIGH = 100;
+    for (int f = 0; f < b->n_frames; f++) {
+        const int k0 = b->kp_begin[f], nk = b->kp_begin[f + 1] - k0;
+        const int m0 = b->mp_begin[f], nm = b->mp_begin[f + 1] - m0;
+        std::unique_ptr<FeaturesGrid> g(new FeaturesGrid);
+        g->assign(b->kp_xy + 2 * (size_t)k0, b->kp_octave + k0, nk, b->bounds + 4 * (size_t)f, b->n_levels);
+        // keypoint "has a map point with Observations() > 0"
+        std::vector<uint8_t> claimed(nk, 0);
+        if (b->kp_claimed) for (int i = 0; i < nk; i++) claimed[i] = b->kp_claimed[k0 + i];
+        for (int i = 0; i < nk; i++) kp_match[k0 + i] = -1;
+        int nmatches = 0;
+        for (int j = 0; j < nm; j++) {
+            const int mj = m0 + j;
+            if (!b->mp_valid[mj]) continue;
+            const int predictedScale = b->mp_level[mj];
+            const float viewCos = b->mp_view_cos[mj];
+            const float r = viewCos > 0.998 ? 2.5f : 4.f;   // RadiusByViewingCos (:53)
+            const float radius = b->th * r * b->scale_factors[predictedScale];
+            const float u = b->mp_proj[3 * (size_t)mj], v = b->mp_proj[3 * (size_t)mj + 1];
+            const float uR = b->mp_proj[3 * (size_t)mj + 2];
+            const std::vector<size_t> indices = g->in_area(u, v, radius, predictedScale - 1, predictedScale);
+            if (indices.empty()) continue;
+            const uint8_t* desc1 = b->mp_desc + 32 * (size_t)mj;
+            int bestDist = 256, bestLevel = -1, secondbestDist = 256, secondBestLevel = -1, bestIdx = -1;
+            for (size_t idx : indices) {
+                if (claimed[idx]) continue;
+                const float ur = b->kp_uright[k0 + idx];
+                if (ur > 0 && std::fabs(uR - ur) > radius) continue;
+                const int dist = hamming(desc1, b->kp_desc + 32 * (size_t)(k0 + idx));
+                if (dist < bestDist) {
+                    secondbestDist = bestDist;
+                    bestDist = dist;
+                    secondBestLevel = bestLevel;
+                    bestLevel = b->kp_octave[k0 + idx];
+                    bestIdx = (int)idx;
+                } else if (dist < secondbestDist) {
+                    secondBestLevel = b->kp_octave[k0 + idx];
+                    secondbestDist = dist;
+                }
+            }
+            if (bestDist <= TH_HIGH) {
+                if (bestLevel == secondBestLevel && bestDist > b->nnratio * secondbestDist) continue;
+                kp_match[k0 + bestIdx] = j;
+                if (b->mp_has_obs[mj]) claimed[bestIdx] = 1;
+                nmatches++;
+            }
+        }
+        n_matches[f] = nmatches;
+    }
     return 0;
 }
 

@@ -43,6 +43,16 @@ class BAResult(C.Structure):
                 ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2)]
 
 
+class ProjBatch(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("total_kp", C.c_int32), ("total_mp", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_uright", C.c_void_p),
+                ("kp_desc", C.c_void_p), ("kp_claimed", C.c_void_p), ("bounds", C.c_void_p),
+                ("mp_begin", C.c_void_p), ("mp_valid", C.c_void_p), ("mp_proj", C.c_void_p),
+                ("mp_view_cos", C.c_void_p), ("mp_level", C.c_void_p), ("mp_desc", C.c_void_p),
+                ("mp_has_obs", C.c_void_p), ("n_levels", C.c_int32), ("scale_factors", C.c_void_p),
+                ("th", C.c_float), ("nnratio", C.c_float)]
+
+
 class PoseBatch(C.Structure):
     _fields_ = [("n_frames", C.c_int32), ("edge_begin", C.c_void_p), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
                 ("cam", C.c_void_p), ("xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
@@ -82,6 +92,8 @@ SIGNATURES = {
                                               C.c_float, VP, VP]),
     "orbx_stereo_matches_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, VP, VP, VP, C.c_int, C.c_float,
                                                    C.c_float, VP, VP, VP]),
+    "orbm_search_by_projection": (C.c_int, [C.POINTER(ProjBatch), VP, VP, C.c_int]),
+    "orbm_search_by_projection_device": (C.c_int, [C.POINTER(ProjBatch), VP, VP, VP]),
     "orbba_local_ba": (C.c_int, [C.POINTER(BAProblem), C.POINTER(BAResult), VP, C.c_int]),
     "orbba_pose_optimization": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), C.c_int]),
     "orbba_pose_optimization_device": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), VP]),

@@ -1,0 +1,517 @@
+// orbp.hip — FeaturesGrid + ORBmatcher::SearchByProjection(Frame&, const std::vector<MapPoint*>&, th)
+// on gfx950, batched over frames.
+//
+// Reference: src/Frame.cc:71-145 (AssignFeatures / GetFeaturesInArea, Round / RoundUp / RoundDn at
+// :32-34), src/ORBmatcher.cc:315-382 (the search) and :53 (RadiusByViewingCos).
+//
+// The reference loop is sequential in one respect only: a keypoint that an earlier map point has
+// claimed (frame.mappoints[idx] with Observations() > 0, :339) is skipped by the later ones.  So
+// the work splits into two data-parallel stages and one thin sequential one:
+//   pj_grid_kernel   one WG per frame: cell of every keypoint (Round of the scaled offset), a
+//                    bitonic sort of (cell << 13 | index) in LDS, the sorted indices and the
+//                    3072 + 1 cell starts.  Cell c = cx * 48 + cy, so a window's column cx is one
+//                    contiguous range and sorted position = GetFeaturesInArea's scan order.
+//   pj_score_kernel  one wavefront per map point: window cells, level / area / entry-claim /
+//                    stereo gates, Hamming distance, and the K smallest keys (dist << 13 | scan
+//                    position) = the first K of the candidates stably sorted by distance, plus
+//                    the candidate count.
+//   pj_walk_kernel   one wavefront per frame walks the map points in order with a claim bitmap
+//                    in LDS: best / second best = the first two unclaimed of the K (the
+//                    reference's strict-< scan keeps exactly the first two of that stable order);
+//                    when fewer than two of the K are unclaimed and more candidates exist, the
+//                    wavefront rescans that map point's window against the bitmap.  Then the
+//                    TH_HIGH / same-level ratio test and the claim.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+
+namespace orbamd {
+
+constexpr int PJ_COLS = ORBM_GRID_COLS, PJ_ROWS = ORBM_GRID_ROWS, PJ_CELLS = PJ_COLS * PJ_ROWS;
+constexpr int PJ_MAXKP = ORBM_PROJ_MAX_KP;
+constexpr int PJ_IDX_BITS = 13;
+static_assert((1 << PJ_IDX_BITS) == PJ_MAXKP, "sort key packs the keypoint index in 13 bits");
+constexpr uint32_t PJ_IDX_MASK = (1u << PJ_IDX_BITS) - 1;
+#ifndef PJ_K_OVERRIDE
+constexpr int PJ_K = 4;          // candidates kept per map point
+#else
+constexpr int PJ_K = PJ_K_OVERRIDE;   // diagnostic builds: K = 1 forces the rescan path
+#endif
+constexpr int PJ_TH_HIGH = 100;  // ORBmatcher.cc:41
+constexpr int PJ_MAX_LEVELS = 32;
+constexpr uint32_t PJ_NONE = 0xffffffffu;
+
+struct PjArgs {
+    int n_frames;
+    const int32_t* kp_begin;
+    const float* kp_xy;
+    const int32_t* kp_oct;
+    const float* kp_ur;
+    const uint8_t* kp_desc;
+    const uint8_t* kp_claimed;
+    const float* bounds;
+    const int32_t* mp_begin;
+    const uint8_t* mp_valid;
+    const float* mp_proj;
+    const float* mp_vcos;
+    const int32_t* mp_level;
+    const uint8_t* mp_desc;
+    const uint8_t* mp_has_obs;
+    int n_levels;
+    float scale[PJ_MAX_LEVELS];
+    float th, nnratio;
+    int total_mp;
+    // workspace
+    int32_t* grid_idx;    // total_kp: frame-relative keypoint index at each sorted position
+    int32_t* grid_start;  // n_frames x (PJ_CELLS + 1)
+    int32_t* mp_cnt;      // total_mp
+    uint2* mp_top;        // total_mp x PJ_K: (key, index | level << 24)
+    // outputs
+    int32_t* kp_match;
+    int32_t* n_matches;
+};
+
+__device__ __forceinline__ int pj_hamming(const uint8_t* a, const uint8_t* b) {
+    const uint4* x = reinterpret_cast<const uint4*>(a);
+    const uint4* y = reinterpret_cast<const uint4*>(b);
+    const uint4 a0 = x[0], a1 = x[1], b0 = y[0], b1 = y[1];
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__device__ __forceinline__ uint32_t pj_wave_min(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
+    return v;
+}
+
+__device__ __forceinline__ int pj_wave_sum(int v) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------- FeaturesGrid::AssignFeatures
+__global__ __launch_bounds__(256) void pj_grid_kernel(PjArgs a) {
+    __shared__ uint32_t keys[PJ_MAXKP];
+    const int f = blockIdx.x;
+    const int k0 = a.kp_begin[f], n = a.kp_begin[f + 1] - k0;
+    int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
+    if (n > PJ_MAXKP) return;   // pj_walk_kernel reports the frame
+    const float* bd = a.bounds + 4 * (size_t)f;
+    const float minx = bd[0], miny = bd[2];
+    const float invW = PJ_COLS / (bd[1] - bd[0]);   // COLS / ImageBounds::Width() (Frame.cc:73)
+    const float invH = PJ_ROWS / (bd[3] - bd[2]);
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += 256) {
+        uint32_t key = PJ_NONE;
+        if (i < n) {
+            const int cx = (int)roundf(invW * (a.kp_xy[2 * (size_t)(k0 + i)] - minx));   // Round (:32, :91)
+            const int cy = (int)roundf(invH * (a.kp_xy[2 * (size_t)(k0 + i) + 1] - miny));
+            if (cx >= 0 && cx < PJ_COLS && cy >= 0 && cy < PJ_ROWS)
+                key = ((uint32_t)(cx * PJ_ROWS + cy) << PJ_IDX_BITS) | (uint32_t)i;
+        }
+        keys[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)       // bitonic sort; keys are unique (index in the low bits)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t x = keys[i], y = keys[ixj];
+                    if ((x > y) == ((i & k) == 0)) { keys[i] = y; keys[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int p = threadIdx.x; p < n; p += 256)
+        a.grid_idx[k0 + p] = keys[p] == PJ_NONE ? -1 : (int32_t)(keys[p] & PJ_IDX_MASK);
+    for (int c = threadIdx.x; c <= PJ_CELLS; c += 256) {   // lower_bound(c << 13)
+        const uint32_t want = (uint32_t)c << PJ_IDX_BITS;
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (keys[mid] < want) lo = mid + 1; else hi = mid;
+        }
+        cs[c] = lo;
+    }
+}
+
+// ---------------------------------------------------------------- GetFeaturesInArea + gates
+struct PjPoint {   // one map point's search window (ORBmatcher.cc:322-333, Frame.cc:109-119)
+    int mincx, maxcx, mincy, maxcy, lvl;
+    float u, v, uR, radius;
+    bool any;
+};
+
+__device__ __forceinline__ PjPoint pj_point(const PjArgs& a, int f, int mj) {
+    PjPoint w;
+    w.lvl = a.mp_level[mj];
+    const float vcos = a.mp_vcos[mj];
+    const float r = (double)vcos > 0.998 ? 2.5f : 4.f;   // RadiusByViewingCos (:53), double compare
+    w.radius = a.th * r * a.scale[w.lvl];
+    w.u = a.mp_proj[3 * (size_t)mj];
+    w.v = a.mp_proj[3 * (size_t)mj + 1];
+    w.uR = a.mp_proj[3 * (size_t)mj + 2];
+    const float* bd = a.bounds + 4 * (size_t)f;
+    const float minx = bd[0], miny = bd[2];
+    const float invW = PJ_COLS / (bd[1] - bd[0]), invH = PJ_ROWS / (bd[3] - bd[2]);
+    w.mincx = max((int)floorf(invW * (w.u - w.radius - minx)), 0);
+    w.maxcx = min((int)ceilf(invW * (w.u + w.radius - minx)), PJ_COLS - 1);
+    w.mincy = max((int)floorf(invH * (w.v - w.radius - miny)), 0);
+    w.maxcy = min((int)ceilf(invH * (w.v + w.radius - miny)), PJ_ROWS - 1);
+    w.any = !(w.mincx >= PJ_COLS || w.maxcx < 0 || w.mincy >= PJ_ROWS || w.maxcy < 0);
+    return w;
+}
+
+// Calls fn(key, idx, level) for each candidate of this lane that passes every gate; key =
+// dist << 13 | sorted position (increasing along GetFeaturesInArea's scan order).
+template <bool DYN, class Fn>
+__device__ __forceinline__ void pj_scan(const PjArgs& a, int f, int mj, const PjPoint& w, const uint32_t* bits,
+                                        int lane, Fn&& fn) {
+    if (!w.any) return;
+    const int k0 = a.kp_begin[f];
+    const int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
+    const uint8_t* d1 = a.mp_desc + 32 * (size_t)mj;
+    for (int cx = w.mincx; cx <= w.maxcx; cx++) {
+        const int p0 = cs[cx * PJ_ROWS + w.mincy], p1 = cs[cx * PJ_ROWS + w.maxcy + 1];
+        for (int p = p0 + lane; p < p1; p += 64) {
+            const int idx = a.grid_idx[k0 + p];
+            const int k = k0 + idx;
+            const int level = a.kp_oct[k];
+            if (level < w.lvl - 1 || level > w.lvl) continue;   // checkLevels (maxLevel >= 0)
+            const float distx = a.kp_xy[2 * (size_t)k] - w.u;
+            const float disty = a.kp_xy[2 * (size_t)k + 1] - w.v;
+            if (!(fabsf(distx) < w.radius && fabsf(disty) < w.radius)) continue;
+            if (a.kp_claimed && a.kp_claimed[k]) continue;
+            if (DYN && ((bits[idx >> 5] >> (idx & 31)) & 1u)) continue;
+            const float ur = a.kp_ur[k];
+            if (ur > 0 && fabsf(w.uR - ur) > w.radius) continue;
+            const int dist = pj_hamming(d1, a.kp_desc + 32 * (size_t)k);
+            fn(((uint32_t)dist << PJ_IDX_BITS) | (uint32_t)p, idx, level);
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void pj_insert(uint32_t (&t)[K], uint32_t key) {
+#pragma unroll
+    for (int r = 0; r < K; r++) {
+        const uint32_t lo = min(t[r], key), hi = max(t[r], key);
+        t[r] = lo;
+        key = hi;
+    }
+}
+
+// Pops the wave's K smallest keys (one lane owns each key: positions are unique).
+template <int K>
+__device__ __forceinline__ void pj_wave_topk(uint32_t (&t)[K], uint32_t (&out)[K]) {
+#pragma unroll
+    for (int r = 0; r < K; r++) {
+        const uint32_t m = pj_wave_min(t[0]);
+        out[r] = m;
+        if (t[0] == m && m != PJ_NONE) {
+#pragma unroll
+            for (int q = 0; q + 1 < K; q++) t[q] = t[q + 1];
+            t[K - 1] = PJ_NONE;
+        }
+    }
+}
+
+__device__ __forceinline__ int pj_frame_of(const int32_t* begin, int n_frames, int j) {   // begin[f] <= j < begin[f+1]
+    int lo = 0, hi = n_frames - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (begin[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------- per map point: top-K candidates
+__global__ __launch_bounds__(256) void pj_score_kernel(PjArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int mj = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (mj >= a.total_mp) return;   // wavefront-uniform
+    const int f = pj_frame_of(a.mp_begin, a.n_frames, mj);
+    const int n = a.kp_begin[f + 1] - a.kp_begin[f];
+    int cnt = 0;
+    uint32_t out[PJ_K];
+#pragma unroll
+    for (int r = 0; r < PJ_K; r++) out[r] = PJ_NONE;
+    const int lvl = a.mp_level[mj];
+    if (n <= PJ_MAXKP && a.mp_valid[mj] && lvl >= 0 && lvl < a.n_levels) {
+        const PjPoint w = pj_point(a, f, mj);
+        uint32_t t[PJ_K];
+#pragma unroll
+        for (int r = 0; r < PJ_K; r++) t[r] = PJ_NONE;
+        int c = 0;
+        pj_scan<false>(a, f, mj, w, nullptr, lane, [&](uint32_t key, int, int) {
+            pj_insert(t, key);
+            c++;
+        });
+        cnt = pj_wave_sum(c);
+        pj_wave_topk(t, out);
+    }
+    if (lane == 0) a.mp_cnt[mj] = cnt;
+    if (lane < PJ_K) {
+        uint32_t key = out[0];
+#pragma unroll
+        for (int r = 1; r < PJ_K; r++) key = lane == r ? out[r] : key;
+        uint32_t ent = 0;
+        if (key != PJ_NONE) {
+            const int k0 = a.kp_begin[f];
+            const int idx = a.grid_idx[k0 + (int)(key & PJ_IDX_MASK)];
+            ent = (uint32_t)idx | ((uint32_t)a.kp_oct[k0 + idx] << 24);
+        }
+        a.mp_top[(size_t)mj * PJ_K + lane] = make_uint2(key, ent);
+    }
+}
+
+// ---------------------------------------------------------------- the ordered claim walk
+constexpr int PJ_CHUNK = 64;
+
+__global__ __launch_bounds__(64) void pj_walk_kernel(PjArgs a) {
+    __shared__ uint32_t bits[PJ_MAXKP / 32];
+    __shared__ uint2 s_top[PJ_CHUNK * PJ_K];
+    __shared__ int s_cnt[PJ_CHUNK];
+    __shared__ uint8_t s_flag[PJ_CHUNK];   // bit 0 valid, bit 1 has_obs
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x;
+    const int k0 = a.kp_begin[f], n = a.kp_begin[f + 1] - k0;
+    const int m0 = a.mp_begin[f], nm = a.mp_begin[f + 1] - m0;
+    for (int i = lane; i < n; i += 64) a.kp_match[k0 + i] = -1;
+    if (n > PJ_MAXKP) {
+        if (lane == 0) a.n_matches[f] = -1;
+        return;
+    }
+    for (int w = lane; w < (n + 31) / 32; w += 64) {
+        uint32_t v = 0;
+        if (a.kp_claimed)
+            for (int b = 0; b < 32 && w * 32 + b < n; b++) v |= (uint32_t)(a.kp_claimed[k0 + w * 32 + b] != 0) << b;
+        bits[w] = v;
+    }
+    int nmatches = 0;
+    for (int c = 0; c < nm; c += PJ_CHUNK) {
+        const int m = min(PJ_CHUNK, nm - c);
+        if (lane < m) {
+            const int mj = m0 + c + lane;
+            const int lvl = a.mp_level[mj];
+            const bool ok = a.mp_valid[mj] && lvl >= 0 && lvl < a.n_levels;
+            s_cnt[lane] = ok ? a.mp_cnt[mj] : 0;
+            s_flag[lane] = (uint8_t)((ok ? 1 : 0) | (a.mp_has_obs[mj] ? 2 : 0));
+        }
+        for (int q = lane; q < m * PJ_K; q += 64) s_top[q] = a.mp_top[(size_t)(m0 + c) * PJ_K + q];
+        __syncthreads();
+        for (int i = 0; i < m; i++) {
+            const int cnt = s_cnt[i];
+            if (cnt == 0) continue;   // invalid, or GetFeaturesInArea / the gates left nothing
+            uint2 e = make_uint2(PJ_NONE, 0);
+            bool avail = false;
+            if (lane < PJ_K) {
+                e = s_top[i * PJ_K + lane];
+                const int idx = (int)(e.y & 0xffffffu);
+                avail = e.x != PJ_NONE && !((bits[idx >> 5] >> (idx & 31)) & 1u);
+            }
+            const unsigned long long mask = __ballot(avail);
+            uint32_t bkey = PJ_NONE, skey = PJ_NONE;
+            int bidx = -1, blev = -1, slev = -1;
+            if (__popcll(mask) >= 2 || cnt <= PJ_K) {
+                if (mask) {
+                    const int l0 = __ffsll((long long)mask) - 1;
+                    bkey = __shfl(e.x, l0, 64);
+                    const uint32_t be = __shfl(e.y, l0, 64);
+                    bidx = (int)(be & 0xffffffu);
+                    blev = (int)(be >> 24);
+                    const unsigned long long rest = mask & (mask - 1);
+                    if (rest) {
+                        const int l1 = __ffsll((long long)rest) - 1;
+                        skey = __shfl(e.x, l1, 64);
+                        slev = (int)(__shfl(e.y, l1, 64) >> 24);
+                    }
+                }
+            } else {   // the K kept candidates are exhausted by earlier claims: rescan the window
+                const int mj = m0 + c + i;
+                const PjPoint w = pj_point(a, f, mj);
+                uint32_t t[2] = {PJ_NONE, PJ_NONE};
+                pj_scan<true>(a, f, mj, w, bits, lane, [&](uint32_t key, int, int) { pj_insert(t, key); });
+                uint32_t o[2];
+                pj_wave_topk(t, o);
+                bkey = o[0];
+                skey = o[1];
+                if (bkey != PJ_NONE) {
+                    bidx = a.grid_idx[k0 + (int)(bkey & PJ_IDX_MASK)];
+                    blev = a.kp_oct[k0 + bidx];
+                }
+                if (skey != PJ_NONE) slev = a.kp_oct[k0 + a.grid_idx[k0 + (int)(skey & PJ_IDX_MASK)]];
+            }
+            const int bestDist = bkey == PJ_NONE ? 256 : (int)(bkey >> PJ_IDX_BITS);
+            const int secondDist = skey == PJ_NONE ? 256 : (int)(skey >> PJ_IDX_BITS);
+            if (bestDist <= PJ_TH_HIGH) {   // :367-377
+                if (blev == slev && (float)bestDist > a.nnratio * (float)secondDist) continue;
+                if (lane == 0) {
+                    a.kp_match[k0 + bidx] = c + i;
+                    if (s_flag[i] & 2) bits[bidx >> 5] |= 1u << (bidx & 31);
+                }
+                nmatches++;
+            }
+        }
+        __syncthreads();
+    }
+    if (lane == 0) a.n_matches[f] = nmatches;
+}
+
+static int launch_projection(PjArgs& a, int total_kp, hipStream_t st) {
+    if (a.n_frames == 0) return ORB_OK;
+    (void)total_kp;
+    hipLaunchKernelGGL(pj_grid_kernel, dim3(a.n_frames), dim3(256), 0, st, a);
+    ORB_HIP_TRY(hipGetLastError());
+    if (a.total_mp > 0) {
+        hipLaunchKernelGGL(pj_score_kernel, dim3((a.total_mp + 3) / 4), dim3(256), 0, st, a);
+        ORB_HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(pj_walk_kernel, dim3(a.n_frames), dim3(64), 0, st, a);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+struct PjScratch {
+    DevBuf ws, io;
+    int device = -1;
+};
+thread_local PjScratch g_pj;
+
+static size_t pj_workspace_bytes(int n_frames, int total_kp, int total_mp) {
+    return align_up((size_t)std::max(total_kp, 1) * 4, 256) + align_up((size_t)n_frames * (PJ_CELLS + 1) * 4, 256) +
+           align_up((size_t)std::max(total_mp, 1) * 4, 256) + align_up((size_t)std::max(total_mp, 1) * PJ_K * 8, 256);
+}
+
+static void pj_carve(PjArgs& a, char* ws, int n_frames, int total_kp, int total_mp) {
+    size_t o = 0;
+    a.grid_idx = (int32_t*)(ws + o);
+    o += align_up((size_t)std::max(total_kp, 1) * 4, 256);
+    a.grid_start = (int32_t*)(ws + o);
+    o += align_up((size_t)n_frames * (PJ_CELLS + 1) * 4, 256);
+    a.mp_cnt = (int32_t*)(ws + o);
+    o += align_up((size_t)std::max(total_mp, 1) * 4, 256);
+    a.mp_top = (uint2*)(ws + o);
+}
+
+static int pj_common_args(const orbm_proj_batch* b, PjArgs& a) {
+    ORB_CHECK_ARG(b, "null argument");
+    ORB_CHECK_ARG(b->n_frames >= 0 && b->total_kp >= 0 && b->total_mp >= 0, "negative sizes");
+    ORB_CHECK_ARG(b->n_levels >= 1 && b->n_levels <= PJ_MAX_LEVELS && b->scale_factors, "bad scale pyramid");
+    std::memset(&a, 0, sizeof(a));
+    a.n_frames = b->n_frames;
+    a.n_levels = b->n_levels;
+    for (int l = 0; l < b->n_levels; l++) a.scale[l] = b->scale_factors[l];
+    a.th = b->th;
+    a.nnratio = b->nnratio;
+    a.total_mp = b->total_mp;
+    return ORB_OK;
+}
+
+}  // namespace orbamd
+
+using namespace orbamd;
+
+extern "C" int orbm_search_by_projection_device(const orbm_proj_batch* b, int32_t* kp_match, int32_t* n_matches,
+                                                void* stream) {
+    PjArgs a;
+    int rc;
+    if ((rc = pj_common_args(b, a))) return rc;
+    if (b->n_frames == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kp_begin && b->mp_begin && b->bounds && kp_match && n_matches, "null array");
+    ORB_CHECK_ARG(b->total_kp == 0 || (b->kp_xy && b->kp_octave && b->kp_uright && b->kp_desc), "null keypoint array");
+    ORB_CHECK_ARG(b->total_mp == 0 || (b->mp_valid && b->mp_proj && b->mp_view_cos && b->mp_level && b->mp_desc &&
+                                       b->mp_has_obs),
+                  "null map point array");
+    a.kp_begin = b->kp_begin; a.kp_xy = b->kp_xy; a.kp_oct = b->kp_octave; a.kp_ur = b->kp_uright;
+    a.kp_desc = b->kp_desc; a.kp_claimed = b->kp_claimed; a.bounds = b->bounds;
+    a.mp_begin = b->mp_begin; a.mp_valid = b->mp_valid; a.mp_proj = b->mp_proj; a.mp_vcos = b->mp_view_cos;
+    a.mp_level = b->mp_level; a.mp_desc = b->mp_desc; a.mp_has_obs = b->mp_has_obs;
+    a.kp_match = kp_match;
+    a.n_matches = n_matches;
+    int dev = 0;
+    ORB_HIP_TRY(hipGetDevice(&dev));
+    if (g_pj.device != dev) {
+        g_pj.ws.release();
+        g_pj.io.release();
+        g_pj.device = dev;
+    }
+    if ((rc = g_pj.ws.reserve(pj_workspace_bytes(b->n_frames, b->total_kp, b->total_mp)))) return rc;
+    pj_carve(a, g_pj.ws.as<char>(), b->n_frames, b->total_kp, b->total_mp);
+    return launch_projection(a, b->total_kp, (hipStream_t)stream);
+}
+
+extern "C" int orbm_search_by_projection(const orbm_proj_batch* b, int32_t* kp_match, int32_t* n_matches,
+                                         int device) {
+    PjArgs a;
+    int rc;
+    if ((rc = pj_common_args(b, a))) return rc;
+    const int F = b->n_frames;
+    if (F == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kp_begin && b->mp_begin && b->bounds && kp_match && n_matches, "null array");
+    ORB_CHECK_ARG(b->kp_begin[0] == 0 && b->mp_begin[0] == 0 && b->kp_begin[F] == b->total_kp &&
+                      b->mp_begin[F] == b->total_mp,
+                  "kp_begin / mp_begin must start at 0 and end at total_kp / total_mp");
+    for (int f = 0; f < F; f++) {
+        ORB_CHECK_ARG(b->kp_begin[f + 1] >= b->kp_begin[f] && b->mp_begin[f + 1] >= b->mp_begin[f],
+                      "offsets must be non-decreasing");
+        ORB_CHECK_ARG(b->kp_begin[f + 1] - b->kp_begin[f] <= PJ_MAXKP, "frame has more than ORBM_PROJ_MAX_KP keypoints");
+    }
+    const int K = b->total_kp, M = b->total_mp;
+    ORB_CHECK_ARG(K == 0 || (b->kp_xy && b->kp_octave && b->kp_uright && b->kp_desc), "null keypoint array");
+    ORB_CHECK_ARG(M == 0 || (b->mp_valid && b->mp_proj && b->mp_view_cos && b->mp_level && b->mp_desc &&
+                             b->mp_has_obs),
+                  "null map point array");
+    for (int j = 0; j < M; j++)
+        ORB_CHECK_ARG(!b->mp_valid[j] || (b->mp_level[j] >= 0 && b->mp_level[j] < b->n_levels),
+                      "trackScaleLevel out of range (scaleFactors[predictedScale], ORBmatcher.cc:328)");
+    ORB_HIP_TRY(hipSetDevice(device));
+    if (g_pj.device != device) {
+        g_pj.ws.release();
+        g_pj.io.release();
+        g_pj.device = device;
+    }
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += align_up(std::max<size_t>(bytes, 1), 256); return o; };
+    const size_t o_kb = take((size_t)(F + 1) * 4), o_xy = take((size_t)K * 8), o_oc = take((size_t)K * 4),
+                 o_ur = take((size_t)K * 4), o_kd = take((size_t)K * 32), o_kc = take(b->kp_claimed ? (size_t)K : 0),
+                 o_bd = take((size_t)F * 16), o_mb = take((size_t)(F + 1) * 4), o_mv = take((size_t)M),
+                 o_mp = take((size_t)M * 12), o_vc = take((size_t)M * 4), o_ml = take((size_t)M * 4),
+                 o_md = take((size_t)M * 32), o_mo = take((size_t)M), o_km = take((size_t)K * 4),
+                 o_nm = take((size_t)F * 4);
+    if ((rc = g_pj.io.reserve(off))) return rc;
+    if ((rc = g_pj.ws.reserve(pj_workspace_bytes(F, K, M)))) return rc;
+    char* d = g_pj.io.as<char>();
+    auto up = [&](size_t o, const void* src, size_t bytes) -> int {
+        if (bytes) ORB_HIP_TRY(hipMemcpy(d + o, src, bytes, hipMemcpyHostToDevice));
+        return ORB_OK;
+    };
+    if ((rc = up(o_kb, b->kp_begin, (size_t)(F + 1) * 4)) || (rc = up(o_xy, b->kp_xy, (size_t)K * 8)) ||
+        (rc = up(o_oc, b->kp_octave, (size_t)K * 4)) || (rc = up(o_ur, b->kp_uright, (size_t)K * 4)) ||
+        (rc = up(o_kd, b->kp_desc, (size_t)K * 32)) ||
+        (b->kp_claimed && (rc = up(o_kc, b->kp_claimed, (size_t)K))) || (rc = up(o_bd, b->bounds, (size_t)F * 16)) ||
+        (rc = up(o_mb, b->mp_begin, (size_t)(F + 1) * 4)) || (rc = up(o_mv, b->mp_valid, (size_t)M)) ||
+        (rc = up(o_mp, b->mp_proj, (size_t)M * 12)) || (rc = up(o_vc, b->mp_view_cos, (size_t)M * 4)) ||
+        (rc = up(o_ml, b->mp_level, (size_t)M * 4)) || (rc = up(o_md, b->mp_desc, (size_t)M * 32)) ||
+        (rc = up(o_mo, b->mp_has_obs, (size_t)M)))
+        return rc;
+    a.kp_begin = (const int32_t*)(d + o_kb); a.kp_xy = (const float*)(d + o_xy); a.kp_oct = (const int32_t*)(d + o_oc);
+    a.kp_ur = (const float*)(d + o_ur); a.kp_desc = (const uint8_t*)(d + o_kd);
+    a.kp_claimed = b->kp_claimed ? (const uint8_t*)(d + o_kc) : nullptr; a.bounds = (const float*)(d + o_bd);
+    a.mp_begin = (const int32_t*)(d + o_mb); a.mp_valid = (const uint8_t*)(d + o_mv);
+    a.mp_proj = (const float*)(d + o_mp); a.mp_vcos = (const float*)(d + o_vc); a.mp_level = (const int32_t*)(d + o_ml);
+    a.mp_desc = (const uint8_t*)(d + o_md); a.mp_has_obs = (const uint8_t*)(d + o_mo);
+    a.kp_match = (int32_t*)(d + o_km);
+    a.n_matches = (int32_t*)(d + o_nm);
+    pj_carve(a, g_pj.ws.as<char>(), F, K, M);
+    if ((rc = launch_projection(a, K, nullptr))) return rc;
+    if (K) ORB_HIP_TRY(hipMemcpy(kp_match, d + o_km, (size_t)K * 4, hipMemcpyDeviceToHost));
+    ORB_HIP_TRY(hipMemcpy(n_matches, d + o_nm, (size_t)F * 4, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}

@@ -132,3 +132,60 @@ def stereo_matches_batch_device(extractor_l, extractor_r, outs_l, outs_r, bf: fl
                                                  C.c_float(baseline), tptr(out[0]), tptr(out[1]), stream_ptr(stream)),
           "orbx_stereo_matches_batch_device")
     return out
+
+
+def _proj_struct(b: dict, conv, total_kp: int, total_mp: int):
+    """orbm_proj_batch from a make_proj_batch-style dict; `conv(array, dtype)` returns a pointer."""
+    from ._lib import ProjBatch
+    F = len(b["kp_begin"]) - 1
+    claimed = b.get("kp_claimed")
+    sf = np.ascontiguousarray(b["scale_factors"], np.float32)
+    return ProjBatch(F, total_kp, total_mp, conv(b["kp_begin"], np.int32),
+                     conv(b["kp_xy"], np.float32), conv(b["kp_octave"], np.int32), conv(b["kp_uright"], np.float32),
+                     conv(b["kp_desc"], np.uint8), conv(claimed, np.uint8) if claimed is not None else None,
+                     conv(b["bounds"], np.float32), conv(b["mp_begin"], np.int32), conv(b["mp_valid"], np.uint8),
+                     conv(b["mp_proj"], np.float32), conv(b["mp_view_cos"], np.float32), conv(b["mp_level"], np.int32),
+                     conv(b["mp_desc"], np.uint8), conv(b["mp_has_obs"], np.uint8), len(sf), ptr(sf),
+                     float(b["th"]), float(b["nnratio"])), sf
+
+
+def SearchByProjection(batch: dict, device: int = 0):
+    """int ORBmatcher::SearchByProjection(Frame& frame, const std::vector<MapPoint*>& mappoints, float th)
+    (include/ORBmatcher.h:58, src/ORBmatcher.cc:315-382) with the frame's FeaturesGrid, batched over frames.
+    Returns (kp_match, n_matches): kp_match[k] = frame-relative index of the map point assigned to
+    keypoint k by this call (frame.mappoints[bestIdx] = mappoint), -1 if none; n_matches per frame."""
+    keep = []
+
+    def conv(a, dt):
+        a = np.ascontiguousarray(a, dt)
+        keep.append(a)
+        return ptr(a)
+
+    pb, sf = _proj_struct(batch, conv, int(batch["kp_begin"][-1]), int(batch["mp_begin"][-1]))
+    kp_match = np.zeros(max(pb.total_kp, 1), np.int32)
+    n = np.zeros(max(pb.n_frames, 1), np.int32)
+    check(lib().orbm_search_by_projection(C.byref(pb), ptr(kp_match), ptr(n), device), "orbm_search_by_projection")
+    return kp_match[:pb.total_kp], n[:pb.n_frames]
+
+
+def search_by_projection_device(batch: dict, kp_match=None, n_matches=None, stream=None):
+    """Device form: array values of `batch` are torch tensors on the GPU (scale_factors / th / nnratio
+    stay host values); one enqueue of the grid, score and walk kernels on `stream`."""
+    import torch
+    from ._lib import stream_ptr, tptr
+    eb = batch["kp_begin"]
+    F = eb.numel() - 1
+    K = int(batch["kp_xy"].shape[0])
+    dev = eb.device
+    if kp_match is None:
+        kp_match = torch.empty(max(K, 1), dtype=torch.int32, device=dev)
+    if n_matches is None:
+        n_matches = torch.empty(max(F, 1), dtype=torch.int32, device=dev)
+
+    def conv(t, dt):
+        return tptr(t)
+
+    pb, sf = _proj_struct(batch, conv, K, int(batch["mp_proj"].shape[0]))
+    check(lib().orbm_search_by_projection_device(C.byref(pb), tptr(kp_match), tptr(n_matches), stream_ptr(stream)),
+          "orbm_search_by_projection_device")
+    return kp_match, n_matches

@@ -203,3 +203,109 @@ def make_pose_batch(seed: int = 0, n_frames: int = 8, n_edges=600, stereo_frac: 
                 cam=np.tile(camv, (n_frames, 1)), xw=cat(xw, 3), obs=cat(obs, 3),
                 inv_sigma2=np.concatenate(info) if sum(counts) else np.zeros(0),
                 gt_R=np.array(gt_R).reshape(n_frames, 9), gt_t=np.array(gt_t).reshape(n_frames, 3))
+
+
+ORB_QUOTA_2000 = (434, 362, 302, 251, 209, 175, 145, 122)
+
+
+def make_proj_batch(seed: int = 0, n_frames: int = 4, n_kp=2000, n_mp=1500, width: float = 1241.0,
+                    height: float = 376.0, th: float = 1.0, nnratio: float = 0.8, dup_frac: float = 0.15,
+                    odd_bounds: bool = False):
+    """C6: SearchByProjection(Frame, local map points) inputs in the orbm_proj_batch layout (§8f row 2).
+
+    Per frame: n_kp keypoints uniform over the image with octaves drawn by the 2000-feature
+    quotas, random descriptors, 40 % stereo (ur = x - U(5, 60)), 5 % already claimed.  Map points:
+    70 % are re-observations of a keypoint (projection = keypoint + N(0, 1.5 * 1.2^oct) px,
+    descriptor = the keypoint's with U{0..60} bits flipped, trackScaleLevel = octave or octave+1),
+    `dup_frac` of those reuse an already used keypoint (claim conflicts) and some carry an exact copy
+    of another candidate's descriptor (distance ties); the rest are random.  90 % trackInView,
+    95 % with observations, viewCos U(0.5, 1) with a third above 0.998.  Bounds are (0, W, 0, H) or
+    fractional undistortion-like bounds when `odd_bounds`.  n_kp / n_mp: int or per-frame list.
+    """
+    rng = np.random.default_rng(seed)
+    kps = [int(n_kp)] * n_frames if np.isscalar(n_kp) else [int(v) for v in n_kp]
+    mps = [int(n_mp)] * n_frames if np.isscalar(n_mp) else [int(v) for v in n_mp]
+    q = np.array(ORB_QUOTA_2000, float)
+    q /= q.sum()
+    scale = (1.2 ** np.arange(8)).astype(np.float32)
+    F = dict(kp_xy=[], kp_octave=[], kp_uright=[], kp_desc=[], kp_claimed=[], bounds=[], mp_valid=[], mp_proj=[],
+             mp_view_cos=[], mp_level=[], mp_desc=[], mp_has_obs=[])
+    for f in range(n_frames):
+        n, m = kps[f], mps[f]
+        if odd_bounds:
+            b = np.array([rng.uniform(-8, 2), width + rng.uniform(-2, 8), rng.uniform(-6, 2), height + rng.uniform(-2, 6)])
+        else:
+            b = np.array([0.0, width, 0.0, height])
+        x = rng.uniform(b[0] - 4, b[1] + 4, n)   # a few fall outside the grid (undistorted points)
+        y = rng.uniform(b[2] - 4, b[3] + 4, n)
+        octv = rng.choice(8, size=n, p=q)
+        desc = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        st = rng.random(n) < 0.4
+        ur = np.where(st, x - rng.uniform(5, 60, n), -1.0)
+        claimed = (rng.random(n) < 0.05).astype(np.uint8)
+        F["kp_xy"].append(np.stack([x, y], 1).astype(np.float32))
+        F["kp_octave"].append(octv.astype(np.int32))
+        F["kp_uright"].append(ur.astype(np.float32))
+        F["kp_desc"].append(desc)
+        F["kp_claimed"].append(claimed)
+        F["bounds"].append(b.astype(np.float32))
+        proj = np.zeros((m, 3))
+        lvl = np.zeros(m, np.int32)
+        mdesc = rng.integers(0, 256, size=(m, 32), dtype=np.uint8)
+        used = []
+        for j in range(m):
+            if n > 0 and rng.random() < 0.7:
+                i = int(rng.choice(used)) if used and rng.random() < dup_frac else int(rng.integers(0, n))
+                used.append(i)
+                s = 1.5 * scale[octv[i]]
+                u, v = x[i] + rng.normal(0, s), y[i] + rng.normal(0, s)
+                d = desc[i].copy()
+                if rng.random() < 0.1:
+                    # an exact copy of a random keypoint's descriptor: ties with the true match
+                    d = desc[int(rng.integers(0, n))].copy()
+                flips = rng.choice(256, size=int(rng.integers(0, 61)), replace=False)
+                for bit in flips:
+                    d[bit >> 3] ^= np.uint8(1 << (bit & 7))
+                mdesc[j] = d
+                lvl[j] = min(int(octv[i]) + int(rng.integers(0, 2)), 7)
+                uR = (u - (x[i] - ur[i]) + rng.normal(0, 1.0)) if st[i] else u - rng.uniform(5, 60)
+                if rng.random() < 0.1:
+                    uR += rng.uniform(-30, 30)
+                proj[j] = (u, v, uR)
+            else:
+                proj[j] = (rng.uniform(b[0], b[1]), rng.uniform(b[2], b[3]), 0.0)
+                proj[j, 2] = proj[j, 0] - rng.uniform(5, 60)
+                lvl[j] = int(rng.integers(0, 8))
+        F["mp_valid"].append((rng.random(m) < 0.9).astype(np.uint8))
+        F["mp_proj"].append(proj.astype(np.float32))
+        vc = rng.uniform(0.5, 1.0, m)
+        vc = np.where(rng.random(m) < 0.33, rng.uniform(0.9975, 1.0, m), vc)
+        F["mp_view_cos"].append(vc.astype(np.float32))
+        F["mp_level"].append(lvl)
+        F["mp_desc"].append(mdesc)
+        F["mp_has_obs"].append((rng.random(m) < 0.95).astype(np.uint8))
+    out = {}
+    for k, v in F.items():
+        out[k] = np.concatenate(v) if k != "bounds" else np.stack(v)
+    out["kp_begin"] = np.concatenate([[0], np.cumsum(kps)]).astype(np.int32)
+    out["mp_begin"] = np.concatenate([[0], np.cumsum(mps)]).astype(np.int32)
+    out["scale_factors"] = scale
+    out["th"] = float(th)
+    out["nnratio"] = float(nnratio)
+    return out
+
+
+def tile_proj_batch(b: dict, reps: int) -> dict:
+    """`reps` copies of a make_proj_batch batch back to back (a large batch without regenerating)."""
+    out = dict(b)
+    F = len(b["kp_begin"]) - 1
+    for k in ("kp_xy", "kp_octave", "kp_uright", "kp_desc", "kp_claimed", "mp_valid", "mp_proj", "mp_view_cos",
+              "mp_level", "mp_desc", "mp_has_obs"):
+        if b.get(k) is not None:
+            out[k] = np.concatenate([b[k]] * reps)
+    out["bounds"] = np.concatenate([b["bounds"]] * reps)
+    for k in ("kp_begin", "mp_begin"):
+        per = np.diff(b[k])
+        out[k] = np.concatenate([[0], np.cumsum(np.tile(per, reps))]).astype(np.int32)
+    assert len(out["kp_begin"]) == F * reps + 1
+    return out

@@ -215,6 +215,59 @@ def local_ba(prob, stop=None):
     return out
 
 
+class ProjBatch(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("total_kp", C.c_int32), ("total_mp", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_uright", C.c_void_p),
+                ("kp_desc", C.c_void_p), ("kp_claimed", C.c_void_p), ("bounds", C.c_void_p),
+                ("mp_begin", C.c_void_p), ("mp_valid", C.c_void_p), ("mp_proj", C.c_void_p),
+                ("mp_view_cos", C.c_void_p), ("mp_level", C.c_void_p), ("mp_desc", C.c_void_p),
+                ("mp_has_obs", C.c_void_p), ("n_levels", C.c_int32), ("scale_factors", C.c_void_p),
+                ("th", C.c_float), ("nnratio", C.c_float)]
+
+
+def proj_batch(keep, b):
+    F = len(b["kp_begin"]) - 1
+    claimed = b.get("kp_claimed")
+    return ProjBatch(F, int(b["kp_begin"][-1]), int(b["mp_begin"][-1]), keep(b["kp_begin"], np.int32),
+                     keep(b["kp_xy"], np.float32), keep(b["kp_octave"], np.int32), keep(b["kp_uright"], np.float32),
+                     keep(b["kp_desc"], np.uint8), keep(claimed, np.uint8) if claimed is not None else None,
+                     keep(b["bounds"], np.float32), keep(b["mp_begin"], np.int32), keep(b["mp_valid"], np.uint8),
+                     keep(b["mp_proj"], np.float32), keep(b["mp_view_cos"], np.float32), keep(b["mp_level"], np.int32),
+                     keep(b["mp_desc"], np.uint8), keep(b["mp_has_obs"], np.uint8), len(b["scale_factors"]),
+                     keep(b["scale_factors"], np.float32), float(b["th"]), float(b["nnratio"]))
+
+
+def search_by_projection(b):
+    """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) per frame (ORBmatcher.cc:315-382)."""
+    keep = _Keep()
+    pb = proj_batch(keep, b)
+    kp_match = np.zeros(pb.total_kp, np.int32)
+    n = np.zeros(pb.n_frames, np.int32)
+    lib().oracle_search_by_projection(C.byref(pb), ptr(kp_match), ptr(n))
+    return kp_match, n
+
+
+def features_grid(xy, octave, bounds):
+    """FeaturesGrid::AssignFeatures (Frame.cc:71-100) as CSR (cell = cx * 48 + cy)."""
+    xy = np.ascontiguousarray(xy, np.float32)
+    octave = np.ascontiguousarray(octave, np.int32)
+    bounds = np.ascontiguousarray(bounds, np.float32)
+    cs = np.zeros(64 * 48 + 1, np.int32)
+    idx = np.zeros(max(len(xy), 1), np.int32)
+    k = lib().oracle_features_grid(ptr(xy), ptr(octave), len(xy), ptr(bounds), ptr(cs), ptr(idx))
+    return cs, idx[:k]
+
+
+def features_in_area(xy, octave, bounds, nlevels, x, y, r, min_level=-1, max_level=-1):
+    xy = np.ascontiguousarray(xy, np.float32)
+    octave = np.ascontiguousarray(octave, np.int32)
+    bounds = np.ascontiguousarray(bounds, np.float32)
+    out = np.zeros(max(len(xy), 1), np.int32)
+    n = lib().oracle_features_in_area(ptr(xy), ptr(octave), len(xy), ptr(bounds), nlevels, C.c_float(x), C.c_float(y),
+                                      C.c_float(r), min_level, max_level, ptr(out), len(out))
+    return out[:n]
+
+
 class PoseBatch(C.Structure):
     _fields_ = [("n_frames", C.c_int32), ("edge_begin", C.c_void_p), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
                 ("cam", C.c_void_p), ("xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
