@@ -229,6 +229,50 @@ int orbm_search_by_projection_device(const orbm_proj_batch* b, int32_t* kp_match
                                      void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Bag of words.  Replaces DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> as ORBVocabulary
+ * (include/ORBVocabulary.h) for Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:208-214,
+ * src/KeyFrame.cc:66-74): loadFromTextFile (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1341-1431)
+ * and transform(features, BowVector&, FeatureVector&, levelsup) (:1130-1196, descent :1221-1263).
+ * BowVector = std::map<WordId, double> and FeatureVector = std::map<NodeId, vector<unsigned>>
+ * (BowVector.h, FeatureVector.h) are returned as ascending arrays / CSR — the FeatureVector CSR is
+ * exactly orbm_tri_frame's node_id / node_off / indices.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct orbv_vocabulary orbv_vocabulary;
+#define ORBV_MAX_FEATURES 4096   /* descriptors per transform (2 x nfeatures of the initial extractor) */
+
+/* Text format of saveToTextFile (:1434-1450): "k L scoring weighting", then one line per node
+ * 1..N-1 in id order: "parent isLeaf d0 .. d31 weight".  Trailing empty lines are ignored (the
+ * reference's eof loop turns a final newline into an extra root child with an uninitialised
+ * descriptor and weight 0). */
+int orbv_load_text(const char* path, int device, orbv_vocabulary** out);
+/* The same content from arrays: node i (1 <= i < n_nodes) has parent[i], is_leaf[i], desc[32 i ..],
+ * weight[i]; entries for i = 0 (the root) are ignored. */
+int orbv_create(int k, int L, int scoring, int weighting, int n_nodes, const int32_t* parent,
+                const uint8_t* is_leaf, const uint8_t* desc, const double* weight, int device,
+                orbv_vocabulary** out);
+int orbv_destroy(orbv_vocabulary* v);
+int orbv_info(const orbv_vocabulary* v, int* k, int* L, int* n_nodes, int* n_words, int* scoring,
+              int* weighting);
+
+/* transform(features, BowVector&, FeatureVector&, levelsup) for one descriptor set, host memory.
+ * bow_word / bow_weight: capacity n each, *n_words entries, word ids ascending.  fv_node: capacity
+ * n, fv_off: n + 1, fv_idx: n; *n_nodes node ids ascending, node t owns fv_idx[fv_off[t] ..
+ * fv_off[t+1]) (feature indices ascending).  Stopped words (weight 0) are in neither vector.
+ * Where the reference's node id is undefined (a leaf shallower than L - levelsup) the leaf's id
+ * is used. */
+int orbv_transform(orbv_vocabulary* v, const uint8_t* desc, int n, int levelsup, uint32_t* bow_word,
+                   double* bow_weight, int* n_words, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_idx,
+                   int* n_nodes);
+/* Batched device form over n_frames descriptor sets (frame f: d_desc + f*cap*32, d_counts[f] rows,
+ * cap <= ORBV_MAX_FEATURES) — e.g. an orbx_extract_batch_device output.  Per frame f the outputs
+ * use slot f: d_bow_word / d_bow_weight / d_fv_node / d_fv_idx at f*cap, d_fv_off at f*(cap+1),
+ * d_n_words[f], d_n_nodes[f].  Enqueue only on `stream`. */
+int orbv_transform_batch_device(orbv_vocabulary* v, const uint8_t* d_desc, const int32_t* d_counts, int cap,
+                                int n_frames, int levelsup, uint32_t* d_bow_word, double* d_bow_weight,
+                                int32_t* d_n_words, uint32_t* d_fv_node, int32_t* d_fv_off, int32_t* d_fv_idx,
+                                int32_t* d_n_nodes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Local bundle adjustment.  Replaces Optimizer::LocalBundleAdjustment (include/Optimizer.h:47,
  * src/Optimizer.cc:491-736) from the vertex/edge setup (:540-631) onwards: the caller
  * gathers local / fixed keyframes and map points and flattens them in reference order.

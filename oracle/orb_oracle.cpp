@@ -26,6 +26,8 @@
  *                  :54-120, core/robust_kernel_impl.cpp:65-91, types/types_six_dof_expmap.{h,cpp},
  *                  types/se3quat.h, types/types_sba.h — Eigen replaced by explicit fp64 code,
  *                  SimplicialLDLT by a dense LDLT of the reduced camera system.
+ *   DBoW2          Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1130-1263 (transform), :1341-1431
+ *                  (loadFromTextFile), BowVector.cpp:34-84, FeatureVector.cpp:31-45, FORB.cpp:80-134.
  *   Grid/Project   src/Frame.cc:32-34,71-145 (FeaturesGrid), src/ORBmatcher.cc:53,315-382
  *                  (SearchByProjection(Frame&, const std::vector<MapPoint*>&, float)).
  *   PoseOpt        src/Optimizer.cc:345-489 (4 x optimize(10) with chi2 classification) over
@@ -54,7 +56,11 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <fstream>
 #include <list>
+#include <map>
+#include <sstream>
+#include <string>
 #include <vector>
 
 #include "orbslam2_amd.h"
@@ -1109,6 +1115,150 @@ struct FeaturesGrid {
 };
 
 // ---------------------------------------------------------------------------------------------
+// DBoW2 TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h, BowVector.cpp,
+// FeatureVector.cpp, FORB.cpp, ScoringObject.h)
+// ---------------------------------------------------------------------------------------------
+struct Vocabulary {
+    struct Node {   // :300-331
+        uint32_t id = 0;
+        double weight = 0;
+        std::vector<uint32_t> children;
+        uint32_t parent = 0;
+        uint8_t desc[32] = {0};
+        uint32_t word_id = 0;
+        bool isLeaf() const { return children.empty(); }
+    };
+    int k = 0, L = 0, scoring = 0, weighting = 0;
+    std::vector<Node> nodes;
+    std::vector<uint32_t> words;
+
+    // loadFromTextFile (:1341-1431); a blank line (the reference's trailing-newline artefact) is skipped
+    bool load_text(const char* path) {
+        std::ifstream f(path);
+        if (!f.is_open() || f.eof()) return false;
+        words.clear();
+        nodes.clear();
+        std::string s;
+        std::getline(f, s);
+        std::stringstream ss;
+        ss << s;
+        int n1 = -1, n2 = -1;
+        ss >> k >> L >> n1 >> n2;
+        if (k < 0 || k > 20 || L < 1 || L > 10 || n1 < 0 || n1 > 5 || n2 < 0 || n2 > 3) return false;
+        scoring = n1;
+        weighting = n2;
+        nodes.resize(1);
+        nodes[0].id = 0;
+        while (!f.eof()) {
+            std::string snode;
+            std::getline(f, snode);
+            if (snode.find_first_not_of(" \t\r") == std::string::npos) continue;
+            std::stringstream ssnode;
+            ssnode << snode;
+            const uint32_t nid = (uint32_t)nodes.size();
+            nodes.resize(nodes.size() + 1);
+            nodes[nid].id = nid;
+            int pid = 0;
+            ssnode >> pid;
+            nodes[nid].parent = (uint32_t)pid;
+            nodes[pid].children.push_back(nid);
+            int nIsLeaf = 0;
+            ssnode >> nIsLeaf;
+            for (int i = 0; i < 32; i++) {   // FORB::fromString (FORB.cpp:119-134)
+                int n = 0;
+                ssnode >> n;
+                nodes[nid].desc[i] = (unsigned char)n;
+            }
+            ssnode >> nodes[nid].weight;
+            if (nIsLeaf > 0) {
+                nodes[nid].word_id = (uint32_t)words.size();
+                words.push_back(nid);
+            }
+        }
+        return true;
+    }
+    void from_arrays(int k_, int L_, int sc, int wt, int n, const int32_t* parent, const uint8_t* is_leaf,
+                     const uint8_t* desc, const double* weight) {
+        k = k_; L = L_; scoring = sc; weighting = wt;
+        nodes.assign(1, Node());
+        words.clear();
+        for (int i = 1; i < n; i++) {
+            Node nd;
+            nd.id = (uint32_t)i;
+            nd.parent = (uint32_t)parent[i];
+            std::memcpy(nd.desc, desc + 32 * (size_t)i, 32);
+            nd.weight = weight[i];
+            nodes.push_back(nd);
+            nodes[parent[i]].children.push_back((uint32_t)i);
+            if (is_leaf[i]) {
+                nodes[i].word_id = (uint32_t)words.size();
+                words.push_back((uint32_t)i);
+            }
+        }
+    }
+    // transform(feature, word_id, weight, nid, levelsup) (:1221-1263); FORB::distance = Hamming
+    void transform1(const uint8_t* feature, uint32_t& word_id, double& weight, uint32_t* nid, int levelsup) const {
+        const int nid_level = L - levelsup;
+        bool nid_set = false;
+        if (nid_level <= 0 && nid != nullptr) { *nid = 0; nid_set = true; }
+        uint32_t final_id = 0;
+        int current_level = 0;
+        do {
+            ++current_level;
+            const std::vector<uint32_t>& ch = nodes[final_id].children;
+            final_id = ch[0];
+            double best_d = hamming(feature, nodes[final_id].desc);
+            for (size_t c = 1; c < ch.size(); c++) {
+                const double d = hamming(feature, nodes[ch[c]].desc);
+                if (d < best_d) { best_d = d; final_id = ch[c]; }
+            }
+            if (nid != nullptr && current_level == nid_level) { *nid = final_id; nid_set = true; }
+        } while (!nodes[final_id].isLeaf());
+        if (nid != nullptr && !nid_set) *nid = final_id;   // undefined in the reference
+        word_id = nodes[final_id].word_id;
+        weight = nodes[final_id].weight;
+    }
+    // transform(features, BowVector&, FeatureVector&, levelsup) (:1130-1196)
+    void transform(const uint8_t* desc, int n, int levelsup, std::map<uint32_t, double>& v,
+                   std::map<uint32_t, std::vector<uint32_t>>& fv) const {
+        v.clear();
+        fv.clear();
+        if (words.empty()) return;
+        const bool must = scoring != 5;          // DotProductScoring: false (ScoringObject.h:74-89)
+        const bool l2 = scoring == 1;            // L2Scoring: L2, the others L1
+        for (int i = 0; i < n; i++) {
+            uint32_t id, nid;
+            double w;
+            transform1(desc + 32 * (size_t)i, id, w, &nid, levelsup);
+            if (w > 0) {
+                if (weighting == 0 || weighting == 1) {   // TF_IDF, TF: addWeight (BowVector.cpp:34-46)
+                    auto it = v.lower_bound(id);
+                    if (it != v.end() && !(id < it->first)) it->second += w;
+                    else v.insert(it, std::make_pair(id, w));
+                } else {                                    // IDF, BINARY: addIfNotExist (:50-58)
+                    auto it = v.lower_bound(id);
+                    if (it == v.end() || id < it->first) v.insert(it, std::make_pair(id, w));
+                }
+                fv[nid].push_back((uint32_t)i);             // FeatureVector::addFeature (:31-45)
+            }
+        }
+        if ((weighting == 0 || weighting == 1) && !v.empty() && !must) {
+            const double nd = (double)v.size();
+            for (auto& e : v) e.second /= nd;
+        }
+        if (must) {   // BowVector::normalize (:62-84)
+            double norm = 0.0;
+            if (!l2) for (auto& e : v) norm += std::fabs(e.second);
+            else {
+                for (auto& e : v) norm += e.second * e.second;
+                norm = std::sqrt(norm);
+            }
+            if (norm > 0.0) for (auto& e : v) e.second /= norm;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
 // PoseOptimization: one SE3 vertex, unary edges (types_six_dof_expmap.h:143-202,
 // types_six_dof_expmap.cpp:266-364), LinearSolverDense under OptimizationAlgorithmLevenberg.
 // ---------------------------------------------------------------------------------------------
@@ -1588,6 +1738,51 @@ int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile i
         }
     }
     std::memcpy(res->points, ba.X.data(), sizeof(double) * 3 * ba.N);
+    return 0;
+}
+
+void* oracle_voc_load_text(const char* path) {
+    std::unique_ptr<Vocabulary> v(new Vocabulary);
+    if (!v->load_text(path)) return nullptr;
+    return v.release();
+}
+void* oracle_voc_create(int k, int L, int scoring, int weighting, int n, const int32_t* parent, const uint8_t* is_leaf,
+                        const uint8_t* desc, const double* weight) {
+    Vocabulary* v = new Vocabulary;
+    v->from_arrays(k, L, scoring, weighting, n, parent, is_leaf, desc, weight);
+    return v;
+}
+void oracle_voc_destroy(void* h) { delete static_cast<Vocabulary*>(h); }
+int oracle_voc_info(void* h, int32_t* out6) {
+    const Vocabulary* v = static_cast<Vocabulary*>(h);
+    out6[0] = v->k; out6[1] = v->L; out6[2] = (int32_t)v->nodes.size(); out6[3] = (int32_t)v->words.size();
+    out6[4] = v->scoring; out6[5] = v->weighting;
+    return 0;
+}
+// Per-feature word id / weight / node id (transform(feature, id, w, &nid, levelsup)).
+void oracle_voc_words(void* h, const uint8_t* desc, int n, int levelsup, uint32_t* word, double* weight, uint32_t* nid) {
+    const Vocabulary* v = static_cast<Vocabulary*>(h);
+    for (int i = 0; i < n; i++) v->transform1(desc + 32 * (size_t)i, word[i], weight[i], &nid[i], levelsup);
+}
+int oracle_voc_transform(void* h, const uint8_t* desc, int n, int levelsup, uint32_t* bow_word, double* bow_weight,
+                         int32_t* n_words, uint32_t* fv_node, int32_t* fv_off, int32_t* fv_idx, int32_t* n_nodes) {
+    const Vocabulary* v = static_cast<Vocabulary*>(h);
+    std::map<uint32_t, double> bv;
+    std::map<uint32_t, std::vector<uint32_t>> fv;
+    v->transform(desc, n, levelsup, bv, fv);
+    int t = 0;
+    for (auto& e : bv) { bow_word[t] = e.first; bow_weight[t] = e.second; t++; }
+    *n_words = t;
+    t = 0;
+    int o = 0;
+    for (auto& e : fv) {
+        fv_node[t] = e.first;
+        fv_off[t] = o;
+        for (uint32_t i : e.second) fv_idx[o++] = (int32_t)i;
+        t++;
+    }
+    fv_off[t] = o;
+    *n_nodes = t;
     return 0;
 }
 

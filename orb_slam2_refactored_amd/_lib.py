@@ -94,6 +94,14 @@ SIGNATURES = {
                                                    C.c_float, VP, VP, VP]),
     "orbm_search_by_projection": (C.c_int, [C.POINTER(ProjBatch), VP, VP, C.c_int]),
     "orbm_search_by_projection_device": (C.c_int, [C.POINTER(ProjBatch), VP, VP, VP]),
+    "orbv_load_text": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(VP)]),
+    "orbv_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, VP, VP, VP, C.c_int, C.POINTER(VP)]),
+    "orbv_destroy": (C.c_int, [VP]),
+    "orbv_info": (C.c_int, [VP, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                            C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "orbv_transform": (C.c_int, [VP, VP, C.c_int, C.c_int, VP, VP, C.POINTER(C.c_int), VP, VP, VP,
+                                 C.POINTER(C.c_int)]),
+    "orbv_transform_batch_device": (C.c_int, [VP, VP, VP, C.c_int, C.c_int, C.c_int, VP, VP, VP, VP, VP, VP, VP, VP]),
     "orbba_local_ba": (C.c_int, [C.POINTER(BAProblem), C.POINTER(BAResult), VP, C.c_int]),
     "orbba_pose_optimization": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), C.c_int]),
     "orbba_pose_optimization_device": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), VP]),

@@ -309,3 +309,82 @@ def tile_proj_batch(b: dict, reps: int) -> dict:
         out[k] = np.concatenate([[0], np.cumsum(np.tile(per, reps))]).astype(np.int32)
     assert len(out["kp_begin"]) == F * reps + 1
     return out
+
+
+def make_vocabulary(seed: int = 0, k: int = 10, L: int = 4, scoring: int = 0, weighting: int = 0,
+                    early_leaf: float = 0.05, stop_frac: float = 0.03, order: str = "bfs"):
+    """A synthetic DBoW2 ORB vocabulary (the real ORBvoc.txt is not available offline).
+
+    A k-ary tree of depth L: children descriptors are the parent's with U{16..48} bits flipped (root
+    children random), so descriptor distance follows the tree.  `early_leaf` of the internal nodes
+    below level 2 stop early (leaves above level L, as k-means trees have), leaves get idf-like
+    weights U(0.5, 8) and `stop_frac` of them weight 0 (stopped words); internal nodes weight 0.
+    Nodes are numbered in `order` ("bfs" or "dfs"; the text format only needs parents first).
+    Returns dict(k, L, scoring, weighting, parent, is_leaf, desc, weight) with node 0 = root."""
+    rng = np.random.default_rng(seed)
+    parent, is_leaf, desc, weight, depth = [0], [0], [np.zeros(32, np.uint8)], [0.0], [0]
+
+    def new_node(p, d):
+        i = len(parent)
+        parent.append(p)
+        depth.append(d)
+        if p == 0:
+            desc.append(rng.integers(0, 256, 32, dtype=np.uint8))
+        else:
+            x = desc[p].copy()
+            for bit in rng.choice(256, size=int(rng.integers(16, 49)), replace=False):
+                x[bit >> 3] ^= np.uint8(1 << (bit & 7))
+            desc.append(x)
+        leaf = d == L or (d >= 2 and rng.random() < early_leaf)
+        is_leaf.append(1 if leaf else 0)
+        weight.append(0.0 if not leaf else (0.0 if rng.random() < stop_frac else float(rng.uniform(0.5, 8.0))))
+        return i
+
+    if order == "bfs":
+        frontier = [0]
+        while frontier:
+            nxt = []
+            for p in frontier:
+                if p != 0 and is_leaf[p]:
+                    continue
+                for _ in range(k):
+                    nxt.append(new_node(p, depth[p] + 1))
+            frontier = nxt
+    else:
+        def rec(p):
+            for _ in range(k):
+                c = new_node(p, depth[p] + 1)
+                if not is_leaf[c]:
+                    rec(c)
+        rec(0)
+    # text round trip precision: weights as the reference's ostream << double (6 significant digits)
+    w = np.array([float(f"{x:g}") for x in weight])
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=np.array(parent, np.int32),
+                is_leaf=np.array(is_leaf, np.uint8), desc=np.stack(desc).astype(np.uint8), weight=w)
+
+
+def write_vocabulary_text(voc: dict, path) -> None:
+    """saveToTextFile format (TemplatedVocabulary.h:1434-1450)."""
+    lines = [f"{voc['k']} {voc['L']}  {voc['scoring']} {voc['weighting']}"]
+    for i in range(1, len(voc["parent"])):
+        d = " ".join(str(int(b)) for b in voc["desc"][i])
+        lines.append(f"{voc['parent'][i]} {int(voc['is_leaf'][i])} {d}  {voc['weight'][i]:g}")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def vocabulary_features(voc: dict, seed: int, n: int, near: float = 0.8) -> np.ndarray:
+    """n descriptors: `near` of them a random leaf's descriptor with U{0..40} flips, the rest random,
+    some repeated (same word several times)."""
+    rng = np.random.default_rng(seed)
+    leaves = np.nonzero(voc["is_leaf"])[0]
+    out = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    for i in range(n):
+        if rng.random() < near and len(leaves):
+            x = voc["desc"][int(rng.choice(leaves))].copy()
+            for bit in rng.choice(256, size=int(rng.integers(0, 41)), replace=False):
+                x[bit >> 3] ^= np.uint8(1 << (bit & 7))
+            out[i] = x
+        if i > 0 and rng.random() < 0.05:
+            out[i] = out[int(rng.integers(0, i))]
+    return out

@@ -328,3 +328,49 @@ def compute_stereo_matches(kpsL, descL, pyrL, kpsR, descR, pyrR, scale, inv_scal
     lib().oracle_compute_stereo_matches(C.byref(vl), C.byref(vr), keep(scale, np.float32), keep(inv_scale, np.float32),
                                         C.c_float(bf), C.c_float(baseline), ptr(ur), ptr(dp))
     return ur, dp
+
+
+class Vocabulary:
+    """DBoW2 restatement handle (oracle/orb_oracle.cpp Vocabulary)."""
+
+    def __init__(self, voc=None, path=None):
+        L = lib()
+        L.oracle_voc_load_text.restype = C.c_void_p
+        L.oracle_voc_create.restype = C.c_void_p
+        L.oracle_voc_destroy.argtypes = [C.c_void_p]
+        if path is not None:
+            self.h = L.oracle_voc_load_text(str(path).encode())
+            assert self.h, "oracle failed to load the vocabulary"
+        else:
+            self._keep = [np.ascontiguousarray(voc["parent"], np.int32), np.ascontiguousarray(voc["is_leaf"], np.uint8),
+                          np.ascontiguousarray(voc["desc"], np.uint8), np.ascontiguousarray(voc["weight"], np.float64)]
+            self.h = L.oracle_voc_create(voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(voc["parent"]),
+                                         *[ptr(a) for a in self._keep])
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_voc_destroy(C.c_void_p(self.h))
+
+    def info(self):
+        o = np.zeros(6, np.int32)
+        lib().oracle_voc_info(C.c_void_p(self.h), ptr(o))
+        return dict(zip(("k", "L", "n_nodes", "n_words", "scoring", "weighting"), o.tolist()))
+
+    def words(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8)
+        n = len(d)
+        w, wt, nid = np.zeros(n, np.uint32), np.zeros(n), np.zeros(n, np.uint32)
+        lib().oracle_voc_words(C.c_void_p(self.h), ptr(d), n, levelsup, ptr(w), ptr(wt), ptr(nid))
+        return w, wt, nid
+
+    def transform(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8)
+        n = len(d)
+        cap = max(n, 1)
+        bw, bv = np.zeros(cap, np.uint32), np.zeros(cap)
+        fn, fo, fi = np.zeros(cap, np.uint32), np.zeros(cap + 1, np.int32), np.zeros(cap, np.int32)
+        nw, nn = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        lib().oracle_voc_transform(C.c_void_p(self.h), ptr(d), n, levelsup, ptr(bw), ptr(bv), ptr(nw), ptr(fn),
+                                   ptr(fo), ptr(fi), ptr(nn))
+        a, b = int(nw[0]), int(nn[0])
+        return (bw[:a], bv[:a]), (fn[:b], fo[:b + 1], fi[:fo[b]])
