@@ -207,6 +207,46 @@ def projection_leg(dev, frames=256, steps=10, cpu=True):
     return r
 
 
+def bow_leg(dev, local, frames=128, n=2000, steps=10, cpu=True):
+    """§8f row 4: Frame::ComputeBoW = ORBVocabulary::transform(desc, BowVector, FeatureVector, 4)
+    (TemplatedVocabulary.h:1130-1263) on an ORBvoc-shaped synthetic tree (k 10, L 6, 1.1 M nodes),
+    `frames` descriptor sets of `n` rows resident in HBM."""
+    import torch
+    from orb_slam2_refactored_amd.synth import make_full_vocabulary
+    from orb_slam2_refactored_amd.vocabulary import ORBVocabulary
+    v = make_full_vocabulary(31)
+    voc = ORBVocabulary.from_arrays(v["k"], v["L"], v["scoring"], v["weighting"], v["parent"], v["is_leaf"],
+                                    v["desc"], v["weight"], device=local)
+    rng = np.random.default_rng(32)
+    X = rng.integers(0, 256, size=(frames, n, 32), dtype=np.uint8)
+    desc = torch.from_numpy(X).to(dev)
+    counts = torch.full((frames,), n, dtype=torch.int32, device=dev)
+    out = voc.transform_batch_device(desc, counts)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        voc.transform_batch_device(desc, counts, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    r = {"workload": f"{frames} frames x {n} descriptors, vocabulary k 10 L 6 (1.11 M nodes), levelsup 4",
+         "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms,
+         "mean_words": float(out["n_words"].double().mean().item())}
+    if cpu:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_api as O
+        o = O.Vocabulary(v)
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 3.0 or k < 8:
+            o.transform(X[k % frames], 4)
+            k += 1
+        r["cpu_baseline"] = {"frames_per_s": k / (time.perf_counter() - t0), "cores": 1, "kind": "port",
+                             "sample": f"{n}-descriptor sets, oracle/orb_oracle.cpp, 1 thread"}
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,6 +261,7 @@ def main():
     ap.add_argument("--no-stereo", action="store_true")
     ap.add_argument("--no-pose", action="store_true")
     ap.add_argument("--no-projection", action="store_true")
+    ap.add_argument("--no-bow", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -371,6 +412,9 @@ def main():
 
     if rank == 0 and not args.no_projection:
         result["search_by_projection"] = projection_leg(dev, cpu=world == 1 and not args.no_cpu_baseline)
+
+    if rank == 0 and not args.no_bow:
+        result["bow"] = bow_leg(dev, local, cpu=world == 1 and not args.no_cpu_baseline)
 
     if rank == 0 and not args.no_pose:
         result["pose_opt"] = pose_leg(dev, cpu=world == 1 and not args.no_cpu_baseline)

@@ -6,6 +6,8 @@
 //   ORB_SLAM2_AMD::ORBmatcher     <- ORB_SLAM2::ORBmatcher Hamming kernels (include/ORBmatcher.h)
 //   ORB_SLAM2_AMD::LocalBundleAdjustment <- Optimizer::LocalBundleAdjustment (include/Optimizer.h:47)
 //   ORB_SLAM2_AMD::PoseOptimization      <- Optimizer::PoseOptimization (include/Optimizer.h:49)
+//   ORB_SLAM2_AMD::SearchByProjection    <- ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
+//   ORB_SLAM2_AMD::ORBVocabulary         <- DBoW2 ORBVocabulary (include/ORBVocabulary.h) transform
 // Plain-type overloads are always available; when OpenCV is on the include path the
 // cv::Mat / cv::KeyPoint overloads with the reference's exact signatures are added.
 // A non-zero C status is turned into an exception, as the reference's CV_Assert does.
@@ -14,6 +16,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <map>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -247,6 +250,88 @@ inline std::vector<int> PoseOptimization(std::vector<PoseFrame>& frames, int dev
     }
     return result;
 }
+
+// int ORBmatcher::SearchByProjection(Frame&, const std::vector<MapPoint*>&, float th)
+// (include/ORBmatcher.h:58, src/ORBmatcher.cc:315-382) with the frame's FeaturesGrid, for one
+// frame.  `keypointsUn` / `descriptors` / `uright` are the frame's, `claimed[i]` is
+// frame.mappoints[i] && ->Observations() > 0; per local map point the IsInFrustum fields
+// (Tracking.cc:554-605).  Returns the match count; kpMatch[i] = index into the map point arrays
+// assigned to keypoint i (frame.mappoints[i] = mappoints[kpMatch[i]]) or -1.
+struct ProjectionPoints {
+    std::vector<uint8_t> valid;      // trackInView && !isBad()
+    std::vector<float> proj;         // 3 per point: trackProjX, trackProjY, trackProjXR
+    std::vector<float> viewCos;      // trackViewCos
+    std::vector<int32_t> level;      // trackScaleLevel
+    std::vector<uint8_t> desc;       // 32 per point: GetDescriptor()
+    std::vector<uint8_t> hasObs;     // Observations() > 0
+};
+
+inline int SearchByProjection(const std::vector<orbx_keypoint>& keypointsUn, const uint8_t* descriptors,
+                              const std::vector<float>& uright, const std::vector<uint8_t>& claimed,
+                              const float bounds[4], const std::vector<float>& scaleFactors,
+                              const ProjectionPoints& mps, float th, float nnratio, std::vector<int32_t>& kpMatch,
+                              int device = 0) {
+    const int n = (int)keypointsUn.size(), m = (int)mps.valid.size();
+    std::vector<float> xy(2 * (size_t)n);
+    std::vector<int32_t> oct(n);
+    for (int i = 0; i < n; i++) { xy[2 * i] = keypointsUn[i].x; xy[2 * i + 1] = keypointsUn[i].y; oct[i] = keypointsUn[i].octave; }
+    const int32_t kb[2] = {0, n}, mb[2] = {0, m};
+    orbm_proj_batch b;
+    b.n_frames = 1; b.total_kp = n; b.total_mp = m;
+    b.kp_begin = kb; b.kp_xy = xy.data(); b.kp_octave = oct.data(); b.kp_uright = uright.data();
+    b.kp_desc = descriptors; b.kp_claimed = claimed.empty() ? nullptr : claimed.data(); b.bounds = bounds;
+    b.mp_begin = mb; b.mp_valid = mps.valid.data(); b.mp_proj = mps.proj.data(); b.mp_view_cos = mps.viewCos.data();
+    b.mp_level = mps.level.data(); b.mp_desc = mps.desc.data(); b.mp_has_obs = mps.hasObs.data();
+    b.n_levels = (int32_t)scaleFactors.size(); b.scale_factors = scaleFactors.data(); b.th = th; b.nnratio = nnratio;
+    kpMatch.assign(n, -1);
+    int32_t nm = 0;
+    check(orbm_search_by_projection(&b, kpMatch.data(), &nm, device), "orbm_search_by_projection");
+    return nm;
+}
+
+// DBoW2 ORBVocabulary: loadFromTextFile + transform(features, BowVector&, FeatureVector&, levelsup)
+// (TemplatedVocabulary.h:1130-1196, :1341-1431) with the reference's container types.
+class ORBVocabulary {
+public:
+    using BowVector = std::map<uint32_t, double>;
+    using FeatureVector = std::map<uint32_t, std::vector<unsigned int>>;
+
+    explicit ORBVocabulary(int device = 0) : device_(device) {}
+    ~ORBVocabulary() { orbv_destroy(h_); }
+    ORBVocabulary(const ORBVocabulary&) = delete;
+    ORBVocabulary& operator=(const ORBVocabulary&) = delete;
+
+    bool loadFromTextFile(const std::string& filename) {
+        orbv_destroy(h_);
+        h_ = nullptr;
+        return orbv_load_text(filename.c_str(), device_, &h_) == ORB_OK;
+    }
+    bool empty() const {
+        int nw = 0;
+        return !h_ || orbv_info(h_, nullptr, nullptr, nullptr, &nw, nullptr, nullptr) != ORB_OK || nw == 0;
+    }
+    // descriptors: n rows of 32 bytes (Converter::toDescriptorVector(descriptors))
+    void transform(const uint8_t* descriptors, int n, BowVector& v, FeatureVector& fv, int levelsup) const {
+        v.clear();
+        fv.clear();
+        if (!h_) return;
+        const size_t cap = (size_t)std::max(n, 1);
+        std::vector<uint32_t> bw(cap), fn(cap);
+        std::vector<double> bv(cap);
+        std::vector<int32_t> fo(cap + 1), fi(cap);
+        int nw = 0, nn = 0;
+        check(orbv_transform(h_, descriptors, n, levelsup, bw.data(), bv.data(), &nw, fn.data(), fo.data(), fi.data(),
+                             &nn),
+              "orbv_transform");
+        for (int i = 0; i < nw; i++) v.emplace_hint(v.end(), bw[i], bv[i]);
+        for (int t = 0; t < nn; t++)
+            fv.emplace_hint(fv.end(), fn[t], std::vector<unsigned int>(fi.begin() + fo[t], fi.begin() + fo[t + 1]));
+    }
+
+private:
+    int device_;
+    orbv_vocabulary* h_ = nullptr;
+};
 
 }  // namespace ORB_SLAM2_AMD
 

@@ -388,3 +388,32 @@ def vocabulary_features(voc: dict, seed: int, n: int, near: float = 0.8) -> np.n
         if i > 0 and rng.random() < 0.05:
             out[i] = out[int(rng.integers(0, i))]
     return out
+
+
+def make_full_vocabulary(seed: int = 0, k: int = 10, L: int = 6):
+    """A full k-ary depth-L tree built level by level (ORBvoc.txt's shape: k = 10, L = 6, ~1.1 M nodes),
+    BFS-numbered, children = parent with ~32 bits flipped, leaf weights U(0.5, 8), TF-IDF / L1."""
+    rng = np.random.default_rng(seed)
+    parents = [np.zeros(1, np.int64)]
+    descs = [np.zeros((1, 32), np.uint8)]
+    start = 0
+    for d in range(1, L + 1):
+        prev = descs[-1]
+        pids = np.repeat(np.arange(start, start + len(prev)), k)
+        base = np.repeat(prev, k, axis=0)
+        if d == 1:
+            base = rng.integers(0, 256, size=base.shape, dtype=np.uint8)
+        else:
+            flips = np.packbits(rng.integers(0, 256, size=(len(base), 256), dtype=np.uint8) < 32, axis=1)
+            base = base ^ flips
+        start += len(prev)
+        parents.append(pids)
+        descs.append(base)
+    parent = np.concatenate(parents).astype(np.int32)
+    desc = np.concatenate(descs)
+    n = len(parent)
+    is_leaf = np.zeros(n, np.uint8)
+    is_leaf[n - k ** L:] = 1
+    weight = np.zeros(n)
+    weight[n - k ** L:] = rng.uniform(0.5, 8.0, k ** L)
+    return dict(k=k, L=L, scoring=0, weighting=0, parent=parent, is_leaf=is_leaf, desc=desc, weight=weight)
