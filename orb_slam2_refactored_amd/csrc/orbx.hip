@@ -56,6 +56,7 @@ struct LevelDev {
     double hx;
     float scale, size;
     long long xtab_off, ytab_off;   // resize coefficient tables (l >= 1)
+    double ssx, ssy;                // (double)w[l-1] / w[l], (double)h[l-1] / h[l] (l >= 1)
 };
 
 struct Geom {
@@ -146,6 +147,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
 // One workgroup = a 64 x 16 tile of level l (256 threads, 4 output pixels each).  The source
 // rectangle of level l-1 it needs is staged in LDS with dword loads; coefficients come from the
 // per-level tables.
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));   // packed u16 pair
+
 constexpr int PYR_TW = 64, PYR_TH = 64;
 constexpr int PYR_SW = 144, PYR_SH = 128;   // LDS source tile capacity (scale factor <= ~1.9)
 
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
                                                             long long in_fstride, int in_step, uint8_t* pyr,
                                                             const int2* __restrict__ xtab,
                                                             const int2* __restrict__ ytab) {
-    __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW];
+    __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW + 16];   // +16: the 8-byte windows may read past the last row
     __shared__ int2 xs_t[PYR_TW], ys_t[PYR_TH];
     const LevelDev& L = g.lv[l];
     const LevelDev& Ls = g.lv[l - 1];
@@ -172,36 +175,36 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
     // conservative source rectangle from the scale (a superset of the tables' taps; no table
     // round trip before the image loads)
     const int sw = Ls.w, sh = Ls.h;
-    const double scx = (double)sw / L.w, scy = (double)sh / L.h;
+    const double scx = L.ssx, scy = L.ssy;
     const int sx_lo = max(0, (int)floor((tx0 + 0.5) * scx - 0.5) - 2);
     const int sx_hi = min(sw - 1, (int)floor((tx0 + tw - 0.5) * scx - 0.5) + 2);
     const int sy_lo = max(0, (int)floor((ty0 + 0.5) * scy - 0.5) - 2);
     const int sy_hi = min(sh - 1, (int)floor((ty0 + th - 0.5) * scy - 0.5) + 2);
     const int xa = sx_lo & ~3;
-    const int nd = (sx_hi - xa + 4) >> 2;   // dwords per source row
+    const int nd = (sx_hi - xa + 4) >> 2;   // dwords per source row (<= PYR_SW / 4 < 64)
     const int nr = sy_hi - sy_lo + 1;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)sstep) & 3) == 0;
     if (aligned) {
-        // flat (row, dword) walk; all of a thread's loads in flight before the LDS stores
-        constexpr int NL = (PYR_SW / 4) * PYR_SH / 256;
-        const int dr = 256 / nd, dm = 256 - dr * nd;
-        int r = threadIdx.x / nd, d = threadIdx.x - (threadIdx.x / nd) * nd;
-        uint32_t v[NL];
-        int rr[NL], dd[NL];
+        // wavefront w stages rows w, w + 4, ...; lane = dword of the row.  The row address is
+        // wave-uniform (SGPR base + a per-lane column offset), so a load costs no VALU; all of a
+        // lane's loads are issued before the LDS stores.
+        constexpr int RPW = PYR_SH / 4;
+        const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int ln = threadIdx.x & 63;
+        const int col = min(xa + 4 * ln, (sw - 1) & ~3);   // in-row dword (row stride >= align4(w))
+        const uint8_t* rbase = src + (long long)sy_lo * sstep + col;
+        uint32_t v[RPW];
 #pragma unroll
-        for (int k = 0; k < NL; k++) {
-            rr[k] = r;
-            dd[k] = d;
-            const int rc = min(r, nr - 1);
-            const int xd = min(xa + 4 * d, (sw - 1) & ~3);   // in-row dword (row stride >= align4(w))
-            v[k] = *reinterpret_cast<const uint32_t*>(src + (long long)(sy_lo + rc) * sstep + xd);
-            r += dr;
-            d += dm;
-            if (d >= nd) { d -= nd; r++; }
+        for (int k = 0; k < RPW; k++) {   // unconditional (row clamped): straight-line loads
+            const int rk = min(wv + 4 * k, nr - 1);
+            v[k] = *reinterpret_cast<const uint32_t*>(rbase + (long long)rk * sstep);
         }
+        if (ln < nd) {
+            uint32_t* drow = reinterpret_cast<uint32_t*>(S) + wv * (PYR_SW / 4) + ln;
 #pragma unroll
-        for (int k = 0; k < NL; k++)
-            if (rr[k] < nr) *reinterpret_cast<uint32_t*>(&S[rr[k] * PYR_SW + 4 * dd[k]]) = v[k];
+            for (int k = 0; k < RPW; k++)
+                if (wv + 4 * k < nr) drow[k * PYR_SW] = v[k];   // row wv + 4k: (wv + 4k) * PYR_SW / 4 dwords
+        }
     } else {   // unaligned caller image (level 0 with an odd base / step): byte loads
         for (int i = threadIdx.x; i < nd * nr; i += blockDim.x) {
             const int r = i / nd, d = i - r * nd;
@@ -214,7 +217,49 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
         }
     }
     __syncthreads();
-    // 16 threads per 64-px output row segment (4 px each), 16 rows per pass
+    {
+        // 32 threads per 64-px output row (2 px each), 8 rows per pass.  Both pixels' four taps lie
+        // in the 8 LDS bytes from dword wd (scale <= ~3), so one row costs two dword reads; v_perm
+        // packs a pixel's taps as u16 (S0, S1) and v_dot2_u32_u16 with the packed (a0, a1) gives
+        // S0*a0 + S1*a1 exactly.  (h >> 4 <= 32640 and the result <= 255: OpenCV's saturations
+        // cannot trigger for coefficients summing to 2048.)
+        const int p0 = (threadIdx.x & 31) * 2;
+        const int2 xv0 = xs_t[min(p0, tw - 1)], xv1 = xs_t[min(p0 + 1, tw - 1)];
+        const int s00 = (xv0.x & 0xffff) - xa, s01 = (xv0.x >> 16) - xa;
+        const int s10 = (xv1.x & 0xffff) - xa, s11 = (xv1.x >> 16) - xa;
+        const int wd = s00 >> 2;
+        const int e00 = s00 - 4 * wd, e01 = s01 - 4 * wd, e10 = s10 - 4 * wd, e11 = s11 - 4 * wd;
+        const bool fits = max(e01, e11) <= 7 && min(e00, e10) >= 0;
+        if (!__syncthreads_or(!fits)) {   // block-uniform: every thread's taps fit its 8-byte window
+            if (p0 >= tw) return;
+            const uint32_t sel0 = (uint32_t)e00 | 0x0c00u | ((uint32_t)e01 << 16) | 0x0c000000u;
+            const uint32_t sel1 = (uint32_t)e10 | 0x0c00u | ((uint32_t)e11 << 16) | 0x0c000000u;
+            const us2 a0 = *reinterpret_cast<const us2*>(&xv0.y), a1 = *reinterpret_cast<const us2*>(&xv1.y);
+            const uint32_t* S32 = reinterpret_cast<const uint32_t*>(S) + wd;
+            uint8_t* dcol = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + p0;
+            for (int ty = threadIdx.x >> 5; ty < th; ty += 8) {
+                const int2 yv = ys_t[ty];
+                const int r0 = ((yv.x & 0xffff) - sy_lo) * (PYR_SW / 4), r1 = ((yv.x >> 16) - sy_lo) * (PYR_SW / 4);
+                const uint32_t b0 = (uint32_t)(yv.y & 0xffff), b1 = (uint32_t)(yv.y >> 16);
+                const uint32_t w00 = S32[r0], w01 = S32[r0 + 1], w10 = S32[r1], w11 = S32[r1 + 1];
+                auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
+                    const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
+                    return *reinterpret_cast<const us2*>(&r);
+                };
+                const uint32_t h0a = __builtin_amdgcn_udot2(tap(w01, w00, sel0), a0, 0u, false) >> 4;
+                const uint32_t h1a = __builtin_amdgcn_udot2(tap(w11, w10, sel0), a0, 0u, false) >> 4;
+                const uint32_t h0b = __builtin_amdgcn_udot2(tap(w01, w00, sel1), a1, 0u, false) >> 4;
+                const uint32_t h1b = __builtin_amdgcn_udot2(tap(w11, w10, sel1), a1, 0u, false) >> 4;
+                const uint32_t va = (((h0a * b0) >> 16) + ((h1a * b1) >> 16) + 2) >> 2;
+                const uint32_t vb = (((h0b * b0) >> 16) + ((h1b * b1) >> 16) + 2) >> 2;
+                uint8_t* dst = dcol + (long long)(ty0 + ty) * L.stride;
+                if (p0 + 1 < tw) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(va | (vb << 8));   // tx0 + p0 even
+                else dst[0] = (uint8_t)va;
+            }
+            return;
+        }
+    }
+    // generic path: 16 threads per 64-px output row segment (4 px each), 16 rows per pass
     const int q0 = (threadIdx.x & 15) * 4;
     if (q0 >= tw) return;
     int sxo[4], a0v[4], a1v[4], sxo1[4];
@@ -308,8 +353,6 @@ __device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t, int cs) {
 // circle-adjacent compass points (positions 0/4/8/12) both brighter than v+t, or both darker than
 // v-t.  With packed u16 lanes: bright <=> max over the 4 adjacent pairs of min(pa, pb) > v + t,
 // dark <=> min over the pairs of max(pa, pb) < v - t (no clamping needed: p <= 255).
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-
 __device__ __forceinline__ us2 lo_pair(uint32_t w) {   // bytes 0,1 -> u16 lanes
     const uint32_t r = __builtin_amdgcn_perm(0u, w, 0x0c010c00u);
     return *reinterpret_cast<const us2*>(&r);
@@ -1524,6 +1567,8 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
             const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
             L.xtab_off = (long long)xtab.size();
             L.ytab_off = (long long)ytab.size();
+            L.ssx = (double)sw / L.w;
+            L.ssy = (double)sh / L.h;
             int xmax = dw;
             std::vector<int> sxs(dw), a0s(dw), a1s(dw);
             for (int dx = 0; dx < dw; dx++) {
