@@ -33,7 +33,7 @@ constexpr int MAX_ZONE = 64;            // max FAST detection-zone side (cellw <
 constexpr int MAX_ROOTS = 32;
 constexpr int PATCH = 43;               // raw neighbourhood: +-21 (rBRIEF reach 18 + blur 3)
 constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
-constexpr int HBS = HBLUR_W;            // LDS row stride of the blurred rows (u16)
+constexpr int HBS = HBLUR_W + 1;        // LDS row stride of the blurred rows (u16): 19 dwords, dword-aligned rows
 
 __constant__ int c_pattern[1024] = {
 #include "orb_pattern31.inc"
@@ -1401,25 +1401,33 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     }
     const float angle = fast_atan2_dev((float)m01, (float)m10);
 
-    // horizontal Q8 blur, one row per lane (sliding window in registers); taps are symmetric
+    // horizontal Q8 blur, one row per lane, two columns per packed-u16 op: P(j) = (v[j], v[j+1]) is
+    // one v_perm of the row's dwords, and 18(P0+P6) + 34(P1+P5) + 48(P2+P4) + 56 P3 <= 65280 fits u16.
     if (lane < PATCH) {
-        int v[PATCH_DW * 4];
+        uint32_t w[PATCH_DW + 1];
 #pragma unroll
-        for (int d = 0; d < PATCH_DW; d++) {   // dword reads of the row, bytes unpacked in registers
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(&R[lane * RS + 4 * d]);
+        for (int d = 0; d < PATCH_DW; d++) w[d] = *reinterpret_cast<const uint32_t*>(&R[lane * RS + 4 * d]);
+        w[PATCH_DW] = 0;
+        auto P = [&](int j) -> us2 {   // bytes j, j+1 of the row as a u16 pair
+            const uint32_t sel = (uint32_t)(j & 3) | 0x0c00u | ((uint32_t)((j & 3) + 1) << 16) | 0x0c000000u;
+            const uint32_t r = __builtin_amdgcn_perm(w[(j >> 2) + 1], w[j >> 2], sel);
+            return *reinterpret_cast<const us2*>(&r);
+        };
+        const us2 k18 = {18, 18}, k34 = {34, 34}, k48 = {48, 48}, k56 = {56, 56};
 #pragma unroll
-            for (int q = 0; q < 4; q++) v[4 * d + q] = (int)((w >> (8 * q)) & 0xffu);
+        for (int c = 0; c < HBLUR_W; c += 2) {
+            const us2 o = k18 * (P(c) + P(c + 6)) + k34 * (P(c + 1) + P(c + 5)) + k48 * (P(c + 2) + P(c + 4)) +
+                          k56 * P(c + 3);
+            *reinterpret_cast<us2*>(&Hb[lane * HBS + c]) = o;   // column HBLUR_W (c = 36's pair) is padding
         }
-#pragma unroll
-        for (int c = 0; c < HBLUR_W; c++)
-            Hb[lane * HBS + c] =
-                (uint16_t)(18 * (v[c] + v[c + 6]) + 34 * (v[c + 1] + v[c + 5]) + 48 * (v[c + 2] + v[c + 4]) + 56 * v[c + 3]);
     }
     __syncthreads();
 
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
-    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+    double sd, cd;   // one sincos: the same values as ::cos / ::sin (double)
+    sincos((double)ang, &sd, &cd);
+    const float a = (float)cd, b = (float)sd;
     auto sample = [&](int idx) -> int {
         const float x = (float)c_pattern[2 * idx], y = (float)c_pattern[2 * idx + 1];
         const int dy = (int)rintf(x * b + y * a);
