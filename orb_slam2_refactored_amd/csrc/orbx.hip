@@ -39,6 +39,7 @@ __constant__ int c_pattern[1024] = {
 #include "orb_pattern31.inc"
 };
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+constexpr int c_umax_h[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // compile-time copy
 __constant__ int c_gauss[7] = {18, 34, 48, 56, 48, 34, 18};   // OpenCV 4.x bit-exact Q8 taps
 // FAST circle (cv::FAST makeOffsets, pattern 16): compile-time so LDS reads use immediate offsets
 constexpr int c_circle_dx_h[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -1385,15 +1386,23 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     }
     __syncthreads();
 
-    // IC_Angle on the unblurred level, patch centre (21, 21)
+    // IC_Angle on the unblurred level, patch centre (21, 21).  Lane = (row parity, u + 15): lanes
+    // 0-31 take rows +-v for odd v, lanes 32-63 for v + 1, so the 15 row pairs take 8 steps.
     int m10 = 0, m01 = 0;
-    if (lane < 31) m10 = (lane - 15) * R[21 * RS + 6 + lane];
-    for (int q = lane; q < 15 * 31; q += 64) {
-        const int v = q / 31 + 1, u = q - (v - 1) * 31 - 15;
-        if (u < -c_umax[v] || u > c_umax[v]) continue;
-        const int vp = R[(21 + v) * RS + 21 + u], vm = R[(21 - v) * RS + 21 + u];
-        m01 += v * (vp - vm);
-        m10 += u * (vp + vm);
+    {
+        const int hv = lane >> 5, u = (lane & 31) - 15;   // u = 16 on lanes 31 / 63: outside every umax
+        if (hv == 0 && u <= 15) m10 = u * R[21 * RS + 21 + u];
+        const uint8_t* cp = R + 21 * RS + 21 + u + hv * RS;
+#pragma unroll
+        for (int vv = 1; vv <= 15; vv += 2) {
+            const int v = vv + hv;
+            const int um = hv ? (vv + 1 <= 15 ? c_umax_h[vv + 1] : -1) : c_umax_h[vv];
+            if (u >= -um && u <= um) {
+                const int vp = cp[vv * RS], vm = cp[-(vv + 2 * hv) * RS];
+                m01 += v * (vp - vm);
+                m10 += u * (vp + vm);
+            }
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         m10 += __shfl_xor(m10, o, 64);
