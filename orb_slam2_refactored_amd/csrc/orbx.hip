@@ -1320,7 +1320,6 @@ constexpr int RS = 44;   // LDS raw-patch row stride
 // One workgroup = one wavefront = one kept keypoint.
 constexpr int DESC_KPW = 1;                               // keypoints per wavefront
 constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords per raw-patch row (RS = 4 * 11)
-constexpr int PATCH_LD = (PATCH * PATCH_DW + 63) / 64;    // dword loads per lane for a whole patch
 
 // One wavefront per DESC_KPW consecutive output keypoints of a frame (output order = level-major
 // list order); waves past the frame's total exit at once.
@@ -1357,25 +1356,31 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
     // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101)
     if (kx >= 21 && ky >= 21 && kx + 21 + 8 < L.w && ky + 21 < L.h) {
-        // interior: aligned dword pairs realigned with v_alignbyte, all loads in flight together
+        // interior: 16 lanes per row (dword d of row 4k + lane/16), 11 row groups; the group's row
+        // address is wave-uniform, so a load costs its realignment only (v_alignbyte of the aligned
+        // dword pair); all loads in flight before the LDS stores
+        constexpr int NG = (PATCH + 3) / 4;
         const uint8_t* base = img + (long long)(ky - 21) * step + (kx - 21);
-        uint32_t lo[PATCH_LD], hi[PATCH_LD];
-        int off[PATCH_LD], sh[PATCH_LD];
+        const int roff = lane >> 4, d = min(lane & 15, PATCH_DW - 1);
+        const int loff = roff * step + 4 * d;
+        uint32_t lo[NG], hi[NG];
+        int sh[NG];
 #pragma unroll
-        for (int t = 0; t < PATCH_LD; t++) {
-            const int it = min(lane + 64 * t, PATCH * PATCH_DW - 1);
-            const int r = it / PATCH_DW, d = it - r * PATCH_DW;
-            const uint8_t* pbyte = base + (long long)r * step + 4 * d;
+        for (int k = 0; k < NG; k++) {
+            const uint8_t* gb = base + (long long)min(4 * k, PATCH - 1 - roff) * step;   // rows <= 42
+            const uint8_t* pbyte = gb + loff;
             const int m = (int)(reinterpret_cast<uintptr_t>(pbyte) & 3);
             const uint32_t* pw = reinterpret_cast<const uint32_t*>(pbyte - m);
-            lo[t] = pw[0];
-            hi[t] = pw[1];
-            sh[t] = m;
-            off[t] = lane + 64 * t < PATCH * PATCH_DW ? r * RS + 4 * d : -1;
+            lo[k] = pw[0];
+            hi[k] = pw[1];
+            sh[k] = m;
         }
+        if ((lane & 15) < PATCH_DW) {
 #pragma unroll
-        for (int t = 0; t < PATCH_LD; t++)
-            if (off[t] >= 0) *reinterpret_cast<uint32_t*>(&R[off[t]]) = __builtin_amdgcn_alignbyte(hi[t], lo[t], sh[t]);
+            for (int k = 0; k < NG; k++)
+                if (4 * k + roff < PATCH)
+                    *reinterpret_cast<uint32_t*>(&R[(4 * k + roff) * RS + 4 * d]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+        }
     } else if (lane < PATCH) {
         const int xx = reflect101(kx - 21 + lane, L.w);
         uint8_t v[PATCH];
