@@ -465,6 +465,41 @@ __device__ __forceinline__ void crop_commit(const CropSrc& c, int lane, const u3
     }
 }
 
+// Row-group staging: lanes per crop row LR = 16 (32, 64 for wider crops), row group k covers
+// rows RPG*k .. RPG*k + RPG-1.  A group's source address is wave-uniform plus a per-lane constant,
+// so a load costs no address VALU; only the realignment (v_alignbyte) and the LDS address remain.
+constexpr int CROP_NG = 10;   // groups whose loads are issued together (40 rows at LR = 16)
+__device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint8_t* crop, int CSd) {
+    const int lrs = c.ndl <= 16 ? 4 : (c.ndl <= 32 ? 5 : 6);
+    const int RPG = 64 >> lrs;
+    const int roff = lane >> lrs, d = lane & ((1 << lrs) - 1);
+    const bool dok = d < c.ndl;
+    const int dd = dok ? d : 0;
+    const uint8_t* g0 = c.img + (long long)c.y0 * c.step + (c.x0 - 1);   // wave-uniform
+    const int loff = roff * c.step + 4 * dd;                            // per-lane constant
+    const int ng = (c.ch + RPG - 1) / RPG;
+    for (int k0 = 0; k0 < ng; k0 += CROP_NG) {
+        u32x2a4 v[CROP_NG];
+        int m[CROP_NG];
+#pragma unroll
+        for (int k = 0; k < CROP_NG; k++) {
+            // group k's rows; a partial last group reads up to RPG-1 rows past the crop, which stay
+            // inside the level (crops end >= 13 rows above its bottom edge); groups past the crop
+            // re-read the last group
+            const int gk = min(k0 + k, ng - 1);
+            const uint8_t* p = g0 + (long long)(RPG * gk) * c.step + loff;
+            m[k] = (int)(reinterpret_cast<uintptr_t>(p) & 3u);
+            v[k] = *reinterpret_cast<const u32x2a4*>(p - m[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < CROP_NG; k++) {
+            const int r = RPG * (k0 + k) + roff;
+            if (dok && r < c.ch)
+                reinterpret_cast<uint32_t*>(crop + r * CSd)[d] = __builtin_amdgcn_alignbyte(v[k].y, v[k].x, m[k]);
+        }
+    }
+}
+
 // One wavefront processes `cpw` consecutive (frame, cell) items of the XCD-swizzled order; item
 // i = f * ncells + cell.  LDS (sized per launch from the largest cell): the crop (zone + 3-px
 // apron), a zone map of corner strengths, a queue of pre-test passers and the ordered corner list.
@@ -508,9 +543,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     const int x0 = src.x0, y0 = src.y0;
     const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
     {
-        u32x2a4 pre[CROP_PF];
-        crop_prefetch(src, lane, pre);   // all of the lane's loads in flight, then the LDS stores
-        crop_commit(src, lane, pre, crop, CSd);
+        crop_stage_rows(src, lane, crop, CSd);
     }
     for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
     wave_lds_sync();
