@@ -545,7 +545,8 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     {
         crop_stage_rows(src, lane, crop, CSd);
     }
-    for (int i = lane; i < zh * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
+    for (int i = lane; i < (zh + 2) * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
+    uint8_t* Mc = Mz + ZSd + 1;   // zone (0, 0); the zero border makes out-of-zone neighbours read 0
     wave_lds_sync();
     if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
 
@@ -610,33 +611,30 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     // corner strengths into the zone map
     for (int j = lane; j < nc; j += 64) {
         const int i = clist[j];
-        Mz[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(corner_strength(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd), 255);
+        Mc[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(corner_strength(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd), 255);
     }
     wave_lds_sync();
 
-    auto nms = [&](int zy, int zx, int m, int t) -> bool {
-        if (m <= t) return false;
-#pragma unroll
-        for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-            for (int dx = -1; dx <= 1; dx++) {
-                if (!dx && !dy) continue;
-                const int yy = zy + dy, xx = zx + dx;
-                if (yy < 0 || yy >= zh || xx < 0 || xx >= zw) continue;
-                const int q = Mz[yy * ZSd + xx];
-                if (q > t && q >= m) return false;
-            }
-        return true;
-    };
     int n_ini = 0, n_min = 0;
     for (int jb = 0, ch2 = 0; jb < nc; jb += 64, ch2++) {
         const int j = jb + lane;
         bool ki = false, km = false;
-        if (j < nc) {
+        if (j < nc) {   // 3x3 NMS at both thresholds from one read of the 8 neighbours
             const int i = clist[j];
-            const int zy = i >> 8, zx = i & 255, m = Mz[zy * ZSd + zx];
-            ki = nms(zy, zx, m, th_ini);
-            km = nms(zy, zx, m, th_min);
+            const uint8_t* c0 = Mc + (i >> 8) * ZSd + (i & 255);
+            const int m = c0[0];
+            ki = m > th_ini;
+            km = m > th_min;
+#pragma unroll
+            for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                for (int dx = -1; dx <= 1; dx++) {
+                    if (!dx && !dy) continue;
+                    const int q = c0[dy * ZSd + dx];
+                    const bool ge = q >= m;
+                    ki = ki && !(ge && q > th_ini);
+                    km = km && !(ge && q > th_min);
+                }
         }
         const unsigned long long bi = __ballot(ki), bmn = __ballot(km);
         if (lane == 0) { bal[2 * ch2] = bi; bal[2 * ch2 + 1] = bmn; }
@@ -658,7 +656,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
             if (r < cap) {
                 const int zy = i >> 8, zx = i & 255;
                 const uint32_t x = (uint32_t)(x0 + 3 + zx), yy = (uint32_t)(y0 + 3 + zy);
-                out[r] = x | (yy << 12) | ((uint32_t)(Mz[zy * ZSd + zx] - 1) << 24);
+                out[r] = x | (yy << 12) | ((uint32_t)(Mc[zy * ZSd + zx] - 1) << 24);
             }
         }
         running += popc64(bm);
@@ -1748,9 +1746,9 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         FastLds fl;
         fl.CS = (int)align_up(mzw + 6 + 8, 4);         // +1 shift, +4 dword over-read each side
         if (fl.CS < 4 * ((mzw + 6 + 1 + 3) / 4)) fl.CS = 4 * ((mzw + 6 + 1 + 3) / 4);
-        fl.ZS = (int)align_up(mzw, 4);
+        fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
         fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6), 16);
-        fl.mz_bytes = (int)align_up((size_t)fl.ZS * mzh, 16);
+        fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
         fl.qcap = 64 + 4 * 64;
         fl.ccap = (int)align_up((size_t)mzw * mzh, 8);
         const int nbal = (fl.ccap + 63) / 64;
