@@ -362,15 +362,64 @@ __device__ __forceinline__ us2 hi_pair(uint32_t w) {   // bytes 2,3 -> u16 lanes
     const uint32_t r = __builtin_amdgcn_perm(0u, w, 0x0c030c02u);
     return *reinterpret_cast<const us2*>(&r);
 }
-__device__ __forceinline__ uint32_t compass2(us2 v, us2 n, us2 e, us2 s, us2 wv, us2 t) {
-    const us2 bmax = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_elementwise_min(n, e), __builtin_elementwise_min(e, s)),
-                                               __builtin_elementwise_max(__builtin_elementwise_min(s, wv), __builtin_elementwise_min(wv, n)));
-    const us2 dmin = __builtin_elementwise_min(__builtin_elementwise_min(__builtin_elementwise_max(n, e), __builtin_elementwise_max(e, s)),
-                                               __builtin_elementwise_min(__builtin_elementwise_max(s, wv), __builtin_elementwise_max(wv, n)));
+// The four adjacent pairs factor: (Bn & Be) | (Be & Bs) | (Bs & Bw) | (Bw & Bn) == (Bn | Bs) & (Be | Bw),
+// so bright <=> min(max(n, s), max(e, w)) > v + t and dark <=> max(min(n, s), min(e, w)) < v - t.
+// Returns a u16 pair that is non-zero in the lanes of the passing pixels.
+__device__ __forceinline__ us2 compass2(us2 v, us2 n, us2 e, us2 s, us2 wv, us2 t) {
+    const us2 bmax = __builtin_elementwise_min(__builtin_elementwise_max(n, s), __builtin_elementwise_max(e, wv));
+    const us2 dmin = __builtin_elementwise_max(__builtin_elementwise_min(n, s), __builtin_elementwise_min(e, wv));
     const us2 hi = v + t;
     const us2 lo = __builtin_elementwise_sub_sat(v, t);
-    const us2 f = __builtin_elementwise_sub_sat(bmax, hi) | __builtin_elementwise_sub_sat(lo, dmin);
-    return (f.x ? 1u : 0u) | (f.y ? 2u : 0u);
+    return __builtin_elementwise_sub_sat(bmax, hi) | __builtin_elementwise_sub_sat(lo, dmin);
+}
+
+// Corner strength M (cornerScore<16> + 1, or 0 when not a corner at any threshold) on packed u16
+// pairs: lane pair k holds circle positions (k, k + 8) as D = p - v + 256 in [1, 511], so every
+// min / max of the arc network covers two arcs at once; position j >= 8 is the swapped pair j - 8.
+// Same value as corner_strength().
+__device__ __forceinline__ us2 swap2(us2 a) { return __builtin_shufflevector(a, a, 1, 0); }
+__device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
+    const unsigned short bias = (unsigned short)(256 - c[0]);
+    const us2 b2 = {bias, bias};
+    us2 D[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const us2 p = {(unsigned short)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]],
+                       (unsigned short)c[c_circle_dy_h[k + 8] * cs + c_circle_dx_h[k + 8]]};
+        D[k] = p + b2;
+    }
+    us2 l[8], h[8], l2[8], h2[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {   // arcs of 2
+        const us2 n = k + 1 < 8 ? D[k + 1] : swap2(D[k - 7]);
+        l[k] = __builtin_elementwise_min(D[k], n);
+        h[k] = __builtin_elementwise_max(D[k], n);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {   // arcs of 4
+        const us2 nl = k + 2 < 8 ? l[k + 2] : swap2(l[k - 6]);
+        const us2 nh = k + 2 < 8 ? h[k + 2] : swap2(h[k - 6]);
+        l2[k] = __builtin_elementwise_min(l[k], nl);
+        h2[k] = __builtin_elementwise_max(h[k], nh);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {   // arcs of 8
+        const us2 nl = k + 4 < 8 ? l2[k + 4] : swap2(l2[k - 4]);
+        const us2 nh = k + 4 < 8 ? h2[k + 4] : swap2(h2[k - 4]);
+        l[k] = __builtin_elementwise_min(l2[k], nl);
+        h[k] = __builtin_elementwise_max(h2[k], nh);
+    }
+    us2 A = {0, 0}, B = {0xffff, 0xffff};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {   // arcs of 9 = two overlapping arcs of 8; max / min over all 16
+        const us2 nl = k + 1 < 8 ? l[k + 1] : swap2(l[k - 7]);
+        const us2 nh = k + 1 < 8 ? h[k + 1] : swap2(h[k - 7]);
+        A = __builtin_elementwise_max(A, __builtin_elementwise_min(l[k], nl));
+        B = __builtin_elementwise_min(B, __builtin_elementwise_max(h[k], nh));
+    }
+    const int bright = (int)max(A.x, A.y) - 256;   // max over arcs of min(p - v)
+    const int dark = 256 - (int)min(B.x, B.y);     // max over arcs of min(v - p)
+    return max(0, max(bright, dark));
 }
 
 // One wavefront per (cell, frame).  LDS (sized per launch from the largest cell): the crop
@@ -383,6 +432,8 @@ __device__ __forceinline__ uint32_t compass2(us2 v, us2 n, us2 e, us2 s, us2 wv,
 //   4. corner strength M (cornerScore + 1) for the corner list; NMS at iniThFAST and minThFAST
 //      over the list (3x3, cell-local: neighbours outside the zone count as 0)
 //   5. emit the iniThFAST set, or the minThFAST set when it is empty (DetectFAST :527-530)
+constexpr int FQ_RING = 512;   // pre-test passer ring (power of two, >= 64 + 256)
+
 struct FastLds {
     int CS, ZS, crop_bytes, mz_bytes, qcap, ccap;
 };
@@ -557,19 +608,29 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     const int QR = 1 << qsh, RPC = 64 >> qsh;
     const int qx = (lane & (QR - 1)) * 4, qy = lane >> qsh;
 
-    int qn = 0, nc = 0;
+    // Pre-test passers go to a ring of FQ_RING entries in row-major order; whenever 64 are
+    // pending they get the corner strength M densely (pending < 64 + 256 <= FQ_RING, so the
+    // ring never overwrites an undrained entry).  Corners (M > min(ini, min)) get M in the
+    // zone map and are appended to the ordered corner list.
+    int qn = 0, head = 0, nc = 0;
     auto drain = [&](int n) {
-        const int i = lane < n ? queue[lane] : -1;
-        bool c = false;
-        if (i >= 0) c = is_corner_t(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], tlo, CSd);
+        const int i = lane < n ? queue[(head + lane) & (FQ_RING - 1)] : -1;
+        int M = 0;
+        if (i >= 0) M = corner_strength_pk(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd);
+        const bool c = M > tlo;
         const unsigned long long bm = __ballot(c);
-        if (c) clist[nc + popc64(bm & lt)] = (short)i;
+        if (c) {
+            clist[nc + popc64(bm & lt)] = (short)i;
+            Mc[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(M, 255);
+        }
         nc += popc64(bm);
+        head += n;
     };
     for (int yb = 0; yb < zh; yb += RPC) {
         const int y = yb + qy;
-        uint32_t mask = 0;
-        if (y < zh && qx < zw) {
+        us2 f0 = {0, 0}, f1 = {0, 0};
+        const bool act = y < zh && qx < zw;
+        if (act) {
             const uint8_t* rowc = crop + (y + 3) * CSd + 4;   // zone (y, 0) = crop (y+3, 3) at byte 4
             const uint32_t wv = *reinterpret_cast<const uint32_t*>(rowc + qx);
             const uint32_t wl = *reinterpret_cast<const uint32_t*>(rowc + qx - 4);
@@ -578,41 +639,30 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
             const uint32_t ws = *reinterpret_cast<const uint32_t*>(rowc - 3 * CSd + qx);   // (0,-3)
             const uint32_t we = __builtin_amdgcn_alignbyte(wr, wv, 3);   // (+3, 0): bytes qx+3..qx+6
             const uint32_t ww = __builtin_amdgcn_alignbyte(wv, wl, 1);   // (-3, 0): bytes qx-3..qx
-            mask = compass2(lo_pair(wv), lo_pair(wn), lo_pair(we), lo_pair(ws), lo_pair(ww), t2) |
-                   (compass2(hi_pair(wv), hi_pair(wn), hi_pair(we), hi_pair(ws), hi_pair(ww), t2) << 2);
-            const int valid = min(4, zw - qx);
-            mask &= (1u << valid) - 1u;
+            f0 = compass2(lo_pair(wv), lo_pair(wn), lo_pair(we), lo_pair(ws), lo_pair(ww), t2);
+            f1 = compass2(hi_pair(wv), hi_pair(wn), hi_pair(we), hi_pair(ws), hi_pair(ww), t2);
         }
-        // ordered compaction of up to 4 passers per lane
-        const int cnt = __popc(mask);
-        const int incl = wave_incl_scan(cnt);
-        int pos = qn + incl - cnt;
-        for (int k = 0; k < 4; k++)
-            if (mask & (1u << k)) queue[pos++] = (short)((y << 8) | (qx + k));
-        qn += __shfl(incl, 63, 64);
+        // ordered compaction of up to 4 passers per lane: one ballot per pixel slot, the lane's
+        // queue position = the passers of the lower lanes (mbcnt) + its own earlier slots
+        const int valid = zw - qx;
+        const bool p0 = act && f0.x, p1 = act && valid > 1 && f0.y;
+        const bool p2 = act && valid > 2 && f1.x, p3 = act && valid > 3 && f1.y;
+        const unsigned long long b0 = __ballot(p0), b1 = __ballot(p1), b2 = __ballot(p2), b3 = __ballot(p3);
+        unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0u));
+        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, pre));
+        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, pre));
+        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, pre));
+        int pos = qn + (int)pre;
+        const short e0 = (short)((y << 8) | qx);
+        if (p0) queue[pos++ & (FQ_RING - 1)] = e0;
+        if (p1) queue[pos++ & (FQ_RING - 1)] = (short)(e0 + 1);
+        if (p2) queue[pos++ & (FQ_RING - 1)] = (short)(e0 + 2);
+        if (p3) queue[pos & (FQ_RING - 1)] = (short)(e0 + 3);
+        qn += popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
         wave_lds_sync();
-        while (qn >= 64) {
-            drain(64);
-            wave_lds_sync();
-            short tail[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) tail[k] = lane + 64 * (k + 1) < qn ? queue[lane + 64 * (k + 1)] : 0;
-            wave_lds_sync();
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (lane + 64 * (k + 1) < qn) queue[lane + 64 * k] = tail[k];
-            qn -= 64;
-            wave_lds_sync();
-        }
+        while (qn - head >= 64) drain(64);
     }
-    if (qn > 0) drain(qn);
-    wave_lds_sync();
-
-    // corner strengths into the zone map
-    for (int j = lane; j < nc; j += 64) {
-        const int i = clist[j];
-        Mc[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(corner_strength(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd), 255);
-    }
+    if (qn > head) drain(qn - head);
     wave_lds_sync();
 
     int n_ini = 0, n_min = 0;
@@ -1749,7 +1799,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
         fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
-        fl.qcap = 64 + 4 * 64;
+        fl.qcap = FQ_RING;
         fl.ccap = (int)align_up((size_t)mzw * mzh, 8);
         const int nbal = (fl.ccap + 63) / 64;
         h->fast_lds = (size_t)fl.crop_bytes + fl.mz_bytes + 2 * (size_t)(fl.qcap + fl.ccap) + 16 * (size_t)nbal;
