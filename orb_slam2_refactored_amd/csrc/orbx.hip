@@ -519,7 +519,9 @@ __device__ __forceinline__ void crop_commit(const CropSrc& c, int lane, const u3
 // Row-group staging: lanes per crop row LR = 16 (32, 64 for wider crops), row group k covers
 // rows RPG*k .. RPG*k + RPG-1.  A group's source address is wave-uniform plus a per-lane constant,
 // so a load costs no address VALU; only the realignment (v_alignbyte) and the LDS address remain.
-constexpr int CROP_NG = 10;   // groups whose loads are issued together (40 rows at LR = 16)
+constexpr int CROP_NG = 10;
+constexpr int FAST_CROP_SLACK = 3;   // crop rows past the tallest crop: a partial last row group (RPG <= 4)
+// groups whose loads are issued together (40 rows at LR = 16)
 __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint8_t* crop, int CSd) {
     const int lrs = c.ndl <= 16 ? 4 : (c.ndl <= 32 ? 5 : 6);
     const int RPG = 64 >> lrs;
@@ -527,8 +529,34 @@ __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint
     const bool dok = d < c.ndl;
     const int dd = dok ? d : 0;
     const uint8_t* g0 = c.img + (long long)c.y0 * c.step + (c.x0 - 1);   // wave-uniform
+    const int ng = (c.ch + RPG - 1) >> (6 - lrs);
+    if ((c.step & 3) == 0) {
+        // dword-multiple row step (every pyramid level; level 0 unless the caller's step is odd):
+        // the misalignment is one wave-uniform shift, the loads are buffer loads off a scalar
+        // resource with a per-lane constant voffset and a per-group soffset (no address VALU),
+        // and a partial last group writes into the crop's slack rows (FAST_CROP_SLACK)
+        const int m = __builtin_amdgcn_readfirstlane((int)(reinterpret_cast<uintptr_t>(g0) & 3u));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g0 - m), 0, 0x7fffffff, 0x00020000);
+        const int voff = roff * c.step + 4 * dd;
+        uint32_t* lrow = reinterpret_cast<uint32_t*>(crop + roff * CSd) + d;
+        const int gstep = RPG * c.step, lstep = RPG * CSd / 4;
+        for (int k0 = 0; k0 < ng; k0 += CROP_NG) {
+            u32x2a4 v[CROP_NG];
+#pragma unroll
+            for (int k = 0; k < CROP_NG; k++) {
+                const int gk = min(k0 + k, ng - 1);   // groups past the crop re-read the last one
+                const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, gk * gstep, 0);
+                v[k] = u32x2a4{t[0], t[1]};
+            }
+            if (dok) {
+#pragma unroll
+                for (int k = 0; k < CROP_NG; k++)
+                    if (k0 + k < ng) lrow[(k0 + k) * lstep] = __builtin_amdgcn_alignbyte(v[k].y, v[k].x, m);
+            }
+        }
+        return;
+    }
     const int loff = roff * c.step + 4 * dd;                            // per-lane constant
-    const int ng = (c.ch + RPG - 1) / RPG;
     for (int k0 = 0; k0 < ng; k0 += CROP_NG) {
         u32x2a4 v[CROP_NG];
         int m[CROP_NG];
@@ -1797,7 +1825,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         fl.CS = (int)align_up(mzw + 6 + 8, 4);         // +1 shift, +4 dword over-read each side
         if (fl.CS < 4 * ((mzw + 6 + 1 + 3) / 4)) fl.CS = 4 * ((mzw + 6 + 1 + 3) / 4);
         fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
-        fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6), 16);
+        fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6 + FAST_CROP_SLACK), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
         fl.qcap = FQ_RING;
         fl.ccap = (int)align_up((size_t)mzw * mzh, 8);

@@ -125,6 +125,32 @@ def test_strided_input(oracle):
     assert_same_kps(kps, okps, desc, odesc)
 
 
+@pytest.mark.parametrize("W", [641, 643, 1277])
+def test_odd_row_step(oracle, W):
+    """A level-0 row step that is not a dword multiple (the host API uploads with step = cols)
+    takes the per-group realignment path of the FAST crop staging; every pyramid level has a
+    16-B aligned stride."""
+    img = synth_image(13 + W, W, 480)
+    kps, desc = make().Extract(img)
+    okps, odesc, _ = oracle.extract(oracle.params(1000), img)
+    assert_same_kps(kps, okps, desc, odesc)
+
+
+def test_batch_device_odd_step(oracle):
+    import torch
+    frames = np.stack([synth_image(40 + i, 701, 480) for i in range(3)])
+    t = torch.from_numpy(frames).cuda()[:, :, 3:643]   # row step 701, base offset 3
+    assert t.stride(1) == 701
+    ex = make()
+    kps_t, desc_t, cnt_t = ex.extract_batch_device(t)
+    torch.cuda.synchronize()
+    for i in range(3):
+        okps, odesc, _ = oracle.extract(oracle.params(1000), np.ascontiguousarray(frames[i][:, 3:643]))
+        n = int(cnt_t[i])
+        kps = ex.kps_to_numpy(kps_t[i, :n].cpu().numpy())
+        assert_same_kps(kps, okps, desc_t[i, :n].cpu().numpy(), odesc)
+
+
 def test_batch_device_matches_single(oracle):
     import torch
     frames = np.stack([synth_image(20 + i, 640, 480) for i in range(5)])
