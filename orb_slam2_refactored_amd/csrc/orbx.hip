@@ -354,6 +354,8 @@ __device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t, int cs) {
 // circle-adjacent compass points (positions 0/4/8/12) both brighter than v+t, or both darker than
 // v-t.  With packed u16 lanes: bright <=> max over the 4 adjacent pairs of min(pa, pb) > v + t,
 // dark <=> min over the pairs of max(pa, pb) < v - t (no clamping needed: p <= 255).
+__device__ __forceinline__ uint32_t us2u(us2 a) { return __builtin_bit_cast(uint32_t, a); }
+__device__ __forceinline__ us2 u2us(uint32_t a) { return __builtin_bit_cast(us2, a); }
 __device__ __forceinline__ us2 lo_pair(uint32_t w) {   // bytes 0,1 -> u16 lanes
     const uint32_t r = __builtin_amdgcn_perm(0u, w, 0x0c010c00u);
     return *reinterpret_cast<const us2*>(&r);
@@ -433,6 +435,7 @@ __device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
 //      over the list (3x3, cell-local: neighbours outside the zone count as 0)
 //   5. emit the iniThFAST set, or the minThFAST set when it is empty (DetectFAST :527-530)
 constexpr int FQ_RING = 512;   // pre-test passer ring (power of two, >= 64 + 256)
+constexpr int FQ2_RING = 128;  // diagonal-filter passer ring (power of two, >= 64 + 64)
 
 struct FastLds {
     int CS, ZS, crop_bytes, mz_bytes, qcap, ccap;
@@ -635,14 +638,23 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     const int qsh = zw <= 32 ? 3 : 4;
     const int QR = 1 << qsh, RPC = 64 >> qsh;
     const int qx = (lane & (QR - 1)) * 4, qy = lane >> qsh;
+    // lane-constant masks of the pixels inside the zone (columns qx .. qx+3 < zw)
+    // (opaque to the compiler, so the AND stays one v_and instead of per-half selects)
+    uint32_t vm0 = (qx < zw ? 0xffffu : 0u) | (qx + 1 < zw ? 0xffff0000u : 0u);
+    uint32_t vm1 = (qx + 2 < zw ? 0xffffu : 0u) | (qx + 3 < zw ? 0xffff0000u : 0u);
+    asm volatile("" : "+v"(vm0), "+v"(vm1));
 
-    // Pre-test passers go to a ring of FQ_RING entries in row-major order; whenever 64 are
-    // pending they get the corner strength M densely (pending < 64 + 256 <= FQ_RING, so the
-    // ring never overwrites an undrained entry).  Corners (M > min(ini, min)) get M in the
-    // zone map and are appended to the ordered corner list.
-    int qn = 0, head = 0, nc = 0;
-    auto drain = [&](int n) {
-        const int i = lane < n ? queue[(head + lane) & (FQ_RING - 1)] : -1;
+    // Pre-test passers go to a ring of FQ_RING entries in row-major order.  Whenever 64 are pending
+    // they are filtered by the diagonal points 2/6/10/14 (a 9-arc also holds two circle-adjacent
+    // ones of them, bright or dark: 14 % -> 5 % of the pixels on the synthetic frames) into a
+    // second ring, and whenever 64 of those are pending they get the corner strength M densely.
+    // (pending < 64 + 256 <= FQ_RING and < 64 + 64 <= FQ2_RING, so no ring overwrites an
+    // undrained entry.)  Corners (M > min(ini, min)) get M in the zone map and are appended to
+    // the ordered corner list.
+    short* queue2 = queue + FQ_RING;
+    int qn = 0, head = 0, q2n = 0, h2 = 0, nc = 0;
+    auto strength = [&](int n) {
+        const int i = lane < n ? queue2[(h2 + lane) & (FQ2_RING - 1)] : -1;
         int M = 0;
         if (i >= 0) M = corner_strength_pk(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd);
         const bool c = M > tlo;
@@ -652,7 +664,23 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
             Mc[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(M, 255);
         }
         nc += popc64(bm);
+        h2 += n;
+    };
+    auto drain = [&](int n) {
+        const int i = lane < n ? queue[(head + lane) & (FQ_RING - 1)] : -1;
+        bool pass = false;
+        if (i >= 0) {
+            const uint8_t* c = &crop[((i >> 8) + 3) * CSd + 4 + (i & 255)];
+            const int v = c[0];
+            const int p2 = c[2 * CSd + 2], p6 = c[-2 * CSd + 2], p10 = c[-2 * CSd - 2], p14 = c[2 * CSd - 2];
+            pass = min(max(p2, p10), max(p6, p14)) > v + tlo || max(min(p2, p10), min(p6, p14)) < v - tlo;
+        }
+        const unsigned long long bm = __ballot(pass);
+        if (pass) queue2[(q2n + popc64(bm & lt)) & (FQ2_RING - 1)] = (short)i;
+        q2n += popc64(bm);
         head += n;
+        wave_lds_sync();
+        if (q2n - h2 >= 64) strength(64);
     };
     for (int yb = 0; yb < zh; yb += RPC) {
         const int y = yb + qy;
@@ -667,14 +695,12 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
             const uint32_t ws = *reinterpret_cast<const uint32_t*>(rowc - 3 * CSd + qx);   // (0,-3)
             const uint32_t we = __builtin_amdgcn_alignbyte(wr, wv, 3);   // (+3, 0): bytes qx+3..qx+6
             const uint32_t ww = __builtin_amdgcn_alignbyte(wv, wl, 1);   // (-3, 0): bytes qx-3..qx
-            f0 = compass2(lo_pair(wv), lo_pair(wn), lo_pair(we), lo_pair(ws), lo_pair(ww), t2);
-            f1 = compass2(hi_pair(wv), hi_pair(wn), hi_pair(we), hi_pair(ws), hi_pair(ww), t2);
+            f0 = u2us(us2u(compass2(lo_pair(wv), lo_pair(wn), lo_pair(we), lo_pair(ws), lo_pair(ww), t2)) & vm0);
+            f1 = u2us(us2u(compass2(hi_pair(wv), hi_pair(wn), hi_pair(we), hi_pair(ws), hi_pair(ww), t2)) & vm1);
         }
         // ordered compaction of up to 4 passers per lane: one ballot per pixel slot, the lane's
         // queue position = the passers of the lower lanes (mbcnt) + its own earlier slots
-        const int valid = zw - qx;
-        const bool p0 = act && f0.x, p1 = act && valid > 1 && f0.y;
-        const bool p2 = act && valid > 2 && f1.x, p3 = act && valid > 3 && f1.y;
+        const bool p0 = f0.x != 0, p1 = f0.y != 0, p2 = f1.x != 0, p3 = f1.y != 0;
         const unsigned long long b0 = __ballot(p0), b1 = __ballot(p1), b2 = __ballot(p2), b3 = __ballot(p3);
         unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0u));
         pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, pre));
@@ -691,6 +717,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         while (qn - head >= 64) drain(64);
     }
     if (qn > head) drain(qn - head);
+    if (q2n > h2) strength(q2n - h2);
     wave_lds_sync();
 
     int n_ini = 0, n_min = 0;
@@ -1827,7 +1854,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
         fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6 + FAST_CROP_SLACK), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
-        fl.qcap = FQ_RING;
+        fl.qcap = FQ_RING + FQ2_RING;
         fl.ccap = (int)align_up((size_t)mzw * mzh, 8);
         const int nbal = (fl.ccap + 63) / 64;
         h->fast_lds = (size_t)fl.crop_bytes + fl.mz_bytes + 2 * (size_t)(fl.qcap + fl.ccap) + 16 * (size_t)nbal;
