@@ -355,8 +355,11 @@ def main():
     traffic = measured_traffic(dom, stages[dom][1] / max(args.steps, 1), B, W, H, args.nfeatures)
     dom_ms, dom_launches = stages[dom]
     per_launch_ms = dom_ms / max(dom_launches, 1)
-    frames_per_launch = B
-    dom_bytes = stage_bytes[dom] * frames_per_launch
+    launches_per_step = dom_launches / max(args.steps, 1)
+    # a stage may run as several launches per step (fast_cells: level 0 on the side stream, levels
+    # 1..7 on the main stream): achieved = the step's algorithmic bytes / the step's summed launch
+    # durations, i.e. per launch = bytes / launches_per_step over the average launch duration
+    dom_bytes = stage_bytes[dom] * B / max(launches_per_step, 1)
     achieved = dom_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
     extract_ms = sum(v[0] for v in stages.values()) / max(args.steps, 1)
     pipeline_gbs = bytes_frame * B / (extract_ms * 1e-3) / 1e9 if extract_ms > 0 else 0.0
@@ -382,6 +385,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": per_launch_ms,
+                     "launches_per_step": launches_per_step,
                      "stage_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
                      "pipeline_algorithmic_GBs": pipeline_gbs, "pipeline_bytes_per_frame": bytes_frame},
         "keypoints_per_frame": n_kp,

@@ -590,7 +590,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
-                                                        int n_items, int cpw) {
+                                                        int n_items, int cpw, int cell_beg, int ncell) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -604,11 +604,10 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     const int lb = xcd_swizzle(blockIdx.x, gridDim.x);
     FAST_STAMP(0, __builtin_amdgcn_s_memtime());
     const int i_beg = lb * cpw, i_end = min(i_beg + cpw, n_items);
-    const int ncells = g.ncells_total;
-
+    // item i = f * ncell + (cell - cell_beg): this launch covers cells [cell_beg, cell_beg + ncell)
     auto source = [&](int item, CellDev& cd, int& f, int& ci) {
-        f = item / ncells;
-        ci = item - f * ncells;
+        f = item / ncell;
+        ci = cell_beg + item - f * ncell;
         cd = cells[ci];
         CropSrc c;
         c.img = level_base(g, cd.level, f, in, in_fstride, in_step, pyr, &c.step);
@@ -1041,7 +1040,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                                                        const uint32_t* __restrict__ slots, const CellDev* cells,
                                                        uint32_t* __restrict__ Pbuf, uint32_t* __restrict__ Tbuf,
                                                        uint32_t* __restrict__ sel, int* __restrict__ sel_cnt, int NC,
-                                                       int PTC, uint32_t* fault) {
+                                                       int PTC, uint32_t* fault, int lev0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     QtNode* na = reinterpret_cast<QtNode*>(smem);
     QtNode* nb = na + NC;
@@ -1057,7 +1056,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     __shared__ int s_sortcnt[2];
     __shared__ int rc[MAX_ROOTS];
 
-    const int f = blockIdx.x, l = blockIdx.y;   // level-major grid: level-0 trees start first
+    const int f = blockIdx.x, l = lev0 + (int)blockIdx.y;   // levels lev0 .. lev0 + gridDim.y - 1
     const LevelDev& L = g.lv[l];
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     int* scnt = sel_cnt + f * g.nlevels + l;
@@ -1648,6 +1647,12 @@ struct orbx_extractor {
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
+    // level-split overlap (launch_chunk): level 0's FAST + quadtree on a side stream.  Off by
+    // default: measured no gain at C2 (the concurrent kernels share the CUs: pyramid 0.26 -> 0.42 ms,
+    // wall time unchanged), and it keeps the per-kernel launch times uncontended.  ORBX_LEVEL_OVERLAP=1
+    bool lvl_overlap = false;
+    hipStream_t lvl_side = nullptr;
+    hipEvent_t lvl_fork = nullptr, lvl_join = nullptr;
     DevBuf d_cells, d_xtab, d_ytab;
 
     // workspace for up to ws_frames frames
@@ -1923,7 +1928,8 @@ struct StageMark {
 // its per-frame buffers from the frame index within the launch, so a chunk is launched with base
 // pointers advanced by f0 frames.
 static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F, long long fstride, int step,
-                         orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st) {
+                         orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st,
+                         hipStream_t side = nullptr) {
     const Geom& g = h->geom;
     uint8_t* pyr = h->d_pyr.as<uint8_t>() + (long long)f0 * g.pyr_frame_bytes;
     d_imgs += (long long)f0 * fstride;
@@ -1936,29 +1942,55 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     uint32_t* Tb = h->d_T.as<uint32_t>() + (long long)f0 * g.cand_frame;
     uint32_t* sel = h->d_sel.as<uint32_t>() + (long long)f0 * g.out_frame;
     int* selcnt = h->d_selcnt.as<int>() + (long long)f0 * g.nlevels;
-    {
-    StageMark m0(h, st, 0);
-    for (int l = 1; l < g.nlevels; l++) {
-        dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
-                  (unsigned)F);
-        hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
-                           h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
-    }
-    }
     uint32_t* fault = h->d_fault.as<uint32_t>();
-    if (g.ncells_total > 0) {
-        StageMark m1(h, st, 1);
-        const int n_items = g.ncells_total * F;
+    auto fast = [&](int cb, int nc, hipStream_t s) {
+        if (nc <= 0) return;
+        StageMark m1(h, s, 1);
+        const int n_items = nc * F;
         const int cpw = h->fast_cpw;
-        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)((n_items + cpw - 1) / cpw)), dim3(64), h->fast_lds, st,
+        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)((n_items + cpw - 1) / cpw)), dim3(64), h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
-                           h->p.minThFAST, slots, cellcnt, fault, h->fl,
-                           n_items, cpw);
-    }
-    {
-    StageMark m2(h, st, 2);
-    hipLaunchKernelGGL(quadtree_kernel, dim3((unsigned)F, (unsigned)g.nlevels), dim3(256), h->qt_lds, st, g,
-                       cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault);
+                           h->p.minThFAST, slots, cellcnt, fault, h->fl, n_items, cpw, cb, nc);
+    };
+    auto quadtree = [&](int l0, int nl, hipStream_t s) {
+        if (nl <= 0) return;
+        StageMark m2(h, s, 2);
+        hipLaunchKernelGGL(quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(256), h->qt_lds, s, g,
+                           cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0);
+    };
+    const int nc0 = g.lv[0].ncells;
+    if (side && nc0 > 0 && g.nlevels > 1) {
+        // Level 0 needs no pyramid: its FAST + quadtree run on the side stream while the main
+        // stream builds levels 1..7 (latency-bound cascade) and runs their FAST / quadtree, so the
+        // level-0 tree's serial rounds overlap the FAST work of the other levels.
+        (void)hipStreamWaitEvent(side, h->lvl_fork, 0);
+        fast(0, nc0, side);
+        quadtree(0, 1, side);
+        (void)hipEventRecord(h->lvl_join, side);
+        {
+            StageMark m0(h, st, 0);
+            for (int l = 1; l < g.nlevels; l++) {
+                dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
+                          (unsigned)F);
+                hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
+                                   h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
+            }
+        }
+        fast(nc0, g.ncells_total - nc0, st);
+        quadtree(1, g.nlevels - 1, st);
+        (void)hipStreamWaitEvent(st, h->lvl_join, 0);
+    } else {
+        {
+            StageMark m0(h, st, 0);
+            for (int l = 1; l < g.nlevels; l++) {
+                dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
+                          (unsigned)F);
+                hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
+                                   h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
+            }
+        }
+        fast(0, g.ncells_total, st);
+        quadtree(0, g.nlevels, st);
     }
     {
     StageMark m3(h, st, 3);
@@ -1975,7 +2007,17 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
                         orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st) {
     int nsub = std::min(h->nsub, F / ORBX_MIN_SUB_FRAMES);
     if (nsub <= 1) {
-        launch_chunk(h, 0, d_imgs, F, fstride, step, d_kps, d_desc, d_counts, cap, st);
+        hipStream_t side = nullptr;
+        if (h->lvl_overlap) {
+            if (!h->lvl_side) {
+                ORB_HIP_TRY(hipStreamCreateWithFlags(&h->lvl_side, hipStreamNonBlocking));
+                ORB_HIP_TRY(hipEventCreateWithFlags(&h->lvl_fork, hipEventDisableTiming));
+                ORB_HIP_TRY(hipEventCreateWithFlags(&h->lvl_join, hipEventDisableTiming));
+            }
+            ORB_HIP_TRY(hipEventRecord(h->lvl_fork, st));
+            side = h->lvl_side;
+        }
+        launch_chunk(h, 0, d_imgs, F, fstride, step, d_kps, d_desc, d_counts, cap, st, side);
         ORB_HIP_TRY(hipGetLastError());
         return ORB_OK;
     }
@@ -2027,6 +2069,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
+    if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     compute_tables(h);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -2051,6 +2094,9 @@ int orbx_destroy(orbx_extractor* h) {
     if (h->stream) (void)hipStreamDestroy(h->stream);
     for (auto& se : h->sub) { (void)hipStreamDestroy(se.first); (void)hipEventDestroy(se.second); }
     if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+    if (h->lvl_side) (void)hipStreamDestroy(h->lvl_side);
+    if (h->lvl_fork) (void)hipEventDestroy(h->lvl_fork);
+    if (h->lvl_join) (void)hipEventDestroy(h->lvl_join);
     delete h;
     return ORB_OK;
 }
