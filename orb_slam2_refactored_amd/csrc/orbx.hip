@@ -24,6 +24,7 @@
 
 #include "common.h"
 #include "qt_sort.h"
+#include "sincos_f.h"
 #include "stereo.h"
 
 namespace orbamd {
@@ -1574,9 +1575,8 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
-    double sd, cd;   // one sincos: the same values as ::cos / ::sin (double)
-    sincos((double)ang, &sd, &cd);
-    const float a = (float)cd, b = (float)sd;
+    float a, b;   // (float)::cos / ::sin((double)ang), sincos_f.h (checked on every float in range)
+    sincos_f2d(ang, &b, &a);
     auto sample = [&](int idx) -> int {
         const float x = (float)c_pattern[2 * idx], y = (float)c_pattern[2 * idx + 1];
         const int dy = (int)rintf(x * b + y * a);
