@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-end evidence in one GPU session: parity tests, smoke, PMC traffic passes, the bench line
+# (reading the fresh traffic json) and the rocprofv3 kernel-trace stats of the same bench command.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r01}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 -ra > gpurun_out/pytest_gpu.log 2>&1 \
+  || { tail -30 gpurun_out/pytest_gpu.log; exit 2; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 3; }
+tail -1 gpurun_out/smoke.log
+bash tools/gpu_traffic.sh $TAG || exit 4
+cp gpurun_out/traffic_$TAG/${TAG}_traffic.json profiles/${TAG}_traffic.json
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_$TAG.log 2>&1 || { tail -30 gpurun_out/bench_$TAG.log; exit 5; }
+grep '^{' gpurun_out/bench_$TAG.log > gpurun_out/${TAG}_bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
+    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_bench.log; exit 6; }
+find gpurun_out/prof_$TAG -name "*stats*"
+echo refresh done
