@@ -22,6 +22,8 @@
 #include <mutex>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "common.h"
 #include "qt_sort.h"
 #include "sincos_f.h"
@@ -1904,25 +1906,20 @@ static hipEvent_t prof_event(orbx_extractor* h) {
 
 constexpr int ORBX_MIN_SUB_FRAMES = 16;
 
-struct StageMark {
-    orbx_extractor* h;
-    hipStream_t st;
-    int stage;
-    hipEvent_t a = nullptr;
-    StageMark(orbx_extractor* h_, hipStream_t s, int k) : h(h_), st(s), stage(k) {
-        if (h->prof) {
-            a = prof_event(h);
-            (void)hipEventRecord(a, st);
-        }
+// Per-launch timing when profiling: hipExtLaunchKernel records the two events as part of the
+// kernel's own dispatch (start / completion of that kernel, no marker packets in the stream), so a
+// stage's time is the sum of its kernels' durations, as rocprofv3 reports them.
+template <typename... KArgs, typename... Args>
+static void launch_timed(orbx_extractor* h, int stage, void (*kernel)(KArgs...), dim3 grid, dim3 block,
+                         uint32_t shmem, hipStream_t s, Args... args) {
+    if (h->prof) {
+        hipEvent_t a = prof_event(h), b = prof_event(h);
+        hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, static_cast<KArgs>(args)...);
+        h->prof_ev[stage].push_back({a, b});
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, shmem, s, static_cast<KArgs>(args)...);
     }
-    ~StageMark() {
-        if (h->prof) {
-            hipEvent_t b = prof_event(h);
-            (void)hipEventRecord(b, st);
-            h->prof_ev[stage].push_back({a, b});
-        }
-    }
-};
+}
 
 // All four stages for frames [f0, f0 + F) of the workspace, enqueued on st.  Every kernel indexes
 // its per-frame buffers from the frame index within the launch, so a chunk is launched with base
@@ -1945,17 +1942,15 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     uint32_t* fault = h->d_fault.as<uint32_t>();
     auto fast = [&](int cb, int nc, hipStream_t s) {
         if (nc <= 0) return;
-        StageMark m1(h, s, 1);
         const int n_items = nc * F;
         const int cpw = h->fast_cpw;
-        hipLaunchKernelGGL(fast_cells_kernel, dim3((unsigned)((n_items + cpw - 1) / cpw)), dim3(64), h->fast_lds, s,
+        launch_timed(h, 1, fast_cells_kernel, dim3((unsigned)((n_items + cpw - 1) / cpw)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
                            h->p.minThFAST, slots, cellcnt, fault, h->fl, n_items, cpw, cb, nc);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
-        StageMark m2(h, s, 2);
-        hipLaunchKernelGGL(quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(256), h->qt_lds, s, g,
+        launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(256), (uint32_t)h->qt_lds, s, g,
                            cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0);
     };
     const int nc0 = g.lv[0].ncells;
@@ -1968,11 +1963,10 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         quadtree(0, 1, side);
         (void)hipEventRecord(h->lvl_join, side);
         {
-            StageMark m0(h, st, 0);
             for (int l = 1; l < g.nlevels; l++) {
                 dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
                           (unsigned)F);
-                hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
+                launch_timed(h, 0, pyramid_level_kernel, grid, dim3(256), 0u, st, g, l, d_imgs, fstride, step, pyr,
                                    h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
             }
         }
@@ -1981,11 +1975,10 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         (void)hipStreamWaitEvent(st, h->lvl_join, 0);
     } else {
         {
-            StageMark m0(h, st, 0);
             for (int l = 1; l < g.nlevels; l++) {
                 dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
                           (unsigned)F);
-                hipLaunchKernelGGL(pyramid_level_kernel, grid, dim3(256), 0, st, g, l, d_imgs, fstride, step, pyr,
+                launch_timed(h, 0, pyramid_level_kernel, grid, dim3(256), 0u, st, g, l, d_imgs, fstride, step, pyr,
                                    h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
             }
         }
@@ -1993,9 +1986,8 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         quadtree(0, g.nlevels, st);
     }
     {
-    StageMark m3(h, st, 3);
-    hipLaunchKernelGGL(describe_kernel, dim3((unsigned)((g.out_frame + DESC_KPW - 1) / DESC_KPW), (unsigned)F), dim3(64),
-                       0, st, g,
+    launch_timed(h, 3, describe_kernel, dim3((unsigned)((g.out_frame + DESC_KPW - 1) / DESC_KPW), (unsigned)F), dim3(64),
+                       0u, st, g,
                        d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
     }
 }

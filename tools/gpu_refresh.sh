@@ -16,7 +16,12 @@ bash tools/gpu_traffic.sh $TAG || exit 4
 cp gpurun_out/traffic_$TAG/${TAG}_traffic.json profiles/${TAG}_traffic.json
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_$TAG.log 2>&1 || { tail -30 gpurun_out/bench_$TAG.log; exit 5; }
 grep '^{' gpurun_out/bench_$TAG.log > gpurun_out/${TAG}_bench.json
+# kernel stats of the C2 bench leg alone (the per-kernel averages that must agree with the bench
+# line's live HIP-event launch times), then of the secondary legs
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_bench.log; exit 6; }
-find gpurun_out/prof_$TAG -name "*stats*"
+    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-ba --no-stereo --no-pose --no-projection --no-bow \
+    > gpurun_out/prof_${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_bench.log; exit 6; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_legs -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_${TAG}_legs.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_legs.log; exit 7; }
+find gpurun_out/prof_$TAG gpurun_out/prof_${TAG}_legs -name "*kernel_stats*"
 echo refresh done

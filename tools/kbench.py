@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--match", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="no per-stage event timing (wall time only)")
     a = ap.parse_args()
     import torch
     from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
@@ -31,7 +32,7 @@ def main():
     m = ORBmatcher(0.6, False)
     prev = torch.tensor([(i - 1) % a.frames for i in range(a.frames)], dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
-    ex.profile(True)
+    ex.profile(not a.no_profile)
     t0 = time.perf_counter()
     for _ in range(a.iters):
         ex.extract_batch_device(frames, kps, desc, cnt)
