@@ -38,7 +38,7 @@ constexpr int PATCH = 43;               // raw neighbourhood: +-21 (rBRIEF reach
 constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
 constexpr int HBS = HBLUR_W + 1;        // LDS row stride of the blurred rows (u16): 19 dwords, dword-aligned rows
 
-__constant__ int c_pattern[1024] = {
+__constant__ float c_pattern[1024] = {   // bit_pattern_31_ (:142-400) as floats (the samples' operands)
 #include "orb_pattern31.inc"
 };
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
@@ -658,12 +658,12 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     auto strength = [&](int n) {
         const int i = lane < n ? queue2[(h2 + lane) & (FQ2_RING - 1)] : -1;
         int M = 0;
-        if (i >= 0) M = corner_strength_pk(&crop[((i >> 8) + 3) * CSd + 4 + (i & 255)], CSd);
+        if (i >= 0) M = corner_strength_pk(&crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)], CSd);
         const bool c = M > tlo;
         const unsigned long long bm = __ballot(c);
         if (c) {
             clist[nc + popc64(bm & lt)] = (short)i;
-            Mc[(i >> 8) * ZSd + (i & 255)] = (uint8_t)min(M, 255);
+            Mc[__mul24(i >> 8, ZSd) + (i & 255)] = (uint8_t)min(M, 255);
         }
         nc += popc64(bm);
         h2 += n;
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         const int i = lane < n ? queue[(head + lane) & (FQ_RING - 1)] : -1;
         bool pass = false;
         if (i >= 0) {
-            const uint8_t* c = &crop[((i >> 8) + 3) * CSd + 4 + (i & 255)];
+            const uint8_t* c = &crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)];
             const int v = c[0];
             const int p2 = c[2 * CSd + 2], p6 = c[-2 * CSd + 2], p10 = c[-2 * CSd - 2], p14 = c[2 * CSd - 2];
             pass = min(max(p2, p10), max(p6, p14)) > v + tlo || max(min(p2, p10), min(p6, p14)) < v - tlo;
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         us2 f0 = {0, 0}, f1 = {0, 0};
         const bool act = y < zh && qx < zw;
         if (act) {
-            const uint8_t* rowc = crop + (y + 3) * CSd + 4;   // zone (y, 0) = crop (y+3, 3) at byte 4
+            const uint8_t* rowc = crop + __mul24(y + 3, CSd) + 4;   // zone (y, 0) = crop (y+3, 3) at byte 4
             const uint32_t wv = *reinterpret_cast<const uint32_t*>(rowc + qx);
             const uint32_t wl = *reinterpret_cast<const uint32_t*>(rowc + qx - 4);
             const uint32_t wr = *reinterpret_cast<const uint32_t*>(rowc + qx + 4);
@@ -728,7 +728,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         bool ki = false, km = false;
         if (j < nc) {   // 3x3 NMS at both thresholds from one read of the 8 neighbours
             const int i = clist[j];
-            const uint8_t* c0 = Mc + (i >> 8) * ZSd + (i & 255);
+            const uint8_t* c0 = Mc + __mul24(i >> 8, ZSd) + (i & 255);
             const int m = c0[0];
             ki = m > th_ini;
             km = m > th_min;
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
             if (r < cap) {
                 const int zy = i >> 8, zx = i & 255;
                 const uint32_t x = (uint32_t)(x0 + 3 + zx), yy = (uint32_t)(y0 + 3 + zy);
-                out[r] = x | (yy << 12) | ((uint32_t)(Mc[zy * ZSd + zx] - 1) << 24);
+                out[r] = x | (yy << 12) | ((uint32_t)(Mc[__mul24(zy, ZSd) + zx] - 1) << 24);
             }
         }
         running += popc64(bm);
@@ -1560,17 +1560,18 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 #pragma unroll
         for (int d = 0; d < PATCH_DW; d++) w[d] = *reinterpret_cast<const uint32_t*>(&R[lane * RS + 4 * d]);
         w[PATCH_DW] = 0;
-        auto P = [&](int j) -> us2 {   // bytes j, j+1 of the row as a u16 pair
-            const uint32_t sel = (uint32_t)(j & 3) | 0x0c00u | ((uint32_t)((j & 3) + 1) << 16) | 0x0c000000u;
-            const uint32_t r = __builtin_amdgcn_perm(w[(j >> 2) + 1], w[j >> 2], sel);
-            return *reinterpret_cast<const us2*>(&r);
+        // out(c) = [18 34 48 56] . v[c..c+3] + [48 34 18 0] . v[c+4..c+7]: two v_dot4_u32_u8 on the
+        // 4-byte windows of the row (a window at byte j is one v_alignbyte of the row's dwords)
+        auto W = [&](int j) -> uint32_t {
+            return (j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], j & 3) : w[j >> 2];
         };
-        const us2 k18 = {18, 18}, k34 = {34, 34}, k48 = {48, 48}, k56 = {56, 56};
+        const uint32_t T0 = 18u | 34u << 8 | 48u << 16 | 56u << 24, T1 = 48u | 34u << 8 | 18u << 16;
+        uint32_t* hrow = reinterpret_cast<uint32_t*>(&Hb[lane * HBS]);
 #pragma unroll
         for (int c = 0; c < HBLUR_W; c += 2) {
-            const us2 o = k18 * (P(c) + P(c + 6)) + k34 * (P(c + 1) + P(c + 5)) + k48 * (P(c + 2) + P(c + 4)) +
-                          k56 * P(c + 3);
-            *reinterpret_cast<us2*>(&Hb[lane * HBS + c]) = o;   // column HBLUR_W (c = 36's pair) is padding
+            const uint32_t o0 = __builtin_amdgcn_udot4(W(c + 4), T1, __builtin_amdgcn_udot4(W(c), T0, 0u, false), false);
+            const uint32_t o1 = __builtin_amdgcn_udot4(W(c + 5), T1, __builtin_amdgcn_udot4(W(c + 1), T0, 0u, false), false);
+            hrow[c >> 1] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);   // (o0, o1) as u16; column 37 is padding
         }
     }
     __syncthreads();
@@ -1580,13 +1581,18 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     float a, b;   // (float)::cos / ::sin((double)ang), sincos_f.h (checked on every float in range)
     sincos_f2d(ang, &b, &a);
     auto sample = [&](int idx) -> int {
-        const float x = (float)c_pattern[2 * idx], y = (float)c_pattern[2 * idx + 1];
+        const float x = c_pattern[2 * idx], y = c_pattern[2 * idx + 1];
         const int dy = (int)rintf(x * b + y * a);
         const int dx = (int)rintf(x * a - y * b);
-        const uint16_t* col = Hb + (18 + dy) * HBS + 18 + dx;
-        const unsigned acc = 18u * (col[0] + col[6 * HBS]) + 34u * (col[HBS] + col[5 * HBS]) +
-                             48u * (col[2 * HBS] + col[4 * HBS]) + 56u * col[3 * HBS];
-        return (int)((acc + (1u << 15)) >> 16);
+        const uint16_t* col = Hb + __mul24(18 + dy, HBS) + 18 + dx;
+        // vertical taps as u16 pairs (d16 / d16_hi loads) into v_dot2_u32_u16, rounding bias as the
+        // accumulator: 18 c0 + 34 c1 + 48 c2 + 56 c3 + 48 c4 + 34 c5 + 18 c6 + 2^15
+        const us2 p01 = {col[0], col[HBS]}, p23 = {col[2 * HBS], col[3 * HBS]}, p45 = {col[4 * HBS], col[5 * HBS]};
+        const us2 k01 = {18, 34}, k23 = {48, 56}, k45 = {48, 34};
+        unsigned acc = __builtin_amdgcn_udot2(p01, k01, 18u * col[6 * HBS] + (1u << 15), false);
+        acc = __builtin_amdgcn_udot2(p23, k23, acc, false);
+        acc = __builtin_amdgcn_udot2(p45, k45, acc, false);
+        return (int)(acc >> 16);
     };
     unsigned long long words[4];
 #pragma unroll
