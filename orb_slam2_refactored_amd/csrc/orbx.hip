@@ -1836,7 +1836,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.cand_frame = std::max<long long>(cand, 1);
     g.out_frame = std::max(out, 1);
     NC = (int)align_up(std::max(NC, 256), 64);   // >= blockDim: the gather reuses the node scratch
-    const int PTC = 4096;   // candidate points kept in LDS (P and T) when a level has at most this many
+    const int PTC = 2048;   // candidate points kept in LDS (P and T) when a level has at most this many (48 KiB in all: 3 WGs per CU)
     const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int)) +
                        (size_t)PTC * 8;
     if (lds > 156 * 1024) {   // gfx950: 160 KiB LDS per workgroup
