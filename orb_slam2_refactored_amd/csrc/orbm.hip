@@ -21,11 +21,13 @@ namespace orbamd {
 // to 0/1 bytes in registers and fed to v_mfma_i32_16x16x64_i8 (4 k-steps per 256 bits).  Any k
 // permutation applied identically to the A and B fragments leaves the dot product unchanged, so
 // lane l (group g = l >> 4) simply takes descriptor bytes 8g..8g+7 and k-step s their bits
-// 16s..16s+15.  Per (row, column) the lane forms key = d << 16 | j; the running best key is the
-// minimum (lowest j on equal d, as the reference's strict-< scan) and the running second key the
-// second order statistic.  Keys with d >= 256 (d == 256 and the padding columns) never displace a
-// real candidate and are mapped back to (256, -1) at the end, which is the reference's
-// bestDist = 256 / bestIdx = -1 initialisation.
+// 16s..16s+15.  A's bits are expanded to int8 0 / -2 and the accumulator starts at |b| + 256, so
+// the MFMA yields S = d - |a| + 256 directly; per (row, column) the lane forms the row-relative key
+// S << 16 | j (one v_lshl_or).  The running best key is the minimum (lowest j on equal d, as the
+// reference's strict-< scan) and the running second key the second order statistic.  After the
+// merge d = S - 256 + |a|; keys with d >= 256 (d == 256 and the padding columns) never displace a
+// real candidate and are mapped back to (256, -1), which is the reference's bestDist = 256 /
+// bestIdx = -1 initialisation.
 typedef int i4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ i4v expand16(uint32_t b) {   // bit k of b -> byte k (0 / 1)
@@ -80,14 +82,9 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
         const int row = min(row_base + 64 * w + 16 * rt + c16, nA - 1);
         const uint2 v = *reinterpret_cast<const uint2*>(Ap + (long long)row * 32 + 8 * g);
 #pragma unroll
-        for (int s2 = 0; s2 < 4; s2++) af[rt][s2] = expand16(chunk16(v, s2));
+        for (int s2 = 0; s2 < 4; s2++) af[rt][s2] = expand16(chunk16(v, s2)) * 0xfe;   // bit -> int8 0 / -2
     }
     __syncthreads();
-    uint32_t pa16[MM_RT][4];
-#pragma unroll
-    for (int rt = 0; rt < MM_RT; rt++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) pa16[rt][r] = (uint32_t)s_pa[64 * w + 16 * rt + 4 * g + r] << 16;
     uint32_t bk[MM_RT][4], sk[MM_RT][4];
 #pragma unroll
     for (int rt = 0; rt < MM_RT; rt++)
@@ -102,19 +99,23 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
         if (jn < nB) bnext = *reinterpret_cast<const uint2*>(Bp + (long long)jn * 32 + 8 * g);
         const int j = j0 + c16;
         const uint2 bv = j < nB ? bcur : make_uint2(0, 0);
-        const uint32_t cj = ((uint32_t)s_pb[j] << 16) | (uint32_t)j;
+        // the accumulator starts at |b| + 256 (one value per lane: a lane holds 4 rows of ONE
+        // column), so the MFMA yields S = |b| + 256 - 2<a, b> = d - |a| + 256 in [0, 512]: a row's
+        // ordering by (S, j) is its ordering by (d, j), and |a| is added back after the merge
+        const int pbv = s_pb[j] + 256;
+        const i4v cinit = {pbv, pbv, pbv, pbv};
         i4v bf[4];
 #pragma unroll
         for (int s2 = 0; s2 < 4; s2++) bf[s2] = expand16(chunk16(bv, s2));
 #pragma unroll
         for (int rt = 0; rt < MM_RT; rt++) {
-            i4v acc = {0, 0, 0, 0};
+            i4v acc = cinit;
 #pragma unroll
             for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[rt][s2], bf[s2], acc, 0, 0, 0);
-            const int dot[4] = {acc.x, acc.y, acc.z, acc.w};
+            const int sv[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const uint32_t key = pa16[rt][r] + cj - ((uint32_t)dot[r] << 17);   // (pa + pb - 2 dot) << 16 | j
+                const uint32_t key = ((uint32_t)sv[r] << 16) | (uint32_t)j;   // row-relative (d, j) key
                 const uint32_t hi = max(bk[rt][r], key);
                 bk[rt][r] = min(bk[rt][r], key);
                 sk[rt][r] = min(sk[rt][r], hi);
@@ -135,9 +136,11 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
             }
             const int row = row_base + 64 * w + 16 * rt + 4 * g + r;
             if (c16 == 0 && row < nA) {
-                const int bd = b1 >> 16 >= 256 ? 256 : (int)(b1 >> 16);
-                const int bi = b1 >> 16 >= 256 ? -1 : (int)(b1 & 0xffffu);
-                const int sd = s1 >> 16 >= 256 ? 256 : (int)(s1 >> 16);
+                const int pa = s_pa[64 * w + 16 * rt + 4 * g + r];
+                const int bdr = (int)(b1 >> 16) - 256 + pa, sdr = (int)(s1 >> 16) - 256 + pa;
+                const int bd = bdr >= 256 ? 256 : bdr;
+                const int bi = bdr >= 256 ? -1 : (int)(b1 & 0xffffu);
+                const int sd = sdr >= 256 ? 256 : sdr;
                 const long long o = (long long)p * strideA + row;
                 if (best_idx) best_idx[o] = bi;
                 if (best) best[o] = bd;
