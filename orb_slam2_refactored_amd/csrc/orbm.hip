@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
     const uint8_t* __restrict__ B, const int32_t* __restrict__ nB_arr, int nB_fixed, int strideB,
     const int32_t* __restrict__ pair_b, float nnratio, int th_low, int32_t* __restrict__ best_idx,
     int32_t* __restrict__ best, int32_t* __restrict__ second, int32_t* __restrict__ match) {
-    extern __shared__ int mm_sm[];   // pa[MM_ROWS] | pb[nB padded to 16]
+    extern __shared__ __attribute__((aligned(16))) int mm_sm[];   // pa[MM_ROWS] | pb[nB padded to 16] | expanded B [2][4][64]
     int* s_pa = mm_sm;
     int* s_pb = mm_sm + MM_ROWS;
     const int p = blockIdx.y;
@@ -90,15 +90,26 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
     for (int rt = 0; rt < MM_RT; rt++)
 #pragma unroll
         for (int r = 0; r < 4; r++) bk[rt][r] = sk[rt][r] = 0xffffffffu;
-    // column tiles of 16, B loads one tile ahead
-    uint2 bnext = make_uint2(0, 0);
-    if (c16 < nB) bnext = *reinterpret_cast<const uint2*>(Bp + (long long)c16 * 32 + 8 * g);
-    for (int j0 = 0; j0 < nB; j0 += 16) {
-        const uint2 bcur = bnext;
-        const int jn = j0 + 16 + c16;
-        if (jn < nB) bnext = *reinterpret_cast<const uint2*>(Bp + (long long)jn * 32 + 8 * g);
+    // Column tiles of 16.  The 0/1 byte expansion of a B tile is shared by the 4 wavefronts (all of
+    // them need the same 16 columns): wavefront w expands k-step w of tile t+1 into an LDS double
+    // buffer while tile t is consumed, one barrier per tile.  Raw B bits load two tiles ahead.
+    i4v* xb = reinterpret_cast<i4v*>(mm_sm + ((MM_ROWS + nBt + 16 + 3) & ~3));   // [2][4][64]
+    auto ldb = [&](int jj) -> uint2 {
+        return jj < nB ? *reinterpret_cast<const uint2*>(Bp + (long long)jj * 32 + 8 * g) : make_uint2(0, 0);
+    };
+    {
+        const uint2 b0 = ldb(c16);
+        xb[w * 64 + lane] = expand16(chunk16(b0, w));
+    }
+    uint2 bnext = ldb(16 + c16);
+    __syncthreads();
+    for (int j0 = 0, t = 0; j0 < nB; j0 += 16, t++) {
+        const int cur = t & 1;
+        if (j0 + 16 < nB) {   // block-uniform
+            xb[((cur ^ 1) * 4 + w) * 64 + lane] = expand16(chunk16(bnext, w));
+            bnext = ldb(j0 + 32 + c16);
+        }
         const int j = j0 + c16;
-        const uint2 bv = j < nB ? bcur : make_uint2(0, 0);
         // the accumulator starts at |b| + 256 (one value per lane: a lane holds 4 rows of ONE
         // column), so the MFMA yields S = |b| + 256 - 2<a, b> = d - |a| + 256 in [0, 512]: a row's
         // ordering by (S, j) is its ordering by (d, j), and |a| is added back after the merge
@@ -106,7 +117,7 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
         const i4v cinit = {pbv, pbv, pbv, pbv};
         i4v bf[4];
 #pragma unroll
-        for (int s2 = 0; s2 < 4; s2++) bf[s2] = expand16(chunk16(bv, s2));
+        for (int s2 = 0; s2 < 4; s2++) bf[s2] = xb[(cur * 4 + s2) * 64 + lane];
 #pragma unroll
         for (int rt = 0; rt < MM_RT; rt++) {
             i4v acc = cinit;
@@ -121,6 +132,7 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
                 sk[rt][r] = min(sk[rt][r], hi);
             }
         }
+        __syncthreads();   // tile t+1 expanded; buffer `cur` free for tile t+2
     }
     // merge the 16 column classes of each row (lanes with the same g)
 #pragma unroll
@@ -154,7 +166,7 @@ static void launch_top2(const uint8_t* A, const int32_t* nA_arr, int nA_fixed, i
                         const int32_t* nB_arr, int nB_fixed, int strideB, const int32_t* pair_b, int n_pairs,
                         float nnratio, int th_low, int32_t* bi, int32_t* bd, int32_t* sd, int32_t* mt,
                         hipStream_t st) {
-    const size_t lds = (size_t)(MM_ROWS + ((strideB + 15) & ~15) + 16) * sizeof(int);
+    const size_t lds = (size_t)(((MM_ROWS + ((strideB + 15) & ~15) + 16 + 3) & ~3) + 2 * 4 * 64 * 4) * sizeof(int);
     hipLaunchKernelGGL(hamming_top2_mfma_kernel, dim3((unsigned)((strideA + MM_ROWS - 1) / MM_ROWS), (unsigned)n_pairs),
                        dim3(256), lds, st, A, nA_arr, nA_fixed, strideA, B, nB_arr, nB_fixed, strideB, pair_b,
                        nnratio, th_low, bi, bd, sd, mt);
