@@ -39,6 +39,12 @@ __device__ __forceinline__ i4v expand16(uint32_t b) {   // bit k of b -> byte k 
     return r;
 }
 
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t chunk16(uint2 v, int s) {
     return ((s < 2 ? v.x : v.y) >> (16 * (s & 1))) & 0xffffu;
 }
@@ -127,9 +133,10 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const uint32_t key = ((uint32_t)sv[r] << 16) | (uint32_t)j;   // row-relative (d, j) key
-                const uint32_t hi = max(bk[rt][r], key);
+                // bk <= sk always, so the new second order statistic min(sk, max(bk, key)) is the
+                // median of the three
+                sk[rt][r] = umed3(bk[rt][r], key, sk[rt][r]);
                 bk[rt][r] = min(bk[rt][r], key);
-                sk[rt][r] = min(sk[rt][r], hi);
             }
         }
         __syncthreads();   // tile t+1 expanded; buffer `cur` free for tile t+2
