@@ -1651,7 +1651,7 @@ struct orbx_extractor {
     size_t qt_lds = 0;
     FastLds fl;
     size_t fast_lds = 0;
-    int fast_cpw = 1;   // FAST cells per wavefront
+    int fast_cpw = 4;   // FAST cells per wavefront (1 -> 4: -3 % at C2; ORBX_FAST_CPW)
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
