@@ -838,6 +838,30 @@ __device__ int4 qt_wave_split(const QtNode& n, const uint32_t* __restrict__ P, u
     return make_int4(c[0], c[1], c[2], c[3]);
 }
 
+// A 16-lane group splits one node of at most 16 points (group = lane >> 4): the same stable 4-way
+// scatter as qt_wave_split with the ballots cut to the group's 16 bits.  Every lane of the
+// wavefront must call it (ballots); lanes of a group without a node pass cnt = 0.
+template <bool SCATTER = true>
+__device__ int4 qt_group16_split(const QtNode& n, int cnt, const uint32_t* __restrict__ P, uint32_t* __restrict__ T) {
+    const int lane = lane_id(), sh = lane & 48, gl = lane & 15;
+    const unsigned lt16 = (1u << gl) - 1u;
+    const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
+    const int ym = n.tly + (n.bry - n.tly + 1) / 2;
+    int q = -1;
+    uint32_t k = 0;
+    if (gl < cnt) {
+        k = P[n.beg + gl];
+        q = kp_x(k) < xm ? (kp_y(k) < ym ? 0 : 2) : (kp_y(k) < ym ? 1 : 3);
+    }
+    unsigned m[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) m[qq] = (unsigned)(__ballot(q == qq) >> sh) & 0xffffu;
+    const int c0 = __popc(m[0]), c1 = __popc(m[1]), c2 = __popc(m[2]), c3 = __popc(m[3]);
+    const int o[4] = {n.beg, n.beg + c0, n.beg + c0 + c1, n.beg + c0 + c1 + c2};
+    if (SCATTER && q >= 0) T[o[q] + __popc(m[q] & lt16)] = k;
+    return make_int4(c0, c1, c2, c3);
+}
+
 // Child counts of one node by a single thread (phase 2 only needs the counts of every divisible
 // node to find where to stop; only the processed prefix is then split for real).
 __device__ __forceinline__ int4 qt_thread_count(const QtNode& n, const uint32_t* __restrict__ P) {
@@ -854,22 +878,6 @@ __device__ __forceinline__ int4 qt_thread_count(const QtNode& n, const uint32_t*
     }
     return make_int4(c0, c1, c2, c3);
 }
-
-// Stable 4-way scatter of one small node by a single thread, child counts known.
-__device__ __forceinline__ void qt_thread_split(const QtNode& n, int4 cnt, const uint32_t* __restrict__ P,
-                                                uint32_t* __restrict__ T) {
-    const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
-    const int ym = n.tly + (n.bry - n.tly + 1) / 2;
-    int o0 = n.beg, o1 = o0 + cnt.x, o2 = o1 + cnt.y, o3 = o2 + cnt.z;
-    for (int j = 0; j < n.cnt; j++) {
-        const uint32_t k = P[n.beg + j];
-        const bool r = kp_x(k) >= xm, d = kp_y(k) >= ym;
-        const int dst = d ? (r ? o3++ : o2++) : (r ? o1++ : o0++);
-        T[dst] = k;
-    }
-}
-
-constexpr int QT_THREAD_SPLIT_MAX = 48;   // nodes up to this many points are split by one thread
 
 __device__ __forceinline__ int ne4(int4 c) { return (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0); }
 __device__ __forceinline__ int dv4(int4 c) { return (c.x > 1) + (c.y > 1) + (c.z > 1) + (c.w > 1); }
@@ -1252,7 +1260,20 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                 kdiv += tot;
             }
             __syncthreads();
+            // nodes of <= 16 points: four per wavefront (16-lane groups); larger: one wavefront each
+            for (int b = 4 * w; b < kdiv; b += 4 * nw) {   // wave-uniform trip count
+                const int j = b + (lane_id() >> 4);
+                QtNode nd{};
+                int cnt = 0;
+                if (j < kdiv) {
+                    nd = na[ia[j]];
+                    cnt = nd.cnt <= 16 ? nd.cnt : 0;
+                }
+                const int4 c = qt_group16_split(nd, cnt, P, T);
+                if (cnt > 0 && (lane_id() & 15) == 0) cc[j] = c;
+            }
             for (int j = w; j < kdiv; j += nw) {
+                if (na[ia[j]].cnt <= 16) continue;   // wave-uniform
                 const int4 c = qt_wave_split(na[ia[j]], P, T);
                 if (lane_id() == 0) cc[j] = c;
             }
@@ -1334,10 +1355,18 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             QT_STAMP(42 + 4 * min(p2_round, 5));
             for (int j = threadIdx.x; j < proc; j += blockDim.x) ia[prev[j].node] = 1;
             // split the processed prefix only: small nodes one thread each, large ones one wave each
-            for (int j = threadIdx.x; j < proc; j += blockDim.x)
-                if (na[prev[j].node].cnt <= QT_THREAD_SPLIT_MAX) qt_thread_split(na[prev[j].node], cc[j], P, T);
+            for (int b = 4 * w; b < proc; b += 4 * nw) {   // <= 16 points: 16-lane groups
+                const int j = b + (lane_id() >> 4);
+                QtNode nd{};
+                int cnt = 0;
+                if (j < proc) {
+                    nd = na[prev[j].node];
+                    cnt = nd.cnt <= 16 ? nd.cnt : 0;
+                }
+                (void)qt_group16_split(nd, cnt, P, T);
+            }
             for (int j = w; j < proc; j += nw)
-                if (na[prev[j].node].cnt > QT_THREAD_SPLIT_MAX) (void)qt_wave_split(na[prev[j].node], P, T);
+                if (na[prev[j].node].cnt > 16) (void)qt_wave_split(na[prev[j].node], P, T);
             __syncthreads();
             int ne_total = 0;
             {
