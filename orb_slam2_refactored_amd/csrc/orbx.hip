@@ -1089,36 +1089,67 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
 #endif
     // ---- gather candidates in cell raster order (DetectFAST push_back order).  Pass 1: total count;
     //      the arrays live in LDS when they fit.  Pass 2: one lane per cell copies its points.
-    int n_total = 0;
-    {
-        int part = 0;
-        for (int i = threadIdx.x; i < L.ncells; i += blockDim.x) part += ccell[i];
-        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-        if (lane_id() == 0) tmp[8 + w] = part;
-        __syncthreads();
-        for (int q = 0; q < nw; q++) n_total += tmp[8 + q];
-        __syncthreads();
-    }
-    if (n_total <= PTC) { P = lds_P; T = lds_T; }
-    int carry = 0;
-    for (int b = 0; b < L.ncells; b += blockDim.x) {
-        const int i = b + threadIdx.x;
-        const int v = i < L.ncells ? ccell[i] : 0;
-        int tot;
-        const int ex = block_excl_scan(v, tmp, &tot);
-        if (v > 0) {
-            const uint32_t* __restrict__ src = fslots + cells[L.cell_base + i].slot;
-            uint32_t* dst = P + carry + ex;
-            for (int j0 = 0; j0 < v; j0 += 8) {
-                uint32_t r[8];
+    int n_total = 0, carry = 0;
+    if (L.ncells <= 4 * (int)blockDim.x) {
+        // thread t owns cells 4t .. 4t+3 (raster order): their counts and slot offsets are loaded
+        // together, one block reduction picks LDS or global candidate arrays, one block scan places
+        // the threads' runs, and every thread's first 8 points per cell are loaded in one batch
+        const int i0 = 4 * threadIdx.x;
+        int cv[4], cs[4];
 #pragma unroll
-                for (int q = 0; q < 8; q++) r[q] = j0 + q < v ? src[j0 + q] : 0;
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (j0 + q < v) dst[j0 + q] = r[q];
-            }
+        for (int k = 0; k < 4; k++) {
+            const int i = i0 + k;
+            cv[k] = i < L.ncells ? ccell[i] : 0;
+            cs[k] = i < L.ncells ? cells[L.cell_base + i].slot : 0;
         }
-        carry += tot;
+        const int sum = cv[0] + cv[1] + cv[2] + cv[3];
+        const int ex = block_excl_scan(sum, tmp, &n_total);
+        if (n_total <= PTC) { P = lds_P; T = lds_T; }
+        uint32_t r[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[k][q] = q < cv[k] ? fslots[cs[k] + q] : 0u;
+        int o = ex;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (q < cv[k]) P[o + q] = r[k][q];
+            for (int q = 8; q < cv[k]; q++) P[o + q] = fslots[cs[k] + q];   // rare: > 8 points in a cell
+            o += cv[k];
+        }
+        carry = n_total;
+    } else {
+        {
+            int part = 0;
+            for (int i = threadIdx.x; i < L.ncells; i += blockDim.x) part += ccell[i];
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            if (lane_id() == 0) tmp[8 + w] = part;
+            __syncthreads();
+            for (int q = 0; q < nw; q++) n_total += tmp[8 + q];
+            __syncthreads();
+        }
+        if (n_total <= PTC) { P = lds_P; T = lds_T; }
+        for (int b = 0; b < L.ncells; b += blockDim.x) {
+            const int i = b + threadIdx.x;
+            const int v = i < L.ncells ? ccell[i] : 0;
+            int tot;
+            const int ex = block_excl_scan(v, tmp, &tot);
+            if (v > 0) {
+                const uint32_t* __restrict__ src = fslots + cells[L.cell_base + i].slot;
+                uint32_t* dst = P + carry + ex;
+                for (int j0 = 0; j0 < v; j0 += 8) {
+                    uint32_t r[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) r[q] = j0 + q < v ? src[j0 + q] : 0;
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (j0 + q < v) dst[j0 + q] = r[q];
+                }
+            }
+            carry += tot;
+        }
     }
     __syncthreads();
     const int n_src = carry;
@@ -1150,6 +1181,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
         for (int r = 0; r < R; r++) counts[r] = 0;
 #pragma unroll
         for (int t = 0; t < QT_RPL; t++) {
+            if (q0 + 64 * t >= q1) { rid[t] = -1; continue; }   // wave-uniform: past this quarter
             const int j = q0 + 64 * t + lane_id();
             int r = -1;
             if (j < q1) {
@@ -1183,6 +1215,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
         }
 #pragma unroll
         for (int t = 0; t < QT_RPL; t++) {
+            if (q0 + 64 * t >= q1) continue;   // wave-uniform
             const int j = q0 + 64 * t + lane_id();
             const uint32_t k = j < q1 ? P[j] : 0;
             const int r = rid[t];
