@@ -112,6 +112,19 @@ __device__ __forceinline__ int xcd_swizzle(int b, int nb) {
     return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
 
+// Sum of an int over the 64 lanes, wave-uniform result: DPP within each row of 16 (quad xor 1, xor 2,
+// row rotate 4, 8), then the four row sums by v_readlane.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false); }
+__device__ __forceinline__ int wave_sum_i32(int v) {
+    v += dpp_i32<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_i32<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_i32<0x124>(v);   // row_ror:4
+    v += dpp_i32<0x128>(v);   // row_ror:8
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Wave-inclusive scan of ints (64 lanes).
@@ -1517,6 +1530,17 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 
 constexpr int RS = 44;   // LDS raw-patch row stride
 
+#ifdef ORB_DESC_STAMPS
+// diagnostic build: phase stamps of every 16th describe wavefront (8 words each)
+__device__ unsigned long long g_desc_stamps[1024 * 8];
+#define DESC_STAMP(k)                                                                              \
+    do {                                                                                           \
+        if (lane == 0 && (lb & 15) == 0 && (lb >> 4) < 1024) g_desc_stamps[(lb >> 4) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define DESC_STAMP(k) do {} while (0)
+#endif
+
 // One workgroup = one wavefront = one kept keypoint.
 constexpr int DESC_KPW = 1;                               // keypoints per wavefront
 constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords per raw-patch row (RS = 4 * 11)
@@ -1549,6 +1573,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     }
     const LevelDev& L = g.lv[l];
     const int s = L.out_base + (oidx - lbase);
+    DESC_STAMP(0);
 
     const uint32_t k = sel[(long long)f * g.out_frame + s];
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
@@ -1590,30 +1615,39 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         for (int r = 0; r < PATCH; r++) R[r * RS + lane] = v[r];
     }
     __syncthreads();
+    DESC_STAMP(1);
 
     // IC_Angle on the unblurred level, patch centre (21, 21).  Lane = (row parity, u + 15): lanes
     // 0-31 take rows +-v for odd v, lanes 32-63 for v + 1, so the 15 row pairs take 8 steps.
     int m10 = 0, m01 = 0;
     {
         const int hv = lane >> 5, u = (lane & 31) - 15;   // u = 16 on lanes 31 / 63: outside every umax
-        if (hv == 0 && u <= 15) m10 = u * R[21 * RS + 21 + u];
         const uint8_t* cp = R + 21 * RS + 21 + u + hv * RS;
+        // every read unconditional (all inside the 43x43 patch) and issued together; the disk mask
+        // is applied to the products
+        int vp[8], vm[8];
 #pragma unroll
-        for (int vv = 1; vv <= 15; vv += 2) {
+        for (int t = 0; t < 8; t++) {
+            const int vv = 2 * t + 1;
+            vp[t] = cp[vv * RS];
+            vm[t] = cp[-(vv + 2 * hv) * RS];
+        }
+        const int c0 = R[21 * RS + 21 + u];
+        m10 = (hv == 0 && u <= 15) ? u * c0 : 0;
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int vv = 2 * t + 1;
             const int v = vv + hv;
             const int um = hv ? (vv + 1 <= 15 ? c_umax_h[vv + 1] : -1) : c_umax_h[vv];
-            if (u >= -um && u <= um) {
-                const int vp = cp[vv * RS], vm = cp[-(vv + 2 * hv) * RS];
-                m01 += v * (vp - vm);
-                m10 += u * (vp + vm);
-            }
+            const bool in = u >= -um && u <= um;
+            m01 += in ? v * (vp[t] - vm[t]) : 0;
+            m10 += in ? u * (vp[t] + vm[t]) : 0;
         }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        m10 += __shfl_xor(m10, o, 64);
-        m01 += __shfl_xor(m01, o, 64);
-    }
+    m10 = wave_sum_i32(m10);
+    m01 = wave_sum_i32(m01);
     const float angle = fast_atan2_dev((float)m01, (float)m10);
+    DESC_STAMP(2);
 
     // horizontal Q8 blur, one row per lane, two columns per packed-u16 op: P(j) = (v[j], v[j+1]) is
     // one v_perm of the row's dwords, and 18(P0+P6) + 34(P1+P5) + 48(P2+P4) + 56 P3 <= 65280 fits u16.
@@ -1641,7 +1675,9 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
     float a, b;   // (float)::cos / ::sin((double)ang), sincos_f.h (checked on every float in range)
+    DESC_STAMP(3);
     sincos_f2d(ang, &b, &a);
+    DESC_STAMP(4);
     auto sample = [&](int idx) -> int {
         const float x = c_pattern[2 * idx], y = c_pattern[2 * idx + 1];
         const int dy = (int)rintf(x * b + y * a);
@@ -1662,6 +1698,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         const int p = r * 64 + lane;
         words[r] = __ballot(sample(2 * p) < sample(2 * p + 1));
     }
+    DESC_STAMP(5);
     const long long o = (long long)f * cap + oidx;
     if (lane < 4) {
         const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
@@ -1680,6 +1717,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         }
         reinterpret_cast<float*>(kps + o)[lane] = fv;
     }
+    DESC_STAMP(6);
     __syncthreads();   // R / Hb are rewritten by the next keypoint
     }   // keypoints of this wavefront
 }
@@ -2439,7 +2477,11 @@ int orbx_debug_fast_stamps(unsigned long long* out, int n_words) {
 }
 
 int orbx_debug_qt_stamps(unsigned long long* out) {
-#ifdef ORB_QT_STAMPS
+#if defined(ORB_DESC_STAMPS)
+    ORB_HIP_TRY(hipDeviceSynchronize());
+    ORB_HIP_TRY(hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_desc_stamps), 1024 * 8 * 8));
+    return ORB_OK;
+#elif defined(ORB_QT_STAMPS)
     ORB_HIP_TRY(hipDeviceSynchronize());
     ORB_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_stamps), 64 * 8));
     ORB_HIP_TRY(hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_qt_wg), 4096 * 2 * 8));

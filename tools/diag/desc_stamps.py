@@ -1,0 +1,32 @@
+"""Diagnostic: describe_kernel phase stamps (every 16th wavefront) with the ORB_DESC_STAMPS build."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+os.environ["ORBSLAM2_AMD_LIB"] = str(ROOT / "tools" / "diag" / "liborbslam2_amd_descstamps.so")
+sys.path.insert(0, str(ROOT))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from orb_slam2_refactored_amd import ORBextractor  # noqa: E402
+from orb_slam2_refactored_amd._lib import lib  # noqa: E402
+from orb_slam2_refactored_amd.synth import synth_image  # noqa: E402
+
+F = 128
+frames = torch.from_numpy(np.stack([synth_image(i % 16, 1280, 720) for i in range(F)])).cuda()
+ex = ORBextractor(ORBextractor.Parameters(nfeatures=2000))
+for _ in range(3):
+    ex.extract_batch_device(frames)
+torch.cuda.synchronize()
+buf = (C.c_ulonglong * (64 + 8192))()
+lib().orbx_debug_qt_stamps.argtypes = [C.c_void_p]
+assert lib().orbx_debug_qt_stamps(C.cast(buf, C.c_void_p)) == 0
+st = np.array(list(buf)[64:], dtype=np.int64).reshape(1024, 8)
+st = st[(st[:, 0] > 0) & (st[:, 6] > 0)]
+d = np.diff(st[:, :7], axis=1)
+names = ["patch load+stage", "IC angle+atan", "H blur", "sincos", "samples+ballots", "stores"]
+print(f"{len(st)} sampled wavefronts; median ticks per phase:")
+for i, n in enumerate(names):
+    print(f"  {n:18s} {int(np.median(d[:, i])):8d}  (p90 {int(np.percentile(d[:, i], 90))})")
+print("  total", int(np.median(st[:, 6] - st[:, 0])))
