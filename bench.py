@@ -316,7 +316,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ex.profile(True)
+    # inside the timed region only the dominant kernel (fast_cells) carries launch events (events on
+    # every kernel cost ~3.5 % of the step); the other stages are timed in a separate pass below
+    ex.profile(True, stages=["fast_cells"])
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -331,7 +333,15 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ex.profile(False)
-    stages = ex.profile_read()
+    timed = ex.profile_read()
+    # per-stage breakdown: a separate short pass with events on every kernel (not the timed region)
+    ex.profile(True)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    ex.profile(False)
+    breakdown = ex.profile_read()
+    brk_steps = 3
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -351,17 +361,22 @@ def main():
         "quadtree": 0,
         "describe": 60 * n_kp,      # keypoint + descriptor writes (neighbourhood reads are L2 re-reads)
     }
-    dom = max(stages, key=lambda k: stages[k][0])
-    traffic = measured_traffic(dom, stages[dom][1] / max(args.steps, 1), B, W, H, args.nfeatures)
-    dom_ms, dom_launches = stages[dom]
+    dom = max(breakdown, key=lambda k: breakdown[k][0])
+    if dom == "fast_cells":   # the live launch times of the timed region
+        dom_ms, dom_launches = timed[dom]
+        dom_steps = args.steps
+    else:                     # another stage dominates: its times from the breakdown pass
+        dom_ms, dom_launches = breakdown[dom]
+        dom_steps = brk_steps
+    traffic = measured_traffic(dom, dom_launches / max(dom_steps, 1), B, W, H, args.nfeatures)
     per_launch_ms = dom_ms / max(dom_launches, 1)
-    launches_per_step = dom_launches / max(args.steps, 1)
+    launches_per_step = dom_launches / max(dom_steps, 1)
     # a stage may run as several launches per step (fast_cells: level 0 on the side stream, levels
     # 1..7 on the main stream): achieved = the step's algorithmic bytes / the step's summed launch
     # durations, i.e. per launch = bytes / launches_per_step over the average launch duration
     dom_bytes = stage_bytes[dom] * B / max(launches_per_step, 1)
     achieved = dom_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
-    extract_ms = sum(v[0] for v in stages.values()) / max(args.steps, 1)
+    extract_ms = sum(v[0] for v in breakdown.values()) / brk_steps
     pipeline_gbs = bytes_frame * B / (extract_ms * 1e-3) / 1e9 if extract_ms > 0 else 0.0
 
     result = {
@@ -386,7 +401,9 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": per_launch_ms,
                      "launches_per_step": launches_per_step,
-                     "stage_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
+                     "timed_from": "timed region" if dom == "fast_cells" else "breakdown pass",
+                     "stage_ms_per_step": {k: v[0] / brk_steps for k, v in breakdown.items()},
+                     "stage_ms_source": "separate 3-step pass with launch events on every kernel",
                      "pipeline_algorithmic_GBs": pipeline_gbs, "pipeline_bytes_per_frame": bytes_frame},
         "keypoints_per_frame": n_kp,
         "matches_last_step": matches,

@@ -346,9 +346,11 @@ int orbba_pose_optimization_device(const orbba_pose_batch* in, orbba_pose_result
 const char* orb_last_error(void);
 int orb_device_count(void);
 
-/* Stage timing with HIP events recorded on the launch stream around each stage
- * (0 pyramid, 1 FAST cells, 2 quadtree, 3 describe).  enable != 0 starts recording; read
- * synchronises, returns the summed milliseconds and launch count per stage, and resets. */
+/* Stage timing with HIP events recorded as part of each kernel's dispatch (hipExtLaunchKernel start /
+ * stop events: the kernel's own duration) for the stages 0 pyramid, 1 FAST cells, 2 quadtree,
+ * 3 describe.  enable > 0 times every stage, enable < 0 only the stages in the bitmask -enable
+ * (e.g. -2: FAST cells only), 0 stops; read synchronises, returns the summed milliseconds and
+ * launch count per stage, and resets. */
 #define ORBX_NSTAGES 4
 int orbx_profile_enable(orbx_extractor* h, int enable);
 int orbx_profile_read(orbx_extractor* h, double* ms, int32_t* launches);

@@ -1770,7 +1770,7 @@ struct orbx_extractor {
     DevBuf d_img, d_kps, d_desc, d_counts;
     DevBuf d_stereo_sad;   // stereo scratch (orbx_stereo_matches_batch_device)
     // stage profiling (events on the launch stream)
-    bool prof = false;
+    int prof = 0;   // bit k: time stage k's launches (orbx_profile_enable)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev[4];
     std::vector<hipEvent_t> ev_pool;
     // last batch (for GetImagePyramid)
@@ -2018,7 +2018,7 @@ constexpr int ORBX_MIN_SUB_FRAMES = 16;
 template <typename... KArgs, typename... Args>
 static void launch_timed(orbx_extractor* h, int stage, void (*kernel)(KArgs...), dim3 grid, dim3 block,
                          uint32_t shmem, hipStream_t s, Args... args) {
-    if (h->prof) {
+    if (h->prof & (1 << stage)) {
         hipEvent_t a = prof_event(h), b = prof_event(h);
         hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, static_cast<KArgs>(args)...);
         h->prof_ev[stage].push_back({a, b});
@@ -2368,7 +2368,8 @@ int orbx_debug_level_selected(const orbx_extractor* h, int frame, int level, uin
 int orbx_profile_enable(orbx_extractor* h, int enable) {
     ORB_CHECK_ARG(h, "null extractor");
     std::lock_guard<std::mutex> lk(h->mu);
-    h->prof = enable != 0;
+    h->prof = enable > 0 ? 0xf : (-enable) & 0xf;   // > 0: every stage; < 0: the stages of bitmask -enable
+
     return ORB_OK;
 }
 

@@ -109,8 +109,12 @@ class ORBextractor:
 
     STAGES = ("pyramid", "fast_cells", "quadtree", "describe")
 
-    def profile(self, enable: bool = True):
-        check(lib().orbx_profile_enable(self._h, int(enable)), "orbx_profile_enable")
+    def profile(self, enable: bool = True, stages=None):
+        """Per-kernel event timing of every stage, or only of `stages` (names of STAGES)."""
+        mode = int(bool(enable))
+        if enable and stages is not None:
+            mode = -sum(1 << self.STAGES.index(s) for s in stages)
+        check(lib().orbx_profile_enable(self._h, mode), "orbx_profile_enable")
 
     def profile_read(self):
         """{stage: (total_ms, launches)} since the last read (HIP events on the launch stream)."""
