@@ -452,6 +452,7 @@ __device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
 //   5. emit the iniThFAST set, or the minThFAST set when it is empty (DetectFAST :527-530)
 constexpr int FQ_RING = 512;   // pre-test passer ring (power of two, >= 64 + 256)
 constexpr int FQ2_RING = 128;  // diagonal-filter passer ring (power of two, >= 64 + 64)
+constexpr int FAST_CLIST_CAP = 256;   // ordered corner list (cells with more take the zone-scan NMS)
 
 struct FastLds {
     int CS, ZS, crop_bytes, mz_bytes, qcap, ccap;
@@ -675,7 +676,8 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         const bool c = M > tlo;
         const unsigned long long bm = __ballot(c);
         if (c) {
-            clist[nc + popc64(bm & lt)] = (short)i;
+            const int pos = nc + popc64(bm & lt);
+            if (pos < fl.ccap) clist[pos] = (short)i;   // past ccap: the cell takes the zone-scan NMS below
             Mc[__mul24(i >> 8, ZSd) + (i & 255)] = (uint8_t)min(M, 255);
         }
         nc += popc64(bm);
@@ -735,7 +737,52 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     if (q2n > h2) strength(q2n - h2);
     wave_lds_sync();
 
-    int n_ini = 0, n_min = 0;
+    uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
+    const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
+    int n_ini = 0, n_min = 0, total = 0;
+    if (nc > fl.ccap) {
+        // Dense cell (more corners than the list holds, e.g. pure noise): NMS over the zone map in
+        // row-major order, one zone row per pass (zw <= 64), the same keep rule: a corner is kept
+        // at threshold t iff M > t and every neighbour is < M (for M > t, a neighbour q >= M is
+        // also > t), so both thresholds share the neighbourhood maximum.
+        auto keep = [&](int y, bool& ki, bool& km) {
+            ki = km = false;
+            if (lane < zw) {
+                const uint8_t* c0 = Mc + __mul24(y, ZSd) + lane;
+                const int m = c0[0];
+                if (m) {
+                    int nmax = 0;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; dx++)
+                            if (dx || dy) nmax = max(nmax, (int)c0[dy * ZSd + dx]);
+                    ki = m > th_ini && nmax < m;
+                    km = m > th_min && nmax < m;
+                }
+            }
+        };
+        for (int y = 0; y < zh; y++) {
+            bool ki, km;
+            keep(y, ki, km);
+            n_ini += popc64(__ballot(ki));
+            n_min += popc64(__ballot(km));
+        }
+        const int which = n_ini > 0 ? 0 : 1;
+        total = which == 0 ? n_ini : n_min;
+        int running = 0;
+        for (int y = 0; y < zh; y++) {
+            bool ki, km;
+            keep(y, ki, km);
+            const bool k = which == 0 ? ki : km;
+            const unsigned long long bm = __ballot(k);
+            const int r = running + popc64(bm & lt);
+            if (k && r < cap)
+                out[r] = (uint32_t)(x0 + 3 + lane) | ((uint32_t)(y0 + 3 + y) << 12) |
+                         ((uint32_t)(Mc[__mul24(y, ZSd) + lane] - 1) << 24);
+            running += popc64(bm);
+        }
+    } else {
     for (int jb = 0, ch2 = 0; jb < nc; jb += 64, ch2++) {
         const int j = jb + lane;
         bool ki = false, km = false;
@@ -764,9 +811,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     wave_lds_sync();
 
     const int which = n_ini > 0 ? 0 : 1;
-    const int total = which == 0 ? n_ini : n_min;
-    uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
-    const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
+    total = which == 0 ? n_ini : n_min;
     int running = 0;
     for (int jb = 0, ch2 = 0; jb < nc; jb += 64, ch2++) {
         const unsigned long long bm = bal[2 * ch2 + which];
@@ -781,6 +826,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         }
         running += popc64(bm);
     }
+    }   // list NMS
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
         cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap);
@@ -1968,7 +2014,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6 + FAST_CROP_SLACK), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
         fl.qcap = FQ_RING + FQ2_RING;
-        fl.ccap = (int)align_up((size_t)mzw * mzh, 8);
+        fl.ccap = std::min(FAST_CLIST_CAP, (int)align_up((size_t)mzw * mzh, 8));
         const int nbal = (fl.ccap + 63) / 64;
         h->fast_lds = (size_t)fl.crop_bytes + fl.mz_bytes + 2 * (size_t)(fl.qcap + fl.ccap) + 16 * (size_t)nbal;
         h->fl = fl;

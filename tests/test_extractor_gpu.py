@@ -48,6 +48,29 @@ def test_fast_candidates_per_level(oracle, W, H, seed):
         assert np.array_equal(got, exp), l
 
 
+@pytest.mark.parametrize("kind", ["noise", "smooth_noise", "mixed"])
+def test_fast_candidates_dense_cells(oracle, kind):
+    """Cells with more corners than the ordered corner list holds (FAST_CLIST_CAP = 256) take the
+    zone-scan NMS; mixed images put dense and sparse cells side by side, ini / min thresholds low."""
+    rng = np.random.default_rng({"noise": 1, "smooth_noise": 2, "mixed": 3}[kind])
+    if kind == "noise":
+        img = rng.integers(0, 256, (480, 640)).astype(np.uint8)
+    elif kind == "smooth_noise":
+        img = np.clip(128 + rng.normal(0, 12, (480, 640)), 0, 255).astype(np.uint8)
+    else:
+        img = synth_image(21, 640, 480)
+        img[100:300, 200:500] = rng.integers(0, 256, (200, 300)).astype(np.uint8)
+    for ini, mn in [(20, 7), (5, 2)]:
+        ex = make(1000, ini, mn)
+        ex.Extract(img)
+        p = oracle.params(1000, ini=ini, mn=mn)
+        lv = oracle.pyramid(p, img)
+        for l in range(8):
+            got = ex.debug_level(l, stage="candidates")
+            exp = oracle.detect_fast(lv[l], ini, mn).astype(np.int32)
+            assert np.array_equal(got, exp), (kind, ini, mn, l, got.shape, exp.shape)
+
+
 @pytest.mark.parametrize("W,H,seed,nf", [(640, 480, 0, 1000), (1280, 720, 3, 2000), (640, 480, 9, 5000)])
 def test_quadtree_per_level(oracle, W, H, seed, nf):
     img = synth_image(seed, W, H)
