@@ -127,14 +127,16 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Wave-inclusive scan of ints (64 lanes).
+// Wave-inclusive scan of ints (64 lanes) on DPP: Hillis-Steele inside each row of 16 (row_shr 1, 2,
+// 4, 8 with zero fill), then row 1 / 3 add lane 15 of the row before (row_bcast:15) and rows 2 / 3
+// add lane 31 (row_bcast:31).  No LDS round trips (a ds_bpermute scan costs six).
 __device__ __forceinline__ int wave_incl_scan(int v) {
-    const int l = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int t = __shfl_up(v, o, 64);
-        if (l >= o) v += t;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
