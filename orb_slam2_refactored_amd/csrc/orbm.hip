@@ -147,12 +147,20 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             uint32_t b1 = bk[rt][r], s1 = sk[rt][r];
-#pragma unroll
-            for (int m = 1; m < 16; m <<= 1) {
-                const uint32_t b2 = (uint32_t)__shfl_xor((int)b1, m, 64), s2v = (uint32_t)__shfl_xor((int)s1, m, 64);
+            // top-2 merge is associative and commutative, so the 16 lanes of a row combine in any
+            // tree: DPP quad_perm [1,0,3,2], [2,3,0,1], then row_ror 4 and 8
+            auto merge = [&](uint32_t b2, uint32_t s2v) {
                 s1 = min(min(s1, s2v), max(b1, b2));
                 b1 = min(b1, b2);
-            }
+            };
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0xB1, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xf, 0xf, false));
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0x4E, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x4E, 0xf, 0xf, false));
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0x124, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x124, 0xf, 0xf, false));
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0x128, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x128, 0xf, 0xf, false));
             const int row = row_base + 64 * w + 16 * rt + 4 * g + r;
             if (c16 == 0 && row < nA) {
                 const int pa = s_pa[64 * w + 16 * rt + 4 * g + r];

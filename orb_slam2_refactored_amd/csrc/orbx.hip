@@ -1185,7 +1185,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
         {
             int part = 0;
             for (int i = threadIdx.x; i < L.ncells; i += blockDim.x) part += ccell[i];
-            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            part = wave_sum_i32(part);
             if (lane_id() == 0) tmp[8 + w] = part;
             __syncthreads();
             for (int q = 0; q < nw; q++) n_total += tmp[8 + q];
@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             {
                 int part = 0;
                 for (int j = threadIdx.x; j < kdiv; j += blockDim.x) part += ne4(cc[j]);
-                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+                part = wave_sum_i32(part);
                 if (lane_id() == 0) tmp[8 + w] = part;
                 __syncthreads();
                 for (int q = 0; q < nw; q++) ne_total += tmp[8 + q];
@@ -1466,7 +1466,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             {
                 int part = 0;
                 for (int j = threadIdx.x; j < proc; j += blockDim.x) part += ne4(cc[j]);
-                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+                part = wave_sum_i32(part);
                 if (lane_id() == 0) tmp[8 + w] = part;
                 __syncthreads();
                 for (int q = 0; q < nw; q++) ne_total += tmp[8 + q];
