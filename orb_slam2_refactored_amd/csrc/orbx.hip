@@ -624,9 +624,16 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     FAST_STAMP(0, __builtin_amdgcn_s_memtime());
     const int i_beg = lb * cpw, i_end = min(i_beg + cpw, n_items);
     // item i = f * ncell + (cell - cell_beg): this launch covers cells [cell_beg, cell_beg + ncell)
+    // (frame, cell) of this wavefront's items: one division for the first, then stepped
+    int src_f = i_beg / ncell, src_c = cell_beg + i_beg - src_f * ncell;
     auto source = [&](int item, CellDev& cd, int& f, int& ci) {
-        f = item / ncell;
-        ci = cell_beg + item - f * ncell;
+        (void)item;
+        f = src_f;
+        ci = src_c;
+        if (++src_c == cell_beg + ncell) {
+            src_c = cell_beg;
+            src_f++;
+        }
         cd = cells[ci];
         CropSrc c;
         c.img = level_base(g, cd.level, f, in, in_fstride, in_step, pyr, &c.step);

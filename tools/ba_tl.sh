@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ba_tl -o run -- python3 tools/babench.py > gpurun_out/ba_tl.log 2>&1 || { tail -5 gpurun_out/ba_tl.log; exit 1; }
+tail -3 gpurun_out/ba_tl.log
+python3 tools/ba_timeline.py gpurun_out/ba_tl v | tail -60
