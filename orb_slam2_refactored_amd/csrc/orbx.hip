@@ -652,7 +652,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     {
         crop_stage_rows(src, lane, crop, CSd);
     }
-    for (int i = lane; i < (zh + 2) * (ZSd / 4); i += 64) reinterpret_cast<uint32_t*>(Mz)[i] = 0;
+    for (int i = lane; i < ((zh + 2) * ZSd + 15) >> 4; i += 64) reinterpret_cast<uint4*>(Mz)[i] = make_uint4(0, 0, 0, 0);
     uint8_t* Mc = Mz + ZSd + 1;   // zone (0, 0); the zero border makes out-of-zone neighbours read 0
     wave_lds_sync();
     if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
