@@ -1608,8 +1608,11 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                                                       const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
                                                       uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
                                                       int cap) {
-    __shared__ __attribute__((aligned(16))) uint8_t R[PATCH * RS];
+    // the raw patch R is dead once every lane holds its row for the horizontal blur (one
+    // wavefront: its LDS reads complete before its later writes), so the blurred rows Hb reuse it
     __shared__ __attribute__((aligned(16))) uint16_t Hb[PATCH * HBS];
+    uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
+    static_assert(PATCH * RS <= PATCH * HBS * 2, "R must fit in Hb");
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
