@@ -171,6 +171,154 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));   // packed u16 
 constexpr int PYR_TW = 64, PYR_TH = 64;
 constexpr int PYR_SW = 144, PYR_SH = 128;   // LDS source tile capacity (scale factor <= ~1.9)
 
+// Level-l output tile (tx0, ty0, tw x th) from the staged source rectangle S (row stride PYR_SW,
+// first row sy_lo, first byte column xa) and the tile's coefficient rows xs_t / ys_t.  Every
+// thread of the workgroup must call it (block-wide vote inside); no barrier follows the vote.
+__device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& L, int f, uint8_t* pyr,
+                                                 const uint8_t* S, const int2* xs_t, const int2* ys_t, int tx0,
+                                                 int ty0, int tw, int th, int xa, int sy_lo) {
+    {
+        // 32 threads per 64-px output row (2 px each), 8 rows per pass.  Both pixels' four taps lie
+        // in the 8 LDS bytes from dword wd (scale <= ~3), so one row costs two dword reads; v_perm
+        // packs a pixel's taps as u16 (S0, S1) and v_dot2_u32_u16 with the packed (a0, a1) gives
+        // S0*a0 + S1*a1 exactly.  (h >> 4 <= 32640 and the result <= 255: OpenCV's saturations
+        // cannot trigger for coefficients summing to 2048.)
+        const int p0 = (threadIdx.x & 31) * 2;
+        const int2 xv0 = xs_t[min(p0, tw - 1)], xv1 = xs_t[min(p0 + 1, tw - 1)];
+        const int s00 = (xv0.x & 0xffff) - xa, s01 = (xv0.x >> 16) - xa;
+        const int s10 = (xv1.x & 0xffff) - xa, s11 = (xv1.x >> 16) - xa;
+        const int wd = s00 >> 2;
+        const int e00 = s00 - 4 * wd, e01 = s01 - 4 * wd, e10 = s10 - 4 * wd, e11 = s11 - 4 * wd;
+        const bool fits = max(e01, e11) <= 7 && min(e00, e10) >= 0;
+        if (!__syncthreads_or(!fits)) {   // block-uniform: every thread's taps fit its 8-byte window
+            if (p0 >= tw) return;   // after the block-wide vote: no barrier follows
+            const uint32_t sel0 = (uint32_t)e00 | 0x0c00u | ((uint32_t)e01 << 16) | 0x0c000000u;
+            const uint32_t sel1 = (uint32_t)e10 | 0x0c00u | ((uint32_t)e11 << 16) | 0x0c000000u;
+            const us2 a0 = *reinterpret_cast<const us2*>(&xv0.y), a1 = *reinterpret_cast<const us2*>(&xv1.y);
+            const uint32_t* S32 = reinterpret_cast<const uint32_t*>(S) + wd;
+            uint8_t* dcol = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + p0;
+            for (int ty = threadIdx.x >> 5; ty < th; ty += 8) {
+                const int2 yv = ys_t[ty];
+                const int r0 = ((yv.x & 0xffff) - sy_lo) * (PYR_SW / 4), r1 = ((yv.x >> 16) - sy_lo) * (PYR_SW / 4);
+                const uint32_t b0 = (uint32_t)yv.y << 16, b1 = (uint32_t)yv.y & 0xffff0000u;
+                const uint32_t w00 = S32[r0], w01 = S32[r0 + 1], w10 = S32[r1], w11 = S32[r1 + 1];
+                auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
+                    const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
+                    return *reinterpret_cast<const us2*>(&r);
+                };
+                const uint32_t h0a = __builtin_amdgcn_udot2(tap(w01, w00, sel0), a0, 0u, false) >> 4;
+                const uint32_t h1a = __builtin_amdgcn_udot2(tap(w11, w10, sel0), a0, 0u, false) >> 4;
+                const uint32_t h0b = __builtin_amdgcn_udot2(tap(w01, w00, sel1), a1, 0u, false) >> 4;
+                const uint32_t h1b = __builtin_amdgcn_udot2(tap(w11, w10, sel1), a1, 0u, false) >> 4;
+                // (h * b) >> 16 == mulhi(h, b << 16)
+                const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
+                const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
+                uint8_t* dst = dcol + (long long)(ty0 + ty) * L.stride;
+                if (p0 + 1 < tw) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(va | (vb << 8));   // tx0 + p0 even
+                else dst[0] = (uint8_t)va;
+            }
+            return;
+        }
+    }
+    // generic path: 16 threads per 64-px output row segment (4 px each), 16 rows per pass
+    const int q0 = (threadIdx.x & 15) * 4;
+    if (q0 >= tw) return;
+    // (cold path: the column coefficients are re-read from LDS per row to keep registers free for
+    // pyramid_tiles_kernel's prefetch)
+    uint8_t* dbase = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + q0;
+#pragma nounroll
+    for (int ty = threadIdx.x >> 4; ty < th; ty += 16) {
+        const int2 yv = ys_t[ty];
+        const int r0 = ((yv.x & 0xffff) - sy_lo) * PYR_SW, r1 = ((yv.x >> 16) - sy_lo) * PYR_SW;
+        const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
+        uint32_t packed = 0;
+#pragma nounroll
+        for (int k = 0; k < 4; k++) {
+            const int2 xv = xs_t[min(q0 + k, tw - 1)];
+            const int sx0 = (xv.x & 0xffff) - xa, sx1 = (xv.x >> 16) - xa, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
+            const int h0 = S[r0 + sx0] * a0 + S[r0 + sx1] * a1;
+            const int h1 = S[r1 + sx0] * a0 + S[r1 + sx1] * a1;
+            const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
+            const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+            packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
+        }
+        uint8_t* dst = dbase + (long long)(ty0 + ty) * L.stride;
+        if (q0 + 3 < tw) *reinterpret_cast<uint32_t*>(dst) = packed;   // stride % 16 == 0, tx0+q0 % 4 == 0
+        else {   // q0 < tw <= q0 + 3
+            dst[0] = (uint8_t)packed;
+            if (q0 + 1 < tw) dst[1] = (uint8_t)(packed >> 8);
+            if (q0 + 2 < tw) dst[2] = (uint8_t)(packed >> 16);
+        }
+    }
+}
+
+// 16-byte staging (every pyramid level; level 0 when the caller's base and step are multiples of
+// 16): the source rectangle is fetched as 16-byte pieces with (row, piece) flattened over the 256
+// threads, i.e. ~3 loads per thread instead of one dword load per source row.
+constexpr int PYR_PF = 5;   // 16-byte pieces per thread: PYR_SH rows x PYR_SW / 16 pieces <= 5 x 256
+
+struct PyrTile {
+    int f, tx0, ty0, tw, th, sy_lo, xa, nc, items, mul;   // mul = ceil(2^20 / nc): row = item * mul >> 20
+    const uint8_t* src;
+    int sstep;
+};
+
+__device__ __forceinline__ PyrTile pyr_tile_geom(const Geom& g, int l, int t, int ntx, int nty, const uint8_t* in,
+                                                 long long in_fstride, int in_step, uint8_t* pyr) {
+    const LevelDev& L = g.lv[l];
+    const LevelDev& Ls = g.lv[l - 1];
+    PyrTile T;
+    const int per = ntx * nty;
+    T.f = t / per;
+    const int r = t - T.f * per;
+    T.ty0 = (r / ntx) * PYR_TH;
+    T.tx0 = (r - (r / ntx) * ntx) * PYR_TW;
+    T.tw = min(PYR_TW, L.w - T.tx0);
+    T.th = min(PYR_TH, L.h - T.ty0);
+    const int sx_lo = max(0, (int)floor((T.tx0 + 0.5) * L.ssx - 0.5) - 2);
+    const int sx_hi = min(Ls.w - 1, (int)floor((T.tx0 + T.tw - 0.5) * L.ssx - 0.5) + 2);
+    T.sy_lo = max(0, (int)floor((T.ty0 + 0.5) * L.ssy - 0.5) - 2);
+    const int sy_hi = min(Ls.h - 1, (int)floor((T.ty0 + T.th - 0.5) * L.ssy - 0.5) + 2);
+    T.xa = sx_lo & ~15;
+    T.nc = ((sx_hi - T.xa) >> 4) + 1;
+    T.items = (sy_hi - T.sy_lo + 1) * T.nc;
+    T.mul = ((1 << 20) + T.nc - 1) / T.nc;
+    T.src = level_base(g, l - 1, T.f, in, in_fstride, in_step, pyr, &T.sstep);
+    // workgroup-uniform by construction: keep the tile in SGPRs, not in VGPRs across the compute
+    auto u = [](int x) { return __builtin_amdgcn_readfirstlane(x); };
+    T.f = u(T.f), T.tx0 = u(T.tx0), T.ty0 = u(T.ty0), T.tw = u(T.tw), T.th = u(T.th), T.sy_lo = u(T.sy_lo);
+    T.xa = u(T.xa), T.nc = u(T.nc), T.items = u(T.items), T.mul = u(T.mul), T.sstep = u(T.sstep);
+    const unsigned long long sp = (unsigned long long)(uintptr_t)T.src;
+    T.src = (const uint8_t*)(uintptr_t)(((unsigned long long)(unsigned)u((int)(sp >> 32)) << 32) |
+                                        (unsigned)u((int)(unsigned)sp));
+    return T;
+}
+
+__device__ __forceinline__ void pyr_piece_load(const PyrTile& T, int i, uint4& v) {
+    if (i < T.items) {
+        const int rr = (int)(((unsigned)i * (unsigned)T.mul) >> 20), c = i - rr * T.nc;
+        v = *reinterpret_cast<const uint4*>(T.src + (long long)(T.sy_lo + rr) * T.sstep + T.xa + 16 * c);
+    }
+}
+
+__device__ __forceinline__ void pyr_fetch(const PyrTile& T, int tid, uint4& v0, uint4& v1, uint4& v2, uint4& v3,
+                                          uint4& v4) {
+    static_assert(PYR_PF == 5, "five pieces per thread");
+    pyr_piece_load(T, tid, v0);
+    pyr_piece_load(T, tid + 256, v1);
+    pyr_piece_load(T, tid + 512, v2);
+    pyr_piece_load(T, tid + 768, v3);
+    pyr_piece_load(T, tid + 1024, v4);
+}
+
+__device__ __forceinline__ void pyr_stage(const PyrTile& T, int tid, uint8_t* S, const uint4& v, int k) {
+    const int i = tid + 256 * k;
+    if (i < T.items) {
+        const int rr = (int)(((unsigned)i * (unsigned)T.mul) >> 20), c = i - rr * T.nc;
+        *reinterpret_cast<uint4*>(&S[rr * PYR_SW + 16 * c]) = v;
+    }
+}
+
 __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const uint8_t* __restrict__ in,
                                                             long long in_fstride, int in_step, uint8_t* pyr,
                                                             const int2* __restrict__ xtab,
@@ -203,6 +351,19 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
     const int nd = (sx_hi - xa + 4) >> 2;   // dwords per source row (<= PYR_SW / 4 < 64)
     const int nr = sy_hi - sy_lo + 1;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)sstep) & 3) == 0;
+    if (((reinterpret_cast<uintptr_t>(src) | (uintptr_t)sstep) & 15) == 0 && sx_hi - (sx_lo & ~15) < PYR_SW) {
+        const PyrTile T = pyr_tile_geom(g, l, lb, gx, gridDim.y, in, in_fstride, in_step, pyr);
+        uint4 v0, v1, v2, v3, v4;
+        pyr_fetch(T, threadIdx.x, v0, v1, v2, v3, v4);
+        pyr_stage(T, threadIdx.x, S, v0, 0);
+        pyr_stage(T, threadIdx.x, S, v1, 1);
+        pyr_stage(T, threadIdx.x, S, v2, 2);
+        pyr_stage(T, threadIdx.x, S, v3, 3);
+        pyr_stage(T, threadIdx.x, S, v4, 4);
+        __syncthreads();
+        pyr_tile_compute(g, L, f, pyr, S, xs_t, ys_t, tx0, ty0, tw, th, T.xa, sy_lo);
+        return;
+    }
     if (aligned) {
         // wavefront w stages rows w, w + 4, ...; lane = dword of the row.  The row address is
         // wave-uniform (SGPR base + a per-lane column offset), so a load costs no VALU; all of a
@@ -236,79 +397,7 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
         }
     }
     __syncthreads();
-    {
-        // 32 threads per 64-px output row (2 px each), 8 rows per pass.  Both pixels' four taps lie
-        // in the 8 LDS bytes from dword wd (scale <= ~3), so one row costs two dword reads; v_perm
-        // packs a pixel's taps as u16 (S0, S1) and v_dot2_u32_u16 with the packed (a0, a1) gives
-        // S0*a0 + S1*a1 exactly.  (h >> 4 <= 32640 and the result <= 255: OpenCV's saturations
-        // cannot trigger for coefficients summing to 2048.)
-        const int p0 = (threadIdx.x & 31) * 2;
-        const int2 xv0 = xs_t[min(p0, tw - 1)], xv1 = xs_t[min(p0 + 1, tw - 1)];
-        const int s00 = (xv0.x & 0xffff) - xa, s01 = (xv0.x >> 16) - xa;
-        const int s10 = (xv1.x & 0xffff) - xa, s11 = (xv1.x >> 16) - xa;
-        const int wd = s00 >> 2;
-        const int e00 = s00 - 4 * wd, e01 = s01 - 4 * wd, e10 = s10 - 4 * wd, e11 = s11 - 4 * wd;
-        const bool fits = max(e01, e11) <= 7 && min(e00, e10) >= 0;
-        if (!__syncthreads_or(!fits)) {   // block-uniform: every thread's taps fit its 8-byte window
-            if (p0 >= tw) return;
-            const uint32_t sel0 = (uint32_t)e00 | 0x0c00u | ((uint32_t)e01 << 16) | 0x0c000000u;
-            const uint32_t sel1 = (uint32_t)e10 | 0x0c00u | ((uint32_t)e11 << 16) | 0x0c000000u;
-            const us2 a0 = *reinterpret_cast<const us2*>(&xv0.y), a1 = *reinterpret_cast<const us2*>(&xv1.y);
-            const uint32_t* S32 = reinterpret_cast<const uint32_t*>(S) + wd;
-            uint8_t* dcol = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + p0;
-            for (int ty = threadIdx.x >> 5; ty < th; ty += 8) {
-                const int2 yv = ys_t[ty];
-                const int r0 = ((yv.x & 0xffff) - sy_lo) * (PYR_SW / 4), r1 = ((yv.x >> 16) - sy_lo) * (PYR_SW / 4);
-                const uint32_t b0 = (uint32_t)(yv.y & 0xffff), b1 = (uint32_t)(yv.y >> 16);
-                const uint32_t w00 = S32[r0], w01 = S32[r0 + 1], w10 = S32[r1], w11 = S32[r1 + 1];
-                auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
-                    const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
-                    return *reinterpret_cast<const us2*>(&r);
-                };
-                const uint32_t h0a = __builtin_amdgcn_udot2(tap(w01, w00, sel0), a0, 0u, false) >> 4;
-                const uint32_t h1a = __builtin_amdgcn_udot2(tap(w11, w10, sel0), a0, 0u, false) >> 4;
-                const uint32_t h0b = __builtin_amdgcn_udot2(tap(w01, w00, sel1), a1, 0u, false) >> 4;
-                const uint32_t h1b = __builtin_amdgcn_udot2(tap(w11, w10, sel1), a1, 0u, false) >> 4;
-                const uint32_t va = (((h0a * b0) >> 16) + ((h1a * b1) >> 16) + 2) >> 2;
-                const uint32_t vb = (((h0b * b0) >> 16) + ((h1b * b1) >> 16) + 2) >> 2;
-                uint8_t* dst = dcol + (long long)(ty0 + ty) * L.stride;
-                if (p0 + 1 < tw) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(va | (vb << 8));   // tx0 + p0 even
-                else dst[0] = (uint8_t)va;
-            }
-            return;
-        }
-    }
-    // generic path: 16 threads per 64-px output row segment (4 px each), 16 rows per pass
-    const int q0 = (threadIdx.x & 15) * 4;
-    if (q0 >= tw) return;
-    int sxo[4], a0v[4], a1v[4], sxo1[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int2 xv = xs_t[min(q0 + k, tw - 1)];
-        sxo[k] = (xv.x & 0xffff) - xa;
-        sxo1[k] = (xv.x >> 16) - xa;
-        a0v[k] = xv.y & 0xffff;
-        a1v[k] = xv.y >> 16;
-    }
-    uint8_t* dbase = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + q0;
-    for (int ty = threadIdx.x >> 4; ty < th; ty += 16) {
-        const int2 yv = ys_t[ty];
-        const int r0 = ((yv.x & 0xffff) - sy_lo) * PYR_SW, r1 = ((yv.x >> 16) - sy_lo) * PYR_SW;
-        const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
-        uint32_t packed = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int h0 = S[r0 + sxo[k]] * a0v[k] + S[r0 + sxo1[k]] * a1v[k];
-            const int h1 = S[r1 + sxo[k]] * a0v[k] + S[r1 + sxo1[k]] * a1v[k];
-            const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
-            const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
-            packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
-        }
-        uint8_t* dst = dbase + (long long)(ty0 + ty) * L.stride;
-        if (q0 + 3 < tw) *reinterpret_cast<uint32_t*>(dst) = packed;   // stride % 16 == 0, tx0+q0 % 4 == 0
-        else
-            for (int k = 0; q0 + k < tw; k++) dst[k] = (uint8_t)(packed >> (8 * k));
-    }
+    pyr_tile_compute(g, L, f, pyr, S, xs_t, ys_t, tx0, ty0, tw, th, xa, sy_lo);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2117,6 +2206,11 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(256), (uint32_t)h->qt_lds, s, g,
                            cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0);
     };
+    auto pyramid = [&](int l) {
+        const int ntx = (g.lv[l].w + PYR_TW - 1) / PYR_TW, nty = (g.lv[l].h + PYR_TH - 1) / PYR_TH;
+        launch_timed(h, 0, pyramid_level_kernel, dim3((unsigned)ntx, (unsigned)nty, (unsigned)F), dim3(256), 0u, st, g, l,
+                     d_imgs, fstride, step, pyr, h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
+    };
     const int nc0 = g.lv[0].ncells;
     if (side && nc0 > 0 && g.nlevels > 1) {
         // Level 0 needs no pyramid: its FAST + quadtree run on the side stream while the main
@@ -2127,24 +2221,14 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         quadtree(0, 1, side);
         (void)hipEventRecord(h->lvl_join, side);
         {
-            for (int l = 1; l < g.nlevels; l++) {
-                dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
-                          (unsigned)F);
-                launch_timed(h, 0, pyramid_level_kernel, grid, dim3(256), 0u, st, g, l, d_imgs, fstride, step, pyr,
-                                   h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
-            }
+            for (int l = 1; l < g.nlevels; l++) pyramid(l);
         }
         fast(nc0, g.ncells_total - nc0, st);
         quadtree(1, g.nlevels - 1, st);
         (void)hipStreamWaitEvent(st, h->lvl_join, 0);
     } else {
         {
-            for (int l = 1; l < g.nlevels; l++) {
-                dim3 grid((unsigned)((g.lv[l].w + PYR_TW - 1) / PYR_TW), (unsigned)((g.lv[l].h + PYR_TH - 1) / PYR_TH),
-                          (unsigned)F);
-                launch_timed(h, 0, pyramid_level_kernel, grid, dim3(256), 0u, st, g, l, d_imgs, fstride, step, pyr,
-                                   h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
-            }
+            for (int l = 1; l < g.nlevels; l++) pyramid(l);
         }
         fast(0, g.ncells_total, st);
         quadtree(0, g.nlevels, st);
