@@ -45,6 +45,15 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
+// The same median, ordered after `dep`.  `key` is an MFMA result: the compiler's hazard recognizer
+// does not see reads inside inline asm, so the asm must come after a compiler-generated read of
+// the same register (the `min` that produces `dep`), which carries the MFMA -> VALU wait states.
+__device__ __forceinline__ uint32_t umed3_after(uint32_t a, uint32_t key, uint32_t c, uint32_t dep) {
+    uint32_t r;
+    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(key), "v"(c), "v"(dep));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t chunk16(uint2 v, int s) {
     return ((s < 2 ? v.x : v.y) >> (16 * (s & 1))) & 0xffffu;
 }
@@ -57,13 +66,15 @@ __device__ __forceinline__ int popc_row(const uint8_t* r) {
 
 constexpr int MM_RT = 4;                 // 16-row tiles per wavefront
 constexpr int MM_ROWS = 4 * 64 * MM_RT / 4;   // 256 query rows per workgroup
+constexpr int MM_CHUNK = 2048;                // columns per chunk key range (128 tiles of 16)
 
+template <bool MULTI>   // MULTI: more than MM_CHUNK columns (chunked, global keys kept across chunks)
 __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
     const uint8_t* __restrict__ A, const int32_t* __restrict__ nA_arr, int nA_fixed, int strideA,
     const uint8_t* __restrict__ B, const int32_t* __restrict__ nB_arr, int nB_fixed, int strideB,
     const int32_t* __restrict__ pair_b, float nnratio, int th_low, int32_t* __restrict__ best_idx,
     int32_t* __restrict__ best, int32_t* __restrict__ second, int32_t* __restrict__ match) {
-    extern __shared__ __attribute__((aligned(16))) int mm_sm[];   // pa[MM_ROWS] | pb[nB padded to 16] | expanded B [2][4][64]
+    extern __shared__ __attribute__((aligned(16))) int mm_sm[];   // pa[MM_ROWS] | pb[nB padded to 32] | expanded B [2][2][4][64]
     int* s_pa = mm_sm;
     int* s_pb = mm_sm + MM_ROWS;
     const int p = blockIdx.y;
@@ -75,8 +86,8 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
     const uint8_t* Ap = A + (long long)p * strideA * 32;
     const uint8_t* Bp = B + (long long)q * strideB * 32;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c16 = lane & 15, g = lane >> 4;
-    const int nBt = (nB + 15) & ~15;
-    for (int j = tid; j < nBt; j += blockDim.x) s_pb[j] = j < nB ? popc_row(Bp + (long long)j * 32) : 256;
+    const int nBt = (nB + 31) & ~31;   // whole pairs of 16-column tiles
+    for (int j = tid; j < nBt; j += blockDim.x) s_pb[j] = 128 * ((j < nB ? popc_row(Bp + (long long)j * 32) : 256) + 256);
     {
         const int row = row_base + tid;
         s_pa[tid] = row < nA ? popc_row(Ap + (long long)row * 32) : 0;
@@ -88,58 +99,95 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
         const int row = min(row_base + 64 * w + 16 * rt + c16, nA - 1);
         const uint2 v = *reinterpret_cast<const uint2*>(Ap + (long long)row * 32 + 8 * g);
 #pragma unroll
-        for (int s2 = 0; s2 < 4; s2++) af[rt][s2] = expand16(chunk16(v, s2)) * 0xfe;   // bit -> int8 0 / -2
+        for (int s2 = 0; s2 < 4; s2++) af[rt][s2] = expand16(chunk16(v, s2)) * 0x80;   // bit -> int8 0 / -128
     }
     __syncthreads();
-    uint32_t bk[MM_RT][4], sk[MM_RT][4];
+    // Inside a chunk of 128 tiles the MFMA itself yields the chunk key 128 S + t (t = tile in the
+    // chunk, S = |b| + 256 - 2<a, b> = d - |a| + 256 in [0, 512]): A is expanded to 0 / -128, B
+    // to 0 / 2, and the accumulator starts at 128 (|b| + 256) + t.  A lane holds one column class
+    // c16 (j = chunk base + 16 t + c16), so the chunk key orders the lane's candidates by (S, j)
+    // with no per-value key build.  With MULTI, global keys (S << 16 | j) carry the top-2 across
+    // chunks.
+    uint32_t bk[MM_RT][4], sk[MM_RT][4], lb[MM_RT][4], ls[MM_RT][4];
 #pragma unroll
     for (int rt = 0; rt < MM_RT; rt++)
 #pragma unroll
         for (int r = 0; r < 4; r++) bk[rt][r] = sk[rt][r] = 0xffffffffu;
-    // Column tiles of 16.  The 0/1 byte expansion of a B tile is shared by the 4 wavefronts (all of
-    // them need the same 16 columns): wavefront w expands k-step w of tile t+1 into an LDS double
-    // buffer while tile t is consumed, one barrier per tile.  Raw B bits load two tiles ahead.
-    i4v* xb = reinterpret_cast<i4v*>(mm_sm + ((MM_ROWS + nBt + 16 + 3) & ~3));   // [2][4][64]
+    // Column tiles of 16, consumed in pairs.  The 0/1 byte expansion of a tile pair is shared by the
+    // 4 wavefronts (all of them need the same columns): wavefront w expands k-step w of both tiles
+    // of the next pair into an LDS double buffer while this pair is consumed, one barrier per pair.
+    i4v* xb = reinterpret_cast<i4v*>(mm_sm + ((MM_ROWS + nBt + 16 + 3) & ~3));   // [2][2][4][64]
     auto ldb = [&](int jj) -> uint2 {
         return jj < nB ? *reinterpret_cast<const uint2*>(Bp + (long long)jj * 32 + 8 * g) : make_uint2(0, 0);
     };
     {
-        const uint2 b0 = ldb(c16);
-        xb[w * 64 + lane] = expand16(chunk16(b0, w));
+        const uint2 b0 = ldb(c16), b1 = ldb(16 + c16);
+        xb[(0 * 4 + w) * 64 + lane] = expand16(chunk16(b0, w)) * 2;
+        xb[(1 * 4 + w) * 64 + lane] = expand16(chunk16(b1, w)) * 2;
     }
-    uint2 bnext = ldb(16 + c16);
+    uint2 bn0 = ldb(32 + c16), bn1 = ldb(48 + c16);
     __syncthreads();
-    for (int j0 = 0, t = 0; j0 < nB; j0 += 16, t++) {
-        const int cur = t & 1;
-        if (j0 + 16 < nB) {   // block-uniform
-            xb[((cur ^ 1) * 4 + w) * 64 + lane] = expand16(chunk16(bnext, w));
-            bnext = ldb(j0 + 32 + c16);
+    for (int c0 = 0; c0 < nB; c0 += MM_CHUNK) {
+#pragma unroll
+        for (int rt = 0; rt < MM_RT; rt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) lb[rt][r] = ls[rt][r] = 0xffffffffu;
+        const int c1 = min(nB, c0 + MM_CHUNK);
+        for (int j0 = c0; j0 < c1; j0 += 32) {
+            const int cur = (j0 >> 5) & 1;
+            if (j0 + 32 < nB) {   // block-uniform
+                xb[(((cur ^ 1) * 2 + 0) * 4 + w) * 64 + lane] = expand16(chunk16(bn0, w)) * 2;   // bit -> 0 / 2
+                xb[(((cur ^ 1) * 2 + 1) * 4 + w) * 64 + lane] = expand16(chunk16(bn1, w)) * 2;
+                bn0 = ldb(j0 + 64 + c16);
+                bn1 = ldb(j0 + 80 + c16);
+            }
+            const int t = (j0 - c0) >> 4;
+#pragma unroll
+            for (int tt = 0; tt < 2; tt++) {
+                const int ci = s_pb[j0 + 16 * tt + c16] + t + tt;
+                const i4v cinit = {ci, ci, ci, ci};
+                i4v bf[4];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) bf[s2] = xb[((cur * 2 + tt) * 4 + s2) * 64 + lane];
+#pragma unroll
+                for (int rt = 0; rt < MM_RT; rt++) {
+                    i4v acc = cinit;
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; s2++)
+                        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[rt][s2], bf[s2], acc, 0, 0, 0);
+                    const int sv[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t key = (uint32_t)sv[r];
+                        // lb <= ls always, so the new second order statistic min(ls, max(lb, key))
+                        // is the median of the three
+                        const uint32_t nb = min(lb[rt][r], key);
+                        ls[rt][r] = umed3_after(lb[rt][r], key, ls[rt][r], nb);
+                        lb[rt][r] = nb;
+                    }
+                }
+            }
+            __syncthreads();   // pair expanded into `cur ^ 1`; buffer `cur` free for the pair after
         }
-        const int j = j0 + c16;
-        // the accumulator starts at |b| + 256 (one value per lane: a lane holds 4 rows of ONE
-        // column), so the MFMA yields S = |b| + 256 - 2<a, b> = d - |a| + 256 in [0, 512]: a row's
-        // ordering by (S, j) is its ordering by (d, j), and |a| is added back after the merge
-        const int pbv = s_pb[j] + 256;
-        const i4v cinit = {pbv, pbv, pbv, pbv};
-        i4v bf[4];
+        // the chunk's top-2 as global keys
+        const uint32_t jb = (uint32_t)(c0 + c16);
 #pragma unroll
-        for (int s2 = 0; s2 < 4; s2++) bf[s2] = xb[(cur * 4 + s2) * 64 + lane];
-#pragma unroll
-        for (int rt = 0; rt < MM_RT; rt++) {
-            i4v acc = cinit;
-#pragma unroll
-            for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[rt][s2], bf[s2], acc, 0, 0, 0);
-            const int sv[4] = {acc.x, acc.y, acc.z, acc.w};
+        for (int rt = 0; rt < MM_RT; rt++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const uint32_t key = ((uint32_t)sv[r] << 16) | (uint32_t)j;   // row-relative (d, j) key
-                // bk <= sk always, so the new second order statistic min(sk, max(bk, key)) is the
-                // median of the three
-                sk[rt][r] = umed3(bk[rt][r], key, sk[rt][r]);
-                bk[rt][r] = min(bk[rt][r], key);
+                auto glob = [&](uint32_t k) {
+                    return k == 0xffffffffu ? k : ((k >> 7) << 16) | (jb + 16 * (k & 127u));
+                };
+                const uint32_t b2 = glob(lb[rt][r]), s2v = glob(ls[rt][r]);
+                if (MULTI) {
+                    sk[rt][r] = min(min(sk[rt][r], s2v), max(bk[rt][r], b2));
+                    bk[rt][r] = min(bk[rt][r], b2);
+                } else {
+                    bk[rt][r] = b2;
+                    sk[rt][r] = s2v;
+                }
             }
-        }
-        __syncthreads();   // tile t+1 expanded; buffer `cur` free for tile t+2
+        if (!MULTI) break;
     }
     // merge the 16 column classes of each row (lanes with the same g)
 #pragma unroll
@@ -181,8 +229,9 @@ static void launch_top2(const uint8_t* A, const int32_t* nA_arr, int nA_fixed, i
                         const int32_t* nB_arr, int nB_fixed, int strideB, const int32_t* pair_b, int n_pairs,
                         float nnratio, int th_low, int32_t* bi, int32_t* bd, int32_t* sd, int32_t* mt,
                         hipStream_t st) {
-    const size_t lds = (size_t)(((MM_ROWS + ((strideB + 15) & ~15) + 16 + 3) & ~3) + 2 * 4 * 64 * 4) * sizeof(int);
-    hipLaunchKernelGGL(hamming_top2_mfma_kernel, dim3((unsigned)((strideA + MM_ROWS - 1) / MM_ROWS), (unsigned)n_pairs),
+    const size_t lds = (size_t)(((MM_ROWS + ((strideB + 31) & ~31) + 16 + 3) & ~3) + 2 * 2 * 4 * 64 * 4) * sizeof(int);
+    auto kern = strideB <= MM_CHUNK ? hamming_top2_mfma_kernel<false> : hamming_top2_mfma_kernel<true>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((strideA + MM_ROWS - 1) / MM_ROWS), (unsigned)n_pairs),
                        dim3(256), lds, st, A, nA_arr, nA_fixed, strideA, B, nB_arr, nB_fixed, strideB, pair_b,
                        nnratio, th_low, bi, bd, sd, mt);
 }

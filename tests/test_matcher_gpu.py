@@ -31,6 +31,25 @@ def test_bf_match_random(oracle, nA, nB):
         assert np.array_equal(g, e)
 
 
+@pytest.mark.parametrize("nA,nB", [(300, 2048), (300, 2049), (100, 4500)])
+def test_bf_match_chunked(oracle, nA, nB):
+    """More than 2048 columns: the chunked kernel carries the top-2 across 2048-column chunks.
+    Ties on best / second straddle the chunk boundaries (the lower index must win)."""
+    rng = np.random.default_rng(nB)
+    A = rand_desc(rng, nA)
+    B = rand_desc(rng, nB)
+    for j in (2047, 2048, nB - 1):
+        if j < nB:
+            B[j] = B[5]
+    A[:10] = B[5] ^ np.uint8(3)      # best tied across chunks
+    A[10:20] = B[nB - 1] ^ np.uint8(1)
+    B[nB - 2] = B[nB - 1] ^ np.uint8(1)   # second in the last chunk
+    got = ORBmatcher().MatchBruteForce(A, B)
+    exp = oracle.bf_match(A, B)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+
+
 def test_bf_match_near_duplicates(oracle):
     rng = np.random.default_rng(3)
     B = rand_desc(rng, 900, 0.5)

@@ -41,8 +41,16 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st = ex.profile_read()
-    print({k: round(v[0] / a.iters, 4) for k, v in st.items()}, f"wall/iter {1e3 * dt / a.iters:.3f} ms",
-          f"fps {a.frames * a.iters / dt:.0f}")
+    out = {k: round(v[0] / a.iters, 4) for k, v in st.items()}
+    if a.match:   # the matcher alone, back to back (launch-bound gaps included)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            m.match_batch_device(desc, cnt, desc, cnt, pair_b=prev)
+        e1.record()
+        torch.cuda.synchronize()
+        out["match"] = round(e0.elapsed_time(e1) / a.iters, 4)
+    print(out, f"wall/iter {1e3 * dt / a.iters:.3f} ms", f"fps {a.frames * a.iters / dt:.0f}")
 
 
 if __name__ == "__main__":
