@@ -21,13 +21,14 @@ namespace orbamd {
 // to 0/1 bytes in registers and fed to v_mfma_i32_16x16x64_i8 (4 k-steps per 256 bits).  Any k
 // permutation applied identically to the A and B fragments leaves the dot product unchanged, so
 // lane l (group g = l >> 4) simply takes descriptor bytes 8g..8g+7 and k-step s their bits
-// 16s..16s+15.  A's bits are expanded to int8 0 / -2 and the accumulator starts at |b| + 256, so
-// the MFMA yields S = d - |a| + 256 directly; per (row, column) the lane forms the row-relative key
-// S << 16 | j (one v_lshl_or).  The running best key is the minimum (lowest j on equal d, as the
-// reference's strict-< scan) and the running second key the second order statistic.  After the
-// merge d = S - 256 + |a|; keys with d >= 256 (d == 256 and the padding columns) never displace a
-// real candidate and are mapped back to (256, -1), which is the reference's bestDist = 256 /
-// bestIdx = -1 initialisation.
+// 16s..16s+15.  A's bits are expanded to int8 0 / -128, B's to 0 / 2, and the accumulator starts
+// at 128 (|b| + 256) + t for column tile t of a 2048-column chunk, so the MFMA yields the key
+// 128 S + t with S = d - |a| + 256 in [0, 512] directly (a lane holds one column class, so t is
+// its column).  The running best key is the minimum (lowest j on equal d, as the reference's
+// strict-< scan) and the running second key the second order statistic.  Chunk keys become global
+// keys S << 16 | j for the cross-lane merge; after it d = S - 256 + |a|; keys with d >= 256
+// (d == 256 and the padding columns) never displace a real candidate and are mapped back to
+// (256, -1), which is the reference's bestDist = 256 / bestIdx = -1 initialisation.
 typedef int i4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ i4v expand16(uint32_t b) {   // bit k of b -> byte k (0 / 1)
@@ -64,8 +65,12 @@ __device__ __forceinline__ int popc_row(const uint8_t* r) {
            __popc(b.w);
 }
 
-constexpr int MM_RT = 4;                 // 16-row tiles per wavefront
-constexpr int MM_ROWS = 4 * 64 * MM_RT / 4;   // 256 query rows per workgroup
+#ifndef MM_RT_DEF
+#define MM_RT_DEF 2
+#endif
+constexpr int MM_RT = MM_RT_DEF;          // 16-row tiles per wavefront
+constexpr int MM_WROWS = 16 * MM_RT;      // query rows per wavefront
+constexpr int MM_ROWS = 4 * MM_WROWS;     // query rows per workgroup (4 wavefronts)
 constexpr int MM_CHUNK = 2048;                // columns per chunk key range (128 tiles of 16)
 
 template <bool MULTI>   // MULTI: more than MM_CHUNK columns (chunked, global keys kept across chunks)
@@ -87,16 +92,17 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
     const uint8_t* Bp = B + (long long)q * strideB * 32;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c16 = lane & 15, g = lane >> 4;
     const int nBt = (nB + 31) & ~31;   // whole pairs of 16-column tiles
+    const bool live = __builtin_amdgcn_readfirstlane(row_base + MM_WROWS * w < nA ? 1 : 0) != 0;
     for (int j = tid; j < nBt; j += blockDim.x) s_pb[j] = 128 * ((j < nB ? popc_row(Bp + (long long)j * 32) : 256) + 256);
     {
         const int row = row_base + tid;
-        s_pa[tid] = row < nA ? popc_row(Ap + (long long)row * 32) : 0;
+        if (tid < MM_ROWS) s_pa[tid] = row < nA ? popc_row(Ap + (long long)row * 32) : 0;
     }
     // A fragments: tile rt rows row_base + 64w + 16rt + c16, bytes 8g..8g+7
     i4v af[MM_RT][4];
 #pragma unroll
     for (int rt = 0; rt < MM_RT; rt++) {
-        const int row = min(row_base + 64 * w + 16 * rt + c16, nA - 1);
+        const int row = min(row_base + MM_WROWS * w + 16 * rt + c16, nA - 1);
         const uint2 v = *reinterpret_cast<const uint2*>(Ap + (long long)row * 32 + 8 * g);
 #pragma unroll
         for (int s2 = 0; s2 < 4; s2++) af[rt][s2] = expand16(chunk16(v, s2)) * 0x80;   // bit -> int8 0 / -128
@@ -142,8 +148,11 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
                 bn1 = ldb(j0 + 80 + c16);
             }
             const int t = (j0 - c0) >> 4;
+            // a wavefront whose rows all lie past nA (the last workgroup of a frame is mostly
+            // empty) only expands its share of the next pair
 #pragma unroll
             for (int tt = 0; tt < 2; tt++) {
+                if (!live) break;   // wavefront-uniform
                 const int ci = s_pb[j0 + 16 * tt + c16] + t + tt;
                 const i4v cinit = {ci, ci, ci, ci};
                 i4v bf[4];
@@ -209,9 +218,9 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
                   (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x124, 0xf, 0xf, false));
             merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0x128, 0xf, 0xf, false),
                   (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x128, 0xf, 0xf, false));
-            const int row = row_base + 64 * w + 16 * rt + 4 * g + r;
+            const int row = row_base + MM_WROWS * w + 16 * rt + 4 * g + r;
             if (c16 == 0 && row < nA) {
-                const int pa = s_pa[64 * w + 16 * rt + 4 * g + r];
+                const int pa = s_pa[MM_WROWS * w + 16 * rt + 4 * g + r];
                 const int bdr = (int)(b1 >> 16) - 256 + pa, sdr = (int)(s1 >> 16) - 256 + pa;
                 const int bd = bdr >= 256 ? 256 : bdr;
                 const int bi = bdr >= 256 ? -1 : (int)(b1 & 0xffffu);
