@@ -797,17 +797,22 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         wave_lds_sync();
         if (q2n - h2 >= 64) strength(64);
     };
+    // per-lane LDS address of zone (qy, qx) = crop (qy+3, qx+3) at byte qx+4 and queue entry
+    // (qy << 8) | qx, both stepped by a wave-uniform amount per chunk of RPC rows
+    const uint8_t* rowq = crop + __mul24(qy + 3, CSd) + 4 + qx;
+    const int e0q = (qy << 8) | qx;
+    const bool qxin = qx < zw;
     for (int yb = 0; yb < zh; yb += RPC) {
         const int y = yb + qy;
         us2 f0 = {0, 0}, f1 = {0, 0};
-        const bool act = y < zh && qx < zw;
+        const bool act = y < zh && qxin;
         if (act) {
-            const uint8_t* rowc = crop + __mul24(y + 3, CSd) + 4;   // zone (y, 0) = crop (y+3, 3) at byte 4
-            const uint32_t wv = *reinterpret_cast<const uint32_t*>(rowc + qx);
-            const uint32_t wl = *reinterpret_cast<const uint32_t*>(rowc + qx - 4);
-            const uint32_t wr = *reinterpret_cast<const uint32_t*>(rowc + qx + 4);
-            const uint32_t wn = *reinterpret_cast<const uint32_t*>(rowc + 3 * CSd + qx);   // (0,+3)
-            const uint32_t ws = *reinterpret_cast<const uint32_t*>(rowc - 3 * CSd + qx);   // (0,-3)
+            const uint8_t* rowc = rowq + __mul24(yb, CSd);   // zone (y, qx)
+            const uint32_t wv = *reinterpret_cast<const uint32_t*>(rowc);
+            const uint32_t wl = *reinterpret_cast<const uint32_t*>(rowc - 4);
+            const uint32_t wr = *reinterpret_cast<const uint32_t*>(rowc + 4);
+            const uint32_t wn = *reinterpret_cast<const uint32_t*>(rowc + 3 * CSd);   // (0,+3)
+            const uint32_t ws = *reinterpret_cast<const uint32_t*>(rowc - 3 * CSd);   // (0,-3)
             const uint32_t we = __builtin_amdgcn_alignbyte(wr, wv, 3);   // (+3, 0): bytes qx+3..qx+6
             const uint32_t ww = __builtin_amdgcn_alignbyte(wv, wl, 1);   // (-3, 0): bytes qx-3..qx
             f0 = u2us(us2u(compass2(lo_pair(wv), lo_pair(wn), lo_pair(we), lo_pair(ws), lo_pair(ww), t2)) & vm0);
@@ -822,7 +827,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, pre));
         pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, pre));
         int pos = qn + (int)pre;
-        const short e0 = (short)((y << 8) | qx);
+        const short e0 = (short)(e0q + (yb << 8));
         if (p0) queue[pos++ & (FQ_RING - 1)] = e0;
         if (p1) queue[pos++ & (FQ_RING - 1)] = (short)(e0 + 1);
         if (p2) queue[pos++ & (FQ_RING - 1)] = (short)(e0 + 2);
