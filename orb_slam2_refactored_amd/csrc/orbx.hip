@@ -400,6 +400,167 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
     pyr_tile_compute(g, L, f, pyr, S, xs_t, ys_t, tx0, ty0, tw, th, xa, sy_lo);
 }
 
+// Two cascaded levels in one launch: level l (from level l-1, both in the pyramid slab) and level
+// l+1, one workgroup per 64x64 tile of level l+1.  The workgroup computes the level-l rectangle
+// its tile's taps need (the conservative rectangle of pyramid_level_kernel, columns from a dword
+// boundary) from a staged level-(l-1) rectangle, keeps it in LDS for the level-(l+1) tile and
+// writes it to the slab.  Neighbouring workgroups' rectangles overlap by the tap margins; they
+// write the same bytes there.  Removes the launch boundary between the two levels and the
+// level-l re-read.
+constexpr int PP_MAXP = 8;   // level-l row passes per thread
+
+__device__ __forceinline__ uint32_t pyr_px_generic(const uint8_t* S, int2 xv, int2 yv, int xa, int ya) {
+    const int r0 = ((yv.x & 0xffff) - ya) * PYR_SW, r1 = ((yv.x >> 16) - ya) * PYR_SW;
+    const int sx0 = (xv.x & 0xffff) - xa, sx1 = (xv.x >> 16) - xa, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
+    const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
+    const int h0 = S[r0 + sx0] * a0 + S[r0 + sx1] * a1;
+    const int h1 = S[r1 + sx0] * a0 + S[r1 + sx1] * a1;
+    const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
+    const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+    return (uint32_t)(v > 255 ? 255 : v);
+}
+
+__global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, uint8_t* pyr, const int2* __restrict__ xtab,
+                                                           const int2* __restrict__ ytab) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW + 16];
+    __shared__ int2 xs1[PYR_SW], ys1[PYR_SH], xs2[PYR_TW], ys2[PYR_TH];
+    const LevelDev& L0 = g.lv[l - 1];
+    const LevelDev& L1 = g.lv[l];
+    const LevelDev& L2 = g.lv[l + 1];
+    const int tid = threadIdx.x;
+    const int gx = gridDim.x, gxy = gridDim.x * gridDim.y;
+    const int lb = xcd_swizzle(blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z, gxy * gridDim.z);
+    const int f = lb / gxy;
+    const int tx0 = (lb % gx) * PYR_TW, ty0 = ((lb % gxy) / gx) * PYR_TH;
+    const int tw = min(PYR_TW, L2.w - tx0), th = min(PYR_TH, L2.h - ty0);
+    auto u = [](int x) { return __builtin_amdgcn_readfirstlane(x); };
+    // level-l rectangle [c0, c1] x [ay0, ay1] (c0 dword aligned)
+    const int ax0 = max(0, (int)floor((tx0 + 0.5) * L2.ssx - 0.5) - 2);
+    const int c1 = u(min(L1.w - 1, (int)floor((tx0 + tw - 0.5) * L2.ssx - 0.5) + 2));
+    const int ay0 = u(max(0, (int)floor((ty0 + 0.5) * L2.ssy - 0.5) - 2));
+    const int ay1 = u(min(L1.h - 1, (int)floor((ty0 + th - 0.5) * L2.ssy - 0.5) + 2));
+    const int c0 = u(ax0 & ~3);
+    const int ncol = c1 - c0 + 1, nrow = ay1 - ay0 + 1;
+    // level-(l-1) rectangle for it, staged as 16-byte pieces
+    PyrTile T;
+    const int bx0 = max(0, (int)floor((c0 + 0.5) * L1.ssx - 0.5) - 2);
+    const int bx1 = min(L0.w - 1, (int)floor((c1 + 0.5) * L1.ssx - 0.5) + 2);
+    T.sy_lo = u(max(0, (int)floor((ay0 + 0.5) * L1.ssy - 0.5) - 2));
+    const int by1 = min(L0.h - 1, (int)floor((ay1 + 0.5) * L1.ssy - 0.5) + 2);
+    T.xa = u(bx0 & ~15);
+    T.nc = u(((bx1 - T.xa) >> 4) + 1);
+    T.items = u((by1 - T.sy_lo + 1) * T.nc);
+    T.mul = u(((1 << 20) + T.nc - 1) / T.nc);
+    T.src = pyr + (long long)f * g.pyr_frame_bytes + L0.off;
+    T.sstep = L0.stride;
+    {
+        uint4 v0, v1, v2, v3, v4;
+        pyr_fetch(T, tid, v0, v1, v2, v3, v4);
+        if (tid < ncol) xs1[tid] = xtab[L1.xtab_off + c0 + tid];
+        if (tid < nrow) ys1[tid] = ytab[L1.ytab_off + ay0 + tid];
+        if (tid < tw) xs2[tid] = xtab[L2.xtab_off + tx0 + tid];
+        if (tid < th) ys2[tid] = ytab[L2.ytab_off + ty0 + tid];
+        pyr_stage(T, tid, S, v0, 0);
+        pyr_stage(T, tid, S, v1, 1);
+        pyr_stage(T, tid, S, v2, 2);
+        pyr_stage(T, tid, S, v3, 3);
+        pyr_stage(T, tid, S, v4, 4);
+    }
+    __syncthreads();
+    // level l: thread = (quad q of 4 columns, first row r0), rows r0 + p * rpp
+    const int ncq = (ncol + 3) >> 2, rpp = 256 / ncq;
+    const int q = tid % ncq, r0 = tid / ncq;
+    const bool act = r0 < rpp;
+    uint32_t out[PP_MAXP];
+    if (act) {
+        uint32_t sel0[2], sel1[2], wdv[2];
+        us2 a0[2], a1[2];
+        int2 xv[4];
+        bool fits = true;
+#pragma unroll
+        for (int k = 0; k < 4; k++) xv[k] = xs1[min(4 * q + k, ncol - 1)];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int2 xv0 = xv[2 * j], xv1 = xv[2 * j + 1];
+            const int s00 = (xv0.x & 0xffff) - T.xa, s01 = (xv0.x >> 16) - T.xa;
+            const int s10 = (xv1.x & 0xffff) - T.xa, s11 = (xv1.x >> 16) - T.xa;
+            const int wd = s00 >> 2;
+            const int e00 = s00 - 4 * wd, e01 = s01 - 4 * wd, e10 = s10 - 4 * wd, e11 = s11 - 4 * wd;
+            fits = fits && max(e01, e11) <= 7 && min(e00, e10) >= 0;
+            sel0[j] = (uint32_t)e00 | 0x0c00u | ((uint32_t)e01 << 16) | 0x0c000000u;
+            sel1[j] = (uint32_t)e10 | 0x0c00u | ((uint32_t)e11 << 16) | 0x0c000000u;
+            wdv[j] = (uint32_t)wd;
+            a0[j] = *reinterpret_cast<const us2*>(&xv0.y);
+            a1[j] = *reinterpret_cast<const us2*>(&xv1.y);
+        }
+        const uint32_t* S32 = reinterpret_cast<const uint32_t*>(S);
+        auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
+            const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
+            return *reinterpret_cast<const us2*>(&r);
+        };
+#pragma unroll
+        for (int pp = 0; pp < PP_MAXP; pp++) {
+            const int r = r0 + pp * rpp;
+            out[pp] = 0;
+            if (r >= nrow) break;
+            const int2 yv = ys1[r];
+            if (fits) {
+                const int rr0 = ((yv.x & 0xffff) - T.sy_lo) * (PYR_SW / 4), rr1 = ((yv.x >> 16) - T.sy_lo) * (PYR_SW / 4);
+                const uint32_t b0 = (uint32_t)yv.y << 16, b1 = (uint32_t)yv.y & 0xffff0000u;
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const uint32_t* s0 = S32 + rr0 + wdv[j];
+                    const uint32_t* s1 = S32 + rr1 + wdv[j];
+                    const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
+                    const uint32_t h0a = __builtin_amdgcn_udot2(tap(w01, w00, sel0[j]), a0[j], 0u, false) >> 4;
+                    const uint32_t h1a = __builtin_amdgcn_udot2(tap(w11, w10, sel0[j]), a0[j], 0u, false) >> 4;
+                    const uint32_t h0b = __builtin_amdgcn_udot2(tap(w01, w00, sel1[j]), a1[j], 0u, false) >> 4;
+                    const uint32_t h1b = __builtin_amdgcn_udot2(tap(w11, w10, sel1[j]), a1[j], 0u, false) >> 4;
+                    const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
+                    const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
+                    out[pp] |= (va | (vb << 8)) << (16 * j);
+                }
+            } else {   // taps outside the 8-byte windows (not at the supported scale factors)
+#pragma unroll
+                for (int k = 0; k < 4; k++) out[pp] |= pyr_px_generic(S, xv[k], yv, T.xa, T.sy_lo) << (8 * k);
+            }
+        }
+    }
+    __syncthreads();   // every read of the level-(l-1) rectangle done: S now takes the level-l one
+    if (act) {
+        uint8_t* lrow = pyr + (long long)f * g.pyr_frame_bytes + L1.off + c0 + 4 * q;
+        // columns past c1 hold clamped-coefficient values: never written to the slab (a
+        // neighbouring workgroup writes the true ones there)
+        const bool full = c0 + 4 * q + 3 <= c1;
+#pragma unroll
+        for (int pp = 0; pp < PP_MAXP; pp++) {
+            const int r = r0 + pp * rpp;
+            if (r >= nrow) break;
+            *reinterpret_cast<uint32_t*>(&S[r * PYR_SW + 4 * q]) = out[pp];
+            uint8_t* dst = lrow + (long long)(ay0 + r) * L1.stride;
+            if (full) {
+                *reinterpret_cast<uint32_t*>(dst) = out[pp];
+            } else {
+                for (int k = 0; k < 3; k++)
+                    if (c0 + 4 * q + k <= c1) dst[k] = (uint8_t)(out[pp] >> (8 * k));
+            }
+        }
+    }
+    __syncthreads();
+    pyr_tile_compute(g, L2, f, pyr, S, xs2, ys2, tx0, ty0, tw, th, c0, ay0);
+}
+
+// Host check of pyramid_pair_kernel's capacities at the level pair's scale factors (with margins
+// for the floor / alignment slack of the conservative rectangles).
+static bool pyr_pair_fits(const Geom& g, int l) {
+    const double s1x = g.lv[l].ssx, s1y = g.lv[l].ssy, s2x = g.lv[l + 1].ssx, s2y = g.lv[l + 1].ssy;
+    const int ncol = (int)std::ceil(PYR_TW * s2x) + 10, nrow = (int)std::ceil(PYR_TH * s2y) + 7;
+    const int ncq = (ncol + 3) / 4, rpp = 256 / ncq;
+    const int bw = (int)std::ceil(ncol * s1x) + 7 + 15, bh = (int)std::ceil(nrow * s1y) + 7;
+    return ncol + 8 <= PYR_SW && nrow <= PYR_SH && (nrow + rpp - 1) / rpp <= PP_MAXP && bw <= PYR_SW && bh <= PYR_SH &&
+           bh * ((bw + 15) / 16) <= PYR_PF * 256;
+}
+
 // ------------------------------------------------------------------------------------------
 // 2. FAST per cell
 // ------------------------------------------------------------------------------------------
@@ -1905,6 +2066,7 @@ struct orbx_extractor {
     size_t fast_lds = 0;
     int fast_cpw = 4;   // FAST cells per wavefront (1 -> 4: -3 % at C2; ORBX_FAST_CPW)
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
+    bool pyr_pair = true;   // pyramid_pair_kernel for levels (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
     // level-split overlap (launch_chunk): level 0's FAST + quadtree on a side stream.  Off by
@@ -2211,10 +2373,19 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(256), (uint32_t)h->qt_lds, s, g,
                            cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0);
     };
-    auto pyramid = [&](int l) {
+    // levels l and l+1 in one pyramid_pair_kernel launch where the shapes fit its LDS rectangles
+    // (returns the number of extra levels built)
+    auto pyramid = [&](int l) -> int {
+        if (h->pyr_pair && l >= 2 && l + 1 < g.nlevels && pyr_pair_fits(g, l)) {
+            const int ntx = (g.lv[l + 1].w + PYR_TW - 1) / PYR_TW, nty = (g.lv[l + 1].h + PYR_TH - 1) / PYR_TH;
+            launch_timed(h, 0, pyramid_pair_kernel, dim3((unsigned)ntx, (unsigned)nty, (unsigned)F), dim3(256), 0u, st,
+                         g, l, pyr, h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
+            return 1;
+        }
         const int ntx = (g.lv[l].w + PYR_TW - 1) / PYR_TW, nty = (g.lv[l].h + PYR_TH - 1) / PYR_TH;
         launch_timed(h, 0, pyramid_level_kernel, dim3((unsigned)ntx, (unsigned)nty, (unsigned)F), dim3(256), 0u, st, g, l,
                      d_imgs, fstride, step, pyr, h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
+        return 0;
     };
     const int nc0 = g.lv[0].ncells;
     if (side && nc0 > 0 && g.nlevels > 1) {
@@ -2226,14 +2397,14 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         quadtree(0, 1, side);
         (void)hipEventRecord(h->lvl_join, side);
         {
-            for (int l = 1; l < g.nlevels; l++) pyramid(l);
+            for (int l = 1; l < g.nlevels; l++) l += pyramid(l);
         }
         fast(nc0, g.ncells_total - nc0, st);
         quadtree(1, g.nlevels - 1, st);
         (void)hipStreamWaitEvent(st, h->lvl_join, 0);
     } else {
         {
-            for (int l = 1; l < g.nlevels; l++) pyramid(l);
+            for (int l = 1; l < g.nlevels; l++) l += pyramid(l);
         }
         fast(0, g.ncells_total, st);
         quadtree(0, g.nlevels, st);
@@ -2314,6 +2485,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
+    if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = atoi(e) != 0;
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     compute_tables(h);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
