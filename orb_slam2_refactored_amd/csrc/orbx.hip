@@ -420,7 +420,9 @@ __device__ __forceinline__ uint32_t pyr_px_generic(const uint8_t* S, int2 xv, in
     return (uint32_t)(v > 255 ? 255 : v);
 }
 
-__global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, uint8_t* pyr, const int2* __restrict__ xtab,
+__global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const uint8_t* __restrict__ in,
+                                                           long long in_fstride, int in_step, uint8_t* pyr,
+                                                           const int2* __restrict__ xtab,
                                                            const int2* __restrict__ ytab) {
     __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW + 16];
     __shared__ int2 xs1[PYR_SW], ys1[PYR_SH], xs2[PYR_TW], ys2[PYR_TH];
@@ -451,8 +453,7 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, uint8_
     T.nc = u(((bx1 - T.xa) >> 4) + 1);
     T.items = u((by1 - T.sy_lo + 1) * T.nc);
     T.mul = u(((1 << 20) + T.nc - 1) / T.nc);
-    T.src = pyr + (long long)f * g.pyr_frame_bytes + L0.off;
-    T.sstep = L0.stride;
+    T.src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &T.sstep);   // 16-byte aligned (host)
     {
         uint4 v0, v1, v2, v3, v4;
         pyr_fetch(T, tid, v0, v1, v2, v3, v4);
@@ -2066,7 +2067,7 @@ struct orbx_extractor {
     size_t fast_lds = 0;
     int fast_cpw = 4;   // FAST cells per wavefront (1 -> 4: -3 % at C2; ORBX_FAST_CPW)
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
-    bool pyr_pair = true;   // pyramid_pair_kernel for levels (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
+    int pyr_pair = 2;   // pyramid_pair_kernel for levels (1,2), (3,4), (5,6) (level 0 16-byte aligned); 1: (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
     // level-split overlap (launch_chunk): level 0's FAST + quadtree on a side stream.  Off by
@@ -2376,10 +2377,12 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     // levels l and l+1 in one pyramid_pair_kernel launch where the shapes fit its LDS rectangles
     // (returns the number of extra levels built)
     auto pyramid = [&](int l) -> int {
-        if (h->pyr_pair && l >= 2 && l + 1 < g.nlevels && pyr_pair_fits(g, l)) {
+        const int first = h->pyr_pair == 2 ? 1 : 2;   // pairs (1,2), (3,4), (5,6) or (2,3), (4,5), (6,7)
+        const bool a16 = l > 1 || (((uintptr_t)d_imgs | (uintptr_t)fstride | (uintptr_t)step) & 15) == 0;
+        if (h->pyr_pair && l >= first && (l - first) % 2 == 0 && l + 1 < g.nlevels && a16 && pyr_pair_fits(g, l)) {
             const int ntx = (g.lv[l + 1].w + PYR_TW - 1) / PYR_TW, nty = (g.lv[l + 1].h + PYR_TH - 1) / PYR_TH;
             launch_timed(h, 0, pyramid_pair_kernel, dim3((unsigned)ntx, (unsigned)nty, (unsigned)F), dim3(256), 0u, st,
-                         g, l, pyr, h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
+                         g, l, d_imgs, fstride, step, pyr, h->d_xtab.as<int2>(), h->d_ytab.as<int2>());
             return 1;
         }
         const int ntx = (g.lv[l].w + PYR_TW - 1) / PYR_TW, nty = (g.lv[l].h + PYR_TH - 1) / PYR_TH;
@@ -2485,7 +2488,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
-    if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = atoi(e) != 0;
+    if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     compute_tables(h);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
