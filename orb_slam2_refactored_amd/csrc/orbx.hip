@@ -1948,14 +1948,16 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         }
         const int c0 = R[21 * RS + 21 + u];
         m10 = (hv == 0 && u <= 15) ? u * c0 : 0;
+        // the disk mask as lane-constant multipliers (branch-free multiply-adds)
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const int vv = 2 * t + 1;
             const int v = vv + hv;
             const int um = hv ? (vv + 1 <= 15 ? c_umax_h[vv + 1] : -1) : c_umax_h[vv];
             const bool in = u >= -um && u <= um;
-            m01 += in ? v * (vp[t] - vm[t]) : 0;
-            m10 += in ? u * (vp[t] + vm[t]) : 0;
+            const int vin = in ? v : 0, uin = in ? u : 0;
+            m01 += vin * (vp[t] - vm[t]);
+            m10 += uin * (vp[t] + vm[t]);
         }
     }
     m10 = wave_sum_i32(m10);
