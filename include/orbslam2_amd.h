@@ -122,6 +122,27 @@ int orbm_bf_match_batch_device(const uint8_t* d_A, const int32_t* d_nA, int stri
 int orbm_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float nnratio, int th_low,
                   int32_t* best_idx, int32_t* best, int32_t* second, int32_t* match);
 
+/* CheckOrientation (src/ORBmatcher.cc:249-309) on a query-indexed match result, applied as
+ * SearchForInitialization applies it (:676-686): for every accepted query i (match[i] = j >= 0, in
+ * ascending i) the rotation bin is cvRound((angleB[j] - angleA[i] (+360 if < 0)) / 30), 30 bins
+ * (bin 30 -> 0); the bins are sorted by size with std::sort's unstable order (libstdc++), the top
+ * 1-3 are kept (a 2nd / 3rd bin below 10 % of the largest ends the kept set, :293-298) and every
+ * other match is reset to -1.  *nmatches = matches kept.  ORBmatcher(nnratio, checkOri=true)
+ * applies it after the brute-force search.  Angles are cv::KeyPoint::angle in [0, 360)
+ * (ORB_EINVAL otherwise; the reference CV_Asserts the bin).  Host memory, synchronous. */
+int orbm_check_orientation(const float* angleA, int nA, const float* angleB, int nB, int32_t* match,
+                           int32_t* nmatches);
+
+/* Batched device form on orbm_bf_match_batch_device's output: pair p's queries have angles
+ * d_angA[(p*capA + i)*kstrideA] (kstrideA = 7 with d_angA = &kps[0].angle of an orbx_keypoint
+ * array), its targets d_angB[(q*capB + j)*kstrideB] with q = d_pair_b ? d_pair_b[p] : p; d_nA[p]
+ * queries; d_match at p*strideM is updated in place; d_nmatches[p] (may be NULL).  One workgroup
+ * per pair; enqueue only. */
+int orbm_check_orientation_batch_device(const float* d_angA, int kstrideA, int capA, const int32_t* d_nA,
+                                        const float* d_angB, int kstrideB, int capB, const int32_t* d_pair_b,
+                                        int n_pairs, int32_t* d_match, int strideM, int32_t* d_nmatches,
+                                        void* stream);
+
 /* One keyframe's view for SearchForTriangulation (src/ORBmatcher.cc:768-866). */
 typedef struct orbm_tri_frame {
     int32_t        n;           /* keyframe->N */

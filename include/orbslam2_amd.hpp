@@ -132,12 +132,21 @@ public:
     // static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b) on 32-byte rows
     static int DescriptorDistance(const uint8_t* a, const uint8_t* b) { return orbm_descriptor_distance(a, b); }
 
-    // Brute-force best / second-best + ratio test over all rows (reference loop semantics).
-    void MatchBruteForce(const uint8_t* A, int nA, const uint8_t* B, int nB, std::vector<int>& match,
-                         int th_low = 50) const {
+    // Brute-force best / second-best + ratio test over all rows (reference loop semantics).  With
+    // checkOri (the default, as the reference's ORBmatcher(nnratio, checkOri=true)) CheckOrientation
+    // (ORBmatcher.cc:249-309) filters `match` as SearchForInitialization applies it (:676-686); the
+    // keypoint angles are then required.  Returns the match count.
+    int MatchBruteForce(const uint8_t* A, int nA, const uint8_t* B, int nB, std::vector<int>& match, int th_low = 50,
+                        const float* angleA = nullptr, const float* angleB = nullptr) const {
+        if (checkOri_ && (!angleA || !angleB))
+            throw std::invalid_argument("ORBmatcher(checkOri=true)::MatchBruteForce needs the keypoint angles");
         std::vector<int32_t> bi(nA), bd(nA), sd(nA), m(nA);
         check(orbm_bf_match(A, nA, B, nB, nnratio_, th_low, bi.data(), bd.data(), sd.data(), m.data()), "orbm_bf_match");
+        int32_t n = 0;
+        for (int i = 0; i < nA; i++) n += m[i] >= 0;
+        if (checkOri_) check(orbm_check_orientation(angleA, nA, angleB, nB, m.data(), &n), "orbm_check_orientation");
         match.assign(m.begin(), m.end());
+        return n;
     }
 
     // int SearchForTriangulation(kf1, kf2, F12, matchIds, onlyStereo) on flattened keyframes.

@@ -1546,6 +1546,43 @@ void oracle_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float n
     }
 }
 
+// CheckOrientation (ORBmatcher.cc:249-309), literally: vector<int> bins and std::sort (libstdc++'s
+// unstable order decides which of several equal-size bins are kept), on a query-indexed result as
+// SearchForInitialization builds it (:670-686): matchIds = (bestIdx2, idx1) in ascending idx1,
+// keypoints1 = B, keypoints2 = A, status = matches12 (indexed by idx1).
+int oracle_check_orientation(const float* angA, int nA, const float* angB, int32_t* match) {
+    const int HISTO_LENGTH = 30;
+    std::vector<std::pair<int, int>> matchIds;
+    for (int i = 0; i < nA; i++)
+        if (match[i] >= 0) matchIds.push_back(std::make_pair(match[i], i));
+    const float factor = 1.f / HISTO_LENGTH;
+    std::vector<int> hist[HISTO_LENGTH];
+    auto diffToBin = [=](float diff) {
+        if (diff < 0) diff += 360;
+        int bin = cv_round(factor * diff);
+        if (bin == HISTO_LENGTH) bin = 0;
+        return bin;
+    };
+    for (const auto& m : matchIds) {
+        const int bin = diffToBin(angB[m.first] - angA[m.second]);
+        if (bin < 0 || bin >= HISTO_LENGTH) return -1;   // CV_Assert
+        hist[bin].push_back(m.second);
+    }
+    std::sort(std::begin(hist), std::end(hist),
+              [](const std::vector<int>& l, const std::vector<int>& r) { return l.size() > r.size(); });
+    const size_t max1 = hist[0].size(), max2 = hist[1].size(), max3 = hist[2].size();
+    int eraseBin = 3;
+    if (max2 < 0.1 * max1) eraseBin = 1;
+    else if (max3 < 0.1 * max1) eraseBin = 2;
+    int reduction = 0;
+    for (int bin = eraseBin; bin < HISTO_LENGTH; bin++)
+        for (int i2 : hist[bin]) {
+            match[i2] = -1;
+            reduction++;
+        }
+    return (int)matchIds.size() - reduction;
+}
+
 // SearchForTriangulation (ORBmatcher.cc:768-866), checkOrientation = false.
 int oracle_search_for_triangulation(const orbm_tri_frame* f1, const orbm_tri_frame* f2, const float* F12,
                                     const float* ep2, const float* scale2, const float* sigma2, int only_stereo,

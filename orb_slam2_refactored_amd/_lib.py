@@ -86,6 +86,9 @@ SIGNATURES = {
     "orbm_bf_match_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, C.c_int, VP, C.c_int, C.c_float, C.c_int,
                                              VP, VP, VP, VP, VP]),
     "orbm_bf_match": (C.c_int, [VP, C.c_int, VP, C.c_int, C.c_float, C.c_int, VP, VP, VP, VP]),
+    "orbm_check_orientation": (C.c_int, [VP, C.c_int, VP, C.c_int, VP, C.POINTER(I32)]),
+    "orbm_check_orientation_batch_device": (C.c_int, [VP, C.c_int, C.c_int, VP, VP, C.c_int, C.c_int, VP, C.c_int,
+                                                      VP, C.c_int, VP, VP]),
     "orbm_search_for_triangulation": (C.c_int, [C.POINTER(TriFrame), C.POINTER(TriFrame), VP, VP, VP, VP,
                                                 C.c_int, C.c_int, VP, C.POINTER(I32)]),
     "orbm_compute_stereo_matches": (C.c_int, [C.POINTER(StereoView), C.POINTER(StereoView), VP, VP, C.c_float,

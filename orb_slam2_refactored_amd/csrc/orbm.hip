@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "common.h"
+#include "qt_sort.h"
 
 namespace orbamd {
 
@@ -245,6 +246,65 @@ static void launch_top2(const uint8_t* A, const int32_t* nA_arr, int nA_fixed, i
                        nnratio, th_low, bi, bd, sd, mt);
 }
 
+// ---------------------------------------------------------------------------------------------
+// CheckOrientation (src/ORBmatcher.cc:249-309) on a query-indexed brute-force result, applied the
+// way SearchForInitialization applies it (:676-686): matchIds = (bestIdx2, idx1) for every accepted
+// query in ascending idx1, keypoints1 = frame B, keypoints2 = frame A, so a match's bin is
+// diffToBin(angleB[j] - angleA[i]) and erasing sets match[i] = -1.  The histogram's 30 bins are
+// sorted by size with libstdc++'s unstable std::sort (qt_sort.h reproduces its move sequence, so
+// equal-size bins land where the reference puts them), then the bins from eraseBin on are erased.
+// One workgroup per pair: counts into LDS, one lane sorts 30 items, then the erase pass.
+constexpr int HISTO_LENGTH = 30;
+
+__device__ __forceinline__ int rot_bin(float angB, float angA) {
+    float diff = angB - angA;
+    if (diff < 0) diff += 360.f;
+    int bin = __float2int_rn((1.f / HISTO_LENGTH) * diff);   // cvRound: round half to even
+    if (bin == HISTO_LENGTH) bin = 0;
+    return min(max(bin, 0), HISTO_LENGTH - 1);   // angles outside [0, 360) (the reference asserts)
+}
+
+__global__ __launch_bounds__(256) void check_orientation_kernel(
+    const float* __restrict__ angA, int kstrideA, int capA, const int32_t* __restrict__ nA_arr,
+    const float* __restrict__ angB, int kstrideB, int capB, const int32_t* __restrict__ pair_b,
+    int32_t* __restrict__ match, int strideM, int32_t* __restrict__ nmatch) {
+    __shared__ int hist[HISTO_LENGTH];
+    __shared__ uint32_t keep;
+    const int p = blockIdx.x, q = pair_b ? pair_b[p] : p, tid = threadIdx.x;
+    const int n = nA_arr[p];
+    const float* aA = angA + (long long)p * capA * kstrideA;
+    const float* aB = angB + (long long)q * capB * kstrideB;
+    int32_t* m = match + (long long)p * strideM;
+    if (tid < HISTO_LENGTH) hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += blockDim.x) {
+        const int j = m[i];
+        if (j >= 0) atomicAdd(&hist[rot_bin(aB[(long long)j * kstrideB], aA[(long long)i * kstrideA])], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        QtItem it[HISTO_LENGTH];
+        for (int b = 0; b < HISTO_LENGTH; b++) it[b] = QtItem{hist[b], b};
+        qt_sort(it, it + HISTO_LENGTH);
+        const double max1 = it[0].size, max2 = it[1].size, max3 = it[2].size;
+        const int eraseBin = max2 < 0.1 * max1 ? 1 : (max3 < 0.1 * max1 ? 2 : 3);
+        uint32_t k = 0;
+        int kept = 0;
+        for (int r = 0; r < eraseBin; r++) {
+            k |= 1u << it[r].node;
+            kept += it[r].size;
+        }
+        keep = k;
+        if (nmatch) nmatch[p] = kept;   // matchIds.size() - reduction
+    }
+    __syncthreads();
+    const uint32_t k = keep;
+    for (int i = tid; i < n; i += blockDim.x) {
+        const int j = m[i];
+        if (j >= 0 && !((k >> rot_bin(aB[(long long)j * kstrideB], aA[(long long)i * kstrideA])) & 1u)) m[i] = -1;
+    }
+}
+
 struct TriQuery {
     int idx1;
     int beg2, end2;   // candidate range in the kf2 index list
@@ -369,6 +429,52 @@ int orbm_bf_match(const uint8_t* A, int nA, const uint8_t* B, int nB, float nnra
         if (second) second[i] = h[2 * nA + i];
         if (match) match[i] = h[3 * nA + i];
     }
+    return ORB_OK;
+}
+
+int orbm_check_orientation_batch_device(const float* d_angA, int kstrideA, int capA, const int32_t* d_nA,
+                                        const float* d_angB, int kstrideB, int capB, const int32_t* d_pair_b,
+                                        int n_pairs, int32_t* d_match, int strideM, int32_t* d_nmatches,
+                                        void* stream) {
+    ORB_CHECK_ARG(n_pairs >= 0 && kstrideA > 0 && kstrideB > 0 && capA > 0 && capB > 0 && strideM > 0,
+                  "bad CheckOrientation arguments");
+    if (n_pairs == 0) return ORB_OK;
+    ORB_CHECK_ARG(d_angA && d_angB && d_nA && d_match, "null CheckOrientation argument");
+    hipLaunchKernelGGL(check_orientation_kernel, dim3((unsigned)n_pairs), dim3(256), 0, (hipStream_t)stream, d_angA,
+                       kstrideA, capA, d_nA, d_angB, kstrideB, capB, d_pair_b, d_match, strideM, d_nmatches);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+int orbm_check_orientation(const float* angA, int nA, const float* angB, int nB, int32_t* match, int32_t* nmatches) {
+    ORB_CHECK_ARG(nA >= 0 && nB >= 0 && match && (nA == 0 || angA), "bad CheckOrientation arguments");
+    for (int i = 0; i < nA; i++) {
+        ORB_CHECK_ARG(match[i] < nB && match[i] >= -1, "match index out of range");
+        ORB_CHECK_ARG(!(match[i] >= 0) || (angA[i] >= 0.f && angA[i] < 360.f && angB[match[i]] >= 0.f &&
+                                           angB[match[i]] < 360.f),
+                      "keypoint angle outside [0, 360) (CV_Assert in CheckOrientation)");
+    }
+    if (nmatches) *nmatches = 0;
+    if (nA == 0) return ORB_OK;
+    HostScratch& s = g_scratch;
+    int rc;
+    const size_t offB = align_up((size_t)nA * 4, 256);
+    if ((rc = s.o3.reserve(offB + (size_t)std::max(nB, 1) * 4))) return rc;
+    if ((rc = s.o4.reserve((size_t)nA * 4 + 8))) return rc;   // matches | nA | match count
+    float* dA = s.o3.as<float>();
+    float* dB = reinterpret_cast<float*>(s.o3.as<char>() + offB);
+    int32_t* dM = s.o4.as<int32_t>();
+    ORB_HIP_TRY(hipMemcpy(dA, angA, (size_t)nA * 4, hipMemcpyHostToDevice));
+    if (nB) ORB_HIP_TRY(hipMemcpy(dB, angB, (size_t)nB * 4, hipMemcpyHostToDevice));
+    ORB_HIP_TRY(hipMemcpy(dM, match, (size_t)nA * 4, hipMemcpyHostToDevice));
+    ORB_HIP_TRY(hipMemcpy(dM + nA, &nA, 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(check_orientation_kernel, dim3(1), dim3(256), 0, (hipStream_t)0, dA, 1, nA, dM + nA, dB, 1,
+                       std::max(nB, 1), nullptr, dM, nA, dM + nA + 1);
+    ORB_HIP_TRY(hipGetLastError());
+    ORB_HIP_TRY(hipMemcpy(match, dM, (size_t)nA * 4, hipMemcpyDeviceToHost));
+    int32_t nm = 0;
+    ORB_HIP_TRY(hipMemcpy(&nm, dM + nA + 1, 4, hipMemcpyDeviceToHost));
+    if (nmatches) *nmatches = nm;
     return ORB_OK;
 }
 

@@ -22,23 +22,44 @@ class ORBmatcher:
         b = np.ascontiguousarray(b, np.uint8).reshape(32)
         return lib().orbm_descriptor_distance(ptr(a), ptr(b))
 
-    def MatchBruteForce(self, descA, descB, th_low: int = TH_LOW):
+    def MatchBruteForce(self, descA, descB, th_low: int = TH_LOW, keypointsA=None, keypointsB=None):
         """Best / second-best search of every row of A over all rows of B with the reference loop
-        semantics (src/ORBmatcher.cc:477-507).  Returns (best_idx, best, second, match)."""
+        semantics (src/ORBmatcher.cc:477-507).  Returns (best_idx, best, second, match).
+
+        With checkOri (the constructor's default, as ORBmatcher(nnratio, checkOri=true)) the
+        rotation-histogram filter CheckOrientation (:249-309) is applied to `match` as
+        SearchForInitialization does (:676-686); it needs the keypoint angles, so keypointsA /
+        keypointsB (KP_DTYPE arrays or float angle arrays) are then required."""
         A = np.ascontiguousarray(descA, np.uint8).reshape(-1, 32)
         B = np.ascontiguousarray(descB, np.uint8).reshape(-1, 32)
         nA = len(A)
         bi, bd, sd, m = (np.zeros(nA, np.int32) for _ in range(4))
+        if self.checkOrientation_ and (keypointsA is None or keypointsB is None):
+            raise ValueError("ORBmatcher(checkOri=True): MatchBruteForce needs keypointsA / keypointsB "
+                             "(CheckOrientation reads their angles)")
         check(lib().orbm_bf_match(ptr(A), nA, ptr(B), len(B), C.c_float(self.fNNRatio_), th_low, ptr(bi), ptr(bd),
                                   ptr(sd), ptr(m)), "orbm_bf_match")
+        if self.checkOrientation_:
+            angA, angB = _angles(keypointsA), _angles(keypointsB)
+            if len(angA) != nA or len(angB) != len(B):
+                raise ValueError("keypoints and descriptors differ in length")
+            n = C.c_int32(0)
+            check(lib().orbm_check_orientation(ptr(angA), nA, ptr(angB), len(angB), ptr(m), C.byref(n)),
+                  "orbm_check_orientation")
         return bi, bd, sd, m
 
-    def match_batch_device(self, descA, nA, descB, nB, th_low: int = TH_LOW, out=None, stream=None, pair_b=None):
+    def match_batch_device(self, descA, nA, descB, nB, th_low: int = TH_LOW, out=None, stream=None, pair_b=None,
+                           kpsA=None, kpsB=None, nmatches=None):
         """Batched pairs on the GPU: descA [P, capA, 32], nA [P] int32, descB [Q, capB, 32], nB [Q];
         pair p uses B frame pair_b[p] (int32 [P] tensor) or p when pair_b is None.
-        Returns int32 tensor [4, P, capA] = (best_idx, best, second, match)."""
+        Returns int32 tensor [4, P, capA] = (best_idx, best, second, match).  With checkOri,
+        CheckOrientation runs on `match` (kpsA [P, capA, 7] / kpsB [Q, capB, 7], the
+        extract_batch_device keypoint slots, are then required; nmatches [P] int32 receives the
+        kept counts when given)."""
         import torch
         P, capA = descA.shape[0], descA.shape[1]
+        if self.checkOrientation_ and (kpsA is None or kpsB is None):
+            raise ValueError("ORBmatcher(checkOri=True): match_batch_device needs kpsA / kpsB")
         if out is None:
             out = torch.empty((4, P, capA), dtype=torch.int32, device=descA.device)
         pb = tptr(pair_b) if pair_b is not None else None
@@ -46,6 +67,17 @@ class ORBmatcher:
                                                P, C.c_float(self.fNNRatio_), th_low, tptr(out[0]), tptr(out[1]),
                                                tptr(out[2]), tptr(out[3]), stream_ptr(stream)),
               "orbm_bf_match_batch_device")
+        if self.checkOrientation_:
+            for t, cap in ((kpsA, capA), (kpsB, descB.shape[1])):
+                if t.dim() != 3 or t.shape[1] != cap or t.shape[2] != 7 or not t.is_contiguous():
+                    raise ValueError("keypoint slots must be contiguous [frames, cap, 7] like the descriptors")
+            angA = C.c_void_p(kpsA.data_ptr() + 12)   # &kps[0].angle (orbx_keypoint: x y size angle ...)
+            angB = C.c_void_p(kpsB.data_ptr() + 12)
+            check(lib().orbm_check_orientation_batch_device(angA, 7, capA, tptr(nA), angB, 7, descB.shape[1], pb, P,
+                                                            tptr(out[3]), capA,
+                                                            tptr(nmatches) if nmatches is not None else None,
+                                                            stream_ptr(stream)),
+                  "orbm_check_orientation_batch_device")
         return out
 
     def SearchForTriangulation(self, kf1, kf2, F12, onlyStereo: bool = False):
@@ -80,6 +112,17 @@ class ORBmatcher:
         out = out[:n1]
         idx1 = np.nonzero(out >= 0)[0]
         return [(int(i), int(out[i])) for i in idx1], out
+
+
+def _angles(kps):
+    """float32 angles from a KP_DTYPE keypoint array, an [N, 7] slot array or a plain angle array."""
+    from ._lib import KP_DTYPE
+    a = np.asarray(kps)
+    if a.dtype == KP_DTYPE:
+        return np.ascontiguousarray(a["angle"], np.float32)
+    if a.ndim == 2 and a.shape[1] == 7:
+        return np.ascontiguousarray(np.ascontiguousarray(a).view(np.float32)[:, 3])
+    return np.ascontiguousarray(a, np.float32).reshape(-1)
 
 
 def _stereo_view(kps, desc, pyramid):

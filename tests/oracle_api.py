@@ -157,6 +157,17 @@ def bf_match(A, B, nnratio=0.6, th_low=50):
     return bi, bd, sd, m
 
 
+def check_orientation(angA, angB, match):
+    """CheckOrientation (ORBmatcher.cc:249-309) on a query-indexed match (SearchForInitialization
+    convention): returns (match after the filter, nmatches)."""
+    angA = np.ascontiguousarray(angA, np.float32)
+    angB = np.ascontiguousarray(angB, np.float32)
+    m = np.array(match, np.int32, copy=True)
+    n = lib().oracle_check_orientation(ptr(angA), len(m), ptr(angB), ptr(m))
+    assert n >= 0, "bin out of range"
+    return m, n
+
+
 def descriptor_distance(a, b):
     a = np.ascontiguousarray(a, np.uint8)
     b = np.ascontiguousarray(b, np.uint8)

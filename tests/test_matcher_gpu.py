@@ -24,7 +24,7 @@ def test_bf_match_random(oracle, nA, nB):
     if nB > 10:
         B[7] = B[3]
         A[: min(nA, 5)] = B[3] ^ np.uint8(1)   # ties on best
-    m = ORBmatcher()
+    m = ORBmatcher(0.6, False)
     got = m.MatchBruteForce(A, B)
     exp = oracle.bf_match(A, B)
     for g, e in zip(got, exp):
@@ -44,7 +44,7 @@ def test_bf_match_chunked(oracle, nA, nB):
     A[:10] = B[5] ^ np.uint8(3)      # best tied across chunks
     A[10:20] = B[nB - 1] ^ np.uint8(1)
     B[nB - 2] = B[nB - 1] ^ np.uint8(1)   # second in the last chunk
-    got = ORBmatcher().MatchBruteForce(A, B)
+    got = ORBmatcher(0.6, False).MatchBruteForce(A, B)
     exp = oracle.bf_match(A, B)
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
@@ -56,7 +56,7 @@ def test_bf_match_near_duplicates(oracle):
     A = B[rng.integers(0, 900, 700)].copy()
     flip = (rng.random(A.shape) < 0.02)
     A ^= (flip * rng.integers(1, 256, A.shape)).astype(np.uint8)
-    got = ORBmatcher().MatchBruteForce(A, B)
+    got = ORBmatcher(0.6, False).MatchBruteForce(A, B)
     exp = oracle.bf_match(A, B)
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
@@ -66,13 +66,13 @@ def test_bf_match_near_duplicates(oracle):
 def test_bf_match_all_256():
     A = np.zeros((3, 32), np.uint8)
     B = np.full((4, 32), 255, np.uint8)
-    bi, bd, sd, m = ORBmatcher().MatchBruteForce(A, B)
+    bi, bd, sd, m = ORBmatcher(0.6, False).MatchBruteForce(A, B)
     assert bi.tolist() == [-1] * 3 and bd.tolist() == [256] * 3 and sd.tolist() == [256] * 3 and m.tolist() == [-1] * 3
 
 
 def test_bf_match_golden():
     g = np.load(GOLDEN / "bf_match_c1.npz")
-    bi, bd, sd, m = ORBmatcher().MatchBruteForce(g["A"], g["B"])
+    bi, bd, sd, m = ORBmatcher(0.6, False).MatchBruteForce(g["A"], g["B"])
     assert np.array_equal(bi, g["best_idx"]) and np.array_equal(bd, g["best"])
     assert np.array_equal(sd, g["second"]) and np.array_equal(m, g["match"])
 
@@ -92,7 +92,7 @@ def test_batch_device(oracle):
     nB = rng.integers(0, cap, P).astype(np.int32)
     A = np.stack([rand_desc(rng, cap) for _ in range(P)])
     B = np.stack([rand_desc(rng, cap) for _ in range(P)])
-    out = ORBmatcher().match_batch_device(torch.from_numpy(A).cuda(), torch.from_numpy(nA).cuda(),
+    out = ORBmatcher(0.6, False).match_batch_device(torch.from_numpy(A).cuda(), torch.from_numpy(nA).cuda(),
                                           torch.from_numpy(B).cuda(), torch.from_numpy(nB).cuda())
     out = out.cpu().numpy()
     for p in range(P):
@@ -101,7 +101,7 @@ def test_batch_device(oracle):
             assert np.array_equal(out[k, p, :nA[p]], exp[k])
     # pair -> B-frame indirection (match each frame against its predecessor without a copy)
     pb = np.array([(p - 1) % P for p in range(P)], np.int32)
-    out = ORBmatcher().match_batch_device(torch.from_numpy(A).cuda(), torch.from_numpy(nA).cuda(),
+    out = ORBmatcher(0.6, False).match_batch_device(torch.from_numpy(A).cuda(), torch.from_numpy(nA).cuda(),
                                           torch.from_numpy(B).cuda(), torch.from_numpy(nB).cuda(),
                                           pair_b=torch.from_numpy(pb).cuda()).cpu().numpy()
     for p in range(P):

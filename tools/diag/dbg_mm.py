@@ -13,7 +13,7 @@ for nA, nB in [(257, 513), (2000, 2000), (64, 255), (300, 40)]:
     A = rand_desc(rng, nA); B = rand_desc(rng, nB)
     if nB > 10:
         B[7] = B[3]; A[: min(nA, 5)] = B[3] ^ np.uint8(1)
-    bi, bd, sd, m = ORBmatcher().MatchBruteForce(A, B)
+    bi, bd, sd, m = ORBmatcher(0.6, False).MatchBruteForce(A, B)
     D = np.array([[hd(A[i], B[j]) for j in range(nB)] for i in range(min(nA, 300))])
     eb = D.min(1); ei = D.argmin(1)
     es = np.array([np.sort(r)[1] if len(r) > 1 else 256 for r in D])
