@@ -87,6 +87,17 @@ int orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int n_fr
                               int cols, size_t frame_stride, size_t step, orbx_keypoint* d_kps,
                               uint8_t* d_desc, int32_t* d_counts, int cap, void* stream);
 
+/* Device-side capacity checks of the batched path.  Every kernel of an extraction ORs a fault bit
+ * into the handle's fault word when a capacity bound is violated (1 quadtree node array, 2 keypoint
+ * outside the root nodes = the reference's CV_Assert :569, 4 FAST cell slot, 8 per-level output);
+ * the batch is then truncated, never written out of bounds.  The word is sticky across batches
+ * until read.  orbx_batch_status waits for `stream`, returns the mask in *fault_mask, clears it and
+ * returns ORB_EINTERNAL when it was non-zero (the single-frame orbx_extract checks it itself).
+ * orbx_fault_word_device returns the word's device address so a pipeline can copy it
+ * asynchronously (e.g. into pinned memory) instead of synchronising. */
+int orbx_batch_status(orbx_extractor* h, void* stream, uint32_t* fault_mask);
+int orbx_fault_word_device(orbx_extractor* h, uint32_t** d_fault);
+
 /* Device pointer to the batch's pyramid (frame f, level s) for downstream consumers
  * (ComputeStereoMatches reads GetImagePyramid(), ORBmatcher.cc:165-166). */
 int orbx_pyramid_device(const orbx_extractor* h, int frame, int level, const uint8_t** ptr,
@@ -170,6 +181,42 @@ int orbm_search_for_triangulation(const orbm_tri_frame* kf1, const orbm_tri_fram
                                   const float* F12, const float* ep2, const float* scale2,
                                   const float* sigma2, int n_levels, int only_stereo,
                                   int32_t* match12, int32_t* nmatches);
+
+/* Batched SearchForTriangulation on HBM-resident extractor output (orbx_extract_batch_device slots),
+ * e.g. the neighbour-keyframe loop of LocalMapping::CreateNewMapPoints (LocalMapping.cc:380-430)
+ * issued as one launch.  Pair p matches keyframe frame1[p] of set 1 (slots at kps1 / desc1 +
+ * frame*cap1, counts1[frame]) against frame2[p] of set 2 (NULL index arrays: p).  Sets 1 and 2 may
+ * be the same arrays.  Per pair: F12 (9 floats, row-major, from ComputeF12 :55-71) and ep2 (2
+ * floats, kf1's camera centre projected by kf2, :772-773; may be non-finite).  uright / has_mappoint
+ * per slot (NULL: every keypoint monocular / without a MapPoint).  FeatureVectors in
+ * orbv_transform_batch_device's layout (node ids / offsets / indices at frame*fv_cap, offsets at
+ * frame*(fv_cap+1), fv_n_nodes[frame]); NULL for both sets = one node holding every keypoint
+ * (all-pairs search under the gates, the vocabulary-free C3 setup).  kf2's scale factors / sigma^2
+ * are host arrays of n_levels (<= ORBM_TRI_MAX_LEVELS).  Outputs: d_match12[p*cap1 + idx1] = idx2
+ * or -1 for idx1 < counts1; d_nmatches[p].  checkOrientation is false at the caller
+ * (LocalMapping.cc:388).  Enqueue only on `stream`. */
+#define ORBM_TRI_MAX_LEVELS 32
+typedef struct orbm_tri_batch {
+    int32_t n_pairs;
+    int32_t cap1, cap2;
+    const orbx_keypoint* kps1; const uint8_t* desc1; const int32_t* counts1;
+    const float* uright1; const uint8_t* has_mappoint1;
+    const orbx_keypoint* kps2; const uint8_t* desc2; const int32_t* counts2;
+    const float* uright2; const uint8_t* has_mappoint2;
+    const int32_t* frame1; const int32_t* frame2;
+    const float* F12;           /* n_pairs x 9 */
+    const float* ep2;           /* n_pairs x 2 */
+    const uint32_t* fv_node1; const int32_t* fv_off1; const int32_t* fv_idx1; const int32_t* fv_n_nodes1;
+    const uint32_t* fv_node2; const int32_t* fv_off2; const int32_t* fv_idx2; const int32_t* fv_n_nodes2;
+    int32_t fv_cap1, fv_cap2;
+    int32_t n_levels;
+    const float* scale_factors2; /* host, n_levels */
+    const float* sigma2;         /* host, n_levels */
+    int32_t only_stereo;
+} orbm_tri_batch;
+
+int orbm_search_for_triangulation_batch_device(const orbm_tri_batch* b, int32_t* d_match12, int32_t* d_nmatches,
+                                               void* stream);
 
 /* Stereo matching.  Replaces ComputeStereoMatches (src/ORBmatcher.cc:72-247, PatchDistance
  * :60-68; called from Frame construction for stereo input, System.cc:458-461): per left keypoint the

@@ -24,6 +24,20 @@ class TriFrame(C.Structure):
                 ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("indices", C.c_void_p)]
 
 
+class TriBatch(C.Structure):
+    """orbm_tri_batch (include/orbslam2_amd.h)."""
+    _fields_ = [("n_pairs", C.c_int32), ("cap1", C.c_int32), ("cap2", C.c_int32),
+                ("kps1", C.c_void_p), ("desc1", C.c_void_p), ("counts1", C.c_void_p), ("uright1", C.c_void_p),
+                ("has_mappoint1", C.c_void_p), ("kps2", C.c_void_p), ("desc2", C.c_void_p), ("counts2", C.c_void_p),
+                ("uright2", C.c_void_p), ("has_mappoint2", C.c_void_p), ("frame1", C.c_void_p),
+                ("frame2", C.c_void_p), ("F12", C.c_void_p), ("ep2", C.c_void_p),
+                ("fv_node1", C.c_void_p), ("fv_off1", C.c_void_p), ("fv_idx1", C.c_void_p),
+                ("fv_n_nodes1", C.c_void_p), ("fv_node2", C.c_void_p), ("fv_off2", C.c_void_p),
+                ("fv_idx2", C.c_void_p), ("fv_n_nodes2", C.c_void_p), ("fv_cap1", C.c_int32),
+                ("fv_cap2", C.c_int32), ("n_levels", C.c_int32), ("scale_factors2", C.c_void_p),
+                ("sigma2", C.c_void_p), ("only_stereo", C.c_int32)]
+
+
 class StereoView(C.Structure):
     _fields_ = [("n", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("n_levels", C.c_int32),
                 ("level", C.c_void_p), ("level_rows", C.c_void_p), ("level_cols", C.c_void_p),
@@ -79,6 +93,8 @@ SIGNATURES = {
     "orbx_extract": (C.c_int, [VP, VP, C.c_int, C.c_int, SZ, VP, VP, C.c_int, C.POINTER(C.c_int)]),
     "orbx_pyramid_level": (C.c_int, [VP, C.c_int, VP, SZ, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "orbx_extract_batch_device": (C.c_int, [VP, VP, C.c_int, C.c_int, C.c_int, SZ, SZ, VP, VP, VP, C.c_int, VP]),
+    "orbx_batch_status": (C.c_int, [VP, VP, C.POINTER(C.c_uint32)]),
+    "orbx_fault_word_device": (C.c_int, [VP, C.POINTER(VP)]),
     "orbx_pyramid_device": (C.c_int, [VP, C.c_int, C.c_int, C.POINTER(VP), C.POINTER(C.c_int),
                                       C.POINTER(C.c_int), C.POINTER(SZ)]),
     "orbm_descriptor_distance": (C.c_int, [VP, VP]),
@@ -91,6 +107,7 @@ SIGNATURES = {
                                                       VP, C.c_int, VP, VP]),
     "orbm_search_for_triangulation": (C.c_int, [C.POINTER(TriFrame), C.POINTER(TriFrame), VP, VP, VP, VP,
                                                 C.c_int, C.c_int, VP, C.POINTER(I32)]),
+    "orbm_search_for_triangulation_batch_device": (C.c_int, [C.POINTER(TriBatch), VP, VP, VP]),
     "orbm_compute_stereo_matches": (C.c_int, [C.POINTER(StereoView), C.POINTER(StereoView), VP, VP, C.c_float,
                                               C.c_float, VP, VP]),
     "orbx_stereo_matches_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, VP, VP, VP, C.c_int, C.c_float,

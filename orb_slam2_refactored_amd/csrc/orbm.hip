@@ -358,6 +358,203 @@ __global__ __launch_bounds__(256) void triangulation_kernel(const TriQuery* __re
     match12[i1] = bi;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batched SearchForTriangulation on extractor output (orbm_search_for_triangulation_batch_device).
+// Per query the reference keeps the LAST candidate (in kf2's index order) whose distance equals
+// the minimum over the gate-passing candidates with d <= TH_LOW: bestDist starts at TH_LOW, a
+// candidate is considered iff d <= bestDist (:823) and, if it passes the epipole / epipolar gates,
+// becomes the best.  `matched2` is never set (§0.5), so queries are independent.
+struct TriTables {
+    float scale2[ORBM_TRI_MAX_LEVELS];
+    float sigma2[ORBM_TRI_MAX_LEVELS];
+    int n_levels;
+};
+
+struct TriArgs {
+    const orbx_keypoint* kps1;
+    const uint8_t* desc1;
+    const int32_t* counts1;
+    const float* ur1;
+    const uint8_t* mp1;
+    const orbx_keypoint* kps2;
+    const uint8_t* desc2;
+    const int32_t* counts2;
+    const float* ur2;
+    const uint8_t* mp2;
+    const int32_t* frame1;
+    const int32_t* frame2;
+    const float* F12;
+    const float* ep2;
+    const uint32_t* fvn1;
+    const int32_t* fvo1;
+    const int32_t* fvi1;
+    const int32_t* fvc1;
+    const uint32_t* fvn2;
+    const int32_t* fvo2;
+    const int32_t* fvi2;
+    const int32_t* fvc2;
+    int cap1, cap2, fvcap1, fvcap2, only_stereo;
+    int32_t* match12;
+    int32_t* nmatches;
+};
+
+// Epipole (mono-mono pairs, :828-833) and epipolar-line (CheckDistEpipolarLine, :384-404) gates.
+// ep2 may be non-finite (a kf1 centre on kf2's principal plane, e.g. a rectified stereo pair): the
+// squared distance is then NaN or inf and the comparisons fall as in the reference.
+__device__ __forceinline__ bool tri_gates(float la, float lb, float lc, bool st1, bool st2, float x2, float y2, int o2,
+                                          float ep2x, float ep2y, const TriTables& t) {
+    o2 = min(max(o2, 0), t.n_levels - 1);
+    if (!st1 && !st2) {
+        const float dx = ep2x - x2, dy = ep2y - y2;
+        if (dx * dx + dy * dy < 100 * t.scale2[o2]) return false;
+    }
+    const float num = la * x2 + lb * y2 + lc;
+    const float den = la * la + lb * lb;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return (double)dsqr < 3.84 * (double)t.sigma2[o2];
+}
+
+__device__ __forceinline__ int hamming8(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+constexpr int TRI_CHUNK = 256;
+
+// Single BoW node holding every keypoint of both keyframes (no vocabulary): every
+// query scans kf2 in ascending index.  One lane per query, 256 queries per workgroup; kf2's
+// descriptors are staged through LDS in chunks of 256 and read as wavefront broadcasts.
+__global__ __launch_bounds__(256) void tri_all_kernel(TriArgs a, TriTables t) {
+    __shared__ uint4 sd[TRI_CHUNK * 2];
+    __shared__ uint32_t sv[TRI_CHUNK / 32];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int f1 = a.frame1 ? a.frame1[p] : p, f2 = a.frame2 ? a.frame2[p] : p;
+    const int n1 = a.counts1[f1], n2 = a.counts2[f2];
+    if (blockIdx.x * 256 >= n1) return;   // block-uniform
+    const int i1 = blockIdx.x * 256 + tid;
+    const long long g1 = (long long)f1 * a.cap1 + i1;
+    const bool in = i1 < n1;
+    const bool st1 = in && a.ur1 && a.ur1[g1] >= 0;
+    const bool act = in && !(a.mp1 && a.mp1[g1]) && (!a.only_stereo || st1);
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    float la = 0, lb = 0, lc = 0;
+    if (in) {
+        a0 = reinterpret_cast<const uint4*>(a.desc1)[2 * g1];
+        a1 = reinterpret_cast<const uint4*>(a.desc1)[2 * g1 + 1];
+        const float x1 = a.kps1[g1].x, y1 = a.kps1[g1].y;
+        const float* F = a.F12 + 9 * (long long)p;
+        la = x1 * F[0] + y1 * F[3] + F[6];   // l = x1' F12 (:391-393)
+        lb = x1 * F[1] + y1 * F[4] + F[7];
+        lc = x1 * F[2] + y1 * F[5] + F[8];
+    }
+    const float ep2x = a.ep2[2 * p], ep2y = a.ep2[2 * p + 1];
+    const long long base2 = (long long)f2 * a.cap2;
+    int bd = 50, bi = -1;   // TH_LOW
+    for (int c0 = 0; c0 < n2; c0 += TRI_CHUNK) {
+        {
+            const int j = c0 + tid;
+            bool v = false;
+            if (j < n2) {
+                const long long g2 = base2 + j;
+                sd[2 * tid] = reinterpret_cast<const uint4*>(a.desc2)[2 * g2];
+                sd[2 * tid + 1] = reinterpret_cast<const uint4*>(a.desc2)[2 * g2 + 1];
+                v = !(a.mp2 && a.mp2[g2]) && (!a.only_stereo || (a.ur2 && a.ur2[g2] >= 0));
+            }
+            const uint64_t bal = __ballot(v);
+            if ((tid & 63) == 0) {
+                sv[2 * (tid >> 6)] = (uint32_t)bal;
+                sv[2 * (tid >> 6) + 1] = (uint32_t)(bal >> 32);
+            }
+        }
+        __syncthreads();
+        if (act) {
+            const int m = min(TRI_CHUNK, n2 - c0);
+            for (int k = 0; k < m; k++) {
+                if (!((sv[k >> 5] >> (k & 31)) & 1u)) continue;   // uniform (every lane reads the same k)
+                const int d = hamming8(a0, a1, sd[2 * k], sd[2 * k + 1]);
+                if (d > bd) continue;
+                const long long g2 = base2 + c0 + k;
+                const orbx_keypoint kp2 = a.kps2[g2];
+                const bool st2 = a.ur2 && a.ur2[g2] >= 0;
+                if (tri_gates(la, lb, lc, st1, st2, kp2.x, kp2.y, kp2.octave, ep2x, ep2y, t)) {
+                    bi = c0 + k;
+                    bd = d;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (in) a.match12[(long long)p * a.cap1 + i1] = bi;
+    const uint64_t got = __ballot(in && bi >= 0);
+    if ((tid & 63) == 0 && got) atomicAdd(a.nmatches + p, (int)__popcll(got));
+}
+
+// General DBoW2 FeatureVectors (orbv_transform_batch_device layout): FeatureVectorIterator
+// (:406-450) pairs equal node ids; each wavefront takes kf1 nodes in turn, finds the node in kf2's
+// ascending list by binary search, and maps the node's queries one per lane over the node's kf2
+// candidates (ascending, as stored).
+__global__ __launch_bounds__(256) void tri_fv_kernel(TriArgs a, TriTables t) {
+    const int p = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int f1 = a.frame1 ? a.frame1[p] : p, f2 = a.frame2 ? a.frame2[p] : p;
+    const int nn1 = a.fvc1[f1], nn2 = a.fvc2[f2];
+    const uint32_t* node1 = a.fvn1 + (long long)f1 * a.fvcap1;
+    const uint32_t* node2 = a.fvn2 + (long long)f2 * a.fvcap2;
+    const int32_t* off1 = a.fvo1 + (long long)f1 * (a.fvcap1 + 1);
+    const int32_t* off2 = a.fvo2 + (long long)f2 * (a.fvcap2 + 1);
+    const int32_t* idx1 = a.fvi1 + (long long)f1 * a.fvcap1;
+    const int32_t* idx2 = a.fvi2 + (long long)f2 * a.fvcap2;
+    const long long base1 = (long long)f1 * a.cap1, base2 = (long long)f2 * a.cap2;
+    const float* F = a.F12 + 9 * (long long)p;
+    const float ep2x = a.ep2[2 * p], ep2y = a.ep2[2 * p + 1];
+    int found = 0;
+    for (int na = w; na < nn1; na += 4) {
+        const uint32_t id = node1[na];
+        int lo = 0, hi = nn2;   // lower_bound
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (node2[mid] < id) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo >= nn2 || node2[lo] != id) continue;
+        const int c0 = off2[lo], c1 = off2[lo + 1];
+        for (int u = off1[na] + lane; u < off1[na + 1]; u += 64) {
+            const int i1 = idx1[u];
+            const long long g1 = base1 + i1;
+            const bool st1 = a.ur1 && a.ur1[g1] >= 0;
+            if ((a.mp1 && a.mp1[g1]) || (a.only_stereo && !st1)) continue;
+            const uint4 a0 = reinterpret_cast<const uint4*>(a.desc1)[2 * g1];
+            const uint4 a1 = reinterpret_cast<const uint4*>(a.desc1)[2 * g1 + 1];
+            const float x1 = a.kps1[g1].x, y1 = a.kps1[g1].y;
+            const float la = x1 * F[0] + y1 * F[3] + F[6];
+            const float lb = x1 * F[1] + y1 * F[4] + F[7];
+            const float lc = x1 * F[2] + y1 * F[5] + F[8];
+            int bd = 50, bi = -1;
+            for (int v = c0; v < c1; v++) {
+                const int i2 = idx2[v];
+                const long long g2 = base2 + i2;
+                if (a.mp2 && a.mp2[g2]) continue;
+                const bool st2 = a.ur2 && a.ur2[g2] >= 0;
+                if (a.only_stereo && !st2) continue;
+                const uint4* b = reinterpret_cast<const uint4*>(a.desc2) + 2 * g2;
+                const int d = hamming8(a0, a1, b[0], b[1]);
+                if (d > bd) continue;
+                const orbx_keypoint kp2 = a.kps2[g2];
+                if (tri_gates(la, lb, lc, st1, st2, kp2.x, kp2.y, kp2.octave, ep2x, ep2y, t)) {
+                    bi = i2;
+                    bd = d;
+                }
+            }
+            if (bi >= 0) {
+                a.match12[(long long)p * a.cap1 + i1] = bi;
+                found++;
+            }
+        }
+    }
+    const int tot = __reduce_add_sync(~0ull, found);
+    if (lane == 0 && tot) atomicAdd(a.nmatches + p, tot);
+}
+
 }  // namespace orbamd
 
 using namespace orbamd;
@@ -475,6 +672,46 @@ int orbm_check_orientation(const float* angA, int nA, const float* angB, int nB,
     int32_t nm = 0;
     ORB_HIP_TRY(hipMemcpy(&nm, dM + nA + 1, 4, hipMemcpyDeviceToHost));
     if (nmatches) *nmatches = nm;
+    return ORB_OK;
+}
+
+int orbm_search_for_triangulation_batch_device(const orbm_tri_batch* b, int32_t* d_match12, int32_t* d_nmatches,
+                                               void* stream) {
+    ORB_CHECK_ARG(b && d_match12 && d_nmatches, "null argument");
+    ORB_CHECK_ARG(b->n_pairs >= 0 && b->cap1 > 0 && b->cap2 > 0, "bad pair count / capacities");
+    ORB_CHECK_ARG(b->n_levels > 0 && b->n_levels <= ORBM_TRI_MAX_LEVELS && b->scale_factors2 && b->sigma2,
+                  "n_levels must be 1..ORBM_TRI_MAX_LEVELS with host scale / sigma2 tables");
+    if (b->n_pairs == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kps1 && b->desc1 && b->counts1 && b->kps2 && b->desc2 && b->counts2 && b->F12 && b->ep2,
+                  "null keyframe arrays");
+    const bool fv1 = b->fv_node1 || b->fv_off1 || b->fv_idx1 || b->fv_n_nodes1;
+    const bool fv2 = b->fv_node2 || b->fv_off2 || b->fv_idx2 || b->fv_n_nodes2;
+    ORB_CHECK_ARG(fv1 == fv2, "give FeatureVectors for both keyframe sets or for neither");
+    if (fv1)
+        ORB_CHECK_ARG(b->fv_node1 && b->fv_off1 && b->fv_idx1 && b->fv_n_nodes1 && b->fv_node2 && b->fv_off2 &&
+                          b->fv_idx2 && b->fv_n_nodes2 && b->fv_cap1 > 0 && b->fv_cap2 > 0,
+                      "incomplete FeatureVector arrays");
+    ORB_CHECK_ARG(b->n_pairs <= 65535, "too many pairs in one launch");
+    TriTables t{};
+    for (int l = 0; l < b->n_levels; l++) {
+        t.scale2[l] = b->scale_factors2[l];
+        t.sigma2[l] = b->sigma2[l];
+    }
+    t.n_levels = b->n_levels;
+    TriArgs a{b->kps1, b->desc1, b->counts1, b->uright1, b->has_mappoint1, b->kps2, b->desc2, b->counts2, b->uright2,
+              b->has_mappoint2, b->frame1, b->frame2, b->F12, b->ep2, b->fv_node1, b->fv_off1, b->fv_idx1,
+              b->fv_n_nodes1, b->fv_node2, b->fv_off2, b->fv_idx2, b->fv_n_nodes2, b->cap1, b->cap2, b->fv_cap1,
+              b->fv_cap2, b->only_stereo ? 1 : 0, d_match12, d_nmatches};
+    hipStream_t st = (hipStream_t)stream;
+    ORB_HIP_TRY(hipMemsetAsync(d_nmatches, 0, (size_t)b->n_pairs * 4, st));
+    if (fv1) {
+        ORB_HIP_TRY(hipMemsetAsync(d_match12, 0xff, (size_t)b->n_pairs * b->cap1 * 4, st));
+        hipLaunchKernelGGL(tri_fv_kernel, dim3((unsigned)b->n_pairs), dim3(256), 0, st, a, t);
+    } else {
+        hipLaunchKernelGGL(tri_all_kernel, dim3((unsigned)((b->cap1 + 255) / 256), (unsigned)b->n_pairs), dim3(256), 0,
+                           st, a, t);
+    }
+    ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
 

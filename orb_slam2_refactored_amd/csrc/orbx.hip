@@ -2069,6 +2069,8 @@ struct orbx_extractor {
     size_t fast_lds = 0;
     int fast_cpw = 4;   // FAST cells per wavefront (1 -> 4: -3 % at C2; ORBX_FAST_CPW)
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
+    int debug_nc = 0;
+    uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
     int pyr_pair = 2;   // pyramid_pair_kernel for levels (1,2), (3,4), (5,6) (level 0 16-byte aligned); 1: (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
@@ -2253,6 +2255,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.cand_frame = std::max<long long>(cand, 1);
     g.out_frame = std::max(out, 1);
     NC = (int)align_up(std::max(NC, 256), 64);   // >= blockDim: the gather reuses the node scratch
+    if (h->debug_nc > 0) NC = (int)align_up(std::max(h->debug_nc, 256), 64);
     const int PTC = 2048;   // candidate points kept in LDS (P and T) when a level has at most this many (48 KiB in all: 3 WGs per CU)
     const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int)) +
                        (size_t)PTC * 8;
@@ -2310,8 +2313,10 @@ static int reserve_workspace(orbx_extractor* h, int frames) {
     if ((rc = h->d_T.reserve((size_t)frames * g.cand_frame * 4))) return rc;
     if ((rc = h->d_sel.reserve((size_t)frames * g.out_frame * 4))) return rc;
     if ((rc = h->d_selcnt.reserve((size_t)frames * g.nlevels * 4))) return rc;
-    if ((rc = h->d_fault.reserve(16))) return rc;
-    ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));
+    if (!h->d_fault.ptr) {   // sticky until read (orbx_batch_status / the host Extract)
+        if ((rc = h->d_fault.reserve(16))) return rc;
+        ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));
+    }
     h->ws_frames = frames;
     return ORB_OK;
 }
@@ -2492,6 +2497,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
+    if (const char* e = getenv("ORBX_DEBUG_NC")) h->debug_nc = atoi(e);
     compute_tables(h);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -2612,6 +2618,37 @@ int orbx_extract(orbx_extractor* h, const uint8_t* img, int rows, int cols, size
     ORB_HIP_TRY(hipMemcpyAsync(kps, h->d_kps.ptr, (size_t)total * sizeof(orbx_keypoint), hipMemcpyDeviceToHost, st));
     ORB_HIP_TRY(hipMemcpyAsync(desc, h->d_desc.ptr, (size_t)total * 32, hipMemcpyDeviceToHost, st));
     ORB_HIP_TRY(hipStreamSynchronize(st));
+    return ORB_OK;
+}
+
+int orbx_batch_status(orbx_extractor* h, void* stream, uint32_t* fault_mask) {
+    ORB_CHECK_ARG(h && fault_mask, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    *fault_mask = 0;
+    if (!h->d_fault.ptr) return ORB_OK;   // nothing has run
+    hipStream_t st = (hipStream_t)stream;
+    ORB_HIP_TRY(hipMemcpyAsync(&h->fault_host, h->d_fault.ptr, 4, hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipMemsetAsync(h->d_fault.ptr, 0, 4, st));
+    ORB_HIP_TRY(hipStreamSynchronize(st));
+    *fault_mask = h->fault_host;
+    if (h->fault_host) {
+        set_error("device capacity check failed in a batch (fault mask " + std::to_string(h->fault_host) + ")");
+        return ORB_EINTERNAL;
+    }
+    return ORB_OK;
+}
+
+int orbx_fault_word_device(orbx_extractor* h, uint32_t** d_fault) {
+    ORB_CHECK_ARG(h && d_fault, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    ORB_HIP_TRY(hipSetDevice(h->device));
+    int rc;
+    if (!h->d_fault.ptr) {
+        if ((rc = h->d_fault.reserve(16))) return rc;
+        ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));
+    }
+    *d_fault = h->d_fault.as<uint32_t>();
     return ORB_OK;
 }
 

@@ -149,10 +149,28 @@ class ORBextractor:
             desc_out = torch.empty((F, cap, 32), dtype=torch.uint8, device=dev)
         if counts_out is None:
             counts_out = torch.empty((F,), dtype=torch.int32, device=dev)
+        # caller-supplied outputs: the kernels write F x cap slots, so shapes, contiguity and device
+        # are checked here (a short or strided buffer would be written out of bounds)
+        for t, shape, dt in ((kps_out, (F, cap, 7), torch.int32), (desc_out, (F, cap, 32), torch.uint8)):
+            if tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"output slots must be contiguous {dt} {shape} on {dev}, got "
+                                 f"{t.dtype} {tuple(t.shape)} on {t.device}")
+        if counts_out.numel() < F or counts_out.dtype != torch.int32 or not counts_out.is_contiguous() or \
+                counts_out.device != dev:
+            raise ValueError("counts_out must be a contiguous int32 tensor of >= F entries on the frames' device")
+        if frames.stride(2) != 1:
+            raise ValueError("frames must have unit column stride (rows may be padded)")
         check(lib().orbx_extract_batch_device(self._h, tptr(frames), F, H, W, C.c_size_t(frames.stride(0)),
                                               C.c_size_t(frames.stride(1)), tptr(kps_out), tptr(desc_out),
                                               tptr(counts_out), cap, stream_ptr(stream)), "orbx_extract_batch_device")
         return kps_out, desc_out, counts_out
+
+    def batch_status(self, stream=None) -> int:
+        """Device capacity-check mask of the batches since the last call (0 = none tripped); waits
+        for `stream`.  Raises OrbError when a check tripped (the batch was truncated)."""
+        m = C.c_uint32(0)
+        check(lib().orbx_batch_status(self._h, stream_ptr(stream), C.byref(m)), "orbx_batch_status")
+        return m.value
 
     @staticmethod
     def kps_to_numpy(kps_i32_row):

@@ -114,6 +114,47 @@ class ORBmatcher:
         return [(int(i), int(out[i])) for i in idx1], out
 
 
+def search_for_triangulation_batch_device(kps1, desc1, counts1, kps2, desc2, counts2, F12, ep2, scale_factors2,
+                                          sigma2, frame1=None, frame2=None, uright1=None, uright2=None,
+                                          has_mappoint1=None, has_mappoint2=None, fv1=None, fv2=None,
+                                          only_stereo=False, out=None, stream=None):
+    """Batched SearchForTriangulation (src/ORBmatcher.cc:768-866) on extract_batch_device slots.
+
+    kps*/desc*/counts*: [F, cap, 7] int32 / [F, cap, 32] uint8 / [F] int32 tensors; pair p matches
+    frame frame1[p] of set 1 against frame2[p] of set 2 (int32 [P] tensors, default p); F12 [P, 9]
+    and ep2 [P, 2] float32 device tensors (the caller's ComputeF12 and epipole); scale_factors2 /
+    sigma2 host arrays (kf2's pyramid); uright* float32 [F, cap] / has_mappoint* uint8 [F, cap] or
+    None; fv1 / fv2 = (node, off, idx, n_nodes) from ORBVocabulary.transform_batch_device, or None
+    for a single node holding every keypoint.  Returns (match12 [P, cap1] int32, nmatches [P])."""
+    import torch
+    from ._lib import TriBatch
+    P = int(F12.shape[0])
+    cap1, cap2 = int(kps1.shape[1]), int(kps2.shape[1])
+    for k, d, cap in ((kps1, desc1, cap1), (kps2, desc2, cap2)):
+        if k.dim() != 3 or k.shape[2] != 7 or d.shape[:2] != k.shape[:2] or d.shape[2] != 32 or \
+                not k.is_contiguous() or not d.is_contiguous():
+            raise ValueError("keypoint / descriptor slots must be contiguous [F, cap, 7] / [F, cap, 32]")
+    if ep2.shape[0] != P or F12.shape[-1] != 9 or ep2.shape[-1] != 2:
+        raise ValueError("F12 must be [P, 9] and ep2 [P, 2]")
+    if out is None:
+        out = (torch.empty((P, cap1), dtype=torch.int32, device=kps1.device),
+               torch.empty((P,), dtype=torch.int32, device=kps1.device))
+    sf = np.ascontiguousarray(scale_factors2, np.float32)
+    s2 = np.ascontiguousarray(sigma2, np.float32)
+    opt = lambda t: tptr(t) if t is not None else None   # noqa: E731
+    f1 = fv1 if fv1 is not None else (None,) * 4
+    f2 = fv2 if fv2 is not None else (None,) * 4
+    b = TriBatch(P, cap1, cap2, tptr(kps1), tptr(desc1), tptr(counts1), opt(uright1), opt(has_mappoint1),
+                 tptr(kps2), tptr(desc2), tptr(counts2), opt(uright2), opt(has_mappoint2), opt(frame1), opt(frame2),
+                 tptr(F12), tptr(ep2), *[opt(t) for t in f1], *[opt(t) for t in f2],
+                 int(f1[0].shape[1]) if fv1 is not None else 0, int(f2[0].shape[1]) if fv2 is not None else 0,
+                 len(sf), ptr(sf), ptr(s2), int(only_stereo))
+    check(lib().orbm_search_for_triangulation_batch_device(C.byref(b), tptr(out[0]), tptr(out[1]),
+                                                           stream_ptr(stream)),
+          "orbm_search_for_triangulation_batch_device")
+    return out
+
+
 def _angles(kps):
     """float32 angles from a KP_DTYPE keypoint array, an [N, 7] slot array or a plain angle array."""
     from ._lib import KP_DTYPE

@@ -145,6 +145,27 @@ def stereo_pair(seed: int, width: int = 1242, height: int = 375, bf: float = KIT
     return L, np.clip(R, 0, 255).astype(np.uint8), zcol
 
 
+def stereo_tri_geometry(cam=KITTI):
+    """SearchForTriangulation geometry of the C3 setup: KF1 = the left camera at
+    [I|0], KF2 = the right camera at [I|(-bf/fx, 0, 0)].  Returns (F12, ep2) in float32 as the caller
+    computes them: F12 = K1^-T [t12]x R12 K2^-1 (ComputeF12, LocalMapping.cc:55-71, with the closed
+    -form inverse of the upper-triangular K) and ep2 = CameraProjection(pose2).WorldToImage(Ow1)
+    (ORBmatcher.cc:772-773, CameraProjection.h:49-55).  KF1's centre lies on KF2's principal plane,
+    so 1/Z = inf and ep2 = (-inf, NaN), exactly as the reference's float arithmetic gives it."""
+    f32 = np.float32
+    fx, fy, cx, cy = f32(cam["fx"]), f32(cam["fy"]), f32(cam["cx"]), f32(cam["cy"])
+    b = f32(cam["bf"]) / fx
+    t12 = np.array([b, 0, 0], f32)          # -R1w R2w^T t2w + t1w with t2w = (-b, 0, 0)
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]], f32)
+    Kinv = np.array([[f32(1) / fx, 0, -cx / fx], [0, f32(1) / fy, -cy / fy], [0, 0, 1]], f32)
+    F12 = (Kinv.T @ tx @ Kinv).astype(f32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        Xc = np.array([-b, 0, 0], f32)      # Rcw * Ow1 + tcw with Ow1 = 0
+        invz = f32(1) / Xc[2]
+        ep2 = np.array([invz * fx * Xc[0] + cx, invz * fy * Xc[1] + cy], f32)
+    return F12.reshape(9), ep2
+
+
 def make_pose_batch(seed: int = 0, n_frames: int = 8, n_edges=600, stereo_frac: float = 0.4,
                     outlier_frac: float = 0.1, rot_deg: float = 0.5, trans_m: float = 0.1, cam=KITTI):
     """C5: a batch of PoseOptimization problems in the orbba_pose_batch layout.

@@ -211,3 +211,45 @@ def test_batch_sub_streams_and_cells_per_wave(monkeypatch, nsub, cpw):
     for i, n in enumerate(cnt):
         assert np.array_equal(k0[i, :n], k1[i, :n]), i
         assert np.array_equal(d0[i, :n], d1[i, :n]), i
+
+
+def test_batch_status_clean_and_induced_fault():
+    """The batched path reports device capacity faults: clean batches read 0; a handle whose quadtree
+    node capacity is shrunk (ORBX_DEBUG_NC test hook) trips FAULT_QT_NODES (bit 0) on a dense level,
+    truncates instead of writing out of bounds, and the word clears once read."""
+    import os
+    import torch
+    from orb_slam2_refactored_amd._lib import OrbError
+    frames = torch.from_numpy(np.stack([synth_image(500 + i, 1280, 720) for i in range(4)])).cuda()
+    ex = ORBextractor(ORBextractor.Parameters(2000))
+    ex.extract_batch_device(frames)
+    assert ex.batch_status() == 0
+    os.environ["ORBX_DEBUG_NC"] = "256"
+    try:
+        bad = ORBextractor(ORBextractor.Parameters(2000))
+    finally:
+        del os.environ["ORBX_DEBUG_NC"]
+    _, _, cnt = bad.extract_batch_device(frames)
+    with pytest.raises(OrbError, match="fault mask 1"):
+        bad.batch_status()
+    assert bad.batch_status() == 0   # cleared by the read
+    assert (cnt.cpu().numpy() <= ex.max_keypoints(720, 1280)).all()
+
+
+def test_batch_device_rejects_bad_output_buffers():
+    import torch
+    frames = torch.from_numpy(np.stack([synth_image(1, 640, 480)] * 2)).cuda()
+    ex = ORBextractor(ORBextractor.Parameters(1000))
+    cap = ex.max_keypoints(480, 640)
+    good_k = torch.empty((2, cap, 7), dtype=torch.int32, device="cuda")
+    good_d = torch.empty((2, cap, 32), dtype=torch.uint8, device="cuda")
+    good_c = torch.empty(2, dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        ex.extract_batch_device(frames, good_k[:, : cap - 1], good_d, good_c)
+    with pytest.raises(ValueError):
+        ex.extract_batch_device(frames, good_k, torch.empty((2, cap, 64), dtype=torch.uint8, device="cuda")[:, :, :32],
+                                good_c)
+    with pytest.raises(ValueError):
+        ex.extract_batch_device(frames, good_k, good_d, good_c[:1])
+    with pytest.raises(ValueError):
+        ex.extract_batch_device(frames.transpose(1, 2).contiguous().transpose(1, 2), good_k, good_d, good_c)
