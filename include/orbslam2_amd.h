@@ -369,9 +369,19 @@ typedef struct orbba_result {
     double*   edge_chi2;    /* n_edges: final chi2 (may be NULL) */
     int32_t   iterations[2];/* LM iterations run by optimize(5) and optimize(10) */
     double    chi2[2];      /* active robust chi2 after each optimize */
+    int32_t   ran;          /* 0: the stop flag was set on entry, nothing was optimised and the caller
+                             * must not write anything back (Optimizer.cc:633-634 returns there) */
 } orbba_result;
 
-/* stop_flag: polled like g2o's force-stop flag (sparse_optimizer.h:188); may be NULL. */
+/* Free keyframes per optimize() (the reduced camera system is 6 x that square).  Up to 21 the system
+ * is factored in LDS; above that in HBM by a 1024-thread blocked LDL^T (slower per trial, same
+ * algorithm).  ORB_EINVAL beyond this limit. */
+#define ORBBA_MAX_FREE_KEYFRAMES 512
+
+/* stop_flag: g2o's force-stop flag (sparse_optimizer.h:188, LocalMapping's abortBA_); may be NULL.
+ * Polled where g2o polls terminate(): before the call, between optimize(5) and optimize(10), and after
+ * every LM trial (the flag is mirrored into device-visible memory while the call waits, and the
+ * device's control kernel ends the loop after the trial in which it saw the flag). */
 int orbba_local_ba(const orbba_problem* prob, orbba_result* res, const volatile int32_t* stop_flag,
                    int device);
 

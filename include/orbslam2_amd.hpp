@@ -209,9 +209,12 @@ inline void ComputeStereoMatches(const std::vector<orbx_keypoint>& keypointsL, c
 // Optimizer::LocalBundleAdjustment from the flattened graph (Optimizer.cc:540-631): the caller
 // gathers local / fixed keyframes and local map points exactly as :493-537, calls this, then
 // erases the outlier observations and writes poses / points back under the map mutex (:677-735).
-inline void LocalBundleAdjustment(const orbba_problem& problem, orbba_result& result, const volatile int32_t* stopFlag,
+// Returns false when the stop flag was already set on entry (the reference returns at
+// Optimizer.cc:633-634): nothing was optimised and nothing must be written back.
+inline bool LocalBundleAdjustment(const orbba_problem& problem, orbba_result& result, const volatile int32_t* stopFlag,
                                   int device = 0) {
     check(orbba_local_ba(&problem, &result, stopFlag, device), "orbba_local_ba");
+    return result.ran != 0;
 }
 
 // int Optimizer::PoseOptimization(Frame*) (include/Optimizer.h:49, src/Optimizer.cc:345-489) over a

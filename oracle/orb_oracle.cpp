@@ -748,8 +748,9 @@ struct BA {
     std::vector<int> hp, hl;   // Hessian index per pose / point (-1 inactive or fixed)
     int np = 0, nl = 0;
     const volatile int32_t* stop = nullptr;
+    int stop_after = -1, trials = 0;   // test hook: the flag "rises" once this many LM trials have run
 
-    bool terminate() const { return stop && *stop; }
+    bool terminate() const { return (stop && *stop) || (stop_after >= 0 && trials >= stop_after); }
 
     double chi2(int e) const {
         const int d = stereo[e] ? 3 : 2;
@@ -1054,6 +1055,7 @@ struct BA {
                     pop();
                 }
                 q++;
+                trials++;
             } while (rho < 0 && q < 10 && !terminate());
             done_iters++;
             final_chi = cur;
@@ -1721,8 +1723,12 @@ int oracle_compute_stereo_matches(const orbm_stereo_view* L, const orbm_stereo_v
     return n;
 }
 
-int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile int32_t* stop) {
+// stop_after >= 0: the stop flag is raised right after that many LM trials (between trials, where
+// g2o polls terminate(): optimization_algorithm_levenberg.cpp:149, sparse_optimizer.cpp:376).
+int oracle_local_ba_stop_after(const orbba_problem* pr, orbba_result* res, const volatile int32_t* stop,
+                               int stop_after) {
     BA ba;
+    ba.stop_after = stop_after;
     ba.P = pr->n_poses; ba.N = pr->n_points; ba.E = pr->n_edges;
     ba.stop = stop;
     ba.pose.resize(ba.P);
@@ -1745,11 +1751,11 @@ int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile i
     ba.err.assign(3 * (size_t)ba.E, 0);
     res->iterations[0] = res->iterations[1] = 0;
     res->chi2[0] = res->chi2[1] = 0;
-    bool run = !(stop && *stop);
+    bool run = !ba.terminate();
     if (run) {
         ba.init_level(0);
         res->iterations[0] = ba.optimize(5, res->chi2[0]);
-        bool more = !(stop && *stop);
+        bool more = !ba.terminate();
         if (more) {
             for (int e = 0; e < ba.E; e++) {
                 const double maxc = ba.stereo[e] ? 7.815 : 5.991;
@@ -1776,6 +1782,10 @@ int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile i
     }
     std::memcpy(res->points, ba.X.data(), sizeof(double) * 3 * ba.N);
     return 0;
+}
+
+int oracle_local_ba(const orbba_problem* pr, orbba_result* res, const volatile int32_t* stop) {
+    return oracle_local_ba_stop_after(pr, res, stop, -1);
 }
 
 void* oracle_voc_load_text(const char* path) {

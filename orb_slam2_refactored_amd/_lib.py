@@ -54,7 +54,7 @@ class BAProblem(C.Structure):
 class BAResult(C.Structure):
     _fields_ = [("pose_R", C.c_void_p), ("pose_t", C.c_void_p), ("pose_q", C.c_void_p),
                 ("points", C.c_void_p), ("edge_outlier", C.c_void_p), ("edge_chi2", C.c_void_p),
-                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2)]
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("ran", C.c_int32)]
 
 
 class ProjBatch(C.Structure):

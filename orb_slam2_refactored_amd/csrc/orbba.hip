@@ -22,6 +22,8 @@
 #include <cstring>
 #include <vector>
 
+#include <thread>
+
 #include "common.h"
 #include "se3.h"
 
@@ -33,7 +35,10 @@ struct BACtl {
     double maxdiag;
     // LM loop state, advanced on the device by ba_decide_kernel (g2o SparseOptimizer::optimize +
     // OptimizationAlgorithmLevenberg::solve): iteration, trial within it, nBad, flags
-    int it, q, nbad, done, need_lin, iters_max, iters_done, pad;
+    int it, q, nbad, done, need_lin, iters_max, iters_done;
+    int trials;    // LM trials since the start of the LocalBA call (both optimize() calls; test hook)
+    int stopped;   // the force-stop flag ended the loop
+    int pad;
     double chi_out;
 };
 
@@ -87,11 +92,14 @@ struct BADev {
     double* Hpp;          // np x 36
     double* bp;           // np x 6
     double* S;            // D x D reduced system
+    double* Sg;           // Dp x (Dp+1) padded working copy for the global-memory solve (D > 128), else null
     double* bs;           // D
     double* x;            // D + 3 nl
     double* rchi;         // Ea: robust chi2 per active slot
     double* part;         // scale partials: nl + np
     BACtl* ctl;
+    const int32_t* stop;   // device view of the host's force-stop flag (mapped pinned mirror), or null
+    int stop_after;        // test hook: stop once this many trials have run (-1: off)
 };
 
 __device__ __forceinline__ double edge_chi2(const BADev& b, int e) {
@@ -608,6 +616,22 @@ __device__ __forceinline__ void solve_trailing_tile(double* A, int ld, int J0, i
     for (int r2 = 0; r2 < 4; r2++) A[(i0 + kq + 4 * r2) * ld + k0 + col] -= u[r2];
 }
 
+__device__ __forceinline__ void solve_trailing_tile_g(double* A, int ld, int J0, int i0, int k0, int col, int kq,
+                                                      const double (&dk)[4]) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) {
+        av[s2] = A[(long long)(i0 + col) * ld + J0 + 4 * s2 + kq];
+        bv[s2] = A[(long long)(k0 + col) * ld + J0 + 4 * s2 + kq] * dk[s2];
+    }
+    d4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], bv[s2], acc, 0, 0, 0);
+    const double u[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int r2 = 0; r2 < 4; r2++) A[(long long)(i0 + kq + 4 * r2) * ld + k0 + col] -= u[r2];
+}
+
 // Schedule per block J (one barrier each after the panel and after the trailing step):
 //   panel J (all waves) | wavefront 0: trailing tile (J+1, J+1), then the diagonal block J+1
 //   (lookahead), while wavefronts 1-3 update every other trailing tile.
@@ -788,6 +812,152 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     BA_STAMP(42);
 }
 
+// The same blocked LDL^T for reduced systems too large for LDS (more than 21 free keyframes, D > 128;
+// the reference's window is every covisible keyframe, Optimizer.cc:494-504, with no upper bound).
+// The padded system lives in HBM / L2 (b.Sg, row stride Dp+1); y, D^-1 and the forward-substitution
+// vector stay in LDS.  One 1024-thread workgroup (16 wavefronts), per block J:
+//   (1) wavefronts 0 / 1 factor the 16x16 diagonal block and form its inverse in an LDS copy (the
+//       same concurrent pair as the LDS kernel), then the block goes back to HBM (L below, Linv in
+//       the upper triangle, as the LDS kernel keeps it);
+//   (2) the panel U_iJ = A_iJ Linv^T and y_i -= U_iJ D^-1 z_J over all 16 wavefronts (MFMA);
+//   (3) the trailing update A_IK -= U_IJ D_J^-1 U_KJ^T, one 16x16 tile per wavefront step (MFMA).
+// Back substitution: x_J on wavefront 0, the updates of earlier rows over the whole workgroup.
+// ~D^3/3 flops at a few hundred GFLOP/s (one CU): 0.1-1 ms per trial for 22-100 free keyframes.
+__global__ __launch_bounds__(1024) void ba_solve_global_kernel(BADev b, int D) {
+    BA_RETURN_IF_DONE(b);
+    extern __shared__ __attribute__((aligned(16))) double ysh[];   // y | dinv | vz, Dp each
+    __shared__ double Ad[SB * (SB + 1)];
+    __shared__ int s_ok, s_flag;
+    const int Dp = solve_dp(D), ld = Dp + 1;
+    double* A = b.Sg;
+    double* y = ysh;
+    double* dinv = y + Dp;
+    double* vz = dinv + Dp;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NW = 16;
+    const int col = lane & 15, kq = lane >> 4;
+    for (long long u = tid; u < (long long)Dp * Dp; u += blockDim.x) {
+        const int r = (int)(u / Dp), c = (int)(u % Dp);
+        A[(long long)r * ld + c] = (r < D && c < D) ? b.S[(long long)r * D + c] : (r == c ? 1.0 : 0.0);
+    }
+    for (int i = tid; i < Dp; i += blockDim.x) y[i] = i < D ? b.bs[i] : 0.0;
+    if (tid == 0) s_ok = 1;
+    __syncthreads();
+    for (int J0 = 0; J0 < Dp; J0 += SB) {
+        const int R0 = J0 + SB;
+        const int nbk = (Dp - R0) / SB;
+        // (1) diagonal block in LDS; Av addresses it with the global (J0, J0) indexing of the helpers
+        if (tid < SB * SB) Ad[(tid >> 4) * (SB + 1) + (tid & 15)] = A[(long long)(J0 + (tid >> 4)) * ld + J0 + (tid & 15)];
+        if (tid == 0) s_flag = 0;
+        __syncthreads();
+        double* Av = Ad - ((long long)J0 * (SB + 1) + J0);
+        if (wv == 0) {
+            if (!solve_diag_factor(Av, y, dinv, SB + 1, J0, lane, &s_flag, D - J0) && lane == 0) s_ok = 0;
+        } else if (wv == 1) {
+            solve_diag_inverse(Av, y, dinv, vz, SB + 1, J0, lane, &s_flag, D - J0);
+        }
+        __syncthreads();
+        if (!s_ok) break;
+        if (tid < SB * SB) A[(long long)(J0 + (tid >> 4)) * ld + J0 + (tid & 15)] = Ad[(tid >> 4) * (SB + 1) + (tid & 15)];
+        if (nbk == 0) break;
+        // (2) panel
+        {
+            double binv[4], bvz[4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++) {
+                const int k = 4 * s2 + kq;
+                const double v = Ad[min(k, col) * (SB + 1) + max(k, col)];
+                binv[s2] = col > k ? v : (col == k ? 1.0 : 0.0);
+                bvz[s2] = col == 0 ? vz[J0 + 4 * s2 + kq] : 0.0;
+            }
+            for (int t = wv; t < nbk; t += NW) {
+                const int i0 = R0 + SB * t;
+                double av[4];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) av[s2] = A[(long long)(i0 + col) * ld + J0 + 4 * s2 + kq];
+                d4 acc = {0, 0, 0, 0}, accy = {0, 0, 0, 0};
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) {
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], binv[s2], acc, 0, 0, 0);
+                    accy = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s2], bvz[s2], accy, 0, 0, 0);
+                }
+                const double u[4] = {acc.x, acc.y, acc.z, acc.w};
+                const double uy[4] = {accy.x, accy.y, accy.z, accy.w};
+#pragma unroll
+                for (int r2 = 0; r2 < 4; r2++) {
+                    const int row = i0 + kq + 4 * r2;
+                    A[(long long)row * ld + J0 + col] = u[r2];
+                    if (col == 0) y[row] -= uy[r2];
+                }
+            }
+        }
+        __syncthreads();
+        // (3) trailing update over the lower block triangle
+        {
+            double dk[4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++) dk[s2] = dinv[J0 + 4 * s2 + kq];
+            const int ntile = nbk * (nbk + 1) / 2;
+            int I = 0, K = wv;   // tile t = I (I + 1) / 2 + K, walked with a stride of NW
+            while (K > I) { K -= I + 1; I++; }
+            for (int t = wv; t < ntile; t += NW) {
+                solve_trailing_tile_g(A, ld, J0, R0 + SB * I, R0 + SB * K, col, kq, dk);
+                K += NW;
+                while (K > I) { K -= I + 1; I++; }
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    const int ok = s_ok;
+    if (ok) {
+        for (int i = tid; i < Dp; i += blockDim.x) y[i] *= dinv[i];   // t = D^-1 z
+        __syncthreads();
+        for (int J0 = Dp - SB; J0 >= 0; J0 -= SB) {
+            if (wv == 0) {   // x_J = Linv_JJ^T t_J
+                double xp[4] = {y[J0 + col], 0, 0, 0};
+#pragma unroll
+                for (int j = 1; j < SB; j++) {
+                    const double lv = A[(long long)(J0 + min(col, j)) * ld + J0 + j];
+                    xp[j & 3] = fma(j > col ? lv : 0.0, y[J0 + j], xp[j & 3]);
+                }
+                const double xc = (xp[0] + xp[1]) + (xp[2] + xp[3]);
+                wave_lds_sync();
+                if (lane < SB) y[J0 + col] = xc;
+            }
+            __syncthreads();
+            double xj[SB];
+#pragma unroll
+            for (int k = 0; k < SB; k++) xj[k] = y[J0 + k];
+            for (int c = tid; c < J0; c += blockDim.x) {
+                double sp[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < SB; k++) sp[k & 3] = fma(A[(long long)(J0 + k) * ld + c], xj[k], sp[k & 3]);
+                y[c] = fma(-((sp[0] + sp[1]) + (sp[2] + sp[3])), dinv[c], y[c]);
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < D; i += blockDim.x) b.x[i] = ok ? y[i] : 0.0;
+    if (tid == 0) b.ctl->ok2 = ok;
+    const double lam = b.ctl->lambda;
+    for (int i = tid; i < b.np; i += blockDim.x) {   // push() + oplus, scale terms x.(lambda x + b)
+        const int id = b.ps_id[i];
+        double q[4], t[3], xi[6], part = 0;
+        for (int j = 0; j < 4; j++) q[j] = b.q[4 * id + j];
+        for (int j = 0; j < 3; j++) t[j] = b.t[3 * id + j];
+        for (int j = 0; j < 6; j++) {
+            xi[j] = ok ? y[6 * i + j] : 0.0;
+            part += xi[j] * (lam * xi[j] + b.bp[6 * i + j]);
+        }
+        b.part[b.nl + i] = part;
+        for (int j = 0; j < 4; j++) b.q_sv[4 * id + j] = q[j];
+        for (int j = 0; j < 3; j++) b.t_sv[3 * id + j] = t[j];
+        se3_exp_update(xi, q, t);
+        for (int j = 0; j < 4; j++) b.q[4 * id + j] = q[j];
+        for (int j = 0; j < 3; j++) b.t[3 * id + j] = t[j];
+    }
+}
+
 // Back-substitution xl = Dinv (bl - Hpl^T xp), push(), point +=, scale term, then the errors and
 // robust chi2 of the point's edges at the new estimate (computeActiveErrors after update()).
 __global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D) {
@@ -877,10 +1047,14 @@ __global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b, BACtl* host_sn
             c->accepted = 0;
         }
         s_acc = c->accepted;
-        // trial / iteration bookkeeping (host loop of levenberg solve + SparseOptimizer::optimize;
-        // the force-stop flag is applied by the host between steps)
+        // trial / iteration bookkeeping (host loop of levenberg solve + SparseOptimizer::optimize)
         c->q += 1;
-        if (rho < 0 && c->q < 10) {
+        c->trials += 1;
+        // g2o polls terminate() after every trial (levenberg.cpp:149) and before every iteration
+        // (sparse_optimizer.cpp:376): a raised flag ends the loop once this trial is done
+        const bool stop = (b.stop && __atomic_load_n(b.stop, __ATOMIC_RELAXED) != 0) ||
+                          (b.stop_after >= 0 && c->trials >= b.stop_after);
+        if (rho < 0 && c->q < 10 && !stop) {
             c->need_lin = 0;   // retry with the new lambda
         } else {
             c->iters_done += 1;
@@ -893,6 +1067,10 @@ __global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b, BACtl* host_sn
             }
             c->it += 1;
             if (c->it >= c->iters_max) term = true;
+            if (stop) {
+                term = true;
+                c->stopped = 1;
+            }
             if (term) c->done = 1;
             else {
                 c->need_lin = 1;
@@ -984,8 +1162,25 @@ struct BAContext {
     BACtl* h_ring = nullptr;  // pinned, device-mapped control snapshots, one per step in flight
     BACtl* d_ring = nullptr;
     hipEvent_t ring_ev[2] = {nullptr, nullptr};
+    int32_t* h_stop = nullptr;   // pinned, device-mapped mirror of the caller's stop flag
+    int32_t* d_stop = nullptr;
     PinnedBuf h_prob, h_struct, h_res;   // pinned staging images (one copy each way)
+    // Everything device-bound belongs to `device`: a call on another device from the same thread
+    // releases it all (buffers, stream, events) before building the new device's set.
+    void reset_device() {
+        if (device >= 0) (void)hipSetDevice(device);
+        if (st) (void)hipStreamSynchronize(st);
+        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
+        for (hipEvent_t& e : ring_ev)
+            if (e) { (void)hipEventDestroy(e); e = nullptr; }
+        if (st) { (void)hipStreamDestroy(st); st = nullptr; }
+        if (h_ring) { (void)hipHostFree(h_ring); h_ring = nullptr; d_ring = nullptr; }
+        if (h_stop) { (void)hipHostFree(h_stop); h_stop = nullptr; d_stop = nullptr; }
+        if (h_ctl) { (void)hipHostFree(h_ctl); h_ctl = nullptr; }
+        device = -1;
+    }
     ~BAContext() {
+        if (h_stop) (void)hipHostFree(h_stop);
         if (h_ring) (void)hipHostFree(h_ring);
         for (hipEvent_t e : ring_ev)
             if (e) (void)hipEventDestroy(e);
@@ -1085,21 +1280,26 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                           pr->edge_pose[e] < P, "edge references a missing vertex");
     BAContext& C = g_ba;
     if (C.device != device) {
+        int ndev = 0;
+        ORB_HIP_TRY(hipGetDeviceCount(&ndev));
+        ORB_CHECK_ARG(device >= 0 && device < ndev, "no such HIP device");
+        C.reset_device();
         ORB_HIP_TRY(hipSetDevice(device));
-        if (C.st) (void)hipStreamDestroy(C.st);
         ORB_HIP_TRY(hipStreamCreateWithFlags(&C.st, hipStreamNonBlocking));
-        if (!C.h_ctl) ORB_HIP_TRY(hipHostMalloc((void**)&C.h_ctl, sizeof(BACtl), hipHostMallocDefault));
-        if (!C.h_ring) {
-            ORB_HIP_TRY(hipHostMalloc((void**)&C.h_ring, 2 * sizeof(BACtl), hipHostMallocMapped));
-            ORB_HIP_TRY(hipHostGetDevicePointer((void**)&C.d_ring, C.h_ring, 0));
-        }
-        for (hipEvent_t& e : C.ring_ev)
-            if (!e) ORB_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ORB_HIP_TRY(hipHostMalloc((void**)&C.h_ctl, sizeof(BACtl), hipHostMallocDefault));
+        ORB_HIP_TRY(hipHostMalloc((void**)&C.h_ring, 2 * sizeof(BACtl), hipHostMallocMapped));
+        ORB_HIP_TRY(hipHostGetDevicePointer((void**)&C.d_ring, C.h_ring, 0));
+        ORB_HIP_TRY(hipHostMalloc((void**)&C.h_stop, 64, hipHostMallocMapped));
+        ORB_HIP_TRY(hipHostGetDevicePointer((void**)&C.d_stop, C.h_stop, 0));
+        for (hipEvent_t& e : C.ring_ev) ORB_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         C.device = device;
     }
     ORB_HIP_TRY(hipSetDevice(device));
     hipStream_t st = C.st;
     auto stopped = [&]() { return stop_flag && *stop_flag; };
+    int stop_after = -1;   // test hook (ORBBA_DEBUG_STOP_AFTER_TRIALS): tests/test_ba_gpu.py
+    if (const char* e = getenv("ORBBA_DEBUG_STOP_AFTER_TRIALS")) stop_after = atoi(e);
+    *C.h_stop = stopped() ? 1 : 0;
 
     // initial estimates: SE3Quat(R, t) -> Quaterniond(R) normalised (Optimizer.cc:145-150)
     std::vector<double> q0(4 * (size_t)P);
@@ -1184,6 +1384,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     double* d_chi = cs.take<double>(E);
     b.fixed = d_fixed; b.ep = d_ep; b.ek = d_ek; b.stereo = d_st; b.obs = d_obs; b.info = d_info; b.cam = d_cam;
     b.ctl = C.ctlbuf.as<BACtl>();
+    b.stop = stop_flag ? C.d_stop : nullptr;
+    b.stop_after = stop_after;
+    ORB_HIP_TRY(hipMemsetAsync(b.ctl, 0, sizeof(BACtl), st));   // trials / stopped count over the whole call
     ORB_HIP_TRY(hipMemcpyAsync(C.prob.ptr, C.h_prob.ptr, cp.off, hipMemcpyHostToDevice, st));
     if (E) {
         ORB_HIP_TRY(hipMemsetAsync(b.robust, 1, E, st));
@@ -1195,6 +1398,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
 
     std::vector<uint8_t> level(E, 0);
     HostStructure hs;
+    bool hook_stopped = false;   // the device ended a loop on the stop flag (or the test hook)
     // ------------------------------------------------------------------ one optimize(iters)
     auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
         build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs);
@@ -1203,10 +1407,13 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         *iters_out = 0;
         *chi_out = 0;
         if (Ea == 0 || np + nl == 0) return ORB_OK;
-        if (D > 128 || solve_lds_doubles(D) * 8 + 4096 > 160 * 1024) {
-            set_error("LocalBA: too many free keyframes for the in-LDS reduced-system solve (max 21)");
+        // reduced system: in LDS up to 21 free keyframes (D <= 128), else in HBM (ba_solve_global_kernel)
+        const bool glob = D > 128 || solve_lds_doubles(D) * 8 + 4096 > 160 * 1024;
+        if (glob && np > ORBBA_MAX_FREE_KEYFRAMES) {
+            set_error("LocalBA: more than ORBBA_MAX_FREE_KEYFRAMES free keyframes in the local window");
             return ORB_EINVAL;
         }
+        const int Dp = solve_dp(D);
         // structure upload
         const size_t sbytes = carve_size<int>(Ea) + carve_size<int>(P) + carve_size<int>(N) + carve_size<int>(nl + 1) +
                               carve_size<int>(Ea) + carve_size<int>(nl) + carve_size<int>(np + 1) +
@@ -1256,7 +1463,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                               carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
                               carve_size<double>((size_t)D * D) + carve_size<double>(D) +
                               carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
-                              carve_size<double>(nl + np) + 64;
+                              carve_size<double>(nl + np) + (glob ? carve_size<double>((size_t)Dp * (Dp + 1)) : 0) +
+                              64;
         if ((rc2 = C.sys.reserve(ybytes))) return rc2;
         Carve cy{C.sys.as<char>()};
         b.J = cy.take<double>(72 * (size_t)Ea);
@@ -1271,10 +1479,12 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.x = cy.take<double>(D + 3 * (size_t)nl);
         b.rchi = cy.take<double>(std::max(Ea, nl));
         b.part = cy.take<double>(nl + np);
+        b.Sg = glob ? cy.take<double>((size_t)Dp * (Dp + 1)) : nullptr;
         ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
-        const size_t ldlt_lds = std::max<size_t>(solve_lds_doubles(D) * 8, 16);
-        ORB_HIP_TRY(hipFuncSetAttribute((const void*)ba_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
+        ORB_HIP_TRY(hipFuncSetAttribute(glob ? (const void*)ba_solve_global_kernel : (const void*)ba_solve_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)std::max<size_t>(ldlt_lds, 1024)));
         const dim3 gg((nl * 8 + 63) / 64);   // 8 lanes per point
         // The LM loop runs on the device (ba_decide_kernel advances it); the host keeps LOOKAHEAD
@@ -1293,7 +1503,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 if (enq == 0) hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
                 hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
                 if (np) hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk), dim3(1024), 0, st, b, D);
-                hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
+                if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
+                else hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
                 hipLaunchKernelGGL(ba_point_update_kernel, gg, dim3(64), 0, st, b, D);
                 const int slot = enq % LOOKAHEAD;
                 hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(1024), 0, st, b, C.d_ring + slot);
@@ -1303,7 +1514,15 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             }
             if (seen == enq) break;
             const int slot = seen % LOOKAHEAD;
-            ORB_HIP_TRY(hipEventSynchronize(C.ring_ev[slot]));
+            // wait for the step, mirroring the caller's stop flag into the device-visible word the
+            // decide kernel polls after every trial
+            for (;;) {
+                const hipError_t q = hipEventQuery(C.ring_ev[slot]);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) ORB_HIP_TRY(q);
+                if (stop_flag) __atomic_store_n(C.h_stop, *stop_flag ? 1 : 0, __ATOMIC_RELEASE);
+                std::this_thread::yield();
+            }
             last = C.h_ring[slot];
             seen++;
             fin = last.done != 0;
@@ -1316,13 +1535,15 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         ORB_HIP_TRY(hipMemcpy(&last, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost));
         *iters_out = last.iters_done;
         *chi_out = last.chi_out;
+        hook_stopped = hook_stopped || last.stopped;
         return ORB_OK;
     };
 
-    const bool run = !stopped();   // Optimizer.cc:633-634: stop before optimising => nothing done
+    const bool run = !stopped() && stop_after != 0;   // Optimizer.cc:633-634: stop before optimising => nothing done
+    res->ran = run ? 1 : 0;
     if (run) {
         if ((rc = optimize(5, &res->iterations[0], &res->chi2[0]))) return rc;
-        if (!stopped()) {
+        if (!stopped() && !hook_stopped) {   // doMore (:639-642)
             // tag outliers (level 1) and drop the robust kernels (:644-670)
             if (E) {
                 hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, (uint8_t*)nullptr,

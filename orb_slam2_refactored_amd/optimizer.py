@@ -39,6 +39,7 @@ def LocalBundleAdjustment(problem: dict, stop_flag=None, device: int = 0) -> dic
     check(lib().orbba_local_ba(C.byref(pr), C.byref(res), sf, device), "orbba_local_ba")
     out["iterations"] = tuple(res.iterations)
     out["chi2"] = tuple(res.chi2)
+    out["ran"] = bool(res.ran)   # False: stop flag set on entry, nothing to write back (Optimizer.cc:633-634)
     return out
 
 

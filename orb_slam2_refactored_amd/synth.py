@@ -49,7 +49,7 @@ def _small_rot(rng, sigma_deg):
 
 
 def make_ba_problem(seed: int = 0, n_kf: int = 20, n_pts: int = 3000, n_fixed: int = 2, stereo_frac: float = 0.2,
-                    outlier_frac: float = 0.03, cam=KITTI):
+                    outlier_frac: float = 0.03, cam=KITTI, yaw_per_kf: float = 0.5):
     """C4: a LocalBundleAdjustment problem in the flattened orbba_problem layout.
 
     n_kf local keyframes moving forward along +z (0.5 m apart, 0.5 deg yaw per KF); KF 0 is the
@@ -64,7 +64,7 @@ def make_ba_problem(seed: int = 0, n_kf: int = 20, n_pts: int = 3000, n_fixed: i
     R_true, t_true, C = [], [], []
     for k in range(P):
         kk = k if k < n_kf else -(k - n_kf + 1)   # fixed cameras behind KF 0
-        Rwc = _rot_y(0.5 * kk)
+        Rwc = _rot_y(yaw_per_kf * kk)   # long windows: a smaller yaw keeps points in front of every camera
         c = np.array([0.02 * np.sin(kk), 0.0, 0.5 * kk])
         Rcw = Rwc.T
         R_true.append(Rcw)

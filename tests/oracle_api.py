@@ -44,7 +44,7 @@ class BAProblem(C.Structure):
 class BAResult(C.Structure):
     _fields_ = [("pose_R", C.c_void_p), ("pose_t", C.c_void_p), ("pose_q", C.c_void_p),
                 ("points", C.c_void_p), ("edge_outlier", C.c_void_p), ("edge_chi2", C.c_void_p),
-                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2)]
+                ("iterations", C.c_int32 * 2), ("chi2", C.c_double * 2), ("ran", C.c_int32)]
 
 
 def build():
@@ -209,7 +209,7 @@ def ba_problem(keep, prob):
                      keep(prob["edge_cam"], np.float64))
 
 
-def local_ba(prob, stop=None):
+def local_ba(prob, stop=None, stop_after=-1):
     keep = _Keep()
     pr = ba_problem(keep, prob)
     P, N, E = pr.n_poses, pr.n_points, pr.n_edges
@@ -220,7 +220,7 @@ def local_ba(prob, stop=None):
     sf = None
     if stop is not None:
         sf = C.byref(C.c_int32(int(stop)))
-    lib().oracle_local_ba(C.byref(pr), C.byref(res), sf)
+    lib().oracle_local_ba_stop_after(C.byref(pr), C.byref(res), sf, int(stop_after))
     out["iterations"] = tuple(res.iterations)
     out["chi2"] = tuple(res.chi2)
     return out

@@ -46,6 +46,7 @@ def test_local_ba_golden():
 def test_local_ba_stop_flag(oracle):
     pr = make_ba_problem(4, n_kf=6, n_pts=300, n_fixed=1)
     g = LocalBundleAdjustment(pr, stop_flag=1)
+    assert not g["ran"]   # Optimizer.cc:633-634: nothing optimised, nothing to write back
     assert tuple(g["iterations"]) == (0, 0)
     assert not g["edge_outlier"].any()
     assert rmse(g["points"], pr["points"]) == 0
@@ -56,3 +57,50 @@ def test_local_ba_deterministic():
     a = LocalBundleAdjustment(pr)
     b = LocalBundleAdjustment(pr)
     assert np.array_equal(a["pose_t"], b["pose_t"]) and np.array_equal(a["points"], b["points"])
+
+
+@pytest.mark.parametrize("seed,kf,pts,yaw", [(10, 24, 3000, 0.5), (11, 40, 5000, 0.5), (12, 64, 6000, 0.1),
+                                              (13, 96, 8000, 0.05)])
+def test_local_ba_large_window(oracle, seed, kf, pts, yaw):
+    """More than 21 free keyframes (D = 6 x free > 128): the reduced system is factored in HBM by
+    ba_solve_global_kernel; same outliers / iteration counts as the oracle's dense LDL^T."""
+    pr = make_ba_problem(seed, n_kf=kf, n_pts=pts, n_fixed=2, yaw_per_kf=yaw)
+    assert int((pr["pose_fixed"] == 0).sum()) > 21
+    g = LocalBundleAdjustment(pr)
+    o = oracle.local_ba(pr)
+    compare(g, o)
+    assert g["ran"] and g["chi2"][1] < g["chi2"][0]
+
+
+@pytest.mark.parametrize("after", [1, 2, 3, 5, 8, 13])
+def test_local_ba_stop_between_trials(oracle, after, monkeypatch):
+    """The force-stop flag takes effect at the next trial boundary, as g2o's terminate() polls
+    (levenberg.cpp:149, sparse_optimizer.cpp:376): the flag is raised right after `after` LM trials
+    (test hook on both sides), and iteration counts / outliers / poses must equal the oracle's."""
+    pr = make_ba_problem(20 + after, n_kf=12, n_pts=1500, n_fixed=1)
+    monkeypatch.setenv("ORBBA_DEBUG_STOP_AFTER_TRIALS", str(after))
+    g = LocalBundleAdjustment(pr)
+    o = oracle.local_ba(pr, stop_after=after)
+    compare(g, o)
+    full = oracle.local_ba(pr)
+    assert sum(g["iterations"]) <= sum(full["iterations"])
+    if after < 5:
+        assert g["iterations"][1] == 0   # stopped inside optimize(5): doMore is false
+
+
+def test_local_ba_stop_flag_async():
+    """A flag raised by another thread while the call runs ends it early without error."""
+    import ctypes
+    import threading
+    import time
+    pr = make_ba_problem(30, n_kf=40, n_pts=5000, n_fixed=2)
+    full = LocalBundleAdjustment(pr)
+    flag = ctypes.c_int32(0)
+    t = threading.Timer(0.002, lambda: setattr(flag, "value", 1))
+    t0 = time.perf_counter()
+    t.start()
+    g = LocalBundleAdjustment(pr, stop_flag=flag)
+    t.join()
+    assert g["ran"]
+    assert sum(g["iterations"]) <= sum(full["iterations"])
+    assert time.perf_counter() - t0 < 5
