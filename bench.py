@@ -1,18 +1,32 @@
 #!/usr/bin/env python3
-"""Benchmark: ORB extract + brute-force Hamming match on 1280x720 frames (BASELINE.json configs[1],
-"1280x720 mono, 8 levels, 2000 features, extract+brute-force Hamming match on 1 MI355X"), plus the
-LocalBundleAdjustment LM-iteration rate on configs[3] (20 KF x 3000 MP).
+"""Benchmark of the ORB front end + LocalBA hot path (BASELINE.json).
 
-One step = one batch of `--frames` synthetic frames already resident in HBM: ORBextractor::Extract on
-every frame (one batched launch per stage) and a brute-force top-2 + ratio match of every frame
-against its predecessor in the batch (frame 0 against the last frame).  With N > 1 GPUs each rank
-processes its own batch (weak scaling: frames are independent) and the step ends with an RCCL
-all-gather of the padded keypoint/descriptor slots (the loop-closure descriptor exchange of
-BASELINE.json configs[4]).
+Headline line (`value`): configs[1] / C2 — 1280x720 mono, 8 levels, 2000 features, extract + brute-force
+Hamming top-2/ratio match of every frame against its predecessor.  One step = one batch of `--frames`
+(default 1024, the C5 batch) synthetic frames already resident in HBM: a camera-pan sequence (frame i =
+frame i-1 shifted by (+3, +2) px with fresh noise, the §8d C2 shifted pair, chained), so frame i is
+matched to i-1 as §8d C5 says.  With N > 1 ranks the 1024-frame job is sharded (strong scaling): rank r
+extracts its contiguous shard, matches frames 1.. of the shard locally, all-gathers the padded
+keypoint / descriptor slots over RCCL (the loop-closure descriptor exchange of configs[4]) and matches
+its first frame against rank r-1's last frame read from the gathered slots (one step later, so the
+gather overlaps the next step's kernels).
 
-Prints ONE JSON line on rank 0.
+Secondary objects on the same JSON line, each with its own rate, roofline and CPU baseline:
+  c1          configs[0]: 640x480, 1000 features — GPU batch throughput + the CPU plumbing median of 200
+              single-frame Extract calls (seeds 0-15)
+  c2_textured C2 on texture-rich frames (dense FAST candidates, deep quadtrees), per-stage times
+  c3          configs[2]: stereo 1242x375, extract L+R + SearchForTriangulation (single BoW node)
+  localba     configs[3]: 20 KF x 3000 MP, optimize(5) + optimize(10), fp64
+  c5          configs[4] semantics at this N (cross-shard pairing, gather bytes); the scaling curve itself
+              comes from the driver's N = 1, 2, 4, 8 runs
+  stereo, search_by_projection, bow, pose_opt: the §8f rows
+
+CPU baselines run the oracle (oracle/orb_oracle.cpp, the C++ restatement; the reference cannot be
+built here) on the GPU box's host cores: one thread and all usable cores (one frame per thread, capped
+at 16 = the box's CPU share), with the CPU model stated.  Prints ONE JSON line on rank 0.
 """
 import argparse
+import concurrent.futures as cf
 import json
 import os
 import sys
@@ -25,9 +39,12 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]   # verbatim
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6    # MI355X spec, FP64 vector (BASELINE.md / SURVEY §8d honest ceiling)
+VALU_PEAK_TOPS = 78.6      # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: wave64 VALU op = 2 clk)
 
 
+# ------------------------------------------------------------------------------------------ helpers
 def level_sizes(W, H, nlevels=8, scale=1.2):
     s = np.float32(1.0)
     out = []
@@ -45,67 +62,362 @@ def algorithmic_bytes(W, H, n_kp, nlevels=8):
     return P + (P - W * H) + 60 * n_kp, P
 
 
+def stage_bytes(W, H, n_kp):
+    sz = level_sizes(W, H)
+    P = sum(w * h for w, h in sz)
+    return {"pyramid": (P - sz[-1][0] * sz[-1][1]) + (P - W * H),   # read l-1, write l
+            "fast_cells": P,                                          # every level read once
+            "quadtree": 0,                                            # intermediates only
+            "describe": 60 * n_kp}                                    # keypoint + descriptor writes
+
+
 STAGE_KERNEL = {"pyramid": "pyramid_level_kernel", "fast_cells": "fast_cells_kernel", "quadtree": "quadtree_kernel",
                 "describe": "describe_kernel"}
 
 
-def measured_traffic(stage, launches_per_step, frames, W, H, nfeat):
+def measured_traffic(stage, frames, W, H, nfeat):
     """HBM bytes per launch of `stage` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (profiles/*_traffic.json, tools/gpu_traffic.sh), corrected by the calibration measured in the same
-    run (FETCH_SIZE counts half the bytes of streaming reads on gfx950; WRITE_SIZE exact).  Only
-    reported when the profiled workload is this one; otherwise None."""
+    (profiles/*_traffic.json, tools/gpu_traffic.sh) of this exact workload, corrected by the
+    calibration measured in the same run (FETCH_SIZE counts half the bytes of streaming reads on
+    gfx950; WRITE_SIZE exact).  None when no profile of this workload is committed."""
     files = sorted(ROOT.glob("profiles/*_traffic.json"))
-    if not files or (frames, W, H, nfeat) != (128, 1280, 720, 2000):
-        return None
-    t = json.loads(files[-1].read_text())
-    k = t["kernels_per_dispatch"].get(STAGE_KERNEL.get(stage, ""))
-    if not k or k.get("fetch_bytes") is None:
-        return None
-    cal = t["calibration"]
-    fetch = k["fetch_bytes"] / cal.get("fetch_ratio_8B", 0.5)
-    write = (k.get("write_bytes") or 0.0) / cal.get("write_ratio_4B", 1.0)
-    # the profile averages over dispatches; a stage with several launches per step (pyramid: one
-    # per level) is reported per average launch, like `achieved`
-    return fetch + write
+    for f in reversed(files):
+        t = json.loads(f.read_text())
+        wl = t.get("workload")
+        if not isinstance(wl, dict):   # r01 files: the 128-frame C2 workload
+            wl = {"frames": 128, "width": 1280, "height": 720, "nfeatures": 2000}
+        if (wl.get("frames"), wl.get("width"), wl.get("height"), wl.get("nfeatures")) != (frames, W, H, nfeat):
+            continue
+        k = t["kernels_per_dispatch"].get(STAGE_KERNEL.get(stage, ""))
+        if not k or k.get("fetch_bytes") is None:
+            return None
+        cal = t["calibration"]
+        fetch = k["fetch_bytes"] / cal.get("fetch_ratio_8B", 0.5)
+        write = (k.get("write_bytes") or 0.0) / cal.get("write_ratio_4B", 1.0)
+        return fetch + write
+    return None
 
 
-def cpu_baseline(frames_np, nfeat, budget_s=12.0):
-    """Oracle (single-threaded C++ restatement) extract + match on a bounded sample."""
+def cpu_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable,
+            "threads_all": max(1, min(16, usable))}
+
+
+def run_threads(work, threads, budget_s):
+    """work(stop_time) -> units done; run on `threads` Python threads (the oracle is called through
+    ctypes, which releases the GIL), return (units/s, units)."""
+    t0 = time.perf_counter()
+    stop = t0 + budget_s
+    with cf.ThreadPoolExecutor(threads) as pool:
+        done = sum(pool.map(lambda _: work(stop), range(threads)))
+    return done / (time.perf_counter() - t0), done
+
+
+def oracle():
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_api as O
+    O.lib()
+    return O
+
+
+def cpu_extract_match(frames_np, nfeat, threads, budget_s):
+    """Oracle extract + brute-force match vs the previous frame, one frame per thread at a time."""
+    O = oracle()
     p = O.params(nfeat)
-    done = 0
-    prev = None
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or done < 3:
-        img = frames_np[done % len(frames_np)]
-        _, d, _ = O.extract(p, img)
-        if prev is not None:
-            O.bf_match(d, prev)
-        prev = d
-        done += 1
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{done} frames of 1280x720 (extract + bf match vs previous), oracle/orb_oracle.cpp, 1 thread"}
+
+    def work(stop):
+        prev, n, i = None, 0, int.from_bytes(os.urandom(2), "little")
+        while time.perf_counter() < stop or n < 2:
+            _, d, _ = O.extract(p, frames_np[i % len(frames_np)])
+            if prev is not None:
+                O.bf_match(d, prev)
+            prev = d
+            n += 1
+            i += 1
+        return n
+
+    return run_threads(work, threads, budget_s)
 
 
-def cpu_ba_baseline(prob, budget_s=6.0):
-    sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_api as O
+def cpu_baseline_block(unit, sample, single, multi, info):
+    v1, n1 = single
+    vN, nN = multi
+    return {"value": vN, "unit": unit, "cores": info["threads_all"], "kind": "port",
+            "sample": f"{sample}; {nN} units on {info['threads_all']} threads, oracle/orb_oracle.cpp (-O3)",
+            "single_thread": {"value": v1, "cores": 1, "units": n1}, "cpu_model": info["cpu_model"],
+            "nproc": info["nproc"], "usable_cpus": info["usable_cpus"]}
+
+
+def event_ms(fn, steps, stream):
+    import torch
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def extract_match_gpu_leg(dev, local, frames_np, nfeat, steps=10, reps=None):
+    """Batched extract + match-vs-predecessor on `frames_np` tiled to `reps` frames; returns the rate,
+    per-stage times and the fast_cells roofline."""
+    import torch
+    from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
+    F = reps or len(frames_np)
+    H, W = frames_np.shape[1:]
+    idx = torch.arange(F) % len(frames_np)
+    frames = torch.from_numpy(frames_np).to(dev)[idx.to(dev)].contiguous()
+    ex = ORBextractor(ORBextractor.Parameters(nfeatures=nfeat), device=local)
+    m = ORBmatcher(0.6, False)
+    prev = torch.tensor([(i - 1) % F for i in range(F)], dtype=torch.int32, device=dev)
+    kps, desc, cnt = ex.extract_batch_device(frames)
+    out = m.match_batch_device(desc, cnt, desc, cnt, pair_b=prev)
+    st = torch.cuda.current_stream()
+
+    def step():
+        ex.extract_batch_device(frames, kps, desc, cnt, stream=st)
+        m.match_batch_device(desc, cnt, desc, cnt, out=out, pair_b=prev, stream=st)
+
+    step()
+    torch.cuda.synchronize()
+    ms = event_ms(step, steps, st)
+    ex.profile(True)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    ex.profile(False)
+    brk = ex.profile_read()
+    ex.batch_status()
+    n_kp = float(cnt.float().mean().item())
+    stg = {k: v[0] / 3 for k, v in brk.items()}
+    fb = stage_bytes(W, H, n_kp)["fast_cells"] * F
+    fms = brk["fast_cells"][0] / max(brk["fast_cells"][1], 1)
+    bytes_frame, _ = algorithmic_bytes(W, H, n_kp)
+    return {"frames_per_step": F, "frames_per_s": F / (ms * 1e-3), "ms_per_step": ms,
+            "keypoints_per_frame": n_kp, "matches_per_frame": float((out[3] >= 0).sum().item()) / F,
+            "stage_ms_per_step": stg,
+            "roofline": {"bound": "hbm", "kernel": "fast_cells", "achieved": fb / (fms * 1e-3) / 1e9 if fms else 0.0,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (fb / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS) if fms else 0.0,
+                         "algorithmic_bytes_per_launch": fb, "avg_launch_ms": fms,
+                         "pipeline_algorithmic_GBs": bytes_frame * F / (sum(stg.values()) * 1e-3) / 1e9}}
+
+
+# ------------------------------------------------------------------------------------------ legs
+def c1_leg(dev, local, frames=1024, cpu=True, info=None):
+    """configs[0]: 640x480, 8 levels, 1000 features.  GPU: batched extract + match throughput (north
+    star "synthetic 640x480 pyramids ... fps and fraction of HBM roofline").  CPU: the plumbing
+    measurement of BASELINE.md — median of 200 single-frame oracle Extract calls over seeds 0-15 after
+    10 warm-ups, one thread (the reference's Extract is single-threaded)."""
+    from orb_slam2_refactored_amd import ORBextractor
+    from orb_slam2_refactored_amd.synth import pan_sequence
+    seq = pan_sequence(0, 640, 480, 16)
+    r = {"workload": "C1: 640x480 mono, 8 levels, 1000 features (GPU: batch of pan-sequence frames, extract + "
+                     "match vs previous frame)"}
+    r.update(extract_match_gpu_leg(dev, local, seq, 1000, reps=frames))
+    # single-frame host API (H2D + extract + D2H, synchronous): the reference's calling convention
+    ex = ORBextractor(ORBextractor.Parameters(1000), device=local)
+    imgs = [seq[i] for i in range(16)]
+    for i in range(10):
+        ex.Extract(imgs[i % 16])
+    lat = []
+    for i in range(200):
+        t0 = time.perf_counter()
+        ex.Extract(imgs[i % 16])
+        lat.append(time.perf_counter() - t0)
+    r["gpu_single_frame_extract_ms_median"] = 1e3 * float(np.median(lat))
+    if cpu:
+        from orb_slam2_refactored_amd.synth import synth_image
+        O = oracle()
+        p = O.params(1000)
+        cimgs = [synth_image(s, 640, 480) for s in range(16)]
+        for i in range(10):
+            O.extract(p, cimgs[i % 16])
+        t = []
+        for i in range(200):
+            t0 = time.perf_counter()
+            O.extract(p, cimgs[i % 16])
+            t.append(time.perf_counter() - t0)
+        med = float(np.median(t))
+        r["cpu_baseline"] = {"value": 1.0 / med, "unit": "frames/s", "cores": 1, "kind": "port",
+                             "median_ms": 1e3 * med, "p90_ms": 1e3 * float(np.percentile(t, 90)),
+                             "sample": "median of 200 single-frame Extract calls, seeds 0-15, 10 warm-ups, "
+                                       "oracle/orb_oracle.cpp, 1 thread", "cpu_model": (info or {}).get("cpu_model")}
+    return r
+
+
+def c2_textured_leg(dev, local, frames=1024, cpu=True, info=None):
+    """C2 on texture-rich frames: FAST fires almost everywhere, thousands of quadtree candidates per
+    level (the LDS-resident path holds 2048; beyond it the global-memory fallback runs)."""
+    from orb_slam2_refactored_amd.synth import textured_image
+    seq = np.stack([textured_image(4000 + i, 1280, 720) for i in range(16)])
+    r = {"workload": "C2 on textured 1280x720 frames (value noise + sigma-12 pixel noise), 2000 features, "
+                     "extract + match vs previous frame"}
+    r.update(extract_match_gpu_leg(dev, local, seq, 2000, reps=frames))
+    if cpu:
+        r["cpu_baseline"] = cpu_baseline_block("frames/s", "textured 1280x720 frames, extract + match vs previous",
+                                               cpu_extract_match(seq[:4], 2000, 1, 4.0),
+                                               cpu_extract_match(seq[:8], 2000, info["threads_all"], 4.0), info)
+    return r
+
+
+def c3_leg(dev, local, pairs=128, steps=10, cpu=True, info=None):
+    """configs[2]: stereo 1242x375 (8 depth bands, KITTI bf), extract L and R (one batched launch set of
+    2 x pairs frames) + SearchForTriangulation(KF1 = L @ [I|0], KF2 = R @ [I|(-bf/fx,0,0)], F12 from
+    ComputeF12, onlyStereo false, uright -1, no MapPoints, a single BoW node) per pair, all on the
+    device (orbm_search_for_triangulation_batch_device on the extractor's slots)."""
+    import torch
+    from orb_slam2_refactored_amd import ORBextractor
+    from orb_slam2_refactored_amd.matcher import search_for_triangulation_batch_device
+    from orb_slam2_refactored_amd.synth import stereo_pair, stereo_tri_geometry
+    pool = [stereo_pair(7000 + i)[:2] for i in range(8)]
+    Lh = np.stack([pool[i % 8][0] for i in range(pairs)])
+    Rh = np.stack([pool[i % 8][1] for i in range(pairs)])
+    frames = torch.from_numpy(np.concatenate([Lh, Rh])).to(dev)
+    ex = ORBextractor(ORBextractor.Parameters(2000), device=local)
+    F12, ep2 = stereo_tri_geometry()
+    Ft = torch.from_numpy(np.tile(F12, (pairs, 1))).to(dev)
+    Et = torch.from_numpy(np.tile(ep2, (pairs, 1))).to(dev)
+    f1 = torch.arange(pairs, dtype=torch.int32, device=dev)
+    f2 = f1 + pairs
+    scale, sigma2 = ex.GetScaleFactors(), ex.GetScaleSigmaSquares()
+    kps, desc, cnt = ex.extract_batch_device(frames)
+    tri = search_for_triangulation_batch_device(kps, desc, cnt, kps, desc, cnt, Ft, Et, scale, sigma2,
+                                                frame1=f1, frame2=f2)
+    st = torch.cuda.current_stream()
+
+    def do_tri():
+        search_for_triangulation_batch_device(kps, desc, cnt, kps, desc, cnt, Ft, Et, scale, sigma2, frame1=f1,
+                                              frame2=f2, out=tri, stream=st)
+
+    def step():
+        ex.extract_batch_device(frames, kps, desc, cnt, stream=st)
+        do_tri()
+
+    step()
+    torch.cuda.synchronize()
+    ms = event_ms(step, steps, st)
+    tri_ms = event_ms(do_tri, steps, st)
+    ex.profile(True)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    ex.profile(False)
+    brk = ex.profile_read()
+    ex.batch_status()
+    n = cnt.cpu().numpy().astype(np.float64)
+    cand = float((n[:pairs] * n[pairs:]).sum())   # query x candidate pairs scanned per step
+    W, H = 1242, 375
+    n_kp = float(n.mean())
+    fb = stage_bytes(W, H, n_kp)["fast_cells"] * 2 * pairs
+    fms = brk["fast_cells"][0] / max(brk["fast_cells"][1], 1)
+    bytes_pair = 2 * algorithmic_bytes(W, H, n_kp)[0]
+    r = {"workload": "C3: stereo 1242x375 (KITTI-shaped synthetic, 8 depth bands), 2000 features, extract L+R + "
+                     "SearchForTriangulation (single BoW node), per stereo pair",
+         "pairs_per_step": pairs, "pairs_per_s": pairs / (ms * 1e-3), "ms_per_step": ms,
+         "triangulation_ms_per_step": tri_ms, "extract_stage_ms_per_step": {k: v[0] / 3 for k, v in brk.items()},
+         "keypoints_per_frame": n_kp, "matches_per_pair": float(tri[1].double().mean().item()),
+         "roofline": {"bound": "hbm", "kernel": "fast_cells", "achieved": fb / (fms * 1e-3) / 1e9 if fms else 0.0,
+                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": fb / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS if fms else 0.0,
+                      "algorithmic_bytes_per_launch": fb, "avg_launch_ms": fms,
+                      "pipeline_algorithmic_GBs": bytes_pair * pairs / (ms * 1e-3) / 1e9},
+         "triangulation_roofline": {"bound": "valu", "kernel": "tri_all_kernel",
+                                    "achieved": 16 * cand / (tri_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS,
+                                    "unit": "T lane-ops/s", "frac": 16 * cand / (tri_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
+                                    "ops": "16 VALU lane-ops (8 xor + 8 popcount) per query x candidate",
+                                    "int8_mfma_equivalent_TOPS": 512 * cand / (tri_ms * 1e-3) / 1e12}}
+    if cpu:
+        O = oracle()
+        p = O.params(2000)
+
+        def work(stop):
+            k = 0
+            i = int.from_bytes(os.urandom(1), "little")
+            while time.perf_counter() < stop or k < 1:
+                L, R = pool[i % 8]
+                kl, dl, _ = O.extract(p, L)
+                kr, dr, _ = O.extract(p, R)
+                keep = O._Keep()
+                one = lambda kk, dd: O.tri_frame(keep, np.ascontiguousarray(np.stack([kk["x"], kk["y"]], 1)),  # noqa
+                                                 kk["octave"], np.full(len(kk), -1, np.float32),
+                                                 np.zeros(len(kk), np.uint8), dd, np.array([0], np.uint32),
+                                                 np.array([0, len(kk)], np.int32), np.arange(len(kk), dtype=np.int32))
+                O.search_for_triangulation(one(kl, dl), one(kr, dr), F12, ep2, scale, sigma2, False)
+                k += 1
+                i += 1
+            return k
+
+        r["cpu_baseline"] = cpu_baseline_block("pairs/s", "stereo pairs (extract L + R + SearchForTriangulation)",
+                                               run_threads(work, 1, 6.0), run_threads(work, info["threads_all"], 6.0),
+                                               info)
+    return r
+
+
+def ba_flops_per_iter(prob):
+    """SURVEY §8d F_iter = 380 E_mono + 520 E_stereo + sum_pts (45 + 144k + 108 k(k+1)) + (6P)^3/3 +
+    4 (6P)^2 + sum_pts (36k + 18), P = free keyframes, k = observations per point."""
+    st = prob["edge_obs"][:, 2] >= 0
+    k = np.bincount(prob["edge_point"], minlength=len(prob["points"])).astype(np.float64)
+    k = k[k > 0]
+    P = int((prob["pose_fixed"] == 0).sum())
+    D = 6.0 * P
+    return (380.0 * (~st).sum() + 520.0 * st.sum() + (45 + 144 * k + 108 * k * (k + 1)).sum() + D ** 3 / 3 +
+            4 * D ** 2 + (36 * k + 18).sum())
+
+
+def localba_leg(local, calls=8, cpu=True, info=None):
+    from orb_slam2_refactored_amd.optimizer import LocalBundleAdjustment
+    from orb_slam2_refactored_amd.synth import make_ba_problem
+    prob = make_ba_problem(0, n_kf=20, n_pts=3000, n_fixed=2)
+    LocalBundleAdjustment(prob, device=local)   # warm-up
     iters = 0
-    calls = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or calls < 2:
-        r = O.local_ba(prob)
+    lat = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        r = LocalBundleAdjustment(prob, device=local)
+        lat.append(time.perf_counter() - t0)
         iters += sum(r["iterations"])
-        calls += 1
-    dt = time.perf_counter() - t0
-    return {"iters_per_s": iters / dt, "ms_per_call": 1e3 * dt / calls, "calls": calls, "cores": 1, "kind": "port"}
+    dt = sum(lat)
+    f_iter = ba_flops_per_iter(prob)
+    ips = iters / dt
+    out = {"workload": "C4: 20 KF x 3000 MP (KF0 + 2 fixed cameras), optimize(5) + optimize(10), fp64",
+           "iters_per_s": ips, "ms_per_call": 1e3 * dt / calls, "ms_per_call_median": 1e3 * float(np.median(lat)),
+           "edges": int(len(prob["edge_point"])), "iterations_per_call": iters / calls,
+           "roofline": {"bound": "fp64", "achieved": f_iter * ips / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": f_iter * ips / 1e12 / FP64_PEAK_TFLOPS, "flops_per_iter": f_iter,
+                        "note": "latency-bound: one 114x114 LDL^T + 8 small launches per LM trial"}}
+    if cpu:
+        O = oracle()
+        it = 0
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 5.0 or n < 2:
+            it += sum(O.local_ba(prob)["iterations"])
+            n += 1
+        d = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": it / d, "unit": "LM iterations/s", "ms_per_call": 1e3 * d / n, "calls": n,
+                               "cores": 1, "kind": "port",
+                               "sample": "oracle g2o restatement (Eigen-free), 1 thread as g2o without OpenMP",
+                               "cpu_model": (info or {}).get("cpu_model")}
+    return out
 
 
 def stereo_leg(dev, local, pairs=64, steps=5):
-    """configs[2]-shaped secondary measurement: 1242x375 stereo pairs (8 depth bands), both sides
-    extracted in one batch each, then ComputeStereoMatches per pair on the on-device pyramids."""
+    """§8f row 1 (ComputeStereoMatches) on C3-shaped pairs, both sides extracted in one batch each."""
     import torch
     from orb_slam2_refactored_amd import ORBextractor
     from orb_slam2_refactored_amd.matcher import stereo_matches_batch_device
@@ -119,28 +431,17 @@ def stereo_leg(dev, local, pairs=64, steps=5):
     outl = exl.extract_batch_device(Ls)
     outr = exr.extract_batch_device(Rs)
     out = stereo_matches_batch_device(exl, exr, outl, outr, bf, base)
+    st = torch.cuda.current_stream()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        exl.extract_batch_device(Ls, *outl)
-        exr.extract_batch_device(Rs, *outr)
-        stereo_matches_batch_device(exl, exr, outl, outr, bf, base, out=out)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    t1 = time.perf_counter()
-    for _ in range(steps):
-        stereo_matches_batch_device(exl, exr, outl, outr, bf, base, out=out)
-    torch.cuda.synchronize()
-    dts = (time.perf_counter() - t1) / steps
+    ms = event_ms(lambda: stereo_matches_batch_device(exl, exr, outl, outr, bf, base, out=out, stream=st), steps, st)
     matched = float((out[1] > 0).sum().item()) / pairs
-    return {"workload": "C3-shaped: 1242x375 stereo pairs, 2000 features, extract L+R + ComputeStereoMatches",
-            "pairs_per_step": pairs, "pairs_per_s": pairs / dt, "stereo_match_ms_per_step": 1e3 * dts,
+    return {"workload": "ComputeStereoMatches on 1242x375 stereo pairs (extracted on the device), 2000 features",
+            "pairs_per_step": pairs, "pairs_per_s": pairs / (ms * 1e-3), "stereo_match_ms_per_step": ms,
             "matched_per_pair": matched}
 
 
 def pose_leg(dev, frames=1024, edges=1000, steps=10, cpu=True):
-    """§8f row 3: batched PoseOptimization (Optimizer.cc:345-489), frames x edges map-point matches
-    (KITTI-tracking sized), inputs resident in HBM, one launch per step; CPU oracle beside it."""
+    """§8f row 3: batched PoseOptimization (Optimizer.cc:345-489), inputs resident in HBM."""
     import torch
     from orb_slam2_refactored_amd.optimizer import pose_optimization_device
     from orb_slam2_refactored_amd.synth import make_pose_batch
@@ -148,23 +449,17 @@ def pose_leg(dev, frames=1024, edges=1000, steps=10, cpu=True):
     d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items() if not k.startswith("gt_")}
     out = pose_optimization_device(d)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        pose_optimization_device(d, out=out)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+    st = torch.cuda.current_stream()
+    ms = event_ms(lambda: pose_optimization_device(d, out=out), steps, st)
     r = {"workload": f"{frames} frames x {edges} edges (40 % stereo, 10 % outliers), 4 x optimize(10), fp64",
          "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms,
          "mean_inliers": float(out["n_inliers"].double().mean().item())}
     if cpu:
-        sys.path.insert(0, str(ROOT / "tests"))
-        import oracle_api as O
+        O = oracle()
         sub = make_pose_batch(13, n_frames=16, n_edges=edges)
         t0 = time.perf_counter()
         n = 0
-        while time.perf_counter() - t0 < 4.0 or n < 16:
+        while time.perf_counter() - t0 < 3.0 or n < 16:
             O.pose_optimization(sub)
             n += 16
         r["cpu_baseline"] = {"frames_per_s": n / (time.perf_counter() - t0), "cores": 1, "kind": "port",
@@ -173,8 +468,7 @@ def pose_leg(dev, frames=1024, edges=1000, steps=10, cpu=True):
 
 
 def projection_leg(dev, frames=256, steps=10, cpu=True):
-    """§8f row 2: batched SearchByProjection + FeaturesGrid (ORBmatcher.cc:315-382, Frame.cc:71-145):
-    per frame 2000 keypoints and 1500 local map points (th 1, nnratio 0.8), inputs in HBM."""
+    """§8f row 2: batched SearchByProjection + FeaturesGrid: 2000 keypoints / 1500 map points per frame."""
     import torch
     from orb_slam2_refactored_amd.matcher import search_by_projection_device
     from orb_slam2_refactored_amd.synth import make_proj_batch, tile_proj_batch
@@ -184,19 +478,12 @@ def projection_leg(dev, frames=256, steps=10, cpu=True):
              else v) for k, v in b.items()}
     km, nm = search_by_projection_device(d)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        search_by_projection_device(d, km, nm)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+    st = torch.cuda.current_stream()
+    ms = event_ms(lambda: search_by_projection_device(d, km, nm), steps, st)
     r = {"workload": f"{frames} frames x (2000 keypoints, 1500 map points), th 1, grid + score + claim walk",
-         "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms,
-         "mean_matches": float(nm.double().mean().item())}
+         "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms, "mean_matches": float(nm.double().mean().item())}
     if cpu:
-        sys.path.insert(0, str(ROOT / "tests"))
-        import oracle_api as O
+        O = oracle()
         t0 = time.perf_counter()
         n = 0
         while time.perf_counter() - t0 < 3.0 or n < 16:
@@ -208,9 +495,8 @@ def projection_leg(dev, frames=256, steps=10, cpu=True):
 
 
 def bow_leg(dev, local, frames=128, n=2000, steps=10, cpu=True):
-    """§8f row 4: Frame::ComputeBoW = ORBVocabulary::transform(desc, BowVector, FeatureVector, 4)
-    (TemplatedVocabulary.h:1130-1263) on an ORBvoc-shaped synthetic tree (k 10, L 6, 1.1 M nodes),
-    `frames` descriptor sets of `n` rows resident in HBM."""
+    """§8f row 4: ORBVocabulary::transform(desc, BowVector, FeatureVector, 4) on an ORBvoc-shaped
+    synthetic tree (k 10, L 6, 1.1 M nodes)."""
     import torch
     from orb_slam2_refactored_amd.synth import make_full_vocabulary
     from orb_slam2_refactored_amd.vocabulary import ORBVocabulary
@@ -223,19 +509,12 @@ def bow_leg(dev, local, frames=128, n=2000, steps=10, cpu=True):
     counts = torch.full((frames,), n, dtype=torch.int32, device=dev)
     out = voc.transform_batch_device(desc, counts)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        voc.transform_batch_device(desc, counts, out=out)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+    st = torch.cuda.current_stream()
+    ms = event_ms(lambda: voc.transform_batch_device(desc, counts, out=out), steps, st)
     r = {"workload": f"{frames} frames x {n} descriptors, vocabulary k 10 L 6 (1.11 M nodes), levelsup 4",
-         "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms,
-         "mean_words": float(out["n_words"].double().mean().item())}
+         "frames_per_s": frames / (ms * 1e-3), "ms_per_step": ms, "mean_words": float(out["n_words"].double().mean().item())}
     if cpu:
-        sys.path.insert(0, str(ROOT / "tests"))
-        import oracle_api as O
+        O = oracle()
         o = O.Vocabulary(v)
         t0 = time.perf_counter()
         k = 0
@@ -247,21 +526,20 @@ def bow_leg(dev, local, frames=128, n=2000, steps=10, cpu=True):
     return r
 
 
+# ------------------------------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=128, help="frames per step per GPU")
+    ap.add_argument("--frames", type=int, default=1024, help="frames per step for the whole job (sharded over ranks)")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-ba", action="store_true")
-    ap.add_argument("--no-stereo", action="store_true")
-    ap.add_argument("--no-pose", action="store_true")
-    ap.add_argument("--no-projection", action="store_true")
-    ap.add_argument("--no-bow", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="only the headline C2 measurement")
+    for leg in ("c1", "textured", "c3", "ba", "stereo", "pose", "projection", "bow"):
+        ap.add_argument(f"--no-{leg}", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -276,57 +554,81 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
-    from orb_slam2_refactored_amd.synth import synth_image
-    from orb_slam2_refactored_amd.shard import SlotExchange, Slots, shard_range
+    from orb_slam2_refactored_amd.shard import SlotExchange, Slots, cross_shard_predecessor, shard_range
+    from orb_slam2_refactored_amd.synth import pan_sequence
 
-    W, H, B = args.width, args.height, args.frames
-    # synthetic frames: this rank's shard of world*B global frames (seed = global frame index);
-    # a pool of 16 distinct images is tiled over the batch
-    g0, _ = shard_range(world * B, world, rank)
-    pool = min(B, 16)
-    base = np.stack([synth_image(g0 + i, W, H) for i in range(pool)])
-    frames_np = np.concatenate([base[i % pool][None] for i in range(B)])
-    frames = torch.from_numpy(frames_np).to(dev)
+    W, H = args.width, args.height
+    total = args.frames
+    if total % world:
+        raise SystemExit("--frames must be a multiple of the number of ranks (equal shards for the all-gather)")
+    g0, B = shard_range(total, world, rank)
+    # the global job is a pan sequence of 16 distinct frames repeated (frame g = base[g % 16]); every
+    # frame is its own buffer in HBM (1024 x 0.92 MB >> the 256 MB Infinity Cache)
+    base = pan_sequence(0, W, H, 16)
+    gidx = torch.arange(g0, g0 + B) % 16
+    frames = torch.from_numpy(base).to(dev)[gidx.to(dev)].contiguous()
+    frames_np = base
     ex = ORBextractor(ORBextractor.Parameters(nfeatures=args.nfeatures), device=local)
     m = ORBmatcher(0.6, False)
     cap = ex.max_keypoints(H, W)
-    prev_idx = torch.tensor([(i - 1) % B for i in range(B)], dtype=torch.int32, device=dev)
-    match_out = torch.empty((4, B, cap), dtype=torch.int32, device=dev)
-    # world > 1: double-buffered async all-gather of every rank's slots (shard.SlotExchange);
-    # step k's collectives overlap step k+1's kernels.
-    xchg = SlotExchange(B, cap, dev) if world > 1 else None
-    single = Slots.empty(B, cap, dev)
     stream = torch.cuda.current_stream()
-    last = [single]
+    match_out = torch.empty((4, B, cap), dtype=torch.int32, device=dev)
+    if world == 1:
+        # frame i vs i-1 (frame 0 vs the job's last frame)
+        prev_idx = torch.tensor([(i - 1) % B for i in range(B)], dtype=torch.int32, device=dev)
+        single = Slots.empty(B, cap, dev)
+        xchg = None
+    else:
+        # frames 1.. of the shard vs their in-shard predecessor; frame 0 vs rank r-1's last frame from the
+        # gathered slots (cross_shard_predecessor), matched one step later behind the gather's wait
+        prev_idx = torch.arange(0, B - 1, dtype=torch.int32, device=dev)
+        xchg = SlotExchange(B, cap, dev)
+        pred = cross_shard_predecessor(rank, world, B)
+        pred_idx = torch.tensor([pred], dtype=torch.int32, device=dev)
+        cross_out = torch.empty((4, 1, cap), dtype=torch.int32, device=dev)
+    state = {"pending": None}
+
+    def cross_match(i):
+        xchg.wait(i)
+        loc, glob = xchg.local[i], xchg.gathered(i)
+        m.match_batch_device(loc.desc[0:1], loc.counts[0:1], glob.desc, glob.counts, out=cross_out, stream=stream,
+                             pair_b=pred_idx)
 
     def step():
-        local = xchg.acquire() if xchg else single
-        ex.extract_batch_device(frames, local.kps, local.desc, local.counts, stream=stream)
-        m.match_batch_device(local.desc, local.counts, local.desc, local.counts, out=match_out, stream=stream,
-                             pair_b=prev_idx)
-        if xchg:
-            xchg.publish()
-        last[0] = local
+        if xchg is None:
+            ex.extract_batch_device(frames, single.kps, single.desc, single.counts, stream=stream)
+            m.match_batch_device(single.desc, single.counts, single.desc, single.counts, out=match_out, stream=stream,
+                                 pair_b=prev_idx)
+            return
+        loc = xchg.acquire()
+        ex.extract_batch_device(frames, loc.kps, loc.desc, loc.counts, stream=stream)
+        if B > 1:
+            m.match_batch_device(loc.desc[1:], loc.counts[1:], loc.desc, loc.counts, out=match_out[:, 1:],
+                                 stream=stream, pair_b=prev_idx)
+        i = xchg.publish()
+        if state["pending"] is not None:
+            cross_match(state["pending"])
+        state["pending"] = i
+
+    def finish():
+        if xchg is not None and state["pending"] is not None:
+            cross_match(state["pending"])
+            state["pending"] = None
 
     for _ in range(args.warmup):
         step()
-    if xchg:
-        xchg.drain()
+    finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # inside the timed region only the dominant kernel (fast_cells) carries launch events (events on
-    # every kernel cost ~3.5 % of the step); the other stages are timed in a separate pass below
+    # inside the timed region only the dominant kernel (fast_cells) carries launch events (events on every
+    # kernel cost ~3.5 %); the other stages are timed in a separate pass below
     ex.profile(True, stages=["fast_cells"])
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
         step()
-    if xchg:
-        xchg.drain()
-    ev1.record(stream)
+    finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -334,10 +636,11 @@ def main():
     elapsed = time.perf_counter() - t0
     ex.profile(False)
     timed = ex.profile_read()
-    # per-stage breakdown: a separate short pass with events on every kernel (not the timed region)
+    fault = ex.batch_status()   # raises if any device capacity check tripped in the timed steps
     ex.profile(True)
     for _ in range(3):
         step()
+    finish()
     torch.cuda.synchronize()
     ex.profile(False)
     breakdown = ex.profile_read()
@@ -347,37 +650,24 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    n_kp = float(last[0].counts.float().mean().item())
+    counts = (single.counts if xchg is None else xchg.local[0].counts)
+    n_kp = float(counts.float().mean().item())
     matches = int((match_out[3] >= 0).sum().item())
-    total_frames = world * B * args.steps
-    value = total_frames / elapsed
+    value = total * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
-
-    # roofline of the dominant kernel (per-launch algorithmic bytes / average launch time)
     bytes_frame, P = algorithmic_bytes(W, H, n_kp)
-    stage_bytes = {
-        "pyramid": (P - W * H) + (P - level_sizes(W, H)[-1][0] * level_sizes(W, H)[-1][1]),   # read l-1, write l
-        "fast_cells": P + 4 * 0,    # every level read once (candidate lists are intermediates)
-        "quadtree": 0,
-        "describe": 60 * n_kp,      # keypoint + descriptor writes (neighbourhood reads are L2 re-reads)
-    }
+    sb = stage_bytes(W, H, n_kp)
     dom = max(breakdown, key=lambda k: breakdown[k][0])
-    if dom == "fast_cells":   # the live launch times of the timed region
-        dom_ms, dom_launches = timed[dom]
-        dom_steps = args.steps
-    else:                     # another stage dominates: its times from the breakdown pass
-        dom_ms, dom_launches = breakdown[dom]
-        dom_steps = brk_steps
-    traffic = measured_traffic(dom, dom_launches / max(dom_steps, 1), B, W, H, args.nfeatures)
+    if dom == "fast_cells":
+        dom_ms, dom_launches, dom_steps = timed[dom][0], timed[dom][1], args.steps
+    else:
+        dom_ms, dom_launches, dom_steps = breakdown[dom][0], breakdown[dom][1], brk_steps
     per_launch_ms = dom_ms / max(dom_launches, 1)
     launches_per_step = dom_launches / max(dom_steps, 1)
-    # a stage may run as several launches per step (fast_cells: level 0 on the side stream, levels
-    # 1..7 on the main stream): achieved = the step's algorithmic bytes / the step's summed launch
-    # durations, i.e. per launch = bytes / launches_per_step over the average launch duration
-    dom_bytes = stage_bytes[dom] * B / max(launches_per_step, 1)
+    dom_bytes = sb[dom] * B / max(launches_per_step, 1)
     achieved = dom_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
+    traffic = measured_traffic(dom, B, W, H, args.nfeatures)
     extract_ms = sum(v[0] for v in breakdown.values()) / brk_steps
-    pipeline_gbs = bytes_frame * B / (extract_ms * 1e-3) / 1e9 if extract_ms > 0 else 0.0
 
     result = {
         "metric": METRIC,
@@ -388,15 +678,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic",
+        "data": "synthetic (pan sequence of §8d G frames, shifted (+3,+2) px per frame)",
         "config": {"workload": f"C2: {W}x{H} mono, 8 levels, {args.nfeatures} features, extract + brute-force "
-                               f"Hamming top-2/ratio match vs previous frame",
-                   "frames_per_step_per_gpu": B, "width": W, "height": H, "nlevels": 8,
-                   "nfeatures": args.nfeatures, "parallelism": f"frames sharded over {world} GPU(s)"
-                   + (", RCCL all-gather of descriptor slots" if world > 1 else "")},
+                               f"Hamming top-2/ratio match of every frame vs its predecessor",
+                   "frames_per_step": total, "frames_per_step_per_gpu": B, "width": W, "height": H, "nlevels": 8,
+                   "nfeatures": args.nfeatures, "parallelism": f"{total}-frame job sharded over {world} GPU(s)"
+                   + (", RCCL all-gather of descriptor slots, cross-shard predecessor match" if world > 1 else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": per_launch_ms,
@@ -404,45 +694,44 @@ def main():
                      "timed_from": "timed region" if dom == "fast_cells" else "breakdown pass",
                      "stage_ms_per_step": {k: v[0] / brk_steps for k, v in breakdown.items()},
                      "stage_ms_source": "separate 3-step pass with launch events on every kernel",
-                     "pipeline_algorithmic_GBs": pipeline_gbs, "pipeline_bytes_per_frame": bytes_frame},
+                     "pipeline_algorithmic_GBs": bytes_frame * B / (extract_ms * 1e-3) / 1e9 if extract_ms else 0.0,
+                     "pipeline_bytes_per_frame": bytes_frame},
         "keypoints_per_frame": n_kp,
         "matches_last_step": matches,
+        "device_fault_mask": fault,
+        "timed_region_s": elapsed,
     }
+    if world > 1:
+        slot_bytes = cap * (28 + 32) + 4
+        result["c5"] = {"workload": "C5 semantics: frames sharded, RCCL all-gather of padded slots, frame i matched "
+                                    "to i-1 across shard boundaries from the gathered slots",
+                        "gather_bytes_per_step": slot_bytes * total, "cross_shard_predecessor": pred,
+                        "cross_match_first_frame_matches": int((cross_out[3] >= 0).sum().item())}
 
-    if rank == 0 and not args.no_ba:
-        from orb_slam2_refactored_amd.optimizer import LocalBundleAdjustment
-        from orb_slam2_refactored_amd.synth import make_ba_problem
-        prob = make_ba_problem(0, n_kf=20, n_pts=3000, n_fixed=2)
-        LocalBundleAdjustment(prob, device=local)   # warm-up
-        iters = 0
-        t1 = time.perf_counter()
-        calls = 0
-        while calls < 5:
-            r = LocalBundleAdjustment(prob, device=local)
-            iters += sum(r["iterations"])
-            calls += 1
-        dtb = time.perf_counter() - t1
-        result["localba"] = {"workload": "C4: 20 KF x 3000 MP, optimize(5)+optimize(10), fp64",
-                             "iters_per_s": iters / dtb, "ms_per_call": 1e3 * dtb / calls,
-                             "edges": int(len(prob["edge_point"]))}
-        if world == 1 and not args.no_cpu_baseline:
-            result["localba"]["cpu_baseline"] = cpu_ba_baseline(prob)
-
-    if rank == 0 and not args.no_stereo:
+    legs = rank == 0 and not args.no_legs
+    cpu = world == 1 and not args.no_cpu_baseline and rank == 0
+    info = cpu_info()
+    if legs and not args.no_c1:
+        result["c1"] = c1_leg(dev, local, cpu=cpu, info=info)
+    if legs and not args.no_textured:
+        result["c2_textured"] = c2_textured_leg(dev, local, cpu=cpu, info=info)
+    if legs and not args.no_c3:
+        result["c3"] = c3_leg(dev, local, cpu=cpu, info=info)
+    if legs and not args.no_ba:
+        result["localba"] = localba_leg(local, cpu=cpu, info=info)
+    if legs and not args.no_stereo:
         result["stereo"] = stereo_leg(dev, local)
-
-    if rank == 0 and not args.no_projection:
-        result["search_by_projection"] = projection_leg(dev, cpu=world == 1 and not args.no_cpu_baseline)
-
-    if rank == 0 and not args.no_bow:
-        result["bow"] = bow_leg(dev, local, cpu=world == 1 and not args.no_cpu_baseline)
-
-    if rank == 0 and not args.no_pose:
-        result["pose_opt"] = pose_leg(dev, cpu=world == 1 and not args.no_cpu_baseline)
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(frames_np[:4], args.nfeatures)
-        result["cpu_baseline"]["host"] = os.uname().nodename
+    if legs and not args.no_projection:
+        result["search_by_projection"] = projection_leg(dev, cpu=cpu)
+    if legs and not args.no_bow:
+        result["bow"] = bow_leg(dev, local, cpu=cpu)
+    if legs and not args.no_pose:
+        result["pose_opt"] = pose_leg(dev, cpu=cpu)
+    if cpu:
+        result["cpu_baseline"] = cpu_baseline_block(
+            "frames/s", f"{W}x{H} pan-sequence frames, extract + brute-force match vs previous",
+            cpu_extract_match(frames_np[:4], args.nfeatures, 1, 8.0),
+            cpu_extract_match(frames_np[:8], args.nfeatures, info["threads_all"], 8.0), info)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -30,6 +30,15 @@ def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     return start, base + (1 if rank < extra else 0)
 
 
+def cross_shard_predecessor(rank: int, world: int, frames_per_rank: int) -> int:
+    """Index, in the gathered slot buffer (rank-major: rank r's local frame f at r*frames_per_rank + f),
+    of the predecessor of this rank's first frame: global frame g0 - 1, i.e. rank r-1's last frame
+    (wrapping to the job's last frame for rank 0).  §8d C5: "frame i matched to i-1"."""
+    if world <= 0 or not (0 <= rank < world) or frames_per_rank <= 0:
+        raise ValueError("bad shard arguments")
+    return (rank * frames_per_rank - 1) % (world * frames_per_rank)
+
+
 @dataclass
 class Slots:
     """One rank's extraction output for a batch of frames (device or CPU tensors)."""
@@ -92,6 +101,10 @@ class SlotExchange:
         for w in self._work[i]:
             w.wait()
         self._work[i] = []
+
+    def wait(self, i: int) -> None:
+        """Order the current stream after the gather of set i (no host sync with NCCL; gloo blocks)."""
+        self._wait(i)
 
     def drain(self) -> None:
         for i in range(self.depth):

@@ -28,6 +28,36 @@ def shifted_pair(seed: int, width: int, height: int, dx: int = 3, dy: int = 2):
     return a, b
 
 
+def pan_sequence(seed: int, width: int, height: int, n: int, dx: int = 3, dy: int = 2) -> np.ndarray:
+    """A camera-pan sequence for the C2 / C5 "frame i matched to i-1" workload: frame 0 = G(seed) and
+    frame k = frame k-1 shifted by (dx, dy) with edge replicate and fresh noise U{-3..3} (the
+    shifted pair of SURVEY.md §8d C2, chained).  Returns [n, H, W] uint8."""
+    out = np.empty((n, height, width), np.uint8)
+    out[0] = synth_image(seed, width, height)
+    rng = np.random.default_rng(seed + 1000)
+    for k in range(1, n):
+        base = np.pad(out[k - 1].astype(np.int16), ((dy, 0), (dx, 0)), mode="edge")[:height, :width]
+        out[k] = np.clip(base + rng.integers(-3, 4, size=(height, width)), 0, 255).astype(np.uint8)
+    return out
+
+
+def textured_image(seed: int, width: int, height: int) -> np.ndarray:
+    """Texture-rich frame (FAST fires almost everywhere, thousands of candidates per level):
+    low-frequency value noise (1/8 resolution, bilinear) at +-40 grey levels plus per-pixel
+    Gaussian noise sigma 12, around 128."""
+    rng = np.random.default_rng(seed)
+    gh, gw = height // 8 + 2, width // 8 + 2
+    g = rng.normal(0, 40, (gh, gw))
+    ys = np.arange(height) / 8.0
+    xs = np.arange(width) / 8.0
+    y0, x0 = ys.astype(int), xs.astype(int)
+    fy, fx = (ys - y0)[:, None], (xs - x0)[None, :]
+    low = (g[y0][:, x0] * (1 - fy) * (1 - fx) + g[y0 + 1][:, x0] * fy * (1 - fx) +
+           g[y0][:, x0 + 1] * (1 - fy) * fx + g[y0 + 1][:, x0 + 1] * fy * fx)
+    img = 128 + low + rng.normal(0, 12, (height, width))
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
 # KITTI 00-02 intrinsics (Examples/Stereo/KITTI00-02.yaml:8-25)
 KITTI = dict(fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, bf=386.1448, width=1241, height=376)
 

@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-from orb_slam2_refactored_amd.shard import SlotExchange, Slots, shard_range, unpack  # noqa: E402
+from orb_slam2_refactored_amd.shard import SlotExchange, Slots, cross_shard_predecessor, shard_range, unpack  # noqa: E402
 
 FRAMES, CAP, STEPS = 3, 40, 5
 
@@ -70,6 +70,25 @@ def _worker(rank, world, port, errq):
         per_frame = unpack(g)
         assert len(per_frame) == world * FRAMES
         assert [int(k.shape[0]) for k, _ in per_frame] == g.counts.tolist()
+        # C5 cross-shard pairing (bench.py): this rank's first frame (global g0) is matched against the
+        # gathered slot of global frame g0 - 1, which is rank r-1's last local frame (rank 0 wraps to
+        # the job's last frame); the matcher reads it from the gathered buffer
+        pred = cross_shard_predecessor(rank, world, FRAMES)
+        pr, pf = divmod(pred, FRAMES)
+        assert pr == (rank - 1) % world and pf == FRAMES - 1
+        assert shard_range(world * FRAMES, world, pr)[0] + pf == (start - 1) % (world * FRAMES)
+        want_prev = fake_slots(shard_range(world * FRAMES, world, pr)[0], STEPS - 1)
+        assert torch.equal(g.desc[pred], want_prev.desc[FRAMES - 1])
+        assert int(g.counts[pred]) == int(want_prev.counts[FRAMES - 1])
+        # the cross-shard match on the gathered data equals the match against the predecessor's own slots
+        import oracle_api as O
+        mine = fake_slots(start, STEPS - 1)
+        na, nb = int(mine.counts[0]), int(g.counts[pred])
+        a = mine.desc[0, :na].numpy()
+        got = O.bf_match(a, g.desc[pred, :nb].numpy())
+        exp = O.bf_match(a, want_prev.desc[FRAMES - 1, :nb].numpy())
+        for x, y in zip(got, exp):
+            assert (x == y).all()
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:  # pragma: no cover - reported by the parent
@@ -77,7 +96,7 @@ def _worker(rank, world, port, errq):
         raise
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_slot_exchange_gloo(world):
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
@@ -104,6 +123,13 @@ def test_shard_range_partitions():
             assert seen == list(range(n))
     with pytest.raises(ValueError):
         shard_range(4, 2, 2)
+
+
+def test_cross_shard_predecessor():
+    assert cross_shard_predecessor(0, 1, 5) == 4
+    assert [cross_shard_predecessor(r, 4, 3) for r in range(4)] == [11, 2, 5, 8]
+    with pytest.raises(ValueError):
+        cross_shard_predecessor(2, 2, 3)
 
 
 def test_single_process_exchange_is_copy():
