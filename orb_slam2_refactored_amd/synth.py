@@ -30,13 +30,15 @@ def shifted_pair(seed: int, width: int, height: int, dx: int = 3, dy: int = 2):
 
 def pan_sequence(seed: int, width: int, height: int, n: int, dx: int = 3, dy: int = 2) -> np.ndarray:
     """A camera-pan sequence for the C2 / C5 "frame i matched to i-1" workload: frame 0 = G(seed) and
-    frame k = frame k-1 shifted by (dx, dy) with edge replicate and fresh noise U{-3..3} (the
-    shifted pair of SURVEY.md §8d C2, chained).  Returns [n, H, W] uint8."""
+    frame k = G(seed) shifted by k*(dx, dy) with edge replicate plus fresh noise U{-3..3} (frame k and
+    k-1 are the shifted pair of SURVEY.md §8d C2; the noise does not accumulate along the chain).
+    Returns [n, H, W] uint8."""
     out = np.empty((n, height, width), np.uint8)
-    out[0] = synth_image(seed, width, height)
+    a = synth_image(seed, width, height).astype(np.int16)
+    out[0] = a
     rng = np.random.default_rng(seed + 1000)
     for k in range(1, n):
-        base = np.pad(out[k - 1].astype(np.int16), ((dy, 0), (dx, 0)), mode="edge")[:height, :width]
+        base = np.pad(a, ((k * dy, 0), (k * dx, 0)), mode="edge")[:height, :width]
         out[k] = np.clip(base + rng.integers(-3, 4, size=(height, width)), 0, 255).astype(np.uint8)
     return out
 
