@@ -3,9 +3,11 @@
 
 Headline line (`value`): configs[1] / C2 — 1280x720 mono, 8 levels, 2000 features, extract + brute-force
 Hamming top-2/ratio match of every frame against its predecessor.  One step = one batch of `--frames`
-(default 1024, the C5 batch) synthetic frames already resident in HBM: a camera-pan sequence (frame i =
-frame i-1 shifted by (+3, +2) px with fresh noise, the §8d C2 shifted pair, chained), so frame i is
-matched to i-1 as §8d C5 says.  With N > 1 ranks the 1024-frame job is sharded (strong scaling): rank r
+(default 8192 = eight 1024-frame C5 jobs, so the driver's 20 steps time > 1 s and at N = 8 every GPU
+holds the 1024 frames C5 gives the whole node) synthetic frames already resident in HBM: a camera-pan
+sequence (frame i = frame 0 shifted by i * (+3, +2) px with fresh noise: consecutive frames are the §8d
+C2 shifted pair), so frame i is matched to i-1 as §8d C5 says.  With N > 1 ranks the job is sharded
+(strong scaling): rank r
 extracts its contiguous shard, matches frames 1.. of the shard locally, all-gathers the padded
 keypoint / descriptor slots over RCCL (the loop-closure descriptor exchange of configs[4]) and matches
 its first frame against rank r-1's last frame read from the gathered slots (one step later, so the
@@ -532,7 +534,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=1024, help="frames per step for the whole job (sharded over ranks)")
+    ap.add_argument("--frames", type=int, default=8192, help="frames per step for the whole job (sharded over ranks)")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--nfeatures", type=int, default=2000)
@@ -563,7 +565,7 @@ def main():
         raise SystemExit("--frames must be a multiple of the number of ranks (equal shards for the all-gather)")
     g0, B = shard_range(total, world, rank)
     # the global job is a pan sequence of 16 distinct frames repeated (frame g = base[g % 16]); every
-    # frame is its own buffer in HBM (1024 x 0.92 MB >> the 256 MB Infinity Cache)
+    # frame is its own buffer in HBM (8192 x 0.92 MB >> the 256 MB Infinity Cache)
     base = pan_sequence(0, W, H, 16)
     gidx = torch.arange(g0, g0 + B) % 16
     frames = torch.from_numpy(base).to(dev)[gidx.to(dev)].contiguous()

@@ -1001,6 +1001,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     if (qn > head) drain(qn - head);
     if (q2n > h2) strength(q2n - h2);
     wave_lds_sync();
+    if (item == i_beg) FAST_STAMP(3, __builtin_amdgcn_s_memtime());
 
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
     const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
@@ -1092,6 +1093,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         running += popc64(bm);
     }
     }   // list NMS
+    if (item == i_beg) FAST_STAMP(4, __builtin_amdgcn_s_memtime());
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
         cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap);

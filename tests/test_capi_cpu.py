@@ -42,12 +42,31 @@ def test_product_fails_loudly_without_library(tmp_path):
 
 
 def test_package_does_not_import_oracle():
+    """The product (the package, its native sources and bench.py's timed path) never imports, loads or
+    executes the oracle: no `import oracle_api` / `from oracle...`, no ctypes / CDLL load of
+    liborb_oracle, no subprocess into oracle/.  bench.py may use it only in its cpu_baseline legs."""
+    bad = [re.compile(r"^\s*(import|from)\s+(oracle_api|oracle)\b", re.M),
+           re.compile(r"liborb_oracle"),
+           re.compile(r"oracle/_build"),
+           re.compile(r"CDLL\([^)]*oracle", re.I),
+           re.compile(r"subprocess\.[a-z_]+\([^)]*oracle", re.I)]
     for p in (ROOT / "orb_slam2_refactored_amd").rglob("*.py"):
         src = p.read_text()
-        assert "oracle" not in src.replace("oracle/", "").lower() or "no " in src.lower(), p
+        for rx in bad:
+            assert not rx.search(src), (p, rx.pattern)
     for p in (ROOT / "orb_slam2_refactored_amd" / "csrc").glob("*"):
-        if p.suffix in (".hip", ".h", ".cpp"):
-            assert "orb_oracle" not in p.read_text(), p
+        if p.suffix in (".hip", ".h", ".cpp", ".inc"):
+            src = p.read_text()
+            assert "orb_oracle" not in src and "oracle_" not in src, p
+    # bench.py: the oracle is reached only through oracle(), called only from cpu-baseline code
+    src = (ROOT / "bench.py").read_text()
+    assert "liborb_oracle" not in src
+    body = src[src.index("def main():"):]
+    assert "oracle" not in body.replace("cpu_baseline", "").replace("oracle/orb_oracle.cpp", ""), \
+        "main() must not touch the oracle outside the cpu-baseline helpers"
+    for m in re.finditer(r"(?<!def )oracle\(\)", src):
+        fn = src[:m.start()].rsplit("\ndef ", 1)[-1].split("(", 1)[0]
+        assert fn.startswith("cpu_") or fn.endswith("_leg") or fn == "oracle", fn
 
 
 def test_cpp_wrapper_compiles_and_links(tmp_path):
