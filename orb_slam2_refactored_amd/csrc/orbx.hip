@@ -1011,41 +1011,47 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         // row-major order, one zone row per pass (zw <= 64), the same keep rule: a corner is kept
         // at threshold t iff M > t and every neighbour is < M (for M > t, a neighbour q >= M is
         // also > t), so both thresholds share the neighbourhood maximum.
-        auto keep = [&](int y, bool& ki, bool& km) {
-            ki = km = false;
-            if (lane < zw) {
-                const uint8_t* c0 = Mc + __mul24(y, ZSd) + lane;
+        // Rows per pass: two 32-lane rows when the zone is at most 32 wide (every C1-C3 cell but the
+        // widest cells of the smallest levels), else one 64-lane row.  The keep ballots of both
+        // thresholds are computed once and kept in the (drained) passer ring for the emission pass;
+        // lane order within a pass is row-major, so the emission order is the reference's.
+        const int rsh = zw <= 32 ? 5 : 6, RP = 64 >> rsh;
+        const int zx = lane & ((1 << rsh) - 1), zr = lane >> rsh;
+        unsigned long long* dbal = reinterpret_cast<unsigned long long*>(queue);   // 2 per pass, <= 160
+        int npass = 0;
+        for (int yb = 0; yb < zh; yb += RP, npass++) {
+            const int y = yb + zr;
+            bool ki = false, km = false;
+            if (zx < zw && y < zh) {
+                const uint8_t* c0 = Mc + __mul24(y, ZSd) + zx;
                 const int m = c0[0];
                 if (m) {
-                    int nmax = 0;
-#pragma unroll
-                    for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; dx++)
-                            if (dx || dy) nmax = max(nmax, (int)c0[dy * ZSd + dx]);
+                    const int n0 = max(max((int)c0[-ZSd - 1], (int)c0[-ZSd]), (int)c0[-ZSd + 1]);
+                    const int n1 = max((int)c0[-1], (int)c0[1]);
+                    const int n2 = max(max((int)c0[ZSd - 1], (int)c0[ZSd]), (int)c0[ZSd + 1]);
+                    const int nmax = max(max(n0, n1), n2);
                     ki = m > th_ini && nmax < m;
                     km = m > th_min && nmax < m;
                 }
             }
-        };
-        for (int y = 0; y < zh; y++) {
-            bool ki, km;
-            keep(y, ki, km);
-            n_ini += popc64(__ballot(ki));
-            n_min += popc64(__ballot(km));
+            const unsigned long long bi = __ballot(ki), bmn = __ballot(km);
+            if (lane == 0) { dbal[2 * npass] = bi; dbal[2 * npass + 1] = bmn; }
+            n_ini += popc64(bi);
+            n_min += popc64(bmn);
         }
+        wave_lds_sync();
         const int which = n_ini > 0 ? 0 : 1;
         total = which == 0 ? n_ini : n_min;
         int running = 0;
-        for (int y = 0; y < zh; y++) {
-            bool ki, km;
-            keep(y, ki, km);
-            const bool k = which == 0 ? ki : km;
-            const unsigned long long bm = __ballot(k);
-            const int r = running + popc64(bm & lt);
-            if (k && r < cap)
-                out[r] = (uint32_t)(x0 + 3 + lane) | ((uint32_t)(y0 + 3 + y) << 12) |
-                         ((uint32_t)(Mc[__mul24(y, ZSd) + lane] - 1) << 24);
+        for (int pp = 0; pp < npass; pp++) {
+            const unsigned long long bm = dbal[2 * pp + which];
+            if (bm & (1ull << lane)) {
+                const int r = running + popc64(bm & lt);
+                const int y = pp * RP + zr;
+                if (r < cap)
+                    out[r] = (uint32_t)(x0 + 3 + zx) | ((uint32_t)(y0 + 3 + y) << 12) |
+                             ((uint32_t)(Mc[__mul24(y, ZSd) + zx] - 1) << 24);
+            }
             running += popc64(bm);
         }
     } else {
@@ -2283,6 +2289,10 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     {
         int mzw = 1, mzh = 1;
         for (const CellDev& c : cells) { mzw = std::max(mzw, c.zwzh & 0xffff); mzh = std::max(mzh, c.zwzh >> 16); }
+        if (mzw > 64 || mzh > (FQ_RING + FQ2_RING) / 8) {   // DetectFAST cells are < 60 px (:508-511)
+            set_error("FAST cell larger than the kernel supports");
+            return ORB_EINTERNAL;
+        }
         FastLds fl;
         fl.CS = (int)align_up(mzw + 6 + 8, 4);         // +1 shift, +4 dword over-read each side
         if (fl.CS < 4 * ((mzw + 6 + 1 + 3) / 4)) fl.CS = 4 * ((mzw + 6 + 1 + 3) / 4);

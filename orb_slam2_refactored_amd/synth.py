@@ -57,7 +57,7 @@ def textured_image(seed: int, width: int, height: int) -> np.ndarray:
     low = (g[y0][:, x0] * (1 - fy) * (1 - fx) + g[y0 + 1][:, x0] * fy * (1 - fx) +
            g[y0][:, x0 + 1] * (1 - fy) * fx + g[y0 + 1][:, x0 + 1] * fy * fx)
     img = 128 + low + rng.normal(0, 12, (height, width))
-    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8))
 
 
 # KITTI 00-02 intrinsics (Examples/Stereo/KITTI00-02.yaml:8-25)

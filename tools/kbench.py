@@ -20,12 +20,19 @@ def main():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--match", action="store_true")
+    ap.add_argument("--pan", action="store_true", help="bench.py's frames: the §8d pan sequence (default: G frames)")
+    ap.add_argument("--textured", action="store_true", help="texture-rich frames (bench.py c2_textured)")
     ap.add_argument("--no-profile", action="store_true", help="no per-stage event timing (wall time only)")
     a = ap.parse_args()
     import torch
     from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
-    from orb_slam2_refactored_amd.synth import synth_image
-    pool = np.stack([synth_image(i, a.width, a.height) for i in range(min(16, a.frames))])
+    from orb_slam2_refactored_amd.synth import pan_sequence, synth_image, textured_image
+    if a.pan:
+        pool = pan_sequence(0, a.width, a.height, min(16, a.frames))
+    elif a.textured:
+        pool = np.stack([textured_image(4000 + i, a.width, a.height) for i in range(min(16, a.frames))])
+    else:
+        pool = np.stack([synth_image(i, a.width, a.height) for i in range(min(16, a.frames))])
     frames = torch.from_numpy(np.concatenate([pool[i % len(pool)][None] for i in range(a.frames)])).cuda()
     ex = ORBextractor(ORBextractor.Parameters(nfeatures=a.nfeatures))
     kps, desc, cnt = ex.extract_batch_device(frames)

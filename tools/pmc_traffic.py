@@ -25,7 +25,7 @@ def per_dispatch(d, counter):
     return {k: sum(v.values()) / len(v) for k, v in acc.items()}
 
 
-def main(src, dst):
+def main(src, dst, frames=128):
     src = Path(src)
     cf = per_dispatch(src / "calib_FETCH_SIZE", "FETCH_SIZE")
     cw = per_dispatch(src / "calib_WRITE_SIZE", "WRITE_SIZE")
@@ -46,10 +46,12 @@ def main(src, dst):
             continue
         kernels[k] = {"fetch_bytes": kf.get(k), "write_bytes": kw.get(k)}
     out = {"source": str(src), "calibration": calib, "kernels_per_dispatch": kernels,
-           "workload": "tools/kbench.py defaults: 128 frames 1280x720, nfeatures 2000"}
+           "workload": {"frames": int(frames), "width": 1280, "height": 720, "nfeatures": 2000,
+                        "data": "tools/kbench.py --pan (bench.py's pan-sequence frames)" if int(frames) != 128
+                        else "tools/kbench.py defaults (G frames)"}}
     Path(dst).write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))
