@@ -1516,7 +1516,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             const int slot = seen % LOOKAHEAD;
             // wait for the step, mirroring the caller's stop flag into the device-visible word the
             // decide kernel polls after every trial
-            for (;;) {
+            if (!stop_flag) ORB_HIP_TRY(hipEventSynchronize(C.ring_ev[slot]));
+            while (stop_flag) {
                 const hipError_t q = hipEventQuery(C.ring_ev[slot]);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) ORB_HIP_TRY(q);
