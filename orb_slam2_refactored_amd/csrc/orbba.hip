@@ -3,17 +3,19 @@
 // g2o's Levenberg-Marquardt over SE3Expmap poses and marginalised XYZ points, fp64 throughout.
 // Points own their edges (CSR); a point is served by a group of 8 lanes (one edge per lane,
 // fixed-order shuffle reductions), so per-point work spreads over ~N/8 wavefronts.
-//   per LM iteration (OptimizationAlgorithmLevenberg::solve, levenberg.cpp:61-164)
-//     ba_iter_kernel         computeActiveErrors + robust chi2 + linearizeOplus +
-//                            constructQuadraticForm; Hll / b_l per point, per-edge pose parts
-//     ba_pose_accum_kernel   Hpp / b_p per free pose (fixed-order sums); extra block: chi2 total
-//   per trial (do { ... } while (rho < 0 ...))
-//     ba_schur_point_kernel  D^-1 = (Hll + lambda I)^-1, W = Hpl D^-1, Hpl D^-1 b_l
-//     ba_schur_block_kernel  S(i1,i2) = Hpp + lambda I - sum W Hpl^T; b_schur on diagonal blocks
+//   per LM trial (OptimizationAlgorithmLevenberg::solve, levenberg.cpp:61-164; the do { ... } while
+//   (rho < 0 ...) retries re-run only the lambda-dependent parts), five launches:
+//     ba_iter_kernel         on a new iteration: computeActiveErrors + robust chi2 + linearizeOplus +
+//                            constructQuadraticForm, Hll / b_l per point, per-edge pose parts; then
+//                            (lambda known) D^-1 = (Hll + lambda I)^-1, W = Hpl D^-1, Hpl D^-1 b_l
+//     ba_schur_block_kernel  on a new iteration: Hpp / b_p per free pose and the chi2 total; then
+//                            S(i1,i2) = Hpp + lambda I - sum W Hpl^T, b_schur on diagonal blocks
 //     ba_solve_kernel        blocked LDL^T of the (6P)^2 reduced camera system in LDS, triangular
 //                            solves, push + SE3 exp-update of the free poses
 //     ba_point_update_kernel back-substitution, push, point +=, errors + robust chi2 of its edges
 //     ba_decide_kernel       rho, lambda / nu update, accept or pop (restore)
+//   The first trial of an optimize() call runs ba_pose_accum_kernel, ba_lambda_init_kernel
+//   (computeLambdaInit) and ba_schur_point_kernel between the first two.
 // Every reduction runs in a fixed order, so results are bit-reproducible run to run.  The LM
 // control scalars live on the device; the host reads one small status block per trial to decide
 // whether to run another (the reference's loop condition), and polls the stop flag like g2o.
@@ -22,6 +24,7 @@
 #include <cstring>
 #include <vector>
 
+#include <chrono>
 #include <thread>
 
 #include "common.h"
@@ -33,12 +36,12 @@ struct BACtl {
     double lambda, ni, cur, ini, tmp, scale, rho;
     int ok2, accepted;
     double maxdiag;
-    // LM loop state, advanced on the device by ba_decide_kernel (g2o SparseOptimizer::optimize +
+    // LM loop state, advanced on the device by ba_decide_step (g2o SparseOptimizer::optimize +
     // OptimizationAlgorithmLevenberg::solve): iteration, trial within it, nBad, flags
     int it, q, nbad, done, need_lin, iters_max, iters_done;
     int trials;    // LM trials since the start of the LocalBA call (both optimize() calls; test hook)
     int stopped;   // the force-stop flag ended the loop
-    int pad;
+    int seq;       // host snapshot sequence id (written last; see ba_decide_step)
     double chi_out;
 };
 
@@ -149,15 +152,60 @@ __device__ __forceinline__ double grp_sum(double v) {
 
 constexpr int GRP = 8;   // lanes per point
 
-// Per LM iteration: errors + robust chi2 (computeActiveErrors / activeRobustChi2), linearizeOplus
-// and constructQuadraticForm of every active edge (types_six_dof_expmap.cpp:103-139,188-234;
-// base_binary_edge.hpp:54-120), Hll / b_l summed per point, pose parts stored per edge.
+__device__ __forceinline__ bool inv3(const double* m, double* o);
+
+// BlockSolver::solve, landmark part (block_solver.hpp:377-419) for point l: every lane of the point's
+// group forms D^-1 = (Hll + lambda I)^-1 (same values), each lane handles its edges'
+// W = Hpl D^-1 and Hpl D^-1 b_l.  H / bl are the point's Hll / b_l (identical in every lane).
+__device__ __forceinline__ void schur_point_terms(const BADev& b, int l, int sub, const double (&H)[9],
+                                                  const double (&bl)[3], double lam) {
+    double D[9], Di[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) D[i] = H[i];
+    D[0] += lam; D[4] += lam; D[8] += lam;
+    inv3(D, Di);
+    if (sub == 0)
+        for (int i = 0; i < 9; i++) b.Dinv[9 * l + i] = Di[i];
+    double db[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
+    for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
+        const int k = b.pt_slot[u];
+        if (b.hp[b.ek[b.act[k]]] < 0) continue;
+        const double* Hpl = b.J + (long long)k * 72 + 54;
+        double* W = b.W + (long long)k * 24;
+        for (int r = 0; r < 6; r++) {
+            for (int c = 0; c < 3; c++)
+                W[3 * r + c] = Hpl[3 * r] * Di[c] + Hpl[3 * r + 1] * Di[3 + c] + Hpl[3 * r + 2] * Di[6 + c];
+            W[18 + r] = Hpl[3 * r] * db[0] + Hpl[3 * r + 1] * db[1] + Hpl[3 * r + 2] * db[2];
+        }
+    }
+}
+
+// Per LM trial, point side.  On a linearising trial: errors + robust chi2 (computeActiveErrors /
+// activeRobustChi2), linearizeOplus and constructQuadraticForm of every active edge
+// (types_six_dof_expmap.cpp:103-139,188-234; base_binary_edge.hpp:54-120), Hll / b_l summed per
+// point, pose parts stored per edge.  Then, once lambda is known (every trial but the very first of
+// an optimize() call, whose lambda comes from computeLambdaInit), the point's Schur terms; a retry
+// trial (rho < 0) does only those, with the new lambda.
 __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
-    if (b.ctl->done || !b.ctl->need_lin) return;
+    if (b.ctl->done) return;
+    const bool lin = b.ctl->need_lin != 0;
+    const bool schur = !lin || b.ctl->it > 0;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = t / GRP, sub = t % GRP;
     const bool live = l < b.nl;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, chi = 0;
+    if (!lin) {
+        if (live) {
+#pragma unroll
+            for (int i = 0; i < 9; i++) H[i] = b.Hll[9 * l + i];
+#pragma unroll
+            for (int i = 0; i < 3; i++) g[i] = b.bl[3 * l + i];
+            schur_point_terms(b, l, sub, H, g, b.ctl->lambda);
+        }
+        return;
+    }
     if (live) {
         for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
             const int k = b.pt_slot[u];
@@ -206,32 +254,45 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
             double r0, r1;
             robustify(b, e, edge_chi2(b, e), r0, r1);
             const double w = r1 * b.info[e];
-            double om_r[3] = {0, 0, 0};
-            for (int r = 0; r < d; r++) om_r[r] = -b.info[e] * b.err[3 * e + r] * r1;
+            // row 2 of A / Bm and om_r[2] are zero for a mono edge, so the fixed 3-row sums add exact
+            // zeros to the reference's 2-row sums (same values) and every array stays in registers
+            double om_r[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) om_r[r] = r < d ? -b.info[e] * b.err[3 * e + r] * r1 : 0.0;
+#pragma unroll
             for (int i = 0; i < 3; i++) {
                 double s = 0;
-                for (int r = 0; r < d; r++) s += A[r][i] * om_r[r];
+#pragma unroll
+                for (int r = 0; r < 3; r++) s += A[r][i] * om_r[r];
                 g[i] += s;
+#pragma unroll
                 for (int j = 0; j < 3; j++) {
                     double h = 0;
-                    for (int r = 0; r < d; r++) h += A[r][i] * w * A[r][j];
+#pragma unroll
+                    for (int r = 0; r < 3; r++) h += A[r][i] * w * A[r][j];
                     H[3 * i + j] += h;
                 }
             }
             if (b.hp[pi] >= 0) {
                 double* J = b.J + (long long)k * 72;
+#pragma unroll
                 for (int i = 0; i < 6; i++) {
                     double s = 0;
-                    for (int r = 0; r < d; r++) s += Bm[r][i] * om_r[r];
+#pragma unroll
+                    for (int r = 0; r < 3; r++) s += Bm[r][i] * om_r[r];
                     J[48 + i] = s;
+#pragma unroll
                     for (int j = 0; j < 6; j++) {
                         double h = 0;
-                        for (int r = 0; r < d; r++) h += Bm[r][i] * w * Bm[r][j];
+#pragma unroll
+                        for (int r = 0; r < 3; r++) h += Bm[r][i] * w * Bm[r][j];
                         J[12 + 6 * i + j] = h;
                     }
+#pragma unroll
                     for (int j = 0; j < 3; j++) {
                         double h = 0;
-                        for (int r = 0; r < d; r++) h += Bm[r][i] * w * A[r][j];
+#pragma unroll
+                        for (int r = 0; r < 3; r++) h += Bm[r][i] * w * A[r][j];
                         J[54 + 3 * i + j] = h;
                     }
                 }
@@ -248,6 +309,8 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
         for (int i = 0; i < 3; i++) b.bl[3 * l + i] = g[i];
         b.rchi[l] = chi;
     }
+    // the lane's own J writes above are visible to its own reads in schur_point_terms
+    if (live && schur) schur_point_terms(b, l, sub, H, g, b.ctl->lambda);
 }
 
 // Deterministic single-workgroup sum (fixed strided order + fixed tree).
@@ -268,18 +331,23 @@ __device__ double block_sum_1024(const double* v, int n, double* sh) {
 // One workgroup (1008 threads) per free pose: 42 sums (Hpp 36 + b 6), 24 partial groups with
 // four interleaved accumulators each, combined in a fixed order.  Block np: chi2 total.
 constexpr int PA_G = 24;
-__global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b, int set_ini) {
+__device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh);
+__device__ __forceinline__ void chi_total(const BADev& b, double* sh) {
+    const double c = block_sum_1024(b.rchi, b.nl, sh);
+    if (threadIdx.x == 0) {
+        b.ctl->cur = c;
+        b.ctl->ini = c;
+    }
+}
+// The first trial of an optimize() call (computeLambdaInit needs Hpp before the Schur step);
+// later linearising trials accumulate inside ba_schur_block_kernel.
+__global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b) {
     if (b.ctl->done || !b.ctl->need_lin) return;
     __shared__ double sh[1024];
-    const int i = blockIdx.x;
-    if (i == b.np) {
-        const double c = block_sum_1024(b.rchi, b.nl, sh);
-        if (threadIdx.x == 0) {
-            b.ctl->cur = c;
-            if (set_ini) b.ctl->ini = c;
-        }
-        return;
-    }
+    if ((int)blockIdx.x == b.np) chi_total(b, sh);
+    else pose_accum(b, blockIdx.x, sh);
+}
+__device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh) {
     const int g = threadIdx.x / 42, c = threadIdx.x % 42;
     const int beg = b.ps_beg[i], end = b.ps_beg[i + 1];
     if (g < PA_G) {
@@ -301,6 +369,7 @@ __global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b, int set_in
         if (threadIdx.x < 36) b.Hpp[36 * i + threadIdx.x] = s;
         else b.bp[6 * i + threadIdx.x - 36] = s;
     }
+    __syncthreads();   // sh reused by the caller; Hpp / bp read back by the same workgroup
 }
 
 // computeLambdaInit (levenberg.cpp:166-180): tau * max |diag H| over active vertices.
@@ -334,43 +403,37 @@ __device__ __forceinline__ bool inv3(const double* m, double* o) {
     return true;
 }
 
-// BlockSolver::solve, landmark part (block_solver.hpp:377-419): every lane of a point's group
-// forms D^-1 (same values), each lane handles its edges' W = Hpl D^-1 and Hpl D^-1 b_l.
+// The first trial of an optimize() call: the Schur point terms after computeLambdaInit.
 __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
     BA_RETURN_IF_DONE(b);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = t / GRP, sub = t % GRP;
     if (l >= b.nl) return;
-    const double lam = b.ctl->lambda;
-    double D[9], Di[9];
-    for (int i = 0; i < 9; i++) D[i] = b.Hll[9 * l + i];
-    D[0] += lam; D[4] += lam; D[8] += lam;
-    inv3(D, Di);
-    if (sub == 0)
-        for (int i = 0; i < 9; i++) b.Dinv[9 * l + i] = Di[i];
-    double db[3];
-    for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * b.bl[3 * l] + Di[3 * i + 1] * b.bl[3 * l + 1] + Di[3 * i + 2] * b.bl[3 * l + 2];
-    for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
-        const int k = b.pt_slot[u];
-        if (b.hp[b.ek[b.act[k]]] < 0) continue;
-        const double* Hpl = b.J + (long long)k * 72 + 54;
-        double* W = b.W + (long long)k * 24;
-        for (int r = 0; r < 6; r++) {
-            for (int c = 0; c < 3; c++)
-                W[3 * r + c] = Hpl[3 * r] * Di[c] + Hpl[3 * r + 1] * Di[3 + c] + Hpl[3 * r + 2] * Di[6 + c];
-            W[18 + r] = Hpl[3 * r] * db[0] + Hpl[3 * r + 1] * db[1] + Hpl[3 * r + 2] * db[2];
-        }
-    }
+    double H[9], g[3];
+#pragma unroll
+    for (int i = 0; i < 9; i++) H[i] = b.Hll[9 * l + i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) g[i] = b.bl[3 * l + i];
+    schur_point_terms(b, l, sub, H, g, b.ctl->lambda);
 }
 
 // Reduced camera system block (i1, i2): 36 entries x 28 partial groups (two accumulators each),
 // fixed-order combine.  Diagonal blocks also form b_schur = b_p - sum Hpl D^-1 b_l.
+// With `accum` (every step but an optimize() call's first), a linearising trial also forms here what
+// ba_pose_accum_kernel would: each diagonal block's workgroup the Hpp / b_p sums of its pose first,
+// workgroup nblk the chi2 total.
 constexpr int SB_G = 28;
-__global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D) {
+__global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, int accum) {
     BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
     const int blk = blockIdx.x;
+    const bool acc = accum && b.ctl->need_lin;
+    if (blk == b.nblk) {
+        if (acc) chi_total(b, sh);
+        return;
+    }
     const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
+    if (acc && i1 == i2) pose_accum(b, i1, sh);
     const int g = threadIdx.x / 36, c = threadIdx.x % 36;
     const int r = c / 6, cc = c % 6;
     if (g < SB_G) {
@@ -422,7 +485,6 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D) {
     }
 }
 
-__device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const long long u = __double_as_longlong(v);
@@ -430,22 +492,6 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     const int hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-template <int J>
-__device__ __forceinline__ double row_bcast_t(double v);
-// j must fold to a constant after unrolling (it does inside the fully unrolled loops below)
-__device__ __forceinline__ double row_bcast_d(double v, int j) {
-    switch (j) {
-        case 0: return row_bcast_t<0>(v);   case 1: return row_bcast_t<1>(v);
-        case 2: return row_bcast_t<2>(v);   case 3: return row_bcast_t<3>(v);
-        case 4: return row_bcast_t<4>(v);   case 5: return row_bcast_t<5>(v);
-        case 6: return row_bcast_t<6>(v);   case 7: return row_bcast_t<7>(v);
-        case 8: return row_bcast_t<8>(v);   case 9: return row_bcast_t<9>(v);
-        case 10: return row_bcast_t<10>(v); case 11: return row_bcast_t<11>(v);
-        case 12: return row_bcast_t<12>(v); case 13: return row_bcast_t<13>(v);
-        case 14: return row_bcast_t<14>(v); default: return row_bcast_t<15>(v);
-    }
-}
-
 // Reduced camera system solve + pose update: right-looking blocked LDL^T of the (6P)^2 system in
 // LDS, padded with identity to Dp = 16*ceil(D/16) so every block is a full 16 columns (the padded
 // unknowns solve to 0).  Row stride Dp+1 (odd) keeps column walks bank-conflict free.  The forward
@@ -465,19 +511,18 @@ __device__ unsigned long long g_ba_stamps[64];
     do {                                                                                         \
         if (threadIdx.x == 0 && (k) < 64) g_ba_stamps[(k)] = __builtin_amdgcn_s_memtime();       \
     } while (0)
+#define BA_STAMPW(k)                                                                             \
+    do {                                                                                         \
+        if ((threadIdx.x & 63) == 0 && (k) < 64) g_ba_stamps[(k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define BA_STAMP(k) do {} while (0)
+#define BA_STAMPW(k) do {} while (0)
 #endif
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 typedef double d4 __attribute__((ext_vector_type(4)));
-
-// Value of lane J of each 16-lane row (DPP row_newbcast), for a double.
-template <int J>
-__device__ __forceinline__ double row_bcast_t(double v) {   // one v_mov_b64_dpp row_newbcast:J
-    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, false);
-}
 
 __host__ __device__ constexpr int solve_dp(int D) { return (D + SB - 1) / SB * SB; }
 __host__ __device__ constexpr size_t solve_lds_doubles(int D) {
@@ -523,80 +568,107 @@ __device__ __forceinline__ void trailing_update(double* A, const double* dinv, i
         for (int c = 0; c <= a; c++) A[(R0 + ty + SB * a) * ld + R0 + tx + SB * c] -= acc[a][c];
 }
 
-// (1) of the solve, split over two wavefronts that run concurrently:
-//   solve_diag_factor (wavefront 0): LDL^T of diagonal block J0 in registers (lane i owns row i, pivot
-//     rows broadcast with DPP row_newbcast; every 16-lane row holds the same copy) and the forward
-//     substitution z_J.  After pivot step m it stores column m of L and raises flag[0] = m + 1.
-//   solve_diag_inverse (wavefront 1): Linv_JJ = L_JJ^-1 column by column (lane c), right-looking, each
-//     step m as soon as column m of L is out; then v_J = Linv^T D^-1 z_J for the panel's rhs update.
-//     Linv[j][k] is kept at (k, j), the block's unused upper triangle.
-__device__ __forceinline__ int lds_flag_read(const int* f) { return __atomic_load_n(f, __ATOMIC_RELAXED); }
-
-__device__ __forceinline__ bool solve_diag_factor(double* A, double* y, double* dinv, int ld, int J0, int lane,
-                                                  int* flag, int nreal) {
-    const int i = lane & (SB - 1);
-    double r[SB];
-#pragma unroll
-    for (int k = 0; k < SB; k++) r[k] = A[(J0 + max(i, k)) * ld + J0 + min(i, k)];
-    double yi = y[J0 + i];
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < SB; j++) {
-        if (j < nreal) {   // past nreal: identity padding, nothing left to eliminate (uniform)
-            const double dj = row_bcast_d(r[j], j);
-            ok = ok && dj != 0 && isfinite(dj);
-            const double l = i > j ? r[j] * rcp_d(dj) : 0.0;
-            if (lane < SB && i > j) A[(J0 + i) * ld + J0 + j] = l;   // column j of L
-            const double yj = row_bcast_d(yi, j);
-#pragma unroll
-            for (int k = j + 1; k < SB; k++) r[k] = fma(-l, row_bcast_d(r[k], j), r[k]);
-            yi = fma(-l, yj, yi);
-            r[j] = i > j ? l : r[j];
-        }
-        if (j < SB - 1) {   // a wavefront's LDS operations execute in order: no wait needed here
-            asm volatile("" ::: "memory");
-            if (lane == 0) __atomic_store_n(flag, j + 1, __ATOMIC_RELAXED);
-        }
+// v_fmac_f64 with src0 = lane J's value of each 16-lane row (DPP row_newbcast): r += bcast_J(r) * nl,
+// and the plain broadcast.  The compiler's hazard recognizer does not look inside inline asm, so each
+// statement carries the 2 wait states a DPP read needs after a VALU write of its source (s_nop 1);
+// the code that uses them has no EXEC writes (no divergent branches), whose DPP hazard is 5 states.
+// The statements are not volatile, so the scheduler may interleave independent ones.
+template <int J>
+__device__ __forceinline__ void fmac_bcast_t(double& r, double nl) {
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(r) : "v"(nl), "n"(J));
+}
+template <int J>
+__device__ __forceinline__ double bcast_nop_t(double v) {
+    double o;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(o) : "v"(v), "n"(J));
+    return o;
+}
+// j must fold to a constant after unrolling
+__device__ __forceinline__ void fmac_bcast(double& r, double nl, int j) {
+    switch (j) {
+        case 0: fmac_bcast_t<0>(r, nl); break;
+        case 1: fmac_bcast_t<1>(r, nl); break;
+        case 2: fmac_bcast_t<2>(r, nl); break;
+        case 3: fmac_bcast_t<3>(r, nl); break;
+        case 4: fmac_bcast_t<4>(r, nl); break;
+        case 5: fmac_bcast_t<5>(r, nl); break;
+        case 6: fmac_bcast_t<6>(r, nl); break;
+        case 7: fmac_bcast_t<7>(r, nl); break;
+        case 8: fmac_bcast_t<8>(r, nl); break;
+        case 9: fmac_bcast_t<9>(r, nl); break;
+        case 10: fmac_bcast_t<10>(r, nl); break;
+        case 11: fmac_bcast_t<11>(r, nl); break;
+        case 12: fmac_bcast_t<12>(r, nl); break;
+        case 13: fmac_bcast_t<13>(r, nl); break;
+        case 14: fmac_bcast_t<14>(r, nl); break;
+        default: fmac_bcast_t<15>(r, nl); break;
     }
-    double di = r[0];
-#pragma unroll
-    for (int k = 1; k < SB; k++) di = k == i ? r[k] : di;
-    if (lane < SB) {
-        dinv[J0 + i] = rcp_d(di);
-        y[J0 + i] = yi;
+}
+__device__ __forceinline__ double bcast_nop(double v, int j) {
+    switch (j) {
+        case 0: return bcast_nop_t<0>(v);
+        case 1: return bcast_nop_t<1>(v);
+        case 2: return bcast_nop_t<2>(v);
+        case 3: return bcast_nop_t<3>(v);
+        case 4: return bcast_nop_t<4>(v);
+        case 5: return bcast_nop_t<5>(v);
+        case 6: return bcast_nop_t<6>(v);
+        case 7: return bcast_nop_t<7>(v);
+        case 8: return bcast_nop_t<8>(v);
+        case 9: return bcast_nop_t<9>(v);
+        case 10: return bcast_nop_t<10>(v);
+        case 11: return bcast_nop_t<11>(v);
+        case 12: return bcast_nop_t<12>(v);
+        case 13: return bcast_nop_t<13>(v);
+        case 14: return bcast_nop_t<14>(v);
+        default: return bcast_nop_t<15>(v);
     }
-    wave_lds_sync();
-    if (lane == 0) __atomic_store_n(flag, SB, __ATOMIC_RELAXED);   // dinv, z_J out as well
-    return ok;
 }
 
-__device__ __forceinline__ void solve_diag_inverse(double* A, const double* y, const double* dinv, double* vz,
-                                                   int ld, int J0, int lane, const int* flag, int nreal) {
-    const int c = lane & (SB - 1);
-    double x[SB];
+// Diagonal block J0 of the blocked LDL^T on ONE wavefront, in registers: lane i (of every 16-lane
+// row; the four rows hold the same copy) owns row i of the block (r), of Linv = L_JJ^-1 (x) and the
+// rhs entry y_i.  Pivot j: d_j and 1/d_j by a DPP broadcast + v_rcp_f64 and two Newton steps,
+// nl_i = -L_ij (rows below the pivot, else 0), then fused broadcast-FMAs: the trailing columns
+// r_k += nl * r_j[k], the forward substitution y_i += nl * z_j and the inverse rows
+// x_i[c] += nl * x_j[c] (c <= j: row j of Linv is final after pivot j-1).  The next pivot's column is
+// updated first, so its broadcast and reciprocal chain interleave with the rest of the step
+// (ordered volatile asm from tools/gen_ba_diag.py: the in-order issue then hides the chain).
+// Outputs: dinv_J, z_J (in y), Linv in the block's upper triangle (Linv[i][c] at (c, i), c < i) and
+// vz_J = Linv^T D^-1 z_J; the lower triangle is not needed by the later steps.
+__device__ __forceinline__ bool solve_diag_block(double* A, double* y, double* dinv, double* vz, int ld, int J0,
+                                                 int lane, int nreal) {
+    const int i = lane & (SB - 1);
+    double r[SB], x[SB];
 #pragma unroll
-    for (int m = 0; m < SB; m++) x[m] = 0;
+    for (int k = 0; k < SB; k++) r[k] = A[(J0 + max(i, k)) * ld + J0 + min(i, k)];
 #pragma unroll
-    for (int m = 0; m < SB - 1; m++) {
-        const double xm = m < c ? 0.0 : (m == c ? 1.0 : -x[m]);
-        x[m] = xm;
-        if (m < nreal) {   // padded columns of L are zero
-            while (lds_flag_read(flag) < m + 1) __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (int j = m + 1; j < SB; j++) x[j] = fma(A[(J0 + j) * ld + J0 + m], xm, x[j]);
-        }
-    }
-    x[SB - 1] = (SB - 1) < c ? 0.0 : ((SB - 1) == c ? 1.0 : -x[SB - 1]);
-    while (lds_flag_read(flag) < SB) __builtin_amdgcn_s_sleep(1);
-    double v = 0;   // v_c = sum_{j>=c} Linv[j][c] dinv_j z_j
-#pragma unroll
-    for (int j = 0; j < SB; j++) v = fma(x[j], dinv[J0 + j] * y[J0 + j], v);
+    for (int c = 0; c < SB; c++) x[c] = c == i ? 1.0 : 0.0;
+    double yi = y[J0 + i];
+    double rci = 1.0;   // 1/d_i (identity padding rows: d = 1)
+    bool ok = true;
+    double dj = bcast_nop(r[0], 0);
+    double rc = rcp_d(dj);
+    // 16 pivot steps, unrolled with the next pivot's broadcast + reciprocal interleaved into the
+    // current step's broadcast-FMAs (tools/gen_ba_diag.py)
+#include "orbba_diag.inc"
     if (lane < SB) {
+        dinv[J0 + i] = rci;
+        y[J0 + i] = yi;
 #pragma unroll
-        for (int j = 1; j < SB; j++)
-            if (j > c) A[(J0 + c) * ld + J0 + j] = x[j];
-        vz[J0 + c] = v;
+        for (int c = 0; c < SB - 1; c++)
+            if (c < i) A[(J0 + c) * ld + J0 + i] = x[c];
     }
+    wave_lds_sync();
+    // v_c = sum_{j >= c} Linv[j][c] dinv_j z_j
+    double v = dinv[J0 + i] * y[J0 + i];
+#pragma unroll
+    for (int j = 1; j < SB; j++) {
+        const double lv = A[(J0 + min(i, j)) * ld + J0 + j];   // Linv[j][i] for j > i
+        v = fma(j > i ? lv : 0.0, dinv[J0 + j] * y[J0 + j], v);
+    }
+    if (lane < SB) vz[J0 + i] = v;
+    wave_lds_sync();
+    return ok;
 }
 
 // One 16x16 tile of the trailing update: A[i0.., k0..] -= U_I D_J^-1 U_K^T (v_mfma_f64_16x16x4).
@@ -645,7 +717,6 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     double* dinv = y + Dp;
     double* vz = dinv + Dp;
     __shared__ int s_ok;
-    __shared__ int s_flag;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int col = lane & 15, kq = lane >> 4;
     BA_STAMP(41);
@@ -657,49 +728,45 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
         for (int j = 0; j < 3; j++) t_pre[j] = b.t[3 * id + j];
         for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
     }
-    // S -> LDS (padded with identity): wavefront w takes rows w, w+4, ...; 8 rows (16 loads per lane)
-    // in flight per batch
-    for (int r0 = wv; r0 < Dp; r0 += 32) {
-        double v[8][2];
+    // S -> LDS: D = 6 np is even, so every row of S starts 16-byte aligned; lane c of a wavefront
+    // takes the 16-byte piece c of its rows (w, w+4, ...), 16 rows of loads in flight per batch
+    {
+        const int npc = D / 2;
+        const double2* S2 = reinterpret_cast<const double2*>(b.S);
+        for (int r0 = wv; r0 < D; r0 += 64) {
+            double2 v[16];
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int r = r0 + 4 * q;
+            for (int q = 0; q < 16; q++) {
+                const int r = min(r0 + 4 * q, D - 1);
+                v[q] = lane < npc ? S2[r * npc + lane] : make_double2(0.0, 0.0);
+            }
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int c = lane + 64 * h;
-                const double sv = b.S[min(r, D - 1) * D + min(c, D - 1)];   // unconditional: no branch
-                v[q][h] = (r < D && c < D) ? sv : (r == c ? 1.0 : 0.0);
+            for (int q = 0; q < 16; q++) {
+                const int r = r0 + 4 * q;
+                if (r < D && lane < npc) {
+                    A[r * ld + 2 * lane] = v[q].x;
+                    A[r * ld + 2 * lane + 1] = v[q].y;
+                }
             }
         }
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int r = r0 + 4 * q;
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int c = lane + 64 * h;
-                if (r < Dp && c < Dp) A[r * ld + c] = v[q][h];
-            }
+        // identity padding: columns D..Dp-1 of the real rows, then the padded rows
+        for (int u = tid; u < D * (Dp - D); u += blockDim.x) A[(u / (Dp - D)) * ld + D + u % (Dp - D)] = 0.0;
+        for (int u = tid; u < (Dp - D) * Dp; u += blockDim.x) {
+            const int r = D + u / Dp, c = u % Dp;
+            A[r * ld + c] = r == c ? 1.0 : 0.0;
         }
     }
     for (int i = tid; i < Dp; i += blockDim.x) y[i] = i < D ? b.bs[i] : 0.0;
-    if (tid == 0) {
-        s_ok = 1;
-        s_flag = 0;
-    }
+    if (tid == 0) s_ok = 1;
     __syncthreads();
     BA_STAMP(0);
-    if (wv == 0) {
-        if (!solve_diag_factor(A, y, dinv, ld, 0, lane, &s_flag, D) && lane == 0) s_ok = 0;
-    } else if (wv == 1) {
-        solve_diag_inverse(A, y, dinv, vz, ld, 0, lane, &s_flag, D);
-    }
+    if (wv == 0 && !solve_diag_block(A, y, dinv, vz, ld, 0, lane, D) && lane == 0) s_ok = 0;
     __syncthreads();
     for (int J0 = 0; J0 < Dp && s_ok; J0 += SB) {
         const int R0 = J0 + SB;
         const int nbk = (Dp - R0) / SB;
         BA_STAMP(1 + 3 * (J0 / SB));
         if (nbk == 0) break;
-        if (tid == 0) s_flag = 0;   // read by wavefront 1 only after the panel's barrier
         // (2) panel U_I = A_IJ Linv^T per 16-row tile (MFMA); rhs y_i -= A_iJ v with v = Linv^T D^-1 z_J
         if (wv < nbk) {
             double binv[4], bvz[4];
@@ -742,49 +809,50 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
             if (wv == 0) {
                 solve_trailing_tile(A, ld, J0, R0, R0, col, kq, dk);
                 wave_lds_sync();
-                if (!solve_diag_factor(A, y, dinv, ld, R0, lane, &s_flag, D - R0) && lane == 0) s_ok = 0;
-            } else if (wv == 1) {
-                solve_diag_inverse(A, y, dinv, vz, ld, R0, lane, &s_flag, D - R0);
+                if (J0 == 32) BA_STAMPW(44);
+                if (!solve_diag_block(A, y, dinv, vz, ld, R0, lane, D - R0) && lane == 0) s_ok = 0;
+                if (J0 == 32) BA_STAMPW(45);
             } else {
                 const int ntile = nbk * (nbk + 1) / 2;
-                for (int t = wv - 1; t < ntile; t += 2) {   // tile 0 = (J+1, J+1) belongs to wavefront 0
+                for (int t = wv; t < ntile; t += 3) {   // tile 0 = (J+1, J+1) belongs to wavefront 0
                     int I = 0;
                     while ((I + 1) * (I + 2) / 2 <= t) I++;
                     const int K = t - I * (I + 1) / 2;
                     solve_trailing_tile(A, ld, J0, R0 + SB * I, R0 + SB * K, col, kq, dk);
                 }
+                if (J0 == 32) BA_STAMPW(45 + wv);
             }
         }
         __syncthreads();
         BA_STAMP(3 + 3 * (J0 / SB));
     }
     const int ok = s_ok;
-    if (ok && wv == 0) {
-        for (int i = lane; i < Dp; i += 64) y[i] *= dinv[i];   // t = D^-1 z
-        wave_lds_sync();
+    if (ok) {   // back substitution, block by block from the last: x_J on wavefront 0, then every
+                // earlier column's update (one thread per column) on the whole workgroup
+        for (int i = tid; i < Dp; i += blockDim.x) y[i] *= dinv[i];   // t = D^-1 z
+        __syncthreads();
         for (int J0 = Dp - SB; J0 >= 0; J0 -= SB) {
-            // x_J = Linv_JJ^T t_J: x_c = t_c + sum_{j>c} Linv[j][c] t_j (four partial sums)
-            double xp[4] = {y[J0 + col], 0, 0, 0};
+            if (wv == 0) {
+                // x_J = Linv_JJ^T t_J: x_c = t_c + sum_{j>c} Linv[j][c] t_j (four partial sums)
+                double xp[4] = {y[J0 + col], 0, 0, 0};
 #pragma unroll
-            for (int j = 1; j < SB; j++) {
-                const double lv = A[(J0 + min(col, j)) * ld + J0 + j];   // Linv[j][col] for j > col
-                xp[j & 3] = fma(j > col ? lv : 0.0, y[J0 + j], xp[j & 3]);   // select, not a branch
+                for (int j = 1; j < SB; j++) {
+                    const double lv = A[(J0 + min(col, j)) * ld + J0 + j];   // Linv[j][col] for j > col
+                    xp[j & 3] = fma(j > col ? lv : 0.0, y[J0 + j], xp[j & 3]);   // select, not a branch
+                }
+                const double xc = (xp[0] + xp[1]) + (xp[2] + xp[3]);
+                wave_lds_sync();
+                if (lane < SB) y[J0 + col] = xc;
             }
-            const double xc = (xp[0] + xp[1]) + (xp[2] + xp[3]);
-            wave_lds_sync();
-            if (lane < SB) y[J0 + col] = xc;
-            wave_lds_sync();
+            __syncthreads();
             // t_c -= sum_{i in J} L_ic x_i, L_ic = U_ic dinv_c, for all earlier columns c < J0
-            double xj[SB];
-#pragma unroll
-            for (int k = 0; k < SB; k++) xj[k] = y[J0 + k];
-            for (int c = lane; c < J0; c += 64) {
+            for (int c = tid; c < J0; c += blockDim.x) {
                 double sp[4] = {0, 0, 0, 0};
 #pragma unroll
-                for (int k = 0; k < SB; k++) sp[k & 3] = fma(A[(J0 + k) * ld + c], xj[k], sp[k & 3]);
+                for (int k = 0; k < SB; k++) sp[k & 3] = fma(A[(J0 + k) * ld + c], y[J0 + k], sp[k & 3]);
                 y[c] = fma(-((sp[0] + sp[1]) + (sp[2] + sp[3])), dinv[c], y[c]);
             }
-            wave_lds_sync();
+            __syncthreads();
         }
     }
     __syncthreads();
@@ -827,7 +895,7 @@ __global__ __launch_bounds__(1024) void ba_solve_global_kernel(BADev b, int D) {
     BA_RETURN_IF_DONE(b);
     extern __shared__ __attribute__((aligned(16))) double ysh[];   // y | dinv | vz, Dp each
     __shared__ double Ad[SB * (SB + 1)];
-    __shared__ int s_ok, s_flag;
+    __shared__ int s_ok;
     const int Dp = solve_dp(D), ld = Dp + 1;
     double* A = b.Sg;
     double* y = ysh;
@@ -847,14 +915,9 @@ __global__ __launch_bounds__(1024) void ba_solve_global_kernel(BADev b, int D) {
         const int nbk = (Dp - R0) / SB;
         // (1) diagonal block in LDS; Av addresses it with the global (J0, J0) indexing of the helpers
         if (tid < SB * SB) Ad[(tid >> 4) * (SB + 1) + (tid & 15)] = A[(long long)(J0 + (tid >> 4)) * ld + J0 + (tid & 15)];
-        if (tid == 0) s_flag = 0;
         __syncthreads();
         double* Av = Ad - ((long long)J0 * (SB + 1) + J0);
-        if (wv == 0) {
-            if (!solve_diag_factor(Av, y, dinv, SB + 1, J0, lane, &s_flag, D - J0) && lane == 0) s_ok = 0;
-        } else if (wv == 1) {
-            solve_diag_inverse(Av, y, dinv, vz, SB + 1, J0, lane, &s_flag, D - J0);
-        }
+        if (wv == 0 && !solve_diag_block(Av, y, dinv, vz, SB + 1, J0, lane, D - J0) && lane == 0) s_ok = 0;
         __syncthreads();
         if (!s_ok) break;
         if (tid < SB * SB) A[(long long)(J0 + (tid >> 4)) * ld + J0 + (tid & 15)] = Ad[(tid >> 4) * (SB + 1) + (tid & 15)];
@@ -958,9 +1021,25 @@ __global__ __launch_bounds__(1024) void ba_solve_global_kernel(BADev b, int D) {
     }
 }
 
+// A point-update workgroup's chi2 / scale partials: its 8 points (group leaders, lanes 0, 8, .., 56)
+// summed in order; ba_decide_kernel sums the workgroups' partials in a fixed order.
+__device__ __forceinline__ void ba_point_update_partials(double* wgpart, double chi, double part) {
+    double pc = 0, pp = 0;
+#pragma unroll
+    for (int g = 0; g < 64; g += GRP) {
+        pc += readlane_d(chi, g);
+        pp += readlane_d(part, g);
+    }
+    if (threadIdx.x == 0) {
+        wgpart[2 * blockIdx.x] = pc;
+        wgpart[2 * blockIdx.x + 1] = pp;
+    }
+}
+
 // Back-substitution xl = Dinv (bl - Hpl^T xp), push(), point +=, scale term, then the errors and
 // robust chi2 of the point's edges at the new estimate (computeActiveErrors after update()).
-__global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D) {
+// The workgroups' chi2 / scale partials go to wgpart (ba_decide_kernel sums them).
+__global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D, double* wgpart) {
     BA_RETURN_IF_DONE(b);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = t / GRP, sub = t % GRP;
@@ -979,111 +1058,77 @@ __global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D) {
             }
         }
     for (int c = 0; c < 3; c++) cl[c] = grp_sum(cl[c]);
-    if (!live) return;
-    const double lam = b.ctl->lambda;
-    double bl[3], xl[3];
-    for (int c = 0; c < 3; c++) bl[c] = b.bl[3 * l + c];
-    const double* Di = b.Dinv + 9 * l;
-    for (int c = 0; c < 3; c++) cl[c] = bl[c] - cl[c];
-    const int id = b.pt_id[l];
-    double Xn[3];
-    double part = 0;
-    for (int i = 0; i < 3; i++) {
-        xl[i] = Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1] + Di[3 * i + 2] * cl[2];
-        Xn[i] = b.X[3 * id + i] + xl[i];
-        part += xl[i] * (lam * xl[i] + bl[i]);
-    }
-    // every lane of the group read X before lane 0 overwrites it below (same wavefront, in order)
-    __builtin_amdgcn_wave_barrier();
-    if (sub == 0) {
+    double chi = 0, part = 0;   // every lane of a group ends with the same part
+    if (live) {
+        const double lam = b.ctl->lambda;
+        double bl[3], xl[3];
+        for (int c = 0; c < 3; c++) bl[c] = b.bl[3 * l + c];
+        const double* Di = b.Dinv + 9 * l;
+        for (int c = 0; c < 3; c++) cl[c] = bl[c] - cl[c];
+        const int id = b.pt_id[l];
+        double Xn[3];
         for (int i = 0; i < 3; i++) {
-            b.x[D + 3 * l + i] = xl[i];
-            b.X_sv[3 * id + i] = b.X[3 * id + i];
-            b.X[3 * id + i] = Xn[i];
+            xl[i] = Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1] + Di[3 * i + 2] * cl[2];
+            Xn[i] = b.X[3 * id + i] + xl[i];
+            part += xl[i] * (lam * xl[i] + bl[i]);
         }
-        b.part[l] = part;
-    }
-    double chi = 0;
-    for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
-        const int e = b.act[b.pt_slot[u]];
-        const int pi = b.ek[e];
-        double Xc[3];
-        se3_map(b.q + 4 * pi, b.t + 3 * pi, Xn, Xc);
-        chi += edge_error(b, e, Xc);
+        // every lane of the group read X before lane 0 overwrites it below (same wavefront, in order)
+        __builtin_amdgcn_wave_barrier();
+        if (sub == 0) {
+            for (int i = 0; i < 3; i++) {
+                b.x[D + 3 * l + i] = xl[i];
+                b.X_sv[3 * id + i] = b.X[3 * id + i];
+                b.X[3 * id + i] = Xn[i];
+            }
+            b.part[l] = part;
+        }
+        for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
+            const int e = b.act[b.pt_slot[u]];
+            const int pi = b.ek[e];
+            double Xc[3];
+            se3_map(b.q + 4 * pi, b.t + 3 * pi, Xn, Xc);
+            chi += edge_error(b, e, Xc);
+        }
     }
     // group partial (lanes of a group are contiguous; sum in fixed order via shuffles)
     chi += __shfl_xor(chi, 1, 64);
     chi += __shfl_xor(chi, 2, 64);
     chi += __shfl_xor(chi, 4, 64);
-    if (sub == 0) b.rchi[l] = chi;
+    if (live && sub == 0) b.rchi[l] = chi;
+    ba_point_update_partials(wgpart, chi, part);
 }
 
-// levenberg.cpp:120-147 — sums, accept / reject, lambda / nu update, pop() on reject.
-__global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b, BACtl* host_snap) {
+__device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double tmp_sum, double scale_sum);
+
+// The decide step after a trial: fixed-order sums of the point-update workgroups' partials (thread-
+// strided, then a fixed tree) + the pose scale terms of the solve, ba_decide_step on one thread, and
+// pop() (restore the pushed estimates) on a rejected step.
+__global__ __launch_bounds__(256) void ba_decide_kernel(BADev b, BACtl* host_snap, int seq, const double* wgpart,
+                                                        int G) {
     BA_RETURN_IF_DONE(b);
-    __shared__ double sh[1024];
+    __shared__ double sc[256], sp[256];
     __shared__ int s_acc;
-    const double tmp_sum = block_sum_1024(b.rchi, b.nl, sh);
-    const double scale_sum = block_sum_1024(b.part, b.nl + b.np, sh);
-    BACtl* c = b.ctl;
-    if (threadIdx.x == 0) {
-        c->tmp = tmp_sum;
-        c->scale = scale_sum;
-        double tmp = tmp_sum;
-        if (!c->ok2) tmp = 1.7976931348623157e308;   // std::numeric_limits<double>::max()
-        double rho = c->cur - tmp;
-        rho /= (scale_sum + 1e-3);
-        c->rho = rho;
-        if (rho > 0 && isfinite(tmp)) {
-            double alpha = 1. - pow((2 * rho - 1), 3);
-            alpha = fmin(alpha, 2. / 3.);
-            c->lambda *= fmax(1. / 3., alpha);
-            c->ni = 2;
-            c->cur = tmp;
-            c->accepted = 1;
-        } else {
-            c->lambda *= c->ni;
-            c->ni *= 2;
-            c->accepted = 0;
-        }
-        s_acc = c->accepted;
-        // trial / iteration bookkeeping (host loop of levenberg solve + SparseOptimizer::optimize)
-        c->q += 1;
-        c->trials += 1;
-        // g2o polls terminate() after every trial (levenberg.cpp:149) and before every iteration
-        // (sparse_optimizer.cpp:376): a raised flag ends the loop once this trial is done
-        const bool stop = (b.stop && __atomic_load_n(b.stop, __ATOMIC_RELAXED) != 0) ||
-                          (b.stop_after >= 0 && c->trials >= b.stop_after);
-        if (rho < 0 && c->q < 10 && !stop) {
-            c->need_lin = 0;   // retry with the new lambda
-        } else {
-            c->iters_done += 1;
-            c->chi_out = c->cur;
-            bool term = c->q == 10 || rho == 0;
-            if (!term) {
-                if ((c->ini - c->cur) * 1e3 < c->ini) c->nbad++;
-                else c->nbad = 0;
-                term = c->nbad >= 3;
-            }
-            c->it += 1;
-            if (c->it >= c->iters_max) term = true;
-            if (stop) {
-                term = true;
-                c->stopped = 1;
-            }
-            if (term) c->done = 1;
-            else {
-                c->need_lin = 1;
-                c->q = 0;
-            }
-        }
-        // control snapshot straight into pinned host memory (no copy on the stream)
-        *host_snap = *c;
-        __threadfence_system();
+    const int tid = threadIdx.x;
+    double c0 = 0, p0 = 0;
+    for (int w = tid; w < G; w += 256) {
+        c0 += wgpart[2 * w];
+        p0 += wgpart[2 * w + 1];
     }
+    for (int i = tid; i < b.np; i += 256) p0 += b.part[b.nl + i];
+    sc[tid] = c0;
+    sp[tid] = p0;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            sc[tid] += sc[tid + o];
+            sp[tid] += sp[tid + o];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) s_acc = ba_decide_step(b, host_snap, seq, sc[0], sp[0]);
     __syncthreads();
     if (s_acc) return;
-    for (int t = threadIdx.x; t < b.nl + b.np; t += blockDim.x) {
+    for (int t = tid; t < b.nl + b.np; t += 256) {   // pop(): restore the pushed estimates
         if (t < b.nl) {
             const int id = b.pt_id[t];
             for (int i = 0; i < 3; i++) b.X[3 * id + i] = b.X_sv[3 * id + i];
@@ -1093,6 +1138,70 @@ __global__ __launch_bounds__(1024) void ba_decide_kernel(BADev b, BACtl* host_sn
             for (int j = 0; j < 3; j++) b.t[3 * id + j] = b.t_sv[3 * id + j];
         }
     }
+}
+
+// levenberg.cpp:120-147 — accept / reject, lambda / nu update, then the trial / iteration bookkeeping
+// of g2o's solve() / optimize(); one thread.  Returns whether the step was accepted.
+__device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double tmp_sum, double scale_sum) {
+    BACtl* c = b.ctl;
+    c->tmp = tmp_sum;
+    c->scale = scale_sum;
+    double tmp = tmp_sum;
+    if (!c->ok2) tmp = 1.7976931348623157e308;   // std::numeric_limits<double>::max()
+    double rho = c->cur - tmp;
+    rho /= (scale_sum + 1e-3);
+    c->rho = rho;
+    if (rho > 0 && isfinite(tmp)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        c->lambda *= fmax(1. / 3., alpha);
+        c->ni = 2;
+        c->cur = tmp;
+        c->accepted = 1;
+    } else {
+        c->lambda *= c->ni;
+        c->ni *= 2;
+        c->accepted = 0;
+    }
+    // trial / iteration bookkeeping (host loop of levenberg solve + SparseOptimizer::optimize)
+    c->q += 1;
+    c->trials += 1;
+    // g2o polls terminate() after every trial (levenberg.cpp:149) and before every iteration
+    // (sparse_optimizer.cpp:376): a raised flag ends the loop once this trial is done
+    const bool stop = (b.stop && __atomic_load_n(b.stop, __ATOMIC_RELAXED) != 0) ||
+                      (b.stop_after >= 0 && c->trials >= b.stop_after);
+    if (rho < 0 && c->q < 10 && !stop) {
+        c->need_lin = 0;   // retry with the new lambda
+    } else {
+        c->iters_done += 1;
+        c->chi_out = c->cur;
+        bool term = c->q == 10 || rho == 0;
+        if (!term) {
+            if ((c->ini - c->cur) * 1e3 < c->ini) c->nbad++;
+            else c->nbad = 0;
+            term = c->nbad >= 3;
+        }
+        c->it += 1;
+        if (c->it >= c->iters_max) term = true;
+        if (stop) {
+            term = true;
+            c->stopped = 1;
+        }
+        if (term) c->done = 1;
+        else {
+            c->need_lin = 1;
+            c->q = 0;
+        }
+    }
+    // control snapshot straight into pinned host memory (no copy on the stream, no event): the
+    // body first, then the sequence id the host polls for, ordered by a system-scope fence
+    BACtl snap = *c;
+    snap.seq = -1;
+    *host_snap = snap;
+    __threadfence_system();
+    __atomic_store_n(&host_snap->seq, seq, __ATOMIC_RELAXED);
+    __threadfence_system();
+    return c->accepted != 0;
 }
 
 // final outlier classification (Optimizer.cc:644-670, :686-699) + chi2 out
@@ -1161,7 +1270,7 @@ struct BAContext {
     BACtl* h_ctl = nullptr;   // pinned
     BACtl* h_ring = nullptr;  // pinned, device-mapped control snapshots, one per step in flight
     BACtl* d_ring = nullptr;
-    hipEvent_t ring_ev[2] = {nullptr, nullptr};
+    int step_seq = 0;         // id of the last enqueued LM step (snapshot sequence)
     int32_t* h_stop = nullptr;   // pinned, device-mapped mirror of the caller's stop flag
     int32_t* d_stop = nullptr;
     PinnedBuf h_prob, h_struct, h_res;   // pinned staging images (one copy each way)
@@ -1171,8 +1280,6 @@ struct BAContext {
         if (device >= 0) (void)hipSetDevice(device);
         if (st) (void)hipStreamSynchronize(st);
         prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
-        for (hipEvent_t& e : ring_ev)
-            if (e) { (void)hipEventDestroy(e); e = nullptr; }
         if (st) { (void)hipStreamDestroy(st); st = nullptr; }
         if (h_ring) { (void)hipHostFree(h_ring); h_ring = nullptr; d_ring = nullptr; }
         if (h_stop) { (void)hipHostFree(h_stop); h_stop = nullptr; d_stop = nullptr; }
@@ -1182,8 +1289,6 @@ struct BAContext {
     ~BAContext() {
         if (h_stop) (void)hipHostFree(h_stop);
         if (h_ring) (void)hipHostFree(h_ring);
-        for (hipEvent_t e : ring_ev)
-            if (e) (void)hipEventDestroy(e);
         prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (st) (void)hipStreamDestroy(st);
@@ -1207,24 +1312,29 @@ size_t carve_size(size_t n) { return align_up(std::max<size_t>(n, 1) * sizeof(T)
 struct HostStructure {
     std::vector<int> act, hp, hl, pt_beg, pt_slot, pt_id, ps_beg, ps_slot, ps_id, blk_i1, blk_i2, blk_beg;
     std::vector<int2> blk_pair;
+    std::vector<int> blk_index, blk_fill, fs_beg, fs_slot, fs_hp;   // scratch (capacity kept across calls)
+    std::vector<uint8_t> pa, la;
     int np = 0, nl = 0;
 };
 
 // SparseOptimizer::initializeOptimization(level) (sparse_optimizer.cpp:206-264) and the
 // BlockSolver structure (block_solver.hpp:142-295): active edges / vertices, Hessian indices, and
-// the Schur fill pattern (pose pairs that share a point).
+// the Schur fill pattern (pose pairs that share a point).  Flat two-pass build (count, then fill)
+// into vectors that keep their capacity across calls: no allocation per point or per block.
+// Pair order inside a block: points ascending, then (slot a, slot c) in the point's slot order.
 void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
                      const int* ek, HostStructure& s) {
     const int E = (int)level.size();
-    std::vector<uint8_t> pa(P, 0), la(N, 0);
+    s.pa.assign(P, 0);
+    s.la.assign(N, 0);
     s.act.clear();
     for (int e = 0; e < E; e++)
-        if (level[e] == 0) { s.act.push_back(e); pa[ek[e]] = 1; la[ep[e]] = 1; }
+        if (level[e] == 0) { s.act.push_back(e); s.pa[ek[e]] = 1; s.la[ep[e]] = 1; }
     s.hp.assign(P, -1); s.hl.assign(N, -1);
     s.ps_id.clear(); s.pt_id.clear();
     s.np = 0; s.nl = 0;
-    for (int i = 0; i < P; i++) if (pa[i] && !fixed[i]) { s.hp[i] = s.np++; s.ps_id.push_back(i); }
-    for (int i = 0; i < N; i++) if (la[i]) { s.hl[i] = s.nl++; s.pt_id.push_back(i); }
+    for (int i = 0; i < P; i++) if (s.pa[i] && !fixed[i]) { s.hp[i] = s.np++; s.ps_id.push_back(i); }
+    for (int i = 0; i < N; i++) if (s.la[i]) { s.hl[i] = s.nl++; s.pt_id.push_back(i); }
     const int Ea = (int)s.act.size();
     s.pt_beg.assign(s.nl + 1, 0); s.ps_beg.assign(s.np + 1, 0);
     for (int k = 0; k < Ea; k++) {
@@ -1234,37 +1344,76 @@ void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint
     }
     for (int i = 0; i < s.nl; i++) s.pt_beg[i + 1] += s.pt_beg[i];
     for (int i = 0; i < s.np; i++) s.ps_beg[i + 1] += s.ps_beg[i];
-    s.pt_slot.assign(Ea, 0); s.ps_slot.assign(s.ps_beg[s.np], 0);
-    std::vector<int> fp(s.pt_beg.begin(), s.pt_beg.end() - 1), fq(s.ps_beg.begin(), s.ps_beg.end() - 1);
-    for (int k = 0; k < Ea; k++) {
-        const int e = s.act[k];
-        s.pt_slot[fp[s.hl[ep[e]]]++] = k;
-        if (s.hp[ek[e]] >= 0) s.ps_slot[fq[s.hp[ek[e]]]++] = k;
+    s.pt_slot.resize(Ea); s.ps_slot.resize(s.ps_beg[s.np]);
+    {
+        // fill cursors: blk_fill doubles as scratch here (nl + np entries)
+        s.blk_fill.assign(s.pt_beg.begin(), s.pt_beg.end() - 1);
+        s.blk_fill.insert(s.blk_fill.end(), s.ps_beg.begin(), s.ps_beg.end() - 1);
+        int* fp = s.blk_fill.data();
+        int* fq = fp + s.nl;
+        for (int k = 0; k < Ea; k++) {
+            const int e = s.act[k];
+            s.pt_slot[fp[s.hl[ep[e]]]++] = k;
+            if (s.hp[ek[e]] >= 0) s.ps_slot[fq[s.hp[ek[e]]]++] = k;
+        }
     }
-    // pose-pair blocks: (i1 <= i2), pairs (slot with pose i1, slot with pose i2) per shared point
+    // pose-pair blocks (i1 <= i2): pass 1 counts the pairs per block, pass 2 fills them.  Per point,
+    // its slots whose pose is free (slot order) with their Hessian pose index, as one flat CSR.
     const int np = s.np;
-    std::vector<std::vector<int2>> pairs((size_t)np * np);
-    std::vector<int> blk_index((size_t)np * np, -1);
+    s.fs_beg.resize(s.nl + 1);
+    s.fs_slot.clear();
+    s.fs_hp.clear();
     for (int l = 0; l < s.nl; l++) {
-        std::vector<int> sl;
-        for (int u = s.pt_beg[l]; u < s.pt_beg[l + 1]; u++)
-            if (s.hp[ek[s.act[s.pt_slot[u]]]] >= 0) sl.push_back(s.pt_slot[u]);
-        for (int a : sl)
-            for (int c : sl) {
-                const int i1 = s.hp[ek[s.act[a]]], i2 = s.hp[ek[s.act[c]]];
-                if (i1 <= i2) pairs[(size_t)i1 * np + i2].push_back(make_int2(a, c));
-            }
+        s.fs_beg[l] = (int)s.fs_slot.size();
+        for (int u = s.pt_beg[l]; u < s.pt_beg[l + 1]; u++) {
+            const int k = s.pt_slot[u];
+            const int h = s.hp[ek[s.act[k]]];
+            if (h >= 0) { s.fs_slot.push_back(k); s.fs_hp.push_back(h); }
+        }
     }
-    s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0); s.blk_pair.clear();
+    s.fs_beg[s.nl] = (int)s.fs_slot.size();
+    s.blk_index.assign((size_t)np * np, 0);
+    {
+        const int* fh = s.fs_hp.data();
+        int* cnt = s.blk_index.data();
+        for (int l = 0; l < s.nl; l++) {
+            const int b0 = s.fs_beg[l], b1 = s.fs_beg[l + 1];
+            for (int a = b0; a < b1; a++) {
+                const int i1 = fh[a];
+                int* row = cnt + (size_t)i1 * np;
+                for (int c = b0; c < b1; c++) row[fh[c]] += i1 <= fh[c];
+            }
+        }
+    }
+    s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0);
+    int total = 0;
     for (int i1 = 0; i1 < np; i1++)
         for (int i2 = i1; i2 < np; i2++) {
-            const auto& v = pairs[(size_t)i1 * np + i2];
-            if (v.empty() && i1 != i2) continue;
+            int& cnt = s.blk_index[(size_t)i1 * np + i2];
+            if (cnt == 0 && i1 != i2) { cnt = -1; continue; }
             s.blk_i1.push_back(i1);
             s.blk_i2.push_back(i2);
-            s.blk_pair.insert(s.blk_pair.end(), v.begin(), v.end());
-            s.blk_beg.push_back((int)s.blk_pair.size());
+            const int beg = total;
+            total += cnt;
+            cnt = beg;   // now the block's fill cursor
+            s.blk_beg.push_back(total);
         }
+    s.blk_pair.resize(total);
+    {
+        const int* fh = s.fs_hp.data();
+        const int* fsl = s.fs_slot.data();
+        int* cur = s.blk_index.data();
+        int2* out = s.blk_pair.data();
+        for (int l = 0; l < s.nl; l++) {
+            const int b0 = s.fs_beg[l], b1 = s.fs_beg[l + 1];
+            for (int a = b0; a < b1; a++) {
+                const int i1 = fh[a];
+                int* row = cur + (size_t)i1 * np;
+                for (int c = b0; c < b1; c++)
+                    if (i1 <= fh[c]) out[row[fh[c]]++] = make_int2(fsl[a], fsl[c]);
+            }
+        }
+    }
 }
 
 }  // namespace
@@ -1275,9 +1424,17 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     const int P = pr->n_poses, N = pr->n_points, E = pr->n_edges;
     ORB_CHECK_ARG(P >= 0 && N >= 0 && E >= 0, "negative sizes");
     ORB_CHECK_ARG(res->pose_R && res->pose_t && res->points && res->edge_outlier, "null result buffers");
+    // host-side phase timing (ORBBA_DEBUG_TIMING=1: printed to stderr at the end of the call)
+    static const bool tdbg = getenv("ORBBA_DEBUG_TIMING") != nullptr;
+    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> marks;
+    auto mark = [&](const char* n) {
+        if (tdbg) marks.emplace_back(n, std::chrono::steady_clock::now());
+    };
+    mark("entry");
     for (int e = 0; e < E; e++)
         ORB_CHECK_ARG(pr->edge_point[e] >= 0 && pr->edge_point[e] < N && pr->edge_pose[e] >= 0 &&
                           pr->edge_pose[e] < P, "edge references a missing vertex");
+    mark("edge checks");
     BAContext& C = g_ba;
     if (C.device != device) {
         int ndev = 0;
@@ -1291,7 +1448,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         ORB_HIP_TRY(hipHostGetDevicePointer((void**)&C.d_ring, C.h_ring, 0));
         ORB_HIP_TRY(hipHostMalloc((void**)&C.h_stop, 64, hipHostMallocMapped));
         ORB_HIP_TRY(hipHostGetDevicePointer((void**)&C.d_stop, C.h_stop, 0));
-        for (hipEvent_t& e : C.ring_ev) ORB_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (int k = 0; k < 2; k++) C.h_ring[k].seq = -1;
         C.device = device;
     }
     ORB_HIP_TRY(hipSetDevice(device));
@@ -1301,6 +1458,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     if (const char* e = getenv("ORBBA_DEBUG_STOP_AFTER_TRIALS")) stop_after = atoi(e);
     *C.h_stop = stopped() ? 1 : 0;
 
+    mark("context");
     // initial estimates: SE3Quat(R, t) -> Quaterniond(R) normalised (Optimizer.cc:145-150)
     std::vector<double> q0(4 * (size_t)P);
     for (int i = 0; i < P; i++) {
@@ -1396,12 +1554,14 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     res->iterations[0] = res->iterations[1] = 0;
     res->chi2[0] = res->chi2[1] = 0;
 
+    mark("staging + upload enqueued");
     std::vector<uint8_t> level(E, 0);
-    HostStructure hs;
+    thread_local HostStructure hs;   // capacity kept across calls
     bool hook_stopped = false;   // the device ended a loop on the stop flag (or the test hook)
     // ------------------------------------------------------------------ one optimize(iters)
     auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
         build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs);
+        mark("build_structure");
         const int Ea = (int)hs.act.size(), np = hs.np, nl = hs.nl, D = 6 * np;
         const int nblk = (int)hs.blk_i1.size();
         *iters_out = 0;
@@ -1464,6 +1624,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                               carve_size<double>((size_t)D * D) + carve_size<double>(D) +
                               carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
                               carve_size<double>(nl + np) + (glob ? carve_size<double>((size_t)Dp * (Dp + 1)) : 0) +
+                              carve_size<double>(2 * (size_t)((nl * 8 + 63) / 64)) +
                               64;
         if ((rc2 = C.sys.reserve(ybytes))) return rc2;
         Carve cy{C.sys.as<char>()};
@@ -1480,6 +1641,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.rchi = cy.take<double>(std::max(Ea, nl));
         b.part = cy.take<double>(nl + np);
         b.Sg = glob ? cy.take<double>((size_t)Dp * (Dp + 1)) : nullptr;
+        double* d_wgpart = cy.take<double>(2 * (size_t)((nl * 8 + 63) / 64));   // point-update workgroup partials
         ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
         const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
@@ -1487,42 +1649,55 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                                         hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)std::max<size_t>(ldlt_lds, 1024)));
         const dim3 gg((nl * 8 + 63) / 64);   // 8 lanes per point
-        // The LM loop runs on the device (ba_decide_kernel advances it); the host keeps LOOKAHEAD
+        // The LM loop runs on the device (ba_decide_step advances it); the host keeps LOOKAHEAD
         // steps enqueued and reads each step's control snapshot from a pinned ring, so no trial
         // waits for a host round trip.  Steps enqueued past the end return immediately.
+        mark("structure upload enqueued");
         hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, iters);
         constexpr int LOOKAHEAD = 2;
         const int max_steps = iters * 10;
         int enq = 0, seen = 0;
+        int ids[LOOKAHEAD] = {0, 0};
         bool fin = false, stop_sent = false;
         BACtl last{};
         while (!fin) {
             while (enq < max_steps && enq - seen < LOOKAHEAD) {
                 hipLaunchKernelGGL(ba_iter_kernel, gg, dim3(64), 0, st, b);
-                hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b, 1);
-                if (enq == 0) hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
-                hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
-                if (np) hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk), dim3(1024), 0, st, b, D);
+                if (enq == 0) {   // first trial: computeLambdaInit needs Hpp before the Schur step
+                    hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b);
+                    hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
+                    hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
+                }
+                hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
                 if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
                 else hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
-                hipLaunchKernelGGL(ba_point_update_kernel, gg, dim3(64), 0, st, b, D);
                 const int slot = enq % LOOKAHEAD;
-                hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(1024), 0, st, b, C.d_ring + slot);
+                C.step_seq = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;
+                ids[slot] = C.step_seq;
+                hipLaunchKernelGGL(ba_point_update_kernel, gg, dim3(64), 0, st, b, D, d_wgpart);
+                hipLaunchKernelGGL(ba_decide_kernel, dim3(1), dim3(256), 0, st, b, C.d_ring + slot, ids[slot],
+                                   (const double*)d_wgpart, (int)gg.x);
                 ORB_HIP_TRY(hipGetLastError());
-                ORB_HIP_TRY(hipEventRecord(C.ring_ev[slot], st));
                 enq++;
             }
-            if (seen == enq) break;
+            if (seen == enq || stop_sent) break;
             const int slot = seen % LOOKAHEAD;
-            // wait for the step, mirroring the caller's stop flag into the device-visible word the
-            // decide kernel polls after every trial
-            if (!stop_flag) ORB_HIP_TRY(hipEventSynchronize(C.ring_ev[slot]));
-            while (stop_flag) {
-                const hipError_t q = hipEventQuery(C.ring_ev[slot]);
-                if (q == hipSuccess) break;
-                if (q != hipErrorNotReady) ORB_HIP_TRY(q);
+            // wait for the step's snapshot (a step that runs always writes one), mirroring the
+            // caller's stop flag into the device-visible word the decide kernel polls after every
+            // trial; the stream is queried now and then so a failed launch cannot hang the host
+            auto t_q = std::chrono::steady_clock::now();
+            while (__atomic_load_n(&C.h_ring[slot].seq, __ATOMIC_ACQUIRE) != ids[slot]) {
                 if (stop_flag) __atomic_store_n(C.h_stop, *stop_flag ? 1 : 0, __ATOMIC_RELEASE);
-                std::this_thread::yield();
+                const auto now = std::chrono::steady_clock::now();
+                if (now - t_q > std::chrono::microseconds(200)) {
+                    t_q = now;
+                    const hipError_t q = hipStreamQuery(st);
+                    if (q != hipSuccess && q != hipErrorNotReady) ORB_HIP_TRY(q);
+                    if (q == hipSuccess && __atomic_load_n(&C.h_ring[slot].seq, __ATOMIC_ACQUIRE) != ids[slot]) {
+                        set_error("LocalBA: LM step finished without a control snapshot");
+                        return ORB_EHIP;
+                    }
+                }
             }
             last = C.h_ring[slot];
             seen++;
@@ -1532,8 +1707,13 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 stop_sent = true;
             }
         }
-        ORB_HIP_TRY(hipStreamSynchronize(st));
-        ORB_HIP_TRY(hipMemcpy(&last, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost));
+        mark("LM loop done");
+        if (!fin) {   // loop cut short (step cap or force stop): the device state is authoritative
+            ORB_HIP_TRY(hipStreamSynchronize(st));
+            ORB_HIP_TRY(hipMemcpy(&last, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost));
+        }
+        // else: `last` is the final snapshot; the steps still queued return at once, stream-ordered
+        // before anything the caller enqueues next
         *iters_out = last.iters_done;
         *chi_out = last.chi_out;
         hook_stopped = hook_stopped || last.stopped;
@@ -1552,6 +1732,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 ORB_HIP_TRY(hipMemcpyAsync(level.data(), d_level, E, hipMemcpyDeviceToHost, st));
                 ORB_HIP_TRY(hipStreamSynchronize(st));
             }
+            mark("classify + level copy");
             if ((rc = optimize(10, &res->iterations[1], &res->chi2[1]))) return rc;
         }
     }
@@ -1576,6 +1757,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (res->edge_chi2) ORB_HIP_TRY(hipMemcpyAsync(hc, d_chi, 8 * (size_t)E, hipMemcpyDeviceToHost, st));
     }
     ORB_HIP_TRY(hipStreamSynchronize(st));
+    mark("results copied");
     std::memcpy(res->pose_t, ht, 24 * (size_t)P);
     std::memcpy(res->points, hX, 24 * (size_t)N);
     if (run) std::memcpy(res->edge_outlier, ho, E);
@@ -1585,6 +1767,11 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         q_to_R(&hq[4 * i], res->pose_R + 9 * i);
         if (res->pose_q) std::memcpy(res->pose_q + 4 * i, &hq[4 * i], 32);
     }
+    mark("end");
+    if (tdbg)
+        for (size_t i = 1; i < marks.size(); i++)
+            fprintf(stderr, "orbba %-28s %8.1f us\n", marks[i].first,
+                    std::chrono::duration<double, std::micro>(marks[i].second - marks[i - 1].second).count());
     return ORB_OK;
 }
 

@@ -36,3 +36,7 @@ for blk in range(16):
     print(line)
     prev = last
 print(f"back-substitution {v[40] - last}, total {v[40] - t0} ticks; load S {v[0] - v[41]}, pose update tail {v[42] - v[40]}")
+b2 = v[2 + 3 * 2]   # block 2 panel end = start of its lookahead phase
+if v[44] > b2:
+    print(f"block 2 lookahead by wave: w0 trailing tile {v[44] - b2}, w0 diag factor {v[45] - v[44]} (ends {v[45] - b2}), "
+          f"w1 inverse ends {v[46] - b2}, w2 tiles end {v[47] - b2}, w3 tiles end {v[48] - b2}")
