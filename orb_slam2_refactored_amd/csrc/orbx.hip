@@ -860,7 +860,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
-                                                        int n_items, int cpw, int cell_beg, int ncell) {
+                                                        int n_items, int cpw, int cell_beg, int ncell, int spec_min) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -894,6 +894,12 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         c.ndl = ((cd.zwzh & 0xffff) + 6 + 1 + 3) >> 2;   // LDS dwords per crop row
         return c;
     };
+    // Speculative iniThFAST pass: a cell whose predecessor in this wavefront (the neighbouring cell
+    // of the same level row) kept >= spec_min corners at iniThFAST is first run with the pre-test,
+    // the diagonal filter and the corner list at iniThFAST only.  When the NMS keeps one of them
+    // that is DetectFAST's answer (:527); otherwise the cell is re-run at min(ini, min).  On
+    // texture-rich frames most pixels pass at minThFAST but few at iniThFAST.
+    int prev_ini = 0;
     for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
     int f, ci;
@@ -903,13 +909,19 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     {
         crop_stage_rows(src, lane, crop, CSd);
     }
-    for (int i = lane; i < ((zh + 2) * ZSd + 15) >> 4; i += 64) reinterpret_cast<uint4*>(Mz)[i] = make_uint4(0, 0, 0, 0);
+    const int tlo = min(th_ini, th_min);
+    bool spec = spec_min > 0 && th_ini > tlo && prev_ini >= spec_min;
     uint8_t* Mc = Mz + ZSd + 1;   // zone (0, 0); the zero border makes out-of-zone neighbours read 0
+    uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
+    const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
+    int n_ini = 0, n_min = 0, total = 0;
+    for (;;) {   // passes: speculative (iniThFAST) and / or full (min(ini, min))
+    for (int i = lane; i < ((zh + 2) * ZSd + 15) >> 4; i += 64) reinterpret_cast<uint4*>(Mz)[i] = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
     if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
 
-    const int tlo = min(th_ini, th_min);
-    const us2 t2 = {(unsigned short)tlo, (unsigned short)tlo};
+    const int tp = spec ? th_ini : tlo;   // threshold of this pass
+    const us2 t2 = {(unsigned short)tp, (unsigned short)tp};
     // lanes: QR quads per row (8 or 16), 64/QR rows per chunk
     const int qsh = zw <= 32 ? 3 : 4;
     const int QR = 1 << qsh, RPC = 64 >> qsh;
@@ -933,7 +945,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         const int i = lane < n ? queue2[(h2 + lane) & (FQ2_RING - 1)] : -1;
         int M = 0;
         if (i >= 0) M = corner_strength_pk(&crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)], CSd);
-        const bool c = M > tlo;
+        const bool c = M > tp;
         const unsigned long long bm = __ballot(c);
         if (c) {
             const int pos = nc + popc64(bm & lt);
@@ -950,7 +962,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
             const uint8_t* c = &crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)];
             const int v = c[0];
             const int p2 = c[2 * CSd + 2], p6 = c[-2 * CSd + 2], p10 = c[-2 * CSd - 2], p14 = c[2 * CSd - 2];
-            pass = min(max(p2, p10), max(p6, p14)) > v + tlo || max(min(p2, p10), min(p6, p14)) < v - tlo;
+            pass = min(max(p2, p10), max(p6, p14)) > v + tp || max(min(p2, p10), min(p6, p14)) < v - tp;
         }
         const unsigned long long bm = __ballot(pass);
         if (pass) queue2[(q2n + popc64(bm & lt)) & (FQ2_RING - 1)] = (short)i;
@@ -1003,14 +1015,15 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
     wave_lds_sync();
     if (item == i_beg) FAST_STAMP(3, __builtin_amdgcn_s_memtime());
 
-    uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
-    const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
-    int n_ini = 0, n_min = 0, total = 0;
+    n_ini = 0;
+    n_min = 0;
     if (nc > fl.ccap) {
         // Dense cell (more corners than the list holds, e.g. pure noise): NMS over the zone map in
         // row-major order, one zone row per pass (zw <= 64), the same keep rule: a corner is kept
         // at threshold t iff M > t and every neighbour is < M (for M > t, a neighbour q >= M is
-        // also > t), so both thresholds share the neighbourhood maximum.
+        // also > t), so both thresholds share the neighbourhood maximum.  (The speculative pass's
+        // map holds only the corners at iniThFAST: a neighbour with M <= ini < m never suppresses
+        // at iniThFAST, so its iniThFAST set is the full pass's.)
         // Rows per pass: two 32-lane rows when the zone is at most 32 wide (every C1-C3 cell but the
         // widest cells of the smallest levels), else one 64-lane row.  The keep ballots of both
         // thresholds are computed once and kept in the (drained) passer ring for the emission pass;
@@ -1040,6 +1053,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
             n_min += popc64(bmn);
         }
         wave_lds_sync();
+        if (spec && n_ini == 0) goto full_pass;
         const int which = n_ini > 0 ? 0 : 1;
         total = which == 0 ? n_ini : n_min;
         int running = 0;
@@ -1081,6 +1095,7 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         n_min += popc64(bmn);
     }
     wave_lds_sync();
+    if (spec && n_ini == 0) goto full_pass;
 
     const int which = n_ini > 0 ? 0 : 1;
     total = which == 0 ? n_ini : n_min;
@@ -1099,6 +1114,11 @@ __global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev
         running += popc64(bm);
     }
     }   // list NMS
+    break;
+full_pass:   // the speculative pass kept no corner at iniThFAST: the full pass decides
+    spec = false;
+    }   // passes
+    prev_ini = n_ini;
     if (item == i_beg) FAST_STAMP(4, __builtin_amdgcn_s_memtime());
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
@@ -2076,6 +2096,9 @@ struct orbx_extractor {
     FastLds fl;
     size_t fast_lds = 0;
     int fast_cpw = 4;   // FAST cells per wavefront (1 -> 4: -3 % at C2; ORBX_FAST_CPW)
+    // a cell runs the speculative iniThFAST pass when the wavefront's previous cell kept at least
+    // fast_spec corners at iniThFAST (texture-rich regions); 0 = never (ORBX_FAST_SPEC)
+    int fast_spec = 8;
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     int debug_nc = 0;
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
@@ -2386,7 +2409,7 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         const int cpw = h->fast_cpw;
         launch_timed(h, 1, fast_cells_kernel, dim3((unsigned)((n_items + cpw - 1) / cpw)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
-                           h->p.minThFAST, slots, cellcnt, fault, h->fl, n_items, cpw, cb, nc);
+                           h->p.minThFAST, slots, cellcnt, fault, h->fl, n_items, cpw, cb, nc, h->fast_spec);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
@@ -2506,6 +2529,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->p = *params;
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
+    if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(0, atoi(e));
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;

@@ -71,6 +71,67 @@ def test_fast_candidates_dense_cells(oracle, kind):
             assert np.array_equal(got, exp), (kind, ini, mn, l, got.shape, exp.shape)
 
 
+def _patchwork(seed, W, H):
+    """Textured, low-contrast-textured (many pixels pass the pre-test at minThFAST, few or no
+    corners at iniThFAST) and flat cells side by side, in blocks of 1-3 cells."""
+    from orb_slam2_refactored_amd.synth import textured_image
+    rng = np.random.default_rng(seed)
+    img = synth_image(seed, W, H).copy()
+    tex = textured_image(seed + 1, W, H)
+    weak = np.clip(128 + rng.normal(0, 4, (H, W)), 0, 255).astype(np.uint8)
+    y = 0
+    while y < H:
+        h = int(rng.integers(30, 91))
+        x = 0
+        while x < W:
+            w = int(rng.integers(30, 91))
+            k = rng.integers(0, 3)
+            if k == 1:
+                img[y:y + h, x:x + w] = tex[y:y + h, x:x + w]
+            elif k == 2:
+                img[y:y + h, x:x + w] = weak[y:y + h, x:x + w]
+            x += w
+        y += h
+    return img
+
+
+@pytest.mark.parametrize("spec", [1, 8])
+@pytest.mark.parametrize("kind", ["textured", "patchwork"])
+def test_fast_speculative_pass(oracle, monkeypatch, spec, kind):
+    """The speculative iniThFAST pass (ORBX_FAST_SPEC: run when the wavefront's previous cell
+    kept >= spec corners at iniThFAST) and its fall-back full pass leave every candidate
+    unchanged; spec 1 sends nearly every cell after a textured one through the fall-back."""
+    from orb_slam2_refactored_amd.synth import textured_image
+    img = textured_image(77, 640, 480) if kind == "textured" else _patchwork(5, 640, 480)
+    monkeypatch.setenv("ORBX_FAST_SPEC", str(spec))
+    ex = make(2000)
+    ex.Extract(img)
+    lv = oracle.pyramid(oracle.params(2000), img)
+    for l in range(8):
+        got = ex.debug_level(l, stage="candidates")
+        exp = oracle.detect_fast(lv[l]).astype(np.int32)
+        assert np.array_equal(got, exp), (kind, spec, l, got.shape, exp.shape)
+
+
+def test_fast_speculative_pass_batch_equal(monkeypatch):
+    """Batched device output with the speculative pass off (0) and on (1, 8) is bit-identical."""
+    import torch
+    frames = np.stack([_patchwork(40 + i, 320, 240) for i in range(24)])
+    t = torch.from_numpy(frames).cuda()
+    outs = []
+    for spec in (0, 1, 8):
+        monkeypatch.setenv("ORBX_FAST_SPEC", str(spec))
+        o = make(500).extract_batch_device(t)
+        torch.cuda.synchronize()
+        outs.append([x.cpu().numpy() for x in o])
+    cnt = outs[0][2]
+    for o in outs[1:]:
+        assert np.array_equal(cnt, o[2])
+        for i, n in enumerate(cnt):
+            assert np.array_equal(outs[0][0][i, :n], o[0][i, :n]), i
+            assert np.array_equal(outs[0][1][i, :n], o[1][i, :n]), i
+
+
 @pytest.mark.parametrize("W,H,seed,nf", [(640, 480, 0, 1000), (1280, 720, 3, 2000), (640, 480, 9, 5000)])
 def test_quadtree_per_level(oracle, W, H, seed, nf):
     img = synth_image(seed, W, H)
