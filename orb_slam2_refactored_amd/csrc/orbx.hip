@@ -1126,7 +1126,7 @@ full_pass:   // the speculative pass kept no corner at iniThFAST: the full pass 
     }
     if (item == i_beg) {
         FAST_STAMP(2, __builtin_amdgcn_s_memtime());
-        FAST_STAMP(6, ((unsigned long long)cell.level << 48) | ((unsigned long long)nc << 16) | (unsigned)total);
+        FAST_STAMP(6, ((unsigned long long)cell.level << 48) | ((unsigned long long)n_min << 16) | (unsigned)total);
     }
     wave_lds_sync();
     }   // items

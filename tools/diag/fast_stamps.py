@@ -14,8 +14,14 @@ from orb_slam2_refactored_amd._lib import lib  # noqa: E402
 from orb_slam2_refactored_amd.synth import synth_image, textured_image  # noqa: E402
 
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 128
-gen = textured_image if len(sys.argv) > 2 and sys.argv[2] == "textured" else synth_image
-frames = torch.from_numpy(np.stack([gen(i % 16, 1280, 720) for i in range(F)])).cuda()
+kind = sys.argv[2] if len(sys.argv) > 2 else "g"
+if kind == "pan":
+    from orb_slam2_refactored_amd.synth import pan_sequence
+    pool = pan_sequence(0, 1280, 720, 16)
+    frames = torch.from_numpy(np.stack([pool[i % 16] for i in range(F)])).cuda()
+else:
+    gen = textured_image if kind == "textured" else synth_image
+    frames = torch.from_numpy(np.stack([gen(i % 16, 1280, 720) for i in range(F)])).cuda()
 ex = ORBextractor(ORBextractor.Parameters(nfeatures=2000))
 for _ in range(3):
     ex.extract_batch_device(frames)
