@@ -1156,11 +1156,44 @@ __device__ __forceinline__ void qt_child_geom(const QtNode& n, int c, QtNode& ch
     ch.bry = (short)((c & 2) ? n.bry : ym);
 }
 
-// One wave splits one node: counts per child (returned) and stable scatter into T.
+// One wave splits one node: counts per child (returned) and stable scatter into T.  A node of at
+// most 512 points is loaded once (8 independent loads per lane) and split from registers.
 __device__ int4 qt_wave_split(const QtNode& n, const uint32_t* __restrict__ P, uint32_t* __restrict__ T) {
     const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
     const int ym = n.tly + (n.bry - n.tly + 1) / 2;
     int c[4] = {0, 0, 0, 0};
+    if (n.cnt <= 512) {
+        const int lane = lane_id();
+        const unsigned long long lt = lanemask_lt();
+        uint32_t k[8];
+        int q[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int j = 64 * t + lane;
+            k[t] = j < n.cnt ? P[n.beg + j] : 0u;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int j = 64 * t + lane;
+            q[t] = j < n.cnt ? (kp_x(k[t]) < xm ? (kp_y(k[t]) < ym ? 0 : 2) : (kp_y(k[t]) < ym ? 1 : 3)) : -1;
+            if (64 * t < n.cnt) {   // wave-uniform
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) c[qq] += popc64(__ballot(q[t] == qq));
+            }
+        }
+        int o[4] = {n.beg, n.beg + c[0], n.beg + c[0] + c[1], n.beg + c[0] + c[1] + c[2]};
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (64 * t >= n.cnt) break;   // wave-uniform
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const unsigned long long m = __ballot(q[t] == qq);
+                if (q[t] == qq) T[o[qq] + popc64(m & lt)] = k[t];
+                o[qq] += popc64(m);
+            }
+        }
+        return make_int4(c[0], c[1], c[2], c[3]);
+    }
     for (int b = 0; b < n.cnt; b += 64) {
         const int j = b + lane_id();
         int q = -1;
@@ -1214,19 +1247,106 @@ __device__ int4 qt_group16_split(const QtNode& n, int cnt, const uint32_t* __res
     return make_int4(c0, c1, c2, c3);
 }
 
+// All threads of the (256-thread) block split one large node: child counts by a block reduction,
+// then the stable scatter in tiles of 1024 points, point u*256 + tid of a tile in thread tid, its
+// position from the per-(u, child, wave) ballot counts of the tile.  sc: 64 ints of LDS scratch.
+// Every thread must call it; the counts are block-uniform.
+constexpr int QT_BIG = 2048;   // phase-1 nodes above this size are split by the whole block
+__device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, uint32_t* __restrict__ T, int* sc) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const unsigned long long lt = lanemask_lt();
+    const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
+    const int ym = n.tly + (n.bry - n.tly + 1) / 2;
+    auto quad = [&](uint32_t k) { return kp_x(k) < xm ? (kp_y(k) < ym ? 0 : 2) : (kp_y(k) < ym ? 1 : 3); };
+    int c[4] = {0, 0, 0, 0};
+    for (int b = 0; b < n.cnt; b += 1024) {
+        uint32_t k[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int j = b + 256 * u + tid;
+            k[u] = j < n.cnt ? P[n.beg + j] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = b + 256 * u + tid < n.cnt ? quad(k[u]) : -1;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) c[qq] += q == qq;
+        }
+    }
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) {
+        const int v = wave_sum_i32(c[qq]);
+        if (lane == 0) sc[4 * w + qq] = v;
+    }
+    __syncthreads();
+    int tot[4], o[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) tot[qq] = sc[qq] + sc[4 + qq] + sc[8 + qq] + sc[12 + qq];
+    o[0] = n.beg;
+    o[1] = o[0] + tot[0];
+    o[2] = o[1] + tot[1];
+    o[3] = o[2] + tot[2];
+    __syncthreads();
+    for (int b = 0; b < n.cnt; b += 1024) {
+        uint32_t k[4];
+        int q[4];
+        unsigned long long m[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int j = b + 256 * u + tid;
+            k[u] = j < n.cnt ? P[n.beg + j] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            q[u] = b + 256 * u + tid < n.cnt ? quad(k[u]) : -1;
+            m[u] = 0;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const unsigned long long bm = __ballot(q[u] == qq);
+                if (q[u] == qq) m[u] = bm;
+                if (lane == 0) sc[16 * u + 4 * qq + w] = popc64(bm);   // (u, child, wave)
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (q[u] < 0) continue;
+            const int* cq = sc + 4 * q[u];
+            int off = o[q[u]];
+            for (int uu = 0; uu < u; uu++) off += cq[16 * uu] + cq[16 * uu + 1] + cq[16 * uu + 2] + cq[16 * uu + 3];
+            for (int ww = 0; ww < w; ww++) off += cq[16 * u + ww];
+            T[off + popc64(m[u] & lt)] = k[u];
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++)
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                o[qq] += sc[16 * u + 4 * qq] + sc[16 * u + 4 * qq + 1] + sc[16 * u + 4 * qq + 2] + sc[16 * u + 4 * qq + 3];
+        __syncthreads();
+    }
+    return make_int4(tot[0], tot[1], tot[2], tot[3]);
+}
+
 // Child counts of one node by a single thread (phase 2 only needs the counts of every divisible
-// node to find where to stop; only the processed prefix is then split for real).
+// node to find where to stop; only the processed prefix is then split for real); 8 loads in flight.
 __device__ __forceinline__ int4 qt_thread_count(const QtNode& n, const uint32_t* __restrict__ P) {
     const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
     const int ym = n.tly + (n.bry - n.tly + 1) / 2;
     int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    for (int j = 0; j < n.cnt; j++) {
-        const uint32_t k = P[n.beg + j];
-        const bool r = kp_x(k) >= xm, d = kp_y(k) >= ym;
-        c0 += !r && !d;
-        c1 += r && !d;
-        c2 += !r && d;
-        c3 += r && d;
+    for (int j0 = 0; j0 < n.cnt; j0 += 8) {
+        uint32_t kk[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) kk[u] = j0 + u < n.cnt ? P[n.beg + j0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t k = kk[u];
+            const bool in = j0 + u < n.cnt;
+            const bool r = kp_x(k) >= xm, d = kp_y(k) >= ym;
+            c0 += in && !r && !d;
+            c1 += in && r && !d;
+            c2 += in && !r && d;
+            c3 += in && r && d;
+        }
     }
     return make_int4(c0, c1, c2, c3);
 }
@@ -1417,6 +1537,8 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
     __shared__ int tmp[16];
     __shared__ int s_n, s_ndiv, s_state, s_proc, s_fail;
     __shared__ int s_sortcnt[2];
+    __shared__ int s_anybig;
+    __shared__ int s_split[64];
     __shared__ int rc[MAX_ROOTS];
 
     const int f = blockIdx.x, l = lev0 + (int)blockIdx.y;   // levels lev0 .. lev0 + gridDim.y - 1
@@ -1468,7 +1590,14 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
 #pragma unroll
             for (int q = 0; q < 8; q++)
                 if (q < cv[k]) P[o + q] = r[k][q];
-            for (int q = 8; q < cv[k]; q++) P[o + q] = fslots[cs[k] + q];   // rare: > 8 points in a cell
+            for (int q0 = 8; q0 < cv[k]; q0 += 8) {   // > 8 points in a cell: batches of 8 loads
+                uint32_t r2[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) r2[q] = q0 + q < cv[k] ? fslots[cs[k] + q0 + q] : 0u;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (q0 + q < cv[k]) P[o + q0 + q] = r2[q];
+            }
             o += cv[k];
         }
         carry = n_total;
@@ -1543,10 +1672,19 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             rid[t] = r;
             for (int q = 0; q < R; q++) counts[q] += popc64(__ballot(r == q));
         }
-        for (int b = q0 + 64 * QT_RPL; b < q1; b += 64) {   // quarters longer than 64*QT_RPL points
-            const int j = b + lane_id();
-            const int r = j < q1 ? root_of(P[j]) : -1;
-            for (int q = 0; q < R; q++) counts[q] += popc64(__ballot(r == q));
+        for (int b = q0 + 64 * QT_RPL; b < q1; b += 256) {   // quarters longer than 64*QT_RPL points
+            uint32_t kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = b + 64 * u + lane_id();
+                kk[u] = j < q1 ? P[j] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = b + 64 * u + lane_id();
+                const int r = j < q1 ? root_of(kk[u]) : -1;
+                for (int q = 0; q < R; q++) counts[q] += popc64(__ballot(r == q));
+            }
         }
         if (lane_id() == 0)
             for (int q = 0; q < R; q++) s_rcnt[w][q] = counts[q];
@@ -1577,19 +1715,32 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                 o[q] += popc64(m);
             }
         }
-        for (int b = q0 + 64 * QT_RPL; b < q1; b += 64) {
-            const int j = b + lane_id();
-            const uint32_t k = j < q1 ? P[j] : 0;
-            const int r = j < q1 ? root_of(k) : -1;
-            for (int q = 0; q < R; q++) {
-                const unsigned long long m = __ballot(r == q);
-                if (r == q) T[o[q] + popc64(m & lanemask_lt())] = k;
-                o[q] += popc64(m);
+        for (int b = q0 + 64 * QT_RPL; b < q1; b += 256) {
+            uint32_t kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = b + 64 * u + lane_id();
+                kk[u] = j < q1 ? P[j] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = b + 64 * u + lane_id();
+                const uint32_t k = kk[u];
+                const int r = j < q1 ? root_of(k) : -1;
+                for (int q = 0; q < R; q++) {
+                    const unsigned long long m = __ballot(r == q);
+                    if (r == q) T[o[q] + popc64(m & lanemask_lt())] = k;
+                    o[q] += popc64(m);
+                }
             }
         }
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < n_src; j += blockDim.x) P[j] = T[j];
+    {   // the partitioned copy becomes P (every thread swaps the same pointers)
+        uint32_t* t = P;
+        P = T;
+        T = t;
+    }
     if (threadIdx.x == 0) {
         int n = 0, acc = 0;
         for (int q = 0; q < R; q++) {
@@ -1608,6 +1759,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
         s_n = n;
         s_state = 0;   // 0 = phase 1, 1 = phase 2, 2 = finished
         s_ndiv = 0;
+        s_anybig = 0;
     }
     __syncthreads();
 
@@ -1631,10 +1783,11 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
         if (state == 0) {
             // Phase 1 pass (:588-630): split every divisible node in list order.
             // D positions via compaction
-            int kdiv = 0, nnd = 0;
+            int kdiv = 0, nnd = 0;   // (s_anybig was cleared before the last barrier)
             for (int b = 0; b < n; b += blockDim.x) {
                 const int i = b + threadIdx.x;
                 const int dvf = (i < n && na[i].cnt > 1) ? 1 : 0;
+                if (i < n && na[i].cnt > QT_BIG) s_anybig = 1;
                 int tot;
                 const int ex = block_excl_scan(dvf, tmp, &tot);
                 if (i < n) {
@@ -1658,9 +1811,17 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                 if (cnt > 0 && (lane_id() & 15) == 0) cc[j] = c;
             }
             for (int j = w; j < kdiv; j += nw) {
-                if (na[ia[j]].cnt <= 16) continue;   // wave-uniform
+                const int cn = na[ia[j]].cnt;
+                if (cn <= 16 || cn > QT_BIG) continue;   // wave-uniform
                 const int4 c = qt_wave_split(na[ia[j]], P, T);
                 if (lane_id() == 0) cc[j] = c;
+            }
+            if (s_anybig) {   // block-uniform (set before the scans' barriers)
+                for (int j = 0; j < kdiv; j++) {
+                    if (na[ia[j]].cnt <= QT_BIG) continue;   // block-uniform
+                    const int4 c = qt_block_split(na[ia[j]], P, T, s_split);
+                    if (threadIdx.x == 0) cc[j] = c;
+                }
             }
             __syncthreads();
             // group positions: reverse processing order; divisibles: forward order
@@ -1692,16 +1853,21 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             const int n_new = ne_total + nnd;
             for (int i = threadIdx.x; i < n; i += blockDim.x)
                 if (na[i].cnt <= 1 && ne_total + ib[i] < NC) nb[ne_total + ib[i]] = na[i];
-            // commit the splits T -> P
-            for (int j = w; j < kdiv; j += nw) {
-                const QtNode& p = na[ia[j]];
-                for (int q = lane_id(); q < p.cnt; q += 64) P[p.beg + q] = T[p.beg + q];
+            // commit: the single points of the non-divisible nodes join the split nodes' points in
+            // T, which becomes P (every thread swaps the same pointers)
+            for (int i = threadIdx.x; i < n; i += blockDim.x)
+                if (na[i].cnt == 1) T[na[i].beg] = P[na[i].beg];
+            {
+                uint32_t* t = P;
+                P = T;
+                T = t;
             }
             __syncthreads();
             if (threadIdx.x == 0) {
                 if (n_new > NC) { s_fail = 1; atomicOr(fault, FAULT_QT_NODES); }
                 s_n = min(n_new, NC);
                 s_ndiv = dv_carry;
+                s_anybig = 0;
                 if (n_new >= nfeat || n_new == n || s_fail) s_state = 2;
                 else if (n_new + 3 * dv_carry > nfeat) s_state = 1;
             }

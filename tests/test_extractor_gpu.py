@@ -146,6 +146,32 @@ def test_quadtree_per_level(oracle, W, H, seed, nf):
         assert np.array_equal(got, exp), l
 
 
+@pytest.mark.parametrize("kind,W,H,nf", [("textured", 1280, 720, 2000), ("textured", 1920, 1080, 4000),
+                                         ("patchwork", 1280, 720, 2000), ("noise", 1280, 720, 1000)])
+def test_quadtree_per_level_dense(oracle, kind, W, H, nf):
+    """Levels with tens of thousands of candidates: global candidate arrays, whole-block splits of
+    nodes above QT_BIG points, register-resident wave splits, batched gathers of full cells."""
+    from orb_slam2_refactored_amd.synth import textured_image
+    if kind == "textured":
+        img = textured_image(9, W, H)
+    elif kind == "patchwork":
+        img = _patchwork(11, W, H)
+    else:
+        img = np.random.default_rng(12).integers(0, 256, (H, W)).astype(np.uint8)
+    ex = make(nf)
+    kps, desc = ex.Extract(img)
+    p = oracle.params(nf)
+    lv = oracle.pyramid(p, img)
+    quota = oracle.scale_tables(p)["quota"]
+    for l in range(8):
+        cand = oracle.detect_fast(lv[l])
+        exp = oracle.quadtree(cand, lv[l].shape[0], lv[l].shape[1], int(quota[l])).astype(np.int32)
+        got = ex.debug_level(l, stage="selected")
+        assert np.array_equal(got, exp), (kind, l, len(cand), got.shape, exp.shape)
+    okps, odesc, _ = oracle.extract(p, img)
+    assert_same_kps(kps, okps, desc, odesc)
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2, 3])
 def test_extract_c1_golden(seed):
     g = np.load(GOLDEN / f"extract_c1_seed{seed}.npz")

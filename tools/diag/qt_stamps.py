@@ -11,10 +11,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from orb_slam2_refactored_amd import ORBextractor  # noqa: E402
 from orb_slam2_refactored_amd._lib import lib  # noqa: E402
-from orb_slam2_refactored_amd.synth import synth_image  # noqa: E402
+from orb_slam2_refactored_amd.synth import synth_image, textured_image  # noqa: E402
 
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 128
-frames = torch.from_numpy(np.stack([synth_image(i % 16, 1280, 720) for i in range(F)])).cuda()
+gen = textured_image if len(sys.argv) > 2 and sys.argv[2] == "textured" else synth_image
+frames = torch.from_numpy(np.stack([gen(i % 16, 1280, 720) for i in range(F)])).cuda()
 ex = ORBextractor(ORBextractor.Parameters(nfeatures=2000))
 for _ in range(3):
     ex.extract_batch_device(frames)
