@@ -14,8 +14,9 @@
 //                            solves, push + SE3 exp-update of the free poses
 //     ba_point_update_kernel back-substitution, push, point +=, errors + robust chi2 of its edges
 //     ba_decide_kernel       rho, lambda / nu update, accept or pop (restore)
-//   The first trial of an optimize() call runs ba_pose_accum_kernel, ba_lambda_init_kernel
-//   (computeLambdaInit) and ba_schur_point_kernel between the first two.
+//   The first trial of an optimize() call runs ba_pose_accum_kernel and ba_schur_point_kernel
+//   (computeLambdaInit from the diagonal maxima the first two gather, then the Schur point terms)
+//   between the first two.
 // Every reduction runs in a fixed order, so results are bit-reproducible run to run.  The LM
 // control scalars live on the device; the host reads one small status block per trial to decide
 // whether to run another (the reference's loop condition), and polls the stop flag like g2o.
@@ -36,6 +37,7 @@ struct BACtl {
     double lambda, ni, cur, ini, tmp, scale, rho;
     int ok2, accepted;
     double maxdiag;
+    unsigned long long maxdiag_bits;   // computeLambdaInit's max |diag H| as the bits of a double >= 0
     // LM loop state, advanced on the device by ba_decide_step (g2o SparseOptimizer::optimize +
     // OptimizationAlgorithmLevenberg::solve): iteration, trial within it, nBad, flags
     int it, q, nbad, done, need_lin, iters_max, iters_done;
@@ -304,6 +306,12 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
 #pragma unroll
     for (int i = 0; i < 3; i++) g[i] = grp_sum(g[i]);
     chi = grp_sum(chi);
+    if (b.ctl->it == 0) {   // first trial of an optimize(): computeLambdaInit's max over the points' diagonals
+        double m = live && sub == 0 ? fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))) : 0.0;
+        for (int o = 32; o >= GRP; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+        if (threadIdx.x == 0 && m > 0)
+            atomicMax(&b.ctl->maxdiag_bits, (unsigned long long)__double_as_longlong(m));
+    }
     if (live && sub == 0) {
         for (int i = 0; i < 9; i++) b.Hll[9 * l + i] = H[i];
         for (int i = 0; i < 3; i++) b.bl[3 * l + i] = g[i];
@@ -345,7 +353,14 @@ __global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b) {
     if (b.ctl->done || !b.ctl->need_lin) return;
     __shared__ double sh[1024];
     if ((int)blockIdx.x == b.np) chi_total(b, sh);
-    else pose_accum(b, blockIdx.x, sh);
+    else {
+        pose_accum(b, blockIdx.x, sh);   // ends with a barrier: Hpp visible to the workgroup
+        if (threadIdx.x == 0) {   // computeLambdaInit's max over this pose's diagonal
+            double m = 0;
+            for (int k = 0; k < 6; k++) m = fmax(m, fabs(b.Hpp[36 * blockIdx.x + 7 * k]));
+            if (m > 0) atomicMax(&b.ctl->maxdiag_bits, (unsigned long long)__double_as_longlong(m));
+        }
+    }
 }
 __device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh) {
     const int g = threadIdx.x / 42, c = threadIdx.x % 42;
@@ -372,26 +387,6 @@ __device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh) {
     __syncthreads();   // sh reused by the caller; Hpp / bp read back by the same workgroup
 }
 
-// computeLambdaInit (levenberg.cpp:166-180): tau * max |diag H| over active vertices.
-__global__ __launch_bounds__(256) void ba_lambda_init_kernel(BADev b) {
-    if (b.ctl->done || !b.ctl->need_lin || b.ctl->it != 0) return;
-    __shared__ double sh[256];
-    double m = 0;
-    for (int i = threadIdx.x; i < 6 * b.np; i += blockDim.x) m = fmax(m, fabs(b.Hpp[36 * (i / 6) + 7 * (i % 6)]));
-    for (int i = threadIdx.x; i < 3 * b.nl; i += blockDim.x) m = fmax(m, fabs(b.Hll[9 * (i / 3) + 4 * (i % 3)]));
-    sh[threadIdx.x] = m;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + o]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        b.ctl->maxdiag = sh[0];
-        b.ctl->lambda = 1e-5 * sh[0];
-        b.ctl->ni = 2;
-    }
-}
-
 __device__ __forceinline__ bool inv3(const double* m, double* o) {
     const double c00 = m[4] * m[8] - m[5] * m[7], c01 = m[5] * m[6] - m[3] * m[8], c02 = m[3] * m[7] - m[4] * m[6];
     const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
@@ -403,10 +398,19 @@ __device__ __forceinline__ bool inv3(const double* m, double* o) {
     return true;
 }
 
-// The first trial of an optimize() call: the Schur point terms after computeLambdaInit.
+// The first trial of an optimize() call: computeLambdaInit (levenberg.cpp:166-180: tau * max |diag H|
+// over the active vertices, the max gathered by ba_iter_kernel and ba_pose_accum_kernel), then the
+// Schur point terms with that lambda.
 __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
     BA_RETURN_IF_DONE(b);
+    const double maxdiag = __longlong_as_double((long long)b.ctl->maxdiag_bits);
+    const double lam = 1e-5 * maxdiag;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        b.ctl->maxdiag = maxdiag;
+        b.ctl->lambda = lam;
+        b.ctl->ni = 2;
+    }
     const int l = t / GRP, sub = t % GRP;
     if (l >= b.nl) return;
     double H[9], g[3];
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
     for (int i = 0; i < 9; i++) H[i] = b.Hll[9 * l + i];
 #pragma unroll
     for (int i = 0; i < 3; i++) g[i] = b.bl[3 * l + i];
-    schur_point_terms(b, l, sub, H, g, b.ctl->lambda);
+    schur_point_terms(b, l, sub, H, g, lam);
 }
 
 // Reduced camera system block (i1, i2): 36 entries x 28 partial groups (two accumulators each),
@@ -1211,6 +1215,7 @@ __global__ void ba_ctl_start_kernel(BADev b, int iters) {
     c->q = 0;
     c->nbad = 0;
     c->done = iters <= 0 ? 1 : 0;
+    c->maxdiag_bits = 0;
     c->need_lin = 1;
     c->iters_max = iters;
     c->iters_done = 0;
@@ -1220,8 +1225,17 @@ __global__ void ba_ctl_start_kernel(BADev b, int iters) {
 
 __global__ void ba_ctl_stop_kernel(BADev b) { b.ctl->done = 1; }
 
-__global__ void ba_classify_kernel(BADev b, uint8_t* outlier, double* chi2o, uint8_t* level, int set_level) {
+// With rq / rt / rX (the final call) it also gathers the poses and points into the result region,
+// so the results come back in one copy.
+__global__ void ba_classify_kernel(BADev b, uint8_t* outlier, double* chi2o, uint8_t* level, int set_level,
+                                   double* rq, double* rt, double* rX) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rq && e < b.P) {
+        for (int j = 0; j < 4; j++) rq[4 * e + j] = b.q[4 * e + j];
+        for (int j = 0; j < 3; j++) rt[3 * e + j] = b.t[3 * e + j];
+    }
+    if (rX && e < b.N)
+        for (int j = 0; j < 3; j++) rX[3 * e + j] = b.X[3 * e + j];
     if (e >= b.E) return;
     const double maxc = b.stereo[e] ? 7.815 : 5.991;
     const double c = edge_chi2(b, e);
@@ -1266,7 +1280,7 @@ struct PinnedBuf {
 struct BAContext {
     int device = -1;
     hipStream_t st = nullptr;
-    DevBuf prob, state, structure, sys, ctlbuf;
+    DevBuf prob, state, structure, sys, ctlbuf, resbuf;
     BACtl* h_ctl = nullptr;   // pinned
     BACtl* h_ring = nullptr;  // pinned, device-mapped control snapshots, one per step in flight
     BACtl* d_ring = nullptr;
@@ -1279,7 +1293,7 @@ struct BAContext {
     void reset_device() {
         if (device >= 0) (void)hipSetDevice(device);
         if (st) (void)hipStreamSynchronize(st);
-        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
+        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release(); resbuf.release();
         if (st) { (void)hipStreamDestroy(st); st = nullptr; }
         if (h_ring) { (void)hipHostFree(h_ring); h_ring = nullptr; d_ring = nullptr; }
         if (h_stop) { (void)hipHostFree(h_stop); h_stop = nullptr; d_stop = nullptr; }
@@ -1289,7 +1303,7 @@ struct BAContext {
     ~BAContext() {
         if (h_stop) (void)hipHostFree(h_stop);
         if (h_ring) (void)hipHostFree(h_ring);
-        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
+        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release(); resbuf.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -1312,7 +1326,7 @@ size_t carve_size(size_t n) { return align_up(std::max<size_t>(n, 1) * sizeof(T)
 struct HostStructure {
     std::vector<int> act, hp, hl, pt_beg, pt_slot, pt_id, ps_beg, ps_slot, ps_id, blk_i1, blk_i2, blk_beg;
     std::vector<int2> blk_pair;
-    std::vector<int> blk_index, blk_fill, fs_beg, fs_slot, fs_hp;   // scratch (capacity kept across calls)
+    std::vector<int> blk_index, fs_beg, fs_slot, fs_hp, sl, sp, cur;   // scratch (capacity kept across calls)
     std::vector<uint8_t> pa, la;
     int np = 0, nl = 0;
 };
@@ -1320,64 +1334,92 @@ struct HostStructure {
 // SparseOptimizer::initializeOptimization(level) (sparse_optimizer.cpp:206-264) and the
 // BlockSolver structure (block_solver.hpp:142-295): active edges / vertices, Hessian indices, and
 // the Schur fill pattern (pose pairs that share a point).  Flat two-pass build (count, then fill)
-// into vectors that keep their capacity across calls: no allocation per point or per block.
+// over per-slot (point, pose) Hessian ids, into vectors that keep their capacity across calls: no
+// allocation per point or per block.
 // Pair order inside a block: points ascending, then (slot a, slot c) in the point's slot order.
 void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
                      const int* ek, HostStructure& s) {
     const int E = (int)level.size();
     s.pa.assign(P, 0);
     s.la.assign(N, 0);
-    s.act.clear();
-    for (int e = 0; e < E; e++)
-        if (level[e] == 0) { s.act.push_back(e); s.pa[ek[e]] = 1; s.la[ep[e]] = 1; }
-    s.hp.assign(P, -1); s.hl.assign(N, -1);
-    s.ps_id.clear(); s.pt_id.clear();
-    s.np = 0; s.nl = 0;
-    for (int i = 0; i < P; i++) if (s.pa[i] && !fixed[i]) { s.hp[i] = s.np++; s.ps_id.push_back(i); }
-    for (int i = 0; i < N; i++) if (s.la[i]) { s.hl[i] = s.nl++; s.pt_id.push_back(i); }
-    const int Ea = (int)s.act.size();
-    s.pt_beg.assign(s.nl + 1, 0); s.ps_beg.assign(s.np + 1, 0);
+    s.act.resize(E);
+    int Ea = 0;
+    {
+        int* act = s.act.data();
+        uint8_t* pa = s.pa.data();
+        uint8_t* la = s.la.data();
+        for (int e = 0; e < E; e++)
+            if (level[e] == 0) { act[Ea++] = e; pa[ek[e]] = 1; la[ep[e]] = 1; }
+    }
+    s.act.resize(Ea);
+    s.hp.resize(P); s.hl.resize(N);
+    s.ps_id.resize(P); s.pt_id.resize(N);
+    int np = 0, nl = 0;
+    for (int i = 0; i < P; i++) {
+        s.hp[i] = (s.pa[i] && !fixed[i]) ? np : -1;
+        if (s.hp[i] >= 0) s.ps_id[np++] = i;
+    }
+    for (int i = 0; i < N; i++) {
+        s.hl[i] = s.la[i] ? nl : -1;
+        if (s.la[i]) s.pt_id[nl++] = i;
+    }
+    s.ps_id.resize(np); s.pt_id.resize(nl);
+    s.np = np; s.nl = nl;
+    // per active slot k: its point's and pose's Hessian ids
+    s.sl.resize(Ea); s.sp.resize(Ea);
+    int* sl = s.sl.data();
+    int* sp = s.sp.data();
     for (int k = 0; k < Ea; k++) {
         const int e = s.act[k];
-        s.pt_beg[s.hl[ep[e]] + 1]++;
-        if (s.hp[ek[e]] >= 0) s.ps_beg[s.hp[ek[e]] + 1]++;
+        sl[k] = s.hl[ep[e]];
+        sp[k] = s.hp[ek[e]];
     }
-    for (int i = 0; i < s.nl; i++) s.pt_beg[i + 1] += s.pt_beg[i];
-    for (int i = 0; i < s.np; i++) s.ps_beg[i + 1] += s.ps_beg[i];
-    s.pt_slot.resize(Ea); s.ps_slot.resize(s.ps_beg[s.np]);
+    s.pt_beg.assign(nl + 1, 0); s.ps_beg.assign(np + 1, 0); s.fs_beg.assign(nl + 1, 0);
     {
-        // fill cursors: blk_fill doubles as scratch here (nl + np entries)
-        s.blk_fill.assign(s.pt_beg.begin(), s.pt_beg.end() - 1);
-        s.blk_fill.insert(s.blk_fill.end(), s.ps_beg.begin(), s.ps_beg.end() - 1);
-        int* fp = s.blk_fill.data();
-        int* fq = fp + s.nl;
+        int* pb = s.pt_beg.data();
+        int* qb = s.ps_beg.data();
+        int* fb = s.fs_beg.data();
         for (int k = 0; k < Ea; k++) {
-            const int e = s.act[k];
-            s.pt_slot[fp[s.hl[ep[e]]]++] = k;
-            if (s.hp[ek[e]] >= 0) s.ps_slot[fq[s.hp[ek[e]]]++] = k;
+            pb[sl[k] + 1]++;
+            if (sp[k] >= 0) { qb[sp[k] + 1]++; fb[sl[k] + 1]++; }
+        }
+        for (int i = 0; i < nl; i++) { pb[i + 1] += pb[i]; fb[i + 1] += fb[i]; }
+        for (int i = 0; i < np; i++) qb[i + 1] += qb[i];
+    }
+    s.pt_slot.resize(Ea); s.ps_slot.resize(s.ps_beg[np]);
+    s.fs_slot.resize(s.fs_beg[nl]); s.fs_hp.resize(s.fs_beg[nl]);
+    {
+        // fill cursors (k ascending, so every list is in slot order)
+        s.cur.resize(2 * (size_t)nl + np);
+        int* fp = s.cur.data();
+        int* fr = fp + nl;
+        int* fq = fr + nl;
+        std::copy(s.pt_beg.begin(), s.pt_beg.end() - 1, fp);
+        std::copy(s.fs_beg.begin(), s.fs_beg.end() - 1, fr);
+        std::copy(s.ps_beg.begin(), s.ps_beg.end() - 1, fq);
+        int* pts = s.pt_slot.data();
+        int* pss = s.ps_slot.data();
+        int* fss = s.fs_slot.data();
+        int* fsh = s.fs_hp.data();
+        for (int k = 0; k < Ea; k++) {
+            const int l = sl[k], h = sp[k];
+            pts[fp[l]++] = k;
+            if (h >= 0) {
+                pss[fq[h]++] = k;
+                fss[fr[l]] = k;
+                fsh[fr[l]++] = h;
+            }
         }
     }
-    // pose-pair blocks (i1 <= i2): pass 1 counts the pairs per block, pass 2 fills them.  Per point,
-    // its slots whose pose is free (slot order) with their Hessian pose index, as one flat CSR.
-    const int np = s.np;
-    s.fs_beg.resize(s.nl + 1);
-    s.fs_slot.clear();
-    s.fs_hp.clear();
-    for (int l = 0; l < s.nl; l++) {
-        s.fs_beg[l] = (int)s.fs_slot.size();
-        for (int u = s.pt_beg[l]; u < s.pt_beg[l + 1]; u++) {
-            const int k = s.pt_slot[u];
-            const int h = s.hp[ek[s.act[k]]];
-            if (h >= 0) { s.fs_slot.push_back(k); s.fs_hp.push_back(h); }
-        }
-    }
-    s.fs_beg[s.nl] = (int)s.fs_slot.size();
+    // pose-pair blocks (i1 <= i2): pass 1 counts the pairs per block, pass 2 fills them, from each
+    // point's free slots (slot order) with their Hessian pose index.
     s.blk_index.assign((size_t)np * np, 0);
     {
         const int* fh = s.fs_hp.data();
+        const int* fb = s.fs_beg.data();
         int* cnt = s.blk_index.data();
-        for (int l = 0; l < s.nl; l++) {
-            const int b0 = s.fs_beg[l], b1 = s.fs_beg[l + 1];
+        for (int l = 0; l < nl; l++) {
+            const int b0 = fb[l], b1 = fb[l + 1];
             for (int a = b0; a < b1; a++) {
                 const int i1 = fh[a];
                 int* row = cnt + (size_t)i1 * np;
@@ -1401,14 +1443,15 @@ void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint
     s.blk_pair.resize(total);
     {
         const int* fh = s.fs_hp.data();
+        const int* fb = s.fs_beg.data();
         const int* fsl = s.fs_slot.data();
-        int* cur = s.blk_index.data();
+        int* curp = s.blk_index.data();
         int2* out = s.blk_pair.data();
-        for (int l = 0; l < s.nl; l++) {
-            const int b0 = s.fs_beg[l], b1 = s.fs_beg[l + 1];
+        for (int l = 0; l < nl; l++) {
+            const int b0 = fb[l], b1 = fb[l + 1];
             for (int a = b0; a < b1; a++) {
                 const int i1 = fh[a];
-                int* row = cur + (size_t)i1 * np;
+                int* row = curp + (size_t)i1 * np;
                 for (int c = b0; c < b1; c++)
                     if (i1 <= fh[c]) out[row[fh[c]]++] = make_int2(fsl[a], fsl[c]);
             }
@@ -1495,8 +1538,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                             carve_size<double>(5 * (size_t)E) + carve_size<double>(4 * (size_t)P) +
                             carve_size<double>(3 * (size_t)P) + carve_size<double>(3 * (size_t)N);
     const size_t state_bytes = carve_size<double>(4 * (size_t)P) + carve_size<double>(3 * (size_t)P) +
-                               carve_size<double>(3 * (size_t)N) + carve_size<uint8_t>(E) * 3 +
-                               carve_size<double>(3 * (size_t)E) + carve_size<double>(E);
+                               carve_size<double>(3 * (size_t)N) + carve_size<uint8_t>(E) * 2 +
+                               carve_size<double>(3 * (size_t)E);
     const size_t res_bytes = carve_size<double>(4 * (size_t)P) + carve_size<double>(3 * (size_t)P) +
                              carve_size<double>(3 * (size_t)N) + carve_size<uint8_t>(E) + carve_size<double>(E);
     int rc;
@@ -1537,9 +1580,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     b.X_sv = cs.take<double>(3 * (size_t)N);
     b.robust = cs.take<uint8_t>(E);
     uint8_t* d_level = cs.take<uint8_t>(E);
-    uint8_t* d_outl = cs.take<uint8_t>(E);
     b.err = cs.take<double>(3 * (size_t)E);
-    double* d_chi = cs.take<double>(E);
     b.fixed = d_fixed; b.ep = d_ep; b.ek = d_ek; b.stereo = d_st; b.obs = d_obs; b.info = d_info; b.cam = d_cam;
     b.ctl = C.ctlbuf.as<BACtl>();
     b.stop = stop_flag ? C.d_stop : nullptr;
@@ -1665,7 +1706,6 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 hipLaunchKernelGGL(ba_iter_kernel, gg, dim3(64), 0, st, b);
                 if (enq == 0) {   // first trial: computeLambdaInit needs Hpp before the Schur step
                     hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b);
-                    hipLaunchKernelGGL(ba_lambda_init_kernel, dim3(1), dim3(256), 0, st, b);
                     hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
                 }
                 hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
@@ -1728,7 +1768,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             // tag outliers (level 1) and drop the robust kernels (:644-670)
             if (E) {
                 hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, (uint8_t*)nullptr,
-                                   (double*)nullptr, d_level, 1);
+                                   (double*)nullptr, d_level, 1, (double*)nullptr, (double*)nullptr, (double*)nullptr);
                 ORB_HIP_TRY(hipMemcpyAsync(level.data(), d_level, E, hipMemcpyDeviceToHost, st));
                 ORB_HIP_TRY(hipStreamSynchronize(st));
             }
@@ -1736,25 +1776,25 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             if ((rc = optimize(10, &res->iterations[1], &res->chi2[1]))) return rc;
         }
     }
-    if (E) {
-        hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, d_outl, d_chi,
-                           (uint8_t*)nullptr, 0);
-        ORB_HIP_TRY(hipGetLastError());
-    }
-    Carve hres{C.h_res.ptr};
+    // final classification + poses / points gathered into one result region (h_res's layout), one copy
+    if ((rc = C.resbuf.reserve(res_bytes))) return rc;
+    Carve dres{C.resbuf.as<char>()}, hres{C.h_res.ptr};
+    double* rq = dres.take<double>(4 * (size_t)P);
+    double* rt = dres.take<double>(3 * (size_t)P);
+    double* rX = dres.take<double>(3 * (size_t)N);
+    uint8_t* ro = dres.take<uint8_t>(E);
+    double* rch = dres.take<double>(E);
     double* hq = hres.take<double>(4 * (size_t)P);
     double* ht = hres.take<double>(3 * (size_t)P);
     double* hX = hres.take<double>(3 * (size_t)N);
     uint8_t* ho = hres.take<uint8_t>(E);
     double* hc = hres.take<double>(E);
-    if (P) {
-        ORB_HIP_TRY(hipMemcpyAsync(hq, b.q, 32 * (size_t)P, hipMemcpyDeviceToHost, st));
-        ORB_HIP_TRY(hipMemcpyAsync(ht, b.t, 24 * (size_t)P, hipMemcpyDeviceToHost, st));
-    }
-    if (N) ORB_HIP_TRY(hipMemcpyAsync(hX, b.X, 24 * (size_t)N, hipMemcpyDeviceToHost, st));
-    if (E) {
-        ORB_HIP_TRY(hipMemcpyAsync(ho, d_outl, E, hipMemcpyDeviceToHost, st));
-        if (res->edge_chi2) ORB_HIP_TRY(hipMemcpyAsync(hc, d_chi, 8 * (size_t)E, hipMemcpyDeviceToHost, st));
+    if (const int nt = std::max(E, std::max(N, P))) {
+        hipLaunchKernelGGL(ba_classify_kernel, dim3((nt + 255) / 256), dim3(256), 0, st, b, ro, rch, (uint8_t*)nullptr, 0,
+                           rq, rt, rX);
+        ORB_HIP_TRY(hipGetLastError());
+        ORB_HIP_TRY(hipMemcpyAsync(C.h_res.ptr, C.resbuf.ptr, res->edge_chi2 ? dres.off : (size_t)(reinterpret_cast<char*>(rch) - C.resbuf.as<char>()),
+                                   hipMemcpyDeviceToHost, st));
     }
     ORB_HIP_TRY(hipStreamSynchronize(st));
     mark("results copied");
