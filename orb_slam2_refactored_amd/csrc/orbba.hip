@@ -102,6 +102,8 @@ struct BADev {
     double* x;            // D + 3 nl
     double* rchi;         // Ea: robust chi2 per active slot
     double* part;         // scale partials: nl + np
+    double* Spart;         // SB_SPLIT x nblk x 36: the Schur-block parts' partial blocks
+    unsigned* blk_done;    // nblk: parts of the block finished (the last one forms S)
     BACtl* ctl;
     const int32_t* stop;   // device view of the host's force-stop flag (mapped pinned mirror), or null
     int stop_after;        // test hook: stop once this many trials have run (-1: off)
@@ -426,24 +428,30 @@ __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
 // With `accum` (every step but an optimize() call's first), a linearising trial also forms here what
 // ba_pose_accum_kernel would: each diagonal block's workgroup the Hpp / b_p sums of its pose first,
 // workgroup nblk the chi2 total.
+// The pair list of a block is split into SB_SPLIT contiguous parts, one workgroup each (blockIdx.y),
+// each storing its partial block (device-coherent stores, completed before it counts in); the last
+// part of a block to count in adds the partials in part order and writes the block of S.  Part 0
+// also adds Hpp + lambda I and does the diagonal blocks' extras.
 constexpr int SB_G = 28;
+constexpr int SB_SPLIT = 8;
 __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, int accum) {
     BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
-    const int blk = blockIdx.x;
+    const int blk = blockIdx.x, part = blockIdx.y;
     const bool acc = accum && b.ctl->need_lin;
     if (blk == b.nblk) {
-        if (acc) chi_total(b, sh);
+        if (acc && part == 0) chi_total(b, sh);
         return;
     }
     const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
-    if (acc && i1 == i2) pose_accum(b, i1, sh);
+    if (acc && i1 == i2 && part == 0) pose_accum(b, i1, sh);
     const int g = threadIdx.x / 36, c = threadIdx.x % 36;
     const int r = c / 6, cc = c % 6;
     if (g < SB_G) {
         double s0 = 0, s1 = 0;
-        const int end = b.blk_beg[blk + 1];
-        int u = b.blk_beg[blk] + g;
+        const int pb = b.blk_beg[blk], pn = b.blk_beg[blk + 1] - pb;
+        const int end = pb + (int)(((long long)pn * (part + 1)) / SB_SPLIT);
+        int u = pb + (int)(((long long)pn * part) / SB_SPLIT) + g;
         for (; u + SB_G < end; u += 2 * SB_G) {
             const int2 p0 = b.blk_pair[u], p1 = b.blk_pair[u + SB_G];
             const double* W0 = b.W + (long long)p0.x * 24 + 3 * r;
@@ -466,14 +474,30 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
         double s = 0;
         for (int q = 0; q < SB_G; q++) s += sh[q * 36 + threadIdx.x];
         double v = -s;
-        if (i1 == i2) {
+        if (i1 == i2 && part == 0) {
             v += b.Hpp[36 * i1 + threadIdx.x];
             if (r == cc) v += b.ctl->lambda;
         }
+        __hip_atomic_store(&b.Spart[((long long)part * b.nblk + blk) * 36 + threadIdx.x], v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __shared__ int s_last;
+    if (threadIdx.x == 0) {   // wavefront 0 stored the partials: wait for them, then count in
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = __hip_atomic_fetch_add(&b.blk_done[blk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 SB_SPLIT - 1;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < 36) {
+        double v = 0;
+        for (int k = 0; k < SB_SPLIT; k++)
+            v += __hip_atomic_load(&b.Spart[((long long)k * b.nblk + blk) * 36 + threadIdx.x], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         b.S[(long long)(6 * i1 + r) * D + 6 * i2 + cc] = v;
         if (i1 != i2) b.S[(long long)(6 * i2 + cc) * D + 6 * i1 + r] = v;
+        if (threadIdx.x == 0) __hip_atomic_store(&b.blk_done[blk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (i1 != i2) return;
+    if (i1 != i2 || part != 0) return;
     __syncthreads();
     // b_schur for pose i1: 6 entries x 168 partial groups
     const int g2 = threadIdx.x / 6, c2 = threadIdx.x % 6;
@@ -1662,7 +1686,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         const size_t ybytes = carve_size<double>(72 * (size_t)Ea) + carve_size<double>(24 * (size_t)Ea) +
                               carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +
                               carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
-                              carve_size<double>((size_t)D * D) + carve_size<double>(D) +
+                              carve_size<double>((size_t)D * D) + carve_size<double>((size_t)SB_SPLIT * nblk * 36) +
+                              carve_size<unsigned>((size_t)nblk) + carve_size<double>(D) +
                               carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
                               carve_size<double>(nl + np) + (glob ? carve_size<double>((size_t)Dp * (Dp + 1)) : 0) +
                               carve_size<double>(2 * (size_t)((nl * 8 + 63) / 64)) +
@@ -1677,6 +1702,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.Hpp = cy.take<double>(36 * (size_t)np);
         b.bp = cy.take<double>(6 * (size_t)np);
         b.S = cy.take<double>((size_t)D * D);
+        b.Spart = cy.take<double>((size_t)SB_SPLIT * nblk * 36);
+        b.blk_done = cy.take<unsigned>((size_t)nblk);
         b.bs = cy.take<double>(D);
         b.x = cy.take<double>(D + 3 * (size_t)nl);
         b.rchi = cy.take<double>(std::max(Ea, nl));
@@ -1685,6 +1712,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         double* d_wgpart = cy.take<double>(2 * (size_t)((nl * 8 + 63) / 64));   // point-update workgroup partials
         ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
+        if (nblk) ORB_HIP_TRY(hipMemsetAsync(b.blk_done, 0, (size_t)nblk * 4, st));
         const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
         ORB_HIP_TRY(hipFuncSetAttribute(glob ? (const void*)ba_solve_global_kernel : (const void*)ba_solve_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1708,7 +1736,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                     hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b);
                     hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
                 }
-                hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
+                hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
                 if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
                 else hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
                 const int slot = enq % LOOKAHEAD;
