@@ -235,13 +235,200 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
         }
 }
 
+// The same top-2 on the block-scaled FP4 matrix path (v_mfma_scale_f32_16x16x128_f8f6f4, e2m1
+// operands: K = 128 per instruction, twice the i8 form's K at the same issue cost, and half the
+// expanded bytes).  A bit becomes a nibble: A's 1 -> -4 with block scale 2^6 (-256), B's 1 -> 1.0
+// with scale 2^0, so a common bit contributes -256 and, with the f32 accumulator started at
+// 128 (|b| + 256) + t (exact: every value is an integer below 2^17), the MFMA again yields the chunk
+// key 128 S + t, now as an f32.  The keys are non-negative, so their bit patterns order as the
+// values: the running min / median run on the raw bits, converted to integers once per chunk.
+// Lane group g takes descriptor bytes 8g..8g+7; k-step m its bits 32m..32m+31 (any k permutation
+// shared by A and B leaves the dot product unchanged).
+typedef int i8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t spread8(uint32_t b) {   // bit i of the low byte -> bit 4i
+    uint32_t x = b & 0xffu;
+    x = (x | (x << 12)) & 0x000f000fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    return x;
+}
+__device__ __forceinline__ i4v expand32_nib(uint32_t b, uint32_t nib) {   // bit k of b -> nibble k (0 / nib)
+    i4v r;
+    r.x = (int)(spread8(b) * nib);
+    r.y = (int)(spread8(b >> 8) * nib);
+    r.z = (int)(spread8(b >> 16) * nib);
+    r.w = (int)(spread8(b >> 24) * nib);
+    return r;
+}
+constexpr uint32_t FP4_NEG4 = 0xEu, FP4_ONE = 0x2u;    // e2m1: -4.0, 1.0
+constexpr int FP4_SCALE_A = 0x85858585, FP4_SCALE_B = 0x7f7f7f7f;   // e8m0: 2^6, 2^0
+
+__device__ __forceinline__ f4v mfma_fp4(i4v a, i4v b, f4v c) {
+    const i8v a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, -1, -1, -1, -1);
+    const i8v b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, -1, -1, -1, -1);
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 4, 4, 0, FP4_SCALE_A, 0, FP4_SCALE_B);
+}
+
+constexpr int FP_RT = 4;               // 16-row tiles per wavefront (69 -> 114 VGPRs, 4 wavefronts per SIMD)
+constexpr int FP_WROWS = 16 * FP_RT;
+constexpr int FP_ROWS = 4 * FP_WROWS;
+template <bool MULTI>
+__global__ __launch_bounds__(256) void hamming_top2_fp4_kernel(
+    const uint8_t* __restrict__ A, const int32_t* __restrict__ nA_arr, int nA_fixed, int strideA,
+    const uint8_t* __restrict__ B, const int32_t* __restrict__ nB_arr, int nB_fixed, int strideB,
+    const int32_t* __restrict__ pair_b, float nnratio, int th_low, int32_t* __restrict__ best_idx,
+    int32_t* __restrict__ best, int32_t* __restrict__ second, int32_t* __restrict__ match) {
+    extern __shared__ __attribute__((aligned(16))) int mm_sm[];   // pa[FP_ROWS] | pb[nB padded to 32] | expanded B [2][2][2][64]
+    int* s_pa = mm_sm;
+    int* s_pb = mm_sm + FP_ROWS;
+    const int p = blockIdx.y;
+    const int q = pair_b ? pair_b[p] : p;
+    const int nA = nA_arr ? nA_arr[p] : nA_fixed;
+    const int nB = nB_arr ? nB_arr[q] : nB_fixed;
+    const int row_base = blockIdx.x * FP_ROWS;
+    if (row_base >= nA) return;   // block-uniform
+    const uint8_t* Ap = A + (long long)p * strideA * 32;
+    const uint8_t* Bp = B + (long long)q * strideB * 32;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    const int nBt = (nB + 31) & ~31;   // whole pairs of 16-column tiles
+    const bool live = __builtin_amdgcn_readfirstlane(row_base + FP_WROWS * w < nA ? 1 : 0) != 0;
+    for (int j = tid; j < nBt; j += blockDim.x) s_pb[j] = 128 * ((j < nB ? popc_row(Bp + (long long)j * 32) : 256) + 256);
+    {
+        const int row = row_base + tid;
+        if (tid < FP_ROWS) s_pa[tid] = row < nA ? popc_row(Ap + (long long)row * 32) : 0;
+    }
+    i4v af[FP_RT][2];
+#pragma unroll
+    for (int rt = 0; rt < FP_RT; rt++) {
+        const int row = min(row_base + FP_WROWS * w + 16 * rt + c16, nA - 1);
+        const uint2 v = *reinterpret_cast<const uint2*>(Ap + (long long)row * 32 + 8 * g);
+        af[rt][0] = expand32_nib(v.x, FP4_NEG4);
+        af[rt][1] = expand32_nib(v.y, FP4_NEG4);
+    }
+    __syncthreads();
+    uint32_t bk[FP_RT][4], sk[FP_RT][4], lb[FP_RT][4], ls[FP_RT][4];
+#pragma unroll
+    for (int rt = 0; rt < FP_RT; rt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) bk[rt][r] = sk[rt][r] = 0xffffffffu;
+    // Column tiles of 16, consumed in pairs.  Wavefront w expands k-step (w & 1) of tile (w >> 1) of
+    // the next pair into an LDS double buffer while this pair is consumed, one barrier per pair.
+    i4v* xb = reinterpret_cast<i4v*>(mm_sm + ((FP_ROWS + nBt + 16 + 3) & ~3));   // [2][2][2][64]
+    const int xt = w >> 1, xs = w & 1;
+    auto ldb = [&](int jj) -> uint32_t {
+        return jj < nB ? *reinterpret_cast<const uint32_t*>(Bp + (long long)jj * 32 + 8 * g + 4 * xs) : 0u;
+    };
+    xb[((0 * 2 + xt) * 2 + xs) * 64 + lane] = expand32_nib(ldb(16 * xt + c16), FP4_ONE);
+    uint32_t bn = ldb(32 + 16 * xt + c16);
+    __syncthreads();
+    for (int c0 = 0; c0 < nB; c0 += MM_CHUNK) {
+#pragma unroll
+        for (int rt = 0; rt < FP_RT; rt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) lb[rt][r] = ls[rt][r] = 0xffffffffu;
+        const int c1 = min(nB, c0 + MM_CHUNK);
+        for (int j0 = c0; j0 < c1; j0 += 32) {
+            const int cur = (j0 >> 5) & 1;
+            if (j0 + 32 < nB) {   // block-uniform
+                xb[(((cur ^ 1) * 2 + xt) * 2 + xs) * 64 + lane] = expand32_nib(bn, FP4_ONE);
+                bn = ldb(j0 + 64 + 16 * xt + c16);
+            }
+            const int t = (j0 - c0) >> 4;
+#pragma unroll
+            for (int tt = 0; tt < 2; tt++) {
+                if (!live) break;   // wavefront-uniform
+                const float ci = (float)(s_pb[j0 + 16 * tt + c16] + t + tt);
+                const f4v cinit = {ci, ci, ci, ci};
+                const i4v b0 = xb[((cur * 2 + tt) * 2 + 0) * 64 + lane];
+                const i4v b1 = xb[((cur * 2 + tt) * 2 + 1) * 64 + lane];
+#pragma unroll
+                for (int rt = 0; rt < FP_RT; rt++) {
+                    f4v acc = mfma_fp4(af[rt][0], b0, cinit);
+                    acc = mfma_fp4(af[rt][1], b1, acc);
+                    const float sv[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t key = __float_as_uint(sv[r]);   // >= 0: bits order as values
+                        const uint32_t nb = min(lb[rt][r], key);
+                        ls[rt][r] = umed3_after(lb[rt][r], key, ls[rt][r], nb);
+                        lb[rt][r] = nb;
+                    }
+                }
+            }
+            __syncthreads();   // pair expanded into `cur ^ 1`; buffer `cur` free for the pair after
+        }
+        // the chunk's top-2 as global keys (chunk keys back to integers first)
+        const uint32_t jb = (uint32_t)(c0 + c16);
+#pragma unroll
+        for (int rt = 0; rt < FP_RT; rt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                auto glob = [&](uint32_t kb) {
+                    if (kb == 0xffffffffu) return kb;
+                    const uint32_t k = (uint32_t)__uint_as_float(kb);
+                    return ((k >> 7) << 16) | (jb + 16 * (k & 127u));
+                };
+                const uint32_t b2 = glob(lb[rt][r]), s2v = glob(ls[rt][r]);
+                if (MULTI) {
+                    sk[rt][r] = min(min(sk[rt][r], s2v), max(bk[rt][r], b2));
+                    bk[rt][r] = min(bk[rt][r], b2);
+                } else {
+                    bk[rt][r] = b2;
+                    sk[rt][r] = s2v;
+                }
+            }
+        if (!MULTI) break;
+    }
+#pragma unroll
+    for (int rt = 0; rt < FP_RT; rt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            uint32_t b1 = bk[rt][r], s1 = sk[rt][r];
+            auto merge = [&](uint32_t b2, uint32_t s2v) {
+                s1 = min(min(s1, s2v), max(b1, b2));
+                b1 = min(b1, b2);
+            };
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0xB1, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xf, 0xf, false));
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0x4E, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x4E, 0xf, 0xf, false));
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0x124, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x124, 0xf, 0xf, false));
+            merge((uint32_t)__builtin_amdgcn_update_dpp(0, (int)b1, 0x128, 0xf, 0xf, false),
+                  (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0x128, 0xf, 0xf, false));
+            const int row = row_base + FP_WROWS * w + 16 * rt + 4 * g + r;
+            if (c16 == 0 && row < nA) {
+                const int pa = s_pa[FP_WROWS * w + 16 * rt + 4 * g + r];
+                const int bdr = (int)(b1 >> 16) - 256 + pa, sdr = (int)(s1 >> 16) - 256 + pa;
+                const int bd = bdr >= 256 ? 256 : bdr;
+                const int bi = bdr >= 256 ? -1 : (int)(b1 & 0xffffu);
+                const int sd = sdr >= 256 ? 256 : sdr;
+                const long long o = (long long)p * strideA + row;
+                if (best_idx) best_idx[o] = bi;
+                if (best) best[o] = bd;
+                if (second) second[o] = sd;
+                if (match) match[o] = (bd <= th_low && (float)bd < nnratio * (float)sd) ? bi : -1;
+            }
+        }
+}
+
+static int mm_fp4() {   // ORBM_FP4=0 selects the i8 kernel (read per launch: tests switch it)
+    const char* e = getenv("ORBM_FP4");
+    return e ? atoi(e) : 1;
+}
+
 static void launch_top2(const uint8_t* A, const int32_t* nA_arr, int nA_fixed, int strideA, const uint8_t* B,
                         const int32_t* nB_arr, int nB_fixed, int strideB, const int32_t* pair_b, int n_pairs,
                         float nnratio, int th_low, int32_t* bi, int32_t* bd, int32_t* sd, int32_t* mt,
                         hipStream_t st) {
-    const size_t lds = (size_t)(((MM_ROWS + ((strideB + 31) & ~31) + 16 + 3) & ~3) + 2 * 2 * 4 * 64 * 4) * sizeof(int);
-    auto kern = strideB <= MM_CHUNK ? hamming_top2_mfma_kernel<false> : hamming_top2_mfma_kernel<true>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)((strideA + MM_ROWS - 1) / MM_ROWS), (unsigned)n_pairs),
+    const bool fp4 = mm_fp4() != 0;
+    const int rows = fp4 ? FP_ROWS : MM_ROWS;
+    const size_t lds = (size_t)(((rows + ((strideB + 31) & ~31) + 16 + 3) & ~3) + 2 * 2 * (fp4 ? 2 : 4) * 64 * 4) * sizeof(int);
+    auto kern = fp4 ? (strideB <= MM_CHUNK ? hamming_top2_fp4_kernel<false> : hamming_top2_fp4_kernel<true>)
+                    : (strideB <= MM_CHUNK ? hamming_top2_mfma_kernel<false> : hamming_top2_mfma_kernel<true>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((strideA + rows - 1) / rows), (unsigned)n_pairs),
                        dim3(256), lds, st, A, nA_arr, nA_fixed, strideA, B, nB_arr, nB_fixed, strideB, pair_b,
                        nnratio, th_low, bi, bd, sd, mt);
 }

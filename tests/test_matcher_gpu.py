@@ -31,6 +31,27 @@ def test_bf_match_random(oracle, nA, nB):
         assert np.array_equal(g, e)
 
 
+@pytest.mark.parametrize("fp4", ["0", "1"])
+@pytest.mark.parametrize("nA,nB", [(1, 1), (257, 513), (2000, 2000), (300, 2049), (100, 4500)])
+def test_bf_match_both_matrix_paths(oracle, monkeypatch, fp4, nA, nB):
+    """The FP4 block-scaled MFMA kernel (default) and the i8 MFMA kernel (ORBM_FP4=0) are both exact:
+    random descriptors with best / second ties, all-ones and all-zeros rows (distance 0 and 256)."""
+    monkeypatch.setenv("ORBM_FP4", fp4)
+    rng = np.random.default_rng(nA * 3 + nB)
+    A = rand_desc(rng, nA)
+    B = rand_desc(rng, nB)
+    if nB > 10 and nA > 6:
+        B[7] = B[3]
+        A[:5] = B[3] ^ np.uint8(1)
+        A[5] = 0xFF
+        B[9] = 0xFF
+        A[6] = 0
+    got = ORBmatcher(0.6, False).MatchBruteForce(A, B)
+    exp = oracle.bf_match(A, B)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+
+
 @pytest.mark.parametrize("nA,nB", [(300, 2048), (300, 2049), (100, 4500)])
 def test_bf_match_chunked(oracle, nA, nB):
     """More than 2048 columns: the chunked kernel carries the top-2 across 2048-column chunks.
