@@ -36,7 +36,7 @@ constexpr int MAX_ZONE = 64;            // max FAST detection-zone side (cellw <
 constexpr int MAX_ROOTS = 32;
 constexpr int PATCH = 43;               // raw neighbourhood: +-21 (rBRIEF reach 18 + blur 3)
 constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
-constexpr int HBS = HBLUR_W + 1;        // LDS row stride of the blurred rows (u16): 19 dwords, dword-aligned rows
+constexpr int HBS = 40;                 // LDS row stride of the blurred rows (u16): 20 dwords, 8-byte aligned rows
 
 __constant__ float c_pattern[1024] = {   // bit_pattern_31_ (:142-400) as floats (the samples' operands)
 #include "orb_pattern31.inc"
@@ -2033,7 +2033,31 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return i;
 }
 
-constexpr int RS = 44;   // LDS raw-patch row stride
+constexpr int RS = 48;   // LDS raw-patch row stride (16-byte aligned rows for the blur's b128 reads)
+
+// Horizontal Q8 blur as v_mfma_i32_16x16x64_i8 products C[m][n] = sum_k A[m][k] B[k][n]: m = blurred
+// column, n = patch row, k = raw column; A = the 7-tap Toeplitz band A[m][k] = K[k - m]
+// (K = 18 34 48 56 48 34 18), B = raw pixels as i8 (p - 128; sum K = 256, so the accumulator starts
+// at 128 * 256).  Lane l holds A rows m = l % 16 (+16 mt), k = 16 (l / 16) .. +15 — the same k
+// split as its B bytes, so the hardware's k order inside a lane group does not matter.
+struct HBlurA { uint32_t v[3][64][4]; };   // [m tile][lane][dword]
+constexpr HBlurA make_hblur_a() {
+    HBlurA t{};
+    const int K[7] = {18, 34, 48, 56, 48, 34, 18};
+    for (int mt = 0; mt < 3; mt++)
+        for (int l = 0; l < 64; l++)
+            for (int d = 0; d < 4; d++) {
+                uint32_t w = 0;
+                for (int b = 0; b < 4; b++) {
+                    const int o = 16 * (l >> 4) + 4 * d + b - (l & 15) - 16 * mt;
+                    if (o >= 0 && o < 7) w |= (uint32_t)K[o] << (8 * b);
+                }
+                t.v[mt][l][d] = w;
+            }
+    return t;
+}
+__constant__ HBlurA c_hblur_a = make_hblur_a();
+typedef int i4v __attribute__((ext_vector_type(4)));
 
 #ifdef ORB_DESC_STAMPS
 // diagnostic build: phase stamps of every 16th describe wavefront (8 words each)
@@ -2046,12 +2070,10 @@ __device__ unsigned long long g_desc_stamps[1024 * 8];
 #define DESC_STAMP(k) do {} while (0)
 #endif
 
-// One workgroup = one wavefront = one kept keypoint.
-constexpr int DESC_KPW = 1;                               // keypoints per wavefront
-constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords per raw-patch row (RS = 4 * 11)
+// One workgroup = one wavefront = one selection slot (a kept keypoint or an empty slot).
+constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per raw-patch row
 
-// One wavefront per DESC_KPW consecutive output keypoints of a frame (output order = level-major
-// list order); waves past the frame's total exit at once.
+// One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
 __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
                                                       int in_step, const uint8_t* __restrict__ pyr,
                                                       const uint32_t* __restrict__ sel,
@@ -2060,30 +2082,33 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                                                       int cap) {
     // the raw patch R is dead once every lane holds its row for the horizontal blur (one
     // wavefront: its LDS reads complete before its later writes), so the blurred rows Hb reuse it
-    __shared__ __attribute__((aligned(16))) uint16_t Hb[PATCH * HBS];
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[48 * HBS];   // 43 blurred rows + 5 rows of blur slack
     uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
-    static_assert(PATCH * RS <= PATCH * HBS * 2, "R must fit in Hb");
+    static_assert(47 * RS + 64 <= 48 * HBS * 2, "R (and the blur's reads of rows 43..47) must fit in Hb");
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
-    const int wslot = lb % gridDim.x;
-    const int* cnt = sel_cnt + f * g.nlevels;
-    int total = 0;
-    for (int q = 0; q < g.nlevels; q++) total += cnt[q];
-    if (wslot == 0 && lane == 0) counts[f] = total;
-    for (int kk = 0; kk < DESC_KPW; kk++) {
-    const int oidx = wslot * DESC_KPW + kk;
-    if (oidx >= total || oidx >= cap) break;
-    int l = 0, lbase = 0;
-    while (l + 1 < g.nlevels && oidx >= lbase + cnt[l]) {
-        lbase += cnt[l];
-        l++;
-    }
+    const int s = lb % gridDim.x;   // selection slot (level-major, out_cap slots per level)
+    int l = 0;
+    while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_base) l++;
     const LevelDev& L = g.lv[l];
-    const int s = L.out_base + (oidx - lbase);
+    // the slot's keypoint and the frame's per-level counts in one round trip (both addresses are
+    // known from the slot)
+    const uint32_t k = sel[(long long)f * g.out_frame + s];
+    const int* cnt = sel_cnt + f * g.nlevels;
+    int total = 0, lbase = 0;
+    for (int q = 0; q < g.nlevels; q++) {
+        const int c = cnt[q];
+        total += c;
+        if (q < l) lbase += c;
+    }
+    if (s == 0 && lane == 0) counts[f] = total;
+    const int i = s - L.out_base;
+    if (i >= cnt[l]) return;   // slot past the level's kept count
+    const int oidx = lbase + i;   // output order: level-major list order
+    if (oidx >= cap) return;
     DESC_STAMP(0);
 
-    const uint32_t k = sel[(long long)f * g.out_frame + s];
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
     int step;
     const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
@@ -2159,25 +2184,41 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const float angle = fast_atan2_dev((float)m01, (float)m10);
     DESC_STAMP(2);
 
-    // horizontal Q8 blur, one row per lane, two columns per packed-u16 op: P(j) = (v[j], v[j+1]) is
-    // one v_perm of the row's dwords, and 18(P0+P6) + 34(P1+P5) + 48(P2+P4) + 56 P3 <= 65280 fits u16.
-    if (lane < PATCH) {
-        uint32_t w[PATCH_DW + 1];
+    // horizontal Q8 blur on the matrix cores (c_hblur_a): 3 x 3 tiles of 16 blurred columns x 16
+    // rows; lane (n, g) of tile (mt, nt) gets columns 16 mt + 4 g .. +3 of row 16 nt + n.  Every B
+    // read of R is issued before the first Hb write (R aliases Hb; one wavefront's LDS operations
+    // complete in order).  Rows past 42 (stored into slack rows) and columns past 36 are computed
+    // from neighbouring bytes and never read; columns past 39 are not stored.
+    {
+        const int n = lane & 15, g = lane >> 4;
+        i4v bfr[3], afr[3];
 #pragma unroll
-        for (int d = 0; d < PATCH_DW; d++) w[d] = *reinterpret_cast<const uint32_t*>(&R[lane * RS + 4 * d]);
-        w[PATCH_DW] = 0;
-        // out(c) = [18 34 48 56] . v[c..c+3] + [48 34 18 0] . v[c+4..c+7]: two v_dot4_u32_u8 on the
-        // 4-byte windows of the row (a window at byte j is one v_alignbyte of the row's dwords)
-        auto W = [&](int j) -> uint32_t {
-            return (j & 3) ? __builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], j & 3) : w[j >> 2];
+        for (int nt = 0; nt < 3; nt++) {
+            bfr[nt] = *reinterpret_cast<const i4v*>(&R[(n + 16 * nt) * RS + 16 * g]);
+            bfr[nt] ^= (int)0x80808080u;   // u8 -> i8 (p - 128)
+        }
+#pragma unroll
+        for (int mt = 0; mt < 3; mt++) afr[mt] = *reinterpret_cast<const i4v*>(c_hblur_a.v[mt][lane]);
+        const i4v cinit = {128 * 256, 128 * 256, 128 * 256, 128 * 256};
+        i4v acc[3][3];   // all nine products first: their results are not waited on one at a time
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+            for (int mt = 0; mt < 3; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+        auto put = [&](int nt, int mt) {
+            uint2 pk;
+            pk.x = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].y, (uint32_t)acc[nt][mt].x, 0x05040100u);
+            pk.y = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].w, (uint32_t)acc[nt][mt].z, 0x05040100u);
+            *reinterpret_cast<uint2*>(&Hb[(16 * nt + n) * HBS + 16 * mt + 4 * g]) = pk;   // rows 43..47: slack
         };
-        const uint32_t T0 = 18u | 34u << 8 | 48u << 16 | 56u << 24, T1 = 48u | 34u << 8 | 18u << 16;
-        uint32_t* hrow = reinterpret_cast<uint32_t*>(&Hb[lane * HBS]);
 #pragma unroll
-        for (int c = 0; c < HBLUR_W; c += 2) {
-            const uint32_t o0 = __builtin_amdgcn_udot4(W(c + 4), T1, __builtin_amdgcn_udot4(W(c), T0, 0u, false), false);
-            const uint32_t o1 = __builtin_amdgcn_udot4(W(c + 5), T1, __builtin_amdgcn_udot4(W(c + 1), T0, 0u, false), false);
-            hrow[c >> 1] = __builtin_amdgcn_perm(o1, o0, 0x05040100u);   // (o0, o1) as u16; column 37 is padding
+        for (int nt = 0; nt < 3; nt++) {
+            put(nt, 0);
+            put(nt, 1);
+        }
+        if (g < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) put(nt, 2);
         }
     }
     __syncthreads();
@@ -2228,8 +2269,6 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         reinterpret_cast<float*>(kps + o)[lane] = fv;
     }
     DESC_STAMP(6);
-    __syncthreads();   // R / Hb are rewritten by the next keypoint
-    }   // keypoints of this wavefront
 }
 
 __global__ __launch_bounds__(256) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
@@ -2621,7 +2660,7 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         quadtree(0, g.nlevels, st);
     }
     {
-    launch_timed(h, 3, describe_kernel, dim3((unsigned)((g.out_frame + DESC_KPW - 1) / DESC_KPW), (unsigned)F), dim3(64),
+    launch_timed(h, 3, describe_kernel, dim3((unsigned)g.out_frame, (unsigned)F), dim3(64),
                        0u, st, g,
                        d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
     }

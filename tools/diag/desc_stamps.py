@@ -14,7 +14,15 @@ from orb_slam2_refactored_amd._lib import lib  # noqa: E402
 from orb_slam2_refactored_amd.synth import synth_image  # noqa: E402
 
 F = 128
-frames = torch.from_numpy(np.stack([synth_image(i % 16, 1280, 720) for i in range(F)])).cuda()
+kind = sys.argv[1] if len(sys.argv) > 1 else "pan"
+if kind == "pan":
+    from orb_slam2_refactored_amd.synth import pan_sequence
+    pool = pan_sequence(0, 1280, 720, 16)
+    frames = torch.from_numpy(np.stack([pool[i % 16] for i in range(F)])).cuda()
+else:
+    from orb_slam2_refactored_amd.synth import textured_image
+    gen = textured_image if kind == "textured" else synth_image
+    frames = torch.from_numpy(np.stack([gen(i % 16, 1280, 720) for i in range(F)])).cuda()
 ex = ORBextractor(ORBextractor.Parameters(nfeatures=2000))
 for _ in range(3):
     ex.extract_batch_device(frames)
