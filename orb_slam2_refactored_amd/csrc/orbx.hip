@@ -2114,30 +2114,51 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
     // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101)
     if (kx >= 21 && ky >= 21 && kx + 21 + 8 < L.w && ky + 21 < L.h) {
-        // interior: 16 lanes per row (dword d of row 4k + lane/16), 11 row groups; the group's row
-        // address is wave-uniform, so a load costs its realignment only (v_alignbyte of the aligned
-        // dword pair); all loads in flight before the LDS stores
+        // interior: 16 lanes per row (dword d of row 4k + lane/16), 11 row groups; all loads in
+        // flight before the LDS stores
         constexpr int NG = (PATCH + 3) / 4;
         const uint8_t* base = img + (long long)(ky - 21) * step + (kx - 21);
         const int roff = lane >> 4, d = min(lane & 15, PATCH_DW - 1);
-        const int loff = roff * step + 4 * d;
-        uint32_t lo[NG], hi[NG];
-        int sh[NG];
+        uint32_t v[NG];
+        if ((step & 3) == 0) {
+            // dword-multiple row step (every pyramid level; level 0 unless the caller's step is
+            // odd): one wave-uniform realignment, buffer loads off a scalar resource with a per-lane
+            // constant voffset and a per-group soffset (no address VALU).  The resource ends at the
+            // level's last pixel: row 43 of the last group (never stored) may lie past it and reads 0.
+            const int m = __builtin_amdgcn_readfirstlane((int)(reinterpret_cast<uintptr_t>(base) & 3u));
+            const int nrec = (L.h - 1 - (ky - 21)) * step + L.w - (kx - 21) + m;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base - m), 0, nrec, 0x00020000);
+            const int voff = roff * step + 4 * d;
 #pragma unroll
-        for (int k = 0; k < NG; k++) {
-            const uint8_t* gb = base + (long long)min(4 * k, PATCH - 1 - roff) * step;   // rows <= 42
-            const uint8_t* pbyte = gb + loff;
-            const int m = (int)(reinterpret_cast<uintptr_t>(pbyte) & 3);
-            const uint32_t* pw = reinterpret_cast<const uint32_t*>(pbyte - m);
-            lo[k] = pw[0];
-            hi[k] = pw[1];
-            sh[k] = m;
+            for (int k = 0; k < NG; k++) {
+                const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 4 * k * step, 0);
+                v[k] = __builtin_amdgcn_alignbyte(t[1], t[0], m);
+            }
+        } else {
+            // odd caller step: a per-lane realignment (v_alignbyte of the aligned dword pair)
+            const int loff = roff * step + 4 * d;
+            uint32_t lo[NG], hi[NG];
+            int sh[NG];
+#pragma unroll
+            for (int k = 0; k < NG; k++) {
+                const uint8_t* gb = base + (long long)min(4 * k, PATCH - 1 - roff) * step;   // rows <= 42
+                const uint8_t* pbyte = gb + loff;
+                const int m = (int)(reinterpret_cast<uintptr_t>(pbyte) & 3);
+                const uint32_t* pw = reinterpret_cast<const uint32_t*>(pbyte - m);
+                lo[k] = pw[0];
+                hi[k] = pw[1];
+                sh[k] = m;
+            }
+#pragma unroll
+            for (int k = 0; k < NG; k++) v[k] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
         }
+        static_assert(4 * (NG - 1) + 3 == PATCH, "the last row group holds three patch rows");
         if ((lane & 15) < PATCH_DW) {
+            uint32_t* rrow = reinterpret_cast<uint32_t*>(&R[roff * RS + 4 * d]);
 #pragma unroll
-            for (int k = 0; k < NG; k++)
-                if (4 * k + roff < PATCH)
-                    *reinterpret_cast<uint32_t*>(&R[(4 * k + roff) * RS + 4 * d]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+            for (int k = 0; k < NG - 1; k++) rrow[k * RS] = v[k];   // row 4k + roff: (4k + roff) * RS / 4 dwords
+            if (roff < 3) rrow[(NG - 1) * RS] = v[NG - 1];
         }
     } else if (lane < PATCH) {
         const int xx = reflect101(kx - 21 + lane, L.w);
