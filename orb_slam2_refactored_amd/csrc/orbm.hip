@@ -419,6 +419,16 @@ static int mm_fp4() {   // ORBM_FP4=0 selects the i8 kernel (read per launch: te
     return e ? atoi(e) : 1;
 }
 
+static int tri_split() {   // kf2 column parts per query block of the matrix-core path (ORBM_TRI_SPLIT)
+    const char* e = getenv("ORBM_TRI_SPLIT");
+    return e ? std::max(1, std::min(8, atoi(e))) : 1;
+}
+
+static int tri_mm() {   // ORBM_TRI_MM=0 selects the per-lane scan for the all-pairs triangulation search
+    const char* e = getenv("ORBM_TRI_MM");
+    return e ? atoi(e) : 1;
+}
+
 static void launch_top2(const uint8_t* A, const int32_t* nA_arr, int nA_fixed, int strideA, const uint8_t* B,
                         const int32_t* nB_arr, int nB_fixed, int strideB, const int32_t* pair_b, int n_pairs,
                         float nnratio, int th_low, int32_t* bi, int32_t* bd, int32_t* sd, int32_t* mt,
@@ -607,26 +617,52 @@ __device__ __forceinline__ int hamming8(const uint4& a0, const uint4& a1, const 
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-constexpr int TRI_CHUNK = 256;
+constexpr int TRI_SEG = 256;   // kf2 candidates per workgroup
 
 // Single BoW node holding every keypoint of both keyframes (no vocabulary): every
-// query scans kf2 in ascending index.  One lane per query, 256 queries per workgroup; kf2's
-// descriptors are staged through LDS in chunks of 256 and read as wavefront broadcasts.
-__global__ __launch_bounds__(256) void tri_all_kernel(TriArgs a, TriTables t) {
-    __shared__ uint4 sd[TRI_CHUNK * 2];
-    __shared__ uint32_t sv[TRI_CHUNK / 32];
+// query scans all of kf2.  The reference keeps the gate-passing candidate of minimum distance
+// <= TH_LOW and, among equal distances, the largest index (its ascending scan replaces the best on
+// d <= bestDist: the last minimum wins) — an order-independent minimum of the key
+// (d << 16) | (0xFFFF - j).  So kf2 is cut into segments of 256 candidates, one workgroup per
+// (256 queries, segment, pair) scans its segment with one lane per query (descriptors and gate
+// operands staged in LDS, read as wavefront broadcasts) and merges its best key into match12 with
+// atomicMin; tri_finalize_kernel turns the keys into indices.
+__global__ __launch_bounds__(256) void tri_all_kernel(TriArgs a, TriTables t, int nqb) {
+    __shared__ uint4 sd[TRI_SEG * 2];
+    __shared__ float4 sk[TRI_SEG];   // x, y, octave bits, stereo flag
+    __shared__ uint32_t sv[TRI_SEG / 32];
     const int p = blockIdx.y, tid = threadIdx.x;
+    const int qb = blockIdx.x % nqb, c0 = (blockIdx.x / nqb) * TRI_SEG;
     const int f1 = a.frame1 ? a.frame1[p] : p, f2 = a.frame2 ? a.frame2[p] : p;
     const int n1 = a.counts1[f1], n2 = a.counts2[f2];
-    if (blockIdx.x * 256 >= n1) return;   // block-uniform
-    const int i1 = blockIdx.x * 256 + tid;
+    if (qb * 256 >= n1 || c0 >= n2) return;   // block-uniform
+    const int i1 = qb * 256 + tid;
     const long long g1 = (long long)f1 * a.cap1 + i1;
     const bool in = i1 < n1;
     const bool st1 = in && a.ur1 && a.ur1[g1] >= 0;
     const bool act = in && !(a.mp1 && a.mp1[g1]) && (!a.only_stereo || st1);
+    const long long base2 = (long long)f2 * a.cap2;
+    {
+        const int j = c0 + tid;
+        bool v = false;
+        if (j < n2) {
+            const long long g2 = base2 + j;
+            sd[2 * tid] = reinterpret_cast<const uint4*>(a.desc2)[2 * g2];
+            sd[2 * tid + 1] = reinterpret_cast<const uint4*>(a.desc2)[2 * g2 + 1];
+            const orbx_keypoint& kp = a.kps2[g2];
+            const bool st2 = a.ur2 && a.ur2[g2] >= 0;
+            sk[tid] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), st2 ? 1.f : 0.f);
+            v = !(a.mp2 && a.mp2[g2]) && (!a.only_stereo || st2);
+        }
+        const uint64_t bal = __ballot(v);
+        if ((tid & 63) == 0) {
+            sv[2 * (tid >> 6)] = (uint32_t)bal;
+            sv[2 * (tid >> 6) + 1] = (uint32_t)(bal >> 32);
+        }
+    }
     uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
     float la = 0, lb = 0, lc = 0;
-    if (in) {
+    if (act) {
         a0 = reinterpret_cast<const uint4*>(a.desc1)[2 * g1];
         a1 = reinterpret_cast<const uint4*>(a.desc1)[2 * g1 + 1];
         const float x1 = a.kps1[g1].x, y1 = a.kps1[g1].y;
@@ -636,45 +672,243 @@ __global__ __launch_bounds__(256) void tri_all_kernel(TriArgs a, TriTables t) {
         lc = x1 * F[2] + y1 * F[5] + F[8];
     }
     const float ep2x = a.ep2[2 * p], ep2y = a.ep2[2 * p + 1];
-    const long long base2 = (long long)f2 * a.cap2;
+    __syncthreads();
+    if (!act) return;
     int bd = 50, bi = -1;   // TH_LOW
-    for (int c0 = 0; c0 < n2; c0 += TRI_CHUNK) {
-        {
-            const int j = c0 + tid;
-            bool v = false;
-            if (j < n2) {
-                const long long g2 = base2 + j;
-                sd[2 * tid] = reinterpret_cast<const uint4*>(a.desc2)[2 * g2];
-                sd[2 * tid + 1] = reinterpret_cast<const uint4*>(a.desc2)[2 * g2 + 1];
-                v = !(a.mp2 && a.mp2[g2]) && (!a.only_stereo || (a.ur2 && a.ur2[g2] >= 0));
-            }
-            const uint64_t bal = __ballot(v);
-            if ((tid & 63) == 0) {
-                sv[2 * (tid >> 6)] = (uint32_t)bal;
-                sv[2 * (tid >> 6) + 1] = (uint32_t)(bal >> 32);
+    // kf2 descriptors through the scalar path (uniform addresses in the constant address space:
+    // s_load_dwordx8, XORed as SGPR operands), four candidates per batch; the validity mask and
+    // the gate operands only on the rare d <= bd branch
+    typedef const uint32_t __attribute__((address_space(4))) cu32;
+    const cu32* D2 = (const cu32*)(a.desc2 + (base2 + c0) * 32);
+    const int m = min(TRI_SEG, n2 - c0);
+    auto ham = [&](const cu32* dk) {
+        return __popc(a0.x ^ dk[0]) + __popc(a0.y ^ dk[1]) + __popc(a0.z ^ dk[2]) + __popc(a0.w ^ dk[3]) +
+               __popc(a1.x ^ dk[4]) + __popc(a1.y ^ dk[5]) + __popc(a1.z ^ dk[6]) + __popc(a1.w ^ dk[7]);
+    };
+    auto consider = [&](int k, int d) {
+        if (d > bd) return;
+        if (!((sv[k >> 5] >> (k & 31)) & 1u)) return;
+        const float4 kp2 = sk[k];
+        if (tri_gates(la, lb, lc, st1, kp2.w != 0.f, kp2.x, kp2.y, __float_as_int(kp2.z), ep2x, ep2y, t)) {
+            bi = c0 + k;
+            bd = d;
+        }
+    };
+    int k = 0;
+    for (; k + 4 <= m; k += 4) {
+        const int d0 = ham(D2 + 8 * k), d1 = ham(D2 + 8 * k + 8), d2 = ham(D2 + 8 * k + 16), d3 = ham(D2 + 8 * k + 24);
+        consider(k, d0);
+        consider(k + 1, d1);
+        consider(k + 2, d2);
+        consider(k + 3, d3);
+    }
+    for (; k < m; k++) consider(k, ham(D2 + 8 * k));
+    if (bi >= 0)
+        atomicMin(reinterpret_cast<unsigned*>(a.match12) + (long long)p * a.cap1 + i1, ((unsigned)bd << 16) | (0xFFFFu - (unsigned)bi));
+}
+
+// The all-pairs search on the FP4 matrix path (hamming_top2_fp4_kernel's tiling): a workgroup owns
+// 256 queries of one pair and streams all of kf2 through the MFMA.  A key 128 S (S = d - |a| + 256,
+// the accumulator started at 128 (|b| + 256)) below the row's threshold 128 (307 - |a|) is a
+// candidate with d <= TH_LOW; it is appended to the wavefront's LDS event pool as (row, d, j)
+// (slots from a wave-uniform count and the lane's rank in the ballot: no atomics).  After the
+// stream the wavefront's 64 lanes share its events: a candidate whose key (d << 16) | (0xFFFF - j)
+// is below the row's current best is checked for validity and the gates and merged into the row's
+// best with an LDS atomicMin (the order-independent form of the reference's scan, see
+// tri_all_kernel).  Rows whose events did not fit are rescanned exactly by the whole workgroup.
+// Rows the reference skips (a MapPoint, onlyStereo) get threshold 0: no events, result -1.
+#ifndef TRI_POOL_DEF
+#define TRI_POOL_DEF 1024
+#endif
+#ifndef TRI_RT_DEF
+#define TRI_RT_DEF 4
+#endif
+constexpr int TRI_POOL = TRI_POOL_DEF;   // events per wavefront
+constexpr int TRI_RT = TRI_RT_DEF;       // 16-row tiles per wavefront
+constexpr int TRI_WROWS = 16 * TRI_RT, TRI_ROWS = 4 * TRI_WROWS;
+__device__ __forceinline__ bool tri_valid2(const TriArgs& a, long long g2, bool* st2) {
+    *st2 = a.ur2 && a.ur2[g2] >= 0;
+    return !(a.mp2 && a.mp2[g2]) && (!a.only_stereo || *st2);
+}
+
+__global__ __launch_bounds__(256) void tri_mm_kernel(TriArgs a, TriTables t, int nsplit) {
+    extern __shared__ __attribute__((aligned(16))) int mm_sm[];   // row | best | ovf | pa | ev | xb | pb
+    float4* s_row = reinterpret_cast<float4*>(mm_sm);                  // la, lb, lc, st1 (per WG row)
+    uint32_t* s_best = reinterpret_cast<uint32_t*>(mm_sm + 4 * TRI_ROWS);
+    int* s_ovf = mm_sm + 5 * TRI_ROWS;
+    int* s_pa = mm_sm + 6 * TRI_ROWS;
+    uint32_t* s_ev = reinterpret_cast<uint32_t*>(mm_sm + 7 * TRI_ROWS);   // [4 waves][TRI_POOL]
+    i4v* xb = reinterpret_cast<i4v*>(mm_sm + 7 * TRI_ROWS + 4 * TRI_POOL);   // [2][2][2][64]
+    int* s_pb = mm_sm + 7 * TRI_ROWS + 4 * TRI_POOL + 2 * 2 * 2 * 64 * 4;
+    __shared__ int s_anyovf;
+    const int p = blockIdx.y;
+    const int f1 = a.frame1 ? a.frame1[p] : p, f2 = a.frame2 ? a.frame2[p] : p;
+    const int nA = a.counts1[f1], nB = a.counts2[f2];
+    const int row_base = (blockIdx.x / nsplit) * TRI_ROWS;
+    // this workgroup's kf2 columns [jlo, jhi) (a multiple of 32 wide except the last part)
+    const int span = ((nB + nsplit - 1) / nsplit + 31) & ~31;
+    const int jlo = (blockIdx.x % nsplit) * span, jhi = min(nB, jlo + span);
+    if (row_base >= nA || jlo >= jhi) return;   // block-uniform
+    const uint8_t* Ap = a.desc1 + (long long)f1 * a.cap1 * 32;
+    const uint8_t* Bp = a.desc2 + (long long)f2 * a.cap2 * 32;
+    const long long base2 = (long long)f2 * a.cap2;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c16 = lane & 15, g = lane >> 4;
+    const int jht = jlo + ((jhi - jlo + 31) & ~31);
+    const float ep2x = a.ep2[2 * p], ep2y = a.ep2[2 * p + 1];
+    for (int j = jlo + tid; j < jht; j += blockDim.x)   // columns past jhi: padding (S = 512, never an event)
+        s_pb[j - jlo] = 128 * ((j < jhi ? popc_row(Bp + (long long)j * 32) : 256) + 256);
+    if (tid < TRI_ROWS) {
+        const int row = row_base + tid;
+        int pa = -1;   // -1: no events for this row
+        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < nA) {
+            const long long g1 = (long long)f1 * a.cap1 + row;
+            const bool st1 = a.ur1 && a.ur1[g1] >= 0;
+            if (!(a.mp1 && a.mp1[g1]) && (!a.only_stereo || st1)) {
+                pa = popc_row(Ap + (long long)row * 32);
+                const float x1 = a.kps1[g1].x, y1 = a.kps1[g1].y;
+                const float* F = a.F12 + 9 * (long long)p;
+                rv = make_float4(x1 * F[0] + y1 * F[3] + F[6], x1 * F[1] + y1 * F[4] + F[7],
+                                 x1 * F[2] + y1 * F[5] + F[8], st1 ? 1.f : 0.f);   // l = x1' F12 (:391-393)
             }
         }
-        __syncthreads();
-        if (act) {
-            const int m = min(TRI_CHUNK, n2 - c0);
-            for (int k = 0; k < m; k++) {
-                if (!((sv[k >> 5] >> (k & 31)) & 1u)) continue;   // uniform (every lane reads the same k)
-                const int d = hamming8(a0, a1, sd[2 * k], sd[2 * k + 1]);
-                if (d > bd) continue;
-                const long long g2 = base2 + c0 + k;
-                const orbx_keypoint kp2 = a.kps2[g2];
-                const bool st2 = a.ur2 && a.ur2[g2] >= 0;
-                if (tri_gates(la, lb, lc, st1, st2, kp2.x, kp2.y, kp2.octave, ep2x, ep2y, t)) {
-                    bi = c0 + k;
-                    bd = d;
+        s_row[tid] = rv;
+        s_best[tid] = 0xffffffffu;
+        s_ovf[tid] = 0;
+        s_pa[tid] = pa;
+    }
+    if (tid == 0) s_anyovf = 0;
+    const bool live = __builtin_amdgcn_readfirstlane(row_base + TRI_WROWS * w < nA ? 1 : 0) != 0;
+    i4v af[TRI_RT][2];
+#pragma unroll
+    for (int rt = 0; rt < TRI_RT; rt++) {
+        const int row = min(row_base + TRI_WROWS * w + 16 * rt + c16, nA - 1);
+        const uint2 v = *reinterpret_cast<const uint2*>(Ap + (long long)row * 32 + 8 * g);
+        af[rt][0] = expand32_nib(v.x, FP4_NEG4);
+        af[rt][1] = expand32_nib(v.y, FP4_NEG4);
+    }
+    const int xt = w >> 1, xs = w & 1;
+    auto ldb = [&](int jj) -> uint32_t {
+        return jj < jhi ? *reinterpret_cast<const uint32_t*>(Bp + (long long)jj * 32 + 8 * g + 4 * xs) : 0u;
+    };
+    xb[((0 * 2 + xt) * 2 + xs) * 64 + lane] = expand32_nib(ldb(jlo + 16 * xt + c16), FP4_ONE);
+    uint32_t bn = ldb(jlo + 32 + 16 * xt + c16);
+    __syncthreads();
+    float thr[TRI_RT][4];   // 128 (307 - |a|): key < thr <=> d <= TH_LOW
+#pragma unroll
+    for (int rt = 0; rt < TRI_RT; rt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int pa = s_pa[TRI_WROWS * w + 16 * rt + 4 * g + r];
+            thr[rt][r] = pa < 0 ? 0.f : (float)(128 * (307 - pa));
+        }
+    int nev = 0;   // wave-uniform
+    uint32_t* ev = s_ev + w * TRI_POOL;
+    for (int j0 = jlo; j0 < jhi; j0 += 32) {
+        const int cur = ((j0 - jlo) >> 5) & 1;
+        if (j0 + 32 < jhi) {   // block-uniform
+            xb[(((cur ^ 1) * 2 + xt) * 2 + xs) * 64 + lane] = expand32_nib(bn, FP4_ONE);
+            bn = ldb(j0 + 64 + 16 * xt + c16);
+        }
+#pragma unroll
+        for (int tt = 0; tt < 2; tt++) {
+            if (!live) break;   // wavefront-uniform
+            const float ci = (float)s_pb[j0 - jlo + 16 * tt + c16];
+            const f4v cinit = {ci, ci, ci, ci};
+            const i4v b0 = xb[((cur * 2 + tt) * 2 + 0) * 64 + lane];
+            const i4v b1 = xb[((cur * 2 + tt) * 2 + 1) * 64 + lane];
+#pragma unroll
+            for (int rt = 0; rt < TRI_RT; rt++) {
+                f4v acc = mfma_fp4(af[rt][0], b0, cinit);
+                acc = mfma_fp4(af[rt][1], b1, acc);
+                const float kv[4] = {acc.x, acc.y, acc.z, acc.w};
+                const bool any = (kv[0] < thr[rt][0]) | (kv[1] < thr[rt][1]) | (kv[2] < thr[rt][2]) | (kv[3] < thr[rt][3]);
+                if (__builtin_amdgcn_read_exec() & __ballot(any)) {   // wavefront-uniform, rare
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const bool e = kv[r] < thr[rt][r];
+                        const uint64_t bal = __ballot(e);
+                        if (e) {
+                            const int rw = 16 * rt + 4 * g + r;   // row within the wavefront
+                            // d = S - 256 + |a|, |a| = 307 - thr / 128
+                            const int d = ((int)kv[r] >> 7) + 51 - ((int)thr[rt][r] >> 7);
+                            const int j = j0 + 16 * tt + c16;
+                            const int slot = nev + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                            if (slot < TRI_POOL) ev[slot] = ((uint32_t)rw << 22) | ((uint32_t)d << 16) | (uint32_t)j;
+                            else s_ovf[TRI_WROWS * w + rw] = 1;
+                        }
+                        nev += (int)__popcll(bal);
+                    }
                 }
             }
         }
-        __syncthreads();
+        __syncthreads();   // pair expanded into `cur ^ 1`; buffer `cur` free for the pair after
     }
-    if (in) a.match12[(long long)p * a.cap1 + i1] = bi;
-    const uint64_t got = __ballot(in && bi >= 0);
-    if ((tid & 63) == 0 && got) atomicAdd(a.nmatches + p, (int)__popcll(got));
+    // the wavefront's events, shared by its lanes: validity, gates, row best (LDS atomicMin)
+    for (int e = lane; e < min(nev, TRI_POOL); e += 64) {
+        const uint32_t v = ev[e];
+        const int rl = TRI_WROWS * w + (int)(v >> 22), d = (int)((v >> 16) & 63u), j = (int)(v & 0xffffu);
+        const uint32_t key = ((uint32_t)d << 16) | (0xffffu - (uint32_t)j);
+        if (key >= s_best[rl]) continue;
+        bool st2;
+        const long long g2 = base2 + j;
+        if (!tri_valid2(a, g2, &st2)) continue;
+        const float4 rv = s_row[rl];
+        const orbx_keypoint& kp2 = a.kps2[g2];
+        if (tri_gates(rv.x, rv.y, rv.z, rv.w != 0.f, st2, kp2.x, kp2.y, kp2.octave, ep2x, ep2y, t))
+            atomicMin(&s_best[rl], key);
+    }
+    if (nev > TRI_POOL && lane == 0) s_anyovf = 1;
+    __syncthreads();
+    if (s_anyovf) {   // block-uniform, rare: rows whose events did not fit, rescanned by the workgroup
+        for (int rl = 0; rl < TRI_ROWS; rl++) {
+            if (!s_ovf[rl]) continue;   // block-uniform
+            const int row = row_base + rl;
+            const float4 rv = s_row[rl];
+            const uint4 a0 = reinterpret_cast<const uint4*>(Ap)[2 * row], a1 = reinterpret_cast<const uint4*>(Ap)[2 * row + 1];
+            if (tid == 0) s_best[rl] = 0xffffffffu;
+            __syncthreads();
+            for (int j = jlo + tid; j < jhi; j += blockDim.x) {
+                const int d = hamming8(a0, a1, reinterpret_cast<const uint4*>(Bp)[2 * j], reinterpret_cast<const uint4*>(Bp)[2 * j + 1]);
+                if (d > 50) continue;
+                bool st2;
+                if (!tri_valid2(a, base2 + j, &st2)) continue;
+                const orbx_keypoint& kp2 = a.kps2[base2 + j];
+                if (tri_gates(rv.x, rv.y, rv.z, rv.w != 0.f, st2, kp2.x, kp2.y, kp2.octave, ep2x, ep2y, t))
+                    atomicMin(&s_best[rl], ((uint32_t)d << 16) | (0xffffu - (uint32_t)j));
+            }
+            __syncthreads();
+        }
+    }
+    const int row = row_base + tid;
+    bool got = false;
+    if (tid < TRI_ROWS && row < nA) {
+        const uint32_t best = s_best[tid];
+        got = best != 0xffffffffu;
+        if (nsplit > 1) {   // column parts merge their keys; tri_finalize_kernel decodes
+            if (got) atomicMin(reinterpret_cast<unsigned*>(a.match12) + (long long)p * a.cap1 + row, best);
+            return;
+        }
+        a.match12[(long long)p * a.cap1 + row] = got ? (int32_t)(0xffffu - (best & 0xffffu)) : -1;
+    }
+    if (nsplit > 1) return;
+    const uint64_t bal = __ballot(got);
+    if ((tid & 63) == 0 && bal) atomicAdd(a.nmatches + p, (int)__popcll(bal));
+}
+
+// match12 keys -> kf2 indices (-1 where no candidate passed), and the per-pair match count.
+__global__ __launch_bounds__(256) void tri_finalize_kernel(int32_t* __restrict__ match12, int cap1,
+                                                           int32_t* __restrict__ nmatches) {
+    const int p = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    bool got = false;
+    if (i < cap1) {
+        const unsigned key = reinterpret_cast<unsigned*>(match12)[(long long)p * cap1 + i];
+        got = key != 0xFFFFFFFFu;
+        match12[(long long)p * cap1 + i] = got ? (int32_t)(0xFFFFu - (key & 0xFFFFu)) : -1;
+    }
+    const uint64_t bal = __ballot(got);
+    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(nmatches + p, (int)__popcll(bal));
 }
 
 // General DBoW2 FeatureVectors (orbv_transform_batch_device layout): FeatureVectorIterator
@@ -895,8 +1129,30 @@ int orbm_search_for_triangulation_batch_device(const orbm_tri_batch* b, int32_t*
         ORB_HIP_TRY(hipMemsetAsync(d_match12, 0xff, (size_t)b->n_pairs * b->cap1 * 4, st));
         hipLaunchKernelGGL(tri_fv_kernel, dim3((unsigned)b->n_pairs), dim3(256), 0, st, a, t);
     } else {
-        hipLaunchKernelGGL(tri_all_kernel, dim3((unsigned)((b->cap1 + 255) / 256), (unsigned)b->n_pairs), dim3(256), 0,
-                           st, a, t);
+        ORB_CHECK_ARG(b->cap2 <= 65535, "cap2 must be <= 65535 for the all-pairs search");
+        if (tri_mm() && b->cap2 <= 8192) {   // matrix-core path
+            const int nsplit = tri_split();
+            const size_t lds = (size_t)(7 * TRI_ROWS + 4 * TRI_POOL + 2 * 2 * 2 * 64 * 4 + ((b->cap2 + 31) & ~31)) * 4;
+            const int nqb = (b->cap1 + TRI_ROWS - 1) / TRI_ROWS;
+            if (nsplit > 1) ORB_HIP_TRY(hipMemsetAsync(d_match12, 0xff, (size_t)b->n_pairs * b->cap1 * 4, st));
+            hipLaunchKernelGGL(tri_mm_kernel, dim3((unsigned)(nqb * nsplit), (unsigned)b->n_pairs), dim3(256), lds, st, a,
+                               t, nsplit);
+            ORB_HIP_TRY(hipGetLastError());
+            if (nsplit > 1) {
+                hipLaunchKernelGGL(tri_finalize_kernel, dim3((unsigned)((b->cap1 + 255) / 256), (unsigned)b->n_pairs),
+                                   dim3(256), 0, st, d_match12, b->cap1, d_nmatches);
+                ORB_HIP_TRY(hipGetLastError());
+            }
+            return ORB_OK;
+        }
+        // keys (d << 16) | (0xFFFF - j) merged with atomicMin from 0xFFFFFFFF (no candidate)
+        ORB_HIP_TRY(hipMemsetAsync(d_match12, 0xff, (size_t)b->n_pairs * b->cap1 * 4, st));
+        const int nqb = (b->cap1 + 255) / 256, nseg = (b->cap2 + TRI_SEG - 1) / TRI_SEG;
+        hipLaunchKernelGGL(tri_all_kernel, dim3((unsigned)(nqb * nseg), (unsigned)b->n_pairs), dim3(256), 0, st, a, t,
+                           nqb);
+        ORB_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(tri_finalize_kernel, dim3((unsigned)nqb, (unsigned)b->n_pairs), dim3(256), 0, st, d_match12,
+                           b->cap1, d_nmatches);
     }
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;

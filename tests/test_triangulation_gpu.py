@@ -14,6 +14,15 @@ from orb_slam2_refactored_amd.synth import KITTI, stereo_pair, stereo_tri_geomet
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["mm", "mm_split2", "scan"])
+def tri_path(request, monkeypatch):
+    """Both all-pairs kernels: the matrix-core event path (default; also with kf2 cut into two column
+    parts merged through match12 keys) and the per-lane segmented scan."""
+    monkeypatch.setenv("ORBM_TRI_MM", "0" if request.param == "scan" else "1")
+    monkeypatch.setenv("ORBM_TRI_SPLIT", "2" if request.param == "mm_split2" else "1")
+    return request.param
+
+
 def _oracle_pair(O, kps1, d1, n1, kps2, d2, n2, F12, ep2, scale, sigma2, ur1=None, ur2=None, mp1=None, mp2=None,
                  fv1=None, fv2=None, only_stereo=False):
     keep = O._Keep()
@@ -43,7 +52,7 @@ def _c3_batch(pairs, seed0):
     return ex, frames, kps, desc, cnt
 
 
-def test_c3_extracted_pairs(oracle):
+def test_c3_extracted_pairs(oracle, tri_path):
     """The C3 workload as written: extract L+R, single-node FeatureVector, uright = -1, no MapPoints,
     F12 / ep2 of the rectified rig (ep2 = (-inf, NaN): the epipole gate falls as in the reference)."""
     import torch
@@ -73,7 +82,7 @@ def test_c3_extracted_pairs(oracle):
     assert total > 400 * P   # stereo correspondences on the same rows
 
 
-def test_c3_masks_and_only_stereo(oracle):
+def test_c3_masks_and_only_stereo(oracle, tri_path):
     """uright (stereo keypoints skip the epipole gate; onlyStereo drops mono queries / candidates)
     and has_mappoint masks on both keyframes, with a finite epipole."""
     import torch
@@ -103,6 +112,41 @@ def test_c3_masks_and_only_stereo(oracle):
                                   ur1=ur[p], ur2=ur[q], mp1=mp[p], mp2=mp[q], only_stereo=only)
             assert np.array_equal(M[p, :N[p]], exp), (only, p)
             assert NM[p] == n and n > 0
+
+
+def test_c3_event_overflow(oracle, tri_path):
+    """Repeated descriptors: kf2 holds copies of four kf1 descriptors (and near copies), so those rows
+    see a candidate with d <= TH_LOW at every column and the matrix path's per-lane event lists
+    overflow (exact rescan of the marked rows); every other row keeps its events."""
+    import torch
+    P = 2
+    ex, frames, kps, desc, cnt = _c3_batch(P, 9400)
+    N = cnt.cpu().numpy()
+    D = desc.cpu().numpy().copy()
+    rng = np.random.default_rng(11)
+    for p in range(P):
+        q = P + p
+        n2 = N[q]
+        src = D[p, np.arange(n2) % 4]
+        flip = (rng.random((n2, 32)) < 0.02) * (1 << rng.integers(0, 8, (n2, 32)))
+        D[q, :n2] = np.where(rng.random((n2, 1)) < 0.5, src ^ flip.astype(np.uint8), D[q, :n2])
+    dt = torch.from_numpy(D).cuda()
+    F12, ep2 = stereo_tri_geometry()
+    ep2 = np.array([650.0, 190.0], np.float32)
+    Ft = torch.from_numpy(np.tile(F12, (P, 1))).cuda()
+    Et = torch.from_numpy(np.tile(ep2, (P, 1))).cuda()
+    f1 = torch.arange(P, dtype=torch.int32, device="cuda")
+    scale, sigma2 = ex.GetScaleFactors(), ex.GetScaleSigmaSquares()
+    m12, nm = search_for_triangulation_batch_device(kps, dt, cnt, kps, dt, cnt, Ft, Et, scale, sigma2,
+                                                    frame1=f1, frame2=f1 + P)
+    torch.cuda.synchronize()
+    K = kps.cpu().numpy()
+    M, NM = m12.cpu().numpy(), nm.cpu().numpy()
+    for p in range(P):
+        q = P + p
+        exp, n = _oracle_pair(oracle, K[p], D[p], N[p], K[q], D[q], N[q], F12, ep2, scale, sigma2)
+        assert np.array_equal(M[p, :N[p]], exp), p
+        assert NM[p] == n and n > 0
 
 
 def test_c3_feature_vectors(oracle):
