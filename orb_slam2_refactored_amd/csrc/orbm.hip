@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256) void tri_mm_kernel(TriArgs a, TriTables t, int
     // this workgroup's kf2 columns [jlo, jhi) (a multiple of 32 wide except the last part)
     const int span = ((nB + nsplit - 1) / nsplit + 31) & ~31;
     const int jlo = (blockIdx.x % nsplit) * span, jhi = min(nB, jlo + span);
-    if (row_base >= nA || jlo >= jhi) return;   // block-uniform
+    if (row_base >= nA || (nsplit > 1 && jlo >= jhi)) return;   // block-uniform (one part: rows get -1 below)
     const uint8_t* Ap = a.desc1 + (long long)f1 * a.cap1 * 32;
     const uint8_t* Bp = a.desc2 + (long long)f2 * a.cap2 * 32;
     const long long base2 = (long long)f2 * a.cap2;

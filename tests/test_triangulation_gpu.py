@@ -149,6 +149,28 @@ def test_c3_event_overflow(oracle, tri_path):
         assert NM[p] == n and n > 0
 
 
+def test_c3_empty_keyframes(tri_path):
+    """A pair whose kf2 has no keypoints (every query -1, no matches) next to one whose kf1 has none."""
+    import torch
+    P = 2
+    ex, frames, kps, desc, cnt = _c3_batch(P, 9500)
+    c = cnt.clone()
+    c[P] = 0      # kf2 of pair 0
+    c[1] = 0      # kf1 of pair 1
+    F12, ep2 = stereo_tri_geometry()
+    Ft = torch.from_numpy(np.tile(F12, (P, 1))).cuda()
+    Et = torch.from_numpy(np.tile(ep2, (P, 1))).cuda()
+    f1 = torch.arange(P, dtype=torch.int32, device="cuda")
+    scale, sigma2 = ex.GetScaleFactors(), ex.GetScaleSigmaSquares()
+    cap = kps.shape[1]
+    out = (torch.full((P, cap), 7, dtype=torch.int32, device="cuda"), torch.full((P,), 7, dtype=torch.int32, device="cuda"))
+    m12, nm = search_for_triangulation_batch_device(kps, desc, c, kps, desc, c, Ft, Et, scale, sigma2,
+                                                    frame1=f1, frame2=f1 + P, out=out)
+    torch.cuda.synchronize()
+    n0 = int(cnt[0])
+    assert (m12[0, :n0] == -1).all() and int(nm[0]) == 0 and int(nm[1]) == 0
+
+
 def test_c3_feature_vectors(oracle):
     """FeatureVector mode: DBoW2 transform on the device (levelsup 2) feeds the node join."""
     import torch
