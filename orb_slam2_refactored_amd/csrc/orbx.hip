@@ -168,6 +168,13 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
 // per-level tables.
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));   // packed u16 pair
 
+// Vertical taps ((h >> 4) * b) >> 16 on the full-rate 24-bit multiplier: with h4 = (h >> 4) << 4
+// (h < 2^20) and b12 = b << 12 (b <= 2048), mulhi(h4, b12) = ((h >> 4) * b * 2^16) >> 32, and the
+// masks tell the compiler both operands fit in 24 bits (v_mul_hi_u32_u24 instead of the
+// quarter-rate v_mul_hi_u32).
+__device__ __forceinline__ uint32_t htap24(uint32_t h) { return h & 0xffff0u; }
+__device__ __forceinline__ uint32_t vcoef24(int b) { return ((uint32_t)b & 0xfffu) << 12; }
+
 constexpr int PYR_TW = 64, PYR_TH = 64;
 constexpr int PYR_SW = 144, PYR_SH = 128;   // LDS source tile capacity (scale factor <= ~1.9)
 
@@ -199,21 +206,20 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
             uint8_t* dcol = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + p0;
             for (int ty = threadIdx.x >> 5; ty < th; ty += 8) {
                 const int2 yv = ys_t[ty];
-                const int r0 = ((yv.x & 0xffff) - sy_lo) * (PYR_SW / 4), r1 = ((yv.x >> 16) - sy_lo) * (PYR_SW / 4);
-                const uint32_t b0 = (uint32_t)yv.y << 16, b1 = (uint32_t)yv.y & 0xffff0000u;
+                const int r0 = __mul24((yv.x & 0xffff) - sy_lo, PYR_SW / 4), r1 = __mul24((yv.x >> 16) - sy_lo, PYR_SW / 4);
+                const uint32_t b0 = vcoef24(yv.y), b1 = vcoef24(yv.y >> 16);
                 const uint32_t w00 = S32[r0], w01 = S32[r0 + 1], w10 = S32[r1], w11 = S32[r1 + 1];
                 auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
                     const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
                     return *reinterpret_cast<const us2*>(&r);
                 };
-                const uint32_t h0a = __builtin_amdgcn_udot2(tap(w01, w00, sel0), a0, 0u, false) >> 4;
-                const uint32_t h1a = __builtin_amdgcn_udot2(tap(w11, w10, sel0), a0, 0u, false) >> 4;
-                const uint32_t h0b = __builtin_amdgcn_udot2(tap(w01, w00, sel1), a1, 0u, false) >> 4;
-                const uint32_t h1b = __builtin_amdgcn_udot2(tap(w11, w10, sel1), a1, 0u, false) >> 4;
-                // (h * b) >> 16 == mulhi(h, b << 16)
+                const uint32_t h0a = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel0), a0, 0u, false));
+                const uint32_t h1a = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel0), a0, 0u, false));
+                const uint32_t h0b = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel1), a1, 0u, false));
+                const uint32_t h1b = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel1), a1, 0u, false));
                 const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
                 const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
-                uint8_t* dst = dcol + (long long)(ty0 + ty) * L.stride;
+                uint8_t* dst = dcol + __mul24(ty0 + ty, L.stride);
                 if (p0 + 1 < tw) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(va | (vb << 8));   // tx0 + p0 even
                 else dst[0] = (uint8_t)va;
             }
@@ -294,10 +300,18 @@ __device__ __forceinline__ PyrTile pyr_tile_geom(const Geom& g, int l, int t, in
     return T;
 }
 
+// piece i -> (row, 16-byte column): rr = (i * mul) >> 20 as a 24-bit high product (i < 2^11,
+// mul <= 2^20), c = i - rr * nc as a 24-bit product (full-rate multipliers)
+__device__ __forceinline__ int pyr_piece_row(const PyrTile& T, int i) {
+    return (int)(__umulhi(((unsigned)i & 0x7ffu) << 12, (unsigned)T.mul & 0xffffffu) & 0x7ffu);
+}
+__device__ __forceinline__ int mul12(int a, int b) {   // a, b in [0, 4096): one v_mul_u32_u24
+    return (int)(((unsigned)a & 0xfffu) * ((unsigned)b & 0xfffu));
+}
 __device__ __forceinline__ void pyr_piece_load(const PyrTile& T, int i, uint4& v) {
     if (i < T.items) {
-        const int rr = (int)(((unsigned)i * (unsigned)T.mul) >> 20), c = i - rr * T.nc;
-        v = *reinterpret_cast<const uint4*>(T.src + (long long)(T.sy_lo + rr) * T.sstep + T.xa + 16 * c);
+        const int rr = pyr_piece_row(T, i), c = i - mul12(rr, T.nc);
+        v = *reinterpret_cast<const uint4*>(T.src + __mul24(T.sy_lo + rr, T.sstep) + T.xa + 16 * c);
     }
 }
 
@@ -314,8 +328,8 @@ __device__ __forceinline__ void pyr_fetch(const PyrTile& T, int tid, uint4& v0, 
 __device__ __forceinline__ void pyr_stage(const PyrTile& T, int tid, uint8_t* S, const uint4& v, int k) {
     const int i = tid + 256 * k;
     if (i < T.items) {
-        const int rr = (int)(((unsigned)i * (unsigned)T.mul) >> 20), c = i - rr * T.nc;
-        *reinterpret_cast<uint4*>(&S[rr * PYR_SW + 16 * c]) = v;
+        const int rr = pyr_piece_row(T, i), c = i - mul12(rr, T.nc);
+        *reinterpret_cast<uint4*>(&S[mul12(rr, PYR_SW) + 16 * c]) = v;
     }
 }
 
@@ -506,17 +520,17 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
             if (r >= nrow) break;
             const int2 yv = ys1[r];
             if (fits) {
-                const int rr0 = ((yv.x & 0xffff) - T.sy_lo) * (PYR_SW / 4), rr1 = ((yv.x >> 16) - T.sy_lo) * (PYR_SW / 4);
-                const uint32_t b0 = (uint32_t)yv.y << 16, b1 = (uint32_t)yv.y & 0xffff0000u;
+                const int rr0 = __mul24((yv.x & 0xffff) - T.sy_lo, PYR_SW / 4), rr1 = __mul24((yv.x >> 16) - T.sy_lo, PYR_SW / 4);
+                const uint32_t b0 = vcoef24(yv.y), b1 = vcoef24(yv.y >> 16);
 #pragma unroll
                 for (int j = 0; j < 2; j++) {
                     const uint32_t* s0 = S32 + rr0 + wdv[j];
                     const uint32_t* s1 = S32 + rr1 + wdv[j];
                     const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
-                    const uint32_t h0a = __builtin_amdgcn_udot2(tap(w01, w00, sel0[j]), a0[j], 0u, false) >> 4;
-                    const uint32_t h1a = __builtin_amdgcn_udot2(tap(w11, w10, sel0[j]), a0[j], 0u, false) >> 4;
-                    const uint32_t h0b = __builtin_amdgcn_udot2(tap(w01, w00, sel1[j]), a1[j], 0u, false) >> 4;
-                    const uint32_t h1b = __builtin_amdgcn_udot2(tap(w11, w10, sel1[j]), a1[j], 0u, false) >> 4;
+                    const uint32_t h0a = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel0[j]), a0[j], 0u, false));
+                    const uint32_t h1a = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel0[j]), a0[j], 0u, false));
+                    const uint32_t h0b = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel1[j]), a1[j], 0u, false));
+                    const uint32_t h1b = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel1[j]), a1[j], 0u, false));
                     const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
                     const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
                     out[pp] |= (va | (vb << 8)) << (16 * j);
@@ -538,7 +552,7 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
             const int r = r0 + pp * rpp;
             if (r >= nrow) break;
             *reinterpret_cast<uint32_t*>(&S[r * PYR_SW + 4 * q]) = out[pp];
-            uint8_t* dst = lrow + (long long)(ay0 + r) * L1.stride;
+            uint8_t* dst = lrow + __mul24(ay0 + r, L1.stride);
             if (full) {
                 *reinterpret_cast<uint32_t*>(dst) = out[pp];
             } else {
