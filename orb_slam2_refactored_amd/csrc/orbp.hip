@@ -272,13 +272,22 @@ __global__ __launch_bounds__(256) void pj_score_kernel(PjArgs a) {
 }
 
 // ---------------------------------------------------------------- the ordered claim walk
+// One wavefront per frame, 64 map points per chunk, one lane per map point.  A map point's outcome
+// depends on the earlier ones only through the claim bitmap (keypoints whose map point has
+// observations, :339), and only through the claim bits of its K kept candidates while two of them
+// remain available (else the window is rescanned).  So every round decides all remaining lanes of
+// the chunk at once against the current bitmap, marks each claimed keypoint with the lowest
+// claiming lane (LDS atomicMin), and commits the lanes before the first one that either saw an
+// available candidate claimed by an earlier lane of the round or needs a rescan.  Claims set bits
+// as the reference's loop would, in lane order (a committed lane saw no earlier claim on its
+// candidates); kp_match keeps the last map point to match a keypoint (:374) by atomicMax on the map
+// point index, which grows with the walk.  The first undecided lane then runs next round, or — when
+// it needs the rescan — alone on the wavefront as the sequential walk does.
 constexpr int PJ_CHUNK = 64;
 
 __global__ __launch_bounds__(64) void pj_walk_kernel(PjArgs a) {
     __shared__ uint32_t bits[PJ_MAXKP / 32];
-    __shared__ uint2 s_top[PJ_CHUNK * PJ_K];
-    __shared__ int s_cnt[PJ_CHUNK];
-    __shared__ uint8_t s_flag[PJ_CHUNK];   // bit 0 valid, bit 1 has_obs
+    __shared__ int stamp[PJ_MAXKP];   // lowest claiming lane of the round (64: none)
     const int lane = threadIdx.x;
     const int f = blockIdx.x;
     const int k0 = a.kp_begin[f], n = a.kp_begin[f + 1] - k0;
@@ -294,72 +303,111 @@ __global__ __launch_bounds__(64) void pj_walk_kernel(PjArgs a) {
             for (int b = 0; b < 32 && w * 32 + b < n; b++) v |= (uint32_t)(a.kp_claimed[k0 + w * 32 + b] != 0) << b;
         bits[w] = v;
     }
+    for (int i = lane; i < n; i += 64) stamp[i] = 64;
+    __syncthreads();
+    auto bit = [&](int idx) { return (bits[idx >> 5] >> (idx & 31)) & 1u; };
     int nmatches = 0;
     for (int c = 0; c < nm; c += PJ_CHUNK) {
         const int m = min(PJ_CHUNK, nm - c);
+        // this lane's map point: validity, candidate count, observations, K kept candidates
+        int cnt = 0;
+        bool has_obs = false;
+        uint2 e[PJ_K];
+#pragma unroll
+        for (int k = 0; k < PJ_K; k++) e[k] = make_uint2(PJ_NONE, 0);
         if (lane < m) {
             const int mj = m0 + c + lane;
             const int lvl = a.mp_level[mj];
             const bool ok = a.mp_valid[mj] && lvl >= 0 && lvl < a.n_levels;
-            s_cnt[lane] = ok ? a.mp_cnt[mj] : 0;
-            s_flag[lane] = (uint8_t)((ok ? 1 : 0) | (a.mp_has_obs[mj] ? 2 : 0));
+            cnt = ok ? a.mp_cnt[mj] : 0;
+            has_obs = a.mp_has_obs[mj] != 0;
+#pragma unroll
+            for (int k = 0; k < PJ_K; k++) e[k] = a.mp_top[(size_t)mj * PJ_K + k];
         }
-        for (int q = lane; q < m * PJ_K; q += 64) s_top[q] = a.mp_top[(size_t)(m0 + c) * PJ_K + q];
-        __syncthreads();
-        for (int i = 0; i < m; i++) {
-            const int cnt = s_cnt[i];
-            if (cnt == 0) continue;   // invalid, or GetFeaturesInArea / the gates left nothing
-            uint2 e = make_uint2(PJ_NONE, 0);
-            bool avail = false;
-            if (lane < PJ_K) {
-                e = s_top[i * PJ_K + lane];
-                const int idx = (int)(e.y & 0xffffffu);
-                avail = e.x != PJ_NONE && !((bits[idx >> 5] >> (idx & 31)) & 1u);
-            }
-            const unsigned long long mask = __ballot(avail);
-            uint32_t bkey = PJ_NONE, skey = PJ_NONE;
-            int bidx = -1, blev = -1, slev = -1;
-            if (__popcll(mask) >= 2 || cnt <= PJ_K) {
-                if (mask) {
-                    const int l0 = __ffsll((long long)mask) - 1;
-                    bkey = __shfl(e.x, l0, 64);
-                    const uint32_t be = __shfl(e.y, l0, 64);
-                    bidx = (int)(be & 0xffffffu);
-                    blev = (int)(be >> 24);
-                    const unsigned long long rest = mask & (mask - 1);
-                    if (rest) {
-                        const int l1 = __ffsll((long long)rest) - 1;
-                        skey = __shfl(e.x, l1, 64);
-                        slev = (int)(__shfl(e.y, l1, 64) >> 24);
-                    }
+        int start = 0;
+        while (start < m) {   // wavefront-uniform
+            // decide every lane >= start against the current bitmap
+            uint32_t avail = 0;
+#pragma unroll
+            for (int k = 0; k < PJ_K; k++)
+                if (e[k].x != PJ_NONE && !bit((int)(e[k].y & 0xffffffu))) avail |= 1u << k;
+            const bool mine = lane >= start && lane < m && cnt > 0;
+            const bool rescan = mine && !(__popc(avail) >= 2 || cnt <= PJ_K);
+            bool match = false;
+            int bidx = -1;
+            if (mine && !rescan && avail) {
+                const int l0 = __ffs(avail) - 1;
+                const uint32_t rest = avail & (avail - 1);
+                uint32_t bkey = PJ_NONE, skey = PJ_NONE, be = 0, se = 0;
+#pragma unroll
+                for (int k = 0; k < PJ_K; k++)
+                    if (k == l0) { bkey = e[k].x; be = e[k].y; }
+                if (rest) {
+                    const int l1 = __ffs(rest) - 1;
+#pragma unroll
+                    for (int k = 0; k < PJ_K; k++)
+                        if (k == l1) { skey = e[k].x; se = e[k].y; }
                 }
-            } else {   // the K kept candidates are exhausted by earlier claims: rescan the window
+                const int bestDist = (int)(bkey >> PJ_IDX_BITS);
+                const int secondDist = skey == PJ_NONE ? 256 : (int)(skey >> PJ_IDX_BITS);
+                const int blev = (int)(be >> 24), slev = skey == PJ_NONE ? -1 : (int)(se >> 24);
+                if (bestDist <= PJ_TH_HIGH && !(blev == slev && (float)bestDist > a.nnratio * (float)secondDist)) {   // :367-377
+                    match = true;
+                    bidx = (int)(be & 0xffffffu);
+                }
+            }
+            const bool claims = match && has_obs;
+            if (claims) atomicMin(&stamp[bidx], lane);
+            __syncthreads();   // one wavefront: orders its LDS writes before the reads below
+            bool conflict = rescan;
+            if (mine && !rescan) {
+#pragma unroll
+                for (int k = 0; k < PJ_K; k++)
+                    if (((avail >> k) & 1u) && stamp[(int)(e[k].y & 0xffffffu)] < lane) conflict = true;
+            }
+            const unsigned long long cb = __ballot(conflict);
+            const int stop = cb ? __ffsll((long long)cb) - 1 : m;   // first undecided lane
+            // commit [start, stop)
+            const bool commit = lane >= start && lane < stop && match;
+            if (commit) {
+                atomicMax(a.kp_match + k0 + bidx, c + lane);
+                if (claims) atomicOr(&bits[bidx >> 5], 1u << (bidx & 31));
+            }
+            nmatches += (int)__popcll(__ballot(commit));
+            if (claims) stamp[bidx] = 64;
+            __syncthreads();   // one wavefront: orders its LDS writes before the reads below
+            if (stop == start) {
+                // lane `start` needs the rescan: the window with the current bitmap, on the wavefront
+                const int i = start;
                 const int mj = m0 + c + i;
                 const PjPoint w = pj_point(a, f, mj);
                 uint32_t t[2] = {PJ_NONE, PJ_NONE};
                 pj_scan<true>(a, f, mj, w, bits, lane, [&](uint32_t key, int, int) { pj_insert(t, key); });
                 uint32_t o[2];
                 pj_wave_topk(t, o);
-                bkey = o[0];
-                skey = o[1];
+                const uint32_t bkey = o[0], skey = o[1];
+                int bi = -1, blev = -1, slev = -1;
                 if (bkey != PJ_NONE) {
-                    bidx = a.grid_idx[k0 + (int)(bkey & PJ_IDX_MASK)];
-                    blev = a.kp_oct[k0 + bidx];
+                    bi = a.grid_idx[k0 + (int)(bkey & PJ_IDX_MASK)];
+                    blev = a.kp_oct[k0 + bi];
                 }
                 if (skey != PJ_NONE) slev = a.kp_oct[k0 + a.grid_idx[k0 + (int)(skey & PJ_IDX_MASK)]];
-            }
-            const int bestDist = bkey == PJ_NONE ? 256 : (int)(bkey >> PJ_IDX_BITS);
-            const int secondDist = skey == PJ_NONE ? 256 : (int)(skey >> PJ_IDX_BITS);
-            if (bestDist <= PJ_TH_HIGH) {   // :367-377
-                if (blev == slev && (float)bestDist > a.nnratio * (float)secondDist) continue;
-                if (lane == 0) {
-                    a.kp_match[k0 + bidx] = c + i;
-                    if (s_flag[i] & 2) bits[bidx >> 5] |= 1u << (bidx & 31);
+                const int bestDist = bkey == PJ_NONE ? 256 : (int)(bkey >> PJ_IDX_BITS);
+                const int secondDist = skey == PJ_NONE ? 256 : (int)(skey >> PJ_IDX_BITS);
+                const bool obs_i = __shfl(has_obs ? 1 : 0, i, 64) != 0;
+                if (bestDist <= PJ_TH_HIGH && !(blev == slev && (float)bestDist > a.nnratio * (float)secondDist)) {
+                    if (lane == 0) {
+                        atomicMax(a.kp_match + k0 + bi, c + i);
+                        if (obs_i) bits[bi >> 5] |= 1u << (bi & 31);
+                    }
+                    nmatches++;
                 }
-                nmatches++;
+                __syncthreads();   // one wavefront: orders its LDS writes before the reads below
+                start = i + 1;
+            } else {
+                start = stop;
             }
         }
-        __syncthreads();
     }
     if (lane == 0) a.n_matches[f] = nmatches;
 }
