@@ -67,6 +67,7 @@ struct PjArgs {
     int32_t* grid_idx;    // total_kp: frame-relative keypoint index at each sorted position
     int32_t* grid_start;  // n_frames x (PJ_CELLS + 1)
     int32_t* mp_cnt;      // total_mp
+    int32_t* mp_frame;    // total_mp: frame of each map point (pj_grid_kernel)
     uint2* mp_top;        // total_mp x PJ_K: (key, index | level << 24)
     // outputs
     int32_t* kp_match;
@@ -81,15 +82,18 @@ __device__ __forceinline__ int pj_hamming(const uint8_t* a, const uint8_t* b) {
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// reductions over a group of W lanes (W = 64: the wavefront; W = 16: a quarter of it)
+template <int W = 64>
 __device__ __forceinline__ uint32_t pj_wave_min(uint32_t v) {
 #pragma unroll
-    for (int m = 32; m > 0; m >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
+    for (int m = W / 2; m > 0; m >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, W));
     return v;
 }
 
+template <int W = 64>
 __device__ __forceinline__ int pj_wave_sum(int v) {
 #pragma unroll
-    for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+    for (int m = W / 2; m > 0; m >>= 1) v += __shfl_xor(v, m, W);
     return v;
 }
 
@@ -99,6 +103,7 @@ __global__ __launch_bounds__(256) void pj_grid_kernel(PjArgs a) {
     const int f = blockIdx.x;
     const int k0 = a.kp_begin[f], n = a.kp_begin[f + 1] - k0;
     int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
+    for (int j = a.mp_begin[f] + threadIdx.x; j < a.mp_begin[f + 1]; j += 256) a.mp_frame[j] = f;
     if (n > PJ_MAXKP) return;   // pj_walk_kernel reports the frame
     const float* bd = a.bounds + 4 * (size_t)f;
     const float minx = bd[0], miny = bd[2];
@@ -170,7 +175,7 @@ __device__ __forceinline__ PjPoint pj_point(const PjArgs& a, int f, int mj) {
 
 // Calls fn(key, idx, level) for each candidate of this lane that passes every gate; key =
 // dist << 13 | sorted position (increasing along GetFeaturesInArea's scan order).
-template <bool DYN, class Fn>
+template <bool DYN, int W = 64, class Fn>
 __device__ __forceinline__ void pj_scan(const PjArgs& a, int f, int mj, const PjPoint& w, const uint32_t* bits,
                                         int lane, Fn&& fn) {
     if (!w.any) return;
@@ -179,7 +184,7 @@ __device__ __forceinline__ void pj_scan(const PjArgs& a, int f, int mj, const Pj
     const uint8_t* d1 = a.mp_desc + 32 * (size_t)mj;
     for (int cx = w.mincx; cx <= w.maxcx; cx++) {
         const int p0 = cs[cx * PJ_ROWS + w.mincy], p1 = cs[cx * PJ_ROWS + w.maxcy + 1];
-        for (int p = p0 + lane; p < p1; p += 64) {
+        for (int p = p0 + lane; p < p1; p += W) {
             const int idx = a.grid_idx[k0 + p];
             const int k = k0 + idx;
             const int level = a.kp_oct[k];
@@ -208,11 +213,11 @@ __device__ __forceinline__ void pj_insert(uint32_t (&t)[K], uint32_t key) {
 }
 
 // Pops the wave's K smallest keys (one lane owns each key: positions are unique).
-template <int K>
+template <int K, int W = 64>
 __device__ __forceinline__ void pj_wave_topk(uint32_t (&t)[K], uint32_t (&out)[K]) {
 #pragma unroll
     for (int r = 0; r < K; r++) {
-        const uint32_t m = pj_wave_min(t[0]);
+        const uint32_t m = pj_wave_min<W>(t[0]);
         out[r] = m;
         if (t[0] == m && m != PJ_NONE) {
 #pragma unroll
@@ -222,21 +227,15 @@ __device__ __forceinline__ void pj_wave_topk(uint32_t (&t)[K], uint32_t (&out)[K
     }
 }
 
-__device__ __forceinline__ int pj_frame_of(const int32_t* begin, int n_frames, int j) {   // begin[f] <= j < begin[f+1]
-    int lo = 0, hi = n_frames - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (begin[mid] <= j) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
 // ---------------------------------------------------------------- per map point: top-K candidates
+// A 16-lane group per map point (4 per wavefront; the windows at the search radii hold tens of
+// candidates), the frame from pj_grid_kernel's map-point -> frame table.
+constexpr int PJ_GW = 16;
 __global__ __launch_bounds__(256) void pj_score_kernel(PjArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int mj = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (mj >= a.total_mp) return;   // wavefront-uniform
-    const int f = pj_frame_of(a.mp_begin, a.n_frames, mj);
+    const int lane = threadIdx.x & (PJ_GW - 1);
+    const int mj = blockIdx.x * (256 / PJ_GW) + (threadIdx.x / PJ_GW);
+    if (mj >= a.total_mp) return;   // group-uniform (every later reduction stays inside the group)
+    const int f = a.mp_frame[mj];
     const int n = a.kp_begin[f + 1] - a.kp_begin[f];
     int cnt = 0;
     uint32_t out[PJ_K];
@@ -249,12 +248,12 @@ __global__ __launch_bounds__(256) void pj_score_kernel(PjArgs a) {
 #pragma unroll
         for (int r = 0; r < PJ_K; r++) t[r] = PJ_NONE;
         int c = 0;
-        pj_scan<false>(a, f, mj, w, nullptr, lane, [&](uint32_t key, int, int) {
+        pj_scan<false, PJ_GW>(a, f, mj, w, nullptr, lane, [&](uint32_t key, int, int) {
             pj_insert(t, key);
             c++;
         });
-        cnt = pj_wave_sum(c);
-        pj_wave_topk(t, out);
+        cnt = pj_wave_sum<PJ_GW>(c);
+        pj_wave_topk<PJ_K, PJ_GW>(t, out);
     }
     if (lane == 0) a.mp_cnt[mj] = cnt;
     if (lane < PJ_K) {
@@ -418,7 +417,7 @@ static int launch_projection(PjArgs& a, int total_kp, hipStream_t st) {
     hipLaunchKernelGGL(pj_grid_kernel, dim3(a.n_frames), dim3(256), 0, st, a);
     ORB_HIP_TRY(hipGetLastError());
     if (a.total_mp > 0) {
-        hipLaunchKernelGGL(pj_score_kernel, dim3((a.total_mp + 3) / 4), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(pj_score_kernel, dim3((a.total_mp + 256 / PJ_GW - 1) / (256 / PJ_GW)), dim3(256), 0, st, a);
         ORB_HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(pj_walk_kernel, dim3(a.n_frames), dim3(64), 0, st, a);
@@ -434,7 +433,7 @@ thread_local PjScratch g_pj;
 
 static size_t pj_workspace_bytes(int n_frames, int total_kp, int total_mp) {
     return align_up((size_t)std::max(total_kp, 1) * 4, 256) + align_up((size_t)n_frames * (PJ_CELLS + 1) * 4, 256) +
-           align_up((size_t)std::max(total_mp, 1) * 4, 256) + align_up((size_t)std::max(total_mp, 1) * PJ_K * 8, 256);
+           2 * align_up((size_t)std::max(total_mp, 1) * 4, 256) + align_up((size_t)std::max(total_mp, 1) * PJ_K * 8, 256);
 }
 
 static void pj_carve(PjArgs& a, char* ws, int n_frames, int total_kp, int total_mp) {
@@ -444,6 +443,8 @@ static void pj_carve(PjArgs& a, char* ws, int n_frames, int total_kp, int total_
     a.grid_start = (int32_t*)(ws + o);
     o += align_up((size_t)n_frames * (PJ_CELLS + 1) * 4, 256);
     a.mp_cnt = (int32_t*)(ws + o);
+    o += align_up((size_t)std::max(total_mp, 1) * 4, 256);
+    a.mp_frame = (int32_t*)(ws + o);
     o += align_up((size_t)std::max(total_mp, 1) * 4, 256);
     a.mp_top = (uint2*)(ws + o);
 }
