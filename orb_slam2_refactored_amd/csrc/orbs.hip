@@ -40,6 +40,73 @@ __device__ __forceinline__ int st_hamming(uint4 a0, uint4 a1, uint4 b0, uint4 b1
 
 __device__ __forceinline__ void st_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Row table of the right keypoints (ComputeStereoMatches :84-97): keypoint j is listed on every row
+// floor(y - r) .. ceil(y + r), r = 2 scale[octave] (clamped to the image; the reference's
+// vRowIndices).  One workgroup per frame: LDS counts, an exclusive scan, then the entries.
+constexpr int ST_MAX_ROWS = 4096;
+__global__ __launch_bounds__(256) void stereo_rows_kernel(StereoSide L, StereoParams sp,
+                                                          const orbx_keypoint* __restrict__ kpsR,
+                                                          const int32_t* __restrict__ cntR, int nRf, int cap,
+                                                          int32_t* __restrict__ roff, int32_t* __restrict__ rlist,
+                                                          int span) {
+    __shared__ int s_cnt[ST_MAX_ROWS + 1];
+    __shared__ int s_part[256];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int nR = cntR ? cntR[f] : nRf;
+    const int rows = L.rows[0];
+    for (int y = tid; y <= rows; y += 256) s_cnt[y] = 0;
+    __syncthreads();
+    auto band = [&](int j, int& y0, int& y1) {
+        const orbx_keypoint kR = kpsR[(long long)f * cap + j];
+        const float r = 2.f * sp.scale[kR.octave];
+        y0 = max((int)floorf(kR.y - r), 0);
+        y1 = min((int)ceilf(kR.y + r), rows - 1);
+    };
+    for (int j = tid; j < nR; j += 256) {
+        int y0, y1;
+        band(j, y0, y1);
+        for (int y = y0; y <= y1; y++) atomicAdd(&s_cnt[y], 1);
+    }
+    __syncthreads();
+    // exclusive scan of s_cnt[0..rows): contiguous chunks per thread, then a scan of the chunk sums
+    const int per = (rows + 255) / 256, c0 = min(tid * per, rows), c1 = min(c0 + per, rows);
+    int sum = 0;
+    for (int y = c0; y < c1; y++) sum += s_cnt[y];
+    s_part[tid] = sum;
+    __syncthreads();
+    if (tid < 64) {   // 4 chunk sums per lane, a 64-lane inclusive scan of their totals
+        int v[4], acc = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) { v[q] = s_part[4 * tid + q]; acc += v[q]; }
+        int inc = acc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(inc, d, 64);
+            if (tid >= d) inc += o;
+        }
+        int run = inc - acc;
+#pragma unroll
+        for (int q = 0; q < 4; q++) { s_part[4 * tid + q] = run; run += v[q]; }
+    }
+    __syncthreads();
+    int run = s_part[tid];
+    int32_t* ro = roff + (long long)f * (rows + 1);
+    for (int y = c0; y < c1; y++) {
+        const int cnt = s_cnt[y];
+        s_cnt[y] = run;   // becomes the fill cursor
+        ro[y] = run;
+        run += cnt;
+    }
+    if (tid == 255) ro[rows] = run;   // the last chunk ends at the total (chunks past rows are empty)
+    __syncthreads();
+    int32_t* rl = rlist + (long long)f * cap * span;
+    for (int j = tid; j < nR; j += 256) {
+        int y0, y1;
+        band(j, y0, y1);
+        for (int y = y0; y <= y1; y++) rl[atomicAdd(&s_cnt[y], 1)] = j;
+    }
+}
+
 __global__ __launch_bounds__(256) void stereo_match_kernel(StereoSide L, StereoSide R, StereoParams sp,
                                                            const orbx_keypoint* __restrict__ kpsL,
                                                            const uint8_t* __restrict__ descL,
@@ -48,7 +115,8 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(StereoSide L, StereoS
                                                            const uint8_t* __restrict__ descR,
                                                            const int32_t* __restrict__ cntR, int nRf, int cap,
                                                            float* __restrict__ uright, float* __restrict__ depth,
-                                                           int32_t* __restrict__ sad) {
+                                                           int32_t* __restrict__ sad, const int32_t* __restrict__ roff,
+                                                           const int32_t* __restrict__ rlist, int span) {
     __shared__ uint8_t sIL[4][ST_PS * ST_PS + 7];
     __shared__ uint8_t sW[4][ST_PS * ST_WW + 3];
     __shared__ int sAcc[4][16];
@@ -71,12 +139,16 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(StereoSide L, StereoS
         const uint4* dl = reinterpret_cast<const uint4*>(descL + o * 32);
         const uint4 a0 = dl[0], a1 = dl[1];
         uint32_t key = 0xffffffffu;
-        for (int j = lane; j < nR; j += 64) {
+        // the right keypoints whose row band holds this row (stereo_rows_kernel; the reference's
+        // vRowIndices[vL], :99): the first minimum is a min of (d << 16 | j), so list order is free
+        const int32_t* ro = roff + (long long)f * (L.rows[0] + 1);
+        const int32_t* rl = rlist + (long long)f * cap * span;
+        const int t0 = ro[row], t1 = ro[row + 1];
+        (void)nR;
+        for (int t = t0 + lane; t < t1; t += 64) {
+            const int j = rl[t];
             const orbx_keypoint kR = kpsR[(long long)f * cap + j];
-            const float r = 2.f * sp.scale[kR.octave];
-            const int miny = (int)floorf(kR.y - r), maxy = (int)ceilf(kR.y + r);
-            if (row >= miny && row <= maxy && kR.octave >= octL - 1 && kR.octave <= octL + 1 && kR.x >= minu &&
-                kR.x <= maxu) {
+            if (kR.octave >= octL - 1 && kR.octave <= octL + 1 && kR.x >= minu && kR.x <= maxu) {
                 const uint4* dr = reinterpret_cast<const uint4*>(descR + ((long long)f * cap + j) * 32);
                 const int d = st_hamming(a0, a1, dr[0], dr[1]);
                 if (d < ST_TH_HIGH) key = min(key, ((uint32_t)d << 16) | (uint32_t)j);
@@ -192,14 +264,32 @@ __global__ __launch_bounds__(256) void stereo_filter_kernel(const int32_t* __res
     }
 }
 
+int stereo_row_span(const StereoParams& sp, int nlevels) {
+    float smax = 1.f;
+    for (int l = 0; l < nlevels; l++) smax = std::max(smax, sp.scale[l]);
+    return (int)std::ceil(4.f * smax) + 4;   // ceil(y + r) - floor(y - r) + 1 <= 2 r + 3
+}
+
+size_t stereo_scratch_ints(int n_frames, int cap, int rows, int span) {
+    return (size_t)n_frames * ((size_t)cap + (size_t)(rows + 1) + (size_t)cap * span);
+}
+
 int launch_stereo(const StereoSide& L, const StereoSide& R, const StereoParams& sp, int n_frames,
                   const orbx_keypoint* kpsL, const uint8_t* descL, const int32_t* cntL, int nL_fixed,
                   const orbx_keypoint* kpsR, const uint8_t* descR, const int32_t* cntR, int nR_fixed, int cap,
-                  float* uright, float* depth, int32_t* sad, hipStream_t st) {
+                  float* uright, float* depth, int32_t* scratch, hipStream_t st) {
     if (n_frames <= 0 || cap <= 0) return ORB_OK;
     ORB_CHECK_ARG(cap <= 65535, "stereo: cap too large");
+    ORB_CHECK_ARG(L.rows[0] > 0 && L.rows[0] <= ST_MAX_ROWS, "stereo: image rows must be 1..4096");
+    const int span = stereo_row_span(sp, L.nlevels);
+    int32_t* sad = scratch;
+    int32_t* roff = sad + (size_t)n_frames * cap;
+    int32_t* rlist = roff + (size_t)n_frames * (L.rows[0] + 1);
+    hipLaunchKernelGGL(stereo_rows_kernel, dim3((unsigned)n_frames), dim3(256), 0, st, L, sp, kpsR, cntR, nR_fixed, cap,
+                       roff, rlist, span);
     hipLaunchKernelGGL(stereo_match_kernel, dim3((unsigned)((cap + 3) / 4), (unsigned)n_frames), dim3(256), 0, st, L,
-                       R, sp, kpsL, descL, cntL, nL_fixed, kpsR, descR, cntR, nR_fixed, cap, uright, depth, sad);
+                       R, sp, kpsL, descL, cntL, nL_fixed, kpsR, descR, cntR, nR_fixed, cap, uright, depth, sad, roff,
+                       rlist, span);
     hipLaunchKernelGGL(stereo_filter_kernel, dim3((unsigned)n_frames), dim3(256), (size_t)cap * sizeof(int), st, cntL,
                        nL_fixed, cap, uright, depth, sad);
     ORB_HIP_TRY(hipGetLastError());
@@ -216,6 +306,13 @@ struct StereoScratch {
 };
 thread_local StereoScratch g_st;
 }  // namespace
+
+static int stereo_row_span_host(const float* scale, int nlevels) {
+    StereoParams sp;
+    std::memset(&sp, 0, sizeof(sp));
+    for (int l = 0; l < nlevels && l < ST_MAX_LEVELS; l++) sp.scale[l] = scale[l];
+    return stereo_row_span(sp, std::min(nlevels, ST_MAX_LEVELS));
+}
 
 extern "C" int orbm_compute_stereo_matches(const orbm_stereo_view* left, const orbm_stereo_view* right,
                                            const float* scale_factors, const float* inv_scale_factors, float bf,
@@ -237,7 +334,8 @@ extern "C" int orbm_compute_stereo_matches(const orbm_stereo_view* left, const o
     auto take = [&](size_t bytes) { const size_t o = off; off += align_up(std::max<size_t>(bytes, 1), 256); return o; };
     const size_t o_kL = take((size_t)cap * 28), o_kR = take((size_t)cap * 28), o_dL = take((size_t)cap * 32),
                  o_dR = take((size_t)cap * 32), o_u = take((size_t)cap * 4), o_d = take((size_t)cap * 4),
-                 o_s = take((size_t)cap * 4);
+                 o_s = take(stereo_scratch_ints(1, cap, left->level_rows[0],
+                                                stereo_row_span_host(scale_factors, left->n_levels)) * 4);
     size_t o_lv[2][ST_MAX_LEVELS];
     const orbm_stereo_view* views[2] = {left, right};
     for (int v = 0; v < 2; v++)

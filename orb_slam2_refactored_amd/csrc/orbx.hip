@@ -3085,7 +3085,6 @@ int orbx_stereo_matches_batch_device(orbx_extractor* left, orbx_extractor* right
     std::lock_guard<std::mutex> lk(left->mu);
     ORB_HIP_TRY(hipSetDevice(left->device));
     int rc;
-    if ((rc = left->d_stereo_sad.reserve((size_t)n_frames * cap * sizeof(int32_t)))) return rc;
     StereoSide L, R;
     stereo_side(left, L);
     stereo_side(right, R);
@@ -3097,6 +3096,8 @@ int orbx_stereo_matches_batch_device(orbx_extractor* left, orbx_extractor* right
     }
     sp.bf = bf;
     sp.baseline = baseline;
+    const size_t ints = stereo_scratch_ints(n_frames, cap, L.rows[0], stereo_row_span(sp, left->p.nlevels));
+    if ((rc = left->d_stereo_sad.reserve(ints * sizeof(int32_t)))) return rc;
     return launch_stereo(L, R, sp, n_frames, d_kps_l, d_desc_l, d_counts_l, 0, d_kps_r, d_desc_r, d_counts_r, 0, cap,
                          d_uright, d_depth, left->d_stereo_sad.as<int32_t>(), (hipStream_t)stream);
 }

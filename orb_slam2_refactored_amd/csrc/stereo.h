@@ -28,12 +28,18 @@ struct StereoParams {
     float bf, baseline;
 };
 
-// Enqueues the match kernel and the median filter for n_frames frame pairs.  kps/desc/counts are
-// [n_frames][cap] slot arrays (counts may be NULL with n_fixed keypoints per frame).  sad: scratch,
-// n_frames*cap ints.
+// Rows a right keypoint of any level covers in the row table (floor(y - r) .. ceil(y + r), r = 2 s).
+int stereo_row_span(const StereoParams& sp, int nlevels);
+// Scratch ints launch_stereo needs: per frame the SAD distances (cap), the row table's offsets
+// (rows + 1) and its entries (cap * row span).
+size_t stereo_scratch_ints(int n_frames, int cap, int rows, int span);
+
+// Enqueues the row table, the match kernel and the median filter for n_frames frame pairs.
+// kps/desc/counts are [n_frames][cap] slot arrays (counts may be NULL with n_fixed keypoints per
+// frame).  scratch: stereo_scratch_ints(n_frames, cap, L.rows[0], stereo_row_span(sp, L.nlevels)).
 int launch_stereo(const StereoSide& L, const StereoSide& R, const StereoParams& sp, int n_frames,
                   const orbx_keypoint* kpsL, const uint8_t* descL, const int32_t* cntL, int nL_fixed,
                   const orbx_keypoint* kpsR, const uint8_t* descR, const int32_t* cntR, int nR_fixed, int cap,
-                  float* uright, float* depth, int32_t* sad, hipStream_t st);
+                  float* uright, float* depth, int32_t* scratch, hipStream_t st);
 
 }  // namespace orbamd
