@@ -32,9 +32,9 @@ struct orbv_vocabulary {
     int device = 0;
     int k = 0, L = 0, scoring = 0, weighting = 0;
     int n_nodes = 0, n_words = 0, max_children = 0;
-    orbamd::DevBuf buf;   // child_off | child | desc | word | weight
+    orbamd::DevBuf buf;   // child_off | orig | desc | word | weight, in breadth-first node order
     int32_t* child_off = nullptr;
-    int32_t* child = nullptr;
+    int32_t* orig = nullptr;   // breadth-first id -> the file's node id
     uint8_t* desc = nullptr;
     uint32_t* word = nullptr;
     double* weight = nullptr;
@@ -46,9 +46,12 @@ namespace orbamd {
 constexpr uint32_t VOC_NONE = 0xffffffffu;
 constexpr int VOC_MAXF = ORBV_MAX_FEATURES;
 
+// The tree in breadth-first order (voc_upload relabels it): node u's children are the consecutive ids
+// child_off[u] + 1 .. child_off[u + 1], so a child's descriptor address needs no index load; orig maps
+// back to the file's node ids (the FeatureVector's node ids).
 struct VocDev {
     const int32_t* child_off;
-    const int32_t* child;
+    const int32_t* orig;
     const uint8_t* desc;
     const uint32_t* word;
     const double* weight;
@@ -88,19 +91,19 @@ __global__ __launch_bounds__(256) void voc_descend_kernel(VocDev v, const uint8_
         for (int c0 = 0; c0 < cnt; c0 += G) {
             const int c = c0 + lane;
             if (c < cnt) {
-                const int dist = voc_hamming(a0, a1, v.desc + (size_t)v.child[off + c] * 32);
+                const int dist = voc_hamming(a0, a1, v.desc + (size_t)(off + 1 + c) * 32);
                 key = min(key, ((uint32_t)dist << 16) | (uint32_t)c);
             }
         }
 #pragma unroll
         for (int m = G / 2; m > 0; m >>= 1) key = min(key, (uint32_t)__shfl_xor((int)key, m, G));
-        node = (uint32_t)v.child[off + (int)(key & 0xffffu)];
+        node = (uint32_t)(off + 1 + (int)(key & 0xffffu));
         if (level == v.nid_level) nid = node;
     }
     if (lane == 0) {
         out.word[g] = v.word[node];
         out.weight[g] = v.weight[node];
-        out.node[g] = nid == VOC_NONE ? node : nid;   // undefined in the reference: the leaf
+        out.node[g] = (uint32_t)v.orig[nid == VOC_NONE ? node : nid];   // undefined in the reference: the leaf
     }
 }
 
@@ -253,6 +256,18 @@ int voc_upload(orbv_vocabulary* v, int n, const std::vector<int32_t>& parent, co
     for (int i = 0; i < n; i++) off[i + 1] = off[i] + cnt[i];
     std::vector<int32_t> fill(off.begin(), off.end() - 1);
     for (int i = 1; i < n; i++) child[fill[parent[i]]++] = i;   // children in file order (push_back)
+    // breadth-first relabelling: new id -> file id (children of a node get consecutive new ids, in
+    // file order, so the device needs only the offsets); a node the walk from the root cannot reach
+    // (a parent cycle) is an error
+    std::vector<int32_t> bfs(1, 0);
+    bfs.reserve(n);
+    for (size_t h = 0; h < bfs.size() && (int)bfs.size() <= n; h++) {
+        const int u = bfs[h];
+        for (int q = off[u]; q < off[u + 1]; q++) bfs.push_back(child[q]);
+    }
+    ORB_CHECK_ARG((int)bfs.size() == n, "vocabulary: nodes unreachable from the root");
+    std::vector<int32_t> boff(n + 1, 0);
+    for (int u = 0; u < n; u++) boff[u + 1] = boff[u] + cnt[bfs[u]];   // children of new u: boff[u]+1 ..
     std::vector<uint32_t> word(n, 0);
     int nw = 0, maxc = 0;
     for (int i = 1; i < n; i++)
@@ -265,25 +280,30 @@ int voc_upload(orbv_vocabulary* v, int n, const std::vector<int32_t>& parent, co
     ORB_CHECK_ARG(nw == 0 || cnt[0] > 0, "vocabulary: words but an empty root");
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t r = o; o += align_up(std::max<size_t>(bytes, 1), 256); return r; };
-    const size_t o_off = take((size_t)(n + 1) * 4), o_ch = take((size_t)std::max(n - 1, 1) * 4),
-                 o_d = take((size_t)n * 32), o_w = take((size_t)n * 4), o_wt = take((size_t)n * 8);
+    const size_t o_off = take((size_t)(n + 1) * 4), o_or = take((size_t)n * 4), o_d = take((size_t)n * 32),
+                 o_w = take((size_t)n * 4), o_wt = take((size_t)n * 8);
     int rc;
     if ((rc = v->buf.reserve(o))) return rc;
     char* b = v->buf.as<char>();
     v->child_off = (int32_t*)(b + o_off);
-    v->child = (int32_t*)(b + o_ch);
+    v->orig = (int32_t*)(b + o_or);
     v->desc = (uint8_t*)(b + o_d);
     v->word = (uint32_t*)(b + o_w);
     v->weight = (double*)(b + o_wt);
-    std::vector<uint8_t> dd((size_t)n * 32, 0);
-    std::memcpy(dd.data() + 32, desc + 32, (size_t)(n - 1) * 32);
-    std::vector<double> wt(weight);
-    wt[0] = 0;
-    ORB_HIP_TRY(hipMemcpy(v->child_off, off.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice));
-    if (n > 1) ORB_HIP_TRY(hipMemcpy(v->child, child.data(), (size_t)(n - 1) * 4, hipMemcpyHostToDevice));
+    std::vector<uint8_t> dd((size_t)n * 32, 0);   // the root's descriptor stays zero
+    std::vector<uint32_t> bw(n, 0);
+    std::vector<double> bwt(n, 0.0);
+    for (int u = 1; u < n; u++) {
+        const int i = bfs[u];
+        std::memcpy(dd.data() + (size_t)u * 32, desc + (size_t)i * 32, 32);
+        bw[u] = word[i];
+        bwt[u] = weight[i];
+    }
+    ORB_HIP_TRY(hipMemcpy(v->child_off, boff.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice));
+    ORB_HIP_TRY(hipMemcpy(v->orig, bfs.data(), (size_t)n * 4, hipMemcpyHostToDevice));
     ORB_HIP_TRY(hipMemcpy(v->desc, dd.data(), (size_t)n * 32, hipMemcpyHostToDevice));
-    ORB_HIP_TRY(hipMemcpy(v->word, word.data(), (size_t)n * 4, hipMemcpyHostToDevice));
-    ORB_HIP_TRY(hipMemcpy(v->weight, wt.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    ORB_HIP_TRY(hipMemcpy(v->word, bw.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    ORB_HIP_TRY(hipMemcpy(v->weight, bwt.data(), (size_t)n * 8, hipMemcpyHostToDevice));
     return ORB_OK;
 }
 
@@ -317,7 +337,7 @@ int voc_launch(orbv_vocabulary* v, const uint8_t* d_desc, const int32_t* d_count
     char* w = v->ws.as<char>();
     VocFeat ft{(uint32_t*)w, (double*)(w + align_up(slots * 4, 256) * 2), (uint32_t*)(w + align_up(slots * 4, 256))};
     if (v->n_words > 0) {
-        const VocDev dv{v->child_off, v->child, v->desc, v->word, v->weight, v->L - levelsup};
+        const VocDev dv{v->child_off, v->orig, v->desc, v->word, v->weight, v->L - levelsup};
         if (v->max_children <= 16) {
             const long long thr = (long long)slots * 16;
             hipLaunchKernelGGL(voc_descend_kernel<16>, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, dv,
