@@ -338,7 +338,18 @@ int voc_launch(orbv_vocabulary* v, const uint8_t* d_desc, const int32_t* d_count
     VocFeat ft{(uint32_t*)w, (double*)(w + align_up(slots * 4, 256) * 2), (uint32_t*)(w + align_up(slots * 4, 256))};
     if (v->n_words > 0) {
         const VocDev dv{v->child_off, v->orig, v->desc, v->word, v->weight, v->L - levelsup};
-        if (v->max_children <= 16) {
+        // lanes per descriptor for trees of <= 16 children: 8 (two children per lane at k = 10; more
+        // descents in flight per wavefront than 16: 546k -> 583k frames/s); ORBV_LANES = 4 / 16
+        static const int lanes = [] { const char* e = getenv("ORBV_LANES"); return e ? atoi(e) : 8; }();
+        if (v->max_children <= 16 && lanes == 8) {
+            const long long thr = (long long)slots * 8;
+            hipLaunchKernelGGL(voc_descend_kernel<8>, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, dv,
+                               d_desc, d_counts, cap, n_frames, ft);
+        } else if (v->max_children <= 16 && lanes == 4) {
+            const long long thr = (long long)slots * 4;
+            hipLaunchKernelGGL(voc_descend_kernel<4>, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, dv,
+                               d_desc, d_counts, cap, n_frames, ft);
+        } else if (v->max_children <= 16) {
             const long long thr = (long long)slots * 16;
             hipLaunchKernelGGL(voc_descend_kernel<16>, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, dv,
                                d_desc, d_counts, cap, n_frames, ft);
