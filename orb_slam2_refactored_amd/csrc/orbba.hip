@@ -757,19 +757,20 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
         for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
     }
     // S -> LDS: D = 6 np is even, so every row of S starts 16-byte aligned; lane c of a wavefront
-    // takes the 16-byte piece c of its rows (w, w+4, ...), 16 rows of loads in flight per batch
+    // takes the 16-byte piece c of its rows (w, w+4, ...), 32 rows of loads in flight per batch (one
+    // batch up to D = 128: the solve's wavefronts have the VGPRs to spare here)
     {
         const int npc = D / 2;
         const double2* S2 = reinterpret_cast<const double2*>(b.S);
-        for (int r0 = wv; r0 < D; r0 += 64) {
-            double2 v[16];
+        for (int r0 = wv; r0 < D; r0 += 128) {
+            double2 v[32];
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
+            for (int q = 0; q < 32; q++) {
                 const int r = min(r0 + 4 * q, D - 1);
                 v[q] = lane < npc ? S2[r * npc + lane] : make_double2(0.0, 0.0);
             }
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
+            for (int q = 0; q < 32; q++) {
                 const int r = r0 + 4 * q;
                 if (r < D && lane < npc) {
                     A[r * ld + 2 * lane] = v[q].x;
