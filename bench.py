@@ -43,7 +43,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]   # verbatim
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6    # MI355X spec, FP64 vector (BASELINE.md / SURVEY §8d honest ceiling)
-VALU_PEAK_TOPS = 78.6      # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: wave64 VALU op = 2 clk)
+FP4_PEAK_TFLOPS = 10000.0  # MI355X_MICROARCH.md: FP4 / FP6 MFMA ~10 PF dense
 
 
 # ------------------------------------------------------------------------------------------ helpers
@@ -348,11 +348,13 @@ def c3_leg(dev, local, pairs=128, steps=10, cpu=True, info=None):
                       "frac": fb / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS if fms else 0.0,
                       "algorithmic_bytes_per_launch": fb, "avg_launch_ms": fms,
                       "pipeline_algorithmic_GBs": bytes_pair * pairs / (ms * 1e-3) / 1e9},
-         "triangulation_roofline": {"bound": "valu", "kernel": "tri_all_kernel",
-                                    "achieved": 16 * cand / (tri_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS,
-                                    "unit": "T lane-ops/s", "frac": 16 * cand / (tri_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
-                                    "ops": "16 VALU lane-ops (8 xor + 8 popcount) per query x candidate",
-                                    "int8_mfma_equivalent_TOPS": 512 * cand / (tri_ms * 1e-3) / 1e12}}
+         # tri_mm_kernel: a query x candidate pair is a 256-bit dot product on the FP4 matrix path
+         # (2 x 256 = 512 flops of v_mfma_scale_f32_16x16x128_f8f6f4), plus the d <= TH_LOW events
+         "triangulation_roofline": {"bound": "mfma", "kernel": "tri_mm_kernel",
+                                    "achieved": 512 * cand / (tri_ms * 1e-3) / 1e12, "peak": FP4_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s (FP4)", "frac": 512 * cand / (tri_ms * 1e-3) / 1e12 / FP4_PEAK_TFLOPS,
+                                    "ops": "512 FP4 MFMA flops per query x candidate (256 bits)",
+                                    "pairs_per_launch": cand}}
     if cpu:
         O = oracle()
         p = O.params(2000)
