@@ -2527,9 +2527,24 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.out_frame = std::max(out, 1);
     NC = (int)align_up(std::max(NC, 256), 64);   // >= blockDim: the gather reuses the node scratch
     if (h->debug_nc > 0) NC = (int)align_up(std::max(h->debug_nc, 256), 64);
-    const int PTC = 2048;   // candidate points kept in LDS (P and T) when a level has at most this many (48 KiB in all: 3 WGs per CU)
-    const size_t lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int)) +
-                       (size_t)PTC * 8;
+    // PTC: candidate points kept in LDS (P and T) when a level has at most this many (more: HBM).
+    // Sized for workgroups per CU first: the largest multiple of 64 (<= 2048) that fits 4 of them
+    // in the 160 KiB (123 VGPRs allow 4), else 3, else 2, each with at least 512 points.  At C2
+    // (NC = 448) that is 960 points and 4 workgroups per CU instead of 2048 and 3: quadtree 1.44 ->
+    // 1.14 ms per 2048 pan frames, 3.20 -> 2.82 ms per 1024 textured ones.
+    const size_t node_lds = (size_t)NC * (2 * sizeof(QtNode) + sizeof(int4) + 2 * sizeof(QtItem) + 2 * sizeof(int));
+    int PTC = 2048;
+    {
+        hipFuncAttributes fa{};
+        const size_t stat = hipFuncGetAttributes(&fa, (const void*)quadtree_kernel) == hipSuccess ? fa.sharedSizeBytes : 1024;
+        for (int t = 4; t >= 2; t--) {
+            const long long room = (long long)(160 * 1024 / t) - (long long)stat - (long long)node_lds;
+            const int p = (int)std::min<long long>(2048, room / 8) & ~63;
+            if (p >= 512) { PTC = p; break; }
+        }
+    }
+    if (const char* e = getenv("ORBX_QT_PTC")) PTC = std::max(256, std::min(4096, atoi(e)));   // tuning knob
+    const size_t lds = node_lds + (size_t)PTC * 8;
     if (lds > 156 * 1024) {   // gfx950: 160 KiB LDS per workgroup
         set_error("nfeatures too large for the quadtree LDS budget (per-level quota <= ~2100)");
         return ORB_EINVAL;
