@@ -271,7 +271,10 @@ __device__ __forceinline__ f4v mfma_fp4(i4v a, i4v b, f4v c) {
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 4, 4, 0, FP4_SCALE_A, 0, FP4_SCALE_B);
 }
 
-constexpr int FP_RT = 4;               // 16-row tiles per wavefront (69 -> 114 VGPRs, 4 wavefronts per SIMD)
+#ifndef FP_RT_DEF
+#define FP_RT_DEF 3
+#endif
+constexpr int FP_RT = FP_RT_DEF;       // 16-row tiles per wavefront (89 VGPRs: 5 wavefronts per SIMD; 4 tiles: 114, 4)
 constexpr int FP_WROWS = 16 * FP_RT;
 constexpr int FP_ROWS = 4 * FP_WROWS;
 template <bool MULTI>
