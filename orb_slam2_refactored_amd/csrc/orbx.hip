@@ -869,7 +869,10 @@ __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint
 // One wavefront processes `cpw` consecutive (frame, cell) items of the XCD-swizzled order; item
 // i = f * ncells + cell.  LDS (sized per launch from the largest cell): the crop (zone + 3-px
 // apron), a zone map of corner strengths, a queue of pre-test passers and the ordered corner list.
-__global__ __launch_bounds__(64, 6) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
+#ifndef FAST_WAVES_DEF
+#define FAST_WAVES_DEF 6
+#endif
+__global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
