@@ -225,7 +225,9 @@ int orbm_search_for_triangulation_batch_device(const orbm_tri_batch* b, int32_t*
  * level of the left octave, parabola refinement, and the median-distance outlier filter.
  * Outputs uright[i] / depth[i] (-1 = no match), one per left keypoint.
  * A view is one frame: its keypoints (level-0 coordinates, cv::KeyPoint layout), descriptors and
- * unblurred pyramid levels (GetImagePyramid()). */
+ * unblurred pyramid levels (GetImagePyramid()).  The right keypoints' row table (vRowIndices) is
+ * built on the device for images of at most 4096 rows (ORB_EINVAL above); a row band reaching past
+ * the image is clipped to it (the reference indexes outside vRowIndices there). */
 typedef struct orbm_stereo_view {
     int32_t n;
     const orbx_keypoint* kps;
