@@ -90,6 +90,10 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 __device__ __forceinline__ int popc64(unsigned long long m) { return __popcll(m); }
+// popc(m & lanemask_lt) without a lane mask held in VGPRs: v_mbcnt_lo / v_mbcnt_hi
+__device__ __forceinline__ int rank64(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 __device__ __forceinline__ const uint8_t* level_base(const Geom& g, int l, int f, const uint8_t* in,
                                                       long long in_fstride, int in_step, const uint8_t* pyr,
@@ -887,7 +891,6 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     const int CSd = fl.CS, ZSd = fl.ZS;
 
     const int lane = threadIdx.x;
-    const unsigned long long lt = lanemask_lt();
     const int lb = xcd_swizzle(blockIdx.x, gridDim.x);
     FAST_STAMP(0, __builtin_amdgcn_s_memtime());
     const int i_beg = lb * cpw, i_end = min(i_beg + cpw, n_items);
@@ -965,7 +968,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         const bool c = M > tp;
         const unsigned long long bm = __ballot(c);
         if (c) {
-            const int pos = nc + popc64(bm & lt);
+            const int pos = nc + rank64(bm);
             if (pos < fl.ccap) clist[pos] = (short)i;   // past ccap: the cell takes the zone-scan NMS below
             Mc[__mul24(i >> 8, ZSd) + (i & 255)] = (uint8_t)min(M, 255);
         }
@@ -982,7 +985,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
             pass = min(max(p2, p10), max(p6, p14)) > v + tp || max(min(p2, p10), min(p6, p14)) < v - tp;
         }
         const unsigned long long bm = __ballot(pass);
-        if (pass) queue2[(q2n + popc64(bm & lt)) & (FQ2_RING - 1)] = (short)i;
+        if (pass) queue2[(q2n + rank64(bm)) & (FQ2_RING - 1)] = (short)i;
         q2n += popc64(bm);
         head += n;
         wave_lds_sync();
@@ -1077,7 +1080,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         for (int pp = 0; pp < npass; pp++) {
             const unsigned long long bm = dbal[2 * pp + which];
             if (bm & (1ull << lane)) {
-                const int r = running + popc64(bm & lt);
+                const int r = running + rank64(bm);
                 const int y = pp * RP + zr;
                 if (r < cap)
                     out[r] = (uint32_t)(x0 + 3 + zx) | ((uint32_t)(y0 + 3 + y) << 12) |
@@ -1120,7 +1123,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     for (int jb = 0, ch2 = 0; jb < nc; jb += 64, ch2++) {
         const unsigned long long bm = bal[2 * ch2 + which];
         if (bm & (1ull << lane)) {
-            const int r = running + popc64(bm & lt);
+            const int r = running + rank64(bm);
             const int i = clist[jb + lane];
             if (r < cap) {
                 const int zy = i >> 8, zx = i & 255;
