@@ -37,6 +37,7 @@ constexpr int MAX_ROOTS = 32;
 constexpr int PATCH = 43;               // raw neighbourhood: +-21 (rBRIEF reach 18 + blur 3)
 constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
 constexpr int HBS = 40;                 // LDS row stride of the blurred rows (u16): 20 dwords, 8-byte aligned rows
+static_assert(HBLUR_W + 3 <= HBS, "the blur's fourth-column tiles store up to column 39");
 
 __constant__ float c_pattern[1024] = {   // bit_pattern_31_ (:142-400) as floats (the samples' operands)
 #include "orb_pattern31.inc"
@@ -1184,7 +1185,6 @@ __device__ int4 qt_wave_split(const QtNode& n, const uint32_t* __restrict__ P, u
     int c[4] = {0, 0, 0, 0};
     if (n.cnt <= 512) {
         const int lane = lane_id();
-        const unsigned long long lt = lanemask_lt();
         uint32_t k[8];
         int q[8];
 #pragma unroll
@@ -1208,7 +1208,7 @@ __device__ int4 qt_wave_split(const QtNode& n, const uint32_t* __restrict__ P, u
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
                 const unsigned long long m = __ballot(q[t] == qq);
-                if (q[t] == qq) T[o[qq] + popc64(m & lt)] = k[t];
+                if (q[t] == qq) T[o[qq] + rank64(m)] = k[t];
                 o[qq] += popc64(m);
             }
         }
@@ -1236,7 +1236,7 @@ __device__ int4 qt_wave_split(const QtNode& n, const uint32_t* __restrict__ P, u
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {
             const unsigned long long m = __ballot(q == qq);
-            if (q == qq) T[o[qq] + popc64(m & lanemask_lt())] = k;
+            if (q == qq) T[o[qq] + rank64(m)] = k;
             o[qq] += popc64(m);
         }
     }
@@ -1274,7 +1274,6 @@ __device__ int4 qt_group16_split(const QtNode& n, int cnt, const uint32_t* __res
 constexpr int QT_BIG = 2048;   // phase-1 nodes above this size are split by the whole block
 __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, uint32_t* __restrict__ T, int* sc) {
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const unsigned long long lt = lanemask_lt();
     const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
     const int ym = n.tly + (n.bry - n.tly + 1) / 2;
     auto quad = [&](uint32_t k) { return kp_x(k) < xm ? (kp_y(k) < ym ? 0 : 2) : (kp_y(k) < ym ? 1 : 3); };
@@ -1335,7 +1334,7 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
             int off = o[q[u]];
             for (int uu = 0; uu < u; uu++) off += cq[16 * uu] + cq[16 * uu + 1] + cq[16 * uu + 2] + cq[16 * uu + 3];
             for (int ww = 0; ww < w; ww++) off += cq[16 * u + ww];
-            T[off + popc64(m[u] & lt)] = k[u];
+            T[off + rank64(m[u])] = k[u];
         }
 #pragma unroll
         for (int qq = 0; qq < 4; qq++)
@@ -1429,7 +1428,6 @@ __device__ unsigned long long g_qt_wg[4096 * 2];   // per (frame, level) WG: sta
 __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, int* seg_len, QtItem* tmp,
                               int* lists, int list_cap, int* s_cnt) {
     const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const unsigned long long lt = lanemask_lt();
     if (n <= 0) return;
     int* cur = lists;
     int* nxt = lists + 3 * list_cap;
@@ -1466,14 +1464,14 @@ __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, i
                 const int i = base + lane;
                 const bool f = i < hi && a[i].size <= pv;
                 const unsigned long long m = __ballot(f);
-                if (f) Ls[lo + nl + popc64(m & lt)] = i;
+                if (f) Ls[lo + nl + rank64(m)] = i;
                 nl += popc64(m);
             }
             for (int base = hi - 1; base >= lo; base -= 64) {
                 const int j = base - lane;
                 const bool f = j >= lo && a[j].size >= pv;
                 const unsigned long long m = __ballot(f);
-                if (f) Rs[lo + nr + popc64(m & lt)] = j;
+                if (f) Rs[lo + nr + rank64(m)] = j;
                 nr += popc64(m);
             }
             wave_lds_sync();
@@ -1731,7 +1729,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
             const int r = rid[t];
             for (int q = 0; q < R; q++) {
                 const unsigned long long m = __ballot(r == q);
-                if (r == q) T[o[q] + popc64(m & lanemask_lt())] = k;
+                if (r == q) T[o[q] + rank64(m)] = k;
                 o[q] += popc64(m);
             }
         }
@@ -1749,7 +1747,7 @@ __global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __rest
                 const int r = j < q1 ? root_of(k) : -1;
                 for (int q = 0; q < R; q++) {
                     const unsigned long long m = __ballot(r == q);
-                    if (r == q) T[o[q] + popc64(m & lanemask_lt())] = k;
+                    if (r == q) T[o[q] + rank64(m)] = k;
                     o[q] += popc64(m);
                 }
             }
