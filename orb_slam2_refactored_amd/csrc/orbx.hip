@@ -1093,22 +1093,17 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     for (int jb = 0, ch2 = 0; jb < nc; jb += 64, ch2++) {
         const int j = jb + lane;
         bool ki = false, km = false;
-        if (j < nc) {   // 3x3 NMS at both thresholds from one read of the 8 neighbours
+        if (j < nc) {   // 3x3 NMS at both thresholds from one read of the 8 neighbours: for M > t a
+                        // neighbour q >= M is also > t, so both keep rules are M > t && max(q) < M
             const int i = clist[j];
             const uint8_t* c0 = Mc + __mul24(i >> 8, ZSd) + (i & 255);
             const int m = c0[0];
-            ki = m > th_ini;
-            km = m > th_min;
-#pragma unroll
-            for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                for (int dx = -1; dx <= 1; dx++) {
-                    if (!dx && !dy) continue;
-                    const int q = c0[dy * ZSd + dx];
-                    const bool ge = q >= m;
-                    ki = ki && !(ge && q > th_ini);
-                    km = km && !(ge && q > th_min);
-                }
+            const int n0 = max(max((int)c0[-ZSd - 1], (int)c0[-ZSd]), (int)c0[-ZSd + 1]);
+            const int n1 = max((int)c0[-1], (int)c0[1]);
+            const int n2 = max(max((int)c0[ZSd - 1], (int)c0[ZSd]), (int)c0[ZSd + 1]);
+            const bool top = max(max(n0, n1), n2) < m;
+            ki = top && m > th_ini;
+            km = top && m > th_min;
         }
         const unsigned long long bi = __ballot(ki), bmn = __ballot(km);
         if (lane == 0) { bal[2 * ch2] = bi; bal[2 * ch2 + 1] = bmn; }
