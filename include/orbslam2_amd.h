@@ -218,6 +218,36 @@ typedef struct orbm_tri_batch {
 int orbm_search_for_triangulation_batch_device(const orbm_tri_batch* b, int32_t* d_match12, int32_t* d_nmatches,
                                                void* stream);
 
+/* int ORBmatcher::SearchByBoW(KeyFrame* keyframe, Frame& frame, std::vector<MapPoint*>& matches)
+ * (include/ORBmatcher.h:77, src/ORBmatcher.cc:452-516; callers Tracking.cc TrackReferenceKeyFrame /
+ * Relocalization), batched on HBM-resident extractor slots.  Pair p matches keyframe frame1[p] of
+ * set 1 (NULL: p) against frame p of set 2.  FeatureVectorIterator (:406-450) joins equal node ids;
+ * in a common node every keyframe feature idx1 (ascending, as stored) with mp_valid1 != 0
+ * (GetMapPointMatches()[idx1] non-null and not isBad(); NULL = all valid) scans the node's frame
+ * features that no earlier idx1 claimed (the reference's `if (matches[idx2]) continue`), keeps the
+ * lowest-index best and the second-best distance, and claims bestIdx2 when best <= TH_LOW (50) and
+ * (float)best < nnratio * (float)second.  A frame feature sits in one node only, so the claims of
+ * different nodes are independent and the result is the reference's.  With check_orientation the
+ * rotation-histogram filter (CheckOrientation(keyframe->keypointsUn, frame.keypointsUn, ...),
+ * :249-309, :512-513) erases the matches outside the top bins.  FeatureVectors in
+ * orbv_transform_batch_device's layout (both sets required).  Outputs: d_match[p*cap2 + idx2] =
+ * idx1 (the MapPoint of keyframe feature idx1) or -1 for idx2 < counts2[p]; d_nmatches[p] = the
+ * return value.  Enqueue only on `stream`. */
+typedef struct orbm_bow_batch {
+    int32_t n_pairs;
+    int32_t cap1, cap2;
+    const orbx_keypoint* kps1; const uint8_t* desc1; const uint8_t* mp_valid1;
+    const int32_t* frame1;
+    const orbx_keypoint* kps2; const uint8_t* desc2; const int32_t* counts2;
+    const uint32_t* fv_node1; const int32_t* fv_off1; const int32_t* fv_idx1; const int32_t* fv_n_nodes1;
+    const uint32_t* fv_node2; const int32_t* fv_off2; const int32_t* fv_idx2; const int32_t* fv_n_nodes2;
+    int32_t fv_cap1, fv_cap2;
+    float nnratio;
+    int32_t check_orientation;
+} orbm_bow_batch;
+
+int orbm_search_by_bow_batch_device(const orbm_bow_batch* b, int32_t* d_match, int32_t* d_nmatches, void* stream);
+
 /* Stereo matching.  Replaces ComputeStereoMatches (src/ORBmatcher.cc:72-247, PatchDistance
  * :60-68; called from Frame construction for stereo input, System.cc:458-461): per left keypoint the
  * best right keypoint in the row band (+-2*scale[octave_R] rows), octave +-1 and disparity

@@ -165,6 +165,16 @@ public:
         return n;
     }
 
+    // int SearchByBoW(KeyFrame* keyframe, Frame& frame, std::vector<MapPoint*>& matches)
+    // (src/ORBmatcher.cc:452-516), batched on HBM-resident slots: the batch's nnratio and
+    // check_orientation are taken from this matcher.  Enqueue only; d_match[p*cap2 + idx2] = idx1 or -1
+    // (the caller maps idx1 to keyframe->GetMapPointMatches()[idx1]), d_nmatches[p] = the return value.
+    void SearchByBoWBatch(orbm_bow_batch b, int32_t* d_match, int32_t* d_nmatches, void* stream = nullptr) const {
+        b.nnratio = nnratio_;
+        b.check_orientation = checkOri_ ? 1 : 0;
+        check(orbm_search_by_bow_batch_device(&b, d_match, d_nmatches, stream), "orbm_search_by_bow_batch_device");
+    }
+
     float nnratio() const { return nnratio_; }
     bool checkOrientation() const { return checkOri_; }
 

@@ -1585,6 +1585,72 @@ int oracle_check_orientation(const float* angA, int nA, const float* angB, int32
     return (int)matchIds.size() - reduction;
 }
 
+// SearchByBoW(KeyFrame*, Frame&, matches) (ORBmatcher.cc:452-516), literally: FeatureVectorIterator
+// (:406-450), the greedy `matches[idx2]` skip, best / second-best (:477-498), acceptance (:500) and,
+// with check_ori, CheckOrientation(keyframe->keypointsUn, frame.keypointsUn, matchIds, matches)
+// (:249-309) with matchIds in push order.  kf->has_mappoint = mappoint valid (non-null, !isBad).
+// match[idx2] = idx1 or -1; returns nmatches.
+int oracle_search_by_bow(const orbm_tri_frame* kf, const orbm_tri_frame* fr, float nnratio, int check_ori,
+                         const float* ang_kf, const float* ang_fr, int32_t* match) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    for (int i = 0; i < fr->n; i++) match[i] = -1;
+    int nmatches = 0;
+    std::vector<std::pair<int, int>> matchIds;
+    int a = 0, b = 0;
+    while (a < kf->n_nodes && b < fr->n_nodes) {
+        if (kf->node_id[a] == fr->node_id[b]) {
+            for (int u = kf->node_off[a]; u < kf->node_off[a + 1]; u++) {
+                const int idx1 = kf->indices[u];
+                if (!kf->has_mappoint[idx1]) continue;
+                int bestDist = 256, bestIdx2 = -1, secondBestDist = 256;
+                for (int v = fr->node_off[b]; v < fr->node_off[b + 1]; v++) {
+                    const int idx2 = fr->indices[v];
+                    if (match[idx2] >= 0) continue;
+                    const int dist = hamming(kf->desc + 32 * (size_t)idx1, fr->desc + 32 * (size_t)idx2);
+                    if (dist < bestDist) {
+                        secondBestDist = bestDist;
+                        bestDist = dist;
+                        bestIdx2 = idx2;
+                    } else if (dist < secondBestDist) {
+                        secondBestDist = dist;
+                    }
+                }
+                if (bestDist <= TH_LOW && bestDist < nnratio * secondBestDist) {
+                    match[bestIdx2] = idx1;
+                    nmatches++;
+                    if (check_ori) matchIds.push_back(std::make_pair(idx1, bestIdx2));
+                }
+            }
+            a++; b++;
+        } else if (kf->node_id[a] < fr->node_id[b]) a++;
+        else b++;
+    }
+    if (!check_ori) return nmatches;
+    const float factor = 1.f / HISTO_LENGTH;
+    std::vector<int> hist[HISTO_LENGTH];
+    for (const auto& m : matchIds) {
+        float diff = ang_kf[m.first] - ang_fr[m.second];
+        if (diff < 0) diff += 360;
+        int bin = cv_round(factor * diff);
+        if (bin == HISTO_LENGTH) bin = 0;
+        if (bin < 0 || bin >= HISTO_LENGTH) return -1;   // CV_Assert
+        hist[bin].push_back(m.second);
+    }
+    std::sort(std::begin(hist), std::end(hist),
+              [](const std::vector<int>& l, const std::vector<int>& r) { return l.size() > r.size(); });
+    const size_t max1 = hist[0].size(), max2 = hist[1].size(), max3 = hist[2].size();
+    int eraseBin = 3;
+    if (max2 < 0.1 * max1) eraseBin = 1;
+    else if (max3 < 0.1 * max1) eraseBin = 2;
+    int reduction = 0;
+    for (int bin = eraseBin; bin < HISTO_LENGTH; bin++)
+        for (int i2 : hist[bin]) {
+            match[i2] = -1;
+            reduction++;
+        }
+    return (int)matchIds.size() - reduction;
+}
+
 // SearchForTriangulation (ORBmatcher.cc:768-866), checkOrientation = false.
 int oracle_search_for_triangulation(const orbm_tri_frame* f1, const orbm_tri_frame* f2, const float* F12,
                                     const float* ep2, const float* scale2, const float* sigma2, int only_stereo,

@@ -38,6 +38,17 @@ class TriBatch(C.Structure):
                 ("sigma2", C.c_void_p), ("only_stereo", C.c_int32)]
 
 
+class BowBatch(C.Structure):
+    """orbm_bow_batch (include/orbslam2_amd.h)."""
+    _fields_ = [("n_pairs", C.c_int32), ("cap1", C.c_int32), ("cap2", C.c_int32),
+                ("kps1", C.c_void_p), ("desc1", C.c_void_p), ("mp_valid1", C.c_void_p), ("frame1", C.c_void_p),
+                ("kps2", C.c_void_p), ("desc2", C.c_void_p), ("counts2", C.c_void_p),
+                ("fv_node1", C.c_void_p), ("fv_off1", C.c_void_p), ("fv_idx1", C.c_void_p),
+                ("fv_n_nodes1", C.c_void_p), ("fv_node2", C.c_void_p), ("fv_off2", C.c_void_p),
+                ("fv_idx2", C.c_void_p), ("fv_n_nodes2", C.c_void_p), ("fv_cap1", C.c_int32),
+                ("fv_cap2", C.c_int32), ("nnratio", C.c_float), ("check_orientation", C.c_int32)]
+
+
 class StereoView(C.Structure):
     _fields_ = [("n", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("n_levels", C.c_int32),
                 ("level", C.c_void_p), ("level_rows", C.c_void_p), ("level_cols", C.c_void_p),
@@ -108,6 +119,7 @@ SIGNATURES = {
     "orbm_search_for_triangulation": (C.c_int, [C.POINTER(TriFrame), C.POINTER(TriFrame), VP, VP, VP, VP,
                                                 C.c_int, C.c_int, VP, C.POINTER(I32)]),
     "orbm_search_for_triangulation_batch_device": (C.c_int, [C.POINTER(TriBatch), VP, VP, VP]),
+    "orbm_search_by_bow_batch_device": (C.c_int, [C.POINTER(BowBatch), VP, VP, VP]),
     "orbm_compute_stereo_matches": (C.c_int, [C.POINTER(StereoView), C.POINTER(StereoView), VP, VP, C.c_float,
                                               C.c_float, VP, VP]),
     "orbx_stereo_matches_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, VP, VP, VP, C.c_int, C.c_float,

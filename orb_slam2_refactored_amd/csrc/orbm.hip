@@ -979,6 +979,101 @@ __global__ __launch_bounds__(256) void tri_fv_kernel(TriArgs a, TriTables t) {
     if (lane == 0 && tot) atomicAdd(a.nmatches + p, tot);
 }
 
+// SearchByBoW(KeyFrame*, Frame&) (src/ORBmatcher.cc:452-516).  A frame feature belongs to one
+// FeatureVector node, so the claims (`if (matches[idx2]) continue`, :483) of different common nodes
+// never interact: one wavefront per common node walks the node's keyframe features in stored order
+// (the reference's order inside the node), lanes over the node's frame candidates (64 per chunk).
+// Per query every lane keeps its best key (d << 16 | candidate position: the lowest position wins
+// a tie, as the strict '<' of :488) and its second distance; the wave minimum of the keys is the
+// best, the minimum of the other lanes' bests and the winner's second is secondBestDist (the
+// second order statistic the sequential update produces).  A claim sets the winner lane's bit.
+struct BowArgs {
+    const uint8_t* desc1;
+    const uint8_t* mp1;
+    const int32_t* frame1;
+    const uint8_t* desc2;
+    const uint32_t* fvn1; const int32_t* fvo1; const int32_t* fvi1; const int32_t* fvc1;
+    const uint32_t* fvn2; const int32_t* fvo2; const int32_t* fvi2; const int32_t* fvc2;
+    int cap1, cap2, fvcap1, fvcap2;
+    float nnratio;
+    int32_t* match;
+    int32_t* nmatches;
+};
+constexpr int BOW_MAX_CAND = 64 * 64;   // frame candidates per node: one claim bit per lane and chunk
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void search_by_bow_kernel(BowArgs a) {
+    const int p = blockIdx.y, lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), nwv = gridDim.x * 4;
+    const int f1 = a.frame1 ? a.frame1[p] : p;
+    const int nn1 = a.fvc1[f1], nn2 = a.fvc2[p];
+    const uint32_t* node1 = a.fvn1 + (long long)f1 * a.fvcap1;
+    const uint32_t* node2 = a.fvn2 + (long long)p * a.fvcap2;
+    const int32_t* off1 = a.fvo1 + (long long)f1 * (a.fvcap1 + 1);
+    const int32_t* off2 = a.fvo2 + (long long)p * (a.fvcap2 + 1);
+    const int32_t* idx1 = a.fvi1 + (long long)f1 * a.fvcap1;
+    const int32_t* idx2 = a.fvi2 + (long long)p * a.fvcap2;
+    const long long base1 = (long long)f1 * a.cap1, base2 = (long long)p * a.cap2;
+    const uint4* D1 = reinterpret_cast<const uint4*>(a.desc1);
+    const uint4* D2 = reinterpret_cast<const uint4*>(a.desc2);
+    int32_t* out = a.match + base2;
+    int found = 0;
+    for (int na = wv; na < nn1; na += nwv) {
+        const uint32_t id = node1[na];
+        int lo = 0, hi = nn2;   // lower_bound (the iterator's join, :419-442)
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (node2[mid] < id) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo >= nn2 || node2[lo] != id) continue;
+        const int c0 = off2[lo], n2 = min(off2[lo + 1] - c0, BOW_MAX_CAND);
+        const int nch = (n2 + 63) >> 6;
+        unsigned long long claimed = 0;   // bit k: candidate 64k + lane
+        for (int u = off1[na]; u < off1[na + 1]; u++) {
+            const int i1 = idx1[u];
+            const long long g1 = base1 + i1;
+            if (a.mp1 && !a.mp1[g1]) continue;   // !mappoint1 || mappoint1->isBad() (:472)
+            const uint4 q0 = D1[2 * g1], q1 = D1[2 * g1 + 1];
+            uint32_t k1 = 0xffffffffu;
+            int d2 = 256;
+            for (int k = 0; k < nch; k++) {
+                const int pos = 64 * k + lane;
+                if (pos < n2 && !((claimed >> k) & 1ull)) {
+                    const long long g2 = base2 + idx2[c0 + pos];
+                    const int d = hamming8(q0, q1, D2[2 * g2], D2[2 * g2 + 1]);
+                    const uint32_t key = ((uint32_t)d << 16) | (uint32_t)pos;
+                    if (key < k1) {
+                        d2 = min(d2, (int)(k1 >> 16));
+                        k1 = key;
+                    } else if (d < d2) {
+                        d2 = d;
+                    }
+                }
+            }
+            const uint32_t K = wave_min_u32(k1);
+            if (K == 0xffffffffu) continue;   // no unclaimed candidate: bestDist stays 256
+            const int sd = (int)wave_min_u32((uint32_t)(k1 == K ? d2 : min((int)(k1 >> 16), 256)));
+            const int bd = (int)(K >> 16);
+            if (bd <= 50 && (float)bd < a.nnratio * (float)sd) {   // :500
+                const int pos = (int)(K & 0xffffu);
+                if ((pos & 63) == lane) {
+                    claimed |= 1ull << (pos >> 6);
+                    out[idx2[c0 + pos]] = i1;
+                    found++;
+                }
+            }
+        }
+    }
+    const int tot = __reduce_add_sync(~0ull, found);
+    if (lane == 0 && tot) atomicAdd(a.nmatches + p, tot);
+}
+
 }  // namespace orbamd
 
 using namespace orbamd;
@@ -1096,6 +1191,36 @@ int orbm_check_orientation(const float* angA, int nA, const float* angB, int nB,
     int32_t nm = 0;
     ORB_HIP_TRY(hipMemcpy(&nm, dM + nA + 1, 4, hipMemcpyDeviceToHost));
     if (nmatches) *nmatches = nm;
+    return ORB_OK;
+}
+
+int orbm_search_by_bow_batch_device(const orbm_bow_batch* b, int32_t* d_match, int32_t* d_nmatches, void* stream) {
+    ORB_CHECK_ARG(b && d_match && d_nmatches, "null argument");
+    ORB_CHECK_ARG(b->n_pairs >= 0 && b->cap1 > 0 && b->cap2 > 0, "bad pair count / capacities");
+    if (b->n_pairs == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->n_pairs <= 65535, "too many pairs in one launch");
+    ORB_CHECK_ARG(b->cap2 <= BOW_MAX_CAND, "SearchByBoW: frame capacity above 4096 keypoints");
+    ORB_CHECK_ARG(b->desc1 && b->desc2 && b->counts2, "null keyframe / frame arrays");
+    ORB_CHECK_ARG(b->fv_node1 && b->fv_off1 && b->fv_idx1 && b->fv_n_nodes1 && b->fv_node2 && b->fv_off2 && b->fv_idx2 &&
+                      b->fv_n_nodes2 && b->fv_cap1 > 0 && b->fv_cap2 > 0,
+                  "SearchByBoW needs both FeatureVectors");
+    ORB_CHECK_ARG(!b->check_orientation || (b->kps1 && b->kps2), "CheckOrientation needs the keypoint slots");
+    BowArgs a{b->desc1, b->mp_valid1, b->frame1, b->desc2, b->fv_node1, b->fv_off1, b->fv_idx1, b->fv_n_nodes1,
+              b->fv_node2, b->fv_off2, b->fv_idx2, b->fv_n_nodes2, b->cap1, b->cap2, b->fv_cap1, b->fv_cap2, b->nnratio,
+              d_match, d_nmatches};
+    hipStream_t st = (hipStream_t)stream;
+    ORB_HIP_TRY(hipMemsetAsync(d_nmatches, 0, (size_t)b->n_pairs * 4, st));
+    ORB_HIP_TRY(hipMemsetAsync(d_match, 0xff, (size_t)b->n_pairs * b->cap2 * 4, st));
+    const int gx = (std::min(b->fv_cap1, 256) + 3) / 4;   // wavefronts stride over the keyframe's nodes
+    hipLaunchKernelGGL(search_by_bow_kernel, dim3((unsigned)gx, (unsigned)b->n_pairs), dim3(256), 0, st, a);
+    ORB_HIP_TRY(hipGetLastError());
+    if (b->check_orientation) {
+        // CheckOrientation(keyframe->keypointsUn, frame.keypointsUn, matchIds, matches) (:512-513) on the
+        // frame-indexed result: bin of angle1[idx1] - angle2[idx2], matches[idx2] erased
+        hipLaunchKernelGGL(check_orientation_kernel, dim3((unsigned)b->n_pairs), dim3(256), 0, st, &b->kps2[0].angle, 7,
+                           b->cap2, b->counts2, &b->kps1[0].angle, 7, b->cap1, b->frame1, d_match, b->cap2, d_nmatches);
+        ORB_HIP_TRY(hipGetLastError());
+    }
     return ORB_OK;
 }
 

@@ -155,6 +155,36 @@ def search_for_triangulation_batch_device(kps1, desc1, counts1, kps2, desc2, cou
     return out
 
 
+def search_by_bow_batch_device(kps1, desc1, fv1, kps2, desc2, counts2, fv2, frame1=None, mp_valid1=None,
+                               nnratio: float = 0.6, checkOri: bool = True, out=None, stream=None):
+    """Batched SearchByBoW(KeyFrame*, Frame&, matches) (src/ORBmatcher.cc:452-516) on extract_batch_device
+    slots: pair p matches keyframe frame1[p] of set 1 (int32 [P] tensor, default p) against frame p of
+    set 2.  kps*/desc* [F, cap, 7] / [F, cap, 32]; counts2 [P]; fv1 / fv2 = (node, off, idx, n_nodes)
+    from ORBVocabulary.transform_batch_device; mp_valid1 uint8 [F1, cap1] (MapPoint non-null and not
+    bad; None = all valid).  checkOri applies CheckOrientation (:512-513).  Returns (match [P, cap2]
+    int32 = keyframe feature idx1 or -1 per frame feature, nmatches [P])."""
+    import torch
+    from ._lib import BowBatch
+    P = int(counts2.shape[0])
+    cap1, cap2 = int(desc1.shape[1]), int(desc2.shape[1])
+    for k, d in ((kps1, desc1), (kps2, desc2)):
+        if k.dim() != 3 or k.shape[2] != 7 or d.shape[:2] != k.shape[:2] or d.shape[2] != 32 or \
+                not k.is_contiguous() or not d.is_contiguous():
+            raise ValueError("keypoint / descriptor slots must be contiguous [F, cap, 7] / [F, cap, 32]")
+    if desc2.shape[0] < P:
+        raise ValueError("set 2 needs one frame per pair")
+    if out is None:
+        out = (torch.empty((P, cap2), dtype=torch.int32, device=desc2.device),
+               torch.empty((P,), dtype=torch.int32, device=desc2.device))
+    opt = lambda t: tptr(t) if t is not None else None   # noqa: E731
+    b = BowBatch(P, cap1, cap2, tptr(kps1), tptr(desc1), opt(mp_valid1), opt(frame1), tptr(kps2), tptr(desc2),
+                 tptr(counts2), *[tptr(t) for t in fv1], *[tptr(t) for t in fv2], int(fv1[0].shape[1]),
+                 int(fv2[0].shape[1]), float(nnratio), int(bool(checkOri)))
+    check(lib().orbm_search_by_bow_batch_device(C.byref(b), tptr(out[0]), tptr(out[1]), stream_ptr(stream)),
+          "orbm_search_by_bow_batch_device")
+    return out
+
+
 def _angles(kps):
     """float32 angles from a KP_DTYPE keypoint array, an [N, 7] slot array or a plain angle array."""
     from ._lib import KP_DTYPE

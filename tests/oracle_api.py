@@ -201,6 +201,17 @@ def search_for_triangulation(f1, f2, F12, ep2, scale2, sigma2, only_stereo=False
     return out, n
 
 
+def search_by_bow(kf, fr, ang_kf, ang_fr, nnratio=0.6, check_ori=True):
+    """SearchByBoW(KeyFrame*, Frame&) (ORBmatcher.cc:452-516): kf / fr are tri_frame structs (kf's
+    has_mappoint = MapPoint valid).  Returns (match [fr.n] = idx1 or -1, nmatches)."""
+    keep = _Keep()
+    out = np.zeros(max(fr.n, 1), np.int32)
+    n = lib().oracle_search_by_bow(C.byref(kf), C.byref(fr), C.c_float(nnratio), int(check_ori),
+                                   keep(ang_kf, np.float32), keep(ang_fr, np.float32), ptr(out))
+    assert n >= 0, "bin out of range"
+    return out[:fr.n], n
+
+
 def ba_problem(keep, prob):
     return BAProblem(len(prob["pose_R"]), keep(prob["pose_R"], np.float64), keep(prob["pose_t"], np.float64),
                      keep(prob["pose_fixed"], np.uint8), len(prob["points"]), keep(prob["points"], np.float64),

@@ -1,0 +1,144 @@
+"""SearchByBoW(KeyFrame*, Frame&) (src/ORBmatcher.cc:452-516) on the device, fed by extract_batch_device
+and orbv_transform_batch_device, against the oracle's literal restatement (FeatureVectorIterator,
+greedy `matches[idx2]` claims, best / second-best, ratio, CheckOrientation).  Exact match arrays
+and counts.  Nodes of <= 64 candidates (levelsup 2) and of several 64-candidate chunks (levelsup 3),
+MapPoint validity masks, a keyframe shared by several frames and unrelated pairs (CheckOrientation
+over many bins)."""
+import numpy as np
+import pytest
+
+from orb_slam2_refactored_amd import ORBextractor
+from orb_slam2_refactored_amd.matcher import search_by_bow_batch_device
+from orb_slam2_refactored_amd.synth import make_vocabulary, pan_sequence
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(levelsup, n=6, seed=4400):
+    import torch
+    from orb_slam2_refactored_amd.vocabulary import ORBVocabulary
+    frames = torch.from_numpy(pan_sequence(seed, 640, 480, n)).cuda()
+    ex = ORBextractor(ORBextractor.Parameters(1000))
+    kps, desc, cnt = ex.extract_batch_device(frames)
+    voc = make_vocabulary(31, L=4, k=6)
+    g = ORBVocabulary.from_arrays(voc["k"], voc["L"], voc["scoring"], voc["weighting"], voc["parent"],
+                                  voc["is_leaf"], voc["desc"], voc["weight"])
+    bow = g.transform_batch_device(desc, cnt, levelsup=levelsup)
+    fv = (bow["fv_node"], bow["fv_off"], bow["fv_idx"], bow["n_nodes"])
+    return kps, desc, cnt, fv
+
+
+def _host_frame(O, keep, K, D, N, fv, f, mp=None):
+    node, off, idx, nn = fv
+    n = int(N[f])
+    k = int(nn[f])
+    o = off[f, :k + 1]
+    kk = K[f, :n].view(np.float32)
+    has = np.ones(n, np.uint8) if mp is None else mp[f, :n]
+    return O.tri_frame(keep, np.ascontiguousarray(kk[:, :2]), np.ascontiguousarray(kk[:, 5]).view(np.int32),
+                       np.full(n, -1, np.float32), has, D[f, :n], node[f, :k].astype(np.uint32), o, idx[f, :o[-1]])
+
+
+@pytest.mark.parametrize("levelsup", [2, 3])
+@pytest.mark.parametrize("check_ori", [False, True])
+@pytest.mark.parametrize("masked", [False, True])
+def test_search_by_bow_vs_oracle(oracle, levelsup, check_ori, masked):
+    import torch
+    kps, desc, cnt, fv = _setup(levelsup)
+    F = desc.shape[0]
+    P = F - 1
+    # pair p: keyframe frame1[p] against frame p + 1 (set 2 = frames 1..F-1); predecessors, one keyframe
+    # shared by two frames and an unrelated pair
+    f1 = np.array([0, 1, 1, 3, 0][:P], np.int32)
+    frame1 = torch.from_numpy(f1).cuda()
+    mp = None
+    if masked:
+        rng = np.random.default_rng(levelsup)
+        mp = (rng.random((F, desc.shape[1])) < 0.7).astype(np.uint8)
+    mpt = torch.from_numpy(mp).cuda() if mp is not None else None
+    fv2 = tuple(t[1:].contiguous() for t in fv)
+    m, nm = search_by_bow_batch_device(kps, desc, fv, kps[1:], desc[1:], cnt[1:].contiguous(), fv2, frame1=frame1,
+                                       mp_valid1=mpt, checkOri=check_ori)
+    torch.cuda.synchronize()
+    K, D, N = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+    M, NM = m.cpu().numpy(), nm.cpu().numpy()
+    fvh = tuple(t.cpu().numpy() for t in fv)
+    assert fvh[3].min() > 1
+    if levelsup == 3:   # several 64-candidate chunks per node
+        assert max(np.diff(fvh[1][f, :fvh[3][f] + 1]).max() for f in range(F)) > 64
+    total = 0
+    for p in range(P):
+        keep = oracle._Keep()
+        kf = _host_frame(oracle, keep, K, D, N, fvh, int(f1[p]), mp)
+        fr = _host_frame(oracle, keep, K, D, N, fvh, p + 1)
+        ang_kf = K[f1[p], :N[f1[p]]].view(np.float32)[:, 3]
+        ang_fr = K[p + 1, :N[p + 1]].view(np.float32)[:, 3]
+        exp, n = oracle.search_by_bow(kf, fr, ang_kf, ang_fr, 0.6, check_ori)
+        assert np.array_equal(M[p, :N[p + 1]], exp), p
+        assert NM[p] == n, (p, NM[p], n)
+        total += n
+    assert total > 0
+
+
+def test_search_by_bow_greedy_claims(oracle):
+    """Six identical keyframe descriptors in one node against ten frame candidates at distinct
+    distances: each query takes the best candidate the earlier queries left (the reference's
+    `if (matches[idx2]) continue`), the query without a valid MapPoint is skipped, and equal best
+    distances (second == best) fail the ratio test."""
+    import torch
+    cap1, cap2 = 8, 16
+    dist = [9, 5, 7, 6, 8, 12, 11, 10, 13, 14]
+    D2 = np.zeros((1, cap2, 32), np.uint8)
+    for j, d in enumerate(dist):
+        bits = np.zeros(256, np.uint8)
+        bits[(np.arange(d) * 37 + j) % 256] = 1
+        D2[0, j] = np.packbits(bits)
+    D1 = np.zeros((1, cap1, 32), np.uint8)
+    mp = np.ones((1, cap1), np.uint8)
+    mp[0, 2] = 0
+    K1 = np.zeros((1, cap1, 7), np.int32)
+    K2 = np.zeros((1, cap2, 7), np.int32)
+
+    def fv(cap, n):
+        node = np.zeros((1, cap), np.int32)
+        node[0, 0] = 7
+        off = np.zeros((1, cap + 1), np.int32)
+        off[0, 1] = n
+        idx = np.zeros((1, cap), np.int32)
+        idx[0, :n] = np.arange(n)
+        return node, off, idx, np.ones(1, np.int32)
+
+    fv1, fv2 = fv(cap1, 6), fv(cap2, len(dist))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    cnt2 = np.array([len(dist)], np.int32)
+    for ratio in (0.99, 0.6):
+        m, nm = search_by_bow_batch_device(t(K1), t(D1), tuple(map(t, fv1)), t(K2), t(D2), t(cnt2),
+                                           tuple(map(t, fv2)), mp_valid1=t(mp), nnratio=ratio, checkOri=False)
+        torch.cuda.synchronize()
+        keep = oracle._Keep()
+        z1, z2 = np.zeros(cap1, np.float32), np.zeros(len(dist), np.float32)
+        kf = oracle.tri_frame(keep, np.zeros((6, 2), np.float32), np.zeros(6, np.int32), z1[:6], mp[0, :6], D1[0, :6],
+                              fv1[0][0, :1].astype(np.uint32), fv1[1][0, :2], fv1[2][0, :6])
+        fr = oracle.tri_frame(keep, np.zeros((10, 2), np.float32), np.zeros(10, np.int32), z2, np.zeros(10, np.uint8),
+                              D2[0, :10], fv2[0][0, :1].astype(np.uint32), fv2[1][0, :2], fv2[2][0, :10])
+        exp, n = oracle.search_by_bow(kf, fr, z1[:6], z2, ratio, False)
+        got = m[0, :len(dist)].cpu().numpy()
+        assert np.array_equal(got, exp) and int(nm[0]) == n, (ratio, got, exp)
+        if ratio == 0.99:   # queries 0, 1, 3, 4, 5 take distances 5, 6, 7, 8, 9 in turn
+            assert n == 5 and [int(got[j]) for j in (1, 3, 2, 4, 0)] == [0, 1, 3, 4, 5]
+
+
+def test_search_by_bow_rejects_bad_args():
+    import torch
+    from orb_slam2_refactored_amd._lib import OrbError
+    k = torch.zeros((1, 8, 7), dtype=torch.int32, device="cuda")
+    d = torch.zeros((1, 8, 32), dtype=torch.uint8, device="cuda")
+    c = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fv = (torch.zeros((1, 4), dtype=torch.int32, device="cuda"), torch.zeros((1, 5), dtype=torch.int32, device="cuda"),
+          torch.zeros((1, 4), dtype=torch.int32, device="cuda"), torch.zeros(1, dtype=torch.int32, device="cuda"))
+    big = torch.zeros((1, 5000, 7), dtype=torch.int32, device="cuda")
+    bigd = torch.zeros((1, 5000, 32), dtype=torch.uint8, device="cuda")
+    with pytest.raises(OrbError):   # frame capacity above the per-node claim bits
+        search_by_bow_batch_device(k, d, fv, big, bigd, c, fv)
+    with pytest.raises(ValueError):
+        search_by_bow_batch_device(k, d[:, :4], fv, k, d, c, fv)
