@@ -539,6 +539,66 @@ def bow_leg(dev, local, frames=128, n=2000, steps=10, cpu=True):
             k += 1
         r["cpu_baseline"] = {"frames_per_s": k / (time.perf_counter() - t0), "cores": 1, "kind": "port",
                              "sample": f"{n}-descriptor sets, oracle/orb_oracle.cpp, 1 thread"}
+    r["search_by_bow"] = search_by_bow_leg(dev, X, out, voc, steps, cpu)
+    return r
+
+
+def search_by_bow_leg(dev, X, fv1_out, voc, steps, cpu):
+    """SearchByBoW(KeyFrame*, Frame&) (ORBmatcher.cc:452-516): pair p = keyframe p (the bow leg's
+    descriptors) against a frame holding the same features with 8 of 256 bits flipped, both
+    FeatureVectors from the device transform (levelsup 4), CheckOrientation on (random angles)."""
+    import torch
+    from orb_slam2_refactored_amd.matcher import search_by_bow_batch_device
+    frames, n = X.shape[0], X.shape[1]
+    rng = np.random.default_rng(33)
+    flip = np.zeros((frames, n, 256), np.uint8)
+    pos = rng.integers(0, 256, size=(frames, n, 8))
+    np.put_along_axis(flip, pos, 1, axis=2)
+    X2 = X ^ np.packbits(flip, axis=2)
+    desc1 = torch.from_numpy(X).to(dev)
+    desc2 = torch.from_numpy(X2).to(dev)
+    counts = torch.full((frames,), n, dtype=torch.int32, device=dev)
+    fv2_out = voc.transform_batch_device(desc2, counts)
+    kp = np.zeros((frames, n, 7), np.float32)
+    kp[:, :, 3] = rng.random((frames, n)) * 360
+    kp2 = kp.copy()
+    kp2[:, :, 3] = (kp[:, :, 3] + rng.normal(0, 3, (frames, n))) % 360
+    kps1 = torch.from_numpy(kp.view(np.int32)).to(dev)
+    kps2 = torch.from_numpy(kp2.view(np.int32)).to(dev)
+    fv = lambda o: (o["fv_node"], o["fv_off"], o["fv_idx"], o["n_nodes"])   # noqa: E731
+    out = search_by_bow_batch_device(kps1, desc1, fv(fv1_out), kps2, desc2, counts, fv(fv2_out), checkOri=True)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    ms = event_ms(lambda: search_by_bow_batch_device(kps1, desc1, fv(fv1_out), kps2, desc2, counts, fv(fv2_out),
+                                                     checkOri=True, out=out), steps, st)
+    r = {"workload": f"{frames} (keyframe, frame) pairs x {n} features, FeatureVectors at levelsup 4 of the "
+                     "k 10 L 6 vocabulary, 8-bit-flipped frame descriptors, CheckOrientation on",
+         "pairs_per_s": frames / (ms * 1e-3), "ms_per_step": ms,
+         "mean_matches": float(out[1].double().mean().item())}
+    if cpu:
+        O = oracle()
+        h1 = [t.cpu().numpy() for t in fv(fv1_out)]
+        h2 = [t.cpu().numpy() for t in fv(fv2_out)]
+
+        def frame(keep, h, D, p, mp):
+            node, off, idx, nn = h
+            k = int(nn[p])
+            o = off[p, :k + 1]
+            z = np.zeros(n, np.float32)
+            return O.tri_frame(keep, np.zeros((n, 2), np.float32), np.zeros(n, np.int32), z, mp, D[p],
+                               node[p, :k].astype(np.uint32), o, idx[p, :o[-1]])
+
+        ones = np.ones(n, np.uint8)
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 3.0 or k < 8:
+            p = k % frames
+            keep = O._Keep()
+            O.search_by_bow(frame(keep, h1, X, p, ones), frame(keep, h2, X2, p, ones), kp[p, :, 3], kp2[p, :, 3],
+                            0.6, True)
+            k += 1
+        r["cpu_baseline"] = {"pairs_per_s": k / (time.perf_counter() - t0), "cores": 1, "kind": "port",
+                             "sample": "single pairs, oracle/orb_oracle.cpp, 1 thread (FeatureVectors given)"}
     return r
 
 
