@@ -244,9 +244,24 @@ typedef struct orbm_bow_batch {
     int32_t fv_cap1, fv_cap2;
     float nnratio;
     int32_t check_orientation;
+    /* KeyFrame-KeyFrame form only (NULL in the Frame form): */
+    const int32_t* counts1;      /* kf1 keypoint counts (CheckOrientation) */
+    const uint8_t* mp_valid2;    /* kf2 MapPoint valid (NULL: all) */
+    const int32_t* frame2;       /* kf2 slot of pair p (NULL: p) */
 } orbm_bow_batch;
 
 int orbm_search_by_bow_batch_device(const orbm_bow_batch* b, int32_t* d_match, int32_t* d_nmatches, void* stream);
+
+/* int ORBmatcher::SearchByBoW(KeyFrame* keyframe1, KeyFrame* keyframe2, std::vector<MapPoint*>& matches12)
+ * (include/ORBmatcher.h:78, src/ORBmatcher.cc:696-766) on the same batch layout: pair p = (kf1
+ * frame1[p] of set 1, kf2 frame2[p] of set 2).  Differences from the Frame form: candidates need a
+ * valid kf2 MapPoint (mp_valid2) besides being unclaimed (matched2, :733), acceptance is
+ * bestDist < TH_LOW (strict, :750), the result is indexed by idx1 (d_match12[p*cap1 + idx1] = idx2,
+ * i.e. matches12[idx1] = mappoints2[idx2]) and CheckOrientation(keypoints2, keypoints1, ...)
+ * (:762-763) bins angle2[idx2] - angle1[idx1] and erases matches12[idx1] (needs counts1).
+ * Enqueue only on `stream`. */
+int orbm_search_by_bow_kf_batch_device(const orbm_bow_batch* b, int32_t* d_match12, int32_t* d_nmatches,
+                                       void* stream);
 
 /* Stereo matching.  Replaces ComputeStereoMatches (src/ORBmatcher.cc:72-247, PatchDistance
  * :60-68; called from Frame construction for stereo input, System.cc:458-461): per left keypoint the

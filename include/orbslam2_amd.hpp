@@ -175,6 +175,15 @@ public:
         check(orbm_search_by_bow_batch_device(&b, d_match, d_nmatches, stream), "orbm_search_by_bow_batch_device");
     }
 
+    // int SearchByBoW(KeyFrame* keyframe1, KeyFrame* keyframe2, std::vector<MapPoint*>& matches12)
+    // (src/ORBmatcher.cc:696-766), batched: d_match12[p*cap1 + idx1] = idx2 or -1.
+    void SearchByBoWKeyFramesBatch(orbm_bow_batch b, int32_t* d_match12, int32_t* d_nmatches,
+                                   void* stream = nullptr) const {
+        b.nnratio = nnratio_;
+        b.check_orientation = checkOri_ ? 1 : 0;
+        check(orbm_search_by_bow_kf_batch_device(&b, d_match12, d_nmatches, stream), "orbm_search_by_bow_kf_batch_device");
+    }
+
     float nnratio() const { return nnratio_; }
     bool checkOrientation() const { return checkOri_; }
 

@@ -1651,6 +1651,73 @@ int oracle_search_by_bow(const orbm_tri_frame* kf, const orbm_tri_frame* fr, flo
     return (int)matchIds.size() - reduction;
 }
 
+// SearchByBoW(KeyFrame* keyframe1, KeyFrame* keyframe2, matches12) (ORBmatcher.cc:696-766), literally:
+// candidates need an unclaimed idx2 with a valid MapPoint (:733), bestDist < TH_LOW (:750), matches12 by
+// idx1, CheckOrientation(keypoints2, keypoints1, matchIds = (bestIdx2, idx1), matches12) (:762-763).
+// kf1/kf2->has_mappoint = MapPoint valid.  match12[idx1] = idx2 or -1; returns nmatches.
+int oracle_search_by_bow_kf(const orbm_tri_frame* kf1, const orbm_tri_frame* kf2, float nnratio, int check_ori,
+                            const float* ang1, const float* ang2, int32_t* match12) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    for (int i = 0; i < kf1->n; i++) match12[i] = -1;
+    std::vector<char> matched2(kf2->n, 0);
+    int nmatches = 0;
+    std::vector<std::pair<int, int>> matchIds;
+    int a = 0, b = 0;
+    while (a < kf1->n_nodes && b < kf2->n_nodes) {
+        if (kf1->node_id[a] == kf2->node_id[b]) {
+            for (int u = kf1->node_off[a]; u < kf1->node_off[a + 1]; u++) {
+                const int idx1 = kf1->indices[u];
+                if (!kf1->has_mappoint[idx1]) continue;
+                int bestDist = 256, bestIdx2 = -1, secondBestDist = 256;
+                for (int v = kf2->node_off[b]; v < kf2->node_off[b + 1]; v++) {
+                    const int idx2 = kf2->indices[v];
+                    if (matched2[idx2] || !kf2->has_mappoint[idx2]) continue;
+                    const int dist = hamming(kf1->desc + 32 * (size_t)idx1, kf2->desc + 32 * (size_t)idx2);
+                    if (dist < bestDist) {
+                        secondBestDist = bestDist;
+                        bestDist = dist;
+                        bestIdx2 = idx2;
+                    } else if (dist < secondBestDist) {
+                        secondBestDist = dist;
+                    }
+                }
+                if (bestDist < TH_LOW && bestDist < nnratio * secondBestDist) {
+                    match12[idx1] = bestIdx2;
+                    matched2[bestIdx2] = 1;
+                    nmatches++;
+                    if (check_ori) matchIds.push_back(std::make_pair(bestIdx2, idx1));
+                }
+            }
+            a++; b++;
+        } else if (kf1->node_id[a] < kf2->node_id[b]) a++;
+        else b++;
+    }
+    if (!check_ori) return nmatches;
+    const float factor = 1.f / HISTO_LENGTH;
+    std::vector<int> hist[HISTO_LENGTH];
+    for (const auto& m : matchIds) {   // keypoint1 = keypoints2[bestIdx2], keypoint2 = keypoints1[idx1]
+        float diff = ang2[m.first] - ang1[m.second];
+        if (diff < 0) diff += 360;
+        int bin = cv_round(factor * diff);
+        if (bin == HISTO_LENGTH) bin = 0;
+        if (bin < 0 || bin >= HISTO_LENGTH) return -1;
+        hist[bin].push_back(m.second);
+    }
+    std::sort(std::begin(hist), std::end(hist),
+              [](const std::vector<int>& l, const std::vector<int>& r) { return l.size() > r.size(); });
+    const size_t max1 = hist[0].size(), max2 = hist[1].size(), max3 = hist[2].size();
+    int eraseBin = 3;
+    if (max2 < 0.1 * max1) eraseBin = 1;
+    else if (max3 < 0.1 * max1) eraseBin = 2;
+    int reduction = 0;
+    for (int bin = eraseBin; bin < HISTO_LENGTH; bin++)
+        for (int i1 : hist[bin]) {
+            match12[i1] = -1;
+            reduction++;
+        }
+    return (int)matchIds.size() - reduction;
+}
+
 // SearchForTriangulation (ORBmatcher.cc:768-866), checkOrientation = false.
 int oracle_search_for_triangulation(const orbm_tri_frame* f1, const orbm_tri_frame* f2, const float* F12,
                                     const float* ep2, const float* scale2, const float* sigma2, int only_stereo,

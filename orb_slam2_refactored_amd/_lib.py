@@ -46,7 +46,8 @@ class BowBatch(C.Structure):
                 ("fv_node1", C.c_void_p), ("fv_off1", C.c_void_p), ("fv_idx1", C.c_void_p),
                 ("fv_n_nodes1", C.c_void_p), ("fv_node2", C.c_void_p), ("fv_off2", C.c_void_p),
                 ("fv_idx2", C.c_void_p), ("fv_n_nodes2", C.c_void_p), ("fv_cap1", C.c_int32),
-                ("fv_cap2", C.c_int32), ("nnratio", C.c_float), ("check_orientation", C.c_int32)]
+                ("fv_cap2", C.c_int32), ("nnratio", C.c_float), ("check_orientation", C.c_int32),
+                ("counts1", C.c_void_p), ("mp_valid2", C.c_void_p), ("frame2", C.c_void_p)]
 
 
 class StereoView(C.Structure):
@@ -120,6 +121,7 @@ SIGNATURES = {
                                                 C.c_int, C.c_int, VP, C.POINTER(I32)]),
     "orbm_search_for_triangulation_batch_device": (C.c_int, [C.POINTER(TriBatch), VP, VP, VP]),
     "orbm_search_by_bow_batch_device": (C.c_int, [C.POINTER(BowBatch), VP, VP, VP]),
+    "orbm_search_by_bow_kf_batch_device": (C.c_int, [C.POINTER(BowBatch), VP, VP, VP]),
     "orbm_compute_stereo_matches": (C.c_int, [C.POINTER(StereoView), C.POINTER(StereoView), VP, VP, C.c_float,
                                               C.c_float, VP, VP]),
     "orbx_stereo_matches_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, VP, VP, VP, C.c_int, C.c_float,

@@ -467,12 +467,13 @@ __device__ __forceinline__ int rot_bin(float angB, float angA) {
 __global__ __launch_bounds__(256) void check_orientation_kernel(
     const float* __restrict__ angA, int kstrideA, int capA, const int32_t* __restrict__ nA_arr,
     const float* __restrict__ angB, int kstrideB, int capB, const int32_t* __restrict__ pair_b,
-    int32_t* __restrict__ match, int strideM, int32_t* __restrict__ nmatch) {
+    int32_t* __restrict__ match, int strideM, int32_t* __restrict__ nmatch, const int32_t* __restrict__ pair_a) {
     __shared__ int hist[HISTO_LENGTH];
     __shared__ uint32_t keep;
     const int p = blockIdx.x, q = pair_b ? pair_b[p] : p, tid = threadIdx.x;
-    const int n = nA_arr[p];
-    const float* aA = angA + (long long)p * capA * kstrideA;
+    const int pa = pair_a ? pair_a[p] : p;   // A frame of pair p (SearchByBoW(KeyFrame, KeyFrame): kf1 slots)
+    const int n = nA_arr[pa];
+    const float* aA = angA + (long long)pa * capA * kstrideA;
     const float* aB = angB + (long long)q * capB * kstrideB;
     int32_t* m = match + (long long)p * strideM;
     if (tid < HISTO_LENGTH) hist[tid] = 0;
@@ -998,6 +999,9 @@ struct BowArgs {
     float nnratio;
     int32_t* match;
     int32_t* nmatches;
+    const uint8_t* mp2;      // KeyFrame-KeyFrame form: candidate MapPoint valid (NULL: all)
+    const int32_t* frame2;   // KeyFrame-KeyFrame form: kf2 slot of pair p (NULL: p)
+    int kf;                  // 1: SearchByBoW(KeyFrame*, KeyFrame*) (:696-766), matches12 by idx1
 };
 constexpr int BOW_MAX_CAND = 64 * 64;   // frame candidates per node: one claim bit per lane and chunk
 
@@ -1010,18 +1014,20 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 __global__ __launch_bounds__(256) void search_by_bow_kernel(BowArgs a) {
     const int p = blockIdx.y, lane = threadIdx.x & 63;
     const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), nwv = gridDim.x * 4;
-    const int f1 = a.frame1 ? a.frame1[p] : p;
-    const int nn1 = a.fvc1[f1], nn2 = a.fvc2[p];
+    const int f1 = a.frame1 ? a.frame1[p] : p, f2 = a.frame2 ? a.frame2[p] : p;
+    const int nn1 = a.fvc1[f1], nn2 = a.fvc2[f2];
     const uint32_t* node1 = a.fvn1 + (long long)f1 * a.fvcap1;
-    const uint32_t* node2 = a.fvn2 + (long long)p * a.fvcap2;
+    const uint32_t* node2 = a.fvn2 + (long long)f2 * a.fvcap2;
     const int32_t* off1 = a.fvo1 + (long long)f1 * (a.fvcap1 + 1);
-    const int32_t* off2 = a.fvo2 + (long long)p * (a.fvcap2 + 1);
+    const int32_t* off2 = a.fvo2 + (long long)f2 * (a.fvcap2 + 1);
     const int32_t* idx1 = a.fvi1 + (long long)f1 * a.fvcap1;
-    const int32_t* idx2 = a.fvi2 + (long long)p * a.fvcap2;
-    const long long base1 = (long long)f1 * a.cap1, base2 = (long long)p * a.cap2;
+    const int32_t* idx2 = a.fvi2 + (long long)f2 * a.fvcap2;
+    const long long base1 = (long long)f1 * a.cap1, base2 = (long long)f2 * a.cap2;
     const uint4* D1 = reinterpret_cast<const uint4*>(a.desc1);
     const uint4* D2 = reinterpret_cast<const uint4*>(a.desc2);
-    int32_t* out = a.match + base2;
+    // Frame form: matches[idx2] = idx1 (pair p's frame slots); KeyFrame form: matches12[idx1] = idx2
+    int32_t* out = a.match + (long long)p * (a.kf ? a.cap1 : a.cap2);
+    const int th_ok = a.kf ? 49 : 50;   // bestDist < TH_LOW (:750) / bestDist <= TH_LOW (:500)
     int found = 0;
     for (int na = wv; na < nn1; na += nwv) {
         const uint32_t id = node1[na];
@@ -1044,8 +1050,8 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(BowArgs a) {
             int d2 = 256;
             for (int k = 0; k < nch; k++) {
                 const int pos = 64 * k + lane;
-                if (pos < n2 && !((claimed >> k) & 1ull)) {
-                    const long long g2 = base2 + idx2[c0 + pos];
+                const long long g2 = pos < n2 ? base2 + idx2[c0 + pos] : 0;
+                if (pos < n2 && !((claimed >> k) & 1ull) && (!a.mp2 || a.mp2[g2])) {   // matched2 / mappoint2 (:733)
                     const int d = hamming8(q0, q1, D2[2 * g2], D2[2 * g2 + 1]);
                     const uint32_t key = ((uint32_t)d << 16) | (uint32_t)pos;
                     if (key < k1) {
@@ -1060,11 +1066,12 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(BowArgs a) {
             if (K == 0xffffffffu) continue;   // no unclaimed candidate: bestDist stays 256
             const int sd = (int)wave_min_u32((uint32_t)(k1 == K ? d2 : min((int)(k1 >> 16), 256)));
             const int bd = (int)(K >> 16);
-            if (bd <= 50 && (float)bd < a.nnratio * (float)sd) {   // :500
+            if (bd <= th_ok && (float)bd < a.nnratio * (float)sd) {   // :500 / :750
                 const int pos = (int)(K & 0xffffu);
                 if ((pos & 63) == lane) {
                     claimed |= 1ull << (pos >> 6);
-                    out[idx2[c0 + pos]] = i1;
+                    if (a.kf) out[i1] = idx2[c0 + pos];
+                    else out[idx2[c0 + pos]] = i1;
                     found++;
                 }
             }
@@ -1157,7 +1164,8 @@ int orbm_check_orientation_batch_device(const float* d_angA, int kstrideA, int c
     if (n_pairs == 0) return ORB_OK;
     ORB_CHECK_ARG(d_angA && d_angB && d_nA && d_match, "null CheckOrientation argument");
     hipLaunchKernelGGL(check_orientation_kernel, dim3((unsigned)n_pairs), dim3(256), 0, (hipStream_t)stream, d_angA,
-                       kstrideA, capA, d_nA, d_angB, kstrideB, capB, d_pair_b, d_match, strideM, d_nmatches);
+                       kstrideA, capA, d_nA, d_angB, kstrideB, capB, d_pair_b, d_match, strideM, d_nmatches,
+                       (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
@@ -1185,7 +1193,7 @@ int orbm_check_orientation(const float* angA, int nA, const float* angB, int nB,
     ORB_HIP_TRY(hipMemcpy(dM, match, (size_t)nA * 4, hipMemcpyHostToDevice));
     ORB_HIP_TRY(hipMemcpy(dM + nA, &nA, 4, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(check_orientation_kernel, dim3(1), dim3(256), 0, (hipStream_t)0, dA, 1, nA, dM + nA, dB, 1,
-                       std::max(nB, 1), nullptr, dM, nA, dM + nA + 1);
+                       std::max(nB, 1), nullptr, dM, nA, dM + nA + 1, (const int32_t*)nullptr);
     ORB_HIP_TRY(hipGetLastError());
     ORB_HIP_TRY(hipMemcpy(match, dM, (size_t)nA * 4, hipMemcpyDeviceToHost));
     int32_t nm = 0;
@@ -1194,7 +1202,7 @@ int orbm_check_orientation(const float* angA, int nA, const float* angB, int nB,
     return ORB_OK;
 }
 
-int orbm_search_by_bow_batch_device(const orbm_bow_batch* b, int32_t* d_match, int32_t* d_nmatches, void* stream) {
+static int search_by_bow(const orbm_bow_batch* b, int kf, int32_t* d_match, int32_t* d_nmatches, void* stream) {
     ORB_CHECK_ARG(b && d_match && d_nmatches, "null argument");
     ORB_CHECK_ARG(b->n_pairs >= 0 && b->cap1 > 0 && b->cap2 > 0, "bad pair count / capacities");
     if (b->n_pairs == 0) return ORB_OK;
@@ -1205,23 +1213,41 @@ int orbm_search_by_bow_batch_device(const orbm_bow_batch* b, int32_t* d_match, i
                       b->fv_n_nodes2 && b->fv_cap1 > 0 && b->fv_cap2 > 0,
                   "SearchByBoW needs both FeatureVectors");
     ORB_CHECK_ARG(!b->check_orientation || (b->kps1 && b->kps2), "CheckOrientation needs the keypoint slots");
+    ORB_CHECK_ARG(kf || (!b->frame2 && !b->mp_valid2), "frame2 / mp_valid2 belong to the KeyFrame-KeyFrame form");
+    ORB_CHECK_ARG(!kf || !b->check_orientation || b->counts1, "CheckOrientation needs counts1");
     BowArgs a{b->desc1, b->mp_valid1, b->frame1, b->desc2, b->fv_node1, b->fv_off1, b->fv_idx1, b->fv_n_nodes1,
               b->fv_node2, b->fv_off2, b->fv_idx2, b->fv_n_nodes2, b->cap1, b->cap2, b->fv_cap1, b->fv_cap2, b->nnratio,
-              d_match, d_nmatches};
+              d_match, d_nmatches, b->mp_valid2, b->frame2, kf};
     hipStream_t st = (hipStream_t)stream;
     ORB_HIP_TRY(hipMemsetAsync(d_nmatches, 0, (size_t)b->n_pairs * 4, st));
-    ORB_HIP_TRY(hipMemsetAsync(d_match, 0xff, (size_t)b->n_pairs * b->cap2 * 4, st));
+    ORB_HIP_TRY(hipMemsetAsync(d_match, 0xff, (size_t)b->n_pairs * (kf ? b->cap1 : b->cap2) * 4, st));
     const int gx = (std::min(b->fv_cap1, 256) + 3) / 4;   // wavefronts stride over the keyframe's nodes
     hipLaunchKernelGGL(search_by_bow_kernel, dim3((unsigned)gx, (unsigned)b->n_pairs), dim3(256), 0, st, a);
     ORB_HIP_TRY(hipGetLastError());
-    if (b->check_orientation) {
+    if (b->check_orientation && !kf) {
         // CheckOrientation(keyframe->keypointsUn, frame.keypointsUn, matchIds, matches) (:512-513) on the
         // frame-indexed result: bin of angle1[idx1] - angle2[idx2], matches[idx2] erased
         hipLaunchKernelGGL(check_orientation_kernel, dim3((unsigned)b->n_pairs), dim3(256), 0, st, &b->kps2[0].angle, 7,
-                           b->cap2, b->counts2, &b->kps1[0].angle, 7, b->cap1, b->frame1, d_match, b->cap2, d_nmatches);
+                           b->cap2, b->counts2, &b->kps1[0].angle, 7, b->cap1, b->frame1, d_match, b->cap2, d_nmatches,
+                           (const int32_t*)nullptr);
+        ORB_HIP_TRY(hipGetLastError());
+    } else if (b->check_orientation) {
+        // CheckOrientation(keypoints2, keypoints1, matchIds = (bestIdx2, idx1), matches12) (:762-763): bin of
+        // angle2[idx2] - angle1[idx1], matches12[idx1] erased (the query-indexed form, A = kf1)
+        hipLaunchKernelGGL(check_orientation_kernel, dim3((unsigned)b->n_pairs), dim3(256), 0, st, &b->kps1[0].angle, 7,
+                           b->cap1, b->counts1, &b->kps2[0].angle, 7, b->cap2, b->frame2, d_match, b->cap1, d_nmatches,
+                           b->frame1);
         ORB_HIP_TRY(hipGetLastError());
     }
     return ORB_OK;
+}
+
+int orbm_search_by_bow_batch_device(const orbm_bow_batch* b, int32_t* d_match, int32_t* d_nmatches, void* stream) {
+    return search_by_bow(b, 0, d_match, d_nmatches, stream);
+}
+
+int orbm_search_by_bow_kf_batch_device(const orbm_bow_batch* b, int32_t* d_match12, int32_t* d_nmatches, void* stream) {
+    return search_by_bow(b, 1, d_match12, d_nmatches, stream);
 }
 
 int orbm_search_for_triangulation_batch_device(const orbm_tri_batch* b, int32_t* d_match12, int32_t* d_nmatches,

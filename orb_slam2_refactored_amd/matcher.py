@@ -179,9 +179,36 @@ def search_by_bow_batch_device(kps1, desc1, fv1, kps2, desc2, counts2, fv2, fram
     opt = lambda t: tptr(t) if t is not None else None   # noqa: E731
     b = BowBatch(P, cap1, cap2, tptr(kps1), tptr(desc1), opt(mp_valid1), opt(frame1), tptr(kps2), tptr(desc2),
                  tptr(counts2), *[tptr(t) for t in fv1], *[tptr(t) for t in fv2], int(fv1[0].shape[1]),
-                 int(fv2[0].shape[1]), float(nnratio), int(bool(checkOri)))
+                 int(fv2[0].shape[1]), float(nnratio), int(bool(checkOri)), None, None, None)
     check(lib().orbm_search_by_bow_batch_device(C.byref(b), tptr(out[0]), tptr(out[1]), stream_ptr(stream)),
           "orbm_search_by_bow_batch_device")
+    return out
+
+
+def search_by_bow_kf_batch_device(kps1, desc1, counts1, fv1, kps2, desc2, counts2, fv2, n_pairs=None, frame1=None,
+                                  frame2=None, mp_valid1=None, mp_valid2=None, nnratio: float = 0.6,
+                                  checkOri: bool = True, out=None, stream=None):
+    """Batched SearchByBoW(KeyFrame* kf1, KeyFrame* kf2, matches12) (src/ORBmatcher.cc:696-766): pair p =
+    (kf1 frame1[p] of set 1, kf2 frame2[p] of set 2; default p).  mp_valid* uint8 [F, cap] (None = all
+    valid).  Returns (match12 [P, cap1] int32 = idx2 or -1 per kf1 feature, nmatches [P])."""
+    import torch
+    from ._lib import BowBatch
+    P = int(n_pairs if n_pairs is not None else (frame1.shape[0] if frame1 is not None else desc1.shape[0]))
+    cap1, cap2 = int(desc1.shape[1]), int(desc2.shape[1])
+    for k, d in ((kps1, desc1), (kps2, desc2)):
+        if k.dim() != 3 or k.shape[2] != 7 or d.shape[:2] != k.shape[:2] or d.shape[2] != 32 or \
+                not k.is_contiguous() or not d.is_contiguous():
+            raise ValueError("keypoint / descriptor slots must be contiguous [F, cap, 7] / [F, cap, 32]")
+    if out is None:
+        out = (torch.empty((P, cap1), dtype=torch.int32, device=desc1.device),
+               torch.empty((P,), dtype=torch.int32, device=desc1.device))
+    opt = lambda t: tptr(t) if t is not None else None   # noqa: E731
+    b = BowBatch(P, cap1, cap2, tptr(kps1), tptr(desc1), opt(mp_valid1), opt(frame1), tptr(kps2), tptr(desc2),
+                 tptr(counts2), *[tptr(t) for t in fv1], *[tptr(t) for t in fv2], int(fv1[0].shape[1]),
+                 int(fv2[0].shape[1]), float(nnratio), int(bool(checkOri)), tptr(counts1), opt(mp_valid2),
+                 opt(frame2))
+    check(lib().orbm_search_by_bow_kf_batch_device(C.byref(b), tptr(out[0]), tptr(out[1]), stream_ptr(stream)),
+          "orbm_search_by_bow_kf_batch_device")
     return out
 
 

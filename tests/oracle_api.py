@@ -212,6 +212,17 @@ def search_by_bow(kf, fr, ang_kf, ang_fr, nnratio=0.6, check_ori=True):
     return out[:fr.n], n
 
 
+def search_by_bow_kf(kf1, kf2, ang1, ang2, nnratio=0.6, check_ori=True):
+    """SearchByBoW(KeyFrame*, KeyFrame*) (ORBmatcher.cc:696-766): has_mappoint = MapPoint valid on
+    both sides.  Returns (match12 [kf1.n] = idx2 or -1, nmatches)."""
+    keep = _Keep()
+    out = np.zeros(max(kf1.n, 1), np.int32)
+    n = lib().oracle_search_by_bow_kf(C.byref(kf1), C.byref(kf2), C.c_float(nnratio), int(check_ori),
+                                      keep(ang1, np.float32), keep(ang2, np.float32), ptr(out))
+    assert n >= 0, "bin out of range"
+    return out[:kf1.n], n
+
+
 def ba_problem(keep, prob):
     return BAProblem(len(prob["pose_R"]), keep(prob["pose_R"], np.float64), keep(prob["pose_t"], np.float64),
                      keep(prob["pose_fixed"], np.uint8), len(prob["points"]), keep(prob["points"], np.float64),

@@ -142,3 +142,65 @@ def test_search_by_bow_rejects_bad_args():
         search_by_bow_batch_device(k, d, fv, big, bigd, c, fv)
     with pytest.raises(ValueError):
         search_by_bow_batch_device(k, d[:, :4], fv, k, d, c, fv)
+
+
+@pytest.mark.parametrize("levelsup", [2, 3])
+@pytest.mark.parametrize("check_ori", [False, True])
+def test_search_by_bow_keyframes_vs_oracle(oracle, levelsup, check_ori):
+    """SearchByBoW(KeyFrame*, KeyFrame*) (:696-766): MapPoint masks on both sides, kf1 / kf2 index
+    arrays (a keyframe in several pairs, both orders), matches12 by idx1."""
+    import torch
+    from orb_slam2_refactored_amd.matcher import search_by_bow_kf_batch_device
+    kps, desc, cnt, fv = _setup(levelsup)
+    F = desc.shape[0]
+    f1 = np.array([0, 1, 2, 4, 5, 3], np.int32)
+    f2 = np.array([1, 2, 3, 3, 4, 0], np.int32)
+    rng = np.random.default_rng(levelsup + 10)
+    mp = (rng.random((F, desc.shape[1])) < 0.8).astype(np.uint8)
+    mpt = torch.from_numpy(mp).cuda()
+    m, nm = search_by_bow_kf_batch_device(kps, desc, cnt, fv, kps, desc, cnt, fv, frame1=torch.from_numpy(f1).cuda(),
+                                          frame2=torch.from_numpy(f2).cuda(), mp_valid1=mpt, mp_valid2=mpt,
+                                          checkOri=check_ori)
+    torch.cuda.synchronize()
+    K, D, N = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+    M, NM = m.cpu().numpy(), nm.cpu().numpy()
+    fvh = tuple(t.cpu().numpy() for t in fv)
+    total = 0
+    for p in range(len(f1)):
+        a, b = int(f1[p]), int(f2[p])
+        keep = oracle._Keep()
+        k1 = _host_frame(oracle, keep, K, D, N, fvh, a, mp)
+        k2 = _host_frame(oracle, keep, K, D, N, fvh, b, mp)
+        exp, n = oracle.search_by_bow_kf(k1, k2, K[a, :N[a]].view(np.float32)[:, 3], K[b, :N[b]].view(np.float32)[:, 3],
+                                         0.6, check_ori)
+        assert np.array_equal(M[p, :N[a]], exp), p
+        assert NM[p] == n, (p, NM[p], n)
+        total += n
+    assert total > 0
+
+
+def test_search_by_bow_th_low_boundary(oracle):
+    """bestDist == TH_LOW: accepted by SearchByBoW(KeyFrame, Frame) (:500, <=), rejected by the
+    KeyFrame-KeyFrame form (:750, <)."""
+    import torch
+    from orb_slam2_refactored_amd.matcher import search_by_bow_kf_batch_device
+    cap = 8
+    D1 = np.zeros((1, cap, 32), np.uint8)
+    D2 = np.zeros((1, cap, 32), np.uint8)
+    D2[0, 0, :6] = 0xff
+    D2[0, 0, 6] = 0x03          # distance 50
+    D2[0, 1, :] = 0xff          # distance 256 - ... (second far away)
+    K = np.zeros((1, cap, 7), np.int32)
+    node = np.zeros((1, cap), np.int32)
+    off = np.zeros((1, cap + 1), np.int32)
+    off[0, 1] = 2
+    idx = np.zeros((1, cap), np.int32)
+    idx[0, :2] = [0, 1]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    fv = (t(node), t(off), t(idx), t(np.ones(1, np.int32)))
+    c = t(np.array([2], np.int32))
+    m, nm = search_by_bow_batch_device(t(K), t(D1), fv, t(K), t(D2), c, fv, checkOri=False)
+    m12, nm12 = search_by_bow_kf_batch_device(t(K), t(D1), c, fv, t(K), t(D2), c, fv, checkOri=False)
+    torch.cuda.synchronize()
+    assert int(nm[0]) == 1 and int(m[0, 0]) == 0 and int(m[0, 1]) == -1
+    assert int(nm12[0]) == 0 and (m12[0, :2].cpu().numpy() == -1).all()
