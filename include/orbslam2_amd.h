@@ -343,6 +343,47 @@ int orbm_search_by_projection(const orbm_proj_batch* b, int32_t* kp_match, int32
 int orbm_search_by_projection_device(const orbm_proj_batch* b, int32_t* kp_match, int32_t* n_matches,
                                      void* stream);
 
+/* int ORBmatcher::SearchByProjection(Frame& currFrame, const Frame& lastFrame, float th, bool monocular)
+ * (include/ORBmatcher.h:61, src/ORBmatcher.cc:1279-1362; Tracking::TrackWithMotionModel), batched over
+ * frames.  Current frame f: keypoints [kp_begin[f], kp_begin[f+1]) as in orbm_proj_batch, plus
+ * kp_angle (keypointsUn angle, for CheckOrientation).  Last frame's points [mp_begin[f], mp_begin[f+1])
+ * in idx1 order: mp_valid = mappoints[idx1] && !outlier[idx1] && Xc.z >= 0 && imageBounds.Contains(u, v)
+ * (:1295-1311, the caller projects), mp_proj = (u, v, ur = u - DepthToDisparity(Xc.z)), mp_octave =
+ * lastFrame.keypoints[idx1].octave, mp_desc = GetDescriptor(), mp_has_obs = Observations() > 0,
+ * mp_angle = lastFrame.keypointsUn[idx1].angle.  motion[f]: 0, 1 = forward, 2 = backward (:1286-1288).
+ * Window th * scaleFactors[octave] over the levels of :1318-1319, claimed keypoints skipped, the
+ * stereo gate with the window radius, best distance <= TH_HIGH; then CheckOrientation(lastFrame,
+ * currFrame, ...) (:1358-1359) over every accepted (idx1, bestIdx2) pair in order (overwritten ones
+ * included, as the reference's matchIds).  kp_match[k] = frame-relative idx1 the call assigned to
+ * keypoint k (-1: none, or erased by the rotation filter); n_matches[f] = the return value (-1 when
+ * the frame has more than ORBM_PROJ_MAX_KP keypoints).  Enqueue only on `stream`. */
+typedef struct orbm_motion_batch {
+    int32_t        n_frames, total_kp, total_mp;
+    const int32_t* kp_begin;
+    const float*   kp_xy;
+    const int32_t* kp_octave;
+    const float*   kp_uright;
+    const uint8_t* kp_desc;
+    const float*   kp_angle;
+    const uint8_t* kp_claimed;   /* currFrame.mappoints[i] with Observations() > 0 on entry (NULL: none) */
+    const float*   bounds;       /* n_frames x 4 */
+    const int32_t* mp_begin;
+    const uint8_t* mp_valid;
+    const float*   mp_proj;      /* total_mp x 3 */
+    const int32_t* mp_octave;
+    const uint8_t* mp_desc;
+    const uint8_t* mp_has_obs;
+    const float*   mp_angle;
+    const int32_t* motion;       /* n_frames (NULL: all 0) */
+    int32_t        n_levels;
+    const float*   scale_factors;/* host, n_levels */
+    float          th;
+    int32_t        check_orientation;
+} orbm_motion_batch;
+
+int orbm_search_by_projection_motion_device(const orbm_motion_batch* b, int32_t* kp_match, int32_t* n_matches,
+                                            void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Bag of words.  Replaces DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> as ORBVocabulary
  * (include/ORBVocabulary.h) for Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:208-214,

@@ -2046,6 +2046,84 @@ int oracle_search_by_projection(const orbm_proj_batch* b, int32_t* kp_match, int
     return 0;
 }
 
+// SearchByProjection(Frame& currFrame, const Frame& lastFrame, th, monocular) (ORBmatcher.cc:1279-1362),
+// literally, frame by frame: the caller's projection / validity (:1295-1311) in mp_valid / mp_proj.
+int oracle_search_by_projection_motion(const orbm_motion_batch* b, int32_t* kp_match, int32_t* n_matches) {
+    const int TH_HIGH = 100, HISTO_LENGTH = 30;
+    for (int f = 0; f < b->n_frames; f++) {
+        const int k0 = b->kp_begin[f], nk = b->kp_begin[f + 1] - k0;
+        const int m0 = b->mp_begin[f], nm = b->mp_begin[f + 1] - m0;
+        std::unique_ptr<FeaturesGrid> g(new FeaturesGrid);
+        g->assign(b->kp_xy + 2 * (size_t)k0, b->kp_octave + k0, nk, b->bounds + 4 * (size_t)f, b->n_levels);
+        // currFrame.mappoints[i]: -1 none, else the owner's has-observations flag decides the skip
+        std::vector<int> owner(nk, -1);
+        std::vector<uint8_t> claimed(nk, 0);
+        if (b->kp_claimed) for (int i = 0; i < nk; i++) claimed[i] = b->kp_claimed[k0 + i];
+        const int mot = b->motion ? b->motion[f] : 0;
+        const bool forward = mot == 1, backward = mot == 2;
+        std::vector<std::pair<int, int>> matchIds;
+        int nmatches = 0;
+        for (int idx1 = 0; idx1 < nm; idx1++) {
+            const int mj = m0 + idx1;
+            if (!b->mp_valid[mj]) continue;
+            const float u = b->mp_proj[3 * (size_t)mj], v = b->mp_proj[3 * (size_t)mj + 1];
+            const float ur = b->mp_proj[3 * (size_t)mj + 2];
+            const int octave1 = b->mp_octave[mj];
+            const float radius = b->th * b->scale_factors[octave1];
+            const int minLevel = forward ? octave1 : (backward ? 0 : octave1 - 1);
+            const int maxLevel = forward ? -1 : (backward ? octave1 : octave1 + 1);
+            const std::vector<size_t> indices2 = g->in_area(u, v, radius, minLevel, maxLevel);
+            if (indices2.empty()) continue;
+            const uint8_t* desc1 = b->mp_desc + 32 * (size_t)mj;
+            int bestDist = 256, bestIdx2 = -1;
+            for (size_t idx2 : indices2) {
+                if (claimed[idx2]) continue;
+                const float u2 = b->kp_uright[k0 + idx2];
+                if (u2 > 0 && std::fabs(ur - u2) > radius) continue;
+                const int dist = hamming(desc1, b->kp_desc + 32 * (size_t)(k0 + idx2));
+                if (dist < bestDist) {
+                    bestDist = dist;
+                    bestIdx2 = (int)idx2;
+                }
+            }
+            if (bestDist <= TH_HIGH) {
+                owner[bestIdx2] = idx1;
+                claimed[bestIdx2] = b->mp_has_obs[mj] ? 1 : 0;
+                nmatches++;
+                if (b->check_orientation) matchIds.push_back(std::make_pair(idx1, bestIdx2));
+            }
+        }
+        if (b->check_orientation) {
+            const float factor = 1.f / HISTO_LENGTH;
+            std::vector<int> hist[HISTO_LENGTH];
+            for (const auto& m : matchIds) {
+                float diff = b->mp_angle[m0 + m.first] - b->kp_angle[k0 + m.second];
+                if (diff < 0) diff += 360;
+                int bin = cv_round(factor * diff);
+                if (bin == HISTO_LENGTH) bin = 0;
+                if (bin < 0 || bin >= HISTO_LENGTH) return -1;
+                hist[bin].push_back(m.second);
+            }
+            std::sort(std::begin(hist), std::end(hist),
+                      [](const std::vector<int>& l, const std::vector<int>& r) { return l.size() > r.size(); });
+            const size_t max1 = hist[0].size(), max2 = hist[1].size(), max3 = hist[2].size();
+            int eraseBin = 3;
+            if (max2 < 0.1 * max1) eraseBin = 1;
+            else if (max3 < 0.1 * max1) eraseBin = 2;
+            int reduction = 0;
+            for (int bin = eraseBin; bin < HISTO_LENGTH; bin++)
+                for (int i2 : hist[bin]) {
+                    owner[i2] = -1;
+                    reduction++;
+                }
+            nmatches = (int)matchIds.size() - reduction;
+        }
+        for (int i = 0; i < nk; i++) kp_match[k0 + i] = owner[i];
+        n_matches[f] = nmatches;
+    }
+    return 0;
+}
+
 // Optimizer::PoseOptimization (src/Optimizer.cc:345-489), frame by frame.
 int oracle_pose_optimization(const orbba_pose_batch* in, orbba_pose_result* out) {
     const double maxChi2[2] = {5.991, 7.815};   // CHI2_MONO, CHI2_STEREO (:44-45)

@@ -79,6 +79,17 @@ class ProjBatch(C.Structure):
                 ("th", C.c_float), ("nnratio", C.c_float)]
 
 
+class MotionBatch(C.Structure):
+    """orbm_motion_batch (include/orbslam2_amd.h)."""
+    _fields_ = [("n_frames", C.c_int32), ("total_kp", C.c_int32), ("total_mp", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_uright", C.c_void_p),
+                ("kp_desc", C.c_void_p), ("kp_angle", C.c_void_p), ("kp_claimed", C.c_void_p), ("bounds", C.c_void_p),
+                ("mp_begin", C.c_void_p), ("mp_valid", C.c_void_p), ("mp_proj", C.c_void_p), ("mp_octave", C.c_void_p),
+                ("mp_desc", C.c_void_p), ("mp_has_obs", C.c_void_p), ("mp_angle", C.c_void_p), ("motion", C.c_void_p),
+                ("n_levels", C.c_int32), ("scale_factors", C.c_void_p), ("th", C.c_float),
+                ("check_orientation", C.c_int32)]
+
+
 class PoseBatch(C.Structure):
     _fields_ = [("n_frames", C.c_int32), ("edge_begin", C.c_void_p), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
                 ("cam", C.c_void_p), ("xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
@@ -128,6 +139,7 @@ SIGNATURES = {
                                                    C.c_float, VP, VP, VP]),
     "orbm_search_by_projection": (C.c_int, [C.POINTER(ProjBatch), VP, VP, C.c_int]),
     "orbm_search_by_projection_device": (C.c_int, [C.POINTER(ProjBatch), VP, VP, VP]),
+    "orbm_search_by_projection_motion_device": (C.c_int, [C.POINTER(MotionBatch), VP, VP, VP]),
     "orbv_load_text": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(VP)]),
     "orbv_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, VP, VP, VP, C.c_int, C.POINTER(VP)]),
     "orbv_destroy": (C.c_int, [VP]),

@@ -26,6 +26,7 @@
 #include <cstring>
 
 #include "common.h"
+#include "qt_sort.h"
 
 namespace orbamd {
 
@@ -425,6 +426,142 @@ static int launch_projection(PjArgs& a, int total_kp, hipStream_t st) {
     return ORB_OK;
 }
 
+// ---------------------------------------------------------------- SearchByProjection(Frame&, const Frame&, th, mono)
+// (ORBmatcher.cc:1279-1362, TrackWithMotionModel).  Same grid (pj_grid_kernel) and the same claim
+// rule (a keypoint whose current map point has observations is skipped, :1331-1333), but only the
+// best distance counts (no ratio), so one wavefront per frame walks the last frame's points in idx1
+// order: each point's window is scanned by the lanes against the LDS claim bitmap and the wave
+// minimum of (dist << 13 | scan position) is the reference's first-best.  The accepted pair of every
+// point is kept (choice) for CheckOrientation, which counts overwritten pairs too (matchIds).
+struct PjmExtra {
+    const int32_t* motion;
+    const float* kp_angle;
+    const float* mp_angle;
+    int32_t* choice;   // total_mp: accepted idx2 or -1
+};
+
+__global__ __launch_bounds__(64) void pjm_walk_kernel(PjArgs a, PjmExtra e) {
+    __shared__ uint32_t bits[PJ_MAXKP / 32];
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int k0 = a.kp_begin[f], n = a.kp_begin[f + 1] - k0;
+    const int m0 = a.mp_begin[f], m1 = a.mp_begin[f + 1];
+    if (n > PJ_MAXKP) {
+        for (int j = m0 + lane; j < m1; j += 64) e.choice[j] = -1;
+        if (lane == 0) a.n_matches[f] = -1;
+        return;
+    }
+    for (int i = lane; i < PJ_MAXKP / 32; i += 64) bits[i] = 0;
+    for (int i = lane; i < n; i += 64) a.kp_match[k0 + i] = -1;
+    __syncthreads();
+    if (a.kp_claimed)
+        for (int i = lane; i < n; i += 64)
+            if (a.kp_claimed[k0 + i]) atomicOr(&bits[i >> 5], 1u << (i & 31));
+    __syncthreads();
+    const int mot = e.motion ? e.motion[f] : 0;
+    const float* bd = a.bounds + 4 * (size_t)f;
+    const float minx = bd[0], miny = bd[2];
+    const float invW = PJ_COLS / (bd[1] - bd[0]), invH = PJ_ROWS / (bd[3] - bd[2]);
+    const int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
+    int nm = 0;
+    for (int j = m0; j < m1; j++) {
+        int ch = -1;
+        if (a.mp_valid[j]) {
+            const int oct = a.mp_level[j];
+            const float r = a.th * a.scale[oct];   // :1316
+            // :1318-1319 through GetFeaturesInArea's checkLevels (maxLevel < 0 -> nlevels)
+            const int lo = mot == 1 ? oct : (mot == 2 ? 0 : oct - 1);
+            const int hi = mot == 1 ? a.n_levels : (mot == 2 ? oct : oct + 1);
+            const float u = a.mp_proj[3 * (size_t)j], v = a.mp_proj[3 * (size_t)j + 1];
+            const float uR = a.mp_proj[3 * (size_t)j + 2];
+            const int mincx = max((int)floorf(invW * (u - r - minx)), 0);
+            const int maxcx = min((int)ceilf(invW * (u + r - minx)), PJ_COLS - 1);
+            const int mincy = max((int)floorf(invH * (v - r - miny)), 0);
+            const int maxcy = min((int)ceilf(invH * (v + r - miny)), PJ_ROWS - 1);
+            uint32_t best = PJ_NONE;
+            if (!(mincx >= PJ_COLS || maxcx < 0 || mincy >= PJ_ROWS || maxcy < 0)) {
+                const uint8_t* d1 = a.mp_desc + 32 * (size_t)j;
+                for (int cx = mincx; cx <= maxcx; cx++) {
+                    const int p0 = cs[cx * PJ_ROWS + mincy], p1 = cs[cx * PJ_ROWS + maxcy + 1];
+                    for (int p = p0 + lane; p < p1; p += 64) {
+                        const int idx = a.grid_idx[k0 + p];
+                        const int k = k0 + idx;
+                        const int level = a.kp_oct[k];
+                        if (level < lo || level > hi) continue;
+                        const float distx = a.kp_xy[2 * (size_t)k] - u;
+                        const float disty = a.kp_xy[2 * (size_t)k + 1] - v;
+                        if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+                        if ((bits[idx >> 5] >> (idx & 31)) & 1u) continue;
+                        const float ur = a.kp_ur[k];
+                        if (ur > 0 && fabsf(uR - ur) > r) continue;   // :1335
+                        const int dist = pj_hamming(d1, a.kp_desc + 32 * (size_t)k);
+                        best = min(best, ((uint32_t)dist << PJ_IDX_BITS) | (uint32_t)p);
+                    }
+                }
+            }
+            const uint32_t K = pj_wave_min(best);
+            if (K != PJ_NONE && (int)(K >> PJ_IDX_BITS) <= PJ_TH_HIGH) {   // :1347
+                ch = a.grid_idx[k0 + (int)(K & PJ_IDX_MASK)];
+                if (lane == 0) {
+                    a.kp_match[k0 + ch] = j - m0;
+                    if (a.mp_has_obs[j]) bits[ch >> 5] |= 1u << (ch & 31);
+                }
+                nm++;
+                __syncthreads();   // one wavefront: the claim bit before the next point's scan
+            }
+        }
+        if (lane == 0) e.choice[j] = ch;
+    }
+    if (lane == 0) a.n_matches[f] = nm;
+}
+
+__device__ __forceinline__ int pjm_bin(float ang1, float ang2) {   // diffToBin(keypoint1.angle - keypoint2.angle)
+    float diff = ang1 - ang2;
+    if (diff < 0) diff += 360.f;
+    int bin = __float2int_rn((1.f / 30) * diff);
+    if (bin == 30) bin = 0;
+    return min(max(bin, 0), 29);
+}
+
+// CheckOrientation(lastFrame.keypointsUn, currFrame.keypointsUn, matchIds, currFrame.mappoints)
+// (:249-309, :1358-1359): hist of every accepted (idx1, idx2), bins sorted by size with libstdc++'s
+// order (qt_sort), mappoints[idx2] erased for every pair outside the kept bins.
+__global__ __launch_bounds__(256) void pjm_orient_kernel(PjArgs a, PjmExtra e) {
+    __shared__ int hist[30];
+    __shared__ uint32_t keep;
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int k0 = a.kp_begin[f], n = a.kp_begin[f + 1] - k0;
+    const int m0 = a.mp_begin[f], m1 = a.mp_begin[f + 1];
+    if (n > PJ_MAXKP) return;
+    if (tid < 30) hist[tid] = 0;
+    __syncthreads();
+    for (int j = m0 + tid; j < m1; j += 256) {
+        const int ch = e.choice[j];
+        if (ch >= 0) atomicAdd(&hist[pjm_bin(e.mp_angle[j], e.kp_angle[k0 + ch])], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        QtItem it[30];
+        for (int b = 0; b < 30; b++) it[b] = QtItem{hist[b], b};
+        qt_sort(it, it + 30);
+        const double max1 = it[0].size, max2 = it[1].size, max3 = it[2].size;
+        const int eraseBin = max2 < 0.1 * max1 ? 1 : (max3 < 0.1 * max1 ? 2 : 3);
+        uint32_t k = 0;
+        int kept = 0;
+        for (int r = 0; r < eraseBin; r++) {
+            k |= 1u << it[r].node;
+            kept += it[r].size;
+        }
+        keep = k;
+        a.n_matches[f] = kept;
+    }
+    __syncthreads();
+    const uint32_t k = keep;
+    for (int j = m0 + tid; j < m1; j += 256) {
+        const int ch = e.choice[j];
+        if (ch >= 0 && !((k >> pjm_bin(e.mp_angle[j], e.kp_angle[k0 + ch])) & 1u)) a.kp_match[k0 + ch] = -1;
+    }
+}
+
 struct PjScratch {
     DevBuf ws, io;
     int device = -1;
@@ -562,5 +699,53 @@ extern "C" int orbm_search_by_projection(const orbm_proj_batch* b, int32_t* kp_m
     if ((rc = launch_projection(a, K, nullptr))) return rc;
     if (K) ORB_HIP_TRY(hipMemcpy(kp_match, d + o_km, (size_t)K * 4, hipMemcpyDeviceToHost));
     ORB_HIP_TRY(hipMemcpy(n_matches, d + o_nm, (size_t)F * 4, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+extern "C" int orbm_search_by_projection_motion_device(const orbm_motion_batch* b, int32_t* kp_match,
+                                                       int32_t* n_matches, void* stream) {
+    ORB_CHECK_ARG(b, "null argument");
+    ORB_CHECK_ARG(b->n_frames >= 0 && b->total_kp >= 0 && b->total_mp >= 0, "negative sizes");
+    ORB_CHECK_ARG(b->n_levels >= 1 && b->n_levels <= PJ_MAX_LEVELS && b->scale_factors, "bad scale pyramid");
+    if (b->n_frames == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kp_begin && b->mp_begin && b->bounds && kp_match && n_matches, "null array");
+    ORB_CHECK_ARG(b->total_kp == 0 || (b->kp_xy && b->kp_octave && b->kp_uright && b->kp_desc), "null keypoint array");
+    ORB_CHECK_ARG(b->total_mp == 0 || (b->mp_valid && b->mp_proj && b->mp_octave && b->mp_desc && b->mp_has_obs),
+                  "null last-frame point array");
+    ORB_CHECK_ARG(!b->check_orientation || (b->kp_angle && (b->total_mp == 0 || b->mp_angle)),
+                  "CheckOrientation needs kp_angle / mp_angle");
+    PjArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.n_frames = b->n_frames;
+    a.n_levels = b->n_levels;
+    for (int l = 0; l < b->n_levels; l++) a.scale[l] = b->scale_factors[l];
+    a.th = b->th;
+    a.total_mp = b->total_mp;
+    a.kp_begin = b->kp_begin; a.kp_xy = b->kp_xy; a.kp_oct = b->kp_octave; a.kp_ur = b->kp_uright;
+    a.kp_desc = b->kp_desc; a.kp_claimed = b->kp_claimed; a.bounds = b->bounds;
+    a.mp_begin = b->mp_begin; a.mp_valid = b->mp_valid; a.mp_proj = b->mp_proj; a.mp_level = b->mp_octave;
+    a.mp_desc = b->mp_desc; a.mp_has_obs = b->mp_has_obs;
+    a.kp_match = kp_match;
+    a.n_matches = n_matches;
+    int dev = 0, rc;
+    ORB_HIP_TRY(hipGetDevice(&dev));
+    if (g_pj.device != dev) {
+        g_pj.ws.release();
+        g_pj.io.release();
+        g_pj.device = dev;
+    }
+    const size_t base = pj_workspace_bytes(b->n_frames, b->total_kp, b->total_mp);
+    if ((rc = g_pj.ws.reserve(base + align_up((size_t)std::max(b->total_mp, 1) * 4, 256)))) return rc;
+    pj_carve(a, g_pj.ws.as<char>(), b->n_frames, b->total_kp, b->total_mp);
+    PjmExtra e{b->motion, b->kp_angle, b->mp_angle, reinterpret_cast<int32_t*>(g_pj.ws.as<char>() + base)};
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(pj_grid_kernel, dim3(a.n_frames), dim3(256), 0, st, a);
+    ORB_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(pjm_walk_kernel, dim3(a.n_frames), dim3(64), 0, st, a, e);
+    ORB_HIP_TRY(hipGetLastError());
+    if (b->check_orientation) {
+        hipLaunchKernelGGL(pjm_orient_kernel, dim3(a.n_frames), dim3(256), 0, st, a, e);
+        ORB_HIP_TRY(hipGetLastError());
+    }
     return ORB_OK;
 }

@@ -330,3 +330,31 @@ def search_by_projection_device(batch: dict, kp_match=None, n_matches=None, stre
     check(lib().orbm_search_by_projection_device(C.byref(pb), tptr(kp_match), tptr(n_matches), stream_ptr(stream)),
           "orbm_search_by_projection_device")
     return kp_match, n_matches
+
+
+_MOTION_KEYS = ("kp_begin", "kp_xy", "kp_octave", "kp_uright", "kp_desc", "kp_angle", "kp_claimed", "bounds",
+                "mp_begin", "mp_valid", "mp_proj", "mp_octave", "mp_desc", "mp_has_obs", "mp_angle", "motion")
+
+
+def search_by_projection_motion_device(batch: dict, kp_match=None, n_matches=None, stream=None):
+    """SearchByProjection(Frame& currFrame, const Frame& lastFrame, float th, bool monocular)
+    (src/ORBmatcher.cc:1279-1362, TrackWithMotionModel) batched over frames: `batch` holds GPU tensors
+    for the orbm_motion_batch arrays (kp_claimed / motion may be None) and host values for
+    scale_factors, th and check_orientation.  Returns (kp_match [total_kp], n_matches [F])."""
+    import torch
+    from ._lib import MotionBatch
+    eb = batch["kp_begin"]
+    F = eb.numel() - 1
+    K = int(batch["kp_xy"].shape[0])
+    M = int(batch["mp_proj"].shape[0])
+    if kp_match is None:
+        kp_match = torch.empty(max(K, 1), dtype=torch.int32, device=eb.device)
+    if n_matches is None:
+        n_matches = torch.empty(max(F, 1), dtype=torch.int32, device=eb.device)
+    sf = np.ascontiguousarray(batch["scale_factors"], np.float32)
+    ptrs = [tptr(batch[k]) if batch.get(k) is not None else None for k in _MOTION_KEYS]
+    mb = MotionBatch(F, K, M, *ptrs, len(sf), ptr(sf), float(batch["th"]), int(bool(batch["check_orientation"])))
+    check(lib().orbm_search_by_projection_motion_device(C.byref(mb), tptr(kp_match), tptr(n_matches),
+                                                        stream_ptr(stream)),
+          "orbm_search_by_projection_motion_device")
+    return kp_match, n_matches

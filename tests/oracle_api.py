@@ -270,6 +270,36 @@ def proj_batch(keep, b):
                      keep(b["scale_factors"], np.float32), float(b["th"]), float(b["nnratio"]))
 
 
+class MotionBatch(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("total_kp", C.c_int32), ("total_mp", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_uright", C.c_void_p),
+                ("kp_desc", C.c_void_p), ("kp_angle", C.c_void_p), ("kp_claimed", C.c_void_p), ("bounds", C.c_void_p),
+                ("mp_begin", C.c_void_p), ("mp_valid", C.c_void_p), ("mp_proj", C.c_void_p), ("mp_octave", C.c_void_p),
+                ("mp_desc", C.c_void_p), ("mp_has_obs", C.c_void_p), ("mp_angle", C.c_void_p), ("motion", C.c_void_p),
+                ("n_levels", C.c_int32), ("scale_factors", C.c_void_p), ("th", C.c_float),
+                ("check_orientation", C.c_int32)]
+
+
+_MOTION_KEYS = [("kp_begin", np.int32), ("kp_xy", np.float32), ("kp_octave", np.int32), ("kp_uright", np.float32),
+                ("kp_desc", np.uint8), ("kp_angle", np.float32), ("kp_claimed", np.uint8), ("bounds", np.float32),
+                ("mp_begin", np.int32), ("mp_valid", np.uint8), ("mp_proj", np.float32), ("mp_octave", np.int32),
+                ("mp_desc", np.uint8), ("mp_has_obs", np.uint8), ("mp_angle", np.float32), ("motion", np.int32)]
+
+
+def search_by_projection_motion(b):
+    """SearchByProjection(Frame& currFrame, const Frame& lastFrame, th, mono) per frame
+    (ORBmatcher.cc:1279-1362).  b: dict of numpy arrays (orbm_motion_batch fields)."""
+    keep = _Keep()
+    F = len(b["kp_begin"]) - 1
+    ptrs = [keep(b[k], dt) if b.get(k) is not None else None for k, dt in _MOTION_KEYS]
+    mb = MotionBatch(F, int(b["kp_begin"][-1]), int(b["mp_begin"][-1]), *ptrs, len(b["scale_factors"]),
+                     keep(b["scale_factors"], np.float32), float(b["th"]), int(b["check_orientation"]))
+    kp_match = np.zeros(max(mb.total_kp, 1), np.int32)
+    n = np.zeros(F, np.int32)
+    assert lib().oracle_search_by_projection_motion(C.byref(mb), ptr(kp_match), ptr(n)) == 0
+    return kp_match[:mb.total_kp], n
+
+
 def search_by_projection(b):
     """ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) per frame (ORBmatcher.cc:315-382)."""
     keep = _Keep()
