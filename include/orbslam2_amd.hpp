@@ -320,6 +320,16 @@ inline int SearchByProjection(const std::vector<orbx_keypoint>& keypointsUn, con
     return nm;
 }
 
+// int ORBmatcher::SearchByProjection(Frame& currFrame, const Frame& lastFrame, float th, bool monocular)
+// (src/ORBmatcher.cc:1279-1362), batched on HBM arrays (orbm_motion_batch: the caller projects the
+// last frame's points with the motion-model pose and sets motion[f] from tlc / baseline, :1286-1288).
+// Enqueue only; kp_match[k] = idx1 assigned to currFrame keypoint k or -1.
+inline void SearchByProjectionMotionBatch(const orbm_motion_batch& b, int32_t* d_kp_match, int32_t* d_n_matches,
+                                          void* stream = nullptr) {
+    check(orbm_search_by_projection_motion_device(&b, d_kp_match, d_n_matches, stream),
+          "orbm_search_by_projection_motion_device");
+}
+
 // DBoW2 ORBVocabulary: loadFromTextFile + transform(features, BowVector&, FeatureVector&, levelsup)
 // (TemplatedVocabulary.h:1130-1196, :1341-1431) with the reference's container types.
 class ORBVocabulary {

@@ -440,6 +440,67 @@ struct PjmExtra {
     int32_t* choice;   // total_mp: accepted idx2 or -1
 };
 
+// The window scan of one last-frame point (GetFeaturesInArea + the gates of :1329-1339): each lane's
+// smallest (dist << 13 | scan position), against the claim bitmap when `bits` is given.
+__device__ __forceinline__ uint32_t pjm_scan(const PjArgs& a, const PjmExtra& e, int f, int j, const uint32_t* bits,
+                                             int lane, int nlanes) {
+    const int k0 = a.kp_begin[f];
+    const int mot = e.motion ? e.motion[f] : 0;
+    const float* bd = a.bounds + 4 * (size_t)f;
+    const float minx = bd[0], miny = bd[2];
+    const float invW = PJ_COLS / (bd[1] - bd[0]), invH = PJ_ROWS / (bd[3] - bd[2]);
+    const int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
+    const int oct = a.mp_level[j];
+    const float r = a.th * a.scale[oct];   // :1316
+    // :1318-1319 through GetFeaturesInArea's checkLevels (maxLevel < 0 -> nlevels)
+    const int lo = mot == 1 ? oct : (mot == 2 ? 0 : oct - 1);
+    const int hi = mot == 1 ? a.n_levels : (mot == 2 ? oct : oct + 1);
+    const float u = a.mp_proj[3 * (size_t)j], v = a.mp_proj[3 * (size_t)j + 1];
+    const float uR = a.mp_proj[3 * (size_t)j + 2];
+    const int mincx = max((int)floorf(invW * (u - r - minx)), 0);
+    const int maxcx = min((int)ceilf(invW * (u + r - minx)), PJ_COLS - 1);
+    const int mincy = max((int)floorf(invH * (v - r - miny)), 0);
+    const int maxcy = min((int)ceilf(invH * (v + r - miny)), PJ_ROWS - 1);
+    uint32_t best = PJ_NONE;
+    if (mincx >= PJ_COLS || maxcx < 0 || mincy >= PJ_ROWS || maxcy < 0) return best;
+    const uint8_t* d1 = a.mp_desc + 32 * (size_t)j;
+    for (int cx = mincx; cx <= maxcx; cx++) {
+        const int p0 = cs[cx * PJ_ROWS + mincy], p1 = cs[cx * PJ_ROWS + maxcy + 1];
+        for (int p = p0 + lane; p < p1; p += nlanes) {
+            const int idx = a.grid_idx[k0 + p];
+            const int k = k0 + idx;
+            const int level = a.kp_oct[k];
+            if (level < lo || level > hi) continue;
+            const float distx = a.kp_xy[2 * (size_t)k] - u;
+            const float disty = a.kp_xy[2 * (size_t)k + 1] - v;
+            if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+            if (a.kp_claimed && a.kp_claimed[k]) continue;
+            if (bits && ((bits[idx >> 5] >> (idx & 31)) & 1u)) continue;
+            const float ur = a.kp_ur[k];
+            if (ur > 0 && fabsf(uR - ur) > r) continue;   // :1335
+            const int dist = pj_hamming(d1, a.kp_desc + 32 * (size_t)k);
+            best = min(best, ((uint32_t)dist << PJ_IDX_BITS) | (uint32_t)p);
+        }
+    }
+    return best;
+}
+
+// Data-parallel first pass: every point's best key against the entry claims only (a 16-lane group
+// per point).  Claims made during the call only remove candidates, so the walk keeps this key
+// whenever its keypoint is still unclaimed and rescans otherwise.
+__global__ __launch_bounds__(256) void pjm_score_kernel(PjArgs a, PjmExtra e) {
+    const int j = blockIdx.x * (256 / PJ_GW) + (threadIdx.x / PJ_GW), lane = threadIdx.x % PJ_GW;
+    if (j >= a.total_mp) return;
+    const int f = a.mp_frame[j];
+    uint32_t best = PJ_NONE;
+    if (a.kp_begin[f + 1] - a.kp_begin[f] <= PJ_MAXKP && a.mp_valid[j]) best = pjm_scan(a, e, f, j, nullptr, lane, PJ_GW);
+    best = pj_wave_min<PJ_GW>(best);
+    if (lane == 0) a.mp_cnt[j] = (int32_t)best;
+}
+
+// The ordered walk: 64 points per chunk with their first-pass keys in registers; a point whose key's
+// keypoint was claimed earlier in the call (an earlier point with observations took it) rescans its
+// window against the LDS claim bitmap.
 __global__ __launch_bounds__(64) void pjm_walk_kernel(PjArgs a, PjmExtra e) {
     __shared__ uint32_t bits[PJ_MAXKP / 32];
     const int f = blockIdx.x, lane = threadIdx.x;
@@ -453,63 +514,37 @@ __global__ __launch_bounds__(64) void pjm_walk_kernel(PjArgs a, PjmExtra e) {
     for (int i = lane; i < PJ_MAXKP / 32; i += 64) bits[i] = 0;
     for (int i = lane; i < n; i += 64) a.kp_match[k0 + i] = -1;
     __syncthreads();
-    if (a.kp_claimed)
-        for (int i = lane; i < n; i += 64)
-            if (a.kp_claimed[k0 + i]) atomicOr(&bits[i >> 5], 1u << (i & 31));
-    __syncthreads();
-    const int mot = e.motion ? e.motion[f] : 0;
-    const float* bd = a.bounds + 4 * (size_t)f;
-    const float minx = bd[0], miny = bd[2];
-    const float invW = PJ_COLS / (bd[1] - bd[0]), invH = PJ_ROWS / (bd[3] - bd[2]);
-    const int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
     int nm = 0;
-    for (int j = m0; j < m1; j++) {
-        int ch = -1;
-        if (a.mp_valid[j]) {
-            const int oct = a.mp_level[j];
-            const float r = a.th * a.scale[oct];   // :1316
-            // :1318-1319 through GetFeaturesInArea's checkLevels (maxLevel < 0 -> nlevels)
-            const int lo = mot == 1 ? oct : (mot == 2 ? 0 : oct - 1);
-            const int hi = mot == 1 ? a.n_levels : (mot == 2 ? oct : oct + 1);
-            const float u = a.mp_proj[3 * (size_t)j], v = a.mp_proj[3 * (size_t)j + 1];
-            const float uR = a.mp_proj[3 * (size_t)j + 2];
-            const int mincx = max((int)floorf(invW * (u - r - minx)), 0);
-            const int maxcx = min((int)ceilf(invW * (u + r - minx)), PJ_COLS - 1);
-            const int mincy = max((int)floorf(invH * (v - r - miny)), 0);
-            const int maxcy = min((int)ceilf(invH * (v + r - miny)), PJ_ROWS - 1);
-            uint32_t best = PJ_NONE;
-            if (!(mincx >= PJ_COLS || maxcx < 0 || mincy >= PJ_ROWS || maxcy < 0)) {
-                const uint8_t* d1 = a.mp_desc + 32 * (size_t)j;
-                for (int cx = mincx; cx <= maxcx; cx++) {
-                    const int p0 = cs[cx * PJ_ROWS + mincy], p1 = cs[cx * PJ_ROWS + maxcy + 1];
-                    for (int p = p0 + lane; p < p1; p += 64) {
-                        const int idx = a.grid_idx[k0 + p];
-                        const int k = k0 + idx;
-                        const int level = a.kp_oct[k];
-                        if (level < lo || level > hi) continue;
-                        const float distx = a.kp_xy[2 * (size_t)k] - u;
-                        const float disty = a.kp_xy[2 * (size_t)k + 1] - v;
-                        if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
-                        if ((bits[idx >> 5] >> (idx & 31)) & 1u) continue;
-                        const float ur = a.kp_ur[k];
-                        if (ur > 0 && fabsf(uR - ur) > r) continue;   // :1335
-                        const int dist = pj_hamming(d1, a.kp_desc + 32 * (size_t)k);
-                        best = min(best, ((uint32_t)dist << PJ_IDX_BITS) | (uint32_t)p);
-                    }
-                }
-            }
-            const uint32_t K = pj_wave_min(best);
-            if (K != PJ_NONE && (int)(K >> PJ_IDX_BITS) <= PJ_TH_HIGH) {   // :1347
-                ch = a.grid_idx[k0 + (int)(K & PJ_IDX_MASK)];
-                if (lane == 0) {
-                    a.kp_match[k0 + ch] = j - m0;
-                    if (a.mp_has_obs[j]) bits[ch >> 5] |= 1u << (ch & 31);
-                }
-                nm++;
-                __syncthreads();   // one wavefront: the claim bit before the next point's scan
-            }
+    for (int c = m0; c < m1; c += 64) {
+        const int j = c + lane;
+        uint32_t key = PJ_NONE;
+        int idx = -1, obs = 0;
+        if (j < m1) {
+            key = (uint32_t)a.mp_cnt[j];
+            obs = a.mp_has_obs[j];
+            if (key != PJ_NONE) idx = a.grid_idx[k0 + (int)(key & PJ_IDX_MASK)];
         }
-        if (lane == 0) e.choice[j] = ch;
+        int mych = -1;
+        const int cnt = min(64, m1 - c);
+        for (int i = 0; i < cnt; i++) {
+            uint32_t K = (uint32_t)__shfl((int)key, i, 64);
+            if (K == PJ_NONE || (int)(K >> PJ_IDX_BITS) > PJ_TH_HIGH) continue;   // :1347 (a rescan only loses candidates)
+            int ch = __shfl(idx, i, 64);
+            if ((bits[ch >> 5] >> (ch & 31)) & 1u) {   // taken earlier in this call: rescan
+                K = pj_wave_min(pjm_scan(a, e, f, c + i, bits, lane, 64));
+                if (K == PJ_NONE || (int)(K >> PJ_IDX_BITS) > PJ_TH_HIGH) continue;
+                ch = a.grid_idx[k0 + (int)(K & PJ_IDX_MASK)];
+            }
+            const int ob = __shfl(obs, i, 64);   // every lane takes part in the shuffle
+            if (lane == 0) {
+                a.kp_match[k0 + ch] = c + i - m0;
+                if (ob) bits[ch >> 5] |= 1u << (ch & 31);
+            }
+            if (lane == i) mych = ch;
+            nm++;
+            __syncthreads();   // one wavefront: the claim bit before the next point
+        }
+        if (j < m1) e.choice[j] = mych;
     }
     if (lane == 0) a.n_matches[f] = nm;
 }
@@ -741,6 +776,10 @@ extern "C" int orbm_search_by_projection_motion_device(const orbm_motion_batch* 
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(pj_grid_kernel, dim3(a.n_frames), dim3(256), 0, st, a);
     ORB_HIP_TRY(hipGetLastError());
+    if (a.total_mp > 0) {
+        hipLaunchKernelGGL(pjm_score_kernel, dim3((a.total_mp + 256 / PJ_GW - 1) / (256 / PJ_GW)), dim3(256), 0, st, a, e);
+        ORB_HIP_TRY(hipGetLastError());
+    }
     hipLaunchKernelGGL(pjm_walk_kernel, dim3(a.n_frames), dim3(64), 0, st, a, e);
     ORB_HIP_TRY(hipGetLastError());
     if (b->check_orientation) {
