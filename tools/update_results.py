@@ -34,6 +34,8 @@ the timed region is {d['timed_region_s']:.2f} s at 20 steps):
 | SearchByProjection, 256 frames × (2000 keypoints, 1500 map points) | **{d['search_by_projection']['frames_per_s']/1e6:.2f}M frames/s** ({d['search_by_projection']['ms_per_step']:.2f} ms per launch set; round 1: 282k) |
 | ComputeBoW, 128 frames × 2000 descriptors, k 10 L 6 vocabulary | {d['bow']['frames_per_s']/1000:.0f}k frames/s ({d['bow']['ms_per_step']:.2f} ms; round 1: 495k) |
 | PoseOptimization, 1024 frames × 1000 edges (40 % stereo, 10 % outliers) | {d['pose_opt']['frames_per_s']/1e6:.2f}M frames/s ({d['pose_opt']['ms_per_step']:.2f} ms per launch) |
+| SearchByBoW(KeyFrame, Frame), 128 pairs × 2000 features, levelsup 4, CheckOrientation | {d['bow']['search_by_bow']['pairs_per_s']/1000:.0f}k pairs/s ({d['bow']['search_by_bow']['ms_per_step']:.3f} ms; CPU oracle {d['bow']['search_by_bow']['cpu_baseline']['pairs_per_s']/1000:.1f}k pairs/s, 1 thread) |
+| SearchByProjection(Frame, lastFrame) motion model, 256 frames × (2000 keypoints, 1500 points), th 7 | {d['search_by_projection']['motion_model']['frames_per_s']/1000:.0f}k frames/s ({d['search_by_projection']['motion_model']['ms_per_step']:.2f} ms; CPU oracle {d['search_by_projection']['motion_model']['cpu_baseline']['frames_per_s']/1000:.1f}k frames/s, 1 thread) |
 
 PMC busy per kernel this round (`profiles/r02_pmc_busy_summary.txt`, 1024 pan frames): fast_cells
 VALU 84 % / SALU 65 %, describe 71 / 74, pyramid pair 91 / 41, quadtree 35 / 22, FP4 matcher 56 / 7.
@@ -54,6 +56,8 @@ t = t[:a] + (f"Current numbers (one MI355X, `profiles/r02_bench.json`): {d['valu
              f"CPU restatement on 16 threads\n({d['cpu_baseline']['single_thread']['value']:.1f} on one); C3 stereo extract + "
              f"SearchForTriangulation {d['c3']['pairs_per_s']/1000:.1f}k pairs/s; LocalBA (20 KF × 3000 MP)\n"
              f"{lb['iters_per_s']/1000:.2f}k LM iterations/s; SearchByProjection {d['search_by_projection']['frames_per_s']/1e6:.2f}M "
-             f"frames/s (256 × 2000 keypoints × 1500 map points).\n") + t[b:]
+             f"frames/s (256 × 2000 keypoints × 1500 map points); SearchByBoW "
+             f"{d['bow']['search_by_bow']['pairs_per_s']/1000:.0f}k pairs/s; motion-model SearchByProjection "
+             f"{d['search_by_projection']['motion_model']['frames_per_s']/1000:.0f}k frames/s.\n") + t[b:]
 r.write_text(t)
 print("updated", d["value"])
