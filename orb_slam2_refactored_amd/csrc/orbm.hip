@@ -1041,6 +1041,16 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(BowArgs a) {
         const int c0 = off2[lo], n2 = min(off2[lo + 1] - c0, BOW_MAX_CAND);
         const int nch = (n2 + 63) >> 6;
         unsigned long long claimed = 0;   // bit k: candidate 64k + lane
+        // the first 64 candidates stay in registers for all of the node's queries (their index and
+        // descriptor loads are off the per-query dependency chain)
+        uint4 cd0 = make_uint4(0, 0, 0, 0), cd1 = cd0;
+        bool ok0 = false;
+        if (lane < n2) {
+            const long long g2 = base2 + idx2[c0 + lane];
+            ok0 = !a.mp2 || a.mp2[g2];
+            cd0 = D2[2 * g2];
+            cd1 = D2[2 * g2 + 1];
+        }
         for (int u = off1[na]; u < off1[na + 1]; u++) {
             const int i1 = idx1[u];
             const long long g1 = base1 + i1;
@@ -1050,9 +1060,22 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(BowArgs a) {
             int d2 = 256;
             for (int k = 0; k < nch; k++) {
                 const int pos = 64 * k + lane;
-                const long long g2 = pos < n2 ? base2 + idx2[c0 + pos] : 0;
-                if (pos < n2 && !((claimed >> k) & 1ull) && (!a.mp2 || a.mp2[g2])) {   // matched2 / mappoint2 (:733)
-                    const int d = hamming8(q0, q1, D2[2 * g2], D2[2 * g2 + 1]);
+                bool ok;
+                uint4 b0, b1;
+                if (k == 0) {
+                    ok = ok0;
+                    b0 = cd0;
+                    b1 = cd1;
+                } else {
+                    const long long g2 = pos < n2 ? base2 + idx2[c0 + pos] : 0;
+                    ok = pos < n2 && (!a.mp2 || a.mp2[g2]);
+                    if (ok) {
+                        b0 = D2[2 * g2];
+                        b1 = D2[2 * g2 + 1];
+                    }
+                }
+                if (ok && !((claimed >> k) & 1ull)) {   // matched2 / mappoint2 (:733)
+                    const int d = hamming8(q0, q1, b0, b1);
                     const uint32_t key = ((uint32_t)d << 16) | (uint32_t)pos;
                     if (key < k1) {
                         d2 = min(d2, (int)(k1 >> 16));
