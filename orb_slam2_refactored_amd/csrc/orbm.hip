@@ -1051,11 +1051,25 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(BowArgs a) {
             cd0 = D2[2 * g2];
             cd1 = D2[2 * g2 + 1];
         }
-        for (int u = off1[na]; u < off1[na + 1]; u++) {
-            const int i1 = idx1[u];
-            const long long g1 = base1 + i1;
-            if (a.mp1 && !a.mp1[g1]) continue;   // !mappoint1 || mappoint1->isBad() (:472)
-            const uint4 q0 = D1[2 * g1], q1 = D1[2 * g1 + 1];
+        // the next query's index, MapPoint flag and descriptor are loaded while this one is matched
+        const int u1 = off1[na + 1];
+        int i1n = 0;
+        bool vn = false;
+        uint4 qn0 = make_uint4(0, 0, 0, 0), qn1 = qn0;
+        auto fetch = [&](int uu) {
+            i1n = idx1[uu];
+            const long long g = base1 + i1n;
+            vn = !a.mp1 || a.mp1[g];
+            qn0 = D1[2 * g];
+            qn1 = D1[2 * g + 1];
+        };
+        if (off1[na] < u1) fetch(off1[na]);
+        for (int u = off1[na]; u < u1; u++) {
+            const int i1 = i1n;
+            const bool valid = vn;
+            const uint4 q0 = qn0, q1 = qn1;
+            if (u + 1 < u1) fetch(u + 1);
+            if (!valid) continue;   // !mappoint1 || mappoint1->isBad() (:472)
             uint32_t k1 = 0xffffffffu;
             int d2 = 256;
             for (int k = 0; k < nch; k++) {
