@@ -478,21 +478,21 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
             v += b.Hpp[36 * i1 + threadIdx.x];
             if (r == cc) v += b.ctl->lambda;
         }
-        __hip_atomic_store(&b.Spart[((long long)part * b.nblk + blk) * 36 + threadIdx.x], v, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        b.Spart[((long long)part * b.nblk + blk) * 36 + threadIdx.x] = v;
     }
+    // Hand-off by the memory model: the partials' stores happen before thread 0's agent-scope
+    // release (workgroup barrier), and the last part's agent-scope acquire happens before its loads
+    // (the same barrier pattern on the consumer side).
     __shared__ int s_last;
-    if (threadIdx.x == 0) {   // wavefront 0 stored the partials: wait for them, then count in
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = __hip_atomic_fetch_add(&b.blk_done[blk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 SB_SPLIT - 1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_last = __hip_atomic_fetch_add(&b.blk_done[blk], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == SB_SPLIT - 1;
+        if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     if (s_last && threadIdx.x < 36) {
         double v = 0;
-        for (int k = 0; k < SB_SPLIT; k++)
-            v += __hip_atomic_load(&b.Spart[((long long)k * b.nblk + blk) * 36 + threadIdx.x], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < SB_SPLIT; k++) v += b.Spart[((long long)k * b.nblk + blk) * 36 + threadIdx.x];
         b.S[(long long)(6 * i1 + r) * D + 6 * i2 + cc] = v;
         if (i1 != i2) b.S[(long long)(6 * i2 + cc) * D + 6 * i1 + r] = v;
         if (threadIdx.x == 0) __hip_atomic_store(&b.blk_done[blk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

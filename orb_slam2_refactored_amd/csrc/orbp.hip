@@ -451,6 +451,8 @@ __device__ __forceinline__ uint32_t pjm_scan(const PjArgs& a, const PjmExtra& e,
     const float invW = PJ_COLS / (bd[1] - bd[0]), invH = PJ_ROWS / (bd[3] - bd[2]);
     const int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
     const int oct = a.mp_level[j];
+    uint32_t best = PJ_NONE;
+    if (oct < 0 || oct >= a.n_levels) return best;   // no level to project at: no candidate
     const float r = a.th * a.scale[oct];   // :1316
     // :1318-1319 through GetFeaturesInArea's checkLevels (maxLevel < 0 -> nlevels)
     const int lo = mot == 1 ? oct : (mot == 2 ? 0 : oct - 1);
@@ -461,7 +463,6 @@ __device__ __forceinline__ uint32_t pjm_scan(const PjArgs& a, const PjmExtra& e,
     const int maxcx = min((int)ceilf(invW * (u + r - minx)), PJ_COLS - 1);
     const int mincy = max((int)floorf(invH * (v - r - miny)), 0);
     const int maxcy = min((int)ceilf(invH * (v + r - miny)), PJ_ROWS - 1);
-    uint32_t best = PJ_NONE;
     if (mincx >= PJ_COLS || maxcx < 0 || mincy >= PJ_ROWS || maxcy < 0) return best;
     const uint8_t* d1 = a.mp_desc + 32 * (size_t)j;
     for (int cx = mincx; cx <= maxcx; cx++) {
@@ -506,13 +507,13 @@ __global__ __launch_bounds__(64) void pjm_walk_kernel(PjArgs a, PjmExtra e) {
     const int f = blockIdx.x, lane = threadIdx.x;
     const int k0 = a.kp_begin[f], n = a.kp_begin[f + 1] - k0;
     const int m0 = a.mp_begin[f], m1 = a.mp_begin[f + 1];
+    for (int i = lane; i < n; i += 64) a.kp_match[k0 + i] = -1;   // also for an over-limit frame
     if (n > PJ_MAXKP) {
         for (int j = m0 + lane; j < m1; j += 64) e.choice[j] = -1;
         if (lane == 0) a.n_matches[f] = -1;
         return;
     }
     for (int i = lane; i < PJ_MAXKP / 32; i += 64) bits[i] = 0;
-    for (int i = lane; i < n; i += 64) a.kp_match[k0 + i] = -1;
     __syncthreads();
     int nm = 0;
     for (int c = m0; c < m1; c += 64) {

@@ -114,6 +114,36 @@ class ORBmatcher:
         return [(int(i), int(out[i])) for i in idx1], out
 
 
+def _check_fv(fv, n_frames: int, name: str):
+    """A FeatureVector batch (node [F, fv_cap], off [F, fv_cap + 1], idx [F, fv_cap], n_nodes [F]) as
+    ORBVocabulary.transform_batch_device returns it: contiguous int32 tensors of consistent shapes
+    covering at least n_frames frames (the kernels read fv_cap from node's width)."""
+    import torch
+    if not isinstance(fv, (tuple, list)) or len(fv) != 4:
+        raise ValueError(f"{name} must be (node, off, idx, n_nodes)")
+    node, off, idx, nn = fv
+    for t in fv:
+        if not isinstance(t, torch.Tensor) or t.dtype != torch.int32 or not t.is_contiguous():
+            raise ValueError(f"{name}: every FeatureVector tensor must be a contiguous int32 tensor")
+    if node.dim() != 2:
+        raise ValueError(f"{name}: node must be [F, fv_cap]")
+    F, cap = int(node.shape[0]), int(node.shape[1])
+    if tuple(off.shape) != (F, cap + 1) or tuple(idx.shape) != (F, cap) or tuple(nn.shape) != (F,):
+        raise ValueError(f"{name}: off / idx / n_nodes must be [F, fv_cap + 1] / [F, fv_cap] / [F]")
+    if F < n_frames:
+        raise ValueError(f"{name}: {F} frames, {n_frames} needed")
+
+
+def _check_frames(t, P: int, name: str):
+    """An optional per-pair frame index tensor: contiguous int32 [P] (values must index the slot set)."""
+    import torch
+    if t is None:
+        return
+    if not isinstance(t, torch.Tensor) or t.dtype != torch.int32 or not t.is_contiguous() or t.dim() != 1 or \
+            int(t.shape[0]) < P:
+        raise ValueError(f"{name} must be a contiguous int32 [P] tensor")
+
+
 def search_for_triangulation_batch_device(kps1, desc1, counts1, kps2, desc2, counts2, F12, ep2, scale_factors2,
                                           sigma2, frame1=None, frame2=None, uright1=None, uright2=None,
                                           has_mappoint1=None, has_mappoint2=None, fv1=None, fv2=None,
@@ -136,6 +166,12 @@ def search_for_triangulation_batch_device(kps1, desc1, counts1, kps2, desc2, cou
             raise ValueError("keypoint / descriptor slots must be contiguous [F, cap, 7] / [F, cap, 32]")
     if ep2.shape[0] != P or F12.shape[-1] != 9 or ep2.shape[-1] != 2:
         raise ValueError("F12 must be [P, 9] and ep2 [P, 2]")
+    _check_frames(frame1, P, "frame1")
+    _check_frames(frame2, P, "frame2")
+    if fv1 is not None:
+        _check_fv(fv1, int(kps1.shape[0]), "fv1")
+    if fv2 is not None:
+        _check_fv(fv2, int(kps2.shape[0]), "fv2")
     if out is None:
         out = (torch.empty((P, cap1), dtype=torch.int32, device=kps1.device),
                torch.empty((P,), dtype=torch.int32, device=kps1.device))
@@ -173,6 +209,9 @@ def search_by_bow_batch_device(kps1, desc1, fv1, kps2, desc2, counts2, fv2, fram
             raise ValueError("keypoint / descriptor slots must be contiguous [F, cap, 7] / [F, cap, 32]")
     if desc2.shape[0] < P:
         raise ValueError("set 2 needs one frame per pair")
+    _check_frames(frame1, P, "frame1")
+    _check_fv(fv1, int(desc1.shape[0]), "fv1")
+    _check_fv(fv2, P, "fv2")
     if out is None:
         out = (torch.empty((P, cap2), dtype=torch.int32, device=desc2.device),
                torch.empty((P,), dtype=torch.int32, device=desc2.device))
@@ -199,6 +238,12 @@ def search_by_bow_kf_batch_device(kps1, desc1, counts1, fv1, kps2, desc2, counts
         if k.dim() != 3 or k.shape[2] != 7 or d.shape[:2] != k.shape[:2] or d.shape[2] != 32 or \
                 not k.is_contiguous() or not d.is_contiguous():
             raise ValueError("keypoint / descriptor slots must be contiguous [F, cap, 7] / [F, cap, 32]")
+    _check_frames(frame1, P, "frame1")
+    _check_frames(frame2, P, "frame2")
+    if frame1 is None and desc1.shape[0] < P or frame2 is None and desc2.shape[0] < P:
+        raise ValueError("without frame1 / frame2 each set needs one frame per pair")
+    _check_fv(fv1, int(desc1.shape[0]), "fv1")
+    _check_fv(fv2, int(desc2.shape[0]), "fv2")
     if out is None:
         out = (torch.empty((P, cap1), dtype=torch.int32, device=desc1.device),
                torch.empty((P,), dtype=torch.int32, device=desc1.device))
