@@ -588,96 +588,62 @@ static bool pyr_pair_fits(const Geom& g, int l) {
 // A pixel is a FAST-9 corner at threshold t iff M > t, and cornerScore<16> == M - 1 for every
 // detected corner (threshold-independent), so one M map serves both the iniThFAST pass and the
 // minThFAST retry of DetectFAST.
+//
+// Cost model (PMC, tools/pmc_ab.sh): the kernel is issue-bound -- time follows the total count of
+// instructions a wave issues (VALU + SALU + branch + LDS, about 2 cycles each per SIMD) and the VALU
+// pipe's occupancy (v_pk_*, v_perm, v_alignbyte, v_mbcnt, v_cmp take 4 cycles, v_add/v_and/v_or/
+// v_bitop3 and the unpacked 16-bit forms 2: tools/probe/issue_probe3).  So the tests below use the
+// fewest instructions (packed u16, 2 pixels per instruction), not the cheapest ones, and avoid
+// per-pixel branches.
+template <int IMM>
+__device__ __forceinline__ uint32_t bt3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, IMM); }
+constexpr int BT_OR3 = 0xFE;   // a | b | c (truth tables over (a, b, c) = (0xF0, 0xCC, 0xAA))
 
-__device__ __forceinline__ int corner_strength(const uint8_t* c, int cs) {   // c -> centre pixel in LDS
-    const int v = c[0];
-    int d[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]];
-    int lo2[16], hi2[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        lo2[k] = min(d[k], d[(k + 1) & 15]);
-        hi2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int lo4[16], hi4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        lo4[k] = min(lo2[k], lo2[(k + 2) & 15]);
-        hi4[k] = max(hi2[k], hi2[(k + 2) & 15]);
-    }
-    int M = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int lo8 = min(lo4[k], lo4[(k + 4) & 15]);
-        const int hi8 = max(hi4[k], hi4[(k + 4) & 15]);
-        const int lo9 = min(lo8, d[(k + 8) & 15]);
-        const int hi9 = max(hi8, d[(k + 8) & 15]);
-        M = max(M, max(lo9, -hi9));
-    }
-    return M;
-}
-
-// Cheap exact test for "corner at threshold t": a 9-run of bright or of dark circle pixels.
-__device__ __forceinline__ bool is_corner_t(const uint8_t* c, int t, int cs) {
-    const int v = c[0];
-    unsigned br = 0, dk = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int p = c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]];
-        br |= (unsigned)(p > v + t) << k;
-        dk |= (unsigned)(p < v - t) << k;
-    }
-    auto run9 = [](unsigned m) {
-        unsigned x = m | (m << 16);
-        unsigned a = x & (x >> 1);
-        unsigned b = a & (a >> 2);
-        unsigned c2 = b & (b >> 4);
-        return (c2 & (x >> 8) & 0xffffu) != 0;
-    };
-    return run9(br) || run9(dk);
-}
-
-// Necessary condition for a 9-arc at threshold t, on 4 horizontally adjacent pixels at once: two
-// circle-adjacent compass points (positions 0/4/8/12) both brighter than v+t, or both darker than
-// v-t.  With packed u16 lanes: bright <=> max over the 4 adjacent pairs of min(pa, pb) > v + t,
-// dark <=> min over the pairs of max(pa, pb) < v - t (no clamping needed: p <= 255).
-__device__ __forceinline__ uint32_t us2u(us2 a) { return __builtin_bit_cast(uint32_t, a); }
+// Two-of-four pre-test on packed u16 lanes.  A dword w of pixels x..x+3 is used as two words of
+// u16 lanes: the even pixels (x, x+2) unpacked, w & 0x00ff00ff, and the odd pixels (x+1, x+3) in
+// place, i.e. in each lane's high byte with the even pixel as a low byte.  The odd lanes' thresholds
+// carry the low byte that makes the comparison depend on the high byte only:
+//   p*256 + q > (v + t)*256 + 255  <=>  p > v + t     (saturated at 0xffff when v + t > 255)
+//   (v - t)*256 > p*256 + q        <=>  p < v - t     (saturated at 0 when v < t)
+// and max / min of such words order by the high byte first, so the same network serves both halves.
+// Pass condition for four circle points at 90-degree steps (p1, p3 opposite; p2, p4 opposite): two
+// circle-adjacent ones both brighter than v + t or both darker than v - t, which factors to
+// (B1 | B3) & (B2 | B4):  min(max(p1, p3), max(p2, p4)) > hi  or  max(min(p1, p3), min(p2, p4)) < lo.
+struct PkThr {
+    us2 hi_e, lo_e, hi_o, lo_o;
+};
 __device__ __forceinline__ us2 u2us(uint32_t a) { return __builtin_bit_cast(us2, a); }
-__device__ __forceinline__ us2 lo_pair(uint32_t w) {   // bytes 0,1 -> u16 lanes
-    const uint32_t r = __builtin_amdgcn_perm(0u, w, 0x0c010c00u);
-    return *reinterpret_cast<const us2*>(&r);
+__device__ __forceinline__ uint32_t us2u(us2 a) { return __builtin_bit_cast(uint32_t, a); }
+__device__ __forceinline__ us2 pk_even(uint32_t w) { return u2us(w & 0x00ff00ffu); }
+__device__ __forceinline__ PkThr pk_thresholds(uint32_t wv, int t) {
+    const unsigned short tc = (unsigned short)min(max(t, 0), 255);   // cv::FAST clamps the threshold
+    const us2 t1 = {tc, tc}, t8 = {(unsigned short)(tc << 8), (unsigned short)(tc << 8)};
+    PkThr r;
+    const us2 ve = pk_even(wv);
+    r.hi_e = ve + t1;                                                        // <= 510: no wrap
+    r.lo_e = __builtin_elementwise_sub_sat(ve, t1);
+    r.hi_o = __builtin_elementwise_add_sat(u2us(wv | 0x00ff00ffu), t8);      // (v + t)*256 + 255, saturated
+    r.lo_o = __builtin_elementwise_sub_sat(u2us(wv & 0xff00ff00u), t8);      // (v - t)*256, saturated
+    return r;
 }
-__device__ __forceinline__ us2 hi_pair(uint32_t w) {   // bytes 2,3 -> u16 lanes
-    const uint32_t r = __builtin_amdgcn_perm(0u, w, 0x0c030c02u);
-    return *reinterpret_cast<const us2*>(&r);
-}
-// The four adjacent pairs factor: (Bn & Be) | (Be & Bs) | (Bs & Bw) | (Bw & Bn) == (Bn | Bs) & (Be | Bw),
-// so bright <=> min(max(n, s), max(e, w)) > v + t and dark <=> max(min(n, s), min(e, w)) < v - t.
-// Returns a u16 pair that is non-zero in the lanes of the passing pixels.
-__device__ __forceinline__ us2 compass2(us2 v, us2 n, us2 e, us2 s, us2 wv, us2 t) {
-    const us2 bmax = __builtin_elementwise_min(__builtin_elementwise_max(n, s), __builtin_elementwise_max(e, wv));
-    const us2 dmin = __builtin_elementwise_max(__builtin_elementwise_min(n, s), __builtin_elementwise_min(e, wv));
-    const us2 hi = v + t;
-    const us2 lo = __builtin_elementwise_sub_sat(v, t);
+// non-zero u16 lanes where the pixel passes
+__device__ __forceinline__ us2 pk_two_of_four(us2 p1, us2 p3, us2 p2, us2 p4, us2 hi, us2 lo) {
+    const us2 bmax = __builtin_elementwise_min(__builtin_elementwise_max(p1, p3), __builtin_elementwise_max(p2, p4));
+    const us2 dmin = __builtin_elementwise_max(__builtin_elementwise_min(p1, p3), __builtin_elementwise_min(p2, p4));
     return __builtin_elementwise_sub_sat(bmax, hi) | __builtin_elementwise_sub_sat(lo, dmin);
 }
 
 // Corner strength M (cornerScore<16> + 1, or 0 when not a corner at any threshold) on packed u16
-// pairs: lane pair k holds circle positions (k, k + 8) as D = p - v + 256 in [1, 511], so every
-// min / max of the arc network covers two arcs at once; position j >= 8 is the swapped pair j - 8.
-// Same value as corner_strength().
+// pairs: lane pair k holds circle positions (k, k + 8), so every min / max of the arc network covers
+// two arcs at once; position j >= 8 is the swapped pair j - 8.  The network runs on the raw pixels:
+// max over arcs of min(p) - v is the bright strength, v - min over arcs of max(p) the dark one.
 __device__ __forceinline__ us2 swap2(us2 a) { return __builtin_shufflevector(a, a, 1, 0); }
 __device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
-    const unsigned short bias = (unsigned short)(256 - c[0]);
-    const us2 b2 = {bias, bias};
     us2 D[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const us2 p = {(unsigned short)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]],
-                       (unsigned short)c[c_circle_dy_h[k + 8] * cs + c_circle_dx_h[k + 8]]};
-        D[k] = p + b2;
-    }
+    for (int k = 0; k < 8; k++)
+        D[k] = us2{(unsigned short)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]],
+                   (unsigned short)c[c_circle_dy_h[k + 8] * cs + c_circle_dx_h[k + 8]]};
     us2 l[8], h[8], l2[8], h2[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {   // arcs of 2
@@ -707,8 +673,9 @@ __device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
         A = __builtin_elementwise_max(A, __builtin_elementwise_min(l[k], nl));
         B = __builtin_elementwise_min(B, __builtin_elementwise_max(h[k], nh));
     }
-    const int bright = (int)max(A.x, A.y) - 256;   // max over arcs of min(p - v)
-    const int dark = 256 - (int)min(B.x, B.y);     // max over arcs of min(v - p)
+    const int v = c[0];
+    const int bright = (int)max(A.x, A.y) - v;   // max over arcs of min(p - v)
+    const int dark = v - (int)min(B.x, B.y);     // max over arcs of min(v - p)
     return max(0, max(bright, dark));
 }
 
@@ -716,14 +683,14 @@ __device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
 // (zone + 3-px apron, stored one byte right so zone column 0 is dword aligned), a zone map of
 // corner strengths, a queue of pre-test passers and the ordered list of corners.
 //   1. crop -> LDS with aligned dword loads issued together
-//   2. compass pre-test, 4 pixels per lane, passers queued in row-major order
-//   3. queued pixels get the full 9-arc test at min(ini, min) densely, 64 at a time; corners are
-//      appended in row-major order
+//   2. compass pre-test, 4 pixels per lane (SWAR), groups with a passer queued in row-major order
+//   3. diagonal pre-test on the queued groups' passers (SWAR), survivors queued per pixel; those get
+//      the corner strength densely, 64 at a time; corners are appended in row-major order
 //   4. corner strength M (cornerScore + 1) for the corner list; NMS at iniThFAST and minThFAST
 //      over the list (3x3, cell-local: neighbours outside the zone count as 0)
 //   5. emit the iniThFAST set, or the minThFAST set when it is empty (DetectFAST :527-530)
-constexpr int FQ_RING = 512;   // pre-test passer ring (power of two, >= 64 + 256)
-constexpr int FQ2_RING = 128;  // diagonal-filter passer ring (power of two, >= 64 + 64)
+constexpr int GR_RING = 128;   // pre-test group ring (u32 entries; power of two, >= 64 + 64)
+constexpr int FQ2_RING = 512;  // diagonal-filter passer ring (u16 entries; power of two, >= 64 + 256)
 constexpr int FAST_CLIST_CAP = 256;   // ordered corner list (cells with more take the zone-scan NMS)
 
 struct FastLds {
@@ -942,30 +909,33 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
 
     const int tp = spec ? th_ini : tlo;   // threshold of this pass
-    const us2 t2 = {(unsigned short)tp, (unsigned short)tp};
     // lanes: QR quads per row (8 or 16), 64/QR rows per chunk
     const int qsh = zw <= 32 ? 3 : 4;
     const int QR = 1 << qsh, RPC = 64 >> qsh;
     const int qx = (lane & (QR - 1)) * 4, qy = lane >> qsh;
-    // lane-constant masks of the pixels inside the zone (columns qx .. qx+3 < zw)
-    // (opaque to the compiler, so the AND stays one v_and instead of per-half selects)
-    uint32_t vm0 = (qx < zw ? 0xffffu : 0u) | (qx + 1 < zw ? 0xffff0000u : 0u);
-    uint32_t vm1 = (qx + 2 < zw ? 0xffffu : 0u) | (qx + 3 < zw ? 0xffff0000u : 0u);
-    asm volatile("" : "+v"(vm0), "+v"(vm1));
+    // u16-lane masks (1 / 0) of the zone's columns: even lanes hold (qx, qx+2), odd lanes (qx+1, qx+3)
+    const us2 pme = {(unsigned short)(qx < zw), (unsigned short)(qx + 2 < zw)};
+    const us2 pmo = {(unsigned short)(qx + 1 < zw), (unsigned short)(qx + 3 < zw)};
 
-    // Pre-test passers go to a ring of FQ_RING entries in row-major order.  Whenever 64 are pending
-    // they are filtered by the diagonal points 2/6/10/14 (a 9-arc also holds two circle-adjacent
-    // ones of them, bright or dark: 14 % -> 5 % of the pixels on the synthetic frames) into a
-    // second ring, and whenever 64 of those are pending they get the corner strength M densely.
-    // (pending < 64 + 256 <= FQ_RING and < 64 + 64 <= FQ2_RING, so no ring overwrites an
-    // undrained entry.)  Corners (M > min(ini, min)) get M in the zone map and are appended to
-    // the ordered corner list.
-    short* queue2 = queue + FQ_RING;
+    // Stage 1 (dense): the compass pre-test (points 0/4/8/12) on 4 pixels per lane; a lane whose group
+    // of 4 has a passer appends one entry (pass bits 0, 1, 16, 17 = pixels qx .. qx+3, the group's
+    // zone index (y << 8) | qx at bits 2-15) to a ring of GR_RING groups in row-major order.
+    // Stage 2, whenever 64 groups are pending: the diagonal pre-test (points 2/6/10/14: a 9-arc also
+    // holds two circle-adjacent ones of them) on the passers of 64 groups, survivors appended per pixel
+    // to a second ring in row-major order (14 % -> 5 % of the pixels on the synthetic frames).
+    // Stage 3, whenever 64 pixels are pending: the corner strength M densely.  Corners (M > the pass
+    // threshold) get M in the zone map and are appended to the ordered corner list.
+    // (pending groups < 64 + 64 <= GR_RING; pending pixels < 64 + 256 <= FQ2_RING.)
+    uint32_t* gring = reinterpret_cast<uint32_t*>(queue);
+    short* queue2 = queue + 2 * GR_RING;
     int qn = 0, head = 0, q2n = 0, h2 = 0, nc = 0;
     auto strength = [&](int n) {
         const int i = lane < n ? queue2[(h2 + lane) & (FQ2_RING - 1)] : -1;
         int M = 0;
         if (i >= 0) M = corner_strength_pk(&crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)], CSd);
+#ifdef FAST_DUP_STRENGTH   // diagnostic: the strength network twice (result discarded)
+        if (i >= 0) asm volatile("" ::"v"(corner_strength_pk(&crop[__mul24((i >> 8) + 4, CSd) + 4 + (i & 255)], CSd)));
+#endif
         const bool c = M > tp;
         const unsigned long long bm = __ballot(c);
         if (c) {
@@ -977,31 +947,48 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         h2 += n;
     };
     auto drain = [&](int n) {
-        const int i = lane < n ? queue[(head + lane) & (FQ_RING - 1)] : -1;
-        bool pass = false;
-        if (i >= 0) {
-            const uint8_t* c = &crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)];
-            const int v = c[0];
-            const int p2 = c[2 * CSd + 2], p6 = c[-2 * CSd + 2], p10 = c[-2 * CSd - 2], p14 = c[2 * CSd - 2];
-            pass = min(max(p2, p10), max(p6, p14)) > v + tp || max(min(p2, p10), min(p6, p14)) < v - tp;
-        }
-        const unsigned long long bm = __ballot(pass);
-        if (pass) queue2[(q2n + rank64(bm)) & (FQ2_RING - 1)] = (short)i;
-        q2n += popc64(bm);
+        const uint32_t e = lane < n ? gring[(head + lane) & (GR_RING - 1)] : 0u;   // 0: no pass bits
+        const int i0 = (int)((e >> 2) & 0x3fffu);
+        const uint8_t* c = crop + __mul24((i0 >> 8) + 3, CSd) + 4 + (i0 & 255);   // zone (y, x): dword aligned
+        const uint32_t* cp = reinterpret_cast<const uint32_t*>(c + 2 * CSd);
+        const uint32_t* cm = reinterpret_cast<const uint32_t*>(c - 2 * CSd);
+        const uint32_t wv = *reinterpret_cast<const uint32_t*>(c);
+        const uint32_t ap = cp[-1], bp = cp[0], dp = cp[1], am = cm[-1], bm_ = cm[0], dm = cm[1];
+        const uint32_t Lp = __builtin_amdgcn_alignbyte(bp, ap, 2), Rp = __builtin_amdgcn_alignbyte(dp, bp, 2);
+        const uint32_t Lm = __builtin_amdgcn_alignbyte(bm_, am, 2), Rm = __builtin_amdgcn_alignbyte(dm, bm_, 2);
+        // position 2 = (+2, +2): Rp, 10 = (-2, -2): Lm, 6 = (+2, -2): Rm, 14 = (-2, +2): Lp
+        const PkThr T = pk_thresholds(wv, tp);
+        const us2 se = __builtin_elementwise_min(
+            pk_two_of_four(pk_even(Rp), pk_even(Lm), pk_even(Rm), pk_even(Lp), T.hi_e, T.lo_e), u2us(e & 0x00010001u));
+        const us2 so = __builtin_elementwise_min(pk_two_of_four(u2us(Rp), u2us(Lm), u2us(Rm), u2us(Lp), T.hi_o, T.lo_o),
+                                                 u2us((e >> 1) & 0x00010001u));
+        // ordered compaction of up to 4 survivors per lane: one ballot per pixel slot, the lane's
+        // position = the survivors of the lower lanes (mbcnt) + its own earlier slots
+        const bool p0 = se.x != 0, p1 = so.x != 0, p2 = se.y != 0, p3 = so.y != 0;
+        const unsigned long long b0 = __ballot(p0), b1 = __ballot(p1), b2 = __ballot(p2), b3 = __ballot(p3);
+        unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0u));
+        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, pre));
+        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, pre));
+        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, pre));
+        int pos = q2n + (int)pre;
+        if (p0) queue2[pos++ & (FQ2_RING - 1)] = (short)i0;
+        if (p1) queue2[pos++ & (FQ2_RING - 1)] = (short)(i0 + 1);
+        if (p2) queue2[pos++ & (FQ2_RING - 1)] = (short)(i0 + 2);
+        if (p3) queue2[pos & (FQ2_RING - 1)] = (short)(i0 + 3);
+        q2n += popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
         head += n;
         wave_lds_sync();
-        if (q2n - h2 >= 64) strength(64);
+        while (q2n - h2 >= 64) strength(64);
     };
-    // per-lane LDS address of zone (qy, qx) = crop (qy+3, qx+3) at byte qx+4 and queue entry
-    // (qy << 8) | qx, both stepped by a wave-uniform amount per chunk of RPC rows
+    // per-lane LDS address of zone (qy, qx) = crop (qy+3, qx+3) at byte qx+4 and the group's zone index
+    // (qy << 8) | qx at bits 2-15, both stepped by a wave-uniform amount per chunk of RPC rows
     const uint8_t* rowq = crop + __mul24(qy + 3, CSd) + 4 + qx;
-    const int e0q = (qy << 8) | qx;
+    const uint32_t e0s = (uint32_t)((qy << 8) | qx) << 2;
     const bool qxin = qx < zw;
     for (int yb = 0; yb < zh; yb += RPC) {
         const int y = yb + qy;
-        us2 f0 = {0, 0}, f1 = {0, 0};
-        const bool act = y < zh && qxin;
-        if (act) {
+        us2 pe = {0, 0}, po = {0, 0};
+        if (y < zh && qxin) {
             const uint8_t* rowc = rowq + __mul24(yb, CSd);   // zone (y, qx)
             const uint32_t wv = *reinterpret_cast<const uint32_t*>(rowc);
             const uint32_t wl = *reinterpret_cast<const uint32_t*>(rowc - 4);
@@ -1010,26 +997,26 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
             const uint32_t ws = *reinterpret_cast<const uint32_t*>(rowc - 3 * CSd);   // (0,-3)
             const uint32_t we = __builtin_amdgcn_alignbyte(wr, wv, 3);   // (+3, 0): bytes qx+3..qx+6
             const uint32_t ww = __builtin_amdgcn_alignbyte(wv, wl, 1);   // (-3, 0): bytes qx-3..qx
-            f0 = u2us(us2u(compass2(lo_pair(wv), lo_pair(wn), lo_pair(we), lo_pair(ws), lo_pair(ww), t2)) & vm0);
-            f1 = u2us(us2u(compass2(hi_pair(wv), hi_pair(wn), hi_pair(we), hi_pair(ws), hi_pair(ww), t2)) & vm1);
+            const PkThr T = pk_thresholds(wv, tp);
+            pe = __builtin_elementwise_min(
+                pk_two_of_four(pk_even(wn), pk_even(ws), pk_even(we), pk_even(ww), T.hi_e, T.lo_e), pme);
+            po = __builtin_elementwise_min(pk_two_of_four(u2us(wn), u2us(ws), u2us(we), u2us(ww), T.hi_o, T.lo_o), pmo);
+#ifdef FAST_DUP_PRETEST   // diagnostic: the pre-test arithmetic twice (result discarded)
+            {
+                const PkThr T2 = pk_thresholds(wv, tp ^ yb);
+                asm volatile("" ::"v"(us2u(pk_two_of_four(pk_even(wn), pk_even(ws), pk_even(we), pk_even(ww), T2.hi_e, T2.lo_e))),
+                             "v"(us2u(pk_two_of_four(u2us(wn), u2us(ws), u2us(we), u2us(ww), T2.hi_o, T2.lo_o))));
+            }
+#endif
         }
-        // ordered compaction of up to 4 passers per lane: one ballot per pixel slot, the lane's
-        // queue position = the passers of the lower lanes (mbcnt) + its own earlier slots
-        const bool p0 = f0.x != 0, p1 = f0.y != 0, p2 = f1.x != 0, p3 = f1.y != 0;
-        const unsigned long long b0 = __ballot(p0), b1 = __ballot(p1), b2 = __ballot(p2), b3 = __ballot(p3);
-        unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0u));
-        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, pre));
-        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, pre));
-        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, pre));
-        int pos = qn + (int)pre;
-        const short e0 = (short)(e0q + (yb << 8));
-        if (p0) queue[pos++ & (FQ_RING - 1)] = e0;
-        if (p1) queue[pos++ & (FQ_RING - 1)] = (short)(e0 + 1);
-        if (p2) queue[pos++ & (FQ_RING - 1)] = (short)(e0 + 2);
-        if (p3) queue[pos & (FQ_RING - 1)] = (short)(e0 + 3);
-        qn += popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
+        const bool any = (us2u(pe) | us2u(po)) != 0;
+        const unsigned long long bm = __ballot(any);
+        if (any)
+            gring[(qn + rank64(bm)) & (GR_RING - 1)] =
+                bt3<BT_OR3>(us2u(pe), us2u(po) + us2u(po), e0s + ((uint32_t)yb << 10));
+        qn += popc64(bm);
         wave_lds_sync();
-        while (qn - head >= 64) drain(64);
+        if (qn - head >= 64) drain(64);
     }
     if (qn > head) drain(qn - head);
     if (q2n > h2) strength(q2n - h2);
@@ -2566,7 +2553,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     {
         int mzw = 1, mzh = 1;
         for (const CellDev& c : cells) { mzw = std::max(mzw, c.zwzh & 0xffff); mzh = std::max(mzh, c.zwzh >> 16); }
-        if (mzw > 64 || mzh > (FQ_RING + FQ2_RING) / 8) {   // DetectFAST cells are < 60 px (:508-511)
+        if (mzw > 64 || mzh > (2 * GR_RING + FQ2_RING) / 8) {   // DetectFAST cells are < 60 px (:508-511)
             set_error("FAST cell larger than the kernel supports");
             return ORB_EINTERNAL;
         }
@@ -2576,7 +2563,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
         fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6 + FAST_CROP_SLACK), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
-        fl.qcap = FQ_RING + FQ2_RING;
+        fl.qcap = 2 * GR_RING + FQ2_RING;   // in u16 entries
         fl.ccap = std::min(FAST_CLIST_CAP, (int)align_up((size_t)mzw * mzh, 8));
         const int nbal = (fl.ccap + 63) / 64;
         h->fast_lds = (size_t)fl.crop_bytes + fl.mz_bytes + 2 * (size_t)(fl.qcap + fl.ccap) + 16 * (size_t)nbal;
