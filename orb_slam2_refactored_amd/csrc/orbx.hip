@@ -735,7 +735,7 @@ struct CropWalk {
 
 struct CropSrc {
     const uint8_t* img;   // level base of the frame (wave-uniform)
-    int step, x0, y0, ch, ndl;
+    int step, x0, y0, ch, ndl, h;   // h: the level's height
     __device__ __forceinline__ int q(const CropWalk& w) const { return (y0 + w.row) * step + x0 - 1 + 4 * w.mm; }
     __device__ __forceinline__ int mis(int q) const {
         return (int)(((uint32_t)reinterpret_cast<uintptr_t>(img) + (uint32_t)q) & 3u);
@@ -793,18 +793,33 @@ __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint
         // dword-multiple row step (every pyramid level; level 0 unless the caller's step is odd):
         // the misalignment is one wave-uniform shift, the loads are buffer loads off a scalar
         // resource with a per-lane constant voffset and a per-group soffset (no address VALU),
-        // and a partial last group writes into the crop's slack rows (FAST_CROP_SLACK)
+        // and a partial last group writes into the crop's slack rows (FAST_CROP_SLACK).  The resource
+        // ends with the level, so loads of groups past it return 0 instead of needing a clamp, and the
+        // first batch stores all CROP_NG groups unconditionally (the crop buffer holds CROP_NG * 4 rows,
+        // and groups past the crop only fill rows nothing reads): no per-group scalar control.
         const int m = __builtin_amdgcn_readfirstlane((int)(reinterpret_cast<uintptr_t>(g0) & 3u));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g0 - m), 0, 0x7fffffff, 0x00020000);
+        const int avail = (c.h - c.y0) * c.step - (c.x0 - 1) + m;   // bytes from g0 - m to the level's end
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g0 - m), 0, avail, 0x00020000);
         const int voff = roff * c.step + 4 * dd;
         uint32_t* lrow = reinterpret_cast<uint32_t*>(crop + roff * CSd) + d;
         const int gstep = RPG * c.step, lstep = RPG * CSd / 4;
-        for (int k0 = 0; k0 < ng; k0 += CROP_NG) {
+        {
             u32x2a4 v[CROP_NG];
 #pragma unroll
             for (int k = 0; k < CROP_NG; k++) {
-                const int gk = min(k0 + k, ng - 1);   // groups past the crop re-read the last one
-                const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, gk * gstep, 0);
+                const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, k * gstep, 0);
+                v[k] = u32x2a4{t[0], t[1]};
+            }
+            if (dok) {
+#pragma unroll
+                for (int k = 0; k < CROP_NG; k++) lrow[k * lstep] = __builtin_amdgcn_alignbyte(v[k].y, v[k].x, m);
+            }
+        }
+        for (int k0 = CROP_NG; k0 < ng; k0 += CROP_NG) {   // crops taller than CROP_NG groups (rare)
+            u32x2a4 v[CROP_NG];
+#pragma unroll
+            for (int k = 0; k < CROP_NG; k++) {
+                const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (k0 + k) * gstep, 0);
                 v[k] = u32x2a4{t[0], t[1]};
             }
             if (dok) {
@@ -880,6 +895,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         c.y0 = cd.x0y0 >> 16;
         c.ch = (cd.zwzh >> 16) + 6;
         c.ndl = ((cd.zwzh & 0xffff) + 6 + 1 + 3) >> 2;   // LDS dwords per crop row
+        c.h = g.lv[cd.level].h;
         return c;
     };
     // Speculative iniThFAST pass: a cell whose predecessor in this wavefront (the neighbouring cell
@@ -2561,7 +2577,9 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         fl.CS = (int)align_up(mzw + 6 + 8, 4);         // +1 shift, +4 dword over-read each side
         if (fl.CS < 4 * ((mzw + 6 + 1 + 3) / 4)) fl.CS = 4 * ((mzw + 6 + 1 + 3) / 4);
         fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
-        fl.crop_bytes = (int)align_up((size_t)fl.CS * (mzh + 6 + FAST_CROP_SLACK), 16);
+        // rows: the tallest crop + slack, and at least the CROP_NG row groups of 4 rows the staging's first
+        // batch always stores
+        fl.crop_bytes = (int)align_up((size_t)fl.CS * std::max(mzh + 6 + FAST_CROP_SLACK, 4 * CROP_NG), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
         fl.qcap = 2 * GR_RING + FQ2_RING;   // in u16 entries
         fl.ccap = std::min(FAST_CLIST_CAP, (int)align_up((size_t)mzw * mzh, 8));
