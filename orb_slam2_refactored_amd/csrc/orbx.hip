@@ -2337,7 +2337,7 @@ struct orbx_extractor {
     size_t qt_lds = 0;
     FastLds fl;
     size_t fast_lds = 0;
-    int fast_cpw = 4;   // FAST cells per wavefront (1 -> 4: -3 % at C2; ORBX_FAST_CPW)
+    int fast_cpw = 16;  // FAST cells per wavefront (4 -> 16: -2 % pan, -17 % textured: fewer first cells without a speculation hint; ORBX_FAST_CPW)
     // a cell runs the speculative iniThFAST pass when the wavefront's previous cell kept at least
     // fast_spec corners at iniThFAST (texture-rich regions); 0 = never (ORBX_FAST_SPEC)
     int fast_spec = 8;

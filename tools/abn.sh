@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B/n on one GPU box: every tools/ab/lib_*.so (ORBSLAM2_AMD_LIB) and the in-tree library ("new"),
-# alternating, REPS rounds, over SETS (kbench argument sets separated by ';').  Optional parity tests
+# and the in-tree library under each ENVV setting ("NAME=VALUE ..."), alternating, REPS rounds, over SETS (kbench argument sets separated by ';').  Optional parity tests
 # of the in-tree build first (TESTS, "none" to skip).  Each GPU step is time-limited; stops on failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -19,10 +19,13 @@ IFS=';' read -ra SETA <<< "$SETS"
 for set in "${SETA[@]}"; do
   echo "== $set"
   for i in $(seq 1 $REPS); do
-    for lib in tools/ab/lib_*.so new; do
-      if [ "$lib" = new ]; then unset ORBSLAM2_AMD_LIB; v=new; else export ORBSLAM2_AMD_LIB=$PWD/$lib; v=$(basename $lib .so); fi
+    for lib in tools/ab/lib_*.so new $ENVV; do
+      ev=""
+      if [ "$lib" = new ]; then unset ORBSLAM2_AMD_LIB; v=new;
+      elif [[ "$lib" == *=* ]]; then unset ORBSLAM2_AMD_LIB; v=env_${lib//=/_}; ev=$lib;
+      else export ORBSLAM2_AMD_LIB=$PWD/$lib; v=$(basename $lib .so); fi
       lg=gpurun_out/abn_${v}_$i.log
-      timeout -k 10 120 python tools/kbench.py --iters 10 --match $set > $lg 2>&1 || { tail -5 $lg; exit 5; }
+      env $ev timeout -k 10 120 python tools/kbench.py --iters 10 --match $set > $lg 2>&1 || { tail -5 $lg; exit 5; }
       echo "$v: $(grep wall $lg)"
     done
   done
