@@ -384,6 +384,45 @@ typedef struct orbm_motion_batch {
 int orbm_search_by_projection_motion_device(const orbm_motion_batch* b, int32_t* kp_match, int32_t* n_matches,
                                             void* stream);
 
+/* int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
+ * std::vector<int>& vnMatches12, int windowSize) (include/ORBmatcher.h:81, src/ORBmatcher.cc:614-694;
+ * Tracking::MonocularInitialization, Tracking.cc:1052), batched over initialisation pairs.
+ * Pair p: frame F1 (queries idx1) = [q_begin[p], q_begin[p+1]) and frame F2 (searched) =
+ * [kp_begin[p], kp_begin[p+1]), both keypointsUn.  Only octave-0 queries search, over the octave-0
+ * features of F2 inside FeaturesGrid::GetFeaturesInArea(prevMatched, windowSize) (Frame.cc:102-145,
+ * scan order cell by cell); a candidate is skipped when the distance it is already held at
+ * (matchedDistance, INT_MAX on entry) is <= its own, so a later query can take a feature from an
+ * earlier one (matches12 of the earlier query becomes -1, :669-673).  Accept best <= TH_LOW and
+ * best < nnratio * second; then, with check_orientation, CheckOrientation(F2.keypointsUn,
+ * F1.keypointsUn, matchIds, matches12) (:249-309) over every accepted (idx2, idx1) in order,
+ * replaced ones included, whose count is the return value.  prev_matched[q] (total_q x 2, in/out)
+ * becomes F2.keypointsUn[matches12[q]].pt for every surviving match (:690-692).
+ * matches12[q] = F2-relative idx2 or -1; n_matches[p] = the return value, -1 (device entry) when a
+ * frame of the pair has more than ORBM_PROJ_MAX_KP keypoints. */
+typedef struct orbm_init_batch {
+    int32_t        n_pairs, total_kp, total_q;
+    const int32_t* kp_begin;     /* F2: n_pairs + 1 */
+    const float*   kp_xy;        /* F2 keypointsUn pt, total_kp x 2 */
+    const int32_t* kp_octave;    /* F2 keypointsUn octave */
+    const uint8_t* kp_desc;      /* F2 descriptors, total_kp x 32 */
+    const float*   kp_angle;     /* F2 keypointsUn angle (CheckOrientation) */
+    const float*   bounds;       /* F2 imageBounds, n_pairs x 4 */
+    const int32_t* q_begin;      /* F1: n_pairs + 1 */
+    const int32_t* q_octave;     /* F1 keypointsUn octave */
+    const uint8_t* q_desc;       /* F1 descriptors, total_q x 32 */
+    const float*   q_angle;      /* F1 keypointsUn angle */
+    float*         prev_matched; /* total_q x 2, in / out */
+    int32_t        window;       /* windowSize (100 in MonocularInitialization) */
+    float          nnratio;      /* ORBmatcher(0.9f, true) there */
+    int32_t        check_orientation;
+} orbm_init_batch;
+
+/* Host entry: every pointer host memory, synchronous. */
+int orbm_search_for_initialization(const orbm_init_batch* b, int32_t* matches12, int32_t* n_matches, int device);
+/* Device entry: every array in HBM; enqueue only on `stream`. */
+int orbm_search_for_initialization_device(const orbm_init_batch* b, int32_t* matches12, int32_t* n_matches,
+                                          void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Bag of words.  Replaces DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> as ORBVocabulary
  * (include/ORBVocabulary.h) for Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:208-214,

@@ -184,6 +184,49 @@ public:
         check(orbm_search_by_bow_kf_batch_device(&b, d_match12, d_nmatches, stream), "orbm_search_by_bow_kf_batch_device");
     }
 
+    // int SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& prevMatched,
+    //                             std::vector<int>& matches12, int windowSize = 10)
+    // (include/ORBmatcher.h:81, src/ORBmatcher.cc:614-694) on the frames' keypointsUn (cv::KeyPoint
+    // layout), 32-byte descriptors and F2's image bounds; prevMatched as (x, y) pairs, updated in place.
+    // nnratio / checkOri are this matcher's (Tracking.cc:1051 builds ORBmatcher(0.9f, true)).
+    int SearchForInitialization(const std::vector<orbx_keypoint>& keypointsUn1, const uint8_t* descriptors1,
+                                const std::vector<orbx_keypoint>& keypointsUn2, const uint8_t* descriptors2,
+                                const float bounds2[4], std::vector<float>& prevMatched, std::vector<int>& matches12,
+                                int windowSize = 10, int device = 0) const {
+        const int n1 = (int)keypointsUn1.size(), n2 = (int)keypointsUn2.size();
+        if ((int)prevMatched.size() != 2 * n1)
+            throw std::invalid_argument("SearchForInitialization: prevMatched must hold 2 floats per F1 keypoint");
+        std::vector<float> xy2(2 * (size_t)n2), ang2(n2), ang1(n1);
+        std::vector<int32_t> oct2(n2), oct1(n1);
+        for (int i = 0; i < n2; i++) {
+            xy2[2 * i] = keypointsUn2[i].x; xy2[2 * i + 1] = keypointsUn2[i].y;
+            oct2[i] = keypointsUn2[i].octave; ang2[i] = keypointsUn2[i].angle;
+        }
+        for (int i = 0; i < n1; i++) { oct1[i] = keypointsUn1[i].octave; ang1[i] = keypointsUn1[i].angle; }
+        const int32_t kb[2] = {0, n2}, qb[2] = {0, n1};
+        orbm_init_batch b;
+        b.n_pairs = 1; b.total_kp = n2; b.total_q = n1;
+        b.kp_begin = kb; b.kp_xy = xy2.data(); b.kp_octave = oct2.data(); b.kp_desc = descriptors2; b.kp_angle = ang2.data();
+        b.bounds = bounds2; b.q_begin = qb; b.q_octave = oct1.data(); b.q_desc = descriptors1; b.q_angle = ang1.data();
+        b.prev_matched = prevMatched.data(); b.window = windowSize; b.nnratio = nnratio_;
+        b.check_orientation = checkOri_ ? 1 : 0;
+        std::vector<int32_t> m(std::max(n1, 1));
+        int32_t nm = 0;
+        check(orbm_search_for_initialization(&b, m.data(), &nm, device), "orbm_search_for_initialization");
+        matches12.assign(m.begin(), m.begin() + n1);
+        return nm;
+    }
+
+    // The same batched over initialisation pairs on HBM arrays (orbm_init_batch; nnratio / checkOri from
+    // this matcher).  Enqueue only.
+    void SearchForInitializationBatch(orbm_init_batch b, int32_t* d_matches12, int32_t* d_n_matches,
+                                      void* stream = nullptr) const {
+        b.nnratio = nnratio_;
+        b.check_orientation = checkOri_ ? 1 : 0;
+        check(orbm_search_for_initialization_device(&b, d_matches12, d_n_matches, stream),
+              "orbm_search_for_initialization_device");
+    }
+
     float nnratio() const { return nnratio_; }
     bool checkOrientation() const { return checkOri_; }
 

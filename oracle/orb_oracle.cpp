@@ -61,6 +61,7 @@
 #include <map>
 #include <sstream>
 #include <string>
+#include <limits>
 #include <vector>
 
 #include "orbslam2_amd.h"
@@ -2120,6 +2121,95 @@ int oracle_search_by_projection_motion(const orbm_motion_batch* b, int32_t* kp_m
         }
         for (int i = 0; i < nk; i++) kp_match[k0 + i] = owner[i];
         n_matches[f] = nmatches;
+    }
+    return 0;
+}
+
+// ORBmatcher::SearchForInitialization(Frame& frame1, Frame& frame2, prevMatched, matches12, windowSize)
+// (ORBmatcher.cc:614-694), literally, pair by pair: octave-0 queries in idx1 order, GetFeaturesInArea
+// over octave 0 (:629-636), the matchedDistance skip (:650-651), best / second best (:653-662), the
+// ratio test (:665), the take-over of an idx2 held by an earlier query (:667-676), CheckOrientation
+// (frame2.keypointsUn, frame1.keypointsUn, matchIds, matches12) (:682-683) with matchIds in push
+// order (stale pairs included) and the prevMatched update (:686-688).
+int oracle_search_for_initialization(const orbm_init_batch* b, int32_t* matches12_out, int32_t* n_matches) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    for (int p = 0; p < b->n_pairs; p++) {
+        const int k0 = b->kp_begin[p], n2 = b->kp_begin[p + 1] - k0;
+        const int q0 = b->q_begin[p], n1 = b->q_begin[p + 1] - q0;
+        std::unique_ptr<FeaturesGrid> g(new FeaturesGrid);
+        g->assign(b->kp_xy + 2 * (size_t)k0, b->kp_octave + k0, n2, b->bounds + 4 * (size_t)p, 8);
+        int nmatches = 0;
+        std::vector<int> matches12(n1, -1);
+        std::vector<int> matchedDistance(n2, std::numeric_limits<int>::max());
+        std::vector<int> matches21(n2, -1);
+        std::vector<std::pair<int, int>> matchIds;
+        const float radius = static_cast<float>(b->window);
+        for (int idx1 = 0; idx1 < n1; idx1++) {
+            const int level1 = b->q_octave[q0 + idx1];
+            if (level1 > 0) continue;
+            const float u = b->prev_matched[2 * (size_t)(q0 + idx1)], v = b->prev_matched[2 * (size_t)(q0 + idx1) + 1];
+            const std::vector<size_t> indices2 = g->in_area(u, v, radius, level1, level1);
+            if (indices2.empty()) continue;
+            const uint8_t* desc1 = b->q_desc + 32 * (size_t)(q0 + idx1);
+            int bestDist = std::numeric_limits<int>::max();
+            int secondBestDist = std::numeric_limits<int>::max();
+            int bestIdx2 = -1;
+            for (size_t idx2 : indices2) {
+                const int dist = hamming(desc1, b->kp_desc + 32 * (size_t)(k0 + idx2));
+                if (matchedDistance[idx2] <= dist) continue;
+                if (dist < bestDist) {
+                    secondBestDist = bestDist;
+                    bestDist = dist;
+                    bestIdx2 = (int)idx2;
+                } else if (dist < secondBestDist) {
+                    secondBestDist = dist;
+                }
+            }
+            if (bestDist <= TH_LOW && bestDist < secondBestDist * b->nnratio) {
+                if (matches21[bestIdx2] >= 0) {
+                    matches12[matches21[bestIdx2]] = -1;
+                    nmatches--;
+                }
+                matches12[idx1] = bestIdx2;
+                matches21[bestIdx2] = idx1;
+                matchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (b->check_orientation) matchIds.push_back(std::make_pair(bestIdx2, idx1));
+            }
+        }
+        if (b->check_orientation) {   // CheckOrientation(frame2.keypointsUn, frame1.keypointsUn, matchIds, matches12)
+            const float factor = 1.f / HISTO_LENGTH;
+            std::vector<int> hist[HISTO_LENGTH];
+            for (const auto& m : matchIds) {
+                float diff = b->kp_angle[k0 + m.first] - b->q_angle[q0 + m.second];
+                if (diff < 0) diff += 360;
+                int bin = cv_round(factor * diff);
+                if (bin == HISTO_LENGTH) bin = 0;
+                if (bin < 0 || bin >= HISTO_LENGTH) return -1;   // CV_Assert
+                hist[bin].push_back(m.second);
+            }
+            std::sort(std::begin(hist), std::end(hist),
+                      [](const std::vector<int>& l, const std::vector<int>& r) { return l.size() > r.size(); });
+            const size_t max1 = hist[0].size(), max2 = hist[1].size(), max3 = hist[2].size();
+            int eraseBin = 3;
+            if (max2 < 0.1 * max1) eraseBin = 1;
+            else if (max3 < 0.1 * max1) eraseBin = 2;
+            int reduction = 0;
+            for (int bin = eraseBin; bin < HISTO_LENGTH; bin++)
+                for (int i2 : hist[bin]) {
+                    matches12[i2] = -1;
+                    reduction++;
+                }
+            nmatches = (int)matchIds.size() - reduction;
+        }
+        for (int i1 = 0; i1 < n1; i1++) {
+            matches12_out[q0 + i1] = matches12[i1];
+            if (matches12[i1] >= 0) {
+                b->prev_matched[2 * (size_t)(q0 + i1)] = b->kp_xy[2 * (size_t)(k0 + matches12[i1])];
+                b->prev_matched[2 * (size_t)(q0 + i1) + 1] = b->kp_xy[2 * (size_t)(k0 + matches12[i1]) + 1];
+            }
+        }
+        n_matches[p] = nmatches;
     }
     return 0;
 }

@@ -90,6 +90,15 @@ class MotionBatch(C.Structure):
                 ("check_orientation", C.c_int32)]
 
 
+class InitBatch(C.Structure):
+    """orbm_init_batch (include/orbslam2_amd.h)."""
+    _fields_ = [("n_pairs", C.c_int32), ("total_kp", C.c_int32), ("total_q", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_desc", C.c_void_p),
+                ("kp_angle", C.c_void_p), ("bounds", C.c_void_p), ("q_begin", C.c_void_p), ("q_octave", C.c_void_p),
+                ("q_desc", C.c_void_p), ("q_angle", C.c_void_p), ("prev_matched", C.c_void_p), ("window", C.c_int32),
+                ("nnratio", C.c_float), ("check_orientation", C.c_int32)]
+
+
 class PoseBatch(C.Structure):
     _fields_ = [("n_frames", C.c_int32), ("edge_begin", C.c_void_p), ("pose_R", C.c_void_p), ("pose_t", C.c_void_p),
                 ("cam", C.c_void_p), ("xw", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
@@ -140,6 +149,8 @@ SIGNATURES = {
     "orbm_search_by_projection": (C.c_int, [C.POINTER(ProjBatch), VP, VP, C.c_int]),
     "orbm_search_by_projection_device": (C.c_int, [C.POINTER(ProjBatch), VP, VP, VP]),
     "orbm_search_by_projection_motion_device": (C.c_int, [C.POINTER(MotionBatch), VP, VP, VP]),
+    "orbm_search_for_initialization": (C.c_int, [C.POINTER(InitBatch), VP, VP, C.c_int]),
+    "orbm_search_for_initialization_device": (C.c_int, [C.POINTER(InitBatch), VP, VP, VP]),
     "orbv_load_text": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(VP)]),
     "orbv_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, VP, VP, VP, C.c_int, C.POINTER(VP)]),
     "orbv_destroy": (C.c_int, [VP]),

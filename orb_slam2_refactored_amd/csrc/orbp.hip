@@ -636,6 +636,272 @@ static int pj_common_args(const orbm_proj_batch* b, PjArgs& a) {
     return ORB_OK;
 }
 
+// ---------------------------------------------------------------- SearchForInitialization
+// ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:614-694), batched over pairs (F1, F2).
+// The reference walks the octave-0 features of F1 in idx1 order against a state over F2
+// (matchedDistance, matches21): a candidate idx2 is skipped when the distance it is held at is <=
+// its own, and an accepted query takes idx2 from its earlier holder.  Three stages:
+//   pj_grid_kernel   F2's FeaturesGrid (as above; mp_begin = q_begin gives each query its pair)
+//   pi_score_kernel  a 16-lane group per query: the octave-0 candidates of its window in
+//                    GetFeaturesInArea's scan order with their Hamming distances, up to PI_CAP
+//   pi_walk_kernel   one wavefront per pair: the queries in order, lanes over a query's candidates
+//                    against the state in LDS (matchedDistance u16, matches21 / matches12 i16),
+//                    best = min (dist, scan position), second = the second-smallest distance of the
+//                    candidates not skipped; windows with more than PI_CAP candidates are rescanned
+//                    from the grid.  Then CheckOrientation over every push (stale ones included),
+//                    the output and the prevMatched update.
+constexpr int PI_CAP = 128;
+constexpr int PI_TH_LOW = 50;    // ORBmatcher.cc:42
+constexpr int PI_INF = 0xffff;   // matchedDistance = INT_MAX on entry (:618)
+
+struct PiExtra {
+    const int32_t* q_begin;
+    const int32_t* q_oct;
+    const uint8_t* q_desc;
+    const float* q_angle;
+    const float* kp_angle;
+    float* prev;
+    float r, nnratio;
+    int check_ori, total_q;
+    int32_t* cnt;        // total_q: candidates in the query's window (0: not searched / none)
+    uint32_t* cand;      // total_q x PI_CAP: (dist << 13 | idx2) in scan order
+    int32_t* matches12;  // total_q
+};
+
+struct PiWin {
+    int mincx, maxcx, mincy, maxcy, lvl;
+    bool chk, any;
+    float u, v, r;
+};
+
+// GetFeaturesInArea(u, v, windowSize, level1, level1) (Frame.cc:102-145) of query j (octave <= 0).
+__device__ __forceinline__ PiWin pi_window(const PjArgs& a, const PiExtra& e, int f, int j) {
+    PiWin w;
+    w.lvl = e.q_oct[j];
+    w.any = w.lvl <= 0;   // :628-630: level1 > 0 continue
+    w.chk = w.lvl >= 0;   // checkLevels = minLevel > 0 || maxLevel >= 0
+    w.u = e.prev[2 * (size_t)j];
+    w.v = e.prev[2 * (size_t)j + 1];
+    w.r = e.r;
+    const float* bd = a.bounds + 4 * (size_t)f;
+    const float minx = bd[0], miny = bd[2];
+    const float invW = PJ_COLS / (bd[1] - bd[0]), invH = PJ_ROWS / (bd[3] - bd[2]);
+    w.mincx = max((int)floorf(invW * (w.u - w.r - minx)), 0);
+    w.maxcx = min((int)ceilf(invW * (w.u + w.r - minx)), PJ_COLS - 1);
+    w.mincy = max((int)floorf(invH * (w.v - w.r - miny)), 0);
+    w.maxcy = min((int)ceilf(invH * (w.v + w.r - miny)), PJ_ROWS - 1);
+    if (w.mincx >= PJ_COLS || w.maxcx < 0 || w.mincy >= PJ_ROWS || w.maxcy < 0) w.any = false;
+    return w;
+}
+
+// the level / area gates of a keypoint at sorted grid position p of frame f (-1: not a candidate)
+__device__ __forceinline__ int pi_gate(const PjArgs& a, const PiWin& w, int k0, int p) {
+    const int idx = a.grid_idx[k0 + p];
+    const int k = k0 + idx;
+    if (w.chk && a.kp_oct[k] != w.lvl) return -1;
+    const float distx = a.kp_xy[2 * (size_t)k] - w.u, disty = a.kp_xy[2 * (size_t)k + 1] - w.v;
+    return (fabsf(distx) < w.r && fabsf(disty) < w.r) ? idx : -1;
+}
+
+__global__ __launch_bounds__(256) void pi_score_kernel(PjArgs a, PiExtra e) {
+    const int j = blockIdx.x * 16 + (threadIdx.x >> 4), lane = threadIdx.x & 15;
+    if (j >= e.total_q) return;   // whole 16-lane groups
+    const int f = a.mp_frame[j];
+    const int k0 = a.kp_begin[f], n2 = a.kp_begin[f + 1] - k0;
+    int cnt = 0;
+    if (n2 <= PJ_MAXKP) {
+        const PiWin w = pi_window(a, e, f, j);
+        if (w.any) {
+            const uint8_t* d1 = e.q_desc + 32 * (size_t)j;
+            const int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
+            const int gsh = threadIdx.x & 48;   // this group's bit offset in the wave's ballot
+            for (int cx = w.mincx; cx <= w.maxcx; cx++) {
+                const int p0 = cs[cx * PJ_ROWS + w.mincy], p1 = cs[cx * PJ_ROWS + w.maxcy + 1];
+                for (int b = p0; b < p1; b += 16) {
+                    const int p = b + lane;
+                    const int idx = p < p1 ? pi_gate(a, w, k0, p) : -1;
+                    const unsigned long long bm = __ballot(idx >= 0);
+                    const uint32_t gm = (uint32_t)(bm >> gsh) & 0xffffu;
+                    if (idx >= 0) {
+                        const int pos = cnt + __popc(gm & ((1u << lane) - 1u));
+                        if (pos < PI_CAP) {
+                            const int dist = pj_hamming(d1, a.kp_desc + 32 * (size_t)(k0 + idx));
+                            e.cand[(size_t)j * PI_CAP + pos] = ((uint32_t)dist << PJ_IDX_BITS) | (uint32_t)idx;
+                        }
+                    }
+                    cnt += __popc(gm);
+                }
+            }
+        }
+    }
+    if (lane == 0) e.cnt[j] = cnt;
+}
+
+__device__ __forceinline__ unsigned long long pi_wave_min64(unsigned long long v) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, m, 64), hi = (unsigned)__shfl_xor((int)(v >> 32), m, 64);
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(64) void pi_walk_kernel(PjArgs a, PiExtra e) {
+    __shared__ uint16_t mdist[PJ_MAXKP];
+    __shared__ int16_t m21[PJ_MAXKP];
+    __shared__ int16_t m12[PJ_MAXKP];
+    __shared__ int hist[32];
+    __shared__ uint32_t keep_s;
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int k0 = a.kp_begin[f], n2 = a.kp_begin[f + 1] - k0;
+    const int q0 = e.q_begin[f], n1 = e.q_begin[f + 1] - q0;
+    if (n1 > PJ_MAXKP || n2 > PJ_MAXKP) {
+        for (int i = lane; i < n1; i += 64) e.matches12[q0 + i] = -1;
+        if (lane == 0) a.n_matches[f] = -1;
+        return;
+    }
+    for (int i = lane; i < n2; i += 64) { mdist[i] = PI_INF; m21[i] = -1; }
+    for (int i = lane; i < n1; i += 64) m12[i] = -1;
+    if (lane < 32) hist[lane] = 0;
+    __syncthreads();
+    const int32_t* cs = a.grid_start + (size_t)f * (PJ_CELLS + 1);
+    int nm = 0;
+    for (int c = 0; c < n1; c += 64) {
+        const int cnt_l = c + lane < n1 ? e.cnt[q0 + c + lane] : 0;
+        unsigned long long todo = __ballot(cnt_l > 0);
+        while (todo) {
+            const int t = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int qi = c + t, j = q0 + qi;
+            const int cnt = __shfl(cnt_l, t, 64);
+            unsigned long long bkey = ~0ull;   // (dist << 32) | (scan position << 13) | idx2
+            int d1 = PI_INF, d2 = PI_INF;      // the lane's two smallest distances not skipped
+            auto consider = [&](int dist, int idx2, int pos) {
+                if ((int)mdist[idx2] <= dist) return;   // matchedDistance[idx2] <= dist (:650-651)
+                const unsigned long long key = ((unsigned long long)dist << 32) | ((unsigned)pos << PJ_IDX_BITS) | (unsigned)idx2;
+                bkey = key < bkey ? key : bkey;
+                if (dist < d1) { d2 = d1; d1 = dist; } else if (dist < d2) d2 = dist;
+            };
+            if (cnt <= PI_CAP) {
+                for (int k = lane; k < cnt; k += 64) {
+                    const uint32_t key = e.cand[(size_t)j * PI_CAP + k];
+                    consider((int)(key >> PJ_IDX_BITS), (int)(key & PJ_IDX_MASK), k);
+                }
+            } else {   // a window with more than PI_CAP candidates: rescan it from the grid
+                const PiWin w = pi_window(a, e, f, j);
+                const uint8_t* d1p = e.q_desc + 32 * (size_t)j;
+                for (int cx = w.mincx; cx <= w.maxcx; cx++) {
+                    const int p0 = cs[cx * PJ_ROWS + w.mincy], p1 = cs[cx * PJ_ROWS + w.maxcy + 1];
+                    for (int p = p0 + lane; p < p1; p += 64) {
+                        const int idx = pi_gate(a, w, k0, p);
+                        if (idx >= 0) consider(pj_hamming(d1p, a.kp_desc + 32 * (size_t)(k0 + idx)), idx, p);
+                    }
+                }
+            }
+            bkey = pi_wave_min64(bkey);
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) {   // merge the lanes' two smallest: second order statistic
+                const int o1 = __shfl_xor(d1, m, 64), o2 = __shfl_xor(d2, m, 64);
+                d2 = min(max(d1, o1), min(d2, o2));
+                d1 = min(d1, o1);
+            }
+            if (bkey == ~0ull) continue;
+            const int best = (int)(bkey >> 32), b = (int)(bkey & PJ_IDX_MASK);
+            // bestDist < secondBestDist * fNNRatio_ in float, INT_MAX when there is no second (:665)
+            const float second = d2 >= PI_INF ? 2147483648.0f : (float)d2;
+            if (best <= PI_TH_LOW && (float)best < second * e.nnratio) {
+                if (lane == 0) {
+                    const int old = m21[b];
+                    if (old >= 0) { m12[old] = -1; nm--; }   // :667-671
+                    m12[qi] = (int16_t)b;
+                    m21[b] = (int16_t)qi;
+                    mdist[b] = (uint16_t)best;
+                    nm++;
+                    if (e.check_ori) hist[pjm_bin(e.kp_angle[k0 + b], e.q_angle[j])]++;
+                }
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
+    }
+    __syncthreads();
+    if (e.check_ori) {   // CheckOrientation(frame2.keypointsUn, frame1.keypointsUn, matchIds, matches12)
+        if (lane == 0) {
+            QtItem it[30];
+            for (int bb = 0; bb < 30; bb++) it[bb] = QtItem{hist[bb], bb};
+            qt_sort(it, it + 30);
+            const double max1 = it[0].size, max2 = it[1].size, max3 = it[2].size;
+            const int eraseBin = max2 < 0.1 * max1 ? 1 : (max3 < 0.1 * max1 ? 2 : 3);
+            uint32_t k = 0;
+            int kept = 0;
+            for (int r = 0; r < eraseBin; r++) {
+                k |= 1u << it[r].node;
+                kept += it[r].size;
+            }
+            keep_s = k;
+            nm = kept;   // matchIds.size() - reduction
+        }
+        __syncthreads();
+        const uint32_t k = keep_s;
+        for (int i = lane; i < n1; i += 64) {
+            const int m = m12[i];
+            if (m >= 0 && !((k >> pjm_bin(e.kp_angle[k0 + m], e.q_angle[q0 + i])) & 1u)) m12[i] = -1;
+        }
+        __syncthreads();
+    }
+    for (int i = lane; i < n1; i += 64) {   // output and the prevMatched update (:686-688)
+        const int m = m12[i];
+        e.matches12[q0 + i] = m;
+        if (m >= 0) {
+            e.prev[2 * (size_t)(q0 + i)] = a.kp_xy[2 * (size_t)(k0 + m)];
+            e.prev[2 * (size_t)(q0 + i) + 1] = a.kp_xy[2 * (size_t)(k0 + m) + 1];
+        }
+    }
+    if (lane == 0) a.n_matches[f] = nm;
+}
+
+static int launch_init(PjArgs& a, PiExtra& e, hipStream_t st) {
+    hipLaunchKernelGGL(pj_grid_kernel, dim3(a.n_frames), dim3(256), 0, st, a);
+    ORB_HIP_TRY(hipGetLastError());
+    if (e.total_q > 0) {
+        hipLaunchKernelGGL(pi_score_kernel, dim3((e.total_q + 15) / 16), dim3(256), 0, st, a, e);
+        ORB_HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(pi_walk_kernel, dim3(a.n_frames), dim3(64), 0, st, a, e);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
+static size_t pi_workspace_bytes(int n_pairs, int total_kp, int total_q) {
+    return pj_workspace_bytes(n_pairs, total_kp, total_q) + align_up((size_t)std::max(total_q, 1) * 4, 256) +
+           align_up((size_t)std::max(total_q, 1) * PI_CAP * 4, 256);
+}
+
+static void pi_carve(PjArgs& a, PiExtra& e, char* ws, int n_pairs, int total_kp, int total_q) {
+    pj_carve(a, ws, n_pairs, total_kp, total_q);
+    size_t o = pj_workspace_bytes(n_pairs, total_kp, total_q);
+    e.cnt = (int32_t*)(ws + o);
+    o += align_up((size_t)std::max(total_q, 1) * 4, 256);
+    e.cand = (uint32_t*)(ws + o);
+}
+
+static int pi_common(const orbm_init_batch* b, PjArgs& a, PiExtra& e) {
+    ORB_CHECK_ARG(b, "null argument");
+    ORB_CHECK_ARG(b->n_pairs >= 0 && b->total_kp >= 0 && b->total_q >= 0, "negative sizes");
+    ORB_CHECK_ARG(b->window >= 0, "negative windowSize");
+    std::memset(&a, 0, sizeof(a));
+    std::memset(&e, 0, sizeof(e));
+    a.n_frames = b->n_pairs;
+    a.n_levels = 8;
+    a.total_mp = b->total_q;
+    e.r = (float)b->window;   // static_cast<float>(windowSize) (:622)
+    e.nnratio = b->nnratio;
+    e.check_ori = b->check_orientation ? 1 : 0;
+    e.total_q = b->total_q;
+    return ORB_OK;
+}
+
 }  // namespace orbamd
 
 using namespace orbamd;
@@ -787,5 +1053,106 @@ extern "C" int orbm_search_by_projection_motion_device(const orbm_motion_batch* 
         hipLaunchKernelGGL(pjm_orient_kernel, dim3(a.n_frames), dim3(256), 0, st, a, e);
         ORB_HIP_TRY(hipGetLastError());
     }
+    return ORB_OK;
+}
+
+
+extern "C" int orbm_search_for_initialization_device(const orbm_init_batch* b, int32_t* matches12, int32_t* n_matches,
+                                                     void* stream) {
+    PjArgs a;
+    PiExtra e;
+    int rc;
+    if ((rc = pi_common(b, a, e))) return rc;
+    if (b->n_pairs == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kp_begin && b->q_begin && b->bounds && b->prev_matched && matches12 && n_matches, "null array");
+    ORB_CHECK_ARG(b->total_kp == 0 || (b->kp_xy && b->kp_octave && b->kp_desc), "null F2 keypoint array");
+    ORB_CHECK_ARG(b->total_q == 0 || (b->q_octave && b->q_desc), "null F1 keypoint array");
+    ORB_CHECK_ARG(!b->check_orientation || ((b->total_kp == 0 || b->kp_angle) && (b->total_q == 0 || b->q_angle)),
+                  "CheckOrientation needs kp_angle / q_angle");
+    a.kp_begin = b->kp_begin; a.kp_xy = b->kp_xy; a.kp_oct = b->kp_octave; a.kp_desc = b->kp_desc;
+    a.bounds = b->bounds; a.mp_begin = b->q_begin; a.n_matches = n_matches;
+    e.q_begin = b->q_begin; e.q_oct = b->q_octave; e.q_desc = b->q_desc; e.q_angle = b->q_angle;
+    e.kp_angle = b->kp_angle; e.prev = b->prev_matched; e.matches12 = matches12;
+    int dev = 0;
+    ORB_HIP_TRY(hipGetDevice(&dev));
+    if (g_pj.device != dev) {
+        g_pj.ws.release();
+        g_pj.io.release();
+        g_pj.device = dev;
+    }
+    if ((rc = g_pj.ws.reserve(pi_workspace_bytes(b->n_pairs, b->total_kp, b->total_q)))) return rc;
+    pi_carve(a, e, g_pj.ws.as<char>(), b->n_pairs, b->total_kp, b->total_q);
+    return launch_init(a, e, (hipStream_t)stream);
+}
+
+extern "C" int orbm_search_for_initialization(const orbm_init_batch* b, int32_t* matches12, int32_t* n_matches,
+                                              int device) {
+    PjArgs a;
+    PiExtra e;
+    int rc;
+    if ((rc = pi_common(b, a, e))) return rc;
+    const int P = b->n_pairs;
+    if (P == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kp_begin && b->q_begin && b->bounds && b->prev_matched && matches12 && n_matches, "null array");
+    ORB_CHECK_ARG(b->kp_begin[0] == 0 && b->q_begin[0] == 0 && b->kp_begin[P] == b->total_kp &&
+                      b->q_begin[P] == b->total_q,
+                  "kp_begin / q_begin must start at 0 and end at total_kp / total_q");
+    for (int p = 0; p < P; p++) {
+        ORB_CHECK_ARG(b->kp_begin[p + 1] >= b->kp_begin[p] && b->q_begin[p + 1] >= b->q_begin[p],
+                      "offsets must be non-decreasing");
+        ORB_CHECK_ARG(b->kp_begin[p + 1] - b->kp_begin[p] <= PJ_MAXKP && b->q_begin[p + 1] - b->q_begin[p] <= PJ_MAXKP,
+                      "frame has more than ORBM_PROJ_MAX_KP keypoints");
+    }
+    const int K = b->total_kp, Q = b->total_q;
+    ORB_CHECK_ARG(K == 0 || (b->kp_xy && b->kp_octave && b->kp_desc), "null F2 keypoint array");
+    ORB_CHECK_ARG(Q == 0 || (b->q_octave && b->q_desc), "null F1 keypoint array");
+    ORB_CHECK_ARG(!b->check_orientation || ((K == 0 || b->kp_angle) && (Q == 0 || b->q_angle)),
+                  "CheckOrientation needs kp_angle / q_angle");
+    if (b->check_orientation) {
+        for (int k = 0; k < K; k++)
+            ORB_CHECK_ARG(b->kp_angle[k] >= 0.f && b->kp_angle[k] < 360.f, "keypoint angle outside [0, 360) (CV_Assert in CheckOrientation)");
+        for (int q = 0; q < Q; q++)
+            ORB_CHECK_ARG(b->q_angle[q] >= 0.f && b->q_angle[q] < 360.f, "keypoint angle outside [0, 360) (CV_Assert in CheckOrientation)");
+    }
+    ORB_HIP_TRY(hipSetDevice(device));
+    if (g_pj.device != device) {
+        g_pj.ws.release();
+        g_pj.io.release();
+        g_pj.device = device;
+    }
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += align_up(std::max<size_t>(bytes, 1), 256); return o; };
+    const size_t o_kb = take((size_t)(P + 1) * 4), o_xy = take((size_t)K * 8), o_oc = take((size_t)K * 4),
+                 o_kd = take((size_t)K * 32), o_ka = take((size_t)K * 4), o_bd = take((size_t)P * 16),
+                 o_qb = take((size_t)(P + 1) * 4), o_qo = take((size_t)Q * 4), o_qd = take((size_t)Q * 32),
+                 o_qa = take((size_t)Q * 4), o_pm = take((size_t)Q * 8), o_m12 = take((size_t)Q * 4),
+                 o_nm = take((size_t)P * 4);
+    if ((rc = g_pj.io.reserve(off))) return rc;
+    if ((rc = g_pj.ws.reserve(pi_workspace_bytes(P, K, Q)))) return rc;
+    char* d = g_pj.io.as<char>();
+    auto up = [&](size_t o, const void* src, size_t bytes) -> int {
+        if (bytes && src) ORB_HIP_TRY(hipMemcpy(d + o, src, bytes, hipMemcpyHostToDevice));
+        return ORB_OK;
+    };
+    if ((rc = up(o_kb, b->kp_begin, (size_t)(P + 1) * 4)) || (rc = up(o_xy, b->kp_xy, (size_t)K * 8)) ||
+        (rc = up(o_oc, b->kp_octave, (size_t)K * 4)) || (rc = up(o_kd, b->kp_desc, (size_t)K * 32)) ||
+        (rc = up(o_ka, b->kp_angle, (size_t)K * 4)) || (rc = up(o_bd, b->bounds, (size_t)P * 16)) ||
+        (rc = up(o_qb, b->q_begin, (size_t)(P + 1) * 4)) || (rc = up(o_qo, b->q_octave, (size_t)Q * 4)) ||
+        (rc = up(o_qd, b->q_desc, (size_t)Q * 32)) || (rc = up(o_qa, b->q_angle, (size_t)Q * 4)) ||
+        (rc = up(o_pm, b->prev_matched, (size_t)Q * 8)))
+        return rc;
+    a.kp_begin = (const int32_t*)(d + o_kb); a.kp_xy = (const float*)(d + o_xy); a.kp_oct = (const int32_t*)(d + o_oc);
+    a.kp_desc = (const uint8_t*)(d + o_kd); a.bounds = (const float*)(d + o_bd); a.mp_begin = (const int32_t*)(d + o_qb);
+    a.n_matches = (int32_t*)(d + o_nm);
+    e.q_begin = (const int32_t*)(d + o_qb); e.q_oct = (const int32_t*)(d + o_qo); e.q_desc = (const uint8_t*)(d + o_qd);
+    e.q_angle = (const float*)(d + o_qa); e.kp_angle = (const float*)(d + o_ka); e.prev = (float*)(d + o_pm);
+    e.matches12 = (int32_t*)(d + o_m12);
+    pi_carve(a, e, g_pj.ws.as<char>(), P, K, Q);
+    if ((rc = launch_init(a, e, nullptr))) return rc;
+    if (Q) {
+        ORB_HIP_TRY(hipMemcpy(matches12, d + o_m12, (size_t)Q * 4, hipMemcpyDeviceToHost));
+        ORB_HIP_TRY(hipMemcpy(b->prev_matched, d + o_pm, (size_t)Q * 8, hipMemcpyDeviceToHost));
+    }
+    ORB_HIP_TRY(hipMemcpy(n_matches, d + o_nm, (size_t)P * 4, hipMemcpyDeviceToHost));
     return ORB_OK;
 }

@@ -403,3 +403,58 @@ def search_by_projection_motion_device(batch: dict, kp_match=None, n_matches=Non
                                                         stream_ptr(stream)),
           "orbm_search_by_projection_motion_device")
     return kp_match, n_matches
+
+
+_INIT_KEYS = (("kp_begin", np.int32), ("kp_xy", np.float32), ("kp_octave", np.int32), ("kp_desc", np.uint8),
+              ("kp_angle", np.float32), ("bounds", np.float32), ("q_begin", np.int32), ("q_octave", np.int32),
+              ("q_desc", np.uint8), ("q_angle", np.float32), ("prev_matched", np.float32))
+
+
+def SearchForInitialization(batch: dict, device: int = 0):
+    """ORBmatcher::SearchForInitialization(F1, F2, prevMatched, matches12, windowSize)
+    (src/ORBmatcher.cc:614-694) batched over pairs, host arrays (orbm_init_batch fields: F2 keypoints
+    kp_* with kp_begin, F1 keypoints q_* with q_begin, prev_matched [total_q, 2] float32 updated in
+    place, window, nnratio, check_orientation).  Returns (matches12 [total_q] = F2-relative idx2 or
+    -1, n_matches [P])."""
+    from ._lib import InitBatch
+    arrs = {k: np.ascontiguousarray(batch[k], dt) for k, dt in _INIT_KEYS if batch.get(k) is not None}
+    if arrs["prev_matched"] is not batch["prev_matched"]:
+        raise ValueError("prev_matched must be a contiguous float32 array (updated in place)")
+    P = len(arrs["kp_begin"]) - 1
+    K, Q = int(arrs["kp_begin"][-1]), int(arrs["q_begin"][-1])
+    m12 = np.empty(max(Q, 1), np.int32)
+    nm = np.empty(max(P, 1), np.int32)
+    ib = InitBatch(P, K, Q, *[ptr(arrs[k]) if k in arrs else None for k, _ in _INIT_KEYS], int(batch["window"]),
+                   float(batch["nnratio"]), int(bool(batch["check_orientation"])))
+    check(lib().orbm_search_for_initialization(C.byref(ib), ptr(m12), ptr(nm), int(device)),
+          "orbm_search_for_initialization")
+    return m12[:Q], nm[:P]
+
+
+def search_for_initialization_device(batch: dict, matches12=None, n_matches=None, stream=None):
+    """Device form of SearchForInitialization: `batch` holds GPU tensors for the orbm_init_batch arrays
+    (prev_matched float32 [total_q, 2] is updated in place) and host values for window, nnratio and
+    check_orientation.  Returns (matches12 [total_q], n_matches [P]); n_matches[p] = -1 when a frame of
+    the pair has more than ORBM_PROJ_MAX_KP keypoints."""
+    import torch
+    from ._lib import InitBatch
+    kb, qb = batch["kp_begin"], batch["q_begin"]
+    P = kb.numel() - 1
+    if qb.numel() != P + 1:
+        raise ValueError("kp_begin and q_begin must both have n_pairs + 1 entries")
+    for k, dt in _INIT_KEYS:
+        t = batch.get(k)
+        if t is not None and (not t.is_contiguous() or t.dtype != getattr(torch, np.dtype(dt).name)):
+            raise ValueError(f"{k} must be a contiguous {np.dtype(dt).name} tensor")
+    K, Q = int(batch["kp_xy"].shape[0]), int(batch["q_octave"].shape[0])
+    if batch["prev_matched"].shape[0] != Q:
+        raise ValueError("prev_matched must be [total_q, 2]")
+    if matches12 is None:
+        matches12 = torch.empty(max(Q, 1), dtype=torch.int32, device=kb.device)
+    if n_matches is None:
+        n_matches = torch.empty(max(P, 1), dtype=torch.int32, device=kb.device)
+    ib = InitBatch(P, K, Q, *[tptr(batch[k]) if batch.get(k) is not None else None for k, _ in _INIT_KEYS],
+                   int(batch["window"]), float(batch["nnratio"]), int(bool(batch["check_orientation"])))
+    check(lib().orbm_search_for_initialization_device(C.byref(ib), tptr(matches12), tptr(n_matches), stream_ptr(stream)),
+          "orbm_search_for_initialization_device")
+    return matches12, n_matches

@@ -470,3 +470,93 @@ def make_full_vocabulary(seed: int = 0, k: int = 10, L: int = 6):
     weight = np.zeros(n)
     weight[n - k ** L:] = rng.uniform(0.5, 8.0, k ** L)
     return dict(k=k, L=L, scoring=0, weighting=0, parent=parent, is_leaf=is_leaf, desc=desc, weight=weight)
+
+
+def make_init_batch(seed: int = 0, n_pairs: int = 4, n1=4000, n2=4000, width: float = 1280.0, height: float = 720.0,
+                    window: int = 100, nnratio: float = 0.9, check_orientation: bool = True, dup_frac: float = 0.25,
+                    twin_frac: float = 0.15, dense: bool = False):
+    """SearchForInitialization inputs (orbm_init_batch, host arrays) shaped like
+    Tracking::MonocularInitialization (Tracking.cc:1050-1052: the initial extractor's 2x features,
+    windowSize 100, ORBmatcher(0.9f, true)).
+
+    F1 (initial frame): n1 keypoints over the image, octaves by the 2000-feature quotas, random
+    descriptors, angles around a dominant value.  F2 (current frame): for 70 % of F1's keypoints a
+    displaced copy (a common image motion + noise, 0-40 flipped bits, the same octave 75 % of the
+    time), the rest random; a fraction `dup_frac` of F2's copies duplicate an F1 keypoint that already
+    has one (several queries competing for one idx2, so later, closer queries take it from earlier
+    ones), some with an exact descriptor copy (distance ties); `twin_frac` of F1's keypoints sit next
+    to an earlier one with a similar descriptor (the later query takes the feature when it is closer).
+    prevMatched = F1's positions.
+    `dense`: a cluster of 300 octave-0 keypoints in a 150-px box puts more than PI_CAP candidates in
+    the windows around it.  n1 / n2: int or per-pair list."""
+    rng = np.random.default_rng(seed)
+    n1s = [int(n1)] * n_pairs if np.isscalar(n1) else [int(v) for v in n1]
+    n2s = [int(n2)] * n_pairs if np.isscalar(n2) else [int(v) for v in n2]
+    q = np.array(ORB_QUOTA_2000, float)
+    q /= q.sum()
+    F = dict(kp_xy=[], kp_octave=[], kp_desc=[], kp_angle=[], bounds=[], q_octave=[], q_desc=[], q_angle=[],
+             prev_matched=[])
+
+    def flip(d, nbits):
+        d = d.copy()
+        for bit in rng.choice(256, size=nbits, replace=False):
+            d[bit >> 3] ^= np.uint8(1 << (bit & 7))
+        return d
+
+    for p in range(n_pairs):
+        a, b = n1s[p], n2s[p]
+        x1 = rng.uniform(0, width, a)
+        y1 = rng.uniform(0, height, a)
+        o1 = rng.choice(8, size=a, p=q)
+        if dense and a > 300:
+            cx, cy = rng.uniform(200, width - 200), rng.uniform(200, height - 200)
+            x1[:300] = cx + rng.uniform(-75, 75, 300)
+            y1[:300] = cy + rng.uniform(-75, 75, 300)
+            o1[:300] = 0
+        d1 = rng.integers(0, 256, size=(a, 32), dtype=np.uint8)
+        for i in range(1, a):   # twins: a later query near an earlier one with a similar descriptor
+            if rng.random() < twin_frac:
+                j = int(rng.integers(0, i))
+                x1[i], y1[i], o1[i] = x1[j] + rng.normal(0, 2), y1[j] + rng.normal(0, 2), o1[j]
+                d1[i] = flip(d1[j], int(rng.integers(0, 31)))
+        rot = rng.uniform(0, 360)
+        a1 = (rot + rng.normal(0, 20, a)) % 360
+        mot = rng.normal(0, 15, 2)
+        x2 = rng.uniform(0, width, b)
+        y2 = rng.uniform(0, height, b)
+        o2 = rng.choice(8, size=b, p=q)
+        d2 = rng.integers(0, 256, size=(b, 32), dtype=np.uint8)
+        a2 = rng.uniform(0, 360, b)
+        used = []
+        for k in range(b):
+            if a == 0 or rng.random() >= 0.7:
+                continue
+            i = int(rng.choice(used)) if used and rng.random() < dup_frac else int(rng.integers(0, a))
+            used.append(i)
+            x2[k] = x1[i] + mot[0] + rng.normal(0, 3)
+            y2[k] = y1[i] + mot[1] + rng.normal(0, 3)
+            o2[k] = o1[i] if rng.random() < 0.75 else int(rng.integers(0, 8))
+            d2[k] = flip(d1[i], int(rng.integers(0, 41)))
+            if rng.random() < 0.08:
+                d2[k] = d1[i].copy() if rng.random() < 0.5 else d2[int(rng.integers(0, b))].copy()
+            a2[k] = (a1[i] + 25 + rng.normal(0, 8)) % 360
+        F["kp_xy"].append(np.stack([x2, y2], 1).astype(np.float32))
+        F["kp_octave"].append(o2.astype(np.int32))
+        F["kp_desc"].append(d2)
+        F["kp_angle"].append(np.clip(a2, 0, np.nextafter(np.float32(360), np.float32(0))).astype(np.float32))
+        F["bounds"].append(np.array([0.0, width, 0.0, height], np.float32))
+        F["q_octave"].append(o1.astype(np.int32))
+        F["q_desc"].append(d1)
+        F["q_angle"].append(np.clip(a1, 0, np.nextafter(np.float32(360), np.float32(0))).astype(np.float32))
+        F["prev_matched"].append(np.stack([x1, y1], 1).astype(np.float32))
+    shapes = dict(kp_xy=((0, 2), np.float32), kp_octave=((0,), np.int32), kp_desc=((0, 32), np.uint8),
+                  kp_angle=((0,), np.float32), bounds=((0, 4), np.float32), q_octave=((0,), np.int32),
+                  q_desc=((0, 32), np.uint8), q_angle=((0,), np.float32), prev_matched=((0, 2), np.float32))
+    out = {}
+    for k, (shape, dt) in shapes.items():
+        v = F[k] if k != "bounds" else [x[None] for x in F[k]]
+        out[k] = np.ascontiguousarray(np.concatenate(v).astype(dt) if v else np.zeros(shape, dt))
+    out["kp_begin"] = np.concatenate([[0], np.cumsum(n2s)]).astype(np.int32)
+    out["q_begin"] = np.concatenate([[0], np.cumsum(n1s)]).astype(np.int32)
+    out.update(window=int(window), nnratio=float(nnratio), check_orientation=bool(check_orientation))
+    return out

@@ -437,3 +437,32 @@ class Vocabulary:
                                    ptr(fo), ptr(fi), ptr(nn))
         a, b = int(nw[0]), int(nn[0])
         return (bw[:a], bv[:a]), (fn[:b], fo[:b + 1], fi[:fo[b]])
+
+
+class InitBatch(C.Structure):
+    _fields_ = [("n_pairs", C.c_int32), ("total_kp", C.c_int32), ("total_q", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_desc", C.c_void_p),
+                ("kp_angle", C.c_void_p), ("bounds", C.c_void_p), ("q_begin", C.c_void_p), ("q_octave", C.c_void_p),
+                ("q_desc", C.c_void_p), ("q_angle", C.c_void_p), ("prev_matched", C.c_void_p), ("window", C.c_int32),
+                ("nnratio", C.c_float), ("check_orientation", C.c_int32)]
+
+
+_INIT_KEYS = [("kp_begin", np.int32), ("kp_xy", np.float32), ("kp_octave", np.int32), ("kp_desc", np.uint8),
+              ("kp_angle", np.float32), ("bounds", np.float32), ("q_begin", np.int32), ("q_octave", np.int32),
+              ("q_desc", np.uint8), ("q_angle", np.float32)]
+
+
+def search_for_initialization(b):
+    """ORBmatcher::SearchForInitialization per pair (ORBmatcher.cc:614-694).  b: dict of numpy arrays
+    (orbm_init_batch fields).  Returns (matches12, n_matches, prev_matched after the call); b is not
+    modified."""
+    keep = _Keep()
+    P = len(b["kp_begin"]) - 1
+    prev = np.ascontiguousarray(b["prev_matched"], np.float32).copy()
+    ptrs = [keep(b[k], dt) for k, dt in _INIT_KEYS]
+    ib = InitBatch(P, int(b["kp_begin"][-1]), int(b["q_begin"][-1]), *ptrs, ptr(prev), int(b["window"]),
+                   float(b["nnratio"]), int(bool(b["check_orientation"])))
+    m12 = np.zeros(max(ib.total_q, 1), np.int32)
+    n = np.zeros(max(P, 1), np.int32)
+    assert lib().oracle_search_for_initialization(C.byref(ib), ptr(m12), ptr(n)) == 0
+    return m12[:ib.total_q], n[:P], prev
