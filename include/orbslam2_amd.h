@@ -384,6 +384,54 @@ typedef struct orbm_motion_batch {
 int orbm_search_by_projection_motion_device(const orbm_motion_batch* b, int32_t* kp_match, int32_t* n_matches,
                                             void* stream);
 
+/* int ORBmatcher::SearchByProjection(Frame& frame, KeyFrame* keyframe, const std::set<MapPoint*>& alreadyFound,
+ * float th, int ORBdist) (include/ORBmatcher.h:66, src/ORBmatcher.cc:1364-1445; Tracking::Relocalization
+ * calls it with th 10 / ORBdist 100, then th 3 / ORBdist 64, Tracking.cc:403,417), batched over
+ * (frame, candidate keyframe) pairs.  Frame f: keypoints [kp_begin[f], kp_begin[f+1]) as in
+ * orbm_motion_batch (no uright: the search has no stereo gate), kp_claimed = frame.mappoints[i] != NULL
+ * on entry (every non-null entry blocks, :1413-1414), its pose Rcw / tcw and intrinsics.  Keyframe
+ * points [mp_begin[f], mp_begin[f+1]) = GetMapPointMatches() in idx1 order: mp_valid = mappoint &&
+ * !isBad() && !alreadyFound.count(mappoint), mp_xw = GetWorldPos(), mp_max_min = (maxDistance_,
+ * minDistance_) (MapPoint.cc:369-377), mp_angle = keyframe->keypointsUn[idx1].angle.  On the device:
+ * the projection and imageBounds.Contains (:1385-1391), the distance-invariance gate with 0.8f /
+ * 1.2f (:1393-1401, MapPoint.cc:382-392), PredictScale (MapPoint.cc:405-415: ceil(log(ratio) /
+ * logScaleFactor), log taken as ::log(double)), the window th * scaleFactors[predictedScale] over
+ * levels predictedScale +- 1, the first-best distance over the keypoints not yet holding a map point,
+ * bestDist <= ORBdist (< 256), the claim, then CheckOrientation(keyframe->keypointsUn,
+ * frame.keypointsUn, ...) (:1439-1440).  kp_match[k] = idx1 assigned to frame keypoint k (-1: none or
+ * erased), n_matches[f] = the return value (-1 when the frame has more than ORBM_PROJ_MAX_KP
+ * keypoints). */
+typedef struct orbm_reloc_batch {
+    int32_t        n_frames, total_kp, total_mp;
+    const int32_t* kp_begin;
+    const float*   kp_xy;        /* frame keypointsUn pt */
+    const int32_t* kp_octave;
+    const uint8_t* kp_desc;
+    const float*   kp_angle;
+    const uint8_t* kp_claimed;   /* frame.mappoints[i] != NULL on entry (NULL: none) */
+    const float*   bounds;       /* n_frames x 4: imageBounds minx, maxx, miny, maxy */
+    const float*   pose;         /* n_frames x 12: Rcw (row-major 3x3) then tcw */
+    const float*   camera;       /* n_frames x 4: fx, fy, cx, cy */
+    const int32_t* mp_begin;
+    const uint8_t* mp_valid;
+    const float*   mp_xw;        /* total_mp x 3 */
+    const float*   mp_max_min;   /* total_mp x 2: maxDistance_, minDistance_ */
+    const uint8_t* mp_desc;
+    const float*   mp_angle;
+    int32_t        n_levels;
+    const float*   scale_factors;/* host, n_levels */
+    float          log_scale_factor; /* pyramid.logScaleFactor */
+    float          th;
+    int32_t        orb_dist;     /* ORBdist, 0 .. 255 */
+    int32_t        check_orientation;
+} orbm_reloc_batch;
+
+/* Host entry: every pointer host memory, synchronous. */
+int orbm_search_by_projection_reloc(const orbm_reloc_batch* b, int32_t* kp_match, int32_t* n_matches, int device);
+/* Device entry: every array in HBM except scale_factors; enqueue only on `stream`. */
+int orbm_search_by_projection_reloc_device(const orbm_reloc_batch* b, int32_t* kp_match, int32_t* n_matches,
+                                           void* stream);
+
 /* int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
  * std::vector<int>& vnMatches12, int windowSize) (include/ORBmatcher.h:81, src/ORBmatcher.cc:614-694;
  * Tracking::MonocularInitialization, Tracking.cc:1052), batched over initialisation pairs.

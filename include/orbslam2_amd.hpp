@@ -373,6 +373,27 @@ inline void SearchByProjectionMotionBatch(const orbm_motion_batch& b, int32_t* d
           "orbm_search_by_projection_motion_device");
 }
 
+// int ORBmatcher::SearchByProjection(Frame& frame, KeyFrame* keyframe, const std::set<MapPoint*>& alreadyFound,
+// float th, int ORBdist) (include/ORBmatcher.h:66, src/ORBmatcher.cc:1364-1445), batched over (frame,
+// candidate keyframe) pairs on HBM arrays (orbm_reloc_batch: the caller marks mp_valid = mappoint &&
+// !isBad() && !alreadyFound.count(mappoint) and kp_claimed = frame.mappoints[i] != nullptr).  Enqueue
+// only; kp_match[k] = keyframe idx1 assigned to frame keypoint k (frame.mappoints[k] =
+// keyframe->GetMapPointMatches()[idx1]) or -1.
+inline void SearchByProjectionRelocBatch(const orbm_reloc_batch& b, int32_t* d_kp_match, int32_t* d_n_matches,
+                                         void* stream = nullptr) {
+    check(orbm_search_by_projection_reloc_device(&b, d_kp_match, d_n_matches, stream),
+          "orbm_search_by_projection_reloc_device");
+}
+// The same for one (frame, keyframe) pair on host arrays.
+inline int SearchByProjectionReloc(const orbm_reloc_batch& b, std::vector<int32_t>& kpMatch, int device = 0) {
+    if (b.n_frames != 1) throw std::invalid_argument("SearchByProjectionReloc: one frame per call (use the batch form)");
+    kpMatch.assign(std::max(b.total_kp, 1), -1);
+    int32_t nm = 0;
+    check(orbm_search_by_projection_reloc(&b, kpMatch.data(), &nm, device), "orbm_search_by_projection_reloc");
+    kpMatch.resize(b.total_kp);
+    return nm;
+}
+
 // DBoW2 ORBVocabulary: loadFromTextFile + transform(features, BowVector&, FeatureVector&, levelsup)
 // (TemplatedVocabulary.h:1130-1196, :1341-1431) with the reference's container types.
 class ORBVocabulary {

@@ -2125,6 +2125,113 @@ int oracle_search_by_projection_motion(const orbm_motion_batch* b, int32_t* kp_m
     return 0;
 }
 
+// ORBmatcher::SearchByProjection(Frame& frame, KeyFrame* keyframe, alreadyFound, th, ORBdist)
+// (ORBmatcher.cc:1364-1445), literally, frame by frame: CameraProjection::WorldToImage
+// (CameraProjection.h:44-60, cv::Matx float products s = 0; s += a(i,k) * b(k)), ImageBounds::Contains
+// (Frame.cc:51-54), Ow = CameraPose::Invt() (CameraPose.h:45), dist3D = (float)cv::norm(PO) (double sum
+// of squares), Get{Min,Max}DistanceInvariance (MapPoint.cc:382-392), PredictScale (MapPoint.cc:405-415)
+// with log taken as ::log(double) (the float overload is not in scope there, as for cos / sin in
+// ComputeOrbDescriptor), the window over predictedScale +- 1, the skip of every keypoint holding a map
+// point, bestDist <= ORBdist, then CheckOrientation(keyframe->keypointsUn, frame.keypointsUn, ...).
+int oracle_search_by_projection_reloc(const orbm_reloc_batch* b, int32_t* kp_match, int32_t* n_matches) {
+    const int HISTO_LENGTH = 30;
+    for (int f = 0; f < b->n_frames; f++) {
+        const int k0 = b->kp_begin[f], nk = b->kp_begin[f + 1] - k0;
+        const int m0 = b->mp_begin[f], nm = b->mp_begin[f + 1] - m0;
+        std::unique_ptr<FeaturesGrid> g(new FeaturesGrid);
+        g->assign(b->kp_xy + 2 * (size_t)k0, b->kp_octave + k0, nk, b->bounds + 4 * (size_t)f, b->n_levels);
+        std::vector<uint8_t> holds(nk, 0);   // frame.mappoints[i] != NULL
+        if (b->kp_claimed) for (int i = 0; i < nk; i++) holds[i] = b->kp_claimed[k0 + i];
+        std::vector<int> owner(nk, -1);
+        const float* R = b->pose + 12 * (size_t)f;
+        const float* t = R + 9;
+        const float* K = b->camera + 4 * (size_t)f;
+        const float* bd = b->bounds + 4 * (size_t)f;
+        float Ow[3];
+        for (int i = 0; i < 3; i++) {   // -R^T * t: (-R^T)(i, k) = -R(k, i)
+            float sacc = 0;
+            for (int k = 0; k < 3; k++) sacc += (-R[3 * k + i]) * t[k];
+            Ow[i] = sacc;
+        }
+        int nmatches = 0;
+        std::vector<std::pair<int, int>> matchIds;
+        for (int idx1 = 0; idx1 < nm; idx1++) {
+            const int mj = m0 + idx1;
+            if (!b->mp_valid[mj]) continue;
+            const float* Xw = b->mp_xw + 3 * (size_t)mj;
+            float Xc[3];
+            for (int i = 0; i < 3; i++) {
+                float sacc = 0;
+                for (int k = 0; k < 3; k++) sacc += R[3 * i + k] * Xw[k];
+                Xc[i] = sacc + t[i];
+            }
+            const float invZ = 1.f / Xc[2];
+            const float u = invZ * K[0] * Xc[0] + K[2];
+            const float v = invZ * K[1] * Xc[1] + K[3];
+            if (!(u >= bd[0] && u < bd[1] && v >= bd[2] && v < bd[3])) continue;
+            double sq = 0;
+            for (int i = 0; i < 3; i++) {
+                const double d = (double)(Xw[i] - Ow[i]);
+                sq += d * d;
+            }
+            const float dist3D = static_cast<float>(std::sqrt(sq));
+            const float maxDistance = 1.2f * b->mp_max_min[2 * (size_t)mj];
+            const float minDistance = 0.8f * b->mp_max_min[2 * (size_t)mj + 1];
+            if (dist3D < minDistance || dist3D > maxDistance) continue;
+            const float ratio = b->mp_max_min[2 * (size_t)mj] / dist3D;
+            const int scale = static_cast<int>(std::ceil(::log(static_cast<double>(ratio)) / b->log_scale_factor));
+            const int predictedScale = std::max(0, std::min(scale, b->n_levels - 1));
+            const float radius = b->th * b->scale_factors[predictedScale];
+            const std::vector<size_t> indices = g->in_area(u, v, radius, predictedScale - 1, predictedScale + 1);
+            if (indices.empty()) continue;
+            const uint8_t* desc1 = b->mp_desc + 32 * (size_t)mj;
+            int bestDist = 256, bestIdx2 = -1;
+            for (size_t idx2 : indices) {
+                if (holds[idx2]) continue;
+                const int dist = hamming(desc1, b->kp_desc + 32 * (size_t)(k0 + idx2));
+                if (dist < bestDist) {
+                    bestDist = dist;
+                    bestIdx2 = (int)idx2;
+                }
+            }
+            if (bestDist <= b->orb_dist) {
+                holds[bestIdx2] = 1;
+                owner[bestIdx2] = idx1;
+                nmatches++;
+                if (b->check_orientation) matchIds.push_back(std::make_pair(idx1, bestIdx2));
+            }
+        }
+        if (b->check_orientation) {
+            const float factor = 1.f / HISTO_LENGTH;
+            std::vector<int> hist[HISTO_LENGTH];
+            for (const auto& m : matchIds) {
+                float diff = b->mp_angle[m0 + m.first] - b->kp_angle[k0 + m.second];
+                if (diff < 0) diff += 360;
+                int bin = cv_round(factor * diff);
+                if (bin == HISTO_LENGTH) bin = 0;
+                if (bin < 0 || bin >= HISTO_LENGTH) return -1;
+                hist[bin].push_back(m.second);
+            }
+            std::sort(std::begin(hist), std::end(hist),
+                      [](const std::vector<int>& l, const std::vector<int>& r) { return l.size() > r.size(); });
+            const size_t max1 = hist[0].size(), max2 = hist[1].size(), max3 = hist[2].size();
+            int eraseBin = 3;
+            if (max2 < 0.1 * max1) eraseBin = 1;
+            else if (max3 < 0.1 * max1) eraseBin = 2;
+            int reduction = 0;
+            for (int bin = eraseBin; bin < HISTO_LENGTH; bin++)
+                for (int i2 : hist[bin]) {
+                    owner[i2] = -1;
+                    reduction++;
+                }
+            nmatches = (int)matchIds.size() - reduction;
+        }
+        for (int i = 0; i < nk; i++) kp_match[k0 + i] = owner[i];
+        n_matches[f] = nmatches;
+    }
+    return 0;
+}
+
 // ORBmatcher::SearchForInitialization(Frame& frame1, Frame& frame2, prevMatched, matches12, windowSize)
 // (ORBmatcher.cc:614-694), literally, pair by pair: octave-0 queries in idx1 order, GetFeaturesInArea
 // over octave 0 (:629-636), the matchedDistance skip (:650-651), best / second best (:653-662), the

@@ -90,6 +90,17 @@ class MotionBatch(C.Structure):
                 ("check_orientation", C.c_int32)]
 
 
+class RelocBatch(C.Structure):
+    """orbm_reloc_batch (include/orbslam2_amd.h)."""
+    _fields_ = [("n_frames", C.c_int32), ("total_kp", C.c_int32), ("total_mp", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_desc", C.c_void_p),
+                ("kp_angle", C.c_void_p), ("kp_claimed", C.c_void_p), ("bounds", C.c_void_p), ("pose", C.c_void_p),
+                ("camera", C.c_void_p), ("mp_begin", C.c_void_p), ("mp_valid", C.c_void_p), ("mp_xw", C.c_void_p),
+                ("mp_max_min", C.c_void_p), ("mp_desc", C.c_void_p), ("mp_angle", C.c_void_p), ("n_levels", C.c_int32),
+                ("scale_factors", C.c_void_p), ("log_scale_factor", C.c_float), ("th", C.c_float),
+                ("orb_dist", C.c_int32), ("check_orientation", C.c_int32)]
+
+
 class InitBatch(C.Structure):
     """orbm_init_batch (include/orbslam2_amd.h)."""
     _fields_ = [("n_pairs", C.c_int32), ("total_kp", C.c_int32), ("total_q", C.c_int32),
@@ -150,6 +161,8 @@ SIGNATURES = {
     "orbm_search_by_projection_device": (C.c_int, [C.POINTER(ProjBatch), VP, VP, VP]),
     "orbm_search_by_projection_motion_device": (C.c_int, [C.POINTER(MotionBatch), VP, VP, VP]),
     "orbm_search_for_initialization": (C.c_int, [C.POINTER(InitBatch), VP, VP, C.c_int]),
+    "orbm_search_by_projection_reloc": (C.c_int, [C.POINTER(RelocBatch), VP, VP, C.c_int]),
+    "orbm_search_by_projection_reloc_device": (C.c_int, [C.POINTER(RelocBatch), VP, VP, VP]),
     "orbm_search_for_initialization_device": (C.c_int, [C.POINTER(InitBatch), VP, VP, VP]),
     "orbv_load_text": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(VP)]),
     "orbv_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, VP, VP, VP, C.c_int, C.POINTER(VP)]),

@@ -438,6 +438,7 @@ struct PjmExtra {
     const float* kp_angle;
     const float* mp_angle;
     int32_t* choice;   // total_mp: accepted idx2 or -1
+    int max_dist;      // TH_HIGH (:1347); ORBdist for SearchByProjection(Frame&, KeyFrame*, ...) (:1425)
 };
 
 // The window scan of one last-frame point (GetFeaturesInArea + the gates of :1329-1339): each lane's
@@ -458,7 +459,7 @@ __device__ __forceinline__ uint32_t pjm_scan(const PjArgs& a, const PjmExtra& e,
     const int lo = mot == 1 ? oct : (mot == 2 ? 0 : oct - 1);
     const int hi = mot == 1 ? a.n_levels : (mot == 2 ? oct : oct + 1);
     const float u = a.mp_proj[3 * (size_t)j], v = a.mp_proj[3 * (size_t)j + 1];
-    const float uR = a.mp_proj[3 * (size_t)j + 2];
+    const float uR = a.kp_ur ? a.mp_proj[3 * (size_t)j + 2] : 0.f;
     const int mincx = max((int)floorf(invW * (u - r - minx)), 0);
     const int maxcx = min((int)ceilf(invW * (u + r - minx)), PJ_COLS - 1);
     const int mincy = max((int)floorf(invH * (v - r - miny)), 0);
@@ -477,8 +478,10 @@ __device__ __forceinline__ uint32_t pjm_scan(const PjArgs& a, const PjmExtra& e,
             if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
             if (a.kp_claimed && a.kp_claimed[k]) continue;
             if (bits && ((bits[idx >> 5] >> (idx & 31)) & 1u)) continue;
-            const float ur = a.kp_ur[k];
-            if (ur > 0 && fabsf(uR - ur) > r) continue;   // :1335
+            if (a.kp_ur) {   // the stereo gate of :1335 (the relocalisation search has none)
+                const float ur = a.kp_ur[k];
+                if (ur > 0 && fabsf(uR - ur) > r) continue;
+            }
             const int dist = pj_hamming(d1, a.kp_desc + 32 * (size_t)k);
             best = min(best, ((uint32_t)dist << PJ_IDX_BITS) | (uint32_t)p);
         }
@@ -522,18 +525,18 @@ __global__ __launch_bounds__(64) void pjm_walk_kernel(PjArgs a, PjmExtra e) {
         int idx = -1, obs = 0;
         if (j < m1) {
             key = (uint32_t)a.mp_cnt[j];
-            obs = a.mp_has_obs[j];
+            obs = a.mp_has_obs ? a.mp_has_obs[j] : 1;   // NULL: every accepted point claims (relocalisation)
             if (key != PJ_NONE) idx = a.grid_idx[k0 + (int)(key & PJ_IDX_MASK)];
         }
         int mych = -1;
         const int cnt = min(64, m1 - c);
         for (int i = 0; i < cnt; i++) {
             uint32_t K = (uint32_t)__shfl((int)key, i, 64);
-            if (K == PJ_NONE || (int)(K >> PJ_IDX_BITS) > PJ_TH_HIGH) continue;   // :1347 (a rescan only loses candidates)
+            if (K == PJ_NONE || (int)(K >> PJ_IDX_BITS) > e.max_dist) continue;   // :1347 (a rescan only loses candidates)
             int ch = __shfl(idx, i, 64);
             if ((bits[ch >> 5] >> (ch & 31)) & 1u) {   // taken earlier in this call: rescan
                 K = pj_wave_min(pjm_scan(a, e, f, c + i, bits, lane, 64));
-                if (K == PJ_NONE || (int)(K >> PJ_IDX_BITS) > PJ_TH_HIGH) continue;
+                if (K == PJ_NONE || (int)(K >> PJ_IDX_BITS) > e.max_dist) continue;
                 ch = a.grid_idx[k0 + (int)(K & PJ_IDX_MASK)];
             }
             const int ob = __shfl(obs, i, 64);   // every lane takes part in the shuffle
@@ -902,6 +905,121 @@ static int pi_common(const orbm_init_batch* b, PjArgs& a, PiExtra& e) {
     return ORB_OK;
 }
 
+// ---------------------------------------------------------------- SearchByProjection(Frame&, KeyFrame*, alreadyFound, th, ORBdist)
+// (ORBmatcher.cc:1364-1445, Tracking::Relocalization).  reloc_project_kernel turns each keyframe point
+// into the motion-model walk's inputs -- validity, projection (u, v) and predicted scale -- with the
+// reference's float expressions; the walk then runs as pjm_* with the level window predictedScale +- 1
+// (motion 0), no stereo gate, every accepted point claiming and ORBdist as the distance bound.
+struct RelocExtra {
+    const float* pose;      // n_frames x 12
+    const float* camera;    // n_frames x 4
+    const uint8_t* valid;   // caller's flag
+    const float* xw;
+    const float* max_min;
+    float log_sf;
+    uint8_t* out_valid;
+    float* out_proj;        // total_mp x 3 (u, v, 0)
+    int32_t* out_level;
+};
+
+__global__ __launch_bounds__(256) void reloc_project_kernel(PjArgs a, RelocExtra r) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= a.total_mp) return;
+    const int f = a.mp_frame[j];
+    bool ok = r.valid[j] != 0;
+    float u = 0.f, v = 0.f;
+    int ps = 0;
+    if (ok) {
+        const float* P = r.pose + 12 * (size_t)f;
+        const float* K = r.camera + 4 * (size_t)f;
+        const float X0 = r.xw[3 * (size_t)j], X1 = r.xw[3 * (size_t)j + 1], X2 = r.xw[3 * (size_t)j + 2];
+        // Rcw * Xw + tcw (cv::Matx: s = 0; s += a(i, k) * b(k) for k = 0..2), then CameraToImage
+        const float c0 = ((P[0] * X0 + P[1] * X1) + P[2] * X2) + P[9];
+        const float c1 = ((P[3] * X0 + P[4] * X1) + P[5] * X2) + P[10];
+        const float c2 = ((P[6] * X0 + P[7] * X1) + P[8] * X2) + P[11];
+        const float invZ = 1.f / c2;
+        u = invZ * K[0] * c0 + K[2];
+        v = invZ * K[1] * c1 + K[3];
+        const float* bd = a.bounds + 4 * (size_t)f;
+        ok = u >= bd[0] && u < bd[1] && v >= bd[2] && v < bd[3];   // ImageBounds::Contains (Frame.cc:51-54)
+        if (ok) {
+            // Ow = -Rcw^T * tcw (CameraPose::Invt), PO = Xw - Ow, dist3D = (float)cv::norm(PO) (double sum)
+            const float o0 = -((P[0] * P[9] + P[3] * P[10]) + P[6] * P[11]);
+            const float o1 = -((P[1] * P[9] + P[4] * P[10]) + P[7] * P[11]);
+            const float o2 = -((P[2] * P[9] + P[5] * P[10]) + P[8] * P[11]);
+            const double d0 = (double)(X0 - o0), d1 = (double)(X1 - o1), d2 = (double)(X2 - o2);
+            const float dist3D = (float)sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+            const float maxD = r.max_min[2 * (size_t)j], minD = r.max_min[2 * (size_t)j + 1];
+            ok = !(dist3D < 0.8f * minD || dist3D > 1.2f * maxD);   // :1399-1401
+            if (ok) {   // PredictScale(dist3D, &frame) (MapPoint.cc:405-415)
+                const float ratio = maxD / dist3D;
+                const int sc = (int)ceil(log((double)ratio) / (double)r.log_sf);
+                ps = max(0, min(sc, a.n_levels - 1));
+            }
+        }
+    }
+    r.out_valid[j] = ok ? 1 : 0;
+    r.out_proj[3 * (size_t)j] = u;
+    r.out_proj[3 * (size_t)j + 1] = v;
+    r.out_proj[3 * (size_t)j + 2] = 0.f;
+    r.out_level[j] = ps;
+}
+
+static size_t reloc_workspace_bytes(int n_frames, int total_kp, int total_mp) {
+    const size_t M = (size_t)std::max(total_mp, 1);
+    return pj_workspace_bytes(n_frames, total_kp, total_mp) + align_up(M * 4, 256) + align_up(M, 256) +
+           align_up(M * 12, 256) + align_up(M * 4, 256);
+}
+
+static int launch_reloc(PjArgs& a, RelocExtra& r, PjmExtra& e, char* ws, int total_kp, int check_ori, hipStream_t st) {
+    pj_carve(a, ws, a.n_frames, total_kp, a.total_mp);
+    size_t o = pj_workspace_bytes(a.n_frames, total_kp, a.total_mp);
+    const size_t M = (size_t)std::max(a.total_mp, 1);
+    e.choice = (int32_t*)(ws + o);
+    o += align_up(M * 4, 256);
+    r.out_valid = (uint8_t*)(ws + o);
+    o += align_up(M, 256);
+    r.out_proj = (float*)(ws + o);
+    o += align_up(M * 12, 256);
+    r.out_level = (int32_t*)(ws + o);
+    hipLaunchKernelGGL(pj_grid_kernel, dim3(a.n_frames), dim3(256), 0, st, a);
+    ORB_HIP_TRY(hipGetLastError());
+    a.mp_valid = r.out_valid;
+    a.mp_proj = r.out_proj;
+    a.mp_level = r.out_level;
+    if (a.total_mp > 0) {
+        hipLaunchKernelGGL(reloc_project_kernel, dim3((a.total_mp + 255) / 256), dim3(256), 0, st, a, r);
+        ORB_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(pjm_score_kernel, dim3((a.total_mp + 256 / PJ_GW - 1) / (256 / PJ_GW)), dim3(256), 0, st, a, e);
+        ORB_HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(pjm_walk_kernel, dim3(a.n_frames), dim3(64), 0, st, a, e);
+    ORB_HIP_TRY(hipGetLastError());
+    if (check_ori) {
+        hipLaunchKernelGGL(pjm_orient_kernel, dim3(a.n_frames), dim3(256), 0, st, a, e);
+        ORB_HIP_TRY(hipGetLastError());
+    }
+    return ORB_OK;
+}
+
+static int reloc_common(const orbm_reloc_batch* b, PjArgs& a, RelocExtra& r, PjmExtra& e) {
+    ORB_CHECK_ARG(b, "null argument");
+    ORB_CHECK_ARG(b->n_frames >= 0 && b->total_kp >= 0 && b->total_mp >= 0, "negative sizes");
+    ORB_CHECK_ARG(b->n_levels >= 1 && b->n_levels <= PJ_MAX_LEVELS && b->scale_factors, "bad scale pyramid");
+    ORB_CHECK_ARG(b->orb_dist >= 0 && b->orb_dist < 256, "ORBdist must be in [0, 256)");
+    std::memset(&a, 0, sizeof(a));
+    std::memset(&r, 0, sizeof(r));
+    std::memset(&e, 0, sizeof(e));
+    a.n_frames = b->n_frames;
+    a.n_levels = b->n_levels;
+    for (int l = 0; l < b->n_levels; l++) a.scale[l] = b->scale_factors[l];
+    a.th = b->th;
+    a.total_mp = b->total_mp;
+    r.log_sf = b->log_scale_factor;
+    e.max_dist = b->orb_dist;
+    return ORB_OK;
+}
+
 }  // namespace orbamd
 
 using namespace orbamd;
@@ -1039,7 +1157,7 @@ extern "C" int orbm_search_by_projection_motion_device(const orbm_motion_batch* 
     const size_t base = pj_workspace_bytes(b->n_frames, b->total_kp, b->total_mp);
     if ((rc = g_pj.ws.reserve(base + align_up((size_t)std::max(b->total_mp, 1) * 4, 256)))) return rc;
     pj_carve(a, g_pj.ws.as<char>(), b->n_frames, b->total_kp, b->total_mp);
-    PjmExtra e{b->motion, b->kp_angle, b->mp_angle, reinterpret_cast<int32_t*>(g_pj.ws.as<char>() + base)};
+    PjmExtra e{b->motion, b->kp_angle, b->mp_angle, reinterpret_cast<int32_t*>(g_pj.ws.as<char>() + base), PJ_TH_HIGH};
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(pj_grid_kernel, dim3(a.n_frames), dim3(256), 0, st, a);
     ORB_HIP_TRY(hipGetLastError());
@@ -1154,5 +1272,105 @@ extern "C" int orbm_search_for_initialization(const orbm_init_batch* b, int32_t*
         ORB_HIP_TRY(hipMemcpy(b->prev_matched, d + o_pm, (size_t)Q * 8, hipMemcpyDeviceToHost));
     }
     ORB_HIP_TRY(hipMemcpy(n_matches, d + o_nm, (size_t)P * 4, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+
+extern "C" int orbm_search_by_projection_reloc_device(const orbm_reloc_batch* b, int32_t* kp_match, int32_t* n_matches,
+                                                      void* stream) {
+    PjArgs a;
+    RelocExtra r;
+    PjmExtra e;
+    int rc;
+    if ((rc = reloc_common(b, a, r, e))) return rc;
+    if (b->n_frames == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kp_begin && b->mp_begin && b->bounds && b->pose && b->camera && kp_match && n_matches, "null array");
+    ORB_CHECK_ARG(b->total_kp == 0 || (b->kp_xy && b->kp_octave && b->kp_desc), "null keypoint array");
+    ORB_CHECK_ARG(b->total_mp == 0 || (b->mp_valid && b->mp_xw && b->mp_max_min && b->mp_desc), "null keyframe point array");
+    ORB_CHECK_ARG(!b->check_orientation || (b->kp_angle && (b->total_mp == 0 || b->mp_angle)),
+                  "CheckOrientation needs kp_angle / mp_angle");
+    a.kp_begin = b->kp_begin; a.kp_xy = b->kp_xy; a.kp_oct = b->kp_octave; a.kp_ur = nullptr;
+    a.kp_desc = b->kp_desc; a.kp_claimed = b->kp_claimed; a.bounds = b->bounds;
+    a.mp_begin = b->mp_begin; a.mp_desc = b->mp_desc; a.mp_has_obs = nullptr;
+    a.kp_match = kp_match;
+    a.n_matches = n_matches;
+    r.pose = b->pose; r.camera = b->camera; r.valid = b->mp_valid; r.xw = b->mp_xw; r.max_min = b->mp_max_min;
+    e.kp_angle = b->kp_angle; e.mp_angle = b->mp_angle;
+    int dev = 0;
+    ORB_HIP_TRY(hipGetDevice(&dev));
+    if (g_pj.device != dev) {
+        g_pj.ws.release();
+        g_pj.io.release();
+        g_pj.device = dev;
+    }
+    if ((rc = g_pj.ws.reserve(reloc_workspace_bytes(b->n_frames, b->total_kp, b->total_mp)))) return rc;
+    return launch_reloc(a, r, e, g_pj.ws.as<char>(), b->total_kp, b->check_orientation, (hipStream_t)stream);
+}
+
+extern "C" int orbm_search_by_projection_reloc(const orbm_reloc_batch* b, int32_t* kp_match, int32_t* n_matches,
+                                               int device) {
+    PjArgs a;
+    RelocExtra r;
+    PjmExtra e;
+    int rc;
+    if ((rc = reloc_common(b, a, r, e))) return rc;
+    const int F = b->n_frames;
+    if (F == 0) return ORB_OK;
+    ORB_CHECK_ARG(b->kp_begin && b->mp_begin && b->bounds && b->pose && b->camera && kp_match && n_matches, "null array");
+    ORB_CHECK_ARG(b->kp_begin[0] == 0 && b->mp_begin[0] == 0 && b->kp_begin[F] == b->total_kp &&
+                      b->mp_begin[F] == b->total_mp,
+                  "kp_begin / mp_begin must start at 0 and end at total_kp / total_mp");
+    for (int f = 0; f < F; f++) {
+        ORB_CHECK_ARG(b->kp_begin[f + 1] >= b->kp_begin[f] && b->mp_begin[f + 1] >= b->mp_begin[f],
+                      "offsets must be non-decreasing");
+        ORB_CHECK_ARG(b->kp_begin[f + 1] - b->kp_begin[f] <= PJ_MAXKP, "frame has more than ORBM_PROJ_MAX_KP keypoints");
+    }
+    const int K = b->total_kp, M = b->total_mp;
+    ORB_CHECK_ARG(K == 0 || (b->kp_xy && b->kp_octave && b->kp_desc), "null keypoint array");
+    ORB_CHECK_ARG(M == 0 || (b->mp_valid && b->mp_xw && b->mp_max_min && b->mp_desc), "null keyframe point array");
+    ORB_CHECK_ARG(!b->check_orientation || (b->kp_angle && (M == 0 || b->mp_angle)),
+                  "CheckOrientation needs kp_angle / mp_angle");
+    ORB_HIP_TRY(hipSetDevice(device));
+    if (g_pj.device != device) {
+        g_pj.ws.release();
+        g_pj.io.release();
+        g_pj.device = device;
+    }
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += align_up(std::max<size_t>(bytes, 1), 256); return o; };
+    const size_t o_kb = take((size_t)(F + 1) * 4), o_xy = take((size_t)K * 8), o_oc = take((size_t)K * 4),
+                 o_kd = take((size_t)K * 32), o_ka = take((size_t)K * 4), o_kc = take(b->kp_claimed ? (size_t)K : 0),
+                 o_bd = take((size_t)F * 16), o_po = take((size_t)F * 48), o_ca = take((size_t)F * 16),
+                 o_mb = take((size_t)(F + 1) * 4), o_mv = take((size_t)M), o_mx = take((size_t)M * 12),
+                 o_mm = take((size_t)M * 8), o_md = take((size_t)M * 32), o_ma = take((size_t)M * 4),
+                 o_km = take((size_t)K * 4), o_nm = take((size_t)F * 4);
+    if ((rc = g_pj.io.reserve(off))) return rc;
+    if ((rc = g_pj.ws.reserve(reloc_workspace_bytes(F, K, M)))) return rc;
+    char* d = g_pj.io.as<char>();
+    auto up = [&](size_t o, const void* src, size_t bytes) -> int {
+        if (bytes && src) ORB_HIP_TRY(hipMemcpy(d + o, src, bytes, hipMemcpyHostToDevice));
+        return ORB_OK;
+    };
+    if ((rc = up(o_kb, b->kp_begin, (size_t)(F + 1) * 4)) || (rc = up(o_xy, b->kp_xy, (size_t)K * 8)) ||
+        (rc = up(o_oc, b->kp_octave, (size_t)K * 4)) || (rc = up(o_kd, b->kp_desc, (size_t)K * 32)) ||
+        (rc = up(o_ka, b->kp_angle, (size_t)K * 4)) || (rc = up(o_kc, b->kp_claimed, (size_t)K)) ||
+        (rc = up(o_bd, b->bounds, (size_t)F * 16)) || (rc = up(o_po, b->pose, (size_t)F * 48)) ||
+        (rc = up(o_ca, b->camera, (size_t)F * 16)) || (rc = up(o_mb, b->mp_begin, (size_t)(F + 1) * 4)) ||
+        (rc = up(o_mv, b->mp_valid, (size_t)M)) || (rc = up(o_mx, b->mp_xw, (size_t)M * 12)) ||
+        (rc = up(o_mm, b->mp_max_min, (size_t)M * 8)) || (rc = up(o_md, b->mp_desc, (size_t)M * 32)) ||
+        (rc = up(o_ma, b->mp_angle, (size_t)M * 4)))
+        return rc;
+    a.kp_begin = (const int32_t*)(d + o_kb); a.kp_xy = (const float*)(d + o_xy); a.kp_oct = (const int32_t*)(d + o_oc);
+    a.kp_desc = (const uint8_t*)(d + o_kd); a.kp_claimed = b->kp_claimed ? (const uint8_t*)(d + o_kc) : nullptr;
+    a.kp_ur = nullptr; a.bounds = (const float*)(d + o_bd); a.mp_begin = (const int32_t*)(d + o_mb);
+    a.mp_desc = (const uint8_t*)(d + o_md); a.mp_has_obs = nullptr;
+    a.kp_match = (int32_t*)(d + o_km); a.n_matches = (int32_t*)(d + o_nm);
+    r.pose = (const float*)(d + o_po); r.camera = (const float*)(d + o_ca); r.valid = (const uint8_t*)(d + o_mv);
+    r.xw = (const float*)(d + o_mx); r.max_min = (const float*)(d + o_mm);
+    e.kp_angle = b->kp_angle ? (const float*)(d + o_ka) : nullptr;
+    e.mp_angle = b->mp_angle ? (const float*)(d + o_ma) : nullptr;
+    if ((rc = launch_reloc(a, r, e, g_pj.ws.as<char>(), K, b->check_orientation, nullptr))) return rc;
+    if (K) ORB_HIP_TRY(hipMemcpy(kp_match, d + o_km, (size_t)K * 4, hipMemcpyDeviceToHost));
+    ORB_HIP_TRY(hipMemcpy(n_matches, d + o_nm, (size_t)F * 4, hipMemcpyDeviceToHost));
     return ORB_OK;
 }

@@ -458,3 +458,62 @@ def search_for_initialization_device(batch: dict, matches12=None, n_matches=None
     check(lib().orbm_search_for_initialization_device(C.byref(ib), tptr(matches12), tptr(n_matches), stream_ptr(stream)),
           "orbm_search_for_initialization_device")
     return matches12, n_matches
+
+
+_RELOC_KEYS = (("kp_begin", np.int32), ("kp_xy", np.float32), ("kp_octave", np.int32), ("kp_desc", np.uint8),
+               ("kp_angle", np.float32), ("kp_claimed", np.uint8), ("bounds", np.float32), ("pose", np.float32),
+               ("camera", np.float32), ("mp_begin", np.int32), ("mp_valid", np.uint8), ("mp_xw", np.float32),
+               ("mp_max_min", np.float32), ("mp_desc", np.uint8), ("mp_angle", np.float32))
+
+
+def _reloc_struct(batch, conv, K, M):
+    from ._lib import RelocBatch
+    sf = np.ascontiguousarray(batch["scale_factors"], np.float32)
+    F = len(batch["kp_begin"]) - 1
+    rb = RelocBatch(F, K, M, *[conv(batch[k], dt) if batch.get(k) is not None else None for k, dt in _RELOC_KEYS],
+                    len(sf), ptr(sf), float(batch["log_scale_factor"]), float(batch["th"]), int(batch["orb_dist"]),
+                    int(bool(batch["check_orientation"])))
+    return rb, sf
+
+
+def SearchByProjectionReloc(batch: dict, device: int = 0):
+    """ORBmatcher::SearchByProjection(Frame& frame, KeyFrame* keyframe, alreadyFound, th, ORBdist)
+    (src/ORBmatcher.cc:1364-1445, Tracking::Relocalization) batched over (frame, keyframe) pairs, host
+    arrays (orbm_reloc_batch fields; kp_claimed may be None).  Returns (kp_match [total_kp] = keyframe
+    idx1 assigned to each frame keypoint or -1, n_matches [F])."""
+    keep = []
+
+    def conv(a, dt):
+        a = np.ascontiguousarray(a, dt)
+        keep.append(a)
+        return ptr(a)
+    F = len(batch["kp_begin"]) - 1
+    K, M = int(batch["kp_begin"][-1]), int(batch["mp_begin"][-1])
+    rb, _sf = _reloc_struct(batch, conv, K, M)
+    km = np.empty(max(K, 1), np.int32)
+    nm = np.empty(max(F, 1), np.int32)
+    check(lib().orbm_search_by_projection_reloc(C.byref(rb), ptr(km), ptr(nm), int(device)),
+          "orbm_search_by_projection_reloc")
+    return km[:K], nm[:F]
+
+
+def search_by_projection_reloc_device(batch: dict, kp_match=None, n_matches=None, stream=None):
+    """Device form of SearchByProjectionReloc: GPU tensors for the orbm_reloc_batch arrays, host values for
+    scale_factors, log_scale_factor, th, orb_dist and check_orientation."""
+    import torch
+    kb = batch["kp_begin"]
+    F = kb.numel() - 1
+    K, M = int(batch["kp_xy"].shape[0]), int(batch["mp_xw"].shape[0])
+    for k, dt in _RELOC_KEYS:
+        t = batch.get(k)
+        if t is not None and (not t.is_contiguous() or t.dtype != getattr(torch, np.dtype(dt).name)):
+            raise ValueError(f"{k} must be a contiguous {np.dtype(dt).name} tensor")
+    if kp_match is None:
+        kp_match = torch.empty(max(K, 1), dtype=torch.int32, device=kb.device)
+    if n_matches is None:
+        n_matches = torch.empty(max(F, 1), dtype=torch.int32, device=kb.device)
+    rb, _sf = _reloc_struct(batch, lambda t, dt: tptr(t), K, M)
+    check(lib().orbm_search_by_projection_reloc_device(C.byref(rb), tptr(kp_match), tptr(n_matches),
+                                                       stream_ptr(stream)),
+          "orbm_search_by_projection_reloc_device")
+    return kp_match, n_matches

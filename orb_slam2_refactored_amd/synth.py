@@ -560,3 +560,92 @@ def make_init_batch(seed: int = 0, n_pairs: int = 4, n1=4000, n2=4000, width: fl
     out["q_begin"] = np.concatenate([[0], np.cumsum(n1s)]).astype(np.int32)
     out.update(window=int(window), nnratio=float(nnratio), check_orientation=bool(check_orientation))
     return out
+
+
+def make_reloc_batch(seed: int = 0, n_frames: int = 4, n_kp=2000, n_mp=600, th: float = 10.0, orb_dist: int = 100,
+                     check_orientation: bool = True, dup_frac: float = 0.15, claimed_frac: float = 0.1):
+    """SearchByProjection(Frame&, KeyFrame*, alreadyFound, th, ORBdist) inputs (orbm_reloc_batch, host arrays)
+    shaped like Tracking::Relocalization (Tracking.cc:403,417: th 10 / ORBdist 100, then 3 / 64) on a
+    KITTI camera.  Per frame: a pose (small rotation, a few metres of translation); the candidate
+    keyframe's points in front of it (90 % valid), maxDistance_ = dist * 1.2^o * U(0.9, 1.1) for a random
+    octave o and minDistance_ = maxDistance_ / 1.2^7 (MapPoint.cc:369-377), 5 % outside the invariance
+    range; 70 % of the points observed by a keypoint near the projection (octave = the predicted scale
+    +- 1 or off-window, 0-60 flipped bits), `dup_frac` of them sharing a keypoint with another point,
+    plus random keypoints; `claimed_frac` of the keypoints already hold a map point.  Angles around a
+    dominant rotation for CheckOrientation.  n_kp / n_mp: int or per-frame list."""
+    rng = np.random.default_rng(seed)
+    kps = [int(n_kp)] * n_frames if np.isscalar(n_kp) else [int(v) for v in n_kp]
+    mps = [int(n_mp)] * n_frames if np.isscalar(n_mp) else [int(v) for v in n_mp]
+    fx, fy, cx, cy = np.float32(KITTI["fx"]), np.float32(KITTI["fx"]), np.float32(607.1928), np.float32(185.2157)
+    W, H = 1241.0, 376.0
+    cum = np.ones(8, np.float32)
+    for i in range(1, 8):
+        cum[i] = np.float32(cum[i - 1] * np.float32(1.2))
+    F = dict(kp_xy=[], kp_octave=[], kp_desc=[], kp_angle=[], kp_claimed=[], bounds=[], pose=[], camera=[],
+             mp_valid=[], mp_xw=[], mp_max_min=[], mp_desc=[], mp_angle=[])
+    for f in range(n_frames):
+        n, m = kps[f], mps[f]
+        Rcw = _small_rot(rng, 3.0).astype(np.float32)
+        tcw = rng.normal(0, 2.0, 3).astype(np.float32)
+        # points in the camera frame, then to the world: Xw = Rcw^T (Xc - tcw)
+        z = rng.uniform(4, 40, m)
+        u = rng.uniform(-20, W + 20, m)
+        v = rng.uniform(-10, H + 10, m)
+        Xc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+        Xw = ((Xc - tcw[None]) @ Rcw).astype(np.float32)
+        Ow = -(Rcw.T @ tcw)
+        dist = np.linalg.norm(Xw - Ow[None], axis=1)
+        o = rng.integers(0, 8, m)
+        maxd = dist * (1.2 ** o) * rng.uniform(0.9, 1.1, m)
+        bad = rng.random(m) < 0.05
+        maxd = np.where(bad, dist * rng.choice([0.5, 3.0], m), maxd)
+        mind = maxd / cum[7]
+        mdesc = rng.integers(0, 256, size=(m, 32), dtype=np.uint8)
+        rot = rng.uniform(0, 360)
+        mang = rng.uniform(0, 360, m)
+        x = rng.uniform(0, W, n)
+        y = rng.uniform(0, H, n)
+        octv = rng.integers(0, 8, n)
+        desc = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        ang = rng.uniform(0, 360, n)
+        used = []
+        for j in range(m):
+            if n == 0 or rng.random() >= 0.7:
+                continue
+            i = int(rng.choice(used)) if used and rng.random() < dup_frac else int(rng.integers(0, n))
+            used.append(i)
+            x[i] = u[j] + rng.normal(0, 1.5)
+            y[i] = v[j] + rng.normal(0, 1.5)
+            ratio = maxd[j] / max(dist[j], 1e-6)
+            ps = int(min(7, max(0, np.ceil(np.log(ratio) / np.log(1.2)))))
+            octv[i] = min(7, max(0, ps + int(rng.choice([-1, 0, 0, 1, 3]))))
+            d = mdesc[j].copy()
+            for bit in rng.choice(256, size=int(rng.integers(0, 61)), replace=False):
+                d[bit >> 3] ^= np.uint8(1 << (bit & 7))
+            desc[i] = d
+            ang[i] = (mang[j] - rot + rng.normal(0, 6)) % 360
+        F["kp_xy"].append(np.stack([x, y], 1).astype(np.float32))
+        F["kp_octave"].append(octv.astype(np.int32))
+        F["kp_desc"].append(desc)
+        F["kp_angle"].append(np.minimum(ang, 359.99).astype(np.float32))
+        F["kp_claimed"].append((rng.random(n) < claimed_frac).astype(np.uint8))
+        F["bounds"].append(np.array([[0.0, W, 0.0, H]], np.float32))
+        F["pose"].append(np.concatenate([Rcw.reshape(-1), tcw])[None].astype(np.float32))
+        F["camera"].append(np.array([[fx, fy, cx, cy]], np.float32))
+        F["mp_valid"].append((rng.random(m) < 0.9).astype(np.uint8))
+        F["mp_xw"].append(Xw)
+        F["mp_max_min"].append(np.stack([maxd, mind], 1).astype(np.float32))
+        F["mp_desc"].append(mdesc)
+        F["mp_angle"].append(np.minimum(mang, 359.99).astype(np.float32))
+    shapes = dict(kp_xy=(0, 2), kp_octave=(0,), kp_desc=(0, 32), kp_angle=(0,), kp_claimed=(0,), bounds=(0, 4),
+                  pose=(0, 12), camera=(0, 4), mp_valid=(0,), mp_xw=(0, 3), mp_max_min=(0, 2), mp_desc=(0, 32),
+                  mp_angle=(0,))
+    out = {}
+    for k, shape in shapes.items():
+        dt = np.uint8 if k in ("kp_desc", "mp_desc", "kp_claimed", "mp_valid") else (np.int32 if k == "kp_octave" else np.float32)
+        out[k] = np.ascontiguousarray(np.concatenate(F[k]).astype(dt) if F[k] else np.zeros(shape, dt))
+    out["kp_begin"] = np.concatenate([[0], np.cumsum(kps)]).astype(np.int32)
+    out["mp_begin"] = np.concatenate([[0], np.cumsum(mps)]).astype(np.int32)
+    out.update(scale_factors=cum, log_scale_factor=float(np.float32(np.log(np.float64(np.float32(1.2))))), th=float(th),
+               orb_dist=int(orb_dist), check_orientation=bool(check_orientation))
+    return out

@@ -466,3 +466,33 @@ def search_for_initialization(b):
     n = np.zeros(max(P, 1), np.int32)
     assert lib().oracle_search_for_initialization(C.byref(ib), ptr(m12), ptr(n)) == 0
     return m12[:ib.total_q], n[:P], prev
+
+
+class RelocBatch(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("total_kp", C.c_int32), ("total_mp", C.c_int32),
+                ("kp_begin", C.c_void_p), ("kp_xy", C.c_void_p), ("kp_octave", C.c_void_p), ("kp_desc", C.c_void_p),
+                ("kp_angle", C.c_void_p), ("kp_claimed", C.c_void_p), ("bounds", C.c_void_p), ("pose", C.c_void_p),
+                ("camera", C.c_void_p), ("mp_begin", C.c_void_p), ("mp_valid", C.c_void_p), ("mp_xw", C.c_void_p),
+                ("mp_max_min", C.c_void_p), ("mp_desc", C.c_void_p), ("mp_angle", C.c_void_p), ("n_levels", C.c_int32),
+                ("scale_factors", C.c_void_p), ("log_scale_factor", C.c_float), ("th", C.c_float),
+                ("orb_dist", C.c_int32), ("check_orientation", C.c_int32)]
+
+
+_RELOC_KEYS = [("kp_begin", np.int32), ("kp_xy", np.float32), ("kp_octave", np.int32), ("kp_desc", np.uint8),
+               ("kp_angle", np.float32), ("kp_claimed", np.uint8), ("bounds", np.float32), ("pose", np.float32),
+               ("camera", np.float32), ("mp_begin", np.int32), ("mp_valid", np.uint8), ("mp_xw", np.float32),
+               ("mp_max_min", np.float32), ("mp_desc", np.uint8), ("mp_angle", np.float32)]
+
+
+def search_by_projection_reloc(b):
+    """SearchByProjection(Frame&, KeyFrame*, alreadyFound, th, ORBdist) per frame (ORBmatcher.cc:1364-1445)."""
+    keep = _Keep()
+    F = len(b["kp_begin"]) - 1
+    ptrs = [keep(b[k], dt) if b.get(k) is not None else None for k, dt in _RELOC_KEYS]
+    rb = RelocBatch(F, int(b["kp_begin"][-1]), int(b["mp_begin"][-1]), *ptrs, len(b["scale_factors"]),
+                    keep(b["scale_factors"], np.float32), float(b["log_scale_factor"]), float(b["th"]),
+                    int(b["orb_dist"]), int(bool(b["check_orientation"])))
+    km = np.zeros(max(rb.total_kp, 1), np.int32)
+    n = np.zeros(max(F, 1), np.int32)
+    assert lib().oracle_search_by_projection_reloc(C.byref(rb), ptr(km), ptr(n)) == 0
+    return km[:rb.total_kp], n[:F]
