@@ -3,15 +3,14 @@
 
 Headline line (`value`): configs[1] / C2 — 1280x720 mono, 8 levels, 2000 features, extract + brute-force
 Hamming top-2/ratio match of every frame against its predecessor.  One step = one batch of `--frames`
-(default 8192 = eight 1024-frame C5 jobs, so the driver's 20 steps time > 1 s and at N = 8 every GPU
-holds the 1024 frames C5 gives the whole node) synthetic frames already resident in HBM: a camera-pan
-sequence (frame i = frame 0 shifted by i * (+3, +2) px with fresh noise: consecutive frames are the §8d
-C2 shifted pair), so frame i is matched to i-1 as §8d C5 says.  With N > 1 ranks the job is sharded
-(strong scaling): rank r
-extracts its contiguous shard, matches frames 1.. of the shard locally, all-gathers the padded
-keypoint / descriptor slots over RCCL (the loop-closure descriptor exchange of configs[4]) and matches
-its first frame against rank r-1's last frame read from the gathered slots (one step later, so the
-gather overlaps the next step's kernels).
+(default 8192) synthetic frames per GPU already resident in HBM: a camera-pan sequence (frame i = frame 0
+shifted by i * (+3, +2) px with fresh noise: consecutive frames are the §8d C2 shifted pair), so frame i
+is matched to i-1 as §8d C5 says (global frame 0 has no predecessor).  With N > 1 ranks the job is
+N x 8192 frames (weak scaling): rank r extracts its contiguous shard, matches frames 1.. of the shard
+locally, all-gathers the per-frame counts and then its Σn x 32 B descriptor block over RCCL (the
+loop-closure descriptor exchange of configs[4]) and matches its first frame against rank r-1's last
+frame read from the gathered descriptors (one step later, so the gather overlaps the next step's
+kernels).
 
 Secondary objects on the same JSON line, each with its own rate, roofline and CPU baseline:
   c1          configs[0]: 640x480, 1000 features — GPU batch throughput + the CPU plumbing median of 200
@@ -24,8 +23,9 @@ Secondary objects on the same JSON line, each with its own rate, roofline and CP
   stereo, search_by_projection, bow, pose_opt: the §8f rows
 
 CPU baselines run the oracle (oracle/orb_oracle.cpp, the C++ restatement; the reference cannot be
-built here) on the GPU box's host cores: one thread and all usable cores (one frame per thread, capped
-at 16 = the box's CPU share), with the CPU model stated.  Prints ONE JSON line on rank 0.
+built here) on the GPU box's host cores: one thread and 16 threads (one frame per thread) -- 16 is the
+CPU share of a one-GPU box of this pool (its `nproc` reports the whole machine's CPUs, which the box
+does not own) -- with the CPU model stated.  Prints ONE JSON line on rank 0.
 """
 import argparse
 import concurrent.futures as cf
@@ -159,7 +159,9 @@ def cpu_baseline_block(unit, sample, single, multi, info):
     return {"value": vN, "unit": unit, "cores": info["threads_all"], "kind": "port",
             "sample": f"{sample}; {nN} units on {info['threads_all']} threads, oracle/orb_oracle.cpp (-O3)",
             "single_thread": {"value": v1, "cores": 1, "units": n1}, "cpu_model": info["cpu_model"],
-            "nproc": info["nproc"], "usable_cpus": info["usable_cpus"]}
+            "nproc": info["nproc"], "usable_cpus": info["usable_cpus"],
+            "cores_note": "16 threads = the CPU share of this pool's one-GPU box (OMP_NUM_THREADS / MAX_JOBS are 16 "
+                          "there); nproc / affinity report the whole machine's CPUs, which the box does not own"}
 
 
 def event_ms(fn, steps, stream):
@@ -650,11 +652,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=8192, help="frames per step for the whole job (sharded over ranks)")
+    ap.add_argument("--frames", type=int, default=8192, help="frames per step per GPU (weak scaling: the job is frames x world)")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="run the N > 1 exchange path (pack, counts / payload gather, cross-shard match) at N = 1 too")
     ap.add_argument("--no-legs", action="store_true", help="only the headline C2 measurement")
     for leg in ("c1", "textured", "c3", "ba", "stereo", "pose", "projection", "bow"):
         ap.add_argument(f"--no-{leg}", action="store_true")
@@ -672,14 +676,13 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
-    from orb_slam2_refactored_amd.shard import SlotExchange, Slots, cross_shard_predecessor, shard_range
+    from orb_slam2_refactored_amd.shard import CompactExchange, Slots, cross_shard_predecessor, shard_range
     from orb_slam2_refactored_amd.synth import pan_sequence
 
     W, H = args.width, args.height
-    total = args.frames
-    if total % world:
-        raise SystemExit("--frames must be a multiple of the number of ranks (equal shards for the all-gather)")
-    g0, B = shard_range(total, world, rank)
+    B = args.frames                      # frames per GPU per step (weak scaling)
+    total = B * world
+    g0, _ = shard_range(total, world, rank)
     # the global job is a pan sequence of 16 distinct frames repeated (frame g = base[g % 16]); every
     # frame is its own buffer in HBM (8192 x 0.92 MB >> the 256 MB Infinity Cache)
     base = pan_sequence(0, W, H, 16)
@@ -691,47 +694,56 @@ def main():
     cap = ex.max_keypoints(H, W)
     stream = torch.cuda.current_stream()
     match_out = torch.empty((4, B, cap), dtype=torch.int32, device=dev)
-    if world == 1:
-        # frame i vs i-1 (frame 0 vs the job's last frame)
-        prev_idx = torch.tensor([(i - 1) % B for i in range(B)], dtype=torch.int32, device=dev)
+    # frames 1.. of the shard vs their in-shard predecessor (global frame 0 has none: not matched)
+    prev_idx = torch.arange(0, B - 1, dtype=torch.int32, device=dev)
+    pred = cross_shard_predecessor(rank, world, B) if world > 1 else -1
+    if world == 1 and not args.force_exchange:
         single = Slots.empty(B, cap, dev)
         xchg = None
     else:
-        # frames 1.. of the shard vs their in-shard predecessor; frame 0 vs rank r-1's last frame from the
-        # gathered slots (cross_shard_predecessor), matched one step later behind the gather's wait
-        prev_idx = torch.arange(0, B - 1, dtype=torch.int32, device=dev)
-        xchg = SlotExchange(B, cap, dev)
-        pred = cross_shard_predecessor(rank, world, B)
-        pred_idx = torch.tensor([pred], dtype=torch.int32, device=dev)
+        # rank r's first frame vs rank r-1's last frame, read from the gathered descriptors of that step
+        # one step later (the payload gather overlaps the next step's kernels); rank 0's first frame is
+        # global frame 0 and has no predecessor
+        xchg = CompactExchange(B, cap, dev)
         cross_out = torch.empty((4, 1, cap), dtype=torch.int32, device=dev)
-    state = {"pending": None}
+    state = {"k": 0, "cross": 0}
 
-    def cross_match(i):
-        xchg.wait(i)
-        loc, glob = xchg.local[i], xchg.gathered(i)
-        m.match_batch_device(loc.desc[0:1], loc.counts[0:1], glob.desc, glob.counts, out=cross_out, stream=stream,
-                             pair_b=pred_idx)
+    def cross_match(j):
+        xchg.wait(j)
+        if rank == 0:
+            return
+        pb = xchg.frame(j, rank - 1, B - 1)
+        n = int(pb.shape[0])
+        if n == 0:
+            return
+        loc = xchg.local(j)
+        nb = torch.full((1,), n, dtype=torch.int32, device=dev)
+        m.match_batch_device(loc.desc[0:1], loc.counts[0:1], pb.reshape(1, n, 32), nb, out=cross_out, stream=stream)
+        state["cross"] += 1
 
     def step():
         if xchg is None:
             ex.extract_batch_device(frames, single.kps, single.desc, single.counts, stream=stream)
-            m.match_batch_device(single.desc, single.counts, single.desc, single.counts, out=match_out, stream=stream,
-                                 pair_b=prev_idx)
+            if B > 1:
+                m.match_batch_device(single.desc[1:], single.counts[1:], single.desc, single.counts, out=match_out[:, 1:],
+                                     stream=stream, pair_b=prev_idx)
             return
-        loc = xchg.acquire()
+        k = state["k"]
+        loc = xchg.local(k)
         ex.extract_batch_device(frames, loc.kps, loc.desc, loc.counts, stream=stream)
         if B > 1:
             m.match_batch_device(loc.desc[1:], loc.counts[1:], loc.desc, loc.counts, out=match_out[:, 1:],
                                  stream=stream, pair_b=prev_idx)
-        i = xchg.publish()
-        if state["pending"] is not None:
-            cross_match(state["pending"])
-        state["pending"] = i
+        xchg.publish(k)
+        if k >= 1:
+            cross_match(k - 1)
+        state["k"] = k + 1
 
     def finish():
-        if xchg is not None and state["pending"] is not None:
-            cross_match(state["pending"])
-            state["pending"] = None
+        if xchg is not None and xchg.pending is not None:
+            j = xchg.pending
+            xchg.drain()
+            cross_match(j)
 
     for _ in range(args.warmup):
         step()
@@ -768,7 +780,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    counts = (single.counts if xchg is None else xchg.local[0].counts)
+    counts = (single.counts if xchg is None else xchg.local(0).counts)
     n_kp = float(counts.float().mean().item())
     matches = int((match_out[3] >= 0).sum().item())
     value = total * args.steps / elapsed
@@ -796,15 +808,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (pan sequence of §8d G frames, shifted (+3,+2) px per frame)",
         "config": {"workload": f"C2: {W}x{H} mono, 8 levels, {args.nfeatures} features, extract + brute-force "
                                f"Hamming top-2/ratio match of every frame vs its predecessor",
                    "frames_per_step": total, "frames_per_step_per_gpu": B, "width": W, "height": H, "nlevels": 8,
-                   "nfeatures": args.nfeatures, "parallelism": f"{total}-frame job sharded over {world} GPU(s)"
-                   + (", RCCL all-gather of descriptor slots, cross-shard predecessor match" if world > 1 else "")},
+                   "nfeatures": args.nfeatures, "parallelism": f"{total}-frame job sharded over {world} GPU(s), "
+                   f"{B} frames per GPU" + (", RCCL all-gather of the descriptor blocks, cross-shard predecessor match"
+                                          if world > 1 else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": per_launch_ms,
@@ -819,12 +832,25 @@ def main():
         "device_fault_mask": fault,
         "timed_region_s": elapsed,
     }
-    if world > 1:
-        slot_bytes = cap * (28 + 32) + 4
-        result["c5"] = {"workload": "C5 semantics: frames sharded, RCCL all-gather of padded slots, frame i matched "
-                                    "to i-1 across shard boundaries from the gathered slots",
-                        "gather_bytes_per_step": slot_bytes * total, "cross_shard_predecessor": pred,
-                        "cross_match_first_frame_matches": int((cross_out[3] >= 0).sum().item())}
+    if xchg is not None:
+        xchg.collect_gather_times()
+        pay = xchg.payload_bytes[-args.steps:] if xchg.payload_bytes else [0]
+        gms = xchg.gather_ms[-args.steps:] if xchg.gather_ms else [0.0]
+        per_step = float(np.mean(pay)) + world * B * 4   # payload + counts
+        recv = per_step * (world - 1) / world             # bytes each rank receives
+        padded = (cap * (28 + 32) + 4) * total            # the round-2 padded-slot gather, for comparison
+        result["c5"] = {"workload": "C5 semantics: frames sharded (weak scaling, frames_per_step_per_gpu each), "
+                                    "per-frame counts all-gathered, then each rank's Σn x 32 B descriptor block "
+                                    "(padded to the step's largest block) all-gathered over RCCL; frame i matched to "
+                                    "i-1 across shard boundaries from the gathered descriptors",
+                        "gather_bytes_per_step": per_step, "received_bytes_per_rank_per_step": recv,
+                        "padded_slot_gather_bytes_per_step": padded,
+                        "gather_ms_per_step": float(np.mean(gms)),
+                        "gather_GBs_received_per_rank": recv / (float(np.mean(gms)) * 1e-3) / 1e9 if np.mean(gms) else None,
+                        "xgmi_bound_ms": {"all_7_links": recv / (7 * 153e9) * 1e3, "single_link": recv / 153e9 * 1e3},
+                        "cross_shard_predecessor": pred,
+                        "cross_match_first_frame_matches": int((cross_out[3] >= 0).sum().item()) if rank > 0 else None,
+                        "cross_matches_run": state["cross"]}
 
     legs = rank == 0 and not args.no_legs
     cpu = world == 1 and not args.no_cpu_baseline and rank == 0

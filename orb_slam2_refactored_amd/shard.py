@@ -12,6 +12,13 @@ enqueued on the compute stream right behind them.  A set of slot buffers is writ
 only after its gather has been waited on (`SlotExchange.acquire`), which orders the compute
 stream after the collective without a host sync.  The same class runs on `gloo` with CPU
 tensors, which is how tests/test_shard_gloo.py covers the N>1 path here.
+
+`CompactExchange` is the descriptor-sized form bench.py runs: the per-frame counts are gathered
+first, then each rank sends one contiguous block of its Σn descriptors (32 B each; padded at the tail
+to the largest block of the step, since RCCL's all-gather moves equal-sized blocks) instead of
+2024-slot padded keypoint + descriptor slots -- about 0.37x the bytes at C2.  The payload of step k
+is packed and gathered on a side stream one step later (the host needs step k's counts to size it),
+overlapping step k+1's extraction.
 """
 from __future__ import annotations
 
@@ -32,11 +39,12 @@ def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
 
 def cross_shard_predecessor(rank: int, world: int, frames_per_rank: int) -> int:
     """Index, in the gathered slot buffer (rank-major: rank r's local frame f at r*frames_per_rank + f),
-    of the predecessor of this rank's first frame: global frame g0 - 1, i.e. rank r-1's last frame
-    (wrapping to the job's last frame for rank 0).  §8d C5: "frame i matched to i-1"."""
+    of the predecessor of this rank's first frame: global frame g0 - 1, i.e. rank r-1's last frame.
+    Rank 0's first frame is global frame 0, which has no predecessor: -1 (the caller skips it).
+    §8d C5: "frame i matched to i-1"."""
     if world <= 0 or not (0 <= rank < world) or frames_per_rank <= 0:
         raise ValueError("bad shard arguments")
-    return (rank * frames_per_rank - 1) % (world * frames_per_rank)
+    return rank * frames_per_rank - 1 if rank > 0 else -1
 
 
 @dataclass
@@ -119,3 +127,142 @@ def unpack(slots: Slots):
     """Per-frame (keypoints[n], descriptors[n]) views, dropping the padding of every slot."""
     counts = slots.counts.cpu().tolist()
     return [(slots.kps[f, :n], slots.desc[f, :n]) for f, n in enumerate(counts)]
+
+
+class CompactExchange:
+    """Double-buffered ragged all-gather of every rank's descriptors (equal frame counts per rank).
+
+    Usage per step k (after enqueueing step k's extraction into `local(k)` on the current stream)::
+
+        ex.publish(k)        # counts all-gather of step k; then, for step k-1 (counts now on the
+                             # host): pack + payload all-gather on the side stream
+        ex.wait(k - 1)       # current stream waits for step k-1's payload (no host sync)
+
+    and `ex.drain()` at the end (finishes the last published step).  After wait(i), `block(i, r)` is
+    rank r's descriptors of step i as one [tot_r, 32] uint8 tensor (frame order), `frame(i, r, f)` one
+    frame's rows.  Works on CUDA (RCCL, side stream, events) and on CPU (gloo, synchronous).
+    """
+
+    def __init__(self, frames: int, cap: int, device, group=None, depth: int = 2):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.frames, self.cap, self.depth = frames, cap, depth
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.slots = [Slots.empty(frames, cap, device) for _ in range(depth)]
+        self.counts_all = [torch.zeros(self.world * frames, dtype=torch.int32, device=device) for _ in range(depth)]
+        pin = self.cuda
+        self.counts_host = [torch.zeros(self.world * frames, dtype=torch.int32, pin_memory=pin) for _ in range(depth)]
+        self.send = [torch.zeros((0, 32), dtype=torch.uint8, device=device) for _ in range(depth)]
+        self.recv = [torch.zeros((0, 32), dtype=torch.uint8, device=device) for _ in range(depth)]
+        self.maxtot = [0] * depth
+        self.tot = [[0] * self.world for _ in range(depth)]
+        self.pending = None   # step whose payload is not yet packed / gathered
+        self.side = torch.cuda.Stream(device=self.device) if self.cuda else None
+        self.ev_extract = [torch.cuda.Event() for _ in range(depth)] if self.cuda else None
+        self.ev_counts = [torch.cuda.Event() for _ in range(depth)] if self.cuda else None
+        self.ev_payload = [torch.cuda.Event() for _ in range(depth)] if self.cuda else None
+        self._timing = []            # (start, end) events around each payload all-gather, not yet read
+        self.gather_ms = []          # payload all-gather time per step (CUDA events)
+        self.payload_bytes = []      # gathered payload bytes per step (world x maxtot x 32)
+
+    def local(self, k: int) -> Slots:
+        return self.slots[k % self.depth]
+
+    def _side(self):
+        return torch.cuda.stream(self.side) if self.cuda else _NullCtx()
+
+    def publish(self, k: int) -> None:
+        i = k % self.depth
+        src = self.slots[i]
+        if self.cuda:
+            self.ev_extract[i].record()
+        with self._side():
+            if self.cuda:
+                self.side.wait_event(self.ev_extract[i])
+            if self.world > 1:
+                dist.all_gather_into_tensor(self.counts_all[i], src.counts, group=self.group)
+            else:
+                self.counts_all[i].copy_(src.counts)
+            self.counts_host[i].copy_(self.counts_all[i], non_blocking=self.cuda)
+            if self.cuda:
+                self.ev_counts[i].record(self.side)
+        if self.pending is not None:
+            self._payload(self.pending)
+        self.pending = k
+
+    def _payload(self, k: int) -> None:
+        i = k % self.depth
+        if self.cuda:
+            self.ev_counts[i].synchronize()
+        c = self.counts_host[i].view(self.world, self.frames).to(torch.int64)
+        tot = c.sum(1).tolist()
+        self.tot[i] = tot
+        maxtot = max(tot) if tot else 0
+        self.maxtot[i] = maxtot
+        mine = c[self.rank]
+        src = self.slots[i]
+        with self._side():
+            if self.send[i].shape[0] < maxtot:   # grown with headroom: a block rarely outgrows it again
+                self.send[i] = torch.zeros((maxtot + maxtot // 4, 32), dtype=torch.uint8, device=self.device)
+            if self.recv[i].shape[0] < self.world * maxtot:
+                self.recv[i] = torch.zeros((self.world * (maxtot + maxtot // 4), 32), dtype=torch.uint8,
+                                           device=self.device)
+            n = tot[self.rank]
+            if n:
+                # row r of the block: frame fr = the frame whose prefix range holds r, slot r - start[fr]
+                cnt = mine.to(self.device)
+                start = torch.cumsum(cnt, 0) - cnt
+                fr = torch.repeat_interleave(torch.arange(self.frames, device=self.device), cnt, output_size=n)
+                row = torch.arange(n, device=self.device) - start[fr]
+                torch.index_select(src.desc.view(-1, 32), 0, fr * self.cap + row, out=self.send[i][:n])
+            if self.cuda:
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record(self.side)
+            if self.world > 1:
+                dist.all_gather_into_tensor(self.recv[i][:self.world * maxtot], self.send[i][:maxtot], group=self.group)
+            else:
+                self.recv[i][:maxtot].copy_(self.send[i][:maxtot])
+            if self.cuda:
+                t1.record(self.side)
+                self._timing.append((t0, t1))
+                self.ev_payload[i].record(self.side)
+        self.payload_bytes.append(self.world * maxtot * 32)
+
+    def wait(self, k: int) -> None:
+        """Current stream waits for step k's payload (published one step earlier)."""
+        if self.cuda:
+            torch.cuda.current_stream(self.device).wait_event(self.ev_payload[k % self.depth])
+
+    def drain(self) -> None:
+        if self.pending is not None:
+            self._payload(self.pending)
+            self.wait(self.pending)
+            self.pending = None
+
+    def collect_gather_times(self) -> None:
+        """Adds the payload all-gather times of the steps gathered so far (CUDA; call after a sync)."""
+        for t0, t1 in self._timing:
+            self.gather_ms.append(t0.elapsed_time(t1))
+        self._timing = []
+
+    def counts(self, k: int) -> torch.Tensor:
+        return self.counts_host[k % self.depth].view(self.world, self.frames)
+
+    def block(self, k: int, r: int) -> torch.Tensor:
+        i = k % self.depth
+        return self.recv[i][r * self.maxtot[i]: r * self.maxtot[i] + self.tot[i][r]]
+
+    def frame(self, k: int, r: int, f: int) -> torch.Tensor:
+        c = self.counts(k)[r].to(torch.int64)
+        s0 = int(c[:f].sum())
+        return self.block(k, r)[s0: s0 + int(c[f])]
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-from orb_slam2_refactored_amd.shard import SlotExchange, Slots, cross_shard_predecessor, shard_range, unpack  # noqa: E402
+from orb_slam2_refactored_amd.shard import CompactExchange, SlotExchange, Slots, cross_shard_predecessor, shard_range, unpack  # noqa: E402
 
 FRAMES, CAP, STEPS = 3, 40, 5
 
@@ -70,25 +70,28 @@ def _worker(rank, world, port, errq):
         per_frame = unpack(g)
         assert len(per_frame) == world * FRAMES
         assert [int(k.shape[0]) for k, _ in per_frame] == g.counts.tolist()
-        # C5 cross-shard pairing (bench.py): this rank's first frame (global g0) is matched against the
-        # gathered slot of global frame g0 - 1, which is rank r-1's last local frame (rank 0 wraps to
-        # the job's last frame); the matcher reads it from the gathered buffer
+        # C5 cross-shard pairing: this rank's first frame (global g0) is matched against the gathered
+        # slot of global frame g0 - 1, rank r-1's last local frame; rank 0's first frame is global frame
+        # 0 and has no predecessor (-1)
         pred = cross_shard_predecessor(rank, world, FRAMES)
-        pr, pf = divmod(pred, FRAMES)
-        assert pr == (rank - 1) % world and pf == FRAMES - 1
-        assert shard_range(world * FRAMES, world, pr)[0] + pf == (start - 1) % (world * FRAMES)
-        want_prev = fake_slots(shard_range(world * FRAMES, world, pr)[0], STEPS - 1)
-        assert torch.equal(g.desc[pred], want_prev.desc[FRAMES - 1])
-        assert int(g.counts[pred]) == int(want_prev.counts[FRAMES - 1])
-        # the cross-shard match on the gathered data equals the match against the predecessor's own slots
-        import oracle_api as O
-        mine = fake_slots(start, STEPS - 1)
-        na, nb = int(mine.counts[0]), int(g.counts[pred])
-        a = mine.desc[0, :na].numpy()
-        got = O.bf_match(a, g.desc[pred, :nb].numpy())
-        exp = O.bf_match(a, want_prev.desc[FRAMES - 1, :nb].numpy())
-        for x, y in zip(got, exp):
-            assert (x == y).all()
+        if rank == 0:
+            assert pred == -1
+        else:
+            pr, pf = divmod(pred, FRAMES)
+            assert pr == rank - 1 and pf == FRAMES - 1
+            assert shard_range(world * FRAMES, world, pr)[0] + pf == start - 1
+            want_prev = fake_slots(shard_range(world * FRAMES, world, pr)[0], STEPS - 1)
+            assert torch.equal(g.desc[pred], want_prev.desc[FRAMES - 1])
+            assert int(g.counts[pred]) == int(want_prev.counts[FRAMES - 1])
+            # the cross-shard match on the gathered data equals the match against the predecessor's slots
+            import oracle_api as O
+            mine = fake_slots(start, STEPS - 1)
+            na, nb = int(mine.counts[0]), int(g.counts[pred])
+            a = mine.desc[0, :na].numpy()
+            got = O.bf_match(a, g.desc[pred, :nb].numpy())
+            exp = O.bf_match(a, want_prev.desc[FRAMES - 1, :nb].numpy())
+            for x, y in zip(got, exp):
+                assert (x == y).all()
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:  # pragma: no cover - reported by the parent
@@ -126,8 +129,8 @@ def test_shard_range_partitions():
 
 
 def test_cross_shard_predecessor():
-    assert cross_shard_predecessor(0, 1, 5) == 4
-    assert [cross_shard_predecessor(r, 4, 3) for r in range(4)] == [11, 2, 5, 8]
+    assert cross_shard_predecessor(0, 1, 5) == -1
+    assert [cross_shard_predecessor(r, 4, 3) for r in range(4)] == [-1, 2, 5, 8]
     with pytest.raises(ValueError):
         cross_shard_predecessor(2, 2, 3)
 
@@ -143,3 +146,83 @@ def test_single_process_exchange_is_copy():
     ex.drain()
     assert torch.equal(ex.gathered(i).desc, src.desc)
     assert torch.equal(ex.gathered(i).counts, src.counts)
+
+
+def _packed(s: Slots) -> torch.Tensor:
+    """A rank's descriptor block: every frame's first counts[f] rows, frame order."""
+    return torch.cat([s.desc[f, :int(s.counts[f])] for f in range(s.desc.shape[0])])
+
+
+def _compact_worker(rank, world, port, errq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        start, _ = shard_range(world * FRAMES, world, rank)
+        ex = CompactExchange(FRAMES, CAP, "cpu")
+
+        def check(k):   # step k has been gathered: every rank's block and the predecessor frame
+            for r in range(world):
+                r0, _ = shard_range(world * FRAMES, world, r)
+                want = fake_slots(r0, k)
+                assert torch.equal(ex.counts(k)[r], want.counts)
+                assert torch.equal(ex.block(k, r), _packed(want))
+                for f in range(FRAMES):
+                    assert torch.equal(ex.frame(k, r, f), want.desc[f, :int(want.counts[f])])
+            assert ex.payload_bytes[-1] == world * max(int(fake_slots(shard_range(world * FRAMES, world, r)[0], k)
+                                                           .counts.sum()) for r in range(world)) * 32
+            pred = cross_shard_predecessor(rank, world, FRAMES)
+            if rank > 0:
+                pr, pf = divmod(pred, FRAMES)
+                prev = fake_slots(shard_range(world * FRAMES, world, pr)[0], k)
+                assert torch.equal(ex.frame(k, pr, pf), prev.desc[pf, :int(prev.counts[pf])])
+
+        for k in range(STEPS):
+            loc = ex.local(k)
+            src = fake_slots(start, k)
+            loc.kps.copy_(src.kps)
+            loc.desc.copy_(src.desc)
+            loc.counts.copy_(src.counts)
+            ex.publish(k)
+            if k >= 1:
+                ex.wait(k - 1)
+                check(k - 1)
+        ex.drain()
+        check(STEPS - 1)
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # pragma: no cover - reported by the parent
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_compact_exchange_gloo(world):
+    """The ragged descriptor all-gather bench.py runs over RCCL: per step, every rank's Σn x 32 B block
+    (ragged counts incl. 0 and CAP) arrives intact, one step after publish, and the cross-shard
+    predecessor frame is read from it."""
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_compact_worker, args=(r, world, port, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_compact_exchange_single_process():
+    ex = CompactExchange(FRAMES, CAP, "cpu")
+    for k in range(3):
+        src = fake_slots(0, k)
+        loc = ex.local(k)
+        loc.desc.copy_(src.desc)
+        loc.counts.copy_(src.counts)
+        ex.publish(k)
+    ex.drain()
+    assert torch.equal(ex.block(2, 0), _packed(fake_slots(0, 2)))
