@@ -72,6 +72,7 @@ struct BADev {
     const double* cam;    // E x 5
     uint8_t* robust;      // E
     double* err;          // E x 3 (last computed error, g2o's _error)
+    const uint8_t* level; // E: g2o edge level; only level-0 edges take part (initializeOptimization(0))
     // active structure
     int Ea, np, nl, nblk;
     const int* act;       // Ea: edge id per active slot (ascending edge id)
@@ -214,6 +215,7 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
         for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
             const int k = b.pt_slot[u];
             const int e = b.act[k];
+            if (b.level[e]) continue;   // a level-1 edge (second optimize()): no error, no terms (J stays 0)
             const int pi = b.ek[e];
             const double* q4 = b.q + 4 * pi;
             double Xc[3], R[9];
@@ -1113,6 +1115,7 @@ __global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D, dou
         }
         for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
             const int e = b.act[b.pt_slot[u]];
+            if (b.level[e]) continue;   // g2o computes active errors only: a level-1 edge keeps its _error
             const int pi = b.ek[e];
             double Xc[3];
             se3_map(b.q + 4 * pi, b.t + 3 * pi, Xn, Xc);
@@ -1607,6 +1610,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     uint8_t* d_level = cs.take<uint8_t>(E);
     b.err = cs.take<double>(3 * (size_t)E);
     b.fixed = d_fixed; b.ep = d_ep; b.ek = d_ek; b.stereo = d_st; b.obs = d_obs; b.info = d_info; b.cam = d_cam;
+    b.level = d_level;
     b.ctl = C.ctlbuf.as<BACtl>();
     b.stop = stop_flag ? C.d_stop : nullptr;
     b.stop_after = stop_after;
@@ -1625,14 +1629,24 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     thread_local HostStructure hs;   // capacity kept across calls
     bool hook_stopped = false;   // the device ended a loop on the stop flag (or the test hook)
     // ------------------------------------------------------------------ one optimize(iters)
+    // The structure is built once, for the first optimize() (every edge at level 0).  The second
+    // optimize() (initializeOptimization(0) after the outliers went to level 1) reuses it: its active
+    // edges are a subset, the kernels skip level-1 edges (their J / W stay 0, so every sum, Schur block
+    // and dense factorisation sees exact zeros in their place), and a vertex left without active edges
+    // keeps a zero Hessian block (+ lambda), i.e. a zero update, as if it were not in the problem.
+    bool have_structure = false;
     auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
-        build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs);
-        mark("build_structure");
+        if (!have_structure) {
+            build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs);
+            mark("build_structure");
+        }
         const int Ea = (int)hs.act.size(), np = hs.np, nl = hs.nl, D = 6 * np;
         const int nblk = (int)hs.blk_i1.size();
         *iters_out = 0;
         *chi_out = 0;
-        if (Ea == 0 || np + nl == 0) return ORB_OK;
+        int n_active = 0;   // level-0 edges of this optimize()
+        for (int e = 0; e < E; e++) n_active += level[e] == 0;
+        if (Ea == 0 || n_active == 0 || np + nl == 0) return ORB_OK;
         // reduced system: in LDS up to 21 free keyframes (D <= 128), else in HBM (ba_solve_global_kernel)
         const bool glob = D > 128 || solve_lds_doubles(D) * 8 + 4096 > 160 * 1024;
         if (glob && np > ORBBA_MAX_FREE_KEYFRAMES) {
@@ -1646,8 +1660,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                               carve_size<int>(hs.ps_slot.size()) + carve_size<int>(np) + carve_size<int>(nblk) * 2 +
                               carve_size<int>(nblk + 1) + carve_size<int2>(hs.blk_pair.size());
         int rc2;
+        if (!have_structure) {
         if ((rc2 = C.structure.reserve(sbytes))) return rc2;
-        if ((rc2 = C.h_struct.ensure(sbytes))) return rc2;   // previous optimize() has synchronised
+        if ((rc2 = C.h_struct.ensure(sbytes))) return rc2;
         Carve cr{C.structure.as<char>()}, hr{C.h_struct.ptr};
         auto put = [&](const void* src, size_t n, char* hdst) {
             if (n) std::memcpy(hdst, src, n);
@@ -1683,6 +1698,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.act = d_act; b.hp = d_hp; b.hl = d_hl; b.pt_beg = d_ptb; b.pt_slot = d_pts; b.pt_id = d_pti;
         b.ps_beg = d_psb; b.ps_slot = d_pss; b.ps_id = d_psi; b.blk_i1 = d_b1; b.blk_i2 = d_b2; b.blk_beg = d_bb;
         b.blk_pair = d_bp;
+        have_structure = true;
+        }
         // system buffers
         const size_t ybytes = carve_size<double>(72 * (size_t)Ea) + carve_size<double>(24 * (size_t)Ea) +
                               carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +

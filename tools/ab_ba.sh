@@ -9,7 +9,7 @@ rc=$?
 tail -3 gpurun_out/abba_pytest.log
 [ $rc -ne 0 ] && exit $rc
 for i in 1 2 3; do
-  ORBSLAM2_AMD_LIB=$PWD/tools/ab/lib_base.so timeout -k 10 60 python tools/babench.py 40 2>&1 | grep LocalBA | sed 's/^/base: /'
+  ORBSLAM2_AMD_LIB=$PWD/tools/ab/lib_head.so timeout -k 10 60 python tools/babench.py 40 2>&1 | grep LocalBA | sed 's/^/base: /'
   timeout -k 10 60 python tools/babench.py 40 2>&1 | grep LocalBA | sed 's/^/new:  /'
   if [ -f tools/ab/lib_c.so ]; then
     ORBSLAM2_AMD_LIB=$PWD/tools/ab/lib_c.so timeout -k 10 60 python tools/babench.py 40 2>&1 | grep LocalBA | sed 's/^/c:    /'
