@@ -100,6 +100,20 @@ def measured_traffic(stage, frames, W, H, nfeat):
     return None
 
 
+def measured_traffic_step(breakdown, brk_steps, frames, W, H, nfeat):
+    """Measured HBM bytes per step of every profiled extractor stage (measured_traffic x launches per
+    step), or None when a stage of this workload has no committed profile."""
+    tot = 0.0
+    for stage, (ms, launches) in breakdown.items():
+        if stage not in STAGE_KERNEL:
+            continue
+        t = measured_traffic(stage, frames, W, H, nfeat)
+        if t is None:
+            return None
+        tot += t * launches / max(brk_steps, 1)
+    return tot
+
+
 def cpu_info():
     model = None
     try:
@@ -160,8 +174,10 @@ def cpu_baseline_block(unit, sample, single, multi, info):
             "sample": f"{sample}; {nN} units on {info['threads_all']} threads, oracle/orb_oracle.cpp (-O3)",
             "single_thread": {"value": v1, "cores": 1, "units": n1}, "cpu_model": info["cpu_model"],
             "nproc": info["nproc"], "usable_cpus": info["usable_cpus"],
-            "cores_note": "16 threads = the CPU share of this pool's one-GPU box (OMP_NUM_THREADS / MAX_JOBS are 16 "
-                          "there); nproc / affinity report the whole machine's CPUs, which the box does not own"}
+            "cores_note": "16 threads = the CPU share of this pool's one-GPU box: the box runs one GPU of an 8-GPU "
+                          "host and sets OMP_NUM_THREADS / MAX_JOBS to 16; nproc / affinity report the whole "
+                          "host's CPUs, shared with the other GPUs' jobs, so an all-cores run would measure "
+                          "contention, not this port"}
 
 
 def event_ms(fn, steps, stream):
@@ -554,6 +570,69 @@ def motion_projection_leg(dev, base, b, frames, steps, cpu):
     return r
 
 
+def reloc_leg(dev, frames=256, steps=10, cpu=True):
+    """Relocalisation SearchByProjection(Frame&, KeyFrame*, alreadyFound, th 10, ORBdist 100)
+    (ORBmatcher.cc:1364-1445, Tracking.cc:403): 256 (frame, candidate keyframe) pairs, 2000 keypoints and
+    600 keyframe points each, CheckOrientation on."""
+    import torch
+    from orb_slam2_refactored_amd.matcher import search_by_projection_reloc_device
+    from orb_slam2_refactored_amd.synth import make_reloc_batch, tile_ragged_batch
+    b = tile_ragged_batch(make_reloc_batch(41, n_frames=16, n_kp=2000, n_mp=600), frames // 16)
+    d = {k: (torch.from_numpy(np.ascontiguousarray(v)).to(dev) if isinstance(v, np.ndarray) and k != "scale_factors"
+             else v) for k, v in b.items()}
+    km, nm = search_by_projection_reloc_device(d)
+    torch.cuda.synchronize()
+    ms = event_ms(lambda: search_by_projection_reloc_device(d, km, nm), steps, torch.cuda.current_stream())
+    r = {"workload": f"{frames} (frame, keyframe) pairs x (2000 keypoints, 600 keyframe points), th 10, ORBdist 100, "
+                     "projection + invariance gate + PredictScale + claim walk, CheckOrientation on",
+         "pairs_per_s": frames / (ms * 1e-3), "ms_per_step": ms, "mean_matches": float(nm.double().mean().item())}
+    if cpu:
+        O = oracle()
+        b8 = make_reloc_batch(42, n_frames=8, n_kp=2000, n_mp=600)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 3.0 or n < 8:
+            O.search_by_projection_reloc(b8)
+            n += 8
+        r["cpu_baseline"] = {"pairs_per_s": n / (time.perf_counter() - t0), "cores": 1, "kind": "port",
+                             "sample": "8-pair batches, oracle/orb_oracle.cpp, 1 thread"}
+    return r
+
+
+def init_leg(dev, pairs=64, steps=10, cpu=True):
+    """SearchForInitialization(F1, F2, prevMatched, matches12, windowSize 100) with ORBmatcher(0.9, true)
+    (ORBmatcher.cc:614-694, Tracking.cc:1050-1052): 64 pairs of 4000-keypoint frames.  prevMatched is
+    updated in place by each call, so every timed call first restores it (one 2 x 4 B x 256k device copy,
+    inside the timing)."""
+    import torch
+    from orb_slam2_refactored_amd.matcher import search_for_initialization_device
+    from orb_slam2_refactored_amd.synth import make_init_batch, tile_ragged_batch
+    b = tile_ragged_batch(make_init_batch(43, n_pairs=8), pairs // 8)
+    d = {k: (torch.from_numpy(np.ascontiguousarray(v)).to(dev) if isinstance(v, np.ndarray) else v)
+         for k, v in b.items()}
+    pm0 = d["prev_matched"].clone()
+    m12, nm = search_for_initialization_device(d)
+    torch.cuda.synchronize()
+
+    def call():
+        d["prev_matched"].copy_(pm0)
+        search_for_initialization_device(d, m12, nm)
+    ms = event_ms(call, steps, torch.cuda.current_stream())
+    r = {"workload": f"{pairs} pairs x (4000 + 4000 keypoints), window 100, nnratio 0.9, CheckOrientation on",
+         "pairs_per_s": pairs / (ms * 1e-3), "ms_per_step": ms, "mean_matches": float(nm.double().mean().item())}
+    if cpu:
+        O = oracle()
+        b4 = make_init_batch(44, n_pairs=4)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 3.0 or n < 4:
+            O.search_for_initialization(b4)
+            n += 4
+        r["cpu_baseline"] = {"pairs_per_s": n / (time.perf_counter() - t0), "cores": 1, "kind": "port",
+                             "sample": "4-pair batches, oracle/orb_oracle.cpp, 1 thread"}
+    return r
+
+
 def bow_leg(dev, local, frames=128, n=2000, steps=10, cpu=True):
     """§8f row 4: ORBVocabulary::transform(desc, BowVector, FeatureVector, 4) on an ORBvoc-shaped
     synthetic tree (k 10, L 6, 1.1 M nodes)."""
@@ -775,6 +854,18 @@ def main():
     ex.profile(False)
     breakdown = ex.profile_read()
     brk_steps = 3
+    # the matcher alone (3 calls on the last step's descriptors), for its FP4 roofline
+    match_ms = 0.0
+    if B > 1:
+        sl = single if xchg is None else xchg.local(0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(3):
+            m.match_batch_device(sl.desc[1:], sl.counts[1:], sl.desc, sl.counts, out=match_out[:, 1:], stream=stream,
+                                 pair_b=prev_idx)
+        e1.record(stream)
+        e1.synchronize()
+        match_ms = e0.elapsed_time(e1) / 3
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -797,7 +888,9 @@ def main():
     dom_bytes = sb[dom] * B / max(launches_per_step, 1)
     achieved = dom_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
     traffic = measured_traffic(dom, B, W, H, args.nfeatures)
-    extract_ms = sum(v[0] for v in breakdown.values()) / brk_steps
+    extract_ms = sum(v[0] for k, v in breakdown.items() if k in STAGE_KERNEL) / brk_steps
+    pipe_traffic = measured_traffic_step(breakdown, brk_steps, B, W, H, args.nfeatures)
+    match_tflops = 512.0 * n_kp * n_kp * (B - 1) / (match_ms * 1e-3) / 1e12 if match_ms else 0.0
 
     result = {
         "metric": METRIC,
@@ -826,7 +919,17 @@ def main():
                      "stage_ms_per_step": {k: v[0] / brk_steps for k, v in breakdown.items()},
                      "stage_ms_source": "separate 3-step pass with launch events on every kernel",
                      "pipeline_algorithmic_GBs": bytes_frame * B / (extract_ms * 1e-3) / 1e9 if extract_ms else 0.0,
-                     "pipeline_bytes_per_frame": bytes_frame},
+                     "pipeline_bytes_per_frame": bytes_frame,
+                     # the whole step (extract + match + host plumbing) against the extractor's algorithmic bytes
+                     "pipeline_GBs_from_ms_per_step": bytes_frame * B / (ms_per_step * 1e-3) / 1e9,
+                     "pipeline_frac": bytes_frame * B / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "pipeline_traffic_per_step": pipe_traffic,
+                     "pipeline_traffic_over_algorithmic": pipe_traffic / (bytes_frame * B) if pipe_traffic else None},
+        # the brute-force matcher's FP4 MFMA path: every query x candidate pair is a 256-bit dot product
+        "match_roofline": {"bound": "mfma", "kernel": "match (FP4 tiles)", "achieved": match_tflops,
+                           "peak": FP4_PEAK_TFLOPS, "unit": "TFLOP/s (FP4)", "frac": match_tflops / FP4_PEAK_TFLOPS,
+                           "ops": "512 FP4 flops per query x candidate pair, n_kp^2 pairs per matched frame (B - 1 per step)",
+                           "match_ms_per_step": match_ms},
         "keypoints_per_frame": n_kp,
         "matches_last_step": matches,
         "device_fault_mask": fault,
@@ -871,6 +974,8 @@ def main():
         result["stereo"] = stereo_leg(dev, local)
     if legs and not args.no_projection:
         result["search_by_projection"] = projection_leg(dev, cpu=cpu)
+        result["search_by_projection"]["relocalisation"] = reloc_leg(dev, cpu=cpu)
+        result["search_for_initialization"] = init_leg(dev, cpu=cpu)
     if legs and not args.no_bow:
         result["bow"] = bow_leg(dev, local, cpu=cpu)
     if legs and not args.no_pose:

@@ -71,9 +71,17 @@ struct Geom {
     long long slot_frame;     // candidate slots per frame (sum of per-cell capacities)
     long long cand_frame;     // contiguous candidate entries per frame
     int out_frame;            // selected keypoints per frame (sum of out_cap)
-    int nfeat_unused;
+    unsigned of_m;            // n / out_frame = (t + ((n - t) >> of_s1)) >> of_s2, t = mulhi(n, of_m)
+    int of_s1, of_s2;         // (round-up magic, exact for every n < 2^31; divmod_of)
     LevelDev lv[MAX_LEVELS];
 };
+
+// n / g.out_frame for 0 <= n < 2^31 by the host's round-up magic (scalar multiply-high, no
+// reciprocal round trip): the describe grid is out_frame selection slots per frame.
+__device__ __forceinline__ int divmod_of(const Geom& g, int n) {
+    const unsigned t = __umulhi((unsigned)n, g.of_m);
+    return (int)((t + (((unsigned)n - t) >> g.of_s1)) >> g.of_s2);
+}
 
 struct CellDev {
     int level;
@@ -2024,17 +2032,14 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
     const float k = (float)(180 / M_PI);
     const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
     const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    // the reference's two branches (ax >= ay: ay / ax, else 90 - f(ax / ay)) with one division:
+    // the same operations on the same operands
     const float ax = fabsf(x), ay = fabsf(y);
-    float a, c, c2;
-    if (ax >= ay) {
-        c = ay / (ax + (float)DBL_EPSILON);
-        c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        c = ax / (ay + (float)DBL_EPSILON);
-        c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
+    const bool xm = ax >= ay;
+    const float c = (xm ? ay : ax) / ((xm ? ax : ay) + (float)DBL_EPSILON);
+    const float c2 = c * c;
+    float a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    if (!xm) a = 90.f - a;
     if (x < 0) a = 180.f - a;
     if (y < 0) a = 360.f - a;
     return a;
@@ -2103,24 +2108,33 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     static_assert(47 * RS + 64 <= 48 * HBS * 2, "R (and the blur's reads of rows 43..47) must fit in Hb");
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
-    const int f = lb / gridDim.x;
-    const int s = lb % gridDim.x;   // selection slot (level-major, out_cap slots per level)
-    int l = 0;
-    while (l + 1 < g.nlevels && s >= g.lv[l + 1].out_base) l++;
+    const int f = divmod_of(g, lb);
+    const int s = lb - f * g.out_frame;   // selection slot (level-major, out_cap slots per level)
+    // The slot's level and the frame's per-level counts without a dependent chain of loads: the
+    // level is the number of level starts (kernarg) <= s; one vector load brings level q's kept
+    // count to lane q < nlevels and the slot's keypoint word to lane 63, and the level's output base
+    // is an inclusive row scan of the counts (nlevels <= 16: lanes 0-15).
+    const int nl = g.nlevels;
+    const int* lp = lane < nl ? sel_cnt + f * nl + lane
+                              : reinterpret_cast<const int*>(sel + (long long)f * g.out_frame + s);
+    const int cw = (lane < nl || lane == 63) ? *lp : 0;
+    const int cq = lane < nl ? cw : 0;
+    int l = 0;   // levels >= nlevels carry out_base INT_MAX (host); out_base >= 1 above level 0
+#pragma unroll
+    for (int q = 1; q < MAX_LEVELS; q++) l += (int)((unsigned)(g.lv[q].out_base - 1 - s) >> 31);
+    int sc = cq;
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xf, 0xf, true);   // row_shr:1 (zero fill)
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);   // row_shr:2
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xf, 0xf, true);   // row_shr:4
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x118, 0xf, 0xf, true);   // row_shr:8
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane(cw, 63);
+    const int total = __builtin_amdgcn_readlane(sc, 15);
+    const int lbase = l > 0 ? __builtin_amdgcn_readlane(sc, l - 1) : 0;
+    const int cnt_l = __builtin_amdgcn_readlane(cq, l);
     const LevelDev& L = g.lv[l];
-    // the slot's keypoint and the frame's per-level counts in one round trip (both addresses are
-    // known from the slot)
-    const uint32_t k = sel[(long long)f * g.out_frame + s];
-    const int* cnt = sel_cnt + f * g.nlevels;
-    int total = 0, lbase = 0;
-    for (int q = 0; q < g.nlevels; q++) {
-        const int c = cnt[q];
-        total += c;
-        if (q < l) lbase += c;
-    }
     if (s == 0 && lane == 0) counts[f] = total;
     const int i = s - L.out_base;
-    if (i >= cnt[l]) return;   // slot past the level's kept count
+    if (i >= cnt_l) return;   // slot past the level's kept count
     const int oidx = lbase + i;   // output order: level-major list order
     if (oidx >= cap) return;
     DESC_STAMP(0);
@@ -2268,9 +2282,10 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     DESC_STAMP(4);
     auto sample = [&](int idx) -> int {
         const float x = c_pattern[2 * idx], y = c_pattern[2 * idx + 1];
-        const int dy = (int)rintf(x * b + y * a);
-        const int dx = (int)rintf(x * a - y * b);
-        const uint16_t* col = Hb + __mul24(18 + dy, HBS) + 18 + dx;
+        // byte offset of blurred pixel (18 + dy, 18 + dx) from the rounded floats (exact integers)
+        const float dy = rintf(x * b + y * a), dx = rintf(x * a - y * b);
+        const int ob = (int)fmaf(dy, (float)(2 * HBS), fmaf(dx, 2.f, (float)(2 * (18 * HBS + 18))));
+        const uint16_t* col = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(Hb) + ob);
         // vertical taps as u16 pairs (d16 / d16_hi loads) into v_dot2_u32_u16, rounding bias as the
         // accumulator: 18 c0 + 34 c1 + 48 c2 + 56 c3 + 48 c4 + 34 c5 + 18 c6 + 2^15
         const us2 p01 = {col[0], col[HBS]}, p23 = {col[2 * HBS], col[3 * HBS]}, p45 = {col[4 * HBS], col[5 * HBS]};
@@ -2406,6 +2421,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     Geom g;
     std::memset(&g, 0, sizeof(g));
     g.nlevels = Lc;
+    for (int l = Lc; l < MAX_LEVELS; l++) g.lv[l].out_base = INT_MAX;   // describe's level count
     std::vector<int2> xtab, ytab;
     std::vector<CellDev> cells;
     long long pyr_off = 0, slot = 0, cand = 0;
@@ -2527,6 +2543,14 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.slot_frame = std::max<long long>(slot, 1);
     g.cand_frame = std::max<long long>(cand, 1);
     g.out_frame = std::max(out, 1);
+    {   // round-up magic for n / out_frame (Granlund-Montgomery; d = 1: t = 0, shifts 0)
+        const unsigned d = (unsigned)g.out_frame;
+        int lg = 0;
+        while ((1ull << lg) < d) lg++;
+        g.of_m = (unsigned)((((1ull << lg) - d) << 32) / d + 1);
+        g.of_s1 = lg > 0 ? 1 : 0;
+        g.of_s2 = lg > 0 ? lg - 1 : 0;
+    }
     NC = (int)align_up(std::max(NC, 256), 64);   // >= blockDim: the gather reuses the node scratch
     if (h->debug_nc > 0) NC = (int)align_up(std::max(h->debug_nc, 256), 64);
     // PTC: candidate points kept in LDS (P and T) when a level has at most this many (more: HBM).

@@ -364,6 +364,23 @@ def tile_proj_batch(b: dict, reps: int) -> dict:
     return out
 
 
+def tile_ragged_batch(b: dict, reps: int) -> dict:
+    """`reps` copies of a ragged batch back to back (a large batch without regenerating).  Every
+    `*_begin` array (n + 1 prefix offsets) is re-prefixed; an array whose length equals the total of
+    one prefix, or the number of batch entries, is repeated; other values (scalars, host tables such
+    as scale_factors) are kept."""
+    out = dict(b)
+    begins = {k: v for k, v in b.items() if k.endswith("_begin")}
+    n = len(next(iter(begins.values()))) - 1
+    totals = {int(v[-1]) for v in begins.values()}
+    for k, v in b.items():
+        if k in begins:
+            out[k] = np.concatenate([[0], np.cumsum(np.tile(np.diff(v), reps))]).astype(v.dtype)
+        elif isinstance(v, np.ndarray) and v.ndim >= 1 and k != "scale_factors" and (len(v) in totals or len(v) == n):
+            out[k] = np.concatenate([v] * reps)
+    return out
+
+
 def make_vocabulary(seed: int = 0, k: int = 10, L: int = 4, scoring: int = 0, weighting: int = 0,
                     early_leaf: float = 0.05, stop_frac: float = 0.03, order: str = "bfs"):
     """A synthetic DBoW2 ORB vocabulary (the real ORBvoc.txt is not available offline).

@@ -1,0 +1,33 @@
+"""Descriptor determinism probe: the same batch extracted repeatedly (and with ORBX_FAST_SPEC 0 / 1 / 8)
+must give identical keypoints and descriptors; prints the rows that differ (level, x, y, bits)."""
+import os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
+from test_extractor_gpu import _patchwork as patchwork, make
+
+
+frames = np.stack([patchwork(40 + i, 320, 240) for i in range(24)])
+t = torch.from_numpy(frames).cuda()
+outs = []
+for spec in (0, 0, 0, 1, 8):
+    os.environ["ORBX_FAST_SPEC"] = str(spec)
+    ex = make(500)
+    o = ex.extract_batch_device(t)
+    torch.cuda.synchronize()
+    outs.append([x.cpu().numpy() for x in o])
+cnt = outs[0][2]
+bad = 0
+for r, o in enumerate(outs[1:], 1):
+    assert np.array_equal(cnt, o[2]), r
+    for i, n in enumerate(cnt):
+        kd = ~np.all(outs[0][0][i, :n] == o[0][i, :n], axis=1)
+        dd = ~np.all(outs[0][1][i, :n] == o[1][i, :n], axis=1)
+        for j in np.nonzero(kd | dd)[0][:4]:
+            bad += 1
+            kp = outs[0][0][i, j]
+            print(f"run {r} frame {i} row {j}/{n}: kp_diff={bool(kd[j])} kp={kp.tolist()} "
+                  f"bits_diff={int(np.unpackbits(outs[0][1][i, j] ^ o[1][i, j]).sum())}")
+print("differences:", bad)
+sys.exit(1 if bad else 0)
