@@ -435,7 +435,10 @@ __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
 // part of a block to count in adds the partials in part order and writes the block of S.  Part 0
 // also adds Hpp + lambda I and does the diagonal blocks' extras.
 constexpr int SB_G = 28;
-constexpr int SB_SPLIT = 8;
+#ifndef SB_SPLIT_DEF
+#define SB_SPLIT_DEF 2
+#endif
+constexpr int SB_SPLIT = SB_SPLIT_DEF;
 __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, int accum) {
     BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
@@ -559,12 +562,17 @@ __host__ __device__ constexpr size_t solve_lds_doubles(int D) {
     return (size_t)solve_dp(D) * (solve_dp(D) + 1) + 3 * (size_t)solve_dp(D);
 }
 
-__device__ __forceinline__ double rcp_d(double d) {   // 1/d to ~1 ulp: v_rcp_f64 + two Newton steps
+#ifndef ORBBA_NEWTON
+#define ORBBA_NEWTON 2
+#endif
+__device__ __forceinline__ double rcp_d(double d) {   // 1/d: v_rcp_f64 + ORBBA_NEWTON Newton steps
     double r = __builtin_amdgcn_rcp(d);
-    double e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-d, r, 1.0);
-    return fma(r, e, r);
+#pragma unroll
+    for (int k = 0; k < ORBBA_NEWTON; k++) {
+        const double e = fma(-d, r, 1.0);
+        r = fma(r, e, r);
+    }
+    return r;
 }
 
 // A_ik -= sum_j U_ij dinv_j U_kj for the NBK x NBK lower block-triangle below block J.
@@ -680,7 +688,10 @@ __device__ __forceinline__ bool solve_diag_block(double* A, double* y, double* d
     double rc = rcp_d(dj);
     // 16 pivot steps, unrolled with the next pivot's broadcast + reciprocal interleaved into the
     // current step's broadcast-FMAs (tools/gen_ba_diag.py)
-#include "orbba_diag.inc"
+#ifndef ORBBA_DIAG_INC
+#define ORBBA_DIAG_INC "orbba_diag.inc"
+#endif
+#include ORBBA_DIAG_INC
     if (lane < SB) {
         dinv[J0 + i] = rci;
         y[J0 + i] = yi;
