@@ -200,6 +200,10 @@ def lib():
             raise OrbError(f"{LIB_PATH} not found — build it with `python -c 'import __graft_entry__ as g; g.build()'`")
         l = C.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
+            # an A/B build named by ORBSLAM2_AMD_LIB may predate newer entry points: those stay
+            # unbound (calling one fails); the in-tree library must export every symbol
+            if os.environ.get("ORBSLAM2_AMD_LIB") and not hasattr(l, name):
+                continue
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args

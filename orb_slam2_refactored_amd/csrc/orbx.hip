@@ -868,11 +868,12 @@ __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint
 #define FAST_WAVES_DEF 6
 #endif
 __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
+                                                        const int2* __restrict__ strips,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
-                                                        int n_items, int cpw, int cell_beg, int ncell, int spec_min) {
+                                                        int strip_beg, int nstrips, int spec_min) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -884,18 +885,12 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x, gridDim.x);
     FAST_STAMP(0, __builtin_amdgcn_s_memtime());
-    const int i_beg = lb * cpw, i_end = min(i_beg + cpw, n_items);
-    // item i = f * ncell + (cell - cell_beg): this launch covers cells [cell_beg, cell_beg + ncell)
-    // (frame, cell) of this wavefront's items: one division for the first, then stepped
-    int src_f = i_beg / ncell, src_c = cell_beg + i_beg - src_f * ncell;
-    auto source = [&](int item, CellDev& cd, int& f, int& ci) {
-        (void)item;
-        f = src_f;
-        ci = src_c;
-        if (++src_c == cell_beg + ncell) {
-            src_c = cell_beg;
-            src_f++;
-        }
+    // wavefront = (frame, column strip): up to fast_cpw vertically consecutive cells of one column
+    const int f = lb / nstrips;
+    const int2 sd = strips[strip_beg + lb - f * nstrips];
+    const int i_beg = 0, i_end = sd.y & 255, cstride = sd.y >> 8;
+    auto source = [&](int item, CellDev& cd, int& ci) {
+        ci = sd.x + item * cstride;
         cd = cells[ci];
         CropSrc c;
         c.img = level_base(g, cd.level, f, in, in_fstride, in_step, pyr, &c.step);
@@ -906,16 +901,16 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         c.h = g.lv[cd.level].h;
         return c;
     };
-    // Speculative iniThFAST pass: a cell whose predecessor in this wavefront (the neighbouring cell
-    // of the same level row) kept >= spec_min corners at iniThFAST is first run with the pre-test,
+    // Speculative iniThFAST pass: a cell whose predecessor in this wavefront (the cell above it in
+    // the same column) kept >= spec_min corners at iniThFAST is first run with the pre-test,
     // the diagonal filter and the corner list at iniThFAST only.  When the NMS keeps one of them
     // that is DetectFAST's answer (:527); otherwise the cell is re-run at min(ini, min).  On
     // texture-rich frames most pixels pass at minThFAST but few at iniThFAST.
     int prev_ini = 0;
     for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
-    int f, ci;
-    const CropSrc src = source(item, cell, f, ci);
+    int ci;
+    const CropSrc src = source(item, cell, ci);
     const int x0 = src.x0, y0 = src.y0;
     const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
     {
@@ -2369,6 +2364,8 @@ struct orbx_extractor {
     hipStream_t lvl_side = nullptr;
     hipEvent_t lvl_fork = nullptr, lvl_join = nullptr;
     DevBuf d_cells, d_xtab, d_ytab;
+    DevBuf d_strips;                 // FAST work items: column strips of cells (fast_cells_kernel)
+    std::vector<int> strip_beg;      // first strip of each level (nlevels + 1 entries)
 
     // workspace for up to ws_frames frames
     int ws_frames = 0;
@@ -2590,6 +2587,34 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         ORB_HIP_TRY(hipMemcpy(h->d_ytab.ptr, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice));
     h->geom = g;
     h->cells = cells;
+    {   // FAST column strips: up to fast_cpw vertically consecutive cells of one column per wavefront
+        // (the speculation hint comes from the cell above); consecutive strips are neighbouring
+        // columns of the same row block, so the wavefronts running together read adjacent crops
+        // and share their cache lines (rows of one level all have the same cell count).
+        std::vector<int2> strips;
+        h->strip_beg.assign(g.nlevels + 1, 0);
+        const int cpw = std::max(1, std::min(h->fast_cpw, 255));
+        for (int l = 0; l < g.nlevels; l++) {
+            h->strip_beg[l] = (int)strips.size();
+            const LevelDev& L = g.lv[l];
+            if (L.ncells <= 0) continue;
+            const int x00 = cells[L.cell_base].x0y0 & 0xffff;
+            int ncx = 0;
+            while (ncx < L.ncells && (cells[L.cell_base + ncx].x0y0 >> 16) == (cells[L.cell_base].x0y0 >> 16)) ncx++;
+            const int ncy = L.ncells / ncx;
+            if (ncx * ncy != L.ncells || (cells[L.cell_base + ncx - 1].x0y0 & 0xffff) < x00) {
+                set_error("FAST cell grid is not a rectangle");
+                return ORB_EINTERNAL;
+            }
+            for (int rb = 0; rb < ncy; rb += cpw)
+                for (int cx = 0; cx < ncx; cx++)
+                    strips.push_back(make_int2(L.cell_base + rb * ncx + cx, std::min(cpw, ncy - rb) | (ncx << 8)));
+        }
+        h->strip_beg[g.nlevels] = (int)strips.size();
+        if ((rc = h->d_strips.reserve(std::max<size_t>(1, strips.size()) * sizeof(int2)))) return rc;
+        if (!strips.empty())
+            ORB_HIP_TRY(hipMemcpy(h->d_strips.ptr, strips.data(), strips.size() * sizeof(int2), hipMemcpyHostToDevice));
+    }
     {
         int mzw = 1, mzh = 1;
         for (const CellDev& c : cells) { mzw = std::max(mzw, c.zwzh & 0xffff); mzh = std::max(mzh, c.zwzh >> 16); }
@@ -2686,13 +2711,12 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     uint32_t* sel = h->d_sel.as<uint32_t>() + (long long)f0 * g.out_frame;
     int* selcnt = h->d_selcnt.as<int>() + (long long)f0 * g.nlevels;
     uint32_t* fault = h->d_fault.as<uint32_t>();
-    auto fast = [&](int cb, int nc, hipStream_t s) {
-        if (nc <= 0) return;
-        const int n_items = nc * F;
-        const int cpw = h->fast_cpw;
-        launch_timed(h, 1, fast_cells_kernel, dim3((unsigned)((n_items + cpw - 1) / cpw)), dim3(64), (uint32_t)h->fast_lds, s,
-                           g, h->d_cells.as<CellDev>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
-                           h->p.minThFAST, slots, cellcnt, fault, h->fl, n_items, cpw, cb, nc, h->fast_spec);
+    auto fast = [&](int l0, int l1, hipStream_t s) {   // levels [l0, l1)
+        const int sb = h->strip_beg[l0], ns = h->strip_beg[l1] - sb;
+        if (ns <= 0) return;
+        launch_timed(h, 1, fast_cells_kernel, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
+                           g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
+                           h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
@@ -2721,20 +2745,20 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         // stream builds levels 1..7 (latency-bound cascade) and runs their FAST / quadtree, so the
         // level-0 tree's serial rounds overlap the FAST work of the other levels.
         (void)hipStreamWaitEvent(side, h->lvl_fork, 0);
-        fast(0, nc0, side);
+        fast(0, 1, side);
         quadtree(0, 1, side);
         (void)hipEventRecord(h->lvl_join, side);
         {
             for (int l = 1; l < g.nlevels; l++) l += pyramid(l);
         }
-        fast(nc0, g.ncells_total - nc0, st);
+        fast(1, g.nlevels, st);
         quadtree(1, g.nlevels - 1, st);
         (void)hipStreamWaitEvent(st, h->lvl_join, 0);
     } else {
         {
             for (int l = 1; l < g.nlevels; l++) l += pyramid(l);
         }
-        fast(0, g.ncells_total, st);
+        fast(0, g.nlevels, st);
         quadtree(0, g.nlevels, st);
     }
     {
@@ -2831,7 +2855,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
 int orbx_destroy(orbx_extractor* h) {
     if (!h) return ORB_OK;
     (void)hipSetDevice(h->device);
-    DevBuf* bufs[] = {&h->d_cells, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
+    DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
                       &h->d_counts, &h->d_stereo_sad};
     for (DevBuf* b : bufs) b->release();
