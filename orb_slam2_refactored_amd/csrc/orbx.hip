@@ -867,6 +867,10 @@ __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint
 #ifndef FAST_WAVES_DEF
 #define FAST_WAVES_DEF 6
 #endif
+// CST / ZST: the crop and zone-map row strides when known at compile time (the C1-C3 geometries:
+// 48 / 36 and 52 / 40), so every LDS address off a row base folds into the instruction's offset
+// field; 0 = read them from FastLds (any other geometry).
+template <int CST, int ZST>
 __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                         const int2* __restrict__ strips,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
@@ -880,7 +884,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     short* queue = reinterpret_cast<short*>(Mz + fl.mz_bytes);
     short* clist = queue + fl.qcap;
     unsigned long long* bal = reinterpret_cast<unsigned long long*>(clist + fl.ccap);
-    const int CSd = fl.CS, ZSd = fl.ZS;
+    const int CSd = CST ? CST : fl.CS, ZSd = ZST ? ZST : fl.ZS;
 
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -2714,7 +2718,11 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     auto fast = [&](int l0, int l1, hipStream_t s) {   // levels [l0, l1)
         const int sb = h->strip_beg[l0], ns = h->strip_beg[l1] - sb;
         if (ns <= 0) return;
-        launch_timed(h, 1, fast_cells_kernel, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
+        const FastLds& fl = h->fl;
+        auto kern = fl.CS == 48 && fl.ZS == 36   ? fast_cells_kernel<48, 36>
+                    : fl.CS == 52 && fl.ZS == 40 ? fast_cells_kernel<52, 40>
+                                                 : fast_cells_kernel<0, 0>;
+        launch_timed(h, 1, kern, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
                            h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec);
     };

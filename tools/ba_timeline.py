@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
 """Print the LocalBA kernel timeline of the last call in a rocprofv3 kernel trace directory."""
+import re
 import csv
 import sys
 from pathlib import Path
@@ -15,7 +16,7 @@ t0 = int(seq[0]["Start_Timestamp"])
 prev = t0
 tot = {}
 for r in seq:
-    n = r["Kernel_Name"].split("(")[0].replace("orbamd::", "")
+    n = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].replace("orbamd::", "").replace("void ", ""))
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     if len(sys.argv) > 2:
         print(f"{n:28s} start {(s - t0) / 1e3:8.1f} gap {(s - prev) / 1e3:6.1f} dur {(e - s) / 1e3:7.1f}")

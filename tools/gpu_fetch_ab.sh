@@ -17,7 +17,7 @@ v = sys.argv[1]
 acc = collections.defaultdict(list)
 for f in glob.glob(f"gpurun_out/fetch_ab/{v}/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        n = r["Kernel_Name"].split("(")[0].replace("orbamd::", "")
+        n = r["Kernel_Name"].split("(")[0].replace("orbamd::", "").replace("void ", "").split("<")[0]
         acc[n].append(float(r["Counter_Value"]))
 print(v, {k: round(sum(x) / len(x) / 1e9, 3) for k, x in acc.items() if k in ("fast_cells_kernel", "describe_kernel")})
 PY

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 PMC passes: per kernel, the mean per-dispatch value of each counter."""
+import re
 import csv
 import sys
 from collections import defaultdict
@@ -11,7 +12,7 @@ def main(d):
     for f in sorted(Path(d).rglob("run_counter_collection.csv")):
         per = defaultdict(lambda: defaultdict(float))
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0].replace("orbamd::", "")
+            name = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].replace("orbamd::", "").replace("void ", ""))
             per[(name, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
         for (name, _), cs in per.items():
             for c, v in cs.items():

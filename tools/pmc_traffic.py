@@ -5,6 +5,7 @@ FETCH_SIZE and WRITE_SIZE are reported in KiB.  The calibration program reads / 
 1 GiB per dispatch with 4-, 8- and 16-byte lane accesses; its ratios (counter bytes / true bytes)
 are reported next to each extractor kernel's raw and calibration-corrected bytes per dispatch.
 """
+import re
 import csv
 import json
 import sys
@@ -20,7 +21,7 @@ def per_dispatch(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            name = r["Kernel_Name"].split("(")[0].replace("orbamd::", "").replace("void ", "")
+            name = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].replace("orbamd::", "").replace("void ", "")).replace("void ", "")
             acc[name][r["Dispatch_Id"]] += float(r["Counter_Value"]) * 1024.0   # KiB -> bytes
     return {k: sum(v.values()) / len(v) for k, v in acc.items()}
 
