@@ -343,7 +343,13 @@ __device__ double block_sum_1024(const double* v, int n, double* sh) {
 // One workgroup (1008 threads) per free pose: 42 sums (Hpp 36 + b 6), 24 partial groups with
 // four interleaved accumulators each, combined in a fixed order.  Block np: chi2 total.
 constexpr int PA_G = 24;
-__device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh);
+constexpr int PA_SLOTS = 4096;   // a pose's edge-slot list staged in LDS when it has at most this many
+__device__ __forceinline__ void stage_pose_slots(const BADev& b, int i, int* sslot) {
+    const int beg = b.ps_beg[i], n = b.ps_beg[i + 1] - beg;
+    if (n <= PA_SLOTS)
+        for (int u = threadIdx.x; u < n; u += blockDim.x) sslot[u] = b.ps_slot[beg + u];
+}
+__device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh, const int* sslot);
 __device__ __forceinline__ void chi_total(const BADev& b, double* sh) {
     const double c = block_sum_1024(b.rchi, b.nl, sh);
     if (threadIdx.x == 0) {
@@ -356,9 +362,12 @@ __device__ __forceinline__ void chi_total(const BADev& b, double* sh) {
 __global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b) {
     if (b.ctl->done || !b.ctl->need_lin) return;
     __shared__ double sh[1024];
+    __shared__ int sslot[PA_SLOTS];
     if ((int)blockIdx.x == b.np) chi_total(b, sh);
     else {
-        pose_accum(b, blockIdx.x, sh);   // ends with a barrier: Hpp visible to the workgroup
+        stage_pose_slots(b, blockIdx.x, sslot);
+        __syncthreads();
+        pose_accum(b, blockIdx.x, sh, sslot);   // ends with a barrier: Hpp visible to the workgroup
         if (threadIdx.x == 0) {   // computeLambdaInit's max over this pose's diagonal
             double m = 0;
             for (int k = 0; k < 6; k++) m = fmax(m, fabs(b.Hpp[36 * blockIdx.x + 7 * k]));
@@ -366,20 +375,26 @@ __global__ __launch_bounds__(1024) void ba_pose_accum_kernel(BADev b) {
         }
     }
 }
-__device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh) {
+// (the caller staged the pose's slots with stage_pose_slots and a barrier; a pose with more than
+// PA_SLOTS edges reads them from HBM)
+__device__ __forceinline__ void pose_accum(const BADev& b, int i, double* sh, const int* sslot) {
     const int g = threadIdx.x / 42, c = threadIdx.x % 42;
     const int beg = b.ps_beg[i], end = b.ps_beg[i + 1];
-    if (g < PA_G) {
+    auto sum = [&](auto slot) {   // slot(u), u in [beg, end): LDS-staged or HBM (two instantiations)
         double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
         int u = beg + g;
         for (; u + 3 * PA_G < end; u += 4 * PA_G) {
-            s0 += b.J[(long long)b.ps_slot[u] * 72 + 12 + c];
-            s1 += b.J[(long long)b.ps_slot[u + PA_G] * 72 + 12 + c];
-            s2 += b.J[(long long)b.ps_slot[u + 2 * PA_G] * 72 + 12 + c];
-            s3 += b.J[(long long)b.ps_slot[u + 3 * PA_G] * 72 + 12 + c];
+            s0 += b.J[(long long)slot(u) * 72 + 12 + c];
+            s1 += b.J[(long long)slot(u + PA_G) * 72 + 12 + c];
+            s2 += b.J[(long long)slot(u + 2 * PA_G) * 72 + 12 + c];
+            s3 += b.J[(long long)slot(u + 3 * PA_G) * 72 + 12 + c];
         }
-        for (; u < end; u += PA_G) s0 += b.J[(long long)b.ps_slot[u] * 72 + 12 + c];
+        for (; u < end; u += PA_G) s0 += b.J[(long long)slot(u) * 72 + 12 + c];
         sh[g * 42 + c] = (s0 + s1) + (s2 + s3);
+    };
+    if (g < PA_G) {
+        if (end - beg <= PA_SLOTS) sum([&](int u) { return sslot[u - beg]; });
+        else sum([&](int u) { return b.ps_slot[u]; });
     }
     __syncthreads();
     if (threadIdx.x < 42) {
@@ -442,6 +457,7 @@ constexpr int SB_SPLIT = SB_SPLIT_DEF;
 __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, int accum) {
     BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
+    __shared__ int sslot[PA_SLOTS];
     const int blk = blockIdx.x, part = blockIdx.y;
     const bool acc = accum && b.ctl->need_lin;
     if (blk == b.nblk) {
@@ -449,7 +465,12 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
         return;
     }
     const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
-    if (acc && i1 == i2 && part == 0) pose_accum(b, i1, sh);
+    const bool diag0 = i1 == i2 && part == 0;   // workgroup-uniform
+    if (diag0) {   // the pose's edge slots, for its Hpp / b_p sums and b_schur (no dependent HBM loads)
+        stage_pose_slots(b, i1, sslot);
+        __syncthreads();
+    }
+    if (acc && diag0) pose_accum(b, i1, sh, sslot);
     const int g = threadIdx.x / 36, c = threadIdx.x % 36;
     const int r = c / 6, cc = c % 6;
     if (g < SB_G) {
@@ -507,13 +528,30 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
     // b_schur for pose i1: 6 entries x 168 partial groups
     const int g2 = threadIdx.x / 6, c2 = threadIdx.x % 6;
     double s = 0;
-    if (g2 < 168)
-        for (int u = b.ps_beg[i1] + g2; u < b.ps_beg[i1 + 1]; u += 168) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + c2];
+    {
+        const int beg = b.ps_beg[i1], end = b.ps_beg[i1 + 1];
+        if (g2 < 168) {
+            if (end - beg <= PA_SLOTS)
+                for (int u = beg + g2; u < end; u += 168) s += b.W[(long long)sslot[u - beg] * 24 + 18 + c2];
+            else
+                for (int u = beg + g2; u < end; u += 168) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + c2];
+        }
+    }
     sh[threadIdx.x] = g2 < 168 ? s : 0.0;
+    __syncthreads();
+    // two-level fixed-order sum of the 168 partials per entry (8 runs of 21, then the 8 run sums)
+    // instead of one 168-long dependent chain on 6 threads
+    double run = 0;
+    if (threadIdx.x < 48) {
+        const int e = threadIdx.x % 6, h = threadIdx.x / 6;
+        for (int q = 21 * h; q < 21 * h + 21; q++) run += sh[q * 6 + e];
+    }
+    __syncthreads();
+    if (threadIdx.x < 48) sh[threadIdx.x] = run;
     __syncthreads();
     if (threadIdx.x < 6) {
         double tot = 0;
-        for (int q = 0; q < 168; q++) tot += sh[q * 6 + threadIdx.x];
+        for (int h = 0; h < 8; h++) tot += sh[6 * h + threadIdx.x];
         b.bs[6 * i1 + threadIdx.x] = b.bp[6 * i1 + threadIdx.x] - tot;
     }
 }
@@ -769,6 +807,8 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
         for (int j = 0; j < 3; j++) t_pre[j] = b.t[3 * id + j];
         for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
     }
+    // the rhs first: its load is in flight with S's
+    const double bs_v = tid < D ? b.bs[tid] : 0.0;   // D <= 128 < blockDim
     // S -> LDS: D = 6 np is even, so every row of S starts 16-byte aligned; lane c of a wavefront
     // takes the 16-byte piece c of its rows (w, w+4, ...), 32 rows of loads in flight per batch (one
     // batch up to D = 128: the solve's wavefronts have the VGPRs to spare here)
@@ -791,14 +831,15 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
                 }
             }
         }
-        // identity padding: columns D..Dp-1 of the real rows, then the padded rows
-        for (int u = tid; u < D * (Dp - D); u += blockDim.x) A[(u / (Dp - D)) * ld + D + u % (Dp - D)] = 0.0;
-        for (int u = tid; u < (Dp - D) * Dp; u += blockDim.x) {
-            const int r = D + u / Dp, c = u % Dp;
-            A[r * ld + c] = r == c ? 1.0 : 0.0;
-        }
+        // identity padding (no divisions): columns D..Dp-1 of every row, then rows D..Dp-1; a thread
+        // per (row group, column) of each
+        const int npad = Dp - D;
+        for (int r = tid / 16; r < Dp; r += blockDim.x / 16)
+            if ((tid & 15) < npad) A[r * ld + D + (tid & 15)] = r == D + (tid & 15) ? 1.0 : 0.0;
+        for (int r = D + tid / 64; r < Dp; r += blockDim.x / 64)
+            for (int c = lane; c < D; c += 64) A[r * ld + c] = 0.0;
     }
-    for (int i = tid; i < Dp; i += blockDim.x) y[i] = i < D ? b.bs[i] : 0.0;
+    if (tid < Dp) y[tid] = bs_v;
     if (tid == 0) s_ok = 1;
     __syncthreads();
     BA_STAMP(0);
@@ -1237,13 +1278,18 @@ __device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double
         }
     }
     // control snapshot straight into pinned host memory (no copy on the stream, no event): the
-    // body first, then the sequence id the host polls for, ordered by a system-scope fence
+    // body as system-scope stores (write-through, no L2 writeback of the device's other data as a
+    // system fence would do), waited for, then the sequence id the host polls for
     BACtl snap = *c;
     snap.seq = -1;
-    *host_snap = snap;
-    __threadfence_system();
-    __atomic_store_n(&host_snap->seq, seq, __ATOMIC_RELAXED);
-    __threadfence_system();
+    static_assert(sizeof(BACtl) % 8 == 0, "snapshot copied as 8-byte words");
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&snap);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(host_snap);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(BACtl) / 8); k++)
+        __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&host_snap->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return c->accepted != 0;
 }
 
