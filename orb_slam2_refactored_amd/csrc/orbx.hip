@@ -893,16 +893,26 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     const int f = lb / nstrips;
     const int2 sd = strips[strip_beg + lb - f * nstrips];
     const int i_beg = 0, i_end = sd.y & 255, cstride = sd.y >> 8;
+    // every cell of a strip has the same level and zone width (host-checked): the crop's level
+    // base, step and row-dword count and every per-lane quantity that depends on the zone width are
+    // loop-invariant over the strip
+    const CellDev c0 = cells[sd.x];
+    const int zw = c0.zwzh & 0xffff;
+    int lstep;
+    const uint8_t* limg = level_base(g, c0.level, f, in, in_fstride, in_step, pyr, &lstep);
+    const int lh = g.lv[c0.level].h;
+    const int ndl = (zw + 6 + 1 + 3) >> 2;   // LDS dwords per crop row
     auto source = [&](int item, CellDev& cd, int& ci) {
         ci = sd.x + item * cstride;
         cd = cells[ci];
         CropSrc c;
-        c.img = level_base(g, cd.level, f, in, in_fstride, in_step, pyr, &c.step);
+        c.img = limg;
+        c.step = lstep;
         c.x0 = cd.x0y0 & 0xffff;
         c.y0 = cd.x0y0 >> 16;
         c.ch = (cd.zwzh >> 16) + 6;
-        c.ndl = ((cd.zwzh & 0xffff) + 6 + 1 + 3) >> 2;   // LDS dwords per crop row
-        c.h = g.lv[cd.level].h;
+        c.ndl = ndl;
+        c.h = lh;
         return c;
     };
     // Speculative iniThFAST pass: a cell whose predecessor in this wavefront (the cell above it in
@@ -916,7 +926,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     int ci;
     const CropSrc src = source(item, cell, ci);
     const int x0 = src.x0, y0 = src.y0;
-    const int zw = cell.zwzh & 0xffff, zh = cell.zwzh >> 16;
+    const int zh = cell.zwzh >> 16;
     {
         crop_stage_rows(src, lane, crop, CSd);
     }
@@ -2611,8 +2621,15 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
                 return ORB_EINTERNAL;
             }
             for (int rb = 0; rb < ncy; rb += cpw)
-                for (int cx = 0; cx < ncx; cx++)
-                    strips.push_back(make_int2(L.cell_base + rb * ncx + cx, std::min(cpw, ncy - rb) | (ncx << 8)));
+                for (int cx = 0; cx < ncx; cx++) {
+                    const int c0 = L.cell_base + rb * ncx + cx, n = std::min(cpw, ncy - rb);
+                    for (int k = 1; k < n; k++)   // the kernel takes the zone width from the first cell
+                        if ((cells[c0 + k * ncx].zwzh & 0xffff) != (cells[c0].zwzh & 0xffff)) {
+                            set_error("FAST strip with unequal zone widths");
+                            return ORB_EINTERNAL;
+                        }
+                    strips.push_back(make_int2(c0, n | (ncx << 8)));
+                }
         }
         h->strip_beg[g.nlevels] = (int)strips.size();
         if ((rc = h->d_strips.reserve(std::max<size_t>(1, strips.size()) * sizeof(int2)))) return rc;
