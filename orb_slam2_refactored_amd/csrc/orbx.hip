@@ -789,8 +789,12 @@ __device__ __forceinline__ void crop_commit(const CropSrc& c, int lane, const u3
 constexpr int CROP_NG = 10;
 constexpr int FAST_CROP_SLACK = 3;   // crop rows past the tallest crop: a partial last row group (RPG <= 4)
 // groups whose loads are issued together (40 rows at LR = 16)
-__device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint8_t* crop, int CSd) {
-    const int lrs = c.ndl <= 16 ? 4 : (c.ndl <= 32 ? 5 : 6);
+// LRS = log2(lanes per crop row), a template constant so that with a compile-time crop stride the
+// CROP_NG row-group stores share one LDS base address (offset fields) instead of CROP_NG live
+// per-lane addresses.
+template <int LRS>   // 0: from the crop's row-dword count at run time
+__device__ __forceinline__ void crop_stage_rows_t(const CropSrc& c, int lane, uint8_t* crop, int CSd) {
+    const int lrs = LRS ? LRS : (c.ndl <= 16 ? 4 : (c.ndl <= 32 ? 5 : 6));   // 0: run time
     const int RPG = 64 >> lrs;
     const int roff = lane >> lrs, d = lane & ((1 << lrs) - 1);
     const bool dok = d < c.ndl;
@@ -861,6 +865,14 @@ __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint
     }
 }
 
+template <int CST>
+__device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint8_t* crop, int CSd) {
+    if (CST == 0) crop_stage_rows_t<0>(c, lane, crop, CSd);   // run-time stride: one generic copy
+    else if (c.ndl <= 16) crop_stage_rows_t<4>(c, lane, crop, CSd);
+    else if (c.ndl <= 32) crop_stage_rows_t<5>(c, lane, crop, CSd);
+    else crop_stage_rows_t<6>(c, lane, crop, CSd);
+}
+
 // One wavefront processes `cpw` consecutive (frame, cell) items of the XCD-swizzled order; item
 // i = f * ncells + cell.  LDS (sized per launch from the largest cell): the crop (zone + 3-px
 // apron), a zone map of corner strengths, a queue of pre-test passers and the ordered corner list.
@@ -928,7 +940,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     const int x0 = src.x0, y0 = src.y0;
     const int zh = cell.zwzh >> 16;
     {
-        crop_stage_rows(src, lane, crop, CSd);
+        crop_stage_rows<CST>(src, lane, crop, CSd);
     }
     const int tlo = min(th_ini, th_min);
     bool spec = spec_min > 0 && th_ini > tlo && prev_ini >= spec_min;
