@@ -8,8 +8,9 @@
 //     ba_iter_kernel         on a new iteration: computeActiveErrors + robust chi2 + linearizeOplus +
 //                            constructQuadraticForm, Hll / b_l per point, per-edge pose parts; then
 //                            (lambda known) D^-1 = (Hll + lambda I)^-1, W = Hpl D^-1, Hpl D^-1 b_l
-//     ba_schur_block_kernel  on a new iteration: Hpp / b_p per free pose and the chi2 total; then
-//                            S(i1,i2) = Hpp + lambda I - sum W Hpl^T, b_schur on diagonal blocks
+//     ba_schur_block_kernel  S(i1,i2) = Hpp + lambda I - sum W Hpl^T per block (pair list in parts);
+//                            beside them one workgroup per pose: on a new iteration its Hpp / b_p,
+//                            then b_schur; and the chi2 total
 //     ba_solve_kernel        blocked LDL^T of the (6P)^2 reduced camera system in LDS, triangular
 //                            solves, push + SE3 exp-update of the free poses
 //     ba_point_update_kernel back-substitution, push, point +=, errors + robust chi2 of its edges
@@ -103,8 +104,9 @@ struct BADev {
     double* x;            // D + 3 nl
     double* rchi;         // Ea: robust chi2 per active slot
     double* part;         // scale partials: nl + np
-    double* Spart;         // SB_SPLIT x nblk x 36: the Schur-block parts' partial blocks
+    double* Spart;         // (SB_SPLIT + 1) x nblk x 36: the Schur-block parts' partial blocks (+ Hpp)
     unsigned* blk_done;    // nblk: parts of the block finished (the last one forms S)
+    const int* blk_diag;   // np: block index of the diagonal block (i, i)
     BACtl* ctl;
     const int32_t* stop;   // device view of the host's force-stop flag (mapped pinned mirror), or null
     int stop_after;        // test hook: stop once this many trials have run (-1: off)
@@ -441,19 +443,54 @@ __global__ __launch_bounds__(64) void ba_schur_point_kernel(BADev b) {
 }
 
 // Reduced camera system block (i1, i2): 36 entries x 28 partial groups (two accumulators each),
-// fixed-order combine.  Diagonal blocks also form b_schur = b_p - sum Hpl D^-1 b_l.
-// With `accum` (every step but an optimize() call's first), a linearising trial also forms here what
-// ba_pose_accum_kernel would: each diagonal block's workgroup the Hpp / b_p sums of its pose first,
-// workgroup nblk the chi2 total.
+// fixed-order combine.
 // The pair list of a block is split into SB_SPLIT contiguous parts, one workgroup each (blockIdx.y),
 // each storing its partial block (device-coherent stores, completed before it counts in); the last
-// part of a block to count in adds the partials in part order and writes the block of S.  Part 0
-// also adds Hpp + lambda I and does the diagonal blocks' extras.
+// part of a block to count in adds the partials in part order and writes the block of S.
+// Per free pose one more workgroup (blockIdx.x = nblk + 1 + i, part 0): with `accum` (every step but
+// an optimize() call's first) on a linearising trial the Hpp / b_p sums of its pose (what
+// ba_pose_accum_kernel would do), then b_schur = b_p - sum Hpp D^-1 b_l; it counts in on the pose's
+// diagonal block as one more part, so the diagonal block's last arriver finds Hpp published and forms
+// part 0 + Hpp + lambda I exactly as part 0 itself used to (same rounding).  Workgroup nblk: the chi2
+// total.  (Round 3: the pose sums and b_schur ran inside the diagonal blocks' part 0, after its pair
+// loop, on the kernel's critical path.)
 constexpr int SB_G = 28;
 #ifndef SB_SPLIT_DEF
 #define SB_SPLIT_DEF 2
 #endif
 constexpr int SB_SPLIT = SB_SPLIT_DEF;
+
+// count in on block blk (expect arrivals in all); the last arriver forms the block of S
+__device__ __forceinline__ void schur_block_count_in(const BADev& b, int blk, int D, int expect) {
+    __shared__ int s_last;
+    // Hand-off by the memory model: the partials' stores happen before thread 0's agent-scope
+    // release (workgroup barrier), and the last part's agent-scope acquire happens before its loads
+    // (the same barrier pattern on the consumer side).  Callers publish the partial from threads of
+    // wavefront 0 only (the wavefront of the counting thread).
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_last = __hip_atomic_fetch_add(&b.blk_done[blk], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)expect - 1;
+        if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < 36) {
+        const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
+        const int r = threadIdx.x / 6, cc = threadIdx.x % 6;
+        double v = 0;
+        for (int k = 0; k < SB_SPLIT; k++) {
+            double pk = b.Spart[((long long)k * b.nblk + blk) * 36 + threadIdx.x];
+            if (k == 0 && i1 == i2) {   // part 0 + Hpp (the pose workgroup's part) + lambda I, in that order
+                pk += b.Spart[((long long)SB_SPLIT * b.nblk + blk) * 36 + threadIdx.x];
+                if (r == cc) pk += b.ctl->lambda;
+            }
+            v += pk;
+        }
+        b.S[(long long)(6 * i1 + r) * D + 6 * i2 + cc] = v;
+        if (i1 != i2) b.S[(long long)(6 * i2 + cc) * D + 6 * i1 + r] = v;
+        if (threadIdx.x == 0) __hip_atomic_store(&b.blk_done[blk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, int accum) {
     BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
@@ -464,13 +501,54 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
         if (acc && part == 0) chi_total(b, sh);
         return;
     }
-    const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
-    const bool diag0 = i1 == i2 && part == 0;   // workgroup-uniform
-    if (diag0) {   // the pose's edge slots, for its Hpp / b_p sums and b_schur (no dependent HBM loads)
-        stage_pose_slots(b, i1, sslot);
+    if (blk > b.nblk) {   // pose workgroup
+        if (part != 0) return;
+        const int i1 = blk - b.nblk - 1;
+        stage_pose_slots(b, i1, sslot);   // the pose's edge slots (no dependent HBM loads below)
         __syncthreads();
+#ifndef BA_DIAG_NO_PA   // diagnostic timing builds only (wrong results): tools/probe/ba_schur_parts.sh
+        if (acc) {
+            pose_accum(b, i1, sh, sslot);
+            __syncthreads();   // b_p of this trial (global, this workgroup's stores) before b_schur
+        }
+#endif
+        // b_schur for pose i1: 6 entries x 168 partial groups
+        const int g2 = threadIdx.x / 6, c2 = threadIdx.x % 6;
+        double s = 0;
+        {
+            const int beg = b.ps_beg[i1], end = b.ps_beg[i1 + 1];
+            if (g2 < 168) {
+                if (end - beg <= PA_SLOTS)
+                    for (int u = beg + g2; u < end; u += 168) s += b.W[(long long)sslot[u - beg] * 24 + 18 + c2];
+                else
+                    for (int u = beg + g2; u < end; u += 168) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + c2];
+            }
+        }
+        sh[threadIdx.x] = g2 < 168 ? s : 0.0;
+        __syncthreads();
+        // two-level fixed-order sum of the 168 partials per entry (8 runs of 21, then the 8 run sums)
+        // instead of one 168-long dependent chain on 6 threads
+        double run = 0;
+        if (threadIdx.x < 48) {
+            const int e = threadIdx.x % 6, h = threadIdx.x / 6;
+            for (int q = 21 * h; q < 21 * h + 21; q++) run += sh[q * 6 + e];
+        }
+        __syncthreads();
+        if (threadIdx.x < 48) sh[threadIdx.x] = run;
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            double tot = 0;
+            for (int h = 0; h < 8; h++) tot += sh[6 * h + threadIdx.x];
+            b.bs[6 * i1 + threadIdx.x] = b.bp[6 * i1 + threadIdx.x] - tot;
+        }
+        // Hpp (this trial's or the kept one) as the diagonal block's extra part, republished by
+        // wavefront 0 so that the counting wavefront's own release orders it
+        const int dblk = b.blk_diag[i1];
+        if (threadIdx.x < 36) b.Spart[((long long)SB_SPLIT * b.nblk + dblk) * 36 + threadIdx.x] = b.Hpp[36 * i1 + threadIdx.x];
+        schur_block_count_in(b, dblk, D, SB_SPLIT + 1);
+        return;
     }
-    if (acc && diag0) pose_accum(b, i1, sh, sslot);
+    const int i1 = b.blk_i1[blk], i2 = b.blk_i2[blk];
     const int g = threadIdx.x / 36, c = threadIdx.x % 36;
     const int r = c / 6, cc = c % 6;
     if (g < SB_G) {
@@ -499,61 +577,9 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
     if (threadIdx.x < 36) {
         double s = 0;
         for (int q = 0; q < SB_G; q++) s += sh[q * 36 + threadIdx.x];
-        double v = -s;
-        if (i1 == i2 && part == 0) {
-            v += b.Hpp[36 * i1 + threadIdx.x];
-            if (r == cc) v += b.ctl->lambda;
-        }
-        b.Spart[((long long)part * b.nblk + blk) * 36 + threadIdx.x] = v;
+        b.Spart[((long long)part * b.nblk + blk) * 36 + threadIdx.x] = -s;
     }
-    // Hand-off by the memory model: the partials' stores happen before thread 0's agent-scope
-    // release (workgroup barrier), and the last part's agent-scope acquire happens before its loads
-    // (the same barrier pattern on the consumer side).
-    __shared__ int s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        s_last = __hip_atomic_fetch_add(&b.blk_done[blk], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == SB_SPLIT - 1;
-        if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-    if (s_last && threadIdx.x < 36) {
-        double v = 0;
-        for (int k = 0; k < SB_SPLIT; k++) v += b.Spart[((long long)k * b.nblk + blk) * 36 + threadIdx.x];
-        b.S[(long long)(6 * i1 + r) * D + 6 * i2 + cc] = v;
-        if (i1 != i2) b.S[(long long)(6 * i2 + cc) * D + 6 * i1 + r] = v;
-        if (threadIdx.x == 0) __hip_atomic_store(&b.blk_done[blk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (i1 != i2 || part != 0) return;
-    __syncthreads();
-    // b_schur for pose i1: 6 entries x 168 partial groups
-    const int g2 = threadIdx.x / 6, c2 = threadIdx.x % 6;
-    double s = 0;
-    {
-        const int beg = b.ps_beg[i1], end = b.ps_beg[i1 + 1];
-        if (g2 < 168) {
-            if (end - beg <= PA_SLOTS)
-                for (int u = beg + g2; u < end; u += 168) s += b.W[(long long)sslot[u - beg] * 24 + 18 + c2];
-            else
-                for (int u = beg + g2; u < end; u += 168) s += b.W[(long long)b.ps_slot[u] * 24 + 18 + c2];
-        }
-    }
-    sh[threadIdx.x] = g2 < 168 ? s : 0.0;
-    __syncthreads();
-    // two-level fixed-order sum of the 168 partials per entry (8 runs of 21, then the 8 run sums)
-    // instead of one 168-long dependent chain on 6 threads
-    double run = 0;
-    if (threadIdx.x < 48) {
-        const int e = threadIdx.x % 6, h = threadIdx.x / 6;
-        for (int q = 21 * h; q < 21 * h + 21; q++) run += sh[q * 6 + e];
-    }
-    __syncthreads();
-    if (threadIdx.x < 48) sh[threadIdx.x] = run;
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        double tot = 0;
-        for (int h = 0; h < 8; h++) tot += sh[6 * h + threadIdx.x];
-        b.bs[6 * i1 + threadIdx.x] = b.bp[6 * i1 + threadIdx.x] - tot;
-    }
+    schur_block_count_in(b, blk, D, i1 == i2 ? SB_SPLIT + 1 : SB_SPLIT);
 }
 
 
@@ -811,7 +837,11 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     const double bs_v = tid < D ? b.bs[tid] : 0.0;   // D <= 128 < blockDim
     // S -> LDS: D = 6 np is even, so every row of S starts 16-byte aligned; lane c of a wavefront
     // takes the 16-byte piece c of its rows (w, w+4, ...), 32 rows of loads in flight per batch (one
-    // batch up to D = 128: the solve's wavefronts have the VGPRs to spare here)
+    // batch up to D = 128: the solve's wavefronts have the VGPRs to spare here).  Only the lower block
+    // triangle is read (row r: columns up to the end of its 16-column block): the factorisation, the
+    // panels, the trailing updates and the back substitution read nothing above the diagonal blocks,
+    // and the diagonal blocks' upper triangles receive Linv before they are read.  The load is
+    // bandwidth-bound for one CU, so this halves it.
     {
         const int npc = D / 2;
         const double2* S2 = reinterpret_cast<const double2*>(b.S);
@@ -820,12 +850,14 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
 #pragma unroll
             for (int q = 0; q < 32; q++) {
                 const int r = min(r0 + 4 * q, D - 1);
-                v[q] = lane < npc ? S2[r * npc + lane] : make_double2(0.0, 0.0);
+                const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;   // pieces up to the block's end
+                v[q] = lane < npr ? S2[r * npc + lane] : make_double2(0.0, 0.0);
             }
 #pragma unroll
             for (int q = 0; q < 32; q++) {
                 const int r = r0 + 4 * q;
-                if (r < D && lane < npc) {
+                const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;
+                if (r < D && lane < npr) {
                     A[r * ld + 2 * lane] = v[q].x;
                     A[r * ld + 2 * lane + 1] = v[q].y;
                 }
@@ -1224,6 +1256,8 @@ __global__ __launch_bounds__(256) void ba_decide_kernel(BADev b, BACtl* host_sna
     }
 }
 
+__device__ __forceinline__ void snapshot_to_host(const BACtl& snap, int seq, BACtl* host_snap);
+
 // levenberg.cpp:120-147 — accept / reject, lambda / nu update, then the trial / iteration bookkeeping
 // of g2o's solve() / optimize(); one thread.  Returns whether the step was accepted.
 __device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double tmp_sum, double scale_sum) {
@@ -1277,11 +1311,19 @@ __device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double
             c->q = 0;
         }
     }
-    // control snapshot straight into pinned host memory (no copy on the stream, no event): the
-    // body as system-scope stores (write-through, no L2 writeback of the device's other data as a
-    // system fence would do), waited for, then the sequence id the host polls for
+    // control snapshot straight into pinned host memory (no copy on the stream, no event).  (A
+    // forwarder kernel on a side stream, so the decide kernel would not wait for the PCIe writes,
+    // was slower: 1.73 -> 1.92 ms per C4 call.)
     BACtl snap = *c;
     snap.seq = -1;
+    snapshot_to_host(snap, seq, host_snap);
+    return c->accepted != 0;
+}
+
+// The control snapshot into pinned host memory: the body as system-scope stores (write-through, no L2
+// writeback of the device's other data as a system fence would do), waited for, then the sequence
+// id the host polls for.
+__device__ __forceinline__ void snapshot_to_host(const BACtl& snap, int seq, BACtl* host_snap) {
     static_assert(sizeof(BACtl) % 8 == 0, "snapshot copied as 8-byte words");
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&snap);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(host_snap);
@@ -1290,8 +1332,8 @@ __device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double
         __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(&host_snap->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return c->accepted != 0;
 }
+
 
 // final outlier classification (Optimizer.cc:644-670, :686-699) + chi2 out
 __global__ void ba_ctl_start_kernel(BADev b, int iters) {
@@ -1715,7 +1757,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         const size_t sbytes = carve_size<int>(Ea) + carve_size<int>(P) + carve_size<int>(N) + carve_size<int>(nl + 1) +
                               carve_size<int>(Ea) + carve_size<int>(nl) + carve_size<int>(np + 1) +
                               carve_size<int>(hs.ps_slot.size()) + carve_size<int>(np) + carve_size<int>(nblk) * 2 +
-                              carve_size<int>(nblk + 1) + carve_size<int2>(hs.blk_pair.size());
+                              carve_size<int>(nblk + 1) + carve_size<int2>(hs.blk_pair.size()) + carve_size<int>(np);
         int rc2;
         if (!have_structure) {
         if ((rc2 = C.structure.reserve(sbytes))) return rc2;
@@ -1737,6 +1779,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         int* d_b2 = cr.take<int>(nblk);
         int* d_bb = cr.take<int>(nblk + 1);
         int2* d_bp = cr.take<int2>(hs.blk_pair.size());
+        int* d_bd = cr.take<int>(np);
         put(hs.act.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
         put(hs.hp.data(), 4 * (size_t)P, (char*)hr.take<int>(P));
         put(hs.hl.data(), 4 * (size_t)N, (char*)hr.take<int>(N));
@@ -1750,18 +1793,24 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         put(hs.blk_i2.data(), 4 * (size_t)nblk, (char*)hr.take<int>(nblk));
         put(hs.blk_beg.data(), 4 * (size_t)(nblk + 1), (char*)hr.take<int>(nblk + 1));
         put(hs.blk_pair.data(), 8 * hs.blk_pair.size(), (char*)hr.take<int2>(hs.blk_pair.size()));
+        {
+            int* bd = hr.take<int>(np);
+            for (int k = 0; k < nblk; k++)
+                if (hs.blk_i1[k] == hs.blk_i2[k]) bd[hs.blk_i1[k]] = k;
+        }
         ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, cr.off, hipMemcpyHostToDevice, st));
         b.Ea = Ea; b.np = np; b.nl = nl; b.nblk = nblk;
         b.act = d_act; b.hp = d_hp; b.hl = d_hl; b.pt_beg = d_ptb; b.pt_slot = d_pts; b.pt_id = d_pti;
         b.ps_beg = d_psb; b.ps_slot = d_pss; b.ps_id = d_psi; b.blk_i1 = d_b1; b.blk_i2 = d_b2; b.blk_beg = d_bb;
         b.blk_pair = d_bp;
+        b.blk_diag = d_bd;
         have_structure = true;
         }
         // system buffers
         const size_t ybytes = carve_size<double>(72 * (size_t)Ea) + carve_size<double>(24 * (size_t)Ea) +
                               carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +
                               carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
-                              carve_size<double>((size_t)D * D) + carve_size<double>((size_t)SB_SPLIT * nblk * 36) +
+                              carve_size<double>((size_t)D * D) + carve_size<double>((size_t)(SB_SPLIT + 1) * nblk * 36) +
                               carve_size<unsigned>((size_t)nblk) + carve_size<double>(D) +
                               carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
                               carve_size<double>(nl + np) + (glob ? carve_size<double>((size_t)Dp * (Dp + 1)) : 0) +
@@ -1777,7 +1826,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.Hpp = cy.take<double>(36 * (size_t)np);
         b.bp = cy.take<double>(6 * (size_t)np);
         b.S = cy.take<double>((size_t)D * D);
-        b.Spart = cy.take<double>((size_t)SB_SPLIT * nblk * 36);
+        b.Spart = cy.take<double>((size_t)(SB_SPLIT + 1) * nblk * 36);   // + the diagonal blocks' Hpp part
         b.blk_done = cy.take<unsigned>((size_t)nblk);
         b.bs = cy.take<double>(D);
         b.x = cy.take<double>(D + 3 * (size_t)nl);
@@ -1811,7 +1860,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                     hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b);
                     hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
                 }
-                hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
+                hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1 + np, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
                 if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
                 else hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
                 const int slot = enq % LOOKAHEAD;
