@@ -838,47 +838,61 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     }
     // the rhs first: its load is in flight with S's
     const double bs_v = tid < D ? b.bs[tid] : 0.0;   // D <= 128 < blockDim
-    // S -> LDS: D = 6 np is even, so every row of S starts 16-byte aligned; lane c of a wavefront
-    // takes the 16-byte piece c of its rows (w, w+4, ...), 32 rows of loads in flight per batch (one
-    // batch up to D = 128: the solve's wavefronts have the VGPRs to spare here).  Only the lower block
-    // triangle is read (row r: columns up to the end of its 16-column block): the factorisation, the
-    // panels, the trailing updates and the back substitution read nothing above the diagonal blocks,
-    // and the diagonal blocks' upper triangles receive Linv before they are read.  The load is
-    // bandwidth-bound for one CU, so this halves it.
-    {
-        const int npc = D / 2;
-        const double2* S2 = reinterpret_cast<const double2*>(b.S);
-        for (int r0 = wv; r0 < D; r0 += 128) {
-            double2 v[32];
+    // S -> LDS, only its lower block triangle (row r: columns up to the end of its 16-column block):
+    // the factorisation, the panels, the trailing updates and the back substitution read nothing
+    // above the diagonal blocks, and the diagonal blocks' upper triangles receive Linv before they are
+    // read.  Wavefront 0 stages block 0 (rows 0-15, with the identity padding of a system smaller
+    // than one block) and factors it while wavefronts 1-3 load rows 16.. (the load is latency-bound:
+    // 38 rows of 16-byte pieces in flight per lane, lane c = piece c of the row).  D = 6 np is even,
+    // so every row of S starts 16-byte aligned.
+    const int npc = D / 2;
+    const double2* S2 = reinterpret_cast<const double2*>(b.S);
+    if (wv == 0) {
+        double2 v[2];
 #pragma unroll
-            for (int q = 0; q < 32; q++) {
-                const int r = min(r0 + 4 * q, D - 1);
-                const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;   // pieces up to the block's end
-                v[q] = lane < npr ? S2[r * npc + lane] : make_double2(0.0, 0.0);
-            }
+        for (int k = 0; k < 2; k++) {   // 16 rows x 8 pieces over 64 lanes
+            const int p = lane + 64 * k, r = p >> 3, c = 2 * (p & 7);
+            v[k] = r < D && c < D ? S2[r * npc + (c >> 1)] : make_double2(r == c ? 1.0 : 0.0, r == c + 1 ? 1.0 : 0.0);
+        }
 #pragma unroll
-            for (int q = 0; q < 32; q++) {
-                const int r = r0 + 4 * q;
-                const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;
-                if (r < D && lane < npr) {
-                    A[r * ld + 2 * lane] = v[q].x;
-                    A[r * ld + 2 * lane + 1] = v[q].y;
-                }
+        for (int k = 0; k < 2; k++) {
+            const int p = lane + 64 * k, r = p >> 3, c = 2 * (p & 7);
+            A[r * ld + c] = v[k].x;
+            A[r * ld + c + 1] = v[k].y;
+        }
+        if (lane < Dp) y[lane] = bs_v;
+        if (lane == 0) s_ok = 1;
+        wave_lds_sync();
+        BA_STAMPW(0);
+        if (!solve_diag_block(A, y, dinv, vz, ld, 0, lane, D) && lane == 0) s_ok = 0;
+    } else {
+        constexpr int RQ = 38;   // rows per wavefront: 3 x 38 >= 128 - 16
+        const int r0 = SB + wv - 1;
+        double2 v[RQ];
+#pragma unroll
+        for (int q = 0; q < RQ; q++) {
+            const int r = min(r0 + 3 * q, D - 1);
+            const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;   // pieces up to the block's end
+            v[q] = r0 + 3 * q < D && lane < npr ? S2[r * npc + lane] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int q = 0; q < RQ; q++) {
+            const int r = r0 + 3 * q;
+            const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;
+            if (r < D && lane < npr) {
+                A[r * ld + 2 * lane] = v[q].x;
+                A[r * ld + 2 * lane + 1] = v[q].y;
             }
         }
-        // identity padding (no divisions): columns D..Dp-1 of every row, then rows D..Dp-1; a thread
-        // per (row group, column) of each
-        const int npad = Dp - D;
-        for (int r = tid / 16; r < Dp; r += blockDim.x / 16)
-            if ((tid & 15) < npad) A[r * ld + D + (tid & 15)] = r == D + (tid & 15) ? 1.0 : 0.0;
-        for (int r = D + tid / 64; r < Dp; r += blockDim.x / 64)
+        // identity padding of rows 16.. (no divisions): columns D..Dp-1 of every row, then rows
+        // D..Dp-1; a thread per (row group, column) of each
+        const int t = tid - 64, npad = Dp - D;
+        for (int r = SB + t / 16; r < Dp; r += 192 / 16)
+            if ((t & 15) < npad) A[r * ld + D + (t & 15)] = r == D + (t & 15) ? 1.0 : 0.0;
+        for (int r = max(D, SB) + t / 64; r < Dp; r += 3)
             for (int c = lane; c < D; c += 64) A[r * ld + c] = 0.0;
+        if (tid < Dp) y[tid] = bs_v;
     }
-    if (tid < Dp) y[tid] = bs_v;
-    if (tid == 0) s_ok = 1;
-    __syncthreads();
-    BA_STAMP(0);
-    if (wv == 0 && !solve_diag_block(A, y, dinv, vz, ld, 0, lane, D) && lane == 0) s_ok = 0;
     __syncthreads();
     for (int J0 = 0; J0 < Dp && s_ok; J0 += SB) {
         const int R0 = J0 + SB;

@@ -35,7 +35,8 @@ for blk in range(16):
         last = c
     print(line)
     prev = last
-print(f"back-substitution {v[40] - last}, total {v[40] - t0} ticks; load S {v[0] - v[41]}, pose update tail {v[42] - v[40]}")
+print(f"back-substitution {v[40] - last}, total {v[40] - t0} ticks; block 0 staged by wavefront 0 {v[0] - v[41]} "
+      f"(block 0's diag-wait = its factorisation beside the other wavefronts' load of S), pose update tail {v[42] - v[40]}")
 b2 = v[2 + 3 * 2]   # block 2 panel end = start of its lookahead phase
 if v[44] > b2:
     print(f"block 2 lookahead by wave: w0 trailing tile {v[44] - b2}, w0 diag factor {v[45] - v[44]} (ends {v[45] - b2}), "
