@@ -7,7 +7,8 @@ from collections import defaultdict
 from pathlib import Path
 
 
-def main(d):
+def collect(d):
+    """{kernel: {counter: mean per-dispatch value}}"""
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(Path(d).rglob("run_counter_collection.csv")):
         per = defaultdict(lambda: defaultdict(float))
@@ -17,10 +18,14 @@ def main(d):
         for (name, _), cs in per.items():
             for c, v in cs.items():
                 acc[name][c].append(v)
-    for name, cs in sorted(acc.items()):
+    return {n: {c: sum(vs) / len(vs) for c, vs in cs.items()} for n, cs in acc.items()}
+
+
+def main(d):
+    for name, cs in sorted(collect(d).items()):
         print(name)
-        for c, vs in sorted(cs.items()):
-            print(f"   {c:24s} {sum(vs) / len(vs):16.1f}")
+        for c, v in sorted(cs.items()):
+            print(f"   {c:24s} {v:16.1f}")
 
 
 if __name__ == "__main__":
