@@ -2,7 +2,7 @@
 # A/B on one GPU box: tools/ab/lib_base.so (a build of the base commit) against the in-tree library,
 # alternating, after the GPU parity tests of the in-tree build.  KB_ARGS is passed to kbench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TESTS=${TESTS:-"tests/test_extractor_gpu.py tests/test_matcher_gpu.py"}

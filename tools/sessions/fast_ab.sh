@@ -1,7 +1,7 @@
 #!/bin/bash
 # Extractor tuning sweep: parity tests, then kbench over knobs (and the previous commit's library).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -m pytest tests/test_extractor_gpu.py -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_ab.log 2>&1 || { tail -30 gpurun_out/pytest_ab.log; exit 1; }

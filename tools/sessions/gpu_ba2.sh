@@ -1,6 +1,6 @@
 #!/bin/bash
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_ba_gpu.py tests/test_cpp_dropin_gpu.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/ba2.log 2>&1 || { tail -20 gpurun_out/ba2.log; exit 3; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # which LocalBA build fails the oracle comparison (tools/ab/lib_*.so via ORBSLAM2_AMD_LIB, then in-tree)
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 PT="python -u -m pytest -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Baseline session: the whole -m gpu suite, then kernel stage times on pan / textured / G frames.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/base_pytest.log 2>&1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Quick GPU iteration: extractor/matcher parity tests + kernel stage timings (kbench).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TESTS=${TESTS:-"tests/test_extractor_gpu.py tests/test_matcher_gpu.py"}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 GPU check: new matcher rows' parity, then the exchange path at N = 1 and a short bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests/test_init_gpu.py tests/test_projection_reloc_gpu.py tests/test_projection_motion_gpu.py tests/test_projection_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r3a_pytest.log 2>&1 || { tail -30 gpurun_out/r3a_pytest.log; exit 2; }

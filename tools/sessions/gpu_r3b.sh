@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 check: extractor + BA parity of the in-tree build, then extractor A/B (abn) and LocalBA A/B.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 python tools/diag/desc_determinism.py 2>&1 | tail -2 || exit 2

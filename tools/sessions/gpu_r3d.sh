@@ -1,7 +1,7 @@
 #!/bin/bash
 # describe parity + determinism, the new matcher legs and the headline fields on a short bench
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 python tools/diag/desc_determinism.py 2>&1 | tail -1 || exit 2

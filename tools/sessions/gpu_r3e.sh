@@ -1,7 +1,7 @@
 #!/bin/bash
 # FAST strip order: parity, kbench A/B (pan + textured) and FETCH_SIZE vs tools/ab/lib_*.so
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests/test_extractor_gpu.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r3e_ext.log 2>&1 || { tail -20 gpurun_out/r3e_ext.log; exit 3; }
