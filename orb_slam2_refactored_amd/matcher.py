@@ -379,6 +379,40 @@ def search_by_projection_device(batch: dict, kp_match=None, n_matches=None, stre
 
 _MOTION_KEYS = ("kp_begin", "kp_xy", "kp_octave", "kp_uright", "kp_desc", "kp_angle", "kp_claimed", "bounds",
                 "mp_begin", "mp_valid", "mp_proj", "mp_octave", "mp_desc", "mp_has_obs", "mp_angle", "motion")
+_MOTION_DT = (np.int32, np.float32, np.int32, np.float32, np.uint8, np.float32, np.uint8, np.float32,
+              np.int32, np.uint8, np.float32, np.int32, np.uint8, np.uint8, np.float32, np.int32)
+
+# Element counts the C-ABI batches read per array: (row count symbol, elements per row).  F = frames or
+# pairs, F1 = F + 1, K / M / Q = total keypoints / map points / F1-keypoints.  The kernels index by
+# these counts with no bound of their own, so a shorter array would be read out of bounds.
+_BATCH_ROWS = {
+    "kp_begin": ("F1", 1), "q_begin": ("F1", 1), "mp_begin": ("F1", 1),
+    "kp_xy": ("K", 2), "kp_octave": ("K", 1), "kp_uright": ("K", 1), "kp_desc": ("K", 32), "kp_angle": ("K", 1),
+    "kp_claimed": ("K", 1), "bounds": ("F", 4), "pose": ("F", 12), "camera": ("F", 4), "motion": ("F", 1),
+    "mp_valid": ("M", 1), "mp_proj": ("M", 3), "mp_octave": ("M", 1), "mp_desc": ("M", 32), "mp_has_obs": ("M", 1),
+    "mp_angle": ("M", 1), "mp_xw": ("M", 3), "mp_max_min": ("M", 2),
+    "q_octave": ("Q", 1), "q_desc": ("Q", 32), "q_angle": ("Q", 1), "prev_matched": ("Q", 2),
+}
+
+
+def _check_batch_rows(batch: dict, keys, dims: dict, what: str):
+    for k in keys:
+        a = batch.get(k)
+        if a is None:
+            continue
+        sym, per = _BATCH_ROWS[k]
+        want = dims[sym] * per
+        n = int(a.numel()) if hasattr(a, "numel") else int(np.size(a))
+        if n < want:
+            raise ValueError(f"{what}: {k} has {n} elements, needs {want} ({sym} = {dims[sym]} rows x {per})")
+
+
+def _check_device_dtypes(batch: dict, keys_dtypes, what: str):
+    import torch
+    for k, dt in keys_dtypes:
+        t = batch.get(k)
+        if t is not None and (not t.is_contiguous() or t.dtype != getattr(torch, np.dtype(dt).name)):
+            raise ValueError(f"{what}: {k} must be a contiguous {np.dtype(dt).name} tensor")
 
 
 def search_by_projection_motion_device(batch: dict, kp_match=None, n_matches=None, stream=None):
@@ -392,6 +426,8 @@ def search_by_projection_motion_device(batch: dict, kp_match=None, n_matches=Non
     F = eb.numel() - 1
     K = int(batch["kp_xy"].shape[0])
     M = int(batch["mp_proj"].shape[0])
+    _check_device_dtypes(batch, zip(_MOTION_KEYS, _MOTION_DT), "search_by_projection_motion_device")
+    _check_batch_rows(batch, _MOTION_KEYS, {"F": F, "F1": F + 1, "K": K, "M": M}, "search_by_projection_motion_device")
     if kp_match is None:
         kp_match = torch.empty(max(K, 1), dtype=torch.int32, device=eb.device)
     if n_matches is None:
@@ -422,6 +458,7 @@ def SearchForInitialization(batch: dict, device: int = 0):
         raise ValueError("prev_matched must be a contiguous float32 array (updated in place)")
     P = len(arrs["kp_begin"]) - 1
     K, Q = int(arrs["kp_begin"][-1]), int(arrs["q_begin"][-1])
+    _check_batch_rows(arrs, arrs.keys(), {"F": P, "F1": P + 1, "K": K, "Q": Q}, "SearchForInitialization")
     m12 = np.empty(max(Q, 1), np.int32)
     nm = np.empty(max(P, 1), np.int32)
     ib = InitBatch(P, K, Q, *[ptr(arrs[k]) if k in arrs else None for k, _ in _INIT_KEYS], int(batch["window"]),
@@ -442,13 +479,10 @@ def search_for_initialization_device(batch: dict, matches12=None, n_matches=None
     P = kb.numel() - 1
     if qb.numel() != P + 1:
         raise ValueError("kp_begin and q_begin must both have n_pairs + 1 entries")
-    for k, dt in _INIT_KEYS:
-        t = batch.get(k)
-        if t is not None and (not t.is_contiguous() or t.dtype != getattr(torch, np.dtype(dt).name)):
-            raise ValueError(f"{k} must be a contiguous {np.dtype(dt).name} tensor")
+    _check_device_dtypes(batch, _INIT_KEYS, "search_for_initialization_device")
     K, Q = int(batch["kp_xy"].shape[0]), int(batch["q_octave"].shape[0])
-    if batch["prev_matched"].shape[0] != Q:
-        raise ValueError("prev_matched must be [total_q, 2]")
+    _check_batch_rows(batch, [k for k, _ in _INIT_KEYS], {"F": P, "F1": P + 1, "K": K, "Q": Q},
+                      "search_for_initialization_device")
     if matches12 is None:
         matches12 = torch.empty(max(Q, 1), dtype=torch.int32, device=kb.device)
     if n_matches is None:
@@ -489,6 +523,8 @@ def SearchByProjectionReloc(batch: dict, device: int = 0):
         return ptr(a)
     F = len(batch["kp_begin"]) - 1
     K, M = int(batch["kp_begin"][-1]), int(batch["mp_begin"][-1])
+    _check_batch_rows(batch, [k for k, _ in _RELOC_KEYS], {"F": F, "F1": F + 1, "K": K, "M": M},
+                      "SearchByProjectionReloc")
     rb, _sf = _reloc_struct(batch, conv, K, M)
     km = np.empty(max(K, 1), np.int32)
     nm = np.empty(max(F, 1), np.int32)
@@ -504,10 +540,9 @@ def search_by_projection_reloc_device(batch: dict, kp_match=None, n_matches=None
     kb = batch["kp_begin"]
     F = kb.numel() - 1
     K, M = int(batch["kp_xy"].shape[0]), int(batch["mp_xw"].shape[0])
-    for k, dt in _RELOC_KEYS:
-        t = batch.get(k)
-        if t is not None and (not t.is_contiguous() or t.dtype != getattr(torch, np.dtype(dt).name)):
-            raise ValueError(f"{k} must be a contiguous {np.dtype(dt).name} tensor")
+    _check_device_dtypes(batch, _RELOC_KEYS, "search_by_projection_reloc_device")
+    _check_batch_rows(batch, [k for k, _ in _RELOC_KEYS], {"F": F, "F1": F + 1, "K": K, "M": M},
+                      "search_by_projection_reloc_device")
     if kp_match is None:
         kp_match = torch.empty(max(K, 1), dtype=torch.int32, device=kb.device)
     if n_matches is None:
