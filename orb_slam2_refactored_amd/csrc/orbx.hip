@@ -1564,7 +1564,10 @@ __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, i
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
+#ifndef QT_WAVES_DEF
+#define QT_WAVES_DEF 4   // wavefronts per SIMD = workgroups per CU (4 wavefronts each)
+#endif
+__global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
                                                        const uint32_t* __restrict__ slots, const CellDev* cells,
                                                        uint32_t* __restrict__ Pbuf, uint32_t* __restrict__ Tbuf,
                                                        uint32_t* __restrict__ sel, int* __restrict__ sel_cnt, int NC,
@@ -2586,7 +2589,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     {
         hipFuncAttributes fa{};
         const size_t stat = hipFuncGetAttributes(&fa, (const void*)quadtree_kernel) == hipSuccess ? fa.sharedSizeBytes : 1024;
-        for (int t = 4; t >= 2; t--) {
+        for (int t = QT_WAVES_DEF; t >= 2; t--) {
             const long long room = (long long)(160 * 1024 / t) - (long long)stat - (long long)node_lds;
             const int p = (int)std::min<long long>(2048, room / 8) & ~63;
             if (p >= 512) { PTC = p; break; }
