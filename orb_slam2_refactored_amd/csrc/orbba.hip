@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include <chrono>
@@ -45,6 +46,8 @@ struct BACtl {
     int trials;    // LM trials since the start of the LocalBA call (both optimize() calls; test hook)
     int stopped;   // the force-stop flag ended the loop
     int seq;       // host snapshot sequence id (written last; see ba_decide_step)
+    int n_active;  // level-0 edges after the outlier classification between the optimize() calls
+    int pad_;
     double chi_out;
 };
 
@@ -1353,18 +1356,28 @@ __device__ __forceinline__ void snapshot_to_host(const BACtl& snap, int seq, BAC
 
 
 // final outlier classification (Optimizer.cc:644-670, :686-699) + chi2 out
-__global__ void ba_ctl_start_kernel(BADev b, int iters) {
+// check_active (the second optimize()): with no level-0 edge left, g2o's optimize() has nothing to do
+// (initializeOptimization(0) finds no active edge); the loop ends here and the snapshot the host waits
+// for as step 0's (`seq` in ring slot `host_snap`) is written by this kernel, so the host never needs the
+// classification on its side.
+__global__ void ba_ctl_start_kernel(BADev b, int iters, int check_active, BACtl* host_snap, int seq) {
     BACtl* c = b.ctl;
     c->it = 0;
     c->q = 0;
     c->nbad = 0;
-    c->done = iters <= 0 ? 1 : 0;
+    const bool idle = check_active && c->n_active == 0;
+    c->done = (iters <= 0 || idle) ? 1 : 0;
     c->maxdiag_bits = 0;
     c->need_lin = 1;
     c->iters_max = iters;
     c->iters_done = 0;
     c->chi_out = 0;
     c->rho = 0;
+    if (idle) {
+        BACtl snap = *c;
+        snap.seq = -1;
+        snapshot_to_host(snap, seq, host_snap);
+    }
 }
 
 __global__ void ba_ctl_stop_kernel(BADev b) { b.ctl->done = 1; }
@@ -1380,18 +1393,24 @@ __global__ void ba_classify_kernel(BADev b, uint8_t* outlier, double* chi2o, uin
     }
     if (rX && e < b.N)
         for (int j = 0; j < 3; j++) rX[3 * e + j] = b.X[3 * e + j];
-    if (e >= b.E) return;
-    const double maxc = b.stereo[e] ? 7.815 : 5.991;
-    const double c = edge_chi2(b, e);
-    double Xc[3];
-    const int pi = b.ek[e];
-    se3_map(b.q + 4 * pi, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
-    const uint8_t bad = (c > maxc || !(Xc[2] > 0.0)) ? 1 : 0;
-    if (outlier) outlier[e] = bad;
-    if (chi2o) chi2o[e] = c;
-    if (set_level) {
-        if (bad) level[e] = 1;
-        b.robust[e] = 0;
+    uint8_t bad = 1;
+    if (e < b.E) {
+        const double maxc = b.stereo[e] ? 7.815 : 5.991;
+        const double c = edge_chi2(b, e);
+        double Xc[3];
+        const int pi = b.ek[e];
+        se3_map(b.q + 4 * pi, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
+        bad = (c > maxc || !(Xc[2] > 0.0)) ? 1 : 0;
+        if (outlier) outlier[e] = bad;
+        if (chi2o) chi2o[e] = c;
+        if (set_level) {
+            if (bad) level[e] = 1;
+            b.robust[e] = 0;
+        }
+    }
+    if (set_level) {   // the edges left at level 0 (the set_level launch covers E only: no early return above)
+        const int n = __syncthreads_count(!bad);
+        if (threadIdx.x == 0 && n) atomicAdd(&b.ctl->n_active, n);
     }
 }
 
@@ -1472,6 +1491,8 @@ struct HostStructure {
     std::vector<int2> blk_pair;
     std::vector<int> blk_index, fs_beg, fs_slot, fs_hp, sl, sp, cur;   // scratch (capacity kept across calls)
     std::vector<uint8_t> pa, la;
+    std::vector<unsigned long long> col;   // per-pose bitsets over the points (pair blocks)
+    std::vector<int> slot_of;              // [point][pose] -> free slot (pair blocks)
     int np = 0, nl = 0;
 };
 
@@ -1556,7 +1577,62 @@ void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint
         }
     }
     // pose-pair blocks (i1 <= i2): pass 1 counts the pairs per block, pass 2 fills them, from each
-    // point's free slots (slot order) with their Hessian pose index.
+    // point's free slots (slot order) with their Hessian pose index.  Reference order inside a block:
+    // points ascending, then (slot a, slot c) in the point's slot order with pose(a) <= pose(c).
+    //
+    // Bitset path: a point that sees every free pose at most once (a MapPoint holds one observation
+    // per keyframe) has exactly one pair in each block it touches, so block (i1, i2) holds the points
+    // of col[i1] & col[i2] (per-pose bitsets over the points) in ascending order: counts are popcounts
+    // and the fill walks the set bits, with the same result as the two nested slot loops below, which
+    // remain for problems where some point repeats a pose.
+    {
+        const int W = (nl + 63) >> 6;
+        s.col.assign((size_t)np * W, 0ull);
+        s.slot_of.resize((size_t)std::max(nl, 1) * std::max(np, 1));   // read only where written
+        const int* fh = s.fs_hp.data();
+        const int* fb = s.fs_beg.data();
+        const int* fsl = s.fs_slot.data();
+        unsigned long long* col = s.col.data();
+        int* so = s.slot_of.data();
+        bool dup = false;
+        for (int l = 0; l < nl && !dup; l++)
+            for (int a = fb[l]; a < fb[l + 1]; a++) {
+                unsigned long long& w = col[(size_t)fh[a] * W + (l >> 6)];
+                const unsigned long long bit = 1ull << (l & 63);
+                dup |= (w & bit) != 0;
+                w |= bit;
+                so[(size_t)l * np + fh[a]] = fsl[a];
+            }
+        if (!dup) {
+            s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0);
+            int total = 0;
+            for (int i1 = 0; i1 < np; i1++)
+                for (int i2 = i1; i2 < np; i2++) {
+                    const unsigned long long* c1 = col + (size_t)i1 * W;
+                    const unsigned long long* c2 = col + (size_t)i2 * W;
+                    int cnt = 0;
+                    for (int w = 0; w < W; w++) cnt += __builtin_popcountll(c1[w] & c2[w]);
+                    if (cnt == 0 && i1 != i2) continue;
+                    s.blk_i1.push_back(i1);
+                    s.blk_i2.push_back(i2);
+                    total += cnt;
+                    s.blk_beg.push_back(total);
+                }
+            s.blk_pair.resize(total);
+            int2* out = s.blk_pair.data();
+            for (size_t k = 0; k < s.blk_i1.size(); k++) {
+                const int i1 = s.blk_i1[k], i2 = s.blk_i2[k];
+                const unsigned long long* c1 = col + (size_t)i1 * W;
+                const unsigned long long* c2 = col + (size_t)i2 * W;
+                for (int w = 0; w < W; w++)
+                    for (unsigned long long m = c1[w] & c2[w]; m; m &= m - 1) {
+                        const int l = (w << 6) + __builtin_ctzll(m);
+                        *out++ = make_int2(so[(size_t)l * np + i1], so[(size_t)l * np + i2]);
+                    }
+            }
+            return;
+        }
+    }
     s.blk_index.assign((size_t)np * np, 0);
     {
         const int* fh = s.fs_hp.data();
@@ -1751,6 +1827,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     // and dense factorisation sees exact zeros in their place), and a vertex left without active edges
     // keeps a zero Hessian block (+ lambda), i.e. a zero update, as if it were not in the problem.
     bool have_structure = false;
+    bool have_classified = false;   // the outlier classification ran (second optimize())
     auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
         if (!have_structure) {
             build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs);
@@ -1760,9 +1837,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         const int nblk = (int)hs.blk_i1.size();
         *iters_out = 0;
         *chi_out = 0;
-        int n_active = 0;   // level-0 edges of this optimize()
-        for (int e = 0; e < E; e++) n_active += level[e] == 0;
-        if (Ea == 0 || n_active == 0 || np + nl == 0) return ORB_OK;
+        // (the second optimize()'s level-0 edge count is on the device: ba_ctl_start_kernel ends the
+        // loop at once when the classification left none)
+        if (Ea == 0 || np + nl == 0) return ORB_OK;
         // reduced system: in LDS up to 21 free keyframes (D <= 128), else in HBM (ba_solve_global_kernel)
         const bool glob = D > 128 || solve_lds_doubles(D) * 8 + 4096 > 160 * 1024;
         if (glob && np > ORBBA_MAX_FREE_KEYFRAMES) {
@@ -1855,16 +1932,28 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
         if (nblk) ORB_HIP_TRY(hipMemsetAsync(b.blk_done, 0, (size_t)nblk * 4, st));
         const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
-        ORB_HIP_TRY(hipFuncSetAttribute(glob ? (const void*)ba_solve_global_kernel : (const void*)ba_solve_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)std::max<size_t>(ldlt_lds, 1024)));
+        {   // the dynamic LDS limit is a process-wide attribute of the kernel: raised (a host call) only
+            // when a call needs more than any call before it on this device, never lowered
+            static std::mutex mu;
+            static size_t lim[64][2] = {};
+            const size_t need = std::max<size_t>(ldlt_lds, 1024);
+            std::lock_guard<std::mutex> lk(mu);
+            size_t& cur = lim[device & 63][glob ? 1 : 0];
+            if (need > cur) {
+                ORB_HIP_TRY(hipFuncSetAttribute(glob ? (const void*)ba_solve_global_kernel : (const void*)ba_solve_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+                cur = need;
+            }
+        }
         const dim3 gg((nl * 8 + 63) / 64);   // 8 lanes per point
         // The LM loop runs on the device (ba_decide_step advances it); the host keeps LOOKAHEAD
         // steps enqueued and reads each step's control snapshot from a pinned ring, so no trial
         // waits for a host round trip.  Steps enqueued past the end return immediately.
         mark("structure upload enqueued");
-        hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, iters);
         constexpr int LOOKAHEAD = 2;
+        const int first_seq = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;   // step 0's id (slot 0)
+        hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, iters, have_classified ? 1 : 0,
+                           C.d_ring + 0, first_seq);
         const int max_steps = iters * 10;
         int enq = 0, seen = 0;
         int ids[LOOKAHEAD] = {0, 0};
@@ -1935,13 +2024,15 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if ((rc = optimize(5, &res->iterations[0], &res->chi2[0]))) return rc;
         if (!stopped() && !hook_stopped) {   // doMore (:639-642)
             // tag outliers (level 1) and drop the robust kernels (:644-670)
+            // (no host copy of the levels: the structure is not rebuilt and the device counts the
+            // level-0 edges for ba_ctl_start_kernel)
             if (E) {
                 hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, (uint8_t*)nullptr,
                                    (double*)nullptr, d_level, 1, (double*)nullptr, (double*)nullptr, (double*)nullptr);
-                ORB_HIP_TRY(hipMemcpyAsync(level.data(), d_level, E, hipMemcpyDeviceToHost, st));
-                ORB_HIP_TRY(hipStreamSynchronize(st));
+                ORB_HIP_TRY(hipGetLastError());
+                have_classified = true;
             }
-            mark("classify + level copy");
+            mark("classify enqueued");
             if ((rc = optimize(10, &res->iterations[1], &res->chi2[1]))) return rc;
         }
     }
