@@ -104,3 +104,20 @@ def test_local_ba_stop_flag_async():
     assert g["ran"]
     assert sum(g["iterations"]) <= sum(full["iterations"])
     assert time.perf_counter() - t0 < 5
+
+
+def test_local_ba_all_outliers_then_normal(oracle):
+    """Every edge an outlier after optimize(5): the second optimize() has no level-0 edge, which the
+    device learns on its own (no host copy of the levels) and ends at once with 0 iterations, as the
+    oracle's g2o restatement; the next call on the same context runs normally."""
+    pr = make_ba_problem(7, n_kf=6, n_pts=300, n_fixed=1)
+    rng = np.random.default_rng(7)
+    obs = np.array(pr["edge_obs"], np.float64)
+    obs[:, :2] += rng.uniform(1000, 3000, (len(obs), 2)) * rng.choice([-1, 1], (len(obs), 2))
+    pr["edge_obs"] = obs
+    g = LocalBundleAdjustment(pr)
+    o = oracle.local_ba(pr)
+    assert g["edge_outlier"].all() and o["edge_outlier"].all()
+    assert tuple(g["iterations"]) == tuple(o["iterations"]) and g["iterations"][1] == 0
+    pr2 = make_ba_problem(3, n_kf=5, n_pts=200, n_fixed=1)
+    compare(LocalBundleAdjustment(pr2), oracle.local_ba(pr2))
