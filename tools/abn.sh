@@ -21,6 +21,7 @@ for set in "${SETA[@]}"; do
   for i in $(seq 1 $REPS); do
     for lib in tools/ab/lib_*.so new $ENVV; do
       ev=""
+      [[ "$lib" == *.so && ! -e "$lib" ]] && continue   # no tools/ab libraries: the glob stays literal
       if [ "$lib" = new ]; then unset ORBSLAM2_AMD_LIB; v=new;
       elif [[ "$lib" == *=* ]]; then unset ORBSLAM2_AMD_LIB; v=env_${lib//=/_}; ev=$lib;
       else export ORBSLAM2_AMD_LIB=$PWD/$lib; v=$(basename $lib .so); fi
