@@ -2,8 +2,8 @@
 # Round evidence in one GPU session: parity tests, smoke, PMC traffic passes, the bench line (reading
 # the fresh traffic json) and the rocprofv3 kernel-trace stats of the C2 bench leg alone (its per-kernel
 # averages must agree with the bench line's live HIP-event launch times), then of the secondary legs.
-# Every GPU step has its own time limit; the chain stops at the first failure.  Outputs are copied to
-# profiles/ by tools/collect_profiles.py on the CPU side.
+# Every GPU step has its own time limit; the chain stops at the first failure.  Outputs land in
+# gpurun_out/profiles_<tag>/ and are copied into profiles/ on the CPU side after the call.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
