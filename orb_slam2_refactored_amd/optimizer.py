@@ -13,6 +13,15 @@ import numpy as np
 from ._lib import BAProblem, BAResult, PoseBatch, PoseResult, check, lib, ptr, stream_ptr, tptr
 
 
+def _need(arrays: dict, counts: dict, what: str):
+    """Refuse arrays with fewer elements than the C-ABI reads from them (it has no bound of its own)."""
+    for name, want in counts.items():
+        a = arrays[name]
+        n = int(a.numel()) if hasattr(a, "numel") else int(np.size(a))
+        if n < want:
+            raise ValueError(f"{what}: {name} has {n} elements, needs {want}")
+
+
 def LocalBundleAdjustment(problem: dict, stop_flag=None, device: int = 0) -> dict:
     keep = []
 
@@ -21,6 +30,9 @@ def LocalBundleAdjustment(problem: dict, stop_flag=None, device: int = 0) -> dic
         keep.append(a)
         return ptr(a)
 
+    P0, N0, E0 = len(problem["pose_R"]), len(problem["points"]), len(problem["edge_point"])
+    _need(problem, {"pose_R": 9 * P0, "pose_t": 3 * P0, "pose_fixed": P0, "points": 3 * N0, "edge_pose": E0,
+                    "edge_obs": 3 * E0, "edge_inv_sigma2": E0, "edge_cam": 5 * E0}, "LocalBundleAdjustment")
     pr = BAProblem(len(problem["pose_R"]), k(problem["pose_R"], np.float64), k(problem["pose_t"], np.float64),
                    k(problem["pose_fixed"], np.uint8), len(problem["points"]), k(problem["points"], np.float64),
                    len(problem["edge_point"]), k(problem["edge_point"], np.int32), k(problem["edge_pose"], np.int32),
@@ -52,6 +64,9 @@ def _pose_arrays(batch: dict):
         return ptr(a)
 
     n = len(batch["edge_begin"]) - 1
+    E = int(batch["edge_begin"][-1]) if n >= 0 and len(batch["edge_begin"]) else 0
+    _need(batch, {"pose_R": 9 * n, "pose_t": 3 * n, "cam": 5 * n, "xw": 3 * E, "obs": 3 * E, "inv_sigma2": E},
+          "PoseOptimization")
     pb = PoseBatch(n, k(batch["edge_begin"], np.int32), k(batch["pose_R"], np.float64), k(batch["pose_t"], np.float64),
                    k(batch["cam"], np.float64), k(batch["xw"], np.float64), k(batch["obs"], np.float64),
                    k(batch["inv_sigma2"], np.float64))
@@ -81,6 +96,14 @@ def pose_optimization_device(batch: dict, out: dict | None = None, stream=None) 
     eb = batch["edge_begin"]
     n = eb.numel() - 1
     E = batch["inv_sigma2"].numel()
+    _need(batch, {"pose_R": 9 * n, "pose_t": 3 * n, "cam": 5 * n, "xw": 3 * E, "obs": 3 * E},
+          "pose_optimization_device")
+    for name in ("pose_R", "pose_t", "cam", "xw", "obs", "inv_sigma2"):
+        t = batch[name]
+        if t.dtype != torch.float64 or not t.is_contiguous():
+            raise ValueError(f"pose_optimization_device: {name} must be a contiguous float64 tensor")
+    if eb.dtype != torch.int32 or not eb.is_contiguous():
+        raise ValueError("pose_optimization_device: edge_begin must be a contiguous int32 tensor")
     dev = eb.device
     if out is None:
         out = dict(pose_R=torch.empty((n, 9), dtype=torch.float64, device=dev),
