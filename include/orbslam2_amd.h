@@ -599,6 +599,15 @@ int orbba_pose_optimization_device(const orbba_pose_batch* in, orbba_pose_result
 const char* orb_last_error(void);
 int orb_device_count(void);
 
+/* Compact descriptor block for the multi-GPU exchange (BASELINE configs[4]: frame i matched to i-1
+ * across shard boundaries; no reference counterpart, the reference runs one camera stream): frame f's
+ * first counts[f] descriptor rows of desc (n_frames x cap x 32 bytes, the orbx_extract_batch_device
+ * layout) go to out rows [incl[f] - counts[f], incl[f]), with incl the inclusive prefix sum of counts.
+ * counts / incl / desc / out are device memory; enqueue only on `stream`.  One launch, 32-byte rows as
+ * two 16-byte vector copies. */
+int orbx_pack_descriptors(const uint8_t* desc, int32_t cap, const int32_t* counts, const int32_t* incl,
+                          int32_t n_frames, uint8_t* out, void* stream);
+
 /* Stage timing with HIP events recorded as part of each kernel's dispatch (hipExtLaunchKernel start /
  * stop events: the kernel's own duration) for the stages 0 pyramid, 1 FAST cells, 2 quadtree,
  * 3 describe.  enable > 0 times every stage, enable < 0 only the stages in the bitmask -enable

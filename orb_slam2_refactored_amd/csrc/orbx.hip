@@ -2862,6 +2862,21 @@ static int check_fault(orbx_extractor* h) {
     return ORB_OK;
 }
 
+namespace orbamd {
+// One workgroup per frame: rows [0, counts[f]) of the frame's slots -> out rows from incl[f] - counts[f],
+// each 32-byte row as two uint4 (lanes take consecutive 16-byte halves: coalesced both ways).
+__global__ __launch_bounds__(256) void pack_rows_kernel(const uint4* __restrict__ desc, int cap,
+                                                        const int* __restrict__ counts, const int* __restrict__ incl,
+                                                        uint4* __restrict__ out) {
+    const int f = blockIdx.x;
+    const int n = counts[f];
+    const long long o = (long long)(incl[f] - n) * 2;
+    const uint4* src = desc + (long long)f * cap * 2;
+    for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) out[o + i] = src[i];
+}
+
+}  // namespace orbamd
+
 extern "C" {
 
 int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
@@ -3114,6 +3129,19 @@ int orbx_profile_enable(orbx_extractor* h, int enable) {
     std::lock_guard<std::mutex> lk(h->mu);
     h->prof = enable > 0 ? 0xf : (-enable) & 0xf;   // > 0: every stage; < 0: the stages of bitmask -enable
 
+    return ORB_OK;
+}
+
+int orbx_pack_descriptors(const uint8_t* desc, int32_t cap, const int32_t* counts, const int32_t* incl,
+                          int32_t n_frames, uint8_t* out, void* stream) {
+    ORB_CHECK_ARG(n_frames >= 0 && cap >= 0, "negative sizes");
+    if (n_frames == 0) return ORB_OK;
+    ORB_CHECK_ARG(desc && counts && incl && out, "null argument");
+    ORB_CHECK_ARG(((reinterpret_cast<uintptr_t>(desc) | reinterpret_cast<uintptr_t>(out)) & 15) == 0,
+                  "desc / out must be 16-byte aligned");
+    hipLaunchKernelGGL(orbamd::pack_rows_kernel, dim3((unsigned)n_frames), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint4*>(desc), (int)cap, counts, incl, reinterpret_cast<uint4*>(out));
+    ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
 

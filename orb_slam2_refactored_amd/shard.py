@@ -27,6 +27,8 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+from ._lib import check, lib, stream_ptr, tptr
+
 
 def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous shard [start, start+count) of n_total frames for `rank` (sizes differ by <= 1)."""
@@ -210,8 +212,16 @@ class CompactExchange:
                 self.recv[i] = torch.zeros((self.world * (maxtot + maxtot // 4), 32), dtype=torch.uint8,
                                            device=self.device)
             n = tot[self.rank]
-            if n:
-                # row r of the block: frame fr = the frame whose prefix range holds r, slot r - start[fr]
+            if n and self.cuda:
+                # one HIP launch (orbx_pack_descriptors) from the device-side counts of this rank; the
+                # torch gather below costs ~4.7 ms per 8192-frame step on the byte-wise index_select
+                cnt = self.counts_all[i].view(self.world, self.frames)[self.rank]
+                incl = torch.cumsum(cnt, 0, dtype=torch.int32)
+                check(lib().orbx_pack_descriptors(tptr(src.desc), self.cap, tptr(cnt), tptr(incl), self.frames,
+                                                  tptr(self.send[i]), stream_ptr(self.side)),
+                      "orbx_pack_descriptors")
+            elif n:
+                # (CPU / gloo) row r of the block: frame fr = the frame whose prefix range holds r, slot r - start[fr]
                 cnt = mine.to(self.device)
                 start = torch.cumsum(cnt, 0) - cnt
                 fr = torch.repeat_interleave(torch.arange(self.frames, device=self.device), cnt, output_size=n)

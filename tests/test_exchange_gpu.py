@@ -1,0 +1,51 @@
+"""The multi-GPU descriptor exchange on the device: CompactExchange on CUDA packs each step's ragged
+descriptor block with the HIP kernel behind orbx_pack_descriptors (single process, world 1: the
+payload "all-gather" is the local copy), and the block must equal the concatenation of every frame's
+valid rows byte for byte (ragged counts including 0 and the full slot capacity)."""
+import pytest
+import torch
+
+from orb_slam2_refactored_amd import _lib
+from orb_slam2_refactored_amd.shard import CompactExchange
+
+pytestmark = pytest.mark.gpu
+
+
+def _slots(ex, k, seed, frames, cap):
+    g = torch.Generator().manual_seed(seed)
+    loc = ex.local(k)
+    counts = torch.randint(0, cap + 1, (frames,), generator=g, dtype=torch.int32)
+    counts[0], counts[-1] = 0, cap
+    desc = torch.randint(0, 256, (frames, cap, 32), generator=g, dtype=torch.uint8)
+    loc.desc.copy_(desc.cuda())
+    loc.counts.copy_(counts.cuda())
+    return desc, counts
+
+
+@pytest.mark.parametrize("frames,cap", [(7, 33), (64, 2024)])
+def test_compact_exchange_cuda_pack(frames, cap):
+    ex = CompactExchange(frames, cap, "cuda")
+    want = {}
+    for k in range(4):
+        desc, counts = _slots(ex, k, 100 + k, frames, cap)
+        last = (desc, counts)
+        want[k] = torch.cat([desc[f, :int(counts[f])] for f in range(frames)])
+        ex.publish(k)
+        if k >= 1:
+            ex.wait(k - 1)
+            torch.cuda.synchronize()
+            assert torch.equal(ex.block(k - 1, 0).cpu(), want[k - 1])
+    ex.drain()
+    torch.cuda.synchronize()
+    assert torch.equal(ex.block(3, 0).cpu(), want[3])
+    desc, counts = last
+    for f in (0, frames // 2, frames - 1):
+        assert torch.equal(ex.frame(3, 0, f).cpu(), desc[f, :int(counts[f])])
+
+
+def test_pack_descriptors_rejects_misaligned():
+    d = torch.zeros(2 * 4 * 32 + 1, dtype=torch.uint8, device="cuda")
+    c = torch.ones(2, dtype=torch.int32, device="cuda")
+    with pytest.raises(_lib.OrbError):
+        _lib.check(_lib.lib().orbx_pack_descriptors(_lib.tptr(d[1:]), 4, _lib.tptr(c), _lib.tptr(c), 2,
+                                                    _lib.tptr(d), _lib.stream_ptr()), "orbx_pack_descriptors")
