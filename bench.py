@@ -73,44 +73,68 @@ def stage_bytes(W, H, n_kp):
             "describe": 60 * n_kp}                                    # keypoint + descriptor writes
 
 
-STAGE_KERNEL = {"pyramid": "pyramid_level_kernel", "fast_cells": "fast_cells_kernel", "quadtree": "quadtree_kernel",
-                "describe": "describe_kernel"}
+def stage_kernels(nlevels=8):
+    """Kernels per extractor stage and their launches per step: levels 1+2, 3+4, 5+6 are one
+    pyramid_pair_kernel launch each, an odd last level one pyramid_level_kernel (the bench's frames are
+    16-byte aligned, so pairing starts at level 1)."""
+    n = nlevels - 1
+    return {"pyramid": [("pyramid_pair_kernel", n // 2), ("pyramid_level_kernel", n % 2)],
+            "fast_cells": [("fast_cells_kernel", 1)], "quadtree": [("quadtree_kernel", 1)],
+            "describe": [("describe_kernel", 1)]}
 
 
-def measured_traffic(stage, frames, W, H, nfeat):
-    """HBM bytes per launch of `stage` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (profiles/*_traffic.json, tools/gpu_traffic.sh) of this exact workload, corrected by the
-    calibration measured in the same run (FETCH_SIZE counts half the bytes of streaming reads on
-    gfx950; WRITE_SIZE exact).  None when no profile of this workload is committed."""
-    files = sorted(ROOT.glob("profiles/*_traffic.json"))
-    for f in reversed(files):
+STAGE_KERNELS = stage_kernels()
+
+
+def traffic_profile(frames, W, H, nfeat):
+    """The newest committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile (profiles/*_traffic.json,
+    tools/gpu_traffic.sh) of this exact workload, or None."""
+    for f in sorted(ROOT.glob("profiles/*_traffic.json"), reverse=True):
         t = json.loads(f.read_text())
         wl = t.get("workload")
         if not isinstance(wl, dict):   # r01 files: the 128-frame C2 workload
             wl = {"frames": 128, "width": 1280, "height": 720, "nfeatures": 2000}
-        if (wl.get("frames"), wl.get("width"), wl.get("height"), wl.get("nfeatures")) != (frames, W, H, nfeat):
-            continue
-        k = t["kernels_per_dispatch"].get(STAGE_KERNEL.get(stage, ""))
-        if not k or k.get("fetch_bytes") is None:
-            return None
-        cal = t["calibration"]
-        fetch = k["fetch_bytes"] / cal.get("fetch_ratio_8B", 0.5)
-        write = (k.get("write_bytes") or 0.0) / cal.get("write_ratio_4B", 1.0)
-        return fetch + write
+        if (wl.get("frames"), wl.get("width"), wl.get("height"), wl.get("nfeatures")) == (frames, W, H, nfeat):
+            return t
     return None
 
 
-def measured_traffic_step(breakdown, brk_steps, frames, W, H, nfeat):
-    """Measured HBM bytes per step of every profiled extractor stage (measured_traffic x launches per
-    step), or None when a stage of this workload has no committed profile."""
+def kernel_traffic(t, kernel):
+    """HBM bytes per dispatch of `kernel` in profile `t`, corrected by the calibration measured in the same
+    run (FETCH_SIZE counts half the bytes of streaming reads on gfx950; WRITE_SIZE exact); None if absent.
+    A kernel launched several times per step (pyramid_pair_kernel) is the average over its dispatches."""
+    k = t["kernels_per_dispatch"].get(kernel)
+    if not k or k.get("fetch_bytes") is None:
+        return None
+    cal = t["calibration"]
+    return k["fetch_bytes"] / cal.get("fetch_ratio_8B", 0.5) + (k.get("write_bytes") or 0.0) / cal.get("write_ratio_4B", 1.0)
+
+
+def measured_traffic(stage, frames, W, H, nfeat):
+    """HBM bytes per launch of a single-kernel stage (the roofline's dominant kernel), or None."""
+    t = traffic_profile(frames, W, H, nfeat)
+    ks = STAGE_KERNELS.get(stage, [])
+    if t is None or len(ks) != 1:
+        return None
+    return kernel_traffic(t, ks[0][0])
+
+
+def measured_traffic_step(frames, W, H, nfeat, nlevels=8, profile=None):
+    """Measured HBM bytes per step of the whole extractor: every kernel's per-dispatch traffic x its
+    launches per step (3 pyramid_pair_kernel + 1 pyramid_level_kernel at 8 levels), or None when a kernel
+    of this workload has no committed profile (`profile`: a loaded *_traffic.json instead of the newest)."""
+    t = profile if profile is not None else traffic_profile(frames, W, H, nfeat)
+    if t is None:
+        return None
     tot = 0.0
-    for stage, (ms, launches) in breakdown.items():
-        if stage not in STAGE_KERNEL:
-            continue
-        t = measured_traffic(stage, frames, W, H, nfeat)
-        if t is None:
-            return None
-        tot += t * launches / max(brk_steps, 1)
+    for ks in stage_kernels(nlevels).values():
+        for kernel, launches in ks:
+            if not launches:
+                continue
+            b = kernel_traffic(t, kernel)
+            if b is None:
+                return None
+            tot += b * launches
     return tot
 
 
@@ -725,10 +749,317 @@ def search_by_bow_leg(dev, X, fv1_out, voc, steps, cpu):
     return r
 
 
+# ------------------------------------------------------------------------------------------ ranks
+class _StubExtractor:
+    """CPU stand-in used ONLY by `--stub` (tests/test_bench_launcher.py drives the N > 1 launcher and the
+    exchange over gloo without a GPU).  Fills the slots deterministically from the frame index; a stub
+    run says so in its JSON line ("stub": true) and is never a measurement."""
+
+    def __init__(self, nfeat):
+        self.cap = 48
+        self._on, self._launches = False, 0
+
+    def max_keypoints(self, rows, cols):
+        return self.cap
+
+    def extract_batch_device(self, frames, kps, desc, counts, stream=None):
+        import torch
+        g = frames.to(torch.int64)                         # global frame indices of this shard
+        counts.copy_(((g * 7 + 3) % (self.cap + 1)).to(torch.int32))
+        r = torch.arange(self.cap, dtype=torch.int64)
+        desc.copy_(((g[:, None, None] * 131 + r[None, :, None] * 17 + torch.arange(32)[None, None, :]) % 251)
+                   .to(torch.uint8))
+        kps.zero_()
+        if self._on:
+            self._launches += 1
+
+    def profile(self, enable=True, stages=None):
+        self._on, self._launches = enable, (0 if enable else self._launches)
+
+    def profile_read(self):
+        n = self._launches
+        return {"pyramid": (0.0, 4 * n), "fast_cells": (0.0, n), "quadtree": (0.0, n), "describe": (0.0, n)}
+
+    def batch_status(self, stream=None):
+        return 0
+
+
+class _StubMatcher:
+    def match_batch_device(self, descA, nA, descB, nB, out=None, stream=None, pair_b=None):
+        out.fill_(-1)
+        return out
+
+
+class Ranks:
+    """One process per GPU (torch.distributed over RCCL) or, with `stub`, CPU processes over gloo."""
+
+    def __init__(self, stub: bool):
+        import torch
+        import torch.distributed as dist
+        self.stub = stub
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if stub:
+            self.dev = torch.device("cpu")
+        else:
+            torch.cuda.set_device(self.local)
+            self.dev = torch.device("cuda", self.local)
+        if self.world > 1:
+            if stub:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=self.dev)
+            if dist.get_world_size() != self.world:
+                raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, WORLD_SIZE {self.world}")
+
+    def sync(self):
+        if not self.stub:
+            import torch
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def stream(self):
+        if self.stub:
+            return None
+        import torch
+        return torch.cuda.current_stream()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes (this process never touches
+    the GPU: it only counts devices, which does not initialise HIP, and starts children rather than
+    exec'ing), rank 0's stdout is the JSON line.  The driver's own form -- torch.distributed.run setting
+    WORLD_SIZE / RANK / LOCAL_RANK -- runs the same rank code directly."""
+    import socket
+    import subprocess
+    n = args.gpus
+    if not args.stub:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:      # one rank failed: the others would wait in a collective forever
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+# ------------------------------------------------------------------------------------------ sharded steps
+class ShardedRun:
+    """The C2 / C5 step on this rank: extract B frames of the global pan sequence (rank r holds global frames
+    r*B .. r*B+B-1), match frames 1.. of the shard against their in-shard predecessor, and -- with the
+    exchange -- all-gather per-frame counts and the Σn x 32 B descriptor block, matching the shard's first
+    frame against rank r-1's last frame from the gathered block one step later."""
+
+    def __init__(self, ranks, ex, m, base, B, exchange):
+        import torch
+        from orb_slam2_refactored_amd.shard import CompactExchange, Slots, cross_shard_predecessor, shard_range
+        self.ranks, self.ex, self.m, self.B = ranks, ex, m, B
+        world, rank, dev = ranks.world, ranks.rank, ranks.dev
+        H, W = base.shape[1:]
+        self.g0, _ = shard_range(B * world, world, rank)
+        gidx = torch.arange(self.g0, self.g0 + B)
+        if ranks.stub:
+            self.frames = gidx                      # the stub extractor derives its output from the index
+        else:
+            # frame g = base[g % 16]; every frame its own buffer in HBM (8192 x 0.92 MB >> the 256 MB MALL)
+            self.frames = torch.from_numpy(base).to(dev)[(gidx % len(base)).to(dev)].contiguous()
+        self.cap = ex.max_keypoints(H, W)
+        self.match_out = torch.empty((4, B, self.cap), dtype=torch.int32, device=dev)
+        self.prev_idx = torch.arange(0, B - 1, dtype=torch.int32, device=dev)
+        self.pred = cross_shard_predecessor(rank, world, B) if world > 1 else -1
+        if exchange:
+            self.xchg = CompactExchange(B, self.cap, dev)
+            self.cross_out = torch.full((4, 1, self.cap), -1, dtype=torch.int32, device=dev)
+            self.single = None
+        else:
+            self.xchg = None
+            self.single = Slots.empty(B, self.cap, dev)
+        self.k = 0
+        self.cross = 0          # cross-shard matches run
+        self.matched = -1       # last step whose cross-shard match ran (each step's runs once)
+        self.stream = ranks.stream()
+
+    def slots(self):
+        return self.single if self.xchg is None else self.xchg.local(max(self.k - 1, 0))
+
+    def _cross_match(self, j):
+        import torch
+        if j == self.matched:
+            return
+        self.matched = j
+        self.xchg.wait(j)
+        if self.ranks.rank == 0:
+            return
+        pb = self.xchg.frame(j, self.ranks.rank - 1, self.B - 1)
+        n = int(pb.shape[0])
+        if n == 0:
+            return
+        loc = self.xchg.local(j)
+        nb = torch.full((1,), n, dtype=torch.int32, device=self.ranks.dev)
+        self.m.match_batch_device(loc.desc[0:1], loc.counts[0:1], pb.reshape(1, n, 32), nb, out=self.cross_out,
+                                  stream=self.stream)
+        self.cross += 1
+
+    def step(self):
+        B, st = self.B, self.stream
+        if self.xchg is None:
+            s = self.single
+            self.ex.extract_batch_device(self.frames, s.kps, s.desc, s.counts, stream=st)
+            if B > 1:
+                self.m.match_batch_device(s.desc[1:], s.counts[1:], s.desc, s.counts, out=self.match_out[:, 1:],
+                                          stream=st, pair_b=self.prev_idx)
+            self.k += 1
+            return
+        k = self.k
+        loc = self.xchg.local(k)
+        self.ex.extract_batch_device(self.frames, loc.kps, loc.desc, loc.counts, stream=st)
+        if B > 1:
+            self.m.match_batch_device(loc.desc[1:], loc.counts[1:], loc.desc, loc.counts, out=self.match_out[:, 1:],
+                                      stream=st, pair_b=self.prev_idx)
+        had = self.xchg.pending
+        self.xchg.publish(k)
+        if had is not None:
+            self._cross_match(had)
+        self.k = k + 1
+
+    def finish(self):
+        if self.xchg is not None and self.xchg.pending is not None:
+            j = self.xchg.pending
+            self.xchg.drain()
+            self._cross_match(j)
+
+    def timed(self, steps, warmup, profile_stage=None):
+        """W untimed steps, then exactly `steps` steps between barrier + synchronize on both sides;
+        returns the max over ranks of the timed region (s) and, with `profile_stage`, the live HIP-event
+        launch times of that stage inside the timed region."""
+        for _ in range(warmup):
+            self.step()
+        self.finish()
+        self.ranks.sync()
+        self.ranks.barrier()
+        self.ranks.sync()
+        if profile_stage:
+            self.ex.profile(True, stages=[profile_stage])
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.finish()
+        self.ranks.sync()
+        self.ranks.barrier()
+        self.ranks.sync()
+        elapsed = time.perf_counter() - t0
+        prof = None
+        if profile_stage:
+            self.ex.profile(False)
+            prof = self.ex.profile_read()
+        self.fault = self.ex.batch_status()   # raises if a device capacity check tripped in the timed steps
+        return self.ranks.max(elapsed), prof
+
+    def exchange_block(self, steps):
+        """The exchange's numbers over the last `steps` steps (gathered bytes, gather time, xGMI bounds)."""
+        import numpy as np
+        x, world = self.xchg, self.ranks.world
+        if not self.ranks.stub:
+            x.collect_gather_times()
+        pay = x.payload_bytes[-steps:] if x.payload_bytes else [0]
+        gms = x.gather_ms[-steps:] if x.gather_ms else [0.0]
+        per_step = float(np.mean(pay)) + world * self.B * 4   # payload + counts
+        recv = per_step * (world - 1) / world                  # bytes each rank receives
+        g = float(np.mean(gms))
+        return {"gather_bytes_per_step": per_step, "received_bytes_per_rank_per_step": recv,
+                "padded_slot_gather_bytes_per_step": (self.cap * (28 + 32) + 4) * self.B * world,
+                "gather_ms_per_step": g, "gather_ms_max_over_ranks": self.ranks.max(g),
+                "gather_GBs_received_per_rank": recv / (g * 1e-3) / 1e9 if g else None,
+                "xgmi_bound_ms": {"all_7_links": recv / (7 * 153e9) * 1e3, "single_link": recv / 153e9 * 1e3},
+                "cross_shard_predecessor": self.pred,
+                "cross_match_first_frame_matches": (int((self.cross_out[3] >= 0).sum().item())
+                                                    if self.ranks.rank > 0 else None),
+                "cross_matches_run": self.cross,
+                "cross_shard_matches_all_ranks": int(self.ranks.sum(
+                    float((self.cross_out[3] >= 0).sum().item()) if self.ranks.rank > 0 else 0.0)),
+                "cross_matches_run_all_ranks": int(self.ranks.sum(float(self.cross)))}
+
+
+def c5_leg(ranks, ex, m, base, total=1024, steps=20, warmup=3):
+    """configs[4]: 1024 independent 1280x720 frames per step in total, sharded over the N ranks (1024/N per
+    rank: the fixed-size job of C5, i.e. strong scaling), extract + match vs predecessor + the counts /
+    descriptor all-gather and the cross-shard predecessor match.  Runs on every rank (collectives); at N = 1
+    it runs the same exchange path as the curve's first point."""
+    if total % ranks.world:
+        raise SystemExit(f"bench.py: C5's {total} frames do not split over {ranks.world} ranks")
+    B = total // ranks.world
+    run = ShardedRun(ranks, ex, m, base, B, exchange=True)
+    elapsed, _ = run.timed(steps, warmup)
+    out = {"workload": f"C5 (configs[4]): {total} 1280x720 frames per step in total, {B} per rank on "
+                       f"{ranks.world} rank(s), extract + match vs predecessor, RCCL counts + descriptor "
+                       "all-gather, cross-shard predecessor match",
+           "frames_per_step": total, "frames_per_rank": B, "n_ranks": ranks.world, "scaling": "strong",
+           "steps": steps, "warmup": warmup, "frames_per_s": total * steps / elapsed,
+           "ms_per_step": 1e3 * elapsed / steps}
+    out.update(run.exchange_block(steps))
+    return out
+
+
 # ------------------------------------------------------------------------------------------ main
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU: started here when no launcher set WORLD_SIZE; must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=8192, help="frames per step per GPU (weak scaling: the job is frames x world)")
@@ -738,142 +1069,74 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the N > 1 exchange path (pack, counts / payload gather, cross-shard match) at N = 1 too")
-    ap.add_argument("--no-legs", action="store_true", help="only the headline C2 measurement")
-    for leg in ("c1", "textured", "c3", "ba", "stereo", "pose", "projection", "bow"):
+    ap.add_argument("--no-legs", action="store_true", help="only the headline C2 measurement (and C5)")
+    ap.add_argument("--c5-frames", type=int, default=1024, help="C5's total frames per step (configs[4]: 1024)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU test of the launcher / exchange only: gloo, stub extraction, no GPU, no measurement")
+    for leg in ("c1", "textured", "c3", "ba", "stereo", "pose", "projection", "bow", "c5"):
         ap.add_argument(f"--no-{leg}", action="store_true")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    import torch
-    import torch.distributed as dist
 
+def main():
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if not args.stub:
+        import torch
+        have = torch.cuda.device_count()
+        if int(os.environ.get("LOCAL_RANK", "0")) >= have:
+            print(f"bench.py: LOCAL_RANK {os.environ.get('LOCAL_RANK')} but {have} GPU(s) visible", file=sys.stderr,
+                  flush=True)
+            sys.exit(2)
+    ranks = Ranks(args.stub)
+    rank = ranks.rank
 
-    from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
-    from orb_slam2_refactored_amd.shard import CompactExchange, Slots, cross_shard_predecessor, shard_range
     from orb_slam2_refactored_amd.synth import pan_sequence
 
     W, H = args.width, args.height
     B = args.frames                      # frames per GPU per step (weak scaling)
     total = B * world
-    g0, _ = shard_range(total, world, rank)
-    # the global job is a pan sequence of 16 distinct frames repeated (frame g = base[g % 16]); every
-    # frame is its own buffer in HBM (8192 x 0.92 MB >> the 256 MB Infinity Cache)
-    base = pan_sequence(0, W, H, 16)
-    gidx = torch.arange(g0, g0 + B) % 16
-    frames = torch.from_numpy(base).to(dev)[gidx.to(dev)].contiguous()
-    frames_np = base
-    ex = ORBextractor(ORBextractor.Parameters(nfeatures=args.nfeatures), device=local)
-    m = ORBmatcher(0.6, False)
-    cap = ex.max_keypoints(H, W)
-    stream = torch.cuda.current_stream()
-    match_out = torch.empty((4, B, cap), dtype=torch.int32, device=dev)
-    # frames 1.. of the shard vs their in-shard predecessor (global frame 0 has none: not matched)
-    prev_idx = torch.arange(0, B - 1, dtype=torch.int32, device=dev)
-    pred = cross_shard_predecessor(rank, world, B) if world > 1 else -1
-    if world == 1 and not args.force_exchange:
-        single = Slots.empty(B, cap, dev)
-        xchg = None
+    base = pan_sequence(0, W, H, 16)     # the global job: frame g = base[g % 16]
+    if args.stub:
+        ex, m = _StubExtractor(args.nfeatures), _StubMatcher()
     else:
-        # rank r's first frame vs rank r-1's last frame, read from the gathered descriptors of that step
-        # one step later (the payload gather overlaps the next step's kernels); rank 0's first frame is
-        # global frame 0 and has no predecessor
-        xchg = CompactExchange(B, cap, dev)
-        cross_out = torch.empty((4, 1, cap), dtype=torch.int32, device=dev)
-    state = {"k": 0, "cross": 0}
-
-    def cross_match(j):
-        xchg.wait(j)
-        if rank == 0:
-            return
-        pb = xchg.frame(j, rank - 1, B - 1)
-        n = int(pb.shape[0])
-        if n == 0:
-            return
-        loc = xchg.local(j)
-        nb = torch.full((1,), n, dtype=torch.int32, device=dev)
-        m.match_batch_device(loc.desc[0:1], loc.counts[0:1], pb.reshape(1, n, 32), nb, out=cross_out, stream=stream)
-        state["cross"] += 1
-
-    def step():
-        if xchg is None:
-            ex.extract_batch_device(frames, single.kps, single.desc, single.counts, stream=stream)
-            if B > 1:
-                m.match_batch_device(single.desc[1:], single.counts[1:], single.desc, single.counts, out=match_out[:, 1:],
-                                     stream=stream, pair_b=prev_idx)
-            return
-        k = state["k"]
-        loc = xchg.local(k)
-        ex.extract_batch_device(frames, loc.kps, loc.desc, loc.counts, stream=stream)
-        if B > 1:
-            m.match_batch_device(loc.desc[1:], loc.counts[1:], loc.desc, loc.counts, out=match_out[:, 1:],
-                                 stream=stream, pair_b=prev_idx)
-        xchg.publish(k)
-        if k >= 1:
-            cross_match(k - 1)
-        state["k"] = k + 1
-
-    def finish():
-        if xchg is not None and xchg.pending is not None:
-            j = xchg.pending
-            xchg.drain()
-            cross_match(j)
-
-    for _ in range(args.warmup):
-        step()
-    finish()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+        from orb_slam2_refactored_amd import ORBextractor, ORBmatcher
+        ex = ORBextractor(ORBextractor.Parameters(nfeatures=args.nfeatures), device=ranks.local)
+        m = ORBmatcher(0.6, False)
+    run = ShardedRun(ranks, ex, m, base, B, exchange=world > 1 or args.force_exchange)
     # inside the timed region only the dominant kernel (fast_cells) carries launch events (events on every
     # kernel cost ~3.5 %); the other stages are timed in a separate pass below
-    ex.profile(True, stages=["fast_cells"])
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    finish()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ex.profile(False)
-    timed = ex.profile_read()
-    fault = ex.batch_status()   # raises if any device capacity check tripped in the timed steps
+    elapsed, timed = run.timed(args.steps, args.warmup, profile_stage="fast_cells")
     ex.profile(True)
     for _ in range(3):
-        step()
-    finish()
-    torch.cuda.synchronize()
+        run.step()
+    run.finish()
+    ranks.sync()
     ex.profile(False)
     breakdown = ex.profile_read()
     brk_steps = 3
     # the matcher alone (3 calls on the last step's descriptors), for its FP4 roofline
     match_ms = 0.0
-    if B > 1:
-        sl = single if xchg is None else xchg.local(0)
+    sl = run.slots()
+    if B > 1 and not args.stub:
+        import torch
+        st = run.stream
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
+        e0.record(st)
         for _ in range(3):
-            m.match_batch_device(sl.desc[1:], sl.counts[1:], sl.desc, sl.counts, out=match_out[:, 1:], stream=stream,
-                                 pair_b=prev_idx)
-        e1.record(stream)
+            m.match_batch_device(sl.desc[1:], sl.counts[1:], sl.desc, sl.counts, out=run.match_out[:, 1:], stream=st,
+                                 pair_b=run.prev_idx)
+        e1.record(st)
         e1.synchronize()
         match_ms = e0.elapsed_time(e1) / 3
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
-    counts = (single.counts if xchg is None else xchg.local(0).counts)
-    n_kp = float(counts.float().mean().item())
-    matches = int((match_out[3] >= 0).sum().item())
+    n_kp = float(sl.counts.float().mean().item())
+    matches = int((run.match_out[3] >= 0).sum().item())
     value = total * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     bytes_frame, P = algorithmic_bytes(W, H, n_kp)
@@ -888,8 +1151,8 @@ def main():
     dom_bytes = sb[dom] * B / max(launches_per_step, 1)
     achieved = dom_bytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
     traffic = measured_traffic(dom, B, W, H, args.nfeatures)
-    extract_ms = sum(v[0] for k, v in breakdown.items() if k in STAGE_KERNEL) / brk_steps
-    pipe_traffic = measured_traffic_step(breakdown, brk_steps, B, W, H, args.nfeatures)
+    extract_ms = sum(v[0] for k, v in breakdown.items() if k in STAGE_KERNELS) / brk_steps
+    pipe_traffic = measured_traffic_step(B, W, H, args.nfeatures)
     match_tflops = 512.0 * n_kp * n_kp * (B - 1) / (match_ms * 1e-3) / 1e12 if match_ms else 0.0
 
     result = {
@@ -904,7 +1167,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (pan sequence of §8d G frames, shifted (+3,+2) px per frame)",
+        "data": ("STUB (CPU launcher test, no extraction)" if args.stub else
+                 "synthetic (pan sequence of §8d G frames, shifted (+3,+2) px per frame)"),
         "config": {"workload": f"C2: {W}x{H} mono, 8 levels, {args.nfeatures} features, extract + brute-force "
                                f"Hamming top-2/ratio match of every frame vs its predecessor",
                    "frames_per_step": total, "frames_per_step_per_gpu": B, "width": W, "height": H, "nlevels": 8,
@@ -932,32 +1196,23 @@ def main():
                            "match_ms_per_step": match_ms},
         "keypoints_per_frame": n_kp,
         "matches_last_step": matches,
-        "device_fault_mask": fault,
+        "device_fault_mask": run.fault,
         "timed_region_s": elapsed,
     }
-    if xchg is not None:
-        xchg.collect_gather_times()
-        pay = xchg.payload_bytes[-args.steps:] if xchg.payload_bytes else [0]
-        gms = xchg.gather_ms[-args.steps:] if xchg.gather_ms else [0.0]
-        per_step = float(np.mean(pay)) + world * B * 4   # payload + counts
-        recv = per_step * (world - 1) / world             # bytes each rank receives
-        padded = (cap * (28 + 32) + 4) * total            # the round-2 padded-slot gather, for comparison
-        result["c5"] = {"workload": "C5 semantics: frames sharded (weak scaling, frames_per_step_per_gpu each), "
-                                    "per-frame counts all-gathered, then each rank's Σn x 32 B descriptor block "
-                                    "(padded to the step's largest block) all-gathered over RCCL; frame i matched to "
-                                    "i-1 across shard boundaries from the gathered descriptors",
-                        "gather_bytes_per_step": per_step, "received_bytes_per_rank_per_step": recv,
-                        "padded_slot_gather_bytes_per_step": padded,
-                        "gather_ms_per_step": float(np.mean(gms)),
-                        "gather_GBs_received_per_rank": recv / (float(np.mean(gms)) * 1e-3) / 1e9 if np.mean(gms) else None,
-                        "xgmi_bound_ms": {"all_7_links": recv / (7 * 153e9) * 1e3, "single_link": recv / 153e9 * 1e3},
-                        "cross_shard_predecessor": pred,
-                        "cross_match_first_frame_matches": int((cross_out[3] >= 0).sum().item()) if rank > 0 else None,
-                        "cross_matches_run": state["cross"]}
+    if args.stub:
+        result["stub"] = True
+    if run.xchg is not None:
+        result["exchange"] = dict(run.exchange_block(args.steps),
+                                  workload="the headline's exchange (weak scaling, frames_per_step_per_gpu per rank)")
+    # C5 (configs[4]) on every rank: it has collectives, so it runs before the rank-0-only legs
+    if not args.no_c5:
+        result["c5"] = c5_leg(ranks, ex, m, base, total=args.c5_frames)
 
-    legs = rank == 0 and not args.no_legs
-    cpu = world == 1 and not args.no_cpu_baseline and rank == 0
+    legs = rank == 0 and not args.no_legs and not args.stub
+    cpu = world == 1 and not args.no_cpu_baseline and rank == 0 and not args.stub
     info = cpu_info()
+    local = ranks.local
+    dev = ranks.dev
     # LocalBA first: its host loop polls the device, so it is timed before any leg's CPU-baseline
     # thread pool has run in this process
     if legs and not args.no_ba:
@@ -983,12 +1238,35 @@ def main():
     if cpu:
         result["cpu_baseline"] = cpu_baseline_block(
             "frames/s", f"{W}x{H} pan-sequence frames, extract + brute-force match vs previous",
-            cpu_extract_match(frames_np[:4], args.nfeatures, 1, 8.0),
-            cpu_extract_match(frames_np[:8], args.nfeatures, info["threads_all"], 8.0), info)
+            cpu_extract_match(base[:4], args.nfeatures, 1, 8.0),
+            cpu_extract_match(base[:8], args.nfeatures, info["threads_all"], 8.0), info)
+    # the metric's other halves, flat and last on the line (a record that keeps only the tail of stdout
+    # still holds them)
+    result["summary"] = summary(result)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    ranks.close()
+
+
+def summary(r):
+    def g(*path):
+        v = r
+        for p in path:
+            if not isinstance(v, dict) or p not in v:
+                return None
+            v = v[p]
+        return round(v, 4) if isinstance(v, float) else v
+    return {"c2_frames_per_s": g("value"), "c2_ms_per_step": g("ms_per_step"), "n_gpus": g("n_gpus"),
+            "fast_cells_frac": g("roofline", "frac"), "fast_cells_ms": g("roofline", "avg_launch_ms"),
+            "pipeline_traffic_over_algorithmic": g("roofline", "pipeline_traffic_over_algorithmic"),
+            "localba_iters_per_s": g("localba", "iters_per_s"), "localba_ms_per_call": g("localba", "ms_per_call"),
+            "localba_cpu_iters_per_s": g("localba", "cpu_baseline", "value"),
+            "c1_frames_per_s": g("c1", "frames_per_s"), "c1_cpu_median_ms": g("c1", "cpu_baseline", "median_ms"),
+            "c2_1000_frames_per_s": g("c2_1000", "frames_per_s"),
+            "c2_textured_frames_per_s": g("c2_textured", "frames_per_s"),
+            "c3_pairs_per_s": g("c3", "pairs_per_s"),
+            "c5_frames_per_s": g("c5", "frames_per_s"), "c5_n_ranks": g("c5", "n_ranks"),
+            "c5_gather_ms": g("c5", "gather_ms_max_over_ranks"), "cpu_frames_per_s": g("cpu_baseline", "value")}
 
 
 if __name__ == "__main__":

@@ -1340,9 +1340,14 @@ __device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double
     return c->accepted != 0;
 }
 
-// The control snapshot into pinned host memory: the body as system-scope stores (write-through, no L2
-// writeback of the device's other data as a system fence would do), waited for, then the sequence
-// id the host polls for.
+// The control snapshot into pinned host memory: the body as relaxed system-scope stores (write-through
+// to the host, no L2 writeback of the device's other data), then the sequence id the host polls for as a
+// system-scope RELEASE store, so the host's acquire load of `seq` (the host ring poll in orbba_local_ba) orders every
+// body word before it by the memory model, not by the gfx9 rule that vmcnt(0) retires earlier stores
+// (What's weak 8).  ORBBA_SNAP_RELEASE=0 builds the round-3 form for A/B only.
+#ifndef ORBBA_SNAP_RELEASE
+#define ORBBA_SNAP_RELEASE 1
+#endif
 __device__ __forceinline__ void snapshot_to_host(const BACtl& snap, int seq, BACtl* host_snap) {
     static_assert(sizeof(BACtl) % 8 == 0, "snapshot copied as 8-byte words");
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&snap);
@@ -1350,8 +1355,12 @@ __device__ __forceinline__ void snapshot_to_host(const BACtl& snap, int seq, BAC
 #pragma unroll
     for (int k = 0; k < (int)(sizeof(BACtl) / 8); k++)
         __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#if ORBBA_SNAP_RELEASE
+    __hip_atomic_store(&host_snap->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(&host_snap->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
 }
 
 
