@@ -1,6 +1,7 @@
 #!/bin/bash
 # Builds an A/B variant of the library: tools/ab/lib_<name>.so = the in-tree objects with <src>.hip
 # recompiled under extra flags.  Usage: tools/ab_build.sh <name> <src (e.g. orbba)> <flags...>
+# With REV=<git revision>, <src>.hip is taken from that revision instead of the working tree.
 # (runs on the CPU side; the .so travels to the GPU box with the tree).
 set -e
 cd "$(dirname "$0")/../orb_slam2_refactored_amd/csrc"
@@ -9,8 +10,10 @@ make -s
 mkdir -p _build/ab ../../tools/ab
 extra=""
 case $src in orbx|orbm) extra="-mllvm -amdgpu-mfma-vgpr-form";; esac
+file=$src.hip
+if [ -n "$REV" ]; then file=_build/ab/${src}_$name.hip; git show "$REV:orb_slam2_refactored_amd/csrc/$src.hip" > $file; fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result \
-    -I../../include -I. $extra "$@" -c $src.hip -o _build/ab/${src}_$name.o
+    -I../../include -I. $extra "$@" -c $file -o _build/ab/${src}_$name.o
 objs=""
 for o in _build/*.o; do
   b=$(basename $o .o)
