@@ -603,10 +603,12 @@ int orb_device_count(void);
  * across shard boundaries; no reference counterpart, the reference runs one camera stream): frame f's
  * first counts[f] descriptor rows of desc (n_frames x cap x 32 bytes, the orbx_extract_batch_device
  * layout) go to out rows [incl[f] - counts[f], incl[f]), with incl the inclusive prefix sum of counts.
- * counts / incl / desc / out are device memory; enqueue only on `stream`.  One launch, 32-byte rows as
- * two 16-byte vector copies. */
+ * out holds out_rows rows: rows outside [0, out_rows) are not written, and a count outside [0, cap]
+ * copies min(max(counts[f], 0), cap) rows (the device-side counts are never trusted to stay inside the
+ * buffers).  counts / incl / desc / out are device memory; enqueue only on `stream`.  One launch,
+ * 32-byte rows as two 16-byte vector copies. */
 int orbx_pack_descriptors(const uint8_t* desc, int32_t cap, const int32_t* counts, const int32_t* incl,
-                          int32_t n_frames, uint8_t* out, void* stream);
+                          int32_t n_frames, uint8_t* out, int32_t out_rows, void* stream);
 
 /* Stage timing with HIP events recorded as part of each kernel's dispatch (hipExtLaunchKernel start /
  * stop events: the kernel's own duration) for the stages 0 pyramid, 1 FAST cells, 2 quadtree,

@@ -175,7 +175,7 @@ SIGNATURES = {
     "orbba_local_ba": (C.c_int, [C.POINTER(BAProblem), C.POINTER(BAResult), VP, C.c_int]),
     "orbba_pose_optimization": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), C.c_int]),
     "orbba_pose_optimization_device": (C.c_int, [C.POINTER(PoseBatch), C.POINTER(PoseResult), VP]),
-    "orbx_pack_descriptors": (C.c_int, [VP, C.c_int, VP, VP, C.c_int, VP, VP]),
+    "orbx_pack_descriptors": (C.c_int, [VP, C.c_int, VP, VP, C.c_int, VP, C.c_int, VP]),
     "orbx_profile_enable": (C.c_int, [VP, C.c_int]),
     "orbx_profile_read": (C.c_int, [VP, VP, VP]),
     "orbx_debug_level_candidates": (C.c_int, [VP, C.c_int, C.c_int, VP, C.c_int, C.POINTER(C.c_int)]),

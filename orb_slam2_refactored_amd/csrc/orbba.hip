@@ -2076,6 +2076,12 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         q_to_R(&hq[4 * i], res->pose_R + 9 * i);
         if (res->pose_q) std::memcpy(res->pose_q + 4 * i, &hq[4 * i], 32);
     }
+    // the dense pair-block scratch (slot_of: nl x np ints, col: np x nl/64 words) of a very large window
+    // is released rather than kept with the thread (C4 keeps its 0.3 MB)
+    if (hs.slot_of.capacity() * sizeof(int) + hs.col.capacity() * sizeof(unsigned long long) > (8u << 20)) {
+        std::vector<int>().swap(hs.slot_of);
+        std::vector<unsigned long long>().swap(hs.col);
+    }
     mark("end");
     if (tdbg)
         for (size_t i = 1; i < marks.size(); i++)

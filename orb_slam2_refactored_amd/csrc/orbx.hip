@@ -605,99 +605,127 @@ static bool pyr_pair_fits(const Geom& g, int l) {
 // per-pixel branches.
 template <int IMM>
 __device__ __forceinline__ uint32_t bt3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, IMM); }
+constexpr int BT_OR3 = 0xFE;   // a | b | c (truth tables over (a, b, c) = (0xF0, 0xCC, 0xAA))
 
-// Two-of-four tests on guard-bit words (round 4).  A dword of pixels x..x+3 is split into its even
-// pixels (x, x+2: w & 0x00ff00ff) and odd pixels (x+1, x+3: one v_perm), each a pair of u16 lanes
-// holding 0..255.  With per-lane constants K = 2^b - 1 - t - v and J = v + 2^b - 1 - t (b >= 9), one
-// plain 32-bit add / sub compares both lanes at once and leaves the answer in bit b of each lane:
-//   p + K >= 2^b  <=>  p > v + t        J - p >= 2^b  <=>  p < v - t
-// (no carry or borrow crosses a lane: every intermediate lies in [0, 2^(b+1))).  The four results of a
-// dword -- bright / dark of the even and odd pixels -- use b = 9, 10, 11, 12, so they land on distinct
-// bits: pixel 0 at bits 9 (bright) / 10 (dark), pixel 1 at 11 / 12, pixels 2 / 3 at 25-28.  Unlike
-// v_pk_min/max (about 4 cycles per wave64 on gfx950) the adds, subs and bitop3 issue at the 2-cycle rate
-// (tools/probe/issue_probe3).  Pass condition for four circle points at 90-degree steps (p1 / p3 and
-// p2 / p4 opposite): two circle-adjacent ones both brighter (darker) <=> (B1 | B3) & (B2 | B4).
-constexpr uint32_t FB_PX0 = 0x00000600u, FB_PX1 = 0x00001800u, FB_PX2 = 0x06000000u, FB_PX3 = 0x18000000u;
-constexpr uint32_t FB_BE = 0x02000200u, FB_DE = 0x04000400u, FB_BO = 0x08000800u, FB_DO = 0x10001000u;
-constexpr int BT_OR_AND = 0xA8;   // (a | b) & c (truth tables over (a, b, c) = (0xF0, 0xCC, 0xAA))
-
+// Two-of-four pre-test on packed u16 lanes.  A dword w of pixels x..x+3 is used as two words of
+// u16 lanes: the even pixels (x, x+2) unpacked, w & 0x00ff00ff, and the odd pixels (x+1, x+3) in
+// place, i.e. in each lane's high byte with the even pixel as a low byte.  The odd lanes' thresholds
+// carry the low byte that makes the comparison depend on the high byte only:
+//   p*256 + q > (v + t)*256 + 255  <=>  p > v + t     (saturated at 0xffff when v + t > 255)
+//   (v - t)*256 > p*256 + q        <=>  p < v - t     (saturated at 0 when v < t)
+// and max / min of such words order by the high byte first, so the same network serves both halves.
+// Pass condition for four circle points at 90-degree steps (p1, p3 opposite; p2, p4 opposite): two
+// circle-adjacent ones both brighter than v + t or both darker than v - t, which factors to
+// (B1 | B3) & (B2 | B4):  min(max(p1, p3), max(p2, p4)) > hi  or  max(min(p1, p3), min(p2, p4)) < lo.
+struct PkThr {
+    us2 hi_e, lo_e, hi_o, lo_o;
+};
 __device__ __forceinline__ us2 u2us(uint32_t a) { return __builtin_bit_cast(us2, a); }
 __device__ __forceinline__ uint32_t us2u(us2 a) { return __builtin_bit_cast(uint32_t, a); }
-__device__ __forceinline__ uint32_t odd_px(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c01u); }
-struct Thr4 {
-    uint32_t Ke, Je, Ko, Jo;
-};
-struct ThrK {   // per pass: 2^b - 1 - t in both u16 lanes, b = 9 / 10 / 11 / 12 (wave-uniform)
-    uint32_t be, de, bo, dd;
-};
-__device__ __forceinline__ ThrK thr_consts(int tc) {
-    const uint32_t t2 = (uint32_t)tc * 0x00010001u;
-    return ThrK{0x01ff01ffu - t2, 0x03ff03ffu - t2, 0x07ff07ffu - t2, 0x0fff0fffu - t2};
+__device__ __forceinline__ us2 pk_even(uint32_t w) { return u2us(w & 0x00ff00ffu); }
+__device__ __forceinline__ PkThr pk_thresholds(uint32_t wv, int t) {
+    const unsigned short tc = (unsigned short)min(max(t, 0), 255);   // cv::FAST clamps the threshold
+    const us2 t1 = {tc, tc}, t8 = {(unsigned short)(tc << 8), (unsigned short)(tc << 8)};
+    PkThr r;
+    const us2 ve = pk_even(wv);
+    r.hi_e = ve + t1;                                                        // <= 510: no wrap
+    r.lo_e = __builtin_elementwise_sub_sat(ve, t1);
+    r.hi_o = __builtin_elementwise_add_sat(u2us(wv | 0x00ff00ffu), t8);      // (v + t)*256 + 255, saturated
+    r.lo_o = __builtin_elementwise_sub_sat(u2us(wv & 0xff00ff00u), t8);      // (v - t)*256, saturated
+    return r;
 }
-__device__ __forceinline__ Thr4 thr4(uint32_t wv, const ThrK& C) {
-    const uint32_t ve = wv & 0x00ff00ffu, vo = odd_px(wv);
-    return Thr4{C.be - ve, C.de + ve, C.bo - vo, C.dd + vo};
-}
-// p1 / p3 and p2 / p4 opposite circle points, each as (even, odd) words; m0..m3 mask the result bits
-// (bright-even, dark-even, bright-odd, dark-odd) and may clear pixels outside the zone
-__device__ __forceinline__ uint32_t two_of_four4(const Thr4& T, uint32_t p1e, uint32_t p1o, uint32_t p3e, uint32_t p3o,
-                                                 uint32_t p2e, uint32_t p2o, uint32_t p4e, uint32_t p4o, uint32_t m0,
-                                                 uint32_t m1, uint32_t m2, uint32_t m3) {
-    const uint32_t rbe = bt3<BT_OR_AND>(p1e + T.Ke, p3e + T.Ke, (p2e + T.Ke) | (p4e + T.Ke));
-    const uint32_t rde = bt3<BT_OR_AND>(T.Je - p1e, T.Je - p3e, (T.Je - p2e) | (T.Je - p4e));
-    const uint32_t rbo = bt3<BT_OR_AND>(p1o + T.Ko, p3o + T.Ko, (p2o + T.Ko) | (p4o + T.Ko));
-    const uint32_t rdo = bt3<BT_OR_AND>(T.Jo - p1o, T.Jo - p3o, (T.Jo - p2o) | (T.Jo - p4o));
-    return (rbe & m0) | (rde & m1) | (rbo & m2) | (rdo & m3);
+// non-zero u16 lanes where the pixel passes
+__device__ __forceinline__ us2 pk_two_of_four(us2 p1, us2 p3, us2 p2, us2 p4, us2 hi, us2 lo) {
+    const us2 bmax = __builtin_elementwise_min(__builtin_elementwise_max(p1, p3), __builtin_elementwise_max(p2, p4));
+    const us2 dmin = __builtin_elementwise_max(__builtin_elementwise_min(p1, p3), __builtin_elementwise_min(p2, p4));
+    return __builtin_elementwise_sub_sat(bmax, hi) | __builtin_elementwise_sub_sat(lo, dmin);
 }
 
-// Corner strength of ONE polarity on packed u16 pairs: lane pair k holds circle positions (k, k + 8), so
-// every min covers two arcs at once; position j >= 8 is the swapped pair j - 8.  Returns max over the 16
-// nine-pixel arcs of min(p) - v (the bright strength; the dark one is the same on 255 - p, 255 - v).  A
-// pixel cannot have a positive bright and a positive dark strength (two 9-arcs of a 16-circle share a
-// point), so M = max(0, strength of the polarity the pre-tests left open) -- both polarities only when
-// both stayed open.  Windows of 9 pair up by the lattice identity
-//   max(min(a, b), min(b, c)) = min(b, max(a, c)):  35 packed ops per polarity (round 3: 80 for both).
+// Corner strength M (cornerScore<16> + 1, or 0 when not a corner at any threshold) on packed u16
+// pairs: lane pair k holds circle positions (k, k + 8), so every min / max of the arc network covers
+// two arcs at once; position j >= 8 is the swapped pair j - 8.  The network runs on the raw pixels:
+// max over arcs of min(p) - v is the bright strength, v - min over arcs of max(p) the dark one.
 __device__ __forceinline__ us2 swap2(us2 a) { return __builtin_shufflevector(a, a, 1, 0); }
-__device__ __forceinline__ int arc_strength(const us2 (&D)[8], int v) {
-    us2 l2[8], l4[8], l8[8];
+// The 16 circle bytes as packed pairs.  With a compile-time row stride CS the pairs are loaded straight
+// into the u16 halves by ds_read_u8_d16 / ds_read_u8_d16_hi (offsets from the circle's top-left byte),
+// which the compiler does not form on its own (it loads 16 dwords and packs them with 8 v_perm).
+template <int CS>
+__device__ __forceinline__ void circle_pairs(const uint8_t* c, int cs, us2 (&D)[8]) {
+    if constexpr (CS != 0) {
+        // one asm statement with its own wait: the compiler does not know these loads are in flight
+        const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(c - 3 * CS - 3);   // LDS offset (low 32 bits)
+        uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
+#define ORBX_OFF(k) (c_circle_dy_h[k] + 3) * CS + c_circle_dx_h[k] + 3
+        asm volatile(
+            "ds_read_u8_d16 %0, %8 offset:%9\n\tds_read_u8_d16 %1, %8 offset:%10\n\t"
+            "ds_read_u8_d16 %2, %8 offset:%11\n\tds_read_u8_d16 %3, %8 offset:%12\n\t"
+            "ds_read_u8_d16 %4, %8 offset:%13\n\tds_read_u8_d16 %5, %8 offset:%14\n\t"
+            "ds_read_u8_d16 %6, %8 offset:%15\n\tds_read_u8_d16 %7, %8 offset:%16\n\t"
+            "ds_read_u8_d16_hi %0, %8 offset:%17\n\tds_read_u8_d16_hi %1, %8 offset:%18\n\t"
+            "ds_read_u8_d16_hi %2, %8 offset:%19\n\tds_read_u8_d16_hi %3, %8 offset:%20\n\t"
+            "ds_read_u8_d16_hi %4, %8 offset:%21\n\tds_read_u8_d16_hi %5, %8 offset:%22\n\t"
+            "ds_read_u8_d16_hi %6, %8 offset:%23\n\tds_read_u8_d16_hi %7, %8 offset:%24\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
+            : "v"(a), "i"(ORBX_OFF(0)), "i"(ORBX_OFF(1)), "i"(ORBX_OFF(2)), "i"(ORBX_OFF(3)), "i"(ORBX_OFF(4)),
+              "i"(ORBX_OFF(5)), "i"(ORBX_OFF(6)), "i"(ORBX_OFF(7)), "i"(ORBX_OFF(8)), "i"(ORBX_OFF(9)),
+              "i"(ORBX_OFF(10)), "i"(ORBX_OFF(11)), "i"(ORBX_OFF(12)), "i"(ORBX_OFF(13)), "i"(ORBX_OFF(14)),
+              "i"(ORBX_OFF(15))
+            : "memory");
+#undef ORBX_OFF
+        D[0] = __builtin_bit_cast(us2, r0); D[1] = __builtin_bit_cast(us2, r1);
+        D[2] = __builtin_bit_cast(us2, r2); D[3] = __builtin_bit_cast(us2, r3);
+        D[4] = __builtin_bit_cast(us2, r4); D[5] = __builtin_bit_cast(us2, r5);
+        D[6] = __builtin_bit_cast(us2, r6); D[7] = __builtin_bit_cast(us2, r7);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 8; k++) l2[k] = __builtin_elementwise_min(D[k], k + 1 < 8 ? D[k + 1] : swap2(D[k - 7]));
-#pragma unroll
-    for (int k = 0; k < 8; k++) l4[k] = __builtin_elementwise_min(l2[k], k + 2 < 8 ? l2[k + 2] : swap2(l2[k - 6]));
-#pragma unroll
-    for (int k = 0; k < 8; k++) l8[k] = __builtin_elementwise_min(l4[k], k + 4 < 8 ? l4[k + 4] : swap2(l4[k - 4]));
-    us2 A;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {   // windows of 9 starting at j and j + 1 (and j + 8, j + 9)
-        const us2 c = j + 2 < 8 ? l8[j + 2] : swap2(l8[0]);
-        const us2 w = __builtin_elementwise_min(l8[j + 1], __builtin_elementwise_max(l8[j], c));
-        A = j == 0 ? w : __builtin_elementwise_max(A, w);
+        for (int k = 0; k < 8; k++)
+            D[k] = us2{(unsigned short)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]],
+                       (unsigned short)c[c_circle_dy_h[k + 8] * cs + c_circle_dx_h[k + 8]]};
     }
-    return (int)max(A.x, A.y) - v;
 }
-__device__ __forceinline__ void load_circle(const uint8_t* c, int cs, us2 (&D)[8]) {
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-        D[k] = us2{(unsigned short)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]],
-                   (unsigned short)c[c_circle_dy_h[k + 8] * cs + c_circle_dx_h[k + 8]]};
-}
-// M (cornerScore + 1 for a corner at any threshold, else <= the threshold) of the pixel at c for the
-// polarities `pol` leaves open: bit 0 bright, bit 1 dark (never 0 here)
-__device__ __forceinline__ int corner_strength_pol(const uint8_t* c, int cs, int pol) {
+template <int CS>
+__device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
     us2 D[8];
-    load_circle(c, cs, D);
-    const int v = c[0];
-    const uint32_t xm = pol == 2 ? 0x00ff00ffu : 0u;   // dark only: the bright network on 255 - p
-    us2 X[8];
+    circle_pairs<CS>(c, cs, D);
+    us2 l[8], h[8], l2[8], h2[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) X[k] = u2us(us2u(D[k]) ^ xm);
-    int M = arc_strength(X, v ^ (int)(xm & 0xffu));
-    if (pol == 3) {   // both polarities open (rare): the dark network too
-#pragma unroll
-        for (int k = 0; k < 8; k++) X[k] = u2us(us2u(D[k]) ^ 0x00ff00ffu);
-        M = max(M, arc_strength(X, v ^ 0xff));
+    for (int k = 0; k < 8; k++) {   // arcs of 2
+        const us2 n = k + 1 < 8 ? D[k + 1] : swap2(D[k - 7]);
+        l[k] = __builtin_elementwise_min(D[k], n);
+        h[k] = __builtin_elementwise_max(D[k], n);
     }
-    return max(M, 0);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {   // arcs of 4
+        const us2 nl = k + 2 < 8 ? l[k + 2] : swap2(l[k - 6]);
+        const us2 nh = k + 2 < 8 ? h[k + 2] : swap2(h[k - 6]);
+        l2[k] = __builtin_elementwise_min(l[k], nl);
+        h2[k] = __builtin_elementwise_max(h[k], nh);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {   // arcs of 8
+        const us2 nl = k + 4 < 8 ? l2[k + 4] : swap2(l2[k - 4]);
+        const us2 nh = k + 4 < 8 ? h2[k + 4] : swap2(h2[k - 4]);
+        l[k] = __builtin_elementwise_min(l2[k], nl);
+        h[k] = __builtin_elementwise_max(h2[k], nh);
+    }
+    // arcs of 9 = two overlapping arcs of 8, max / min over all 16, two windows at a time by the lattice
+    // identities max(min(a, b), min(b, c)) = min(b, max(a, c)) and min(max(a, b), max(b, c)) =
+    // max(b, min(a, c)): 22 packed ops instead of 32
+    us2 A, B;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {   // windows starting at j and j + 1 (and j + 8, j + 9)
+        const us2 cl = j + 2 < 8 ? l[j + 2] : swap2(l[0]);
+        const us2 ch = j + 2 < 8 ? h[j + 2] : swap2(h[0]);
+        const us2 wl = __builtin_elementwise_min(l[j + 1], __builtin_elementwise_max(l[j], cl));
+        const us2 wh = __builtin_elementwise_max(h[j + 1], __builtin_elementwise_min(h[j], ch));
+        A = j == 0 ? wl : __builtin_elementwise_max(A, wl);
+        B = j == 0 ? wh : __builtin_elementwise_min(B, wh);
+    }
+    const int v = c[0];
+    const int bright = (int)max(A.x, A.y) - v;   // max over arcs of min(p - v)
+    const int dark = v - (int)min(B.x, B.y);     // max over arcs of min(v - p)
+    return max(0, max(bright, dark));
 }
 
 // One wavefront per (cell, frame).  LDS (sized per launch from the largest cell): the crop
@@ -940,16 +968,6 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         c.h = lh;
         return c;
     };
-    // lanes of the pre-test: QR quads of 4 pixels per zone row (8 or 16), 64/QR rows per chunk; the
-    // masks keep the result bits of pixels inside the zone (zone width: strip-invariant)
-    const int qsh = zw <= 32 ? 3 : 4;
-    const int QR = 1 << qsh, RPC = 64 >> qsh;
-    const int qx = (lane & (QR - 1)) * 4, qy = lane >> qsh;
-    const bool qxin = qx < zw;
-    const uint32_t v0 = qx < zw ? 0x0000ffffu : 0u, v1 = qx + 1 < zw ? 0x0000ffffu : 0u;
-    const uint32_t v2 = qx + 2 < zw ? 0xffff0000u : 0u, v3 = qx + 3 < zw ? 0xffff0000u : 0u;
-    const uint32_t zm0 = FB_BE & (v0 | v2), zm1 = FB_DE & (v0 | v2), zm2 = FB_BO & (v1 | v3), zm3 = FB_DO & (v1 | v3);
-    const uint32_t ebase = (uint32_t)(qx >> 2) | ((uint32_t)qy << 13);
     // Speculative iniThFAST pass: a cell whose predecessor in this wavefront (the cell above it in
     // the same column) kept >= spec_min corners at iniThFAST is first run with the pre-test,
     // the diagonal filter and the corner list at iniThFAST only.  When the NMS keeps one of them
@@ -977,27 +995,34 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
 
     const int tp = spec ? th_ini : tlo;   // threshold of this pass
-    const ThrK TK = thr_consts(min(max(tp, 0), 255));   // cv::FAST clamps the threshold
+    // lanes: QR quads per row (8 or 16), 64/QR rows per chunk
+    const int qsh = zw <= 32 ? 3 : 4;
+    const int QR = 1 << qsh, RPC = 64 >> qsh;
+    const int qx = (lane & (QR - 1)) * 4, qy = lane >> qsh;
+    // u16-lane masks (1 / 0) of the zone's columns: even lanes hold (qx, qx+2), odd lanes (qx+1, qx+3)
+    const us2 pme = {(unsigned short)(qx < zw), (unsigned short)(qx + 2 < zw)};
+    const us2 pmo = {(unsigned short)(qx + 1 < zw), (unsigned short)(qx + 3 < zw)};
 
     // Stage 1 (dense): the compass pre-test (points 0/4/8/12) on 4 pixels per lane; a lane whose group
-    // of 4 has a passer appends one entry to a ring of GR_RING groups in row-major order: the bright /
-    // dark pass bits of its pixels (FB_PX0..3) and the group's zone position ((qx >> 2) at bits 0-3,
-    // y at bits 13-18).
+    // of 4 has a passer appends one entry (pass bits 0, 1, 16, 17 = pixels qx .. qx+3, the group's
+    // zone index (y << 8) | qx at bits 2-15) to a ring of GR_RING groups in row-major order.
     // Stage 2, whenever 64 groups are pending: the diagonal pre-test (points 2/6/10/14: a 9-arc also
-    // holds two circle-adjacent ones of them), per polarity and ANDed with the compass bits; survivors
-    // are appended per pixel to a second ring in row-major order as (y << 8 | x) | polarities << 14.
-    // Stage 3, whenever 64 pixels are pending: the corner strength M of the open polarities.  Corners
-    // (M > the pass threshold) get M in the zone map and are appended to the ordered corner list.
+    // holds two circle-adjacent ones of them) on the passers of 64 groups, survivors appended per pixel
+    // to a second ring in row-major order (14 % -> 5 % of the pixels on the synthetic frames).
+    // Stage 3, whenever 64 pixels are pending: the corner strength M densely.  Corners (M > the pass
+    // threshold) get M in the zone map and are appended to the ordered corner list.
     // (pending groups < 64 + 64 <= GR_RING; pending pixels < 64 + 256 <= FQ2_RING.)
     uint32_t* gring = reinterpret_cast<uint32_t*>(queue);
-    unsigned short* queue2 = reinterpret_cast<unsigned short*>(queue + 2 * GR_RING);
+    short* queue2 = queue + 2 * GR_RING;
     int qn = 0, head = 0, q2n = 0, h2 = 0, nc = 0;
     auto strength = [&](int n) {
-        const int e = lane < n ? (int)queue2[(h2 + lane) & (FQ2_RING - 1)] : 0;
-        const int i = e & 0x3fff, pol = e >> 14;   // pol 0: no pixel in this lane
+        const int i = lane < n ? queue2[(h2 + lane) & (FQ2_RING - 1)] : -1;
         int M = 0;
-        if (pol) M = corner_strength_pol(&crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)], CSd, pol);
-        const bool c = pol != 0 && M > tp;
+        if (i >= 0) M = corner_strength_pk<CST>(&crop[__mul24((i >> 8) + 3, CSd) + 4 + (i & 255)], CSd);
+#ifdef FAST_DUP_STRENGTH   // diagnostic: the strength network twice (result discarded)
+        if (i >= 0) asm volatile("" ::"v"(corner_strength_pk<CST>(&crop[__mul24((i >> 8) + 4, CSd) + 4 + (i & 255)], CSd)));
+#endif
+        const bool c = M > tp;
         const unsigned long long bm = __ballot(c);
         if (c) {
             const int pos = nc + rank64(bm);
@@ -1009,45 +1034,46 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     };
     auto drain = [&](int n) {
         const uint32_t e = lane < n ? gring[(head + lane) & (GR_RING - 1)] : 0u;   // 0: no pass bits
-        const int i0 = (int)(((e >> 5) & 0x3f00u) | ((e & 15u) << 2));           // zone (y << 8) | x
+        const int i0 = (int)((e >> 2) & 0x3fffu);
         const uint8_t* c = crop + __mul24((i0 >> 8) + 3, CSd) + 4 + (i0 & 255);   // zone (y, x): dword aligned
         const uint32_t* cp = reinterpret_cast<const uint32_t*>(c + 2 * CSd);
         const uint32_t* cm = reinterpret_cast<const uint32_t*>(c - 2 * CSd);
         const uint32_t wv = *reinterpret_cast<const uint32_t*>(c);
         const uint32_t ap = cp[-1], bp = cp[0], dp = cp[1], am = cm[-1], bm_ = cm[0], dm = cm[1];
-        // (+-2, +-2): R = bytes x+2..x+5, L = bytes x-2..x+1 of rows +-2, split into even / odd pixels
-        const uint32_t Rpe = __builtin_amdgcn_perm(dp, bp, 0x0c040c02u), Rpo = __builtin_amdgcn_perm(dp, bp, 0x0c050c03u);
-        const uint32_t Lpe = __builtin_amdgcn_perm(bp, ap, 0x0c040c02u), Lpo = __builtin_amdgcn_perm(bp, ap, 0x0c050c03u);
-        const uint32_t Rme = __builtin_amdgcn_perm(dm, bm_, 0x0c040c02u), Rmo = __builtin_amdgcn_perm(dm, bm_, 0x0c050c03u);
-        const uint32_t Lme = __builtin_amdgcn_perm(bm_, am, 0x0c040c02u), Lmo = __builtin_amdgcn_perm(bm_, am, 0x0c050c03u);
-        const Thr4 T = thr4(wv, TK);
-        // opposite pairs: (+2, +2) / (-2, -2) and (+2, -2) / (-2, +2)
-        const uint32_t Z = two_of_four4(T, Rpe, Rpo, Lme, Lmo, Rme, Rmo, Lpe, Lpo, FB_BE, FB_DE, FB_BO, FB_DO) & e;
+        const uint32_t Lp = __builtin_amdgcn_alignbyte(bp, ap, 2), Rp = __builtin_amdgcn_alignbyte(dp, bp, 2);
+        const uint32_t Lm = __builtin_amdgcn_alignbyte(bm_, am, 2), Rm = __builtin_amdgcn_alignbyte(dm, bm_, 2);
+        // position 2 = (+2, +2): Rp, 10 = (-2, -2): Lm, 6 = (+2, -2): Rm, 14 = (-2, +2): Lp
+        const PkThr T = pk_thresholds(wv, tp);
+        const us2 se = __builtin_elementwise_min(
+            pk_two_of_four(pk_even(Rp), pk_even(Lm), pk_even(Rm), pk_even(Lp), T.hi_e, T.lo_e), u2us(e & 0x00010001u));
+        const us2 so = __builtin_elementwise_min(pk_two_of_four(u2us(Rp), u2us(Lm), u2us(Rm), u2us(Lp), T.hi_o, T.lo_o),
+                                                 u2us((e >> 1) & 0x00010001u));
         // ordered compaction of up to 4 survivors per lane: one ballot per pixel slot, the lane's
         // position = the survivors of the lower lanes (mbcnt) + its own earlier slots
-        const bool p0 = (Z & FB_PX0) != 0, p1 = (Z & FB_PX1) != 0, p2 = (Z & FB_PX2) != 0, p3 = (Z & FB_PX3) != 0;
+        const bool p0 = se.x != 0, p1 = so.x != 0, p2 = se.y != 0, p3 = so.y != 0;
         const unsigned long long b0 = __ballot(p0), b1 = __ballot(p1), b2 = __ballot(p2), b3 = __ballot(p3);
         unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0u));
         pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, pre));
         pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, pre));
         pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, pre));
         int pos = q2n + (int)pre;
-        // queue entry: zone index | open polarities (bit 14 bright, bit 15 dark)
-        if (p0) queue2[pos++ & (FQ2_RING - 1)] = (unsigned short)(i0 | (((Z >> 9) & 3u) << 14));
-        if (p1) queue2[pos++ & (FQ2_RING - 1)] = (unsigned short)((i0 + 1) | (((Z >> 11) & 3u) << 14));
-        if (p2) queue2[pos++ & (FQ2_RING - 1)] = (unsigned short)((i0 + 2) | (((Z >> 25) & 3u) << 14));
-        if (p3) queue2[pos & (FQ2_RING - 1)] = (unsigned short)((i0 + 3) | ((Z >> 27) << 14));
+        if (p0) queue2[pos++ & (FQ2_RING - 1)] = (short)i0;
+        if (p1) queue2[pos++ & (FQ2_RING - 1)] = (short)(i0 + 1);
+        if (p2) queue2[pos++ & (FQ2_RING - 1)] = (short)(i0 + 2);
+        if (p3) queue2[pos & (FQ2_RING - 1)] = (short)(i0 + 3);
         q2n += popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
         head += n;
         wave_lds_sync();
         while (q2n - h2 >= 64) strength(64);
     };
-    // per-lane LDS address of zone (qy, qx) = crop (qy+3, qx+3) at byte qx+4, stepped by a wave-uniform
-    // amount per chunk of RPC rows
+    // per-lane LDS address of zone (qy, qx) = crop (qy+3, qx+3) at byte qx+4 and the group's zone index
+    // (qy << 8) | qx at bits 2-15, both stepped by a wave-uniform amount per chunk of RPC rows
     const uint8_t* rowq = crop + __mul24(qy + 3, CSd) + 4 + qx;
+    const uint32_t e0s = (uint32_t)((qy << 8) | qx) << 2;
+    const bool qxin = qx < zw;
     for (int yb = 0, yoff = 0; yb < zh; yb += RPC, yoff += RPC * CSd) {
         const int y = yb + qy;
-        uint32_t Z = 0;
+        us2 pe = {0, 0}, po = {0, 0};
         if (y < zh && qxin) {
             const uint8_t* rowc = rowq + yoff;   // zone (y, qx)
             const uint32_t wv = *reinterpret_cast<const uint32_t*>(rowc);
@@ -1055,16 +1081,27 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
             const uint32_t wr = *reinterpret_cast<const uint32_t*>(rowc + 4);
             const uint32_t wn = *reinterpret_cast<const uint32_t*>(rowc + 3 * CSd);   // (0,+3)
             const uint32_t ws = *reinterpret_cast<const uint32_t*>(rowc - 3 * CSd);   // (0,-3)
-            const Thr4 T = thr4(wv, TK);
-            // (+3, 0): bytes qx+3..qx+6, (-3, 0): bytes qx-3..qx, split into even / odd pixels
-            const uint32_t ee = __builtin_amdgcn_perm(wr, wv, 0x0c050c03u), eo = __builtin_amdgcn_perm(wr, wv, 0x0c060c04u);
-            const uint32_t we = __builtin_amdgcn_perm(wv, wl, 0x0c030c01u), wo = __builtin_amdgcn_perm(wv, wl, 0x0c040c02u);
-            Z = two_of_four4(T, wn & 0x00ff00ffu, odd_px(wn), ws & 0x00ff00ffu, odd_px(ws), ee, eo, we, wo, zm0, zm1, zm2,
-                             zm3);
+            const uint32_t we = __builtin_amdgcn_alignbyte(wr, wv, 3);   // (+3, 0): bytes qx+3..qx+6
+            const uint32_t ww = __builtin_amdgcn_alignbyte(wv, wl, 1);   // (-3, 0): bytes qx-3..qx
+            const PkThr T = pk_thresholds(wv, tp);
+            pe = __builtin_elementwise_min(
+                pk_two_of_four(pk_even(wn), pk_even(ws), pk_even(we), pk_even(ww), T.hi_e, T.lo_e), pme);
+            po = __builtin_elementwise_min(pk_two_of_four(u2us(wn), u2us(ws), u2us(we), u2us(ww), T.hi_o, T.lo_o), pmo);
+#ifdef FAST_DUP_PRETEST   // diagnostic: the pre-test arithmetic twice (result discarded)
+            {
+                const PkThr T2 = pk_thresholds(wv, tp ^ yb);
+                asm volatile("" ::"v"(us2u(pk_two_of_four(pk_even(wn), pk_even(ws), pk_even(we), pk_even(ww), T2.hi_e, T2.lo_e))),
+                             "v"(us2u(pk_two_of_four(u2us(wn), u2us(ws), u2us(we), u2us(ww), T2.hi_o, T2.lo_o))));
+            }
+#endif
         }
-        const bool any = Z != 0;
+        const bool any = (us2u(pe) | us2u(po)) != 0;
         const unsigned long long bm = __ballot(any);
-        if (any) gring[(qn + rank64(bm)) & (GR_RING - 1)] = Z | (ebase + ((uint32_t)yb << 13));
+        if (any) {
+            // ring slot = qn + the passers of the lower lanes (mbcnt accumulates qn)
+            const unsigned pos = __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, (unsigned)qn));
+            gring[pos & (GR_RING - 1)] = bt3<BT_OR3>(us2u(pe), us2u(po) + us2u(po), e0s + ((uint32_t)yb << 10));
+        }
         qn += popc64(bm);
         wave_lds_sync();
         if (qn - head >= 64) drain(64);
@@ -2660,8 +2697,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     {
         int mzw = 1, mzh = 1;
         for (const CellDev& c : cells) { mzw = std::max(mzw, c.zwzh & 0xffff); mzh = std::max(mzh, c.zwzh >> 16); }
-        // DetectFAST cells are < 60 px (:508-511); the kernel's queues hold zone rows < 64 (6-bit y)
-        if (mzw > 64 || mzh > std::min(63, (2 * GR_RING + FQ2_RING) / 8)) {
+        if (mzw > 64 || mzh > (2 * GR_RING + FQ2_RING) / 8) {   // DetectFAST cells are < 60 px (:508-511)
             set_error("FAST cell larger than the kernel supports");
             return ORB_EINTERNAL;
         }
@@ -2874,12 +2910,14 @@ namespace orbamd {
 // each 32-byte row as two uint4 (lanes take consecutive 16-byte halves: coalesced both ways).
 __global__ __launch_bounds__(256) void pack_rows_kernel(const uint4* __restrict__ desc, int cap,
                                                         const int* __restrict__ counts, const int* __restrict__ incl,
-                                                        uint4* __restrict__ out) {
+                                                        uint4* __restrict__ out, int out_rows) {
     const int f = blockIdx.x;
-    const int n = counts[f];
-    const long long o = (long long)(incl[f] - n) * 2;
+    const int c = counts[f];
+    const int n = min(max(c, 0), cap);                // never read past the frame's slots
+    const long long start = (long long)incl[f] - c;   // the caller's layout
+    const long long r0 = max(start, 0ll), r1 = min(start + n, (long long)out_rows);   // never write past out
     const uint4* src = desc + (long long)f * cap * 2;
-    for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) out[o + i] = src[i];
+    for (long long i = 2 * r0 + threadIdx.x; i < 2 * r1; i += blockDim.x) out[i] = src[i - 2 * start];
 }
 
 }  // namespace orbamd
@@ -3140,14 +3178,15 @@ int orbx_profile_enable(orbx_extractor* h, int enable) {
 }
 
 int orbx_pack_descriptors(const uint8_t* desc, int32_t cap, const int32_t* counts, const int32_t* incl,
-                          int32_t n_frames, uint8_t* out, void* stream) {
-    ORB_CHECK_ARG(n_frames >= 0 && cap >= 0, "negative sizes");
-    if (n_frames == 0) return ORB_OK;
+                          int32_t n_frames, uint8_t* out, int32_t out_rows, void* stream) {
+    ORB_CHECK_ARG(n_frames >= 0 && cap >= 0 && out_rows >= 0, "negative sizes");
+    if (n_frames == 0 || out_rows == 0) return ORB_OK;
     ORB_CHECK_ARG(desc && counts && incl && out, "null argument");
     ORB_CHECK_ARG(((reinterpret_cast<uintptr_t>(desc) | reinterpret_cast<uintptr_t>(out)) & 15) == 0,
                   "desc / out must be 16-byte aligned");
     hipLaunchKernelGGL(orbamd::pack_rows_kernel, dim3((unsigned)n_frames), dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const uint4*>(desc), (int)cap, counts, incl, reinterpret_cast<uint4*>(out));
+                       reinterpret_cast<const uint4*>(desc), (int)cap, counts, incl, reinterpret_cast<uint4*>(out),
+                       (int)out_rows);
     ORB_HIP_TRY(hipGetLastError());
     return ORB_OK;
 }

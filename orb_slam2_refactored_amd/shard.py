@@ -218,7 +218,7 @@ class CompactExchange:
                 cnt = self.counts_all[i].view(self.world, self.frames)[self.rank]
                 incl = torch.cumsum(cnt, 0, dtype=torch.int32)
                 check(lib().orbx_pack_descriptors(tptr(src.desc), self.cap, tptr(cnt), tptr(incl), self.frames,
-                                                  tptr(self.send[i]), stream_ptr(self.side)),
+                                                  tptr(self.send[i]), int(self.send[i].shape[0]), stream_ptr(self.side)),
                       "orbx_pack_descriptors")
             elif n:
                 # (CPU / gloo) row r of the block: frame fr = the frame whose prefix range holds r, slot r - start[fr]

@@ -13,14 +13,40 @@ ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "orb_slam2_refactored_amd" / "csrc"
 
 
-@pytest.mark.parametrize("src", ["orbba.hip"])
-def test_no_dpp_hazards(tmp_path, src):
+# the shipped build, plus the variants the A/B scripts build: SB_SPLIT_DEF (Schur-block parts) and a
+# diagonal-pivot include generated with no Newton step after v_rcp_f64 (tools/gen_ba_diag.py 0)
+VARIANTS = [("orbba.hip", []), ("orbba.hip", ["-DSB_SPLIT_DEF=8"]), ("orbba.hip", ["newton0"]), ("orbx.hip", [])]
+
+
+@pytest.mark.parametrize("src,flags", VARIANTS, ids=["orbba", "orbba-sb8", "orbba-newton0", "orbx"])
+def test_no_dpp_hazards(tmp_path, src, flags):
     listing = tmp_path / (src + ".s")
+    extra = list(flags)
+    if "newton0" in extra:
+        inc = tmp_path / "orbba_diag_n0.inc"
+        subprocess.run([sys.executable, str(ROOT / "tools" / "gen_ba_diag.py"), "0", str(inc)], check=True,
+                       capture_output=True, timeout=120)
+        extra = [f'-DORBBA_DIAG_INC="{inc}"']
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-           f"-I{ROOT / 'include'}", f"-I{CSRC}", "--cuda-device-only", "-S", str(CSRC / src), "-o", str(listing)]
+           f"-I{ROOT / 'include'}", f"-I{CSRC}", "--cuda-device-only", "-S", str(CSRC / src), "-o", str(listing)] + extra
+    if src == "orbx.hip":
+        cmd += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
     if not Path(cmd[0]).exists():
         pytest.skip("hipcc not available")
     subprocess.run(cmd, check=True, capture_output=True, timeout=600)
     out = subprocess.run([sys.executable, str(ROOT / "tools" / "dpp_hazard_check.py"), str(listing)],
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_checker_follows_branch_edges(tmp_path):
+    """A VALU write 1 wait state before a branch reaches the DPP read at the target through the edge,
+    even though the fall-through path pads it (the checker's round-3 blind spot)."""
+    s = tmp_path / "t.s"
+    s.write_text("kern:\n\tv_mov_b32 v2, v1\n\ts_cbranch_scc1 .L2\n\ts_nop 4\n.L2:\n"
+                 "\tv_add_f64_dpp v[4:5], v[2:3], v[6:7] row_newbcast:1\n\ts_endpgm\n"
+                 "ok:\n\tv_mov_b32 v2, v1\n\ts_cbranch_scc1 .L3\n\ts_nop 4\n.L3:\n\ts_nop 1\n"
+                 "\tv_add_f64_dpp v[4:5], v[2:3], v[6:7] row_newbcast:1\n\ts_endpgm\n")
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "dpp_hazard_check.py"), str(s)], capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode == 1 and "kern:" in out.stdout and "ok:" not in out.stdout, out.stdout

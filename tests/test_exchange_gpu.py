@@ -48,4 +48,26 @@ def test_pack_descriptors_rejects_misaligned():
     c = torch.ones(2, dtype=torch.int32, device="cuda")
     with pytest.raises(_lib.OrbError):
         _lib.check(_lib.lib().orbx_pack_descriptors(_lib.tptr(d[1:]), 4, _lib.tptr(c), _lib.tptr(c), 2,
-                                                    _lib.tptr(d), _lib.stream_ptr()), "orbx_pack_descriptors")
+                                                    _lib.tptr(d), 2, _lib.stream_ptr()), "orbx_pack_descriptors")
+
+
+def test_pack_descriptors_clamps_counts_and_output():
+    """counts past the slot capacity copy only `cap` rows, and rows past out_rows are never
+    written (a guard row after the output stays intact)."""
+    frames, cap = 3, 4
+    g = torch.Generator().manual_seed(7)
+    desc = torch.randint(0, 256, (frames, cap, 32), generator=g, dtype=torch.uint8)
+    counts = torch.tensor([2, 9, 3], dtype=torch.int32)   # frame 1 claims more rows than its slots
+    incl = torch.cumsum(counts, 0, dtype=torch.int32)      # the caller's layout: rows 0-1, 2-10, 11-13
+    out_rows = 12
+    buf = torch.full((out_rows + 1, 32), 0xA5, dtype=torch.uint8, device="cuda")
+    _lib.check(_lib.lib().orbx_pack_descriptors(_lib.tptr(desc.cuda()), cap, _lib.tptr(counts.cuda()),
+                                                _lib.tptr(incl.cuda()), frames, _lib.tptr(buf), out_rows,
+                                                _lib.stream_ptr()), "orbx_pack_descriptors")
+    torch.cuda.synchronize()
+    got = buf.cpu()
+    assert torch.equal(got[0:2], desc[0, :2])
+    assert torch.equal(got[2:6], desc[1, :4])               # clamped to cap rows
+    assert (got[6:11] == 0xA5).all()                        # the rows frame 1 claimed beyond cap: untouched
+    assert torch.equal(got[11:12], desc[2, :1])             # frame 2 clipped at out_rows
+    assert (got[12] == 0xA5).all()                          # the guard row after out_rows: untouched
