@@ -1,0 +1,208 @@
+// LocalBA host-side structure (SparseOptimizer::initializeOptimization + the BlockSolver fill
+// pattern), plain C++ so that a CPU probe (tools/probe/ba_struct_bench.cpp) and orbba.hip share it.
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+namespace orbamd_host {
+
+struct int2h {
+    int x, y;
+};
+
+struct HostStructure {
+    std::vector<int> act, hp, hl, pt_beg, pt_slot, pt_id, ps_beg, ps_slot, ps_id, blk_i1, blk_i2, blk_beg;
+    std::vector<int2h> blk_pair;
+    std::vector<int> blk_index, fs_beg, fs_slot, fs_hp, sl, sp, cur;   // scratch (capacity kept across calls)
+    std::vector<uint8_t> pa, la;
+    std::vector<unsigned long long> col;   // per-pose bitsets over the points (pair blocks)
+    std::vector<int> slot_of;              // [point][pose] -> free slot (pair blocks)
+    int np = 0, nl = 0;
+};
+
+// SparseOptimizer::initializeOptimization(level) (sparse_optimizer.cpp:206-264) and the
+// BlockSolver structure (block_solver.hpp:142-295): active edges / vertices, Hessian indices, and
+// the Schur fill pattern (pose pairs that share a point).  Flat two-pass build (count, then fill)
+// over per-slot (point, pose) Hessian ids, into vectors that keep their capacity across calls: no
+// allocation per point or per block.
+// Pair order inside a block: points ascending, then (slot a, slot c) in the point's slot order.
+inline void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
+                     const int* ek, HostStructure& s) {
+    const int E = (int)level.size();
+    s.pa.assign(P, 0);
+    s.la.assign(N, 0);
+    s.act.resize(E);
+    int Ea = 0;
+    {
+        int* act = s.act.data();
+        uint8_t* pa = s.pa.data();
+        uint8_t* la = s.la.data();
+        for (int e = 0; e < E; e++)
+            if (level[e] == 0) { act[Ea++] = e; pa[ek[e]] = 1; la[ep[e]] = 1; }
+    }
+    s.act.resize(Ea);
+    s.hp.resize(P); s.hl.resize(N);
+    s.ps_id.resize(P); s.pt_id.resize(N);
+    int np = 0, nl = 0;
+    for (int i = 0; i < P; i++) {
+        s.hp[i] = (s.pa[i] && !fixed[i]) ? np : -1;
+        if (s.hp[i] >= 0) s.ps_id[np++] = i;
+    }
+    for (int i = 0; i < N; i++) {
+        s.hl[i] = s.la[i] ? nl : -1;
+        if (s.la[i]) s.pt_id[nl++] = i;
+    }
+    s.ps_id.resize(np); s.pt_id.resize(nl);
+    s.np = np; s.nl = nl;
+    // per active slot k: its point's and pose's Hessian ids
+    s.sl.resize(Ea); s.sp.resize(Ea);
+    int* sl = s.sl.data();
+    int* sp = s.sp.data();
+    for (int k = 0; k < Ea; k++) {
+        const int e = s.act[k];
+        sl[k] = s.hl[ep[e]];
+        sp[k] = s.hp[ek[e]];
+    }
+    s.pt_beg.assign(nl + 1, 0); s.ps_beg.assign(np + 1, 0); s.fs_beg.assign(nl + 1, 0);
+    {
+        int* pb = s.pt_beg.data();
+        int* qb = s.ps_beg.data();
+        int* fb = s.fs_beg.data();
+        for (int k = 0; k < Ea; k++) {
+            pb[sl[k] + 1]++;
+            if (sp[k] >= 0) { qb[sp[k] + 1]++; fb[sl[k] + 1]++; }
+        }
+        for (int i = 0; i < nl; i++) { pb[i + 1] += pb[i]; fb[i + 1] += fb[i]; }
+        for (int i = 0; i < np; i++) qb[i + 1] += qb[i];
+    }
+    s.pt_slot.resize(Ea); s.ps_slot.resize(s.ps_beg[np]);
+    s.fs_slot.resize(s.fs_beg[nl]); s.fs_hp.resize(s.fs_beg[nl]);
+    {
+        // fill cursors (k ascending, so every list is in slot order)
+        s.cur.resize(2 * (size_t)nl + np);
+        int* fp = s.cur.data();
+        int* fr = fp + nl;
+        int* fq = fr + nl;
+        std::copy(s.pt_beg.begin(), s.pt_beg.end() - 1, fp);
+        std::copy(s.fs_beg.begin(), s.fs_beg.end() - 1, fr);
+        std::copy(s.ps_beg.begin(), s.ps_beg.end() - 1, fq);
+        int* pts = s.pt_slot.data();
+        int* pss = s.ps_slot.data();
+        int* fss = s.fs_slot.data();
+        int* fsh = s.fs_hp.data();
+        for (int k = 0; k < Ea; k++) {
+            const int l = sl[k], h = sp[k];
+            pts[fp[l]++] = k;
+            if (h >= 0) {
+                pss[fq[h]++] = k;
+                fss[fr[l]] = k;
+                fsh[fr[l]++] = h;
+            }
+        }
+    }
+    // pose-pair blocks (i1 <= i2): pass 1 counts the pairs per block, pass 2 fills them, from each
+    // point's free slots (slot order) with their Hessian pose index.  Reference order inside a block:
+    // points ascending, then (slot a, slot c) in the point's slot order with pose(a) <= pose(c).
+    //
+    // Bitset path: a point that sees every free pose at most once (a MapPoint holds one observation
+    // per keyframe) has exactly one pair in each block it touches, so block (i1, i2) holds the points
+    // of col[i1] & col[i2] (per-pose bitsets over the points) in ascending order: counts are popcounts
+    // and the fill walks the set bits, with the same result as the two nested slot loops below, which
+    // remain for problems where some point repeats a pose.
+    {
+        const int W = (nl + 63) >> 6;
+        s.col.assign((size_t)np * W, 0ull);
+        s.slot_of.resize((size_t)std::max(nl, 1) * std::max(np, 1));   // read only where written
+        const int* fh = s.fs_hp.data();
+        const int* fb = s.fs_beg.data();
+        const int* fsl = s.fs_slot.data();
+        unsigned long long* col = s.col.data();
+        int* so = s.slot_of.data();
+        bool dup = false;
+        for (int l = 0; l < nl && !dup; l++)
+            for (int a = fb[l]; a < fb[l + 1]; a++) {
+                unsigned long long& w = col[(size_t)fh[a] * W + (l >> 6)];
+                const unsigned long long bit = 1ull << (l & 63);
+                dup |= (w & bit) != 0;
+                w |= bit;
+                so[(size_t)l * np + fh[a]] = fsl[a];
+            }
+        if (!dup) {
+            s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0);
+            int total = 0;
+            for (int i1 = 0; i1 < np; i1++)
+                for (int i2 = i1; i2 < np; i2++) {
+                    const unsigned long long* c1 = col + (size_t)i1 * W;
+                    const unsigned long long* c2 = col + (size_t)i2 * W;
+                    int cnt = 0;
+                    for (int w = 0; w < W; w++) cnt += __builtin_popcountll(c1[w] & c2[w]);
+                    if (cnt == 0 && i1 != i2) continue;
+                    s.blk_i1.push_back(i1);
+                    s.blk_i2.push_back(i2);
+                    total += cnt;
+                    s.blk_beg.push_back(total);
+                }
+            s.blk_pair.resize(total);
+            int2h* out = s.blk_pair.data();
+            for (size_t k = 0; k < s.blk_i1.size(); k++) {
+                const int i1 = s.blk_i1[k], i2 = s.blk_i2[k];
+                const unsigned long long* c1 = col + (size_t)i1 * W;
+                const unsigned long long* c2 = col + (size_t)i2 * W;
+                for (int w = 0; w < W; w++)
+                    for (unsigned long long m = c1[w] & c2[w]; m; m &= m - 1) {
+                        const int l = (w << 6) + __builtin_ctzll(m);
+                        *out++ = int2h{so[(size_t)l * np + i1], so[(size_t)l * np + i2]};
+                    }
+            }
+            return;
+        }
+    }
+    s.blk_index.assign((size_t)np * np, 0);
+    {
+        const int* fh = s.fs_hp.data();
+        const int* fb = s.fs_beg.data();
+        int* cnt = s.blk_index.data();
+        for (int l = 0; l < nl; l++) {
+            const int b0 = fb[l], b1 = fb[l + 1];
+            for (int a = b0; a < b1; a++) {
+                const int i1 = fh[a];
+                int* row = cnt + (size_t)i1 * np;
+                for (int c = b0; c < b1; c++) row[fh[c]] += i1 <= fh[c];
+            }
+        }
+    }
+    s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0);
+    int total = 0;
+    for (int i1 = 0; i1 < np; i1++)
+        for (int i2 = i1; i2 < np; i2++) {
+            int& cnt = s.blk_index[(size_t)i1 * np + i2];
+            if (cnt == 0 && i1 != i2) { cnt = -1; continue; }
+            s.blk_i1.push_back(i1);
+            s.blk_i2.push_back(i2);
+            const int beg = total;
+            total += cnt;
+            cnt = beg;   // now the block's fill cursor
+            s.blk_beg.push_back(total);
+        }
+    s.blk_pair.resize(total);
+    {
+        const int* fh = s.fs_hp.data();
+        const int* fb = s.fs_beg.data();
+        const int* fsl = s.fs_slot.data();
+        int* curp = s.blk_index.data();
+        int2h* out = s.blk_pair.data();
+        for (int l = 0; l < nl; l++) {
+            const int b0 = fb[l], b1 = fb[l + 1];
+            for (int a = b0; a < b1; a++) {
+                const int i1 = fh[a];
+                int* row = curp + (size_t)i1 * np;
+                for (int c = b0; c < b1; c++)
+                    if (i1 <= fh[c]) out[row[fh[c]]++] = int2h{fsl[a], fsl[c]};
+            }
+        }
+    }
+}
+
+
+}  // namespace orbamd_host

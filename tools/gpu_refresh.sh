@@ -23,7 +23,7 @@ cp gpurun_out/traffic_$TAG/${TAG}_traffic.json profiles/${TAG}_traffic.json
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_$TAG.log 2>&1 || { tail -30 gpurun_out/bench_$TAG.log; exit 5; }
 grep '^{' gpurun_out/bench_$TAG.log > gpurun_out/profiles_$TAG/${TAG}_bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-legs \
+    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-legs --no-c5 \
     > gpurun_out/prof_${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_bench.log; exit 6; }
 grep '^{' gpurun_out/prof_${TAG}_bench.log > gpurun_out/profiles_$TAG/${TAG}_bench_under_rocprof.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_legs -o run -- \
