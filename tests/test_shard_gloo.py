@@ -226,3 +226,35 @@ def test_compact_exchange_single_process():
         ex.publish(k)
     ex.drain()
     assert torch.equal(ex.block(2, 0), _packed(fake_slots(0, 2)))
+
+
+def _pack_rows_reference(desc, cap, counts, incl, out_rows):
+    """The index math of orbx_pack_descriptors (csrc/orbx.hip pack_rows_kernel) on the CPU: frame f's first
+    min(max(counts[f], 0), cap) rows go to out rows from incl[f] - counts[f], clipped to [0, out_rows)."""
+    out = torch.zeros((out_rows, 32), dtype=torch.uint8)
+    for f in range(desc.shape[0]):
+        c = int(counts[f])
+        n = min(max(c, 0), cap)
+        start = int(incl[f]) - c
+        for r in range(max(start, 0), min(start + n, out_rows)):
+            out[r] = desc[f, r - start]
+    return out
+
+
+def test_cuda_pack_index_math_matches_gloo_pack():
+    """the device pack (inclusive-prefix offsets, bench.py's CUDA path) and the gloo path's
+    repeat_interleave / index_select pack produce the same block for ragged counts incl. 0 and cap."""
+    g = torch.Generator().manual_seed(11)
+    for frames, cap in ((1, 5), (6, 7), (33, 40)):
+        desc = torch.randint(0, 256, (frames, cap, 32), generator=g, dtype=torch.int64).to(torch.uint8)
+        counts = torch.randint(0, cap + 1, (frames,), generator=g, dtype=torch.int64).to(torch.int32)
+        counts[0] = 0
+        counts[-1] = cap
+        incl = torch.cumsum(counts, 0, dtype=torch.int32)
+        n = int(counts.sum())
+        # the gloo branch of CompactExchange._payload
+        start = torch.cumsum(counts, 0) - counts
+        fr = torch.repeat_interleave(torch.arange(frames), counts.to(torch.int64), output_size=n)
+        row = torch.arange(n) - start[fr]
+        gloo = torch.index_select(desc.view(-1, 32), 0, fr * cap + row)
+        assert torch.equal(_pack_rows_reference(desc, cap, counts, incl, n), gloo)
