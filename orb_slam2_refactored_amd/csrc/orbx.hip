@@ -646,43 +646,16 @@ __device__ __forceinline__ us2 pk_two_of_four(us2 p1, us2 p3, us2 p2, us2 p4, us
 // two arcs at once; position j >= 8 is the swapped pair j - 8.  The network runs on the raw pixels:
 // max over arcs of min(p) - v is the bright strength, v - min over arcs of max(p) the dark one.
 __device__ __forceinline__ us2 swap2(us2 a) { return __builtin_shufflevector(a, a, 1, 0); }
-// The 16 circle bytes as packed pairs.  With a compile-time row stride CS the pairs are loaded straight
-// into the u16 halves by ds_read_u8_d16 / ds_read_u8_d16_hi (offsets from the circle's top-left byte),
-// which the compiler does not form on its own (it loads 16 dwords and packs them with 8 v_perm).
+// The 16 circle bytes as packed pairs (the compiler packs them with v_perm; ds_read_u8_d16_hi cannot
+// be used: with SRAM ECC enabled, as on MI355X, d16 loads zero the other half of the register
+// instead of preserving it -- a round-4 attempt failed tests/test_extractor_gpu.py exactly so).
 template <int CS>
 __device__ __forceinline__ void circle_pairs(const uint8_t* c, int cs, us2 (&D)[8]) {
-    if constexpr (CS != 0) {
-        // one asm statement with its own wait: the compiler does not know these loads are in flight
-        const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(c - 3 * CS - 3);   // LDS offset (low 32 bits)
-        uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
-#define ORBX_OFF(k) (c_circle_dy_h[k] + 3) * CS + c_circle_dx_h[k] + 3
-        asm volatile(
-            "ds_read_u8_d16 %0, %8 offset:%9\n\tds_read_u8_d16 %1, %8 offset:%10\n\t"
-            "ds_read_u8_d16 %2, %8 offset:%11\n\tds_read_u8_d16 %3, %8 offset:%12\n\t"
-            "ds_read_u8_d16 %4, %8 offset:%13\n\tds_read_u8_d16 %5, %8 offset:%14\n\t"
-            "ds_read_u8_d16 %6, %8 offset:%15\n\tds_read_u8_d16 %7, %8 offset:%16\n\t"
-            "ds_read_u8_d16_hi %0, %8 offset:%17\n\tds_read_u8_d16_hi %1, %8 offset:%18\n\t"
-            "ds_read_u8_d16_hi %2, %8 offset:%19\n\tds_read_u8_d16_hi %3, %8 offset:%20\n\t"
-            "ds_read_u8_d16_hi %4, %8 offset:%21\n\tds_read_u8_d16_hi %5, %8 offset:%22\n\t"
-            "ds_read_u8_d16_hi %6, %8 offset:%23\n\tds_read_u8_d16_hi %7, %8 offset:%24\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
-            : "v"(a), "i"(ORBX_OFF(0)), "i"(ORBX_OFF(1)), "i"(ORBX_OFF(2)), "i"(ORBX_OFF(3)), "i"(ORBX_OFF(4)),
-              "i"(ORBX_OFF(5)), "i"(ORBX_OFF(6)), "i"(ORBX_OFF(7)), "i"(ORBX_OFF(8)), "i"(ORBX_OFF(9)),
-              "i"(ORBX_OFF(10)), "i"(ORBX_OFF(11)), "i"(ORBX_OFF(12)), "i"(ORBX_OFF(13)), "i"(ORBX_OFF(14)),
-              "i"(ORBX_OFF(15))
-            : "memory");
-#undef ORBX_OFF
-        D[0] = __builtin_bit_cast(us2, r0); D[1] = __builtin_bit_cast(us2, r1);
-        D[2] = __builtin_bit_cast(us2, r2); D[3] = __builtin_bit_cast(us2, r3);
-        D[4] = __builtin_bit_cast(us2, r4); D[5] = __builtin_bit_cast(us2, r5);
-        D[6] = __builtin_bit_cast(us2, r6); D[7] = __builtin_bit_cast(us2, r7);
-    } else {
+    const int s = CS != 0 ? CS : cs;
 #pragma unroll
-        for (int k = 0; k < 8; k++)
-            D[k] = us2{(unsigned short)c[c_circle_dy_h[k] * cs + c_circle_dx_h[k]],
-                       (unsigned short)c[c_circle_dy_h[k + 8] * cs + c_circle_dx_h[k + 8]]};
-    }
+    for (int k = 0; k < 8; k++)
+        D[k] = us2{(unsigned short)c[c_circle_dy_h[k] * s + c_circle_dx_h[k]],
+                   (unsigned short)c[c_circle_dy_h[k + 8] * s + c_circle_dx_h[k + 8]]};
 }
 template <int CS>
 __device__ __forceinline__ int corner_strength_pk(const uint8_t* c, int cs) {
