@@ -191,12 +191,20 @@ __device__ __forceinline__ uint32_t vcoef24(int b) { return ((uint32_t)b & 0xfff
 constexpr int PYR_TW = 64, PYR_TH = 64;
 constexpr int PYR_SW = 144, PYR_SH = 128;   // LDS source tile capacity (scale factor <= ~1.9)
 
+// A tile row's vertical taps, built once per workgroup (round 4): the byte offsets of its two source rows
+// in the staged rectangle (first row sy_lo, row stride PYR_SW) and the two coefficients in mulhi24 form
+// (b << 12), so a row costs one ds_read_b128 and the address adds instead of ~11 VALU of decoding.
+__device__ __forceinline__ int4 pyr_row_taps(int2 yv, int sy_lo) {
+    return make_int4(((yv.x & 0xffff) - sy_lo) * PYR_SW, ((yv.x >> 16) - sy_lo) * PYR_SW, (int)vcoef24(yv.y),
+                     (int)vcoef24(yv.y >> 16));
+}
+
 // Level-l output tile (tx0, ty0, tw x th) from the staged source rectangle S (row stride PYR_SW,
-// first row sy_lo, first byte column xa) and the tile's coefficient rows xs_t / ys_t.  Every
+// first byte column xa), the tile's column taps xs_t and its row taps ys_t (pyr_row_taps).  Every
 // thread of the workgroup must call it (block-wide vote inside); no barrier follows the vote.
 __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& L, int f, uint8_t* pyr,
-                                                 const uint8_t* S, const int2* xs_t, const int2* ys_t, int tx0,
-                                                 int ty0, int tw, int th, int xa, int sy_lo) {
+                                                 const uint8_t* S, const int2* xs_t, const int4* ys_t, int tx0,
+                                                 int ty0, int tw, int th, int xa) {
     {
         // 32 threads per 64-px output row (2 px each), 8 rows per pass.  Both pixels' four taps lie
         // in the 8 LDS bytes from dword wd (scale <= ~3), so one row costs two dword reads; v_perm
@@ -215,13 +223,15 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
             const uint32_t sel0 = (uint32_t)e00 | 0x0c00u | ((uint32_t)e01 << 16) | 0x0c000000u;
             const uint32_t sel1 = (uint32_t)e10 | 0x0c00u | ((uint32_t)e11 << 16) | 0x0c000000u;
             const us2 a0 = *reinterpret_cast<const us2*>(&xv0.y), a1 = *reinterpret_cast<const us2*>(&xv1.y);
-            const uint32_t* S32 = reinterpret_cast<const uint32_t*>(S) + wd;
+            const uint8_t* Sw = S + 4 * wd;
             uint8_t* dcol = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + p0;
             for (int ty = threadIdx.x >> 5; ty < th; ty += 8) {
-                const int2 yv = ys_t[ty];
-                const int r0 = __mul24((yv.x & 0xffff) - sy_lo, PYR_SW / 4), r1 = __mul24((yv.x >> 16) - sy_lo, PYR_SW / 4);
-                const uint32_t b0 = vcoef24(yv.y), b1 = vcoef24(yv.y >> 16);
-                const uint32_t w00 = S32[r0], w01 = S32[r0 + 1], w10 = S32[r1], w11 = S32[r1 + 1];
+                const int4 yv = ys_t[ty];
+                const uint32_t* s0 = reinterpret_cast<const uint32_t*>(Sw + yv.x);
+                const uint32_t* s1 = reinterpret_cast<const uint32_t*>(Sw + yv.y);
+                // (the masks only tell the compiler b << 12 fits 24 bits: v_mul_hi_u32_u24, not v_mul_hi_u32)
+                const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;
+                const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
                 auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
                     const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
                     return *reinterpret_cast<const us2*>(&r);
@@ -247,9 +257,9 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
     uint8_t* dbase = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + q0;
 #pragma nounroll
     for (int ty = threadIdx.x >> 4; ty < th; ty += 16) {
-        const int2 yv = ys_t[ty];
-        const int r0 = ((yv.x & 0xffff) - sy_lo) * PYR_SW, r1 = ((yv.x >> 16) - sy_lo) * PYR_SW;
-        const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
+        const int4 yv = ys_t[ty];
+        const int r0 = yv.x, r1 = yv.y;
+        const int b0 = yv.z >> 12, b1 = yv.w >> 12;
         uint32_t packed = 0;
 #pragma nounroll
         for (int k = 0; k < 4; k++) {
@@ -351,7 +361,8 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
                                                             const int2* __restrict__ xtab,
                                                             const int2* __restrict__ ytab) {
     __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW + 16];   // +16: the 8-byte windows may read past the last row
-    __shared__ int2 xs_t[PYR_TW], ys_t[PYR_TH];
+    __shared__ int2 xs_t[PYR_TW];
+    __shared__ int4 ys_t[PYR_TH];
     const LevelDev& L = g.lv[l];
     const LevelDev& Ls = g.lv[l - 1];
     const int gx = gridDim.x, gxy = gridDim.x * gridDim.y;
@@ -364,8 +375,6 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
     const int2* xt = xtab + L.xtab_off;
     const int2* yt = ytab + L.ytab_off;
     // coefficient tables -> LDS (independent of the image loads below)
-    if ((int)threadIdx.x < tw) xs_t[threadIdx.x] = xt[tx0 + threadIdx.x];
-    if ((int)threadIdx.x >= 64 && (int)threadIdx.x - 64 < th) ys_t[threadIdx.x - 64] = yt[ty0 + threadIdx.x - 64];
     // conservative source rectangle from the scale (a superset of the tables' taps; no table
     // round trip before the image loads)
     const int sw = Ls.w, sh = Ls.h;
@@ -373,6 +382,9 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
     const int sx_lo = max(0, (int)floor((tx0 + 0.5) * scx - 0.5) - 2);
     const int sx_hi = min(sw - 1, (int)floor((tx0 + tw - 0.5) * scx - 0.5) + 2);
     const int sy_lo = max(0, (int)floor((ty0 + 0.5) * scy - 0.5) - 2);
+    if ((int)threadIdx.x < tw) xs_t[threadIdx.x] = xt[tx0 + threadIdx.x];
+    if ((int)threadIdx.x >= 64 && (int)threadIdx.x - 64 < th)
+        ys_t[threadIdx.x - 64] = pyr_row_taps(yt[ty0 + threadIdx.x - 64], sy_lo);
     const int sy_hi = min(sh - 1, (int)floor((ty0 + th - 0.5) * scy - 0.5) + 2);
     const int xa = sx_lo & ~3;
     const int nd = (sx_hi - xa + 4) >> 2;   // dwords per source row (<= PYR_SW / 4 < 64)
@@ -388,7 +400,7 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
         pyr_stage(T, threadIdx.x, S, v3, 3);
         pyr_stage(T, threadIdx.x, S, v4, 4);
         __syncthreads();
-        pyr_tile_compute(g, L, f, pyr, S, xs_t, ys_t, tx0, ty0, tw, th, T.xa, sy_lo);
+        pyr_tile_compute(g, L, f, pyr, S, xs_t, ys_t, tx0, ty0, tw, th, T.xa);
         return;
     }
     if (aligned) {
@@ -424,7 +436,7 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
         }
     }
     __syncthreads();
-    pyr_tile_compute(g, L, f, pyr, S, xs_t, ys_t, tx0, ty0, tw, th, xa, sy_lo);
+    pyr_tile_compute(g, L, f, pyr, S, xs_t, ys_t, tx0, ty0, tw, th, xa);
 }
 
 // Two cascaded levels in one launch: level l (from level l-1, both in the pyramid slab) and level
@@ -435,11 +447,12 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
 // write the same bytes there.  Removes the launch boundary between the two levels and the
 // level-l re-read.
 constexpr int PP_MAXP = 8;   // level-l row passes per thread
+constexpr int PP_MAXC = 96, PP_MAXR = 96;   // level-l rectangle columns / rows the tables hold
 
-__device__ __forceinline__ uint32_t pyr_px_generic(const uint8_t* S, int2 xv, int2 yv, int xa, int ya) {
-    const int r0 = ((yv.x & 0xffff) - ya) * PYR_SW, r1 = ((yv.x >> 16) - ya) * PYR_SW;
+__device__ __forceinline__ uint32_t pyr_px_generic(const uint8_t* S, int2 xv, int4 yv, int xa) {
+    const int r0 = yv.x, r1 = yv.y;
     const int sx0 = (xv.x & 0xffff) - xa, sx1 = (xv.x >> 16) - xa, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
-    const int b0 = yv.y & 0xffff, b1 = yv.y >> 16;
+    const int b0 = yv.z >> 12, b1 = yv.w >> 12;
     const int h0 = S[r0 + sx0] * a0 + S[r0 + sx1] * a1;
     const int h1 = S[r1 + sx0] * a0 + S[r1 + sx1] * a1;
     const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
@@ -452,7 +465,8 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
                                                            const int2* __restrict__ xtab,
                                                            const int2* __restrict__ ytab) {
     __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW + 16];
-    __shared__ int2 xs1[PYR_SW], ys1[PYR_SH], xs2[PYR_TW], ys2[PYR_TH];
+    __shared__ int2 xs1[PP_MAXC], xs2[PYR_TW];
+    __shared__ int4 ys1[PP_MAXR], ys2[PYR_TH];
     const LevelDev& L0 = g.lv[l - 1];
     const LevelDev& L1 = g.lv[l];
     const LevelDev& L2 = g.lv[l + 1];
@@ -485,9 +499,9 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
         uint4 v0, v1, v2, v3, v4;
         pyr_fetch(T, tid, v0, v1, v2, v3, v4);
         if (tid < ncol) xs1[tid] = xtab[L1.xtab_off + c0 + tid];
-        if (tid < nrow) ys1[tid] = ytab[L1.ytab_off + ay0 + tid];
+        if (tid < nrow) ys1[tid] = pyr_row_taps(ytab[L1.ytab_off + ay0 + tid], T.sy_lo);
         if (tid < tw) xs2[tid] = xtab[L2.xtab_off + tx0 + tid];
-        if (tid < th) ys2[tid] = ytab[L2.ytab_off + ty0 + tid];
+        if (tid < th) ys2[tid] = pyr_row_taps(ytab[L2.ytab_off + ty0 + tid], ay0);
         pyr_stage(T, tid, S, v0, 0);
         pyr_stage(T, tid, S, v1, 1);
         pyr_stage(T, tid, S, v2, 2);
@@ -521,7 +535,6 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
             a0[j] = *reinterpret_cast<const us2*>(&xv0.y);
             a1[j] = *reinterpret_cast<const us2*>(&xv1.y);
         }
-        const uint32_t* S32 = reinterpret_cast<const uint32_t*>(S);
         auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
             const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
             return *reinterpret_cast<const us2*>(&r);
@@ -531,14 +544,13 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
             const int r = r0 + pp * rpp;
             out[pp] = 0;
             if (r >= nrow) break;
-            const int2 yv = ys1[r];
+            const int4 yv = ys1[r];
             if (fits) {
-                const int rr0 = __mul24((yv.x & 0xffff) - T.sy_lo, PYR_SW / 4), rr1 = __mul24((yv.x >> 16) - T.sy_lo, PYR_SW / 4);
-                const uint32_t b0 = vcoef24(yv.y), b1 = vcoef24(yv.y >> 16);
+                const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;   // 24-bit: see above
 #pragma unroll
                 for (int j = 0; j < 2; j++) {
-                    const uint32_t* s0 = S32 + rr0 + wdv[j];
-                    const uint32_t* s1 = S32 + rr1 + wdv[j];
+                    const uint32_t* s0 = reinterpret_cast<const uint32_t*>(S + yv.x + 4 * (int)wdv[j]);
+                    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(S + yv.y + 4 * (int)wdv[j]);
                     const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
                     const uint32_t h0a = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel0[j]), a0[j], 0u, false));
                     const uint32_t h1a = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel0[j]), a0[j], 0u, false));
@@ -550,7 +562,7 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
                 }
             } else {   // taps outside the 8-byte windows (not at the supported scale factors)
 #pragma unroll
-                for (int k = 0; k < 4; k++) out[pp] |= pyr_px_generic(S, xv[k], yv, T.xa, T.sy_lo) << (8 * k);
+                for (int k = 0; k < 4; k++) out[pp] |= pyr_px_generic(S, xv[k], yv, T.xa) << (8 * k);
             }
         }
     }
@@ -575,7 +587,7 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
         }
     }
     __syncthreads();
-    pyr_tile_compute(g, L2, f, pyr, S, xs2, ys2, tx0, ty0, tw, th, c0, ay0);
+    pyr_tile_compute(g, L2, f, pyr, S, xs2, ys2, tx0, ty0, tw, th, c0);
 }
 
 // Host check of pyramid_pair_kernel's capacities at the level pair's scale factors (with margins
@@ -585,7 +597,8 @@ static bool pyr_pair_fits(const Geom& g, int l) {
     const int ncol = (int)std::ceil(PYR_TW * s2x) + 10, nrow = (int)std::ceil(PYR_TH * s2y) + 7;
     const int ncq = (ncol + 3) / 4, rpp = 256 / ncq;
     const int bw = (int)std::ceil(ncol * s1x) + 7 + 15, bh = (int)std::ceil(nrow * s1y) + 7;
-    return ncol + 8 <= PYR_SW && nrow <= PYR_SH && (nrow + rpp - 1) / rpp <= PP_MAXP && bw <= PYR_SW && bh <= PYR_SH &&
+    return ncol + 8 <= PYR_SW && nrow <= PYR_SH && ncol <= PP_MAXC && nrow <= PP_MAXR && (nrow + rpp - 1) / rpp <= PP_MAXP &&
+           bw <= PYR_SW && bh <= PYR_SH &&
            bh * ((bw + 15) / 16) <= PYR_PF * 256;
 }
 
