@@ -85,3 +85,20 @@ def test_pipeline_traffic_from_r03_profile():
     # the pair kernel's average dispatch counts three times, the level kernel once
     assert [k for k, n in bench.stage_kernels(8)["pyramid"]] == ["pyramid_pair_kernel", "pyramid_level_kernel"]
     assert [n for k, n in bench.stage_kernels(8)["pyramid"]] == [3, 1]
+
+
+def test_stage_kernels_by_level_count():
+    # levels 1+2, 3+4, ... as pair launches, an odd last level as one level launch
+    assert bench.stage_kernels(8)["pyramid"] == [("pyramid_pair_kernel", 3), ("pyramid_level_kernel", 1)]
+    assert bench.stage_kernels(7)["pyramid"] == [("pyramid_pair_kernel", 3), ("pyramid_level_kernel", 0)]
+    assert bench.stage_kernels(2)["pyramid"] == [("pyramid_pair_kernel", 0), ("pyramid_level_kernel", 1)]
+
+
+def test_summary_is_flat_and_survives_missing_legs():
+    r = {"value": 1.5, "ms_per_step": 2.0, "n_gpus": 1, "roofline": {"frac": 0.2, "avg_launch_ms": 3.0},
+         "localba": {"iters_per_s": 9000.123456, "cpu_baseline": {"value": 500.0}}, "c5": {"frames_per_s": 7.0}}
+    s = bench.summary(r)
+    assert s["c2_frames_per_s"] == 1.5 and s["fast_cells_frac"] == 0.2 and s["localba_iters_per_s"] == 9000.1235
+    assert s["localba_cpu_iters_per_s"] == 500.0 and s["c5_frames_per_s"] == 7.0
+    assert s["c3_pairs_per_s"] is None and s["c1_frames_per_s"] is None
+    assert all(not isinstance(v, dict) for v in s.values())
