@@ -2403,6 +2403,8 @@ struct orbx_extractor {
     std::vector<CellDev> cells;
     int NC = 0, PTC = 0;
     size_t qt_lds = 0;
+    int qt_ptc0 = 0;        // ORBX_QT_PTC0 (tuning knob): level 0 in its own launch with this LDS point capacity
+    size_t qt_lds0 = 0;
     FastLds fl;
     size_t fast_lds = 0;
     int fast_cpw = 16;  // FAST cells per wavefront (4 -> 16: -2 % pan, -17 % textured: fewer first cells without a speculation hint; ORBX_FAST_CPW)
@@ -2630,9 +2632,16 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         set_error("nfeatures too large for the quadtree LDS budget (per-level quota <= ~2100)");
         return ORB_EINVAL;
     }
-    if (lds > 48 * 1024)
+    int PTC0 = 0;
+    size_t lds0 = 0;
+    if (const char* e = getenv("ORBX_QT_PTC0")) {   // level 0 (the densest) in its own launch
+        PTC0 = std::max(256, std::min(8192, atoi(e))) & ~63;
+        lds0 = node_lds + (size_t)PTC0 * 8;
+        if (lds0 > 156 * 1024) { PTC0 = 0; lds0 = 0; }
+    }
+    if (std::max(lds, lds0) > 48 * 1024)
         ORB_HIP_TRY(hipFuncSetAttribute((const void*)quadtree_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds));
+                                        (int)std::max(lds, lds0)));
     int rc;
     if ((rc = h->d_cells.reserve(std::max<size_t>(1, cells.size()) * sizeof(CellDev)))) return rc;
     if ((rc = h->d_xtab.reserve(std::max<size_t>(1, xtab.size()) * sizeof(int2)))) return rc;
@@ -2704,6 +2713,8 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     h->NC = NC;
     h->PTC = PTC;
     h->qt_lds = lds;
+    h->qt_ptc0 = PTC0;
+    h->qt_lds0 = lds0;
     h->g_rows = rows;
     h->g_cols = cols;
     h->ws_frames = 0;   // force workspace re-layout
@@ -2789,6 +2800,12 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
+        if (h->qt_ptc0 > 0 && l0 == 0) {   // tuning knob: level 0 alone, with its own LDS point capacity
+            launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, 1u), dim3(256), (uint32_t)h->qt_lds0, s, g, cellcnt,
+                         slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->qt_ptc0, fault, 0);
+            l0 = 1;
+            if (--nl <= 0) return;
+        }
         launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(256), (uint32_t)h->qt_lds, s, g,
                            cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0);
     };
