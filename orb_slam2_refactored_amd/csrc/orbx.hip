@@ -206,45 +206,65 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
                                                  const uint8_t* S, const int2* xs_t, const int4* ys_t, int tx0,
                                                  int ty0, int tw, int th, int xa) {
     {
-        // 32 threads per 64-px output row (2 px each), 8 rows per pass.  Both pixels' four taps lie
-        // in the 8 LDS bytes from dword wd (scale <= ~3), so one row costs two dword reads; v_perm
-        // packs a pixel's taps as u16 (S0, S1) and v_dot2_u32_u16 with the packed (a0, a1) gives
-        // S0*a0 + S1*a1 exactly.  (h >> 4 <= 32640 and the result <= 255: OpenCV's saturations
-        // cannot trigger for coefficients summing to 2048.)
-        const int p0 = (threadIdx.x & 31) * 2;
-        const int2 xv0 = xs_t[min(p0, tw - 1)], xv1 = xs_t[min(p0 + 1, tw - 1)];
-        const int s00 = (xv0.x & 0xffff) - xa, s01 = (xv0.x >> 16) - xa;
-        const int s10 = (xv1.x & 0xffff) - xa, s11 = (xv1.x >> 16) - xa;
-        const int wd = s00 >> 2;
-        const int e00 = s00 - 4 * wd, e01 = s01 - 4 * wd, e10 = s10 - 4 * wd, e11 = s11 - 4 * wd;
-        const bool fits = max(e01, e11) <= 7 && min(e00, e10) >= 0;
-        if (!__syncthreads_or(!fits)) {   // block-uniform: every thread's taps fit its 8-byte window
-            if (p0 >= tw) return;   // after the block-wide vote: no barrier follows
-            const uint32_t sel0 = (uint32_t)e00 | 0x0c00u | ((uint32_t)e01 << 16) | 0x0c000000u;
-            const uint32_t sel1 = (uint32_t)e10 | 0x0c00u | ((uint32_t)e11 << 16) | 0x0c000000u;
-            const us2 a0 = *reinterpret_cast<const us2*>(&xv0.y), a1 = *reinterpret_cast<const us2*>(&xv1.y);
-            const uint8_t* Sw = S + 4 * wd;
-            uint8_t* dcol = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + p0;
-            for (int ty = threadIdx.x >> 5; ty < th; ty += 8) {
+        // 16 threads per 64-px output row (4 px each: two pairs), 16 rows per pass (round 4: the row's
+        // table read, address and loop control once per 4 pixels instead of 2).  Both pixels of a pair
+        // have their four taps in the 8 LDS bytes from the pair's dword wd (scale <= ~3), so a pair costs
+        // two dword reads per source row; v_perm packs a pixel's taps as u16 (S0, S1) and v_dot2_u32_u16
+        // with the packed (a0, a1) gives S0*a0 + S1*a1 exactly.  (h >> 4 <= 32640 and the result <= 255:
+        // OpenCV's saturations cannot trigger for coefficients summing to 2048.)
+        const int q0 = (threadIdx.x & 15) * 4;
+        uint32_t sel0[2], sel1[2];
+        int wdb[2];
+        us2 a0[2], a1[2];
+        bool fits = true;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int2 xv0 = xs_t[min(q0 + 2 * j, tw - 1)], xv1 = xs_t[min(q0 + 2 * j + 1, tw - 1)];
+            const int s00 = (xv0.x & 0xffff) - xa, s01 = (xv0.x >> 16) - xa;
+            const int s10 = (xv1.x & 0xffff) - xa, s11 = (xv1.x >> 16) - xa;
+            const int wd = s00 >> 2;
+            const int e00 = s00 - 4 * wd, e01 = s01 - 4 * wd, e10 = s10 - 4 * wd, e11 = s11 - 4 * wd;
+            fits = fits && max(e01, e11) <= 7 && min(e00, e10) >= 0;
+            sel0[j] = (uint32_t)e00 | 0x0c00u | ((uint32_t)e01 << 16) | 0x0c000000u;
+            sel1[j] = (uint32_t)e10 | 0x0c00u | ((uint32_t)e11 << 16) | 0x0c000000u;
+            wdb[j] = 4 * wd;
+            a0[j] = *reinterpret_cast<const us2*>(&xv0.y);
+            a1[j] = *reinterpret_cast<const us2*>(&xv1.y);
+        }
+        if (!__syncthreads_or(!fits)) {   // block-uniform: every thread's taps fit its 8-byte windows
+            if (q0 >= tw) return;   // after the block-wide vote: no barrier follows
+            const bool full = q0 + 3 < tw;
+            auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
+                const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
+                return *reinterpret_cast<const us2*>(&r);
+            };
+            uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + q0 +
+                           (long long)(ty0 + (int)(threadIdx.x >> 4)) * L.stride;
+            const long long dstep = 16ll * L.stride;
+            for (int ty = threadIdx.x >> 4; ty < th; ty += 16, dst += dstep) {
                 const int4 yv = ys_t[ty];
-                const uint32_t* s0 = reinterpret_cast<const uint32_t*>(Sw + yv.x);
-                const uint32_t* s1 = reinterpret_cast<const uint32_t*>(Sw + yv.y);
                 // (the masks only tell the compiler b << 12 fits 24 bits: v_mul_hi_u32_u24, not v_mul_hi_u32)
                 const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;
-                const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
-                auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
-                    const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
-                    return *reinterpret_cast<const us2*>(&r);
-                };
-                const uint32_t h0a = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel0), a0, 0u, false));
-                const uint32_t h1a = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel0), a0, 0u, false));
-                const uint32_t h0b = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel1), a1, 0u, false));
-                const uint32_t h1b = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel1), a1, 0u, false));
-                const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
-                const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
-                uint8_t* dst = dcol + __mul24(ty0 + ty, L.stride);
-                if (p0 + 1 < tw) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)(va | (vb << 8));   // tx0 + p0 even
-                else dst[0] = (uint8_t)va;
+                uint32_t out = 0;
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const uint32_t* s0 = reinterpret_cast<const uint32_t*>(S + yv.x + wdb[j]);
+                    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(S + yv.y + wdb[j]);
+                    const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
+                    const uint32_t h0a = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel0[j]), a0[j], 0u, false));
+                    const uint32_t h1a = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel0[j]), a0[j], 0u, false));
+                    const uint32_t h0b = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel1[j]), a1[j], 0u, false));
+                    const uint32_t h1b = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel1[j]), a1[j], 0u, false));
+                    const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
+                    const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
+                    out |= (va | (vb << 8)) << (16 * j);
+                }
+                if (full) {
+                    *reinterpret_cast<uint32_t*>(dst) = out;   // tx0 + q0 and the row stride: multiples of 4
+                } else {
+                    for (int k = 0; k < 3; k++)
+                        if (q0 + k < tw) dst[k] = (uint8_t)(out >> (8 * k));
+                }
             }
             return;
         }
