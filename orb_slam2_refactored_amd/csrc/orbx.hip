@@ -2151,6 +2151,28 @@ constexpr HBlurA make_hblur_a() {
     return t;
 }
 __constant__ HBlurA c_hblur_a = make_hblur_a();
+
+// IC_Angle (:74-101) as the same i8 products on the blur's B fragments: D_t = A_t B_nt chained over
+// the three row tiles, with A_t[m][k] = the disk weight of patch pixel (row m + 16 nt, column k) —
+// u = k - 21 for m_10, v = m + 16 nt - 21 for m_01, 0 outside the disk |v| <= 15, |u| <= umax[|v|].
+// The diagonal D[n][n] is then the weighted sum of patch row n (+16 nt), and its trace the moment.
+// The disk is symmetric in u and in v, so sum(weights) = 0 and the i8 offset (p - 128) cancels.
+struct AngleA { uint32_t v[3][2][64][4]; };   // [row tile][m_10, m_01][lane][dword]
+constexpr AngleA make_angle_a() {
+    AngleA t{};
+    for (int nt = 0; nt < 3; nt++)
+        for (int l = 0; l < 64; l++)
+            for (int d = 0; d < 4; d++)
+                for (int b = 0; b < 4; b++) {
+                    const int v = (l & 15) + 16 * nt - 21, u = 16 * (l >> 4) + 4 * d + b - 21;
+                    const int av = v < 0 ? -v : v, au = u < 0 ? -u : u;
+                    if (av > 15 || au > c_umax_h[av]) continue;
+                    t.v[nt][0][l][d] |= (uint32_t)(uint8_t)(int8_t)u << (8 * b);
+                    t.v[nt][1][l][d] |= (uint32_t)(uint8_t)(int8_t)v << (8 * b);
+                }
+    return t;
+}
+__constant__ AngleA c_angle_a = make_angle_a();
 typedef int i4v __attribute__((ext_vector_type(4)));
 
 #ifdef ORB_DESC_STAMPS
@@ -2274,53 +2296,23 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     __syncthreads();
     DESC_STAMP(1);
 
-    // IC_Angle on the unblurred level, patch centre (21, 21).  Lane = (row parity, u + 15): lanes
-    // 0-31 take rows +-v for odd v, lanes 32-63 for v + 1, so the 15 row pairs take 8 steps.
-    int m10 = 0, m01 = 0;
-    {
-        const int hv = lane >> 5, u = (lane & 31) - 15;   // u = 16 on lanes 31 / 63: outside every umax
-        const uint8_t* cp = R + 21 * RS + 21 + u + hv * RS;
-        // every read unconditional (all inside the 43x43 patch) and issued together; the disk mask
-        // is applied to the products
-        int vp[8], vm[8];
+    // The raw rows as i8 B fragments (p - 128), shared by the angle and the blur products: lane
+    // (n, g) holds columns 16 g .. +15 of patch row n + 16 nt.  Every read of R is issued before the
+    // first Hb write (R aliases Hb; one wavefront's LDS operations complete in order).
+    const int n = lane & 15, lg = lane >> 4;
+    i4v bfr[3];
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int vv = 2 * t + 1;
-            vp[t] = cp[vv * RS];
-            vm[t] = cp[-(vv + 2 * hv) * RS];
-        }
-        const int c0 = R[21 * RS + 21 + u];
-        m10 = (hv == 0 && u <= 15) ? u * c0 : 0;
-        // the disk mask as lane-constant multipliers (branch-free multiply-adds)
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int vv = 2 * t + 1;
-            const int v = vv + hv;
-            const int um = hv ? (vv + 1 <= 15 ? c_umax_h[vv + 1] : -1) : c_umax_h[vv];
-            const bool in = u >= -um && u <= um;
-            const int vin = in ? v : 0, uin = in ? u : 0;
-            m01 += vin * (vp[t] - vm[t]);
-            m10 += uin * (vp[t] + vm[t]);
-        }
+    for (int nt = 0; nt < 3; nt++) {
+        bfr[nt] = *reinterpret_cast<const i4v*>(&R[(n + 16 * nt) * RS + 16 * lg]);
+        bfr[nt] ^= (int)0x80808080u;
     }
-    m10 = wave_sum_i32(m10);
-    m01 = wave_sum_i32(m01);
-    const float angle = fast_atan2_dev((float)m01, (float)m10);
-    DESC_STAMP(2);
 
     // horizontal Q8 blur on the matrix cores (c_hblur_a): 3 x 3 tiles of 16 blurred columns x 16
-    // rows; lane (n, g) of tile (mt, nt) gets columns 16 mt + 4 g .. +3 of row 16 nt + n.  Every B
-    // read of R is issued before the first Hb write (R aliases Hb; one wavefront's LDS operations
-    // complete in order).  Rows past 42 (stored into slack rows) and columns past 36 are computed
-    // from neighbouring bytes and never read; columns past 39 are not stored.
+    // rows; lane (n, g) of tile (mt, nt) gets columns 16 mt + 4 g .. +3 of row 16 nt + n.  Rows past
+    // 42 (stored into slack rows) and columns past 36 are computed from neighbouring bytes and never
+    // read; columns past 39 are not stored.
     {
-        const int n = lane & 15, g = lane >> 4;
-        i4v bfr[3], afr[3];
-#pragma unroll
-        for (int nt = 0; nt < 3; nt++) {
-            bfr[nt] = *reinterpret_cast<const i4v*>(&R[(n + 16 * nt) * RS + 16 * g]);
-            bfr[nt] ^= (int)0x80808080u;   // u8 -> i8 (p - 128)
-        }
+        i4v afr[3];
 #pragma unroll
         for (int mt = 0; mt < 3; mt++) afr[mt] = *reinterpret_cast<const i4v*>(c_hblur_a.v[mt][lane]);
         const i4v cinit = {128 * 256, 128 * 256, 128 * 256, 128 * 256};
@@ -2333,18 +2325,46 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
             uint2 pk;
             pk.x = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].y, (uint32_t)acc[nt][mt].x, 0x05040100u);
             pk.y = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].w, (uint32_t)acc[nt][mt].z, 0x05040100u);
-            *reinterpret_cast<uint2*>(&Hb[(16 * nt + n) * HBS + 16 * mt + 4 * g]) = pk;   // rows 43..47: slack
+            *reinterpret_cast<uint2*>(&Hb[(16 * nt + n) * HBS + 16 * mt + 4 * lg]) = pk;   // rows 43..47: slack
         };
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
             put(nt, 0);
             put(nt, 1);
         }
-        if (g < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
+        if (lg < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
 #pragma unroll
             for (int nt = 0; nt < 3; nt++) put(nt, 2);
         }
     }
+
+    // IC_Angle on the unblurred patch, centre (21, 21), as six more products (c_angle_a) chained
+    // over the row tiles; the diagonal element D[n][n] sits in lane 20 (n / 4) + n % 4, register
+    // n % 4: each lane takes register lane % 4, and the quads at row offset 4 (lane / 16) are summed.
+    int m10, m01;
+    {
+        i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0};
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            const i4v au = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
+            const i4v av = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
+            du = __builtin_amdgcn_mfma_i32_16x16x64_i8(au, bfr[nt], du, 0, 0, 0);
+            dv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bfr[nt], dv, 0, 0, 0);
+        }
+        const bool q1 = lane & 1, q2 = lane & 2;
+        int tu = q2 ? (q1 ? du.w : du.z) : (q1 ? du.y : du.x);
+        int tv = q2 ? (q1 ? dv.w : dv.z) : (q1 ? dv.y : dv.x);
+        tu += dpp_i32<0xB1>(tu);   // quad_perm [1,0,3,2]
+        tv += dpp_i32<0xB1>(tv);
+        tu += dpp_i32<0x4E>(tu);   // quad_perm [2,3,0,1]
+        tv += dpp_i32<0x4E>(tv);
+        m10 = __builtin_amdgcn_readlane(tu, 0) + __builtin_amdgcn_readlane(tu, 20) +
+              __builtin_amdgcn_readlane(tu, 40) + __builtin_amdgcn_readlane(tu, 60);
+        m01 = __builtin_amdgcn_readlane(tv, 0) + __builtin_amdgcn_readlane(tv, 20) +
+              __builtin_amdgcn_readlane(tv, 40) + __builtin_amdgcn_readlane(tv, 60);
+    }
+    const float angle = fast_atan2_dev((float)m01, (float)m10);
+    DESC_STAMP(2);
     __syncthreads();
 
     const float factorPI = (float)(M_PI / 180.f);
