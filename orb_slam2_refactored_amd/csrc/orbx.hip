@@ -138,6 +138,10 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
            __builtin_amdgcn_readlane(v, 48);
 }
 
+// v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it): a wave-uniform value into
+// one lane of a register, with the compiler's own hazard handling
+extern "C" __device__ uint32_t writelane_u32(uint32_t v, uint32_t lane, uint32_t old) __asm("llvm.amdgcn.writelane.i32");
+
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Wave-inclusive scan of ints (64 lanes) on DPP: Hillis-Steele inside each row of 16 (row_shr 1, 2,
@@ -2233,6 +2237,10 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const int oidx = lbase + i;   // output order: level-major list order
     if (oidx >= cap) return;
     DESC_STAMP(0);
+    // the blur's constant A fragments, in flight under the patch load
+    i4v afr[3];
+#pragma unroll
+    for (int mt = 0; mt < 3; mt++) afr[mt] = *reinterpret_cast<const i4v*>(c_hblur_a.v[mt][lane]);
 
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
     int step;
@@ -2312,9 +2320,6 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     // 42 (stored into slack rows) and columns past 36 are computed from neighbouring bytes and never
     // read; columns past 39 are not stored.
     {
-        i4v afr[3];
-#pragma unroll
-        for (int mt = 0; mt < 3; mt++) afr[mt] = *reinterpret_cast<const i4v*>(c_hblur_a.v[mt][lane]);
         const i4v cinit = {128 * 256, 128 * 256, 128 * 256, 128 * 256};
         i4v acc[3][3];   // all nine products first: their results are not waited on one at a time
 #pragma unroll
@@ -2395,24 +2400,25 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         words[r] = __ballot(sample(2 * p) < sample(2 * p + 1));
     }
     DESC_STAMP(5);
+    // The 32 descriptor bytes and the 7-word keypoint record are wave-uniform: v_writelane places
+    // them in lanes 0..7 / 0..6 of one register each (no per-lane selects or branches), one store each.
     const long long o = (long long)f * cap + oidx;
-    if (lane < 4) {
-        const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-        reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = wv;
+    uint32_t dv = 0, kv = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        dv = writelane_u32((uint32_t)words[r], 2 * r, dv);
+        dv = writelane_u32((uint32_t)(words[r] >> 32), 2 * r + 1, dv);
     }
-    if (lane < 7) {
-        float fv;
-        switch (lane) {
-            case 0: fv = l > 0 ? (float)kx * L.scale : (float)kx; break;
-            case 1: fv = l > 0 ? (float)ky * L.scale : (float)ky; break;
-            case 2: fv = L.size; break;
-            case 3: fv = angle; break;
-            case 4: fv = (float)score; break;
-            case 5: fv = __int_as_float(l); break;
-            default: fv = __int_as_float(-1); break;
-        }
-        reinterpret_cast<float*>(kps + o)[lane] = fv;
-    }
+    const float ks = l > 0 ? L.scale : 1.f;   // (:812-815: pt *= scaleFactors_[s] above level 0; x * 1 = x)
+    kv = writelane_u32(__float_as_uint((float)kx * ks), 0, kv);
+    kv = writelane_u32(__float_as_uint((float)ky * ks), 1, kv);
+    kv = writelane_u32(__float_as_uint(L.size), 2, kv);
+    kv = writelane_u32(__float_as_uint(angle), 3, kv);
+    kv = writelane_u32(__float_as_uint((float)score), 4, kv);
+    kv = writelane_u32((uint32_t)l, 5, kv);
+    kv = writelane_u32(0xffffffffu, 6, kv);
+    if (lane < 8) reinterpret_cast<uint32_t*>(desc + o * 32)[lane] = dv;
+    if (lane < 7) reinterpret_cast<uint32_t*>(kps + o)[lane] = kv;
     DESC_STAMP(6);
 }
 
