@@ -73,6 +73,9 @@ struct Geom {
     int out_frame;            // selected keypoints per frame (sum of out_cap)
     unsigned of_m;            // n / out_frame = (t + ((n - t) >> of_s1)) >> of_s2, t = mulhi(n, of_m)
     int of_s1, of_s2;         // (round-up magic, exact for every n < 2^31; divmod_of)
+    // describe's slot -> level: level q's first slot as u16 field q (q = 0 and unused levels 0x7fff);
+    // the level of slot s is the number of fields <= s (SWAR, describe_level)
+    unsigned lv_start[MAX_LEVELS / 2];
     LevelDev lv[MAX_LEVELS];
 };
 
@@ -2218,9 +2221,14 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                               : reinterpret_cast<const int*>(sel + (long long)f * g.out_frame + s);
     const int cw = (lane < nl || lane == 63) ? *lp : 0;
     const int cq = lane < nl ? cw : 0;
-    int l = 0;   // levels >= nlevels carry out_base INT_MAX (host); out_base >= 1 above level 0
+    // levels >= nlevels carry 0x7fff (host; out_frame < 0x7fff checked there): a field x <= s iff bit
+    // 15 of (x | 0x8000) - (s + 1) is clear, and no field borrows from the next
+    int l = MAX_LEVELS;
+    {
+        const unsigned s1 = (unsigned)(s + 1) * 0x00010001u;
 #pragma unroll
-    for (int q = 1; q < MAX_LEVELS; q++) l += (int)((unsigned)(g.lv[q].out_base - 1 - s) >> 31);
+        for (int d = 0; d < MAX_LEVELS / 2; d++) l -= __popc(((g.lv_start[d] | 0x80008000u) - s1) & 0x80008000u);
+    }
     int sc = cq;
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xf, 0xf, true);   // row_shr:1 (zero fill)
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);   // row_shr:2
@@ -2646,6 +2654,13 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.slot_frame = std::max<long long>(slot, 1);
     g.cand_frame = std::max<long long>(cand, 1);
     g.out_frame = std::max(out, 1);
+    if (g.out_frame >= 0x7fff) {   // describe's u16 level starts (a frame of > 32k selected keypoints)
+        set_error("ORBextractor: more than 32766 selection slots per frame (nfeatures too large)");
+        return ORB_EINVAL;
+    }
+    for (int d = 0; d < MAX_LEVELS / 2; d++) g.lv_start[d] = 0x7fff7fffu;
+    for (int l = 1; l < Lc; l++)
+        g.lv_start[l >> 1] = (g.lv_start[l >> 1] & ~(0xffffu << (16 * (l & 1)))) | ((unsigned)g.lv[l].out_base << (16 * (l & 1)));
     {   // round-up magic for n / out_frame (Granlund-Montgomery; d = 1: t = 0, shifts 0)
         const unsigned d = (unsigned)g.out_frame;
         int lg = 0;
