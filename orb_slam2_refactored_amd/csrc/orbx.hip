@@ -2334,6 +2334,10 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         for (int nt = 0; nt < 3; nt++)
 #pragma unroll
             for (int mt = 0; mt < 3; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+        // A and B live past every product: with -amdgpu-mfma-vgpr-form the allocator may otherwise put
+        // a product's D over its dying A / B registers, which gfx950 computes wrongly now and then
+        // (round 3; tools/mfma_overlap.py, tests/test_mfma_overlap.py)
+        asm volatile("" ::"v"(afr[0]), "v"(afr[1]), "v"(afr[2]));
         auto put = [&](int nt, int mt) {
             uint2 pk;
             pk.x = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].y, (uint32_t)acc[nt][mt].x, 0x05040100u);
@@ -2356,14 +2360,19 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     // n % 4: each lane takes register lane % 4, and the quads at row offset 4 (lane / 16) are summed.
     int m10, m01;
     {
-        i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0};
+        i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0}, au[3], av[3];
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-            const i4v au = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
-            const i4v av = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
-            du = __builtin_amdgcn_mfma_i32_16x16x64_i8(au, bfr[nt], du, 0, 0, 0);
-            dv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bfr[nt], dv, 0, 0, 0);
+            au[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
+            av[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
         }
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            du = __builtin_amdgcn_mfma_i32_16x16x64_i8(au[nt], bfr[nt], du, 0, 0, 0);
+            dv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[nt], bfr[nt], dv, 0, 0, 0);
+        }
+        asm volatile("" ::"v"(au[0]), "v"(au[1]), "v"(au[2]), "v"(av[0]), "v"(av[1]), "v"(av[2]), "v"(bfr[0]),
+                     "v"(bfr[1]), "v"(bfr[2]));   // (as above: no D over a dying A / B)
         const bool q1 = lane & 1, q2 = lane & 2;
         int tu = q2 ? (q1 ? du.w : du.z) : (q1 ? du.y : du.x);
         int tv = q2 ? (q1 ? dv.w : dv.z) : (q1 ? dv.y : dv.x);

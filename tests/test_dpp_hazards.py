@@ -15,10 +15,15 @@ CSRC = ROOT / "orb_slam2_refactored_amd" / "csrc"
 
 # the shipped build, plus the variants the A/B scripts build: SB_SPLIT_DEF (Schur-block parts) and a
 # diagonal-pivot include generated with no Newton step after v_rcp_f64 (tools/gen_ba_diag.py 0)
-VARIANTS = [("orbba.hip", []), ("orbba.hip", ["-DSB_SPLIT_DEF=8"]), ("orbba.hip", ["newton0"]), ("orbx.hip", [])]
+VARIANTS = [("orbba.hip", []), ("orbba.hip", ["-DSB_SPLIT_DEF=8"]), ("orbba.hip", ["newton0"]), ("orbx.hip", []),
+            ("orbm.hip", [])]
+# built with -amdgpu-mfma-vgpr-form (the Makefile's flags for these two): the same listing is also
+# scanned for MFMAs whose D overlaps srcA / srcB (tools/mfma_overlap.py), which the allocator produces
+# when an operand dies at the product and gfx950 then computes wrongly now and then
+VGPR_FORM = ("orbx.hip", "orbm.hip")
 
 
-@pytest.mark.parametrize("src,flags", VARIANTS, ids=["orbba", "orbba-sb8", "orbba-newton0", "orbx"])
+@pytest.mark.parametrize("src,flags", VARIANTS, ids=["orbba", "orbba-sb8", "orbba-newton0", "orbx", "orbm"])
 def test_no_dpp_hazards(tmp_path, src, flags):
     listing = tmp_path / (src + ".s")
     extra = list(flags)
@@ -29,7 +34,7 @@ def test_no_dpp_hazards(tmp_path, src, flags):
         extra = [f'-DORBBA_DIAG_INC="{inc}"']
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
            f"-I{ROOT / 'include'}", f"-I{CSRC}", "--cuda-device-only", "-S", str(CSRC / src), "-o", str(listing)] + extra
-    if src == "orbx.hip":
+    if src in VGPR_FORM:
         cmd += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
     if not Path(cmd[0]).exists():
         pytest.skip("hipcc not available")
@@ -37,6 +42,19 @@ def test_no_dpp_hazards(tmp_path, src, flags):
     out = subprocess.run([sys.executable, str(ROOT / "tools" / "dpp_hazard_check.py"), str(listing)],
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
+    if src in VGPR_FORM:
+        out = subprocess.run([sys.executable, str(ROOT / "tools" / "mfma_overlap.py"), str(listing)],
+                             capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_mfma_overlap_checker(tmp_path):
+    s = tmp_path / "t.s"
+    s.write_text("k:\n\tv_mfma_i32_16x16x64_i8 v[2:5], v[2:5], v[18:21], 0\n"
+                 "\tv_mfma_i32_16x16x64_i8 v[6:9], v[10:13], v[14:17], v[6:9]\n")
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "mfma_overlap.py"), str(s)], capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode == 1 and "overlaps: 1" in out.stdout, out.stdout
 
 
 def test_checker_follows_branch_edges(tmp_path):

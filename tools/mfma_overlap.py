@@ -19,7 +19,7 @@ for path in sys.argv[1:]:
     fn = "?"
     for ln in open(path):
         t = ln.strip()
-        if t.endswith(":") and not t.startswith("."):
+        if t.endswith(":") and not t.startswith((".", ";")):
             fn = t[:-1]
         if not t.startswith("v_mfma"):
             continue
@@ -31,3 +31,4 @@ for path in sys.argv[1:]:
                 bad += 1
                 print(f"{path}: {fn}: {t}")
 print("overlaps:", bad)
+sys.exit(1 if bad else 0)
