@@ -2329,31 +2329,41 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     // read; columns past 39 are not stored.
     {
         const i4v cinit = {128 * 256, 128 * 256, 128 * 256, 128 * 256};
-        i4v acc[3][3];   // all nine products first: their results are not waited on one at a time
-#pragma unroll
-        for (int nt = 0; nt < 3; nt++)
-#pragma unroll
-            for (int mt = 0; mt < 3; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
-        // A and B live past every product (the use takes the products too, so it cannot be scheduled
-        // above them): with -amdgpu-mfma-vgpr-form the allocator may otherwise put a product's D over
-        // the A / B registers of itself or of an earlier product still in flight, which gfx950 computes
-        // wrongly now and then (rounds 3 and 4; tools/mfma_overlap.py in tests/test_dpp_hazards.py)
-        asm volatile("" ::"v"(afr[0]), "v"(afr[1]), "v"(afr[2]), "v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[0][2]),
-                     "v"(acc[1][0]), "v"(acc[1][1]), "v"(acc[1][2]), "v"(acc[2][0]), "v"(acc[2][1]), "v"(acc[2][2]));
-        auto put = [&](int nt, int mt) {
+        // Two groups of products (blurred columns 0..31, then 32..47), each issued before its results
+        // are waited on.  A, B and C stay live past every product of a group (the use takes the
+        // products too, so it cannot be scheduled above them): with -amdgpu-mfma-vgpr-form the allocator
+        // may otherwise put a product's D over the A / B / C registers of itself or of an earlier product
+        // still in flight, which gfx950 computes wrongly now and then (rounds 3 and 4;
+        // tools/mfma_overlap.py in tests/test_dpp_hazards.py).  Two groups keep that within 64 VGPRs.
+        auto put = [&](const i4v& a, int nt, int mt) {
             uint2 pk;
-            pk.x = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].y, (uint32_t)acc[nt][mt].x, 0x05040100u);
-            pk.y = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].w, (uint32_t)acc[nt][mt].z, 0x05040100u);
+            pk.x = __builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, 0x05040100u);
+            pk.y = __builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, 0x05040100u);
             *reinterpret_cast<uint2*>(&Hb[(16 * nt + n) * HBS + 16 * mt + 4 * lg]) = pk;   // rows 43..47: slack
         };
+        {
+            i4v acc[3][2];
 #pragma unroll
-        for (int nt = 0; nt < 3; nt++) {
-            put(nt, 0);
-            put(nt, 1);
+            for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+                for (int mt = 0; mt < 2; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+            asm volatile("" ::"v"(afr[0]), "v"(afr[1]), "v"(cinit), "v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]),
+                         "v"(acc[1][1]), "v"(acc[2][0]), "v"(acc[2][1]));
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) {
+                put(acc[nt][0], nt, 0);
+                put(acc[nt][1], nt, 1);
+            }
         }
-        if (lg < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
+        {
+            i4v acc[3];
 #pragma unroll
-            for (int nt = 0; nt < 3; nt++) put(nt, 2);
+            for (int nt = 0; nt < 3; nt++) acc[nt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[2], bfr[nt], cinit, 0, 0, 0);
+            asm volatile("" ::"v"(afr[2]), "v"(cinit), "v"(acc[0]), "v"(acc[1]), "v"(acc[2]));
+            if (lg < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) put(acc[nt], nt, 2);
+            }
         }
     }
 

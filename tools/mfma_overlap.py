@@ -1,12 +1,13 @@
-"""Scan device asm for MFMAs whose destination overlaps the srcA / srcB registers of the same MFMA or
-of an MFMA issued shortly before it in the same listing (still in flight: its passes read A / B while
-the later product writes D).  With -amdgpu-mfma-vgpr-form this compiler can assign D over a dying
+"""Scan device asm for MFMAs whose destination overlaps the srcA / srcB registers of the same MFMA, or
+the srcA / srcB / srcC registers of an MFMA issued shortly before it in the same listing (still in
+flight: its passes read them while the later product writes D).  With -amdgpu-mfma-vgpr-form this compiler can assign D over a dying
 A / B operand; on gfx950 v_mfma_i32_16x16x64_i8 then returns wrong values now and then
 (describe_kernel, rounds 3 and 4).  Usage: mfma_overlap.py listing.s ... (exit 1 if any)."""
 import re
 import sys
 
-WINDOW = 24   # instructions after an MFMA during which its A / B registers count as in flight
+WINDOW = 16   # instructions after an MFMA during which its sources count as in flight (>= 4 cycles each: a
+# 16-pass product, the longest here, is done 64 cycles after issue)
 
 
 def rng(tok):
@@ -26,13 +27,14 @@ def overlap(a, b):
 bad = 0
 for path in sys.argv[1:]:
     fn = "?"
-    recent = []   # (instruction index, [A, B]) of recent MFMAs
+    recent = []   # (instruction index, [A, B, C], D, C written by an MFMA) of recent MFMAs
+    wrote = []    # every MFMA D of the current function
     idx = 0
     for ln in open(path):
         t = ln.strip()
         m = re.match(r"([A-Za-z_][\w.$]*):", t)
         if m:
-            fn, recent = m.group(1), []
+            fn, recent, wrote = m.group(1), [], []
             continue
         if not t or t.startswith((";", ".")):
             continue
@@ -42,11 +44,26 @@ for path in sys.argv[1:]:
         ops = [o.strip() for o in t.split(None, 1)[1].split(",")]
         d = rng(ops[0])
         srcs = [rng(o) for o in ops[1:3]]
-        recent = [(i, s) for i, s in recent if idx - i <= WINDOW]
-        hit = any(overlap(d, s) for s in srcs) or any(overlap(d, s) for _, ss in recent for s in ss)
+        c = rng(ops[3]) if len(ops) > 3 else None
+        recent = [r for r in recent if idx - r[0] <= WINDOW]
+        # D over its own A / B, or over the A / B / C of an earlier product still in flight (D == its
+        # own C is the accumulate form and allowed)
+        # (a product whose C is an earlier product's D waits for it: the chain is serialised, so the
+        # earlier one and everything before it are no longer in flight)
+        for k in range(len(recent) - 1, -1, -1):
+            if overlap(c, recent[k][2]):
+                recent = recent[k + 1:]
+                break
+        # (an in-flight C that an earlier product wrote is an accumulator chain the hardware orders:
+        # the round-3 matchers run that pattern; a C from a VALU register, e.g. a shared initial value,
+        # is flagged)
+        hit = any(overlap(d, s) for s in srcs) or any(
+            overlap(d, s) for _, ss, _, cw in recent for j, s in enumerate(ss) if not (j == 2 and cw))
         if hit:
             bad += 1
             print(f"{path}: {fn[:90]}: {t}")
-        recent.append((idx, srcs))
+        c_from_mfma = any(overlap(c, r[2]) for r in recent) or any(overlap(c, dd) for dd in wrote)
+        recent.append((idx, srcs + [c], d, c_from_mfma))
+        wrote.append(d)
 print("overlaps:", bad)
 sys.exit(1 if bad else 0)
