@@ -141,6 +141,17 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
            __builtin_amdgcn_readlane(v, 48);
 }
 
+// 20 wait states between a group of i8 products and the first VALU read of their results, with
+// nothing scheduled across: the compiler's own spacing for v_mfma_i32_16x16x64_i8 -> VALU on gfx950
+// was measured short (descriptor bits differed between identical runs whenever a product's result
+// was read within a few instructions of it, DESIGN.md §4 describe round 4); 20 covers the 16-pass
+// requirement of any product here.
+__device__ __forceinline__ void mfma_read_fence() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it): a wave-uniform value into
 // one lane of a register, with the compiler's own hazard handling
 extern "C" __device__ uint32_t writelane_u32(uint32_t v, uint32_t lane, uint32_t old) __asm("llvm.amdgcn.writelane.i32");
@@ -2349,6 +2360,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                 for (int mt = 0; mt < 2; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
             asm volatile("" ::"v"(afr[0]), "v"(afr[1]), "v"(cinit), "v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]),
                          "v"(acc[1][1]), "v"(acc[2][0]), "v"(acc[2][1]));
+            mfma_read_fence();
 #pragma unroll
             for (int nt = 0; nt < 3; nt++) {
                 put(acc[nt][0], nt, 0);
@@ -2360,6 +2372,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 #pragma unroll
             for (int nt = 0; nt < 3; nt++) acc[nt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[2], bfr[nt], cinit, 0, 0, 0);
             asm volatile("" ::"v"(afr[2]), "v"(cinit), "v"(acc[0]), "v"(acc[1]), "v"(acc[2]));
+            mfma_read_fence();
             if (lg < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
 #pragma unroll
                 for (int nt = 0; nt < 3; nt++) put(acc[nt], nt, 2);
@@ -2385,6 +2398,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         }
         asm volatile("" ::"v"(au[0]), "v"(au[1]), "v"(au[2]), "v"(av[0]), "v"(av[1]), "v"(av[2]), "v"(bfr[0]),
                      "v"(bfr[1]), "v"(bfr[2]), "v"(du), "v"(dv));   // (as above: no D over a live-in-flight A / B)
+        mfma_read_fence();
         const bool q1 = lane & 1, q2 = lane & 2;
         int tu = q2 ? (q1 ? du.w : du.z) : (q1 ? du.y : du.x);
         int tv = q2 ? (q1 ? dv.w : dv.z) : (q1 ? dv.y : dv.x);
