@@ -17,7 +17,8 @@ struct HostStructure {
     std::vector<int> blk_index, fs_beg, fs_slot, fs_hp, sl, sp, cur;   // scratch (capacity kept across calls)
     std::vector<uint8_t> pa, la;
     std::vector<unsigned long long> col;   // per-pose bitsets over the points (pair blocks)
-    std::vector<int> slot_of;              // [point][pose] -> free slot (pair blocks)
+    std::vector<int> slot_of;              // [pose][point] -> free slot (pair blocks; a block's fill reads
+                                           // two rows in point order)
     int np = 0, nl = 0;
 };
 
@@ -126,7 +127,7 @@ inline void build_structure(int P, int N, const std::vector<uint8_t>& level, con
                 const unsigned long long bit = 1ull << (l & 63);
                 dup |= (w & bit) != 0;
                 w |= bit;
-                so[(size_t)l * np + fh[a]] = fsl[a];
+                so[(size_t)fh[a] * nl + l] = fsl[a];
             }
         if (!dup) {
             s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0);
@@ -149,10 +150,12 @@ inline void build_structure(int P, int N, const std::vector<uint8_t>& level, con
                 const int i1 = s.blk_i1[k], i2 = s.blk_i2[k];
                 const unsigned long long* c1 = col + (size_t)i1 * W;
                 const unsigned long long* c2 = col + (size_t)i2 * W;
+                const int* s1 = so + (size_t)i1 * nl;
+                const int* s2 = so + (size_t)i2 * nl;
                 for (int w = 0; w < W; w++)
                     for (unsigned long long m = c1[w] & c2[w]; m; m &= m - 1) {
                         const int l = (w << 6) + __builtin_ctzll(m);
-                        *out++ = int2h{so[(size_t)l * np + i1], so[(size_t)l * np + i2]};
+                        *out++ = int2h{s1[l], s2[l]};
                     }
             }
             return;
