@@ -17,6 +17,13 @@ for spec in (0, 0, 0, 1, 8):
     o = ex.extract_batch_device(t)
     torch.cuda.synchronize()
     outs.append([x.cpu().numpy() for x in o])
+    if not np.array_equal(t.cpu().numpy(), frames):
+        print(f"input frames modified after run {len(outs) - 1}")
+# pairwise: identical later runs with only run 0 different would point at a one-time effect
+for a in range(1, len(outs)):
+    for b in range(a + 1, len(outs)):
+        nd = sum(int((~np.all(outs[a][1][i, :n] == outs[b][1][i, :n], axis=1)).sum()) for i, n in enumerate(outs[0][2]))
+        print(f"runs {a} vs {b}: {nd} descriptor rows differ")
 cnt = outs[0][2]
 bad = 0
 for r, o in enumerate(outs[1:], 1):
