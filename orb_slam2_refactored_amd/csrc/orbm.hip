@@ -176,7 +176,6 @@ __global__ __launch_bounds__(256) void hamming_top2_mfma_kernel(
                         lb[rt][r] = nb;
                     }
                 }
-                asm volatile("" :: "v"(bf[0]), "v"(bf[1]), "v"(bf[2]), "v"(bf[3]), "v"(cinit), "v"(lb[MM_RT - 1][3]));   // B and C live past the products (the last use depends on them: no D over an in-flight product's sources, tools/mfma_overlap.py)
             }
             __syncthreads();   // pair expanded into `cur ^ 1`; buffer `cur` free for the pair after
         }
@@ -360,7 +359,6 @@ __global__ __launch_bounds__(256) void hamming_top2_fp4_kernel(
                         lb[rt][r] = nb;
                     }
                 }
-                asm volatile("" :: "v"(b0), "v"(b1), "v"(cinit), "v"(lb[FP_RT - 1][3]));   // B and C live past the products (the last use depends on them: no D over an in-flight product's sources, tools/mfma_overlap.py)
             }
             __syncthreads();   // pair expanded into `cur ^ 1`; buffer `cur` free for the pair after
         }
@@ -848,7 +846,6 @@ __global__ __launch_bounds__(256) void tri_mm_kernel(TriArgs a, TriTables t, int
                     }
                 }
             }
-            asm volatile("" :: "v"(b0), "v"(b1), "v"(cinit), "v"(nev));   // B and C live past the products (the last use depends on them: no D over an in-flight product's sources, tools/mfma_overlap.py)
         }
         __syncthreads();   // pair expanded into `cur ^ 1`; buffer `cur` free for the pair after
     }

@@ -141,17 +141,6 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
            __builtin_amdgcn_readlane(v, 48);
 }
 
-// 20 wait states between a group of i8 products and the first VALU read of their results, with
-// nothing scheduled across: the compiler's own spacing for v_mfma_i32_16x16x64_i8 -> VALU on gfx950
-// was measured short (descriptor bits differed between identical runs whenever a product's result
-// was read within a few instructions of it, DESIGN.md §4 describe round 4); 20 covers the 16-pass
-// requirement of any product here.
-__device__ __forceinline__ void mfma_read_fence() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-}
-
 // v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it): a wave-uniform value into
 // one lane of a register, with the compiler's own hazard handling
 extern "C" __device__ uint32_t writelane_u32(uint32_t v, uint32_t lane, uint32_t old) __asm("llvm.amdgcn.writelane.i32");
@@ -2206,9 +2195,6 @@ __device__ unsigned long long g_desc_stamps[1024 * 8];
 
 // One workgroup = one wavefront = one selection slot (a kept keypoint or an empty slot).
 constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per raw-patch row
-#ifndef DESC_ANGLE_MFMA
-#define DESC_ANGLE_MFMA 1   // IC_Angle as i8 products on the blur's B fragments (0: LDS disk reads)
-#endif
 
 // One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
 __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
@@ -2326,39 +2312,6 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     __syncthreads();
     DESC_STAMP(1);
 
-#if !DESC_ANGLE_MFMA   // the round-3 IC_Angle (LDS disk reads), for A/B builds
-    // IC_Angle on the unblurred level, patch centre (21, 21).  Lane = (row parity, u + 15): lanes
-    // 0-31 take rows +-v for odd v, lanes 32-63 for v + 1, so the 15 row pairs take 8 steps.
-    int m10 = 0, m01 = 0;
-    {
-        const int hv = lane >> 5, u = (lane & 31) - 15;   // u = 16 on lanes 31 / 63: outside every umax
-        const uint8_t* cp = R + 21 * RS + 21 + u + hv * RS;
-        // every read unconditional (all inside the 43x43 patch) and issued together; the disk mask
-        // is applied to the products
-        int vp[8], vm[8];
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int vv = 2 * t + 1;
-            vp[t] = cp[vv * RS];
-            vm[t] = cp[-(vv + 2 * hv) * RS];
-        }
-        const int c0 = R[21 * RS + 21 + u];
-        m10 = (hv == 0 && u <= 15) ? u * c0 : 0;
-        // the disk mask as lane-constant multipliers (branch-free multiply-adds)
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int vv = 2 * t + 1;
-            const int v = vv + hv;
-            const int um = hv ? (vv + 1 <= 15 ? c_umax_h[vv + 1] : -1) : c_umax_h[vv];
-            const bool in = u >= -um && u <= um;
-            const int vin = in ? v : 0, uin = in ? u : 0;
-            m01 += vin * (vp[t] - vm[t]);
-            m10 += uin * (vp[t] + vm[t]);
-        }
-    }
-    m10 = wave_sum_i32(m10);
-    m01 = wave_sum_i32(m01);
-#endif
     // The raw rows as i8 B fragments (p - 128), shared by the angle and the blur products: lane
     // (n, g) holds columns 16 g .. +15 of patch row n + 16 nt.  Every read of R is issued before the
     // first Hb write (R aliases Hb; one wavefront's LDS operations complete in order).
@@ -2376,67 +2329,41 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     // read; columns past 39 are not stored.
     {
         const i4v cinit = {128 * 256, 128 * 256, 128 * 256, 128 * 256};
-        // Two groups of products (blurred columns 0..31, then 32..47), each issued before its results
-        // are waited on.  A, B and C stay live past every product of a group (the use takes the
-        // products too, so it cannot be scheduled above them): with -amdgpu-mfma-vgpr-form the allocator
-        // may otherwise put a product's D over the A / B / C registers of itself or of an earlier product
-        // still in flight, which gfx950 computes wrongly now and then (rounds 3 and 4;
-        // tools/mfma_overlap.py in tests/test_dpp_hazards.py).  Two groups keep that within 64 VGPRs.
-        auto put = [&](const i4v& a, int nt, int mt) {
+        i4v acc[3][3];   // all nine products first: their results are not waited on one at a time
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+            for (int mt = 0; mt < 3; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+        auto put = [&](int nt, int mt) {
             uint2 pk;
-            pk.x = __builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, 0x05040100u);
-            pk.y = __builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, 0x05040100u);
+            pk.x = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].y, (uint32_t)acc[nt][mt].x, 0x05040100u);
+            pk.y = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].w, (uint32_t)acc[nt][mt].z, 0x05040100u);
             *reinterpret_cast<uint2*>(&Hb[(16 * nt + n) * HBS + 16 * mt + 4 * lg]) = pk;   // rows 43..47: slack
         };
-        {
-            i4v acc[3][2];
 #pragma unroll
-            for (int nt = 0; nt < 3; nt++)
-#pragma unroll
-                for (int mt = 0; mt < 2; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
-            asm volatile("" ::"v"(afr[0]), "v"(afr[1]), "v"(cinit), "v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]),
-                         "v"(acc[1][1]), "v"(acc[2][0]), "v"(acc[2][1]));
-            mfma_read_fence();
-#pragma unroll
-            for (int nt = 0; nt < 3; nt++) {
-                put(acc[nt][0], nt, 0);
-                put(acc[nt][1], nt, 1);
-            }
+        for (int nt = 0; nt < 3; nt++) {
+            put(nt, 0);
+            put(nt, 1);
         }
-        {
-            i4v acc[3];
+        if (lg < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
 #pragma unroll
-            for (int nt = 0; nt < 3; nt++) acc[nt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[2], bfr[nt], cinit, 0, 0, 0);
-            asm volatile("" ::"v"(afr[2]), "v"(cinit), "v"(bfr[0]), "v"(bfr[1]), "v"(bfr[2]), "v"(acc[0]), "v"(acc[1]),
-                         "v"(acc[2]));
-            mfma_read_fence();
-            if (lg < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
-#pragma unroll
-                for (int nt = 0; nt < 3; nt++) put(acc[nt], nt, 2);
-            }
+            for (int nt = 0; nt < 3; nt++) put(nt, 2);
         }
     }
 
     // IC_Angle on the unblurred patch, centre (21, 21), as six more products (c_angle_a) chained
     // over the row tiles; the diagonal element D[n][n] sits in lane 20 (n / 4) + n % 4, register
     // n % 4: each lane takes register lane % 4, and the quads at row offset 4 (lane / 16) are summed.
-#if DESC_ANGLE_MFMA
     int m10, m01;
     {
-        i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0}, au[3], av[3];
+        i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0};
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-            au[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
-            av[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
+            const i4v au = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
+            const i4v av = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
+            du = __builtin_amdgcn_mfma_i32_16x16x64_i8(au, bfr[nt], du, 0, 0, 0);
+            dv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bfr[nt], dv, 0, 0, 0);
         }
-#pragma unroll
-        for (int nt = 0; nt < 3; nt++) {
-            du = __builtin_amdgcn_mfma_i32_16x16x64_i8(au[nt], bfr[nt], du, 0, 0, 0);
-            dv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[nt], bfr[nt], dv, 0, 0, 0);
-        }
-        asm volatile("" ::"v"(au[0]), "v"(au[1]), "v"(au[2]), "v"(av[0]), "v"(av[1]), "v"(av[2]), "v"(bfr[0]),
-                     "v"(bfr[1]), "v"(bfr[2]), "v"(du), "v"(dv));   // (as above: no D over a live-in-flight A / B)
-        mfma_read_fence();
         const bool q1 = lane & 1, q2 = lane & 2;
         int tu = q2 ? (q1 ? du.w : du.z) : (q1 ? du.y : du.x);
         int tv = q2 ? (q1 ? dv.w : dv.z) : (q1 ? dv.y : dv.x);
@@ -2449,7 +2376,6 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         m01 = __builtin_amdgcn_readlane(tv, 0) + __builtin_amdgcn_readlane(tv, 20) +
               __builtin_amdgcn_readlane(tv, 40) + __builtin_amdgcn_readlane(tv, 60);
     }
-#endif
     const float angle = fast_atan2_dev((float)m01, (float)m10);
     DESC_STAMP(2);
     __syncthreads();

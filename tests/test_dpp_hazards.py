@@ -16,14 +16,11 @@ CSRC = ROOT / "orb_slam2_refactored_amd" / "csrc"
 # the shipped build, plus the variants the A/B scripts build: SB_SPLIT_DEF (Schur-block parts) and a
 # diagonal-pivot include generated with no Newton step after v_rcp_f64 (tools/gen_ba_diag.py 0)
 VARIANTS = [("orbba.hip", []), ("orbba.hip", ["-DSB_SPLIT_DEF=8"]), ("orbba.hip", ["newton0"]), ("orbx.hip", []),
-            ("orbx.hip", ["-DDESC_ANGLE_MFMA=0"]), ("orbm.hip", [])]
-# built with -amdgpu-mfma-vgpr-form (the Makefile's flags for these two): the same listing is also
-# scanned for MFMAs whose D overlaps srcA / srcB (tools/mfma_overlap.py), which the allocator produces
-# when an operand dies at the product and gfx950 then computes wrongly now and then
-VGPR_FORM = ("orbx.hip", "orbm.hip")
+            ("orbm.hip", [])]
+VGPR_FORM = ("orbx.hip", "orbm.hip")   # built with -amdgpu-mfma-vgpr-form, as the Makefile does
 
 
-@pytest.mark.parametrize("src,flags", VARIANTS, ids=["orbba", "orbba-sb8", "orbba-newton0", "orbx", "orbx-angle-lds", "orbm"])
+@pytest.mark.parametrize("src,flags", VARIANTS, ids=["orbba", "orbba-sb8", "orbba-newton0", "orbx", "orbm"])
 def test_no_dpp_hazards(tmp_path, src, flags):
     listing = tmp_path / (src + ".s")
     extra = list(flags)
@@ -42,10 +39,6 @@ def test_no_dpp_hazards(tmp_path, src, flags):
     out = subprocess.run([sys.executable, str(ROOT / "tools" / "dpp_hazard_check.py"), str(listing)],
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
-    if src in VGPR_FORM:
-        out = subprocess.run([sys.executable, str(ROOT / "tools" / "mfma_overlap.py"), str(listing)],
-                             capture_output=True, text=True, timeout=120)
-        assert out.returncode == 0, out.stdout + out.stderr
 
 
 def test_mfma_overlap_checker(tmp_path):
