@@ -61,9 +61,11 @@ def test_pack_descriptors_clamps_counts_and_output():
     incl = torch.cumsum(counts, 0, dtype=torch.int32)      # the caller's layout: rows 0-1, 2-10, 11-13
     out_rows = 12
     buf = torch.full((out_rows + 1, 32), 0xA5, dtype=torch.uint8, device="cuda")
-    _lib.check(_lib.lib().orbx_pack_descriptors(_lib.tptr(desc.cuda()), cap, _lib.tptr(counts.cuda()),
-                                                _lib.tptr(incl.cuda()), frames, _lib.tptr(buf), out_rows,
-                                                _lib.stream_ptr()), "orbx_pack_descriptors")
+    # device copies held by name: a temporary's memory could be reused before the kernel reads it
+    d_desc, d_counts, d_incl = desc.cuda(), counts.cuda(), incl.cuda()
+    _lib.check(_lib.lib().orbx_pack_descriptors(_lib.tptr(d_desc), cap, _lib.tptr(d_counts), _lib.tptr(d_incl),
+                                                frames, _lib.tptr(buf), out_rows, _lib.stream_ptr()),
+               "orbx_pack_descriptors")
     torch.cuda.synchronize()
     got = buf.cpu()
     assert torch.equal(got[0:2], desc[0, :2])
