@@ -39,7 +39,7 @@ constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
 constexpr int HBS = 40;                 // LDS row stride of the blurred rows (u16): 20 dwords, 8-byte aligned rows
 static_assert(HBLUR_W + 3 <= HBS, "the blur's fourth-column tiles store up to column 39");
 
-__constant__ float c_pattern[1024] = {   // bit_pattern_31_ (:142-400) as floats (the samples' operands)
+__constant__ __attribute__((aligned(16))) float c_pattern[1024] = {   // bit_pattern_31_ (:142-400) as floats (the samples' operands)
 #include "orb_pattern31.inc"
 };
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
@@ -2195,6 +2195,9 @@ __device__ unsigned long long g_desc_stamps[1024 * 8];
 
 // One workgroup = one wavefront = one selection slot (a kept keypoint or an empty slot).
 constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per raw-patch row
+#ifndef DESC_PAT_EARLY
+#define DESC_PAT_EARLY 0   // A/B: the rBRIEF pattern loads issued before the angle chain
+#endif
 
 // One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
 __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
@@ -2351,6 +2354,12 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         }
     }
 
+#if DESC_PAT_EARLY
+    // the lane's four pattern pairs, loaded before the angle / atan / sincos chain hides their latency
+    float4 pat[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) pat[r] = reinterpret_cast<const float4*>(c_pattern)[r * 64 + lane];
+#endif
     // IC_Angle on the unblurred patch, centre (21, 21), as six more products (c_angle_a) chained
     // over the row tiles; the diagonal element D[n][n] sits in lane 20 (n / 4) + n % 4, register
     // n % 4: each lane takes register lane % 4, and the quads at row offset 4 (lane / 16) are summed.
@@ -2386,8 +2395,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     DESC_STAMP(3);
     sincos_f2d(ang, &b, &a);
     DESC_STAMP(4);
-    auto sample = [&](int idx) -> int {
-        const float x = c_pattern[2 * idx], y = c_pattern[2 * idx + 1];
+    auto sample = [&](float x, float y) -> int {
         // byte offset of blurred pixel (18 + dy, 18 + dx) from the rounded floats (exact integers)
         const float dy = rintf(x * b + y * a), dx = rintf(x * a - y * b);
         const int ob = (int)fmaf(dy, (float)(2 * HBS), fmaf(dx, 2.f, (float)(2 * (18 * HBS + 18))));
@@ -2404,8 +2412,12 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     unsigned long long words[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int p = r * 64 + lane;
-        words[r] = __ballot(sample(2 * p) < sample(2 * p + 1));
+#if DESC_PAT_EARLY
+        const float4 q = pat[r];
+#else
+        const float4 q = reinterpret_cast<const float4*>(c_pattern)[r * 64 + lane];   // pairs 2p, 2p + 1
+#endif
+        words[r] = __ballot(sample(q.x, q.y) < sample(q.z, q.w));
     }
     DESC_STAMP(5);
     // The 32 descriptor bytes and the 7-word keypoint record are wave-uniform: v_writelane places
