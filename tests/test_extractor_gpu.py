@@ -278,6 +278,25 @@ def test_batch_device_matches_single(oracle):
         assert_same_kps(kps, okps, desc_all[i, :n], odesc)
 
 
+def test_extract_batch_repeatable():
+    """The same batch extracted three times gives bit-identical keypoints and descriptors (round 4: two
+    builds broke this while every parity test against the oracle still passed)."""
+    import torch
+    frames = np.stack([_patchwork(60 + i, 320, 240) for i in range(16)])
+    t = torch.from_numpy(frames).cuda()
+    ex = make(500)
+    outs = []
+    for _ in range(3):
+        o = ex.extract_batch_device(t)
+        torch.cuda.synchronize()
+        outs.append([x.cpu().numpy() for x in o])
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][2], o[2])
+        for i, n in enumerate(outs[0][2]):
+            assert np.array_equal(outs[0][0][i, :n], o[0][i, :n]), i
+            assert np.array_equal(outs[0][1][i, :n], o[1][i, :n]), i
+
+
 @pytest.mark.parametrize("nsub,cpw", [(1, 1), (2, 4), (3, 3)])
 def test_batch_sub_streams_and_cells_per_wave(monkeypatch, nsub, cpw):
     """Sub-batches on side streams (ORBX_NSUB) and the FAST cells-per-wave pipelining
