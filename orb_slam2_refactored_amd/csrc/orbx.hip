@@ -2196,7 +2196,7 @@ __device__ unsigned long long g_desc_stamps[1024 * 8];
 // One workgroup = one wavefront = one selection slot (a kept keypoint or an empty slot).
 constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per raw-patch row
 #ifndef DESC_PAT_EARLY
-#define DESC_PAT_EARLY 0   // A/B: the rBRIEF pattern loads issued before the angle chain
+#define DESC_PAT_EARLY 1   // the rBRIEF pattern loads issued before the angle chain (0: at the samples; A/B)
 #endif
 
 // One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
