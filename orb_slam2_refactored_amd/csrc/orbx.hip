@@ -2195,6 +2195,9 @@ __device__ unsigned long long g_desc_stamps[1024 * 8];
 
 // One workgroup = one wavefront = one selection slot (a kept keypoint or an empty slot).
 constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per raw-patch row
+#ifndef DESC_ANGLE_MFMA
+#define DESC_ANGLE_MFMA 1   // IC_Angle as i8 products on the blur's B fragments (0: LDS disk reads; A/B)
+#endif
 #ifndef DESC_PAT_EARLY
 #define DESC_PAT_EARLY 1   // the rBRIEF pattern loads issued before the angle chain (0: at the samples; A/B)
 #endif
@@ -2315,6 +2318,39 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     __syncthreads();
     DESC_STAMP(1);
 
+#if !DESC_ANGLE_MFMA   // the round-3 IC_Angle (LDS disk reads), for A/B builds
+    // IC_Angle on the unblurred level, patch centre (21, 21).  Lane = (row parity, u + 15): lanes
+    // 0-31 take rows +-v for odd v, lanes 32-63 for v + 1, so the 15 row pairs take 8 steps.
+    int m10 = 0, m01 = 0;
+    {
+        const int hv = lane >> 5, u = (lane & 31) - 15;   // u = 16 on lanes 31 / 63: outside every umax
+        const uint8_t* cp = R + 21 * RS + 21 + u + hv * RS;
+        // every read unconditional (all inside the 43x43 patch) and issued together; the disk mask
+        // is applied to the products
+        int vp[8], vm[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int vv = 2 * t + 1;
+            vp[t] = cp[vv * RS];
+            vm[t] = cp[-(vv + 2 * hv) * RS];
+        }
+        const int c0 = R[21 * RS + 21 + u];
+        m10 = (hv == 0 && u <= 15) ? u * c0 : 0;
+        // the disk mask as lane-constant multipliers (branch-free multiply-adds)
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int vv = 2 * t + 1;
+            const int v = vv + hv;
+            const int um = hv ? (vv + 1 <= 15 ? c_umax_h[vv + 1] : -1) : c_umax_h[vv];
+            const bool in = u >= -um && u <= um;
+            const int vin = in ? v : 0, uin = in ? u : 0;
+            m01 += vin * (vp[t] - vm[t]);
+            m10 += uin * (vp[t] + vm[t]);
+        }
+    }
+    m10 = wave_sum_i32(m10);
+    m01 = wave_sum_i32(m01);
+#endif
     // The raw rows as i8 B fragments (p - 128), shared by the angle and the blur products: lane
     // (n, g) holds columns 16 g .. +15 of patch row n + 16 nt.  Every read of R is issued before the
     // first Hb write (R aliases Hb; one wavefront's LDS operations complete in order).
@@ -2363,6 +2399,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     // IC_Angle on the unblurred patch, centre (21, 21), as six more products (c_angle_a) chained
     // over the row tiles; the diagonal element D[n][n] sits in lane 20 (n / 4) + n % 4, register
     // n % 4: each lane takes register lane % 4, and the quads at row offset 4 (lane / 16) are summed.
+#if DESC_ANGLE_MFMA
     int m10, m01;
     {
         i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0};
@@ -2385,6 +2422,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         m01 = __builtin_amdgcn_readlane(tv, 0) + __builtin_amdgcn_readlane(tv, 20) +
               __builtin_amdgcn_readlane(tv, 40) + __builtin_amdgcn_readlane(tv, 60);
     }
+#endif
     const float angle = fast_atan2_dev((float)m01, (float)m10);
     DESC_STAMP(2);
     __syncthreads();
