@@ -59,10 +59,6 @@ struct LevelDev {
     int quota, out_cap, out_base;
     int nroots;
     double hx;
-    // root_t[q] (q = 1 .. nroots, nroots <= 7): the smallest dx >= 0 with (int)((double)dx / hx) >= q,
-    // from the host with the same double arithmetic, so a point's root is a count of thresholds;
-    // nroots > 7 keeps the division (root_t[0] = 0 marks the thresholds valid)
-    unsigned short root_t[8];
     float scale, size;
     long long xtab_off, ytab_off;   // resize coefficient tables (l >= 1)
     double ssx, ssy;                // (double)w[l-1] / w[l], (double)h[l-1] / h[l] (l >= 1)
@@ -1755,13 +1751,6 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
     if (threadIdx.x == 0) s_fail = 0;
     __syncthreads();
     auto root_of = [&](uint32_t k) -> int {
-        if (R <= 7) {   // block-uniform: thresholds (exactly the division below for dx >= 0)
-            const int dxi = kp_x(k) - L.rx;
-            int r = 0;
-#pragma unroll
-            for (int q = 1; q < 7; q++) r += (q < R && dxi >= (int)L.root_t[q]) ? 1 : 0;
-            return (dxi < 0 || dxi >= (int)L.root_t[R]) ? -1 : r;   // outside the roots: the fault path
-        }
         const float dx = (float)kp_x(k) - (float)L.rx;   // keypoint.pt.x - roi.x (float)
         return (int)((double)dx / L.hx);
     };
@@ -2703,15 +2692,6 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
                     return ORB_EINVAL;
                 }
                 L.hx = 1. * L.rw / L.nroots;
-                if (L.nroots <= 7) {   // root thresholds: the division's values over dx = 0, 1, ...
-                    int q = 1;
-                    for (int d = 0; q <= L.nroots && d <= 65535; d++)
-                        while (q <= L.nroots && (int)((double)(float)d / L.hx) >= q) L.root_t[q++] = (unsigned short)d;
-                    if (q <= L.nroots) {
-                        set_error("quadtree root thresholds out of range");
-                        return ORB_EINTERNAL;
-                    }
-                }
                 L.out_cap = std::max(L.quota + 3, 4 * L.nroots) + 1;
                 NC = std::max(NC, L.out_cap + 8);
             }
