@@ -2198,6 +2198,9 @@ constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per r
 #ifndef DESC_ANGLE_MFMA
 #define DESC_ANGLE_MFMA 1   // IC_Angle as i8 products on the blur's B fragments (0: LDS disk reads; A/B)
 #endif
+#ifndef DESC_ANGLE_FIRST
+#define DESC_ANGLE_FIRST 0   // A/B: the angle products before the blur's
+#endif
 #ifndef DESC_PAT_EARLY
 #define DESC_PAT_EARLY 1   // the rBRIEF pattern loads issued before the angle chain (0: at the samples; A/B)
 #endif
@@ -2362,6 +2365,43 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         bfr[nt] ^= (int)0x80808080u;
     }
 
+#if DESC_ANGLE_MFMA
+    // IC_Angle on the unblurred patch, centre (21, 21), as six more products (c_angle_a) chained
+    // over the row tiles; the diagonal element D[n][n] sits in lane 20 (n / 4) + n % 4, register
+    // n % 4: each lane takes register lane % 4, and the quads at row offset 4 (lane / 16) are summed.
+    int m10 = 0, m01 = 0;
+    auto angle_products = [&](const i4v (&au)[3], const i4v (&av)[3]) {
+        i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0};
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            du = __builtin_amdgcn_mfma_i32_16x16x64_i8(au[nt], bfr[nt], du, 0, 0, 0);
+            dv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[nt], bfr[nt], dv, 0, 0, 0);
+        }
+        const bool q1 = lane & 1, q2 = lane & 2;
+        int tu = q2 ? (q1 ? du.w : du.z) : (q1 ? du.y : du.x);
+        int tv = q2 ? (q1 ? dv.w : dv.z) : (q1 ? dv.y : dv.x);
+        tu += dpp_i32<0xB1>(tu);   // quad_perm [1,0,3,2]
+        tv += dpp_i32<0xB1>(tv);
+        tu += dpp_i32<0x4E>(tu);   // quad_perm [2,3,0,1]
+        tv += dpp_i32<0x4E>(tv);
+        m10 = __builtin_amdgcn_readlane(tu, 0) + __builtin_amdgcn_readlane(tu, 20) +
+              __builtin_amdgcn_readlane(tu, 40) + __builtin_amdgcn_readlane(tu, 60);
+        m01 = __builtin_amdgcn_readlane(tv, 0) + __builtin_amdgcn_readlane(tv, 20) +
+              __builtin_amdgcn_readlane(tv, 40) + __builtin_amdgcn_readlane(tv, 60);
+    };
+#if DESC_ANGLE_FIRST   // the angle products (and the atan / sincos chain) ahead of the blur's
+    {
+        i4v au[3], av[3];
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            au[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
+            av[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
+        }
+        angle_products(au, av);
+    }
+#endif
+#endif
+
     // horizontal Q8 blur on the matrix cores (c_hblur_a): 3 x 3 tiles of 16 blurred columns x 16
     // rows; lane (n, g) of tile (mt, nt) gets columns 16 mt + 4 g .. +3 of row 16 nt + n.  Rows past
     // 42 (stored into slack rows) and columns past 36 are computed from neighbouring bytes and never
@@ -2396,31 +2436,15 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 #pragma unroll
     for (int r = 0; r < 4; r++) pat[r] = reinterpret_cast<const float4*>(c_pattern)[r * 64 + lane];
 #endif
-    // IC_Angle on the unblurred patch, centre (21, 21), as six more products (c_angle_a) chained
-    // over the row tiles; the diagonal element D[n][n] sits in lane 20 (n / 4) + n % 4, register
-    // n % 4: each lane takes register lane % 4, and the quads at row offset 4 (lane / 16) are summed.
-#if DESC_ANGLE_MFMA
-    int m10, m01;
+#if DESC_ANGLE_MFMA && !DESC_ANGLE_FIRST
     {
-        i4v du = {0, 0, 0, 0}, dv = {0, 0, 0, 0};
+        i4v au[3], av[3];
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-            const i4v au = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
-            const i4v av = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
-            du = __builtin_amdgcn_mfma_i32_16x16x64_i8(au, bfr[nt], du, 0, 0, 0);
-            dv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bfr[nt], dv, 0, 0, 0);
+            au[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
+            av[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
         }
-        const bool q1 = lane & 1, q2 = lane & 2;
-        int tu = q2 ? (q1 ? du.w : du.z) : (q1 ? du.y : du.x);
-        int tv = q2 ? (q1 ? dv.w : dv.z) : (q1 ? dv.y : dv.x);
-        tu += dpp_i32<0xB1>(tu);   // quad_perm [1,0,3,2]
-        tv += dpp_i32<0xB1>(tv);
-        tu += dpp_i32<0x4E>(tu);   // quad_perm [2,3,0,1]
-        tv += dpp_i32<0x4E>(tv);
-        m10 = __builtin_amdgcn_readlane(tu, 0) + __builtin_amdgcn_readlane(tu, 20) +
-              __builtin_amdgcn_readlane(tu, 40) + __builtin_amdgcn_readlane(tu, 60);
-        m01 = __builtin_amdgcn_readlane(tv, 0) + __builtin_amdgcn_readlane(tv, 20) +
-              __builtin_amdgcn_readlane(tv, 40) + __builtin_amdgcn_readlane(tv, 60);
+        angle_products(au, av);
     }
 #endif
     const float angle = fast_atan2_dev((float)m01, (float)m10);
