@@ -987,7 +987,6 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // that is DetectFAST's answer (:527); otherwise the cell is re-run at min(ini, min).  On
     // texture-rich frames most pixels pass at minThFAST but few at iniThFAST.
     int prev_ini = 0;
-    int prev_y0 = -1000, prev_zh = 0;
     for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
     int ci;
@@ -995,25 +994,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     const int x0 = src.x0, y0 = src.y0;
     const int zh = cell.zwzh >> 16;
     {
-        // Round 4: the cell below the previous one (a strip walks a column) shares its crop's last 6
-        // rows (the 3-row aprons): they move inside LDS to rows 0..5 instead of being fetched again
-        // (fast_cells fetched 1.19x the level's bytes, 36 crop rows per 30 new ones).
-        int r0 = 0;
-        if (y0 == prev_y0 + prev_zh && prev_zh >= 6) {   // wave-uniform
-            uint32_t* cw = reinterpret_cast<uint32_t*>(crop);
-            const int ndw = 6 * CSd / 4, sdw = prev_zh * CSd / 4;   // CSd: a multiple of 4
-            const uint32_t t0 = lane < ndw ? cw[sdw + lane] : 0u;
-            const uint32_t t1 = lane + 64 < ndw ? cw[sdw + 64 + lane] : 0u;
-            if (lane < ndw) cw[lane] = t0;
-            if (lane + 64 < ndw) cw[64 + lane] = t1;
-            r0 = 6;
-        }
-        CropSrc rest = src;   // rows r0 .. ch - 1
-        rest.y0 += r0;
-        rest.ch -= r0;
-        crop_stage_rows<CST>(rest, lane, crop + r0 * CSd, CSd);
-        prev_y0 = y0;
-        prev_zh = zh;
+        crop_stage_rows<CST>(src, lane, crop, CSd);
     }
     const int tlo = min(th_ini, th_min);
     bool spec = spec_min > 0 && th_ini > tlo && prev_ini >= spec_min;
@@ -2856,8 +2837,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
         // rows: the tallest crop + slack, and at least the CROP_NG row groups of 4 rows the staging's first
         // batch always stores
-        // (+6 rows: a strip's later cells stage from row 6, their first batch reaching row 6 + 4 CROP_NG - 1)
-        fl.crop_bytes = (int)align_up((size_t)fl.CS * std::max(mzh + 6 + FAST_CROP_SLACK, 4 * CROP_NG + 6), 16);
+        fl.crop_bytes = (int)align_up((size_t)fl.CS * std::max(mzh + 6 + FAST_CROP_SLACK, 4 * CROP_NG), 16);
         fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
         fl.qcap = 2 * GR_RING + FQ2_RING;   // in u16 entries
         fl.ccap = std::min(FAST_CLIST_CAP, (int)align_up((size_t)mzw * mzh, 8));
