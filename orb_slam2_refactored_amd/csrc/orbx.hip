@@ -2204,6 +2204,14 @@ constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per r
 #ifndef DESC_PAT_EARLY
 #define DESC_PAT_EARLY 1   // the rBRIEF pattern loads issued before the angle chain (0: at the samples; A/B)
 #endif
+#ifndef DESC_HBT
+#define DESC_HBT 1   // blurred patch column-major: a sample's 7 vertical taps in 4 dwords (0: row-major, 7 u16 reads)
+#endif
+// column-major blurred patch: column c (0..39) holds rows 0..47 at u16 c * HCS; 26 dwords per column
+// put the 16 columns of one b64 store group on distinct bank pairs
+constexpr int HCS = 52;
+static_assert(HCS % 4 == 0 && HCS >= 48, "8-byte aligned columns of 48 rows (the tiles' slack rows)");
+constexpr int HB_ELEMS = DESC_HBT ? 40 * HCS : 48 * HBS;
 
 // One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
 __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
@@ -2214,9 +2222,9 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                                                       int cap) {
     // the raw patch R is dead once every lane holds its row for the horizontal blur (one
     // wavefront: its LDS reads complete before its later writes), so the blurred rows Hb reuse it
-    __shared__ __attribute__((aligned(16))) uint16_t Hb[48 * HBS];   // 43 blurred rows + 5 rows of blur slack
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];   // 43 blurred rows + 5 rows of blur slack
     uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
-    static_assert(47 * RS + 64 <= 48 * HBS * 2, "R (and the blur's reads of rows 43..47) must fit in Hb");
+    static_assert(47 * RS + 64 <= HB_ELEMS * 2, "R (and the blur's reads of rows 43..47) must fit in Hb");
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int f = divmod_of(g, lb);
@@ -2412,19 +2420,34 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 #pragma unroll
         for (int nt = 0; nt < 3; nt++)
 #pragma unroll
-            for (int mt = 0; mt < 3; mt++) acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+            for (int mt = 0; mt < 3; mt++)
+#if DESC_HBT
+                // the transposed product (patch rows as A, the blur band as B: the same k pairing):
+                // lane (n, g) gets rows 16 nt + 4 g .. +3 of blurred column 16 mt + n
+                acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bfr[nt], afr[mt], cinit, 0, 0, 0);
+#else
+                acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+#endif
         auto put = [&](int nt, int mt) {
             uint2 pk;
             pk.x = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].y, (uint32_t)acc[nt][mt].x, 0x05040100u);
             pk.y = __builtin_amdgcn_perm((uint32_t)acc[nt][mt].w, (uint32_t)acc[nt][mt].z, 0x05040100u);
+#if DESC_HBT
+            *reinterpret_cast<uint2*>(&Hb[(16 * mt + n) * HCS + 16 * nt + 4 * lg]) = pk;   // rows 43..47: slack
+#else
             *reinterpret_cast<uint2*>(&Hb[(16 * nt + n) * HBS + 16 * mt + 4 * lg]) = pk;   // rows 43..47: slack
+#endif
         };
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
             put(nt, 0);
             put(nt, 1);
         }
+#if DESC_HBT
+        if (n < 8) {   // columns 32..39 of the third tile
+#else
         if (lg < 2) {   // columns 32..39 of the third tile (40..47 would wrap into the next row)
+#endif
 #pragma unroll
             for (int nt = 0; nt < 3; nt++) put(nt, 2);
         }
@@ -2460,6 +2483,24 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     auto sample = [&](float x, float y) -> int {
         // byte offset of blurred pixel (18 + dy, 18 + dx) from the rounded floats (exact integers)
         const float dy = rintf(x * b + y * a), dx = rintf(x * a - y * b);
+#if DESC_HBT
+        // u16 index of blurred pixel (18 + dy, 18 + dx) in the column-major map; its 7 vertical taps
+        // (rows 18 + dy .. +6) are u16 q .. q + 6, inside dwords q / 2 .. q / 2 + 3, realigned by q's parity
+        const int q = (int)fmaf(dx, (float)HCS, dy + (float)(18 * HCS + 18));
+        const uint32_t* cw = reinterpret_cast<const uint32_t*>(Hb) + (q >> 1);
+        const uint32_t d0 = cw[0], d1 = cw[1], d2 = cw[2], d3 = cw[3];
+        const uint32_t sh = (uint32_t)(q & 1) * 2u;   // bytes
+        const us2 p01 = u2us(__builtin_amdgcn_alignbyte(d1, d0, sh));
+        const us2 p23 = u2us(__builtin_amdgcn_alignbyte(d2, d1, sh));
+        const us2 p45 = u2us(__builtin_amdgcn_alignbyte(d3, d2, sh));
+        const us2 p6x = u2us(__builtin_amdgcn_alignbyte(d3, d3, sh));   // tap 6 in the low half
+        const us2 k01 = {18, 34}, k23 = {48, 56}, k45 = {48, 34}, k6x = {18, 0};
+        unsigned acc = __builtin_amdgcn_udot2(p6x, k6x, 1u << 15, false);
+        acc = __builtin_amdgcn_udot2(p01, k01, acc, false);
+        acc = __builtin_amdgcn_udot2(p23, k23, acc, false);
+        acc = __builtin_amdgcn_udot2(p45, k45, acc, false);
+        return (int)(acc >> 16);
+#else
         const int ob = (int)fmaf(dy, (float)(2 * HBS), fmaf(dx, 2.f, (float)(2 * (18 * HBS + 18))));
         const uint16_t* col = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(Hb) + ob);
         // vertical taps as u16 pairs (d16 / d16_hi loads) into v_dot2_u32_u16, rounding bias as the
@@ -2470,6 +2511,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         acc = __builtin_amdgcn_udot2(p23, k23, acc, false);
         acc = __builtin_amdgcn_udot2(p45, k45, acc, false);
         return (int)(acc >> 16);
+#endif
     };
     unsigned long long words[4];
 #pragma unroll
