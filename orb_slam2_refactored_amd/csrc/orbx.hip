@@ -2204,6 +2204,9 @@ constexpr int PATCH_DW = (PATCH + 3) / 4;                 // dwords staged per r
 #ifndef DESC_PAT_EARLY
 #define DESC_PAT_EARLY 1   // the rBRIEF pattern loads issued before the angle chain (0: at the samples; A/B)
 #endif
+#ifndef DESC_SCALAR_PRE
+#define DESC_SCALAR_PRE 1   // the slot's keypoint word and the frame's level counts by scalar loads (0: one vector load)
+#endif
 #ifndef DESC_HBT
 #define DESC_HBT 1   // blurred patch column-major: a sample's 7 vertical taps in 4 dwords (0: row-major, 7 u16 reads)
 #endif
@@ -2227,6 +2230,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     static_assert(47 * RS + 64 <= HB_ELEMS * 2, "R (and the blur's reads of rows 43..47) must fit in Hb");
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    DESC_STAMP(7);   // entry (diagnostic build): the preamble's loads are timed from here
     const int f = divmod_of(g, lb);
     const int s = lb - f * g.out_frame;   // selection slot (level-major, out_cap slots per level)
     // The slot's level and the frame's per-level counts without a dependent chain of loads: the
@@ -2234,10 +2238,20 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     // count to lane q < nlevels and the slot's keypoint word to lane 63, and the level's output base
     // is an inclusive row scan of the counts (nlevels <= 16: lanes 0-15).
     const int nl = g.nlevels;
+#if DESC_SCALAR_PRE
+    // every address here is wave-uniform: scalar loads (the scalar cache path, not queued behind the
+    // other wavefronts' patch loads); 16 counts read unconditionally (the count buffer has 64 B of slack)
+    const uint32_t k = sel[(long long)f * g.out_frame + s];
+    const int* cf = sel_cnt + f * nl;
+    int cnt16[MAX_LEVELS];
+#pragma unroll
+    for (int q = 0; q < MAX_LEVELS; q++) cnt16[q] = cf[q];
+#else
     const int* lp = lane < nl ? sel_cnt + f * nl + lane
                               : reinterpret_cast<const int*>(sel + (long long)f * g.out_frame + s);
     const int cw = (lane < nl || lane == 63) ? *lp : 0;
     const int cq = lane < nl ? cw : 0;
+#endif
     // levels >= nlevels carry 0x7fff (host; out_frame < 0x7fff checked there): a field x <= s iff bit
     // 15 of (x | 0x8000) - (s + 1) is clear, and no field borrows from the next
     int l = MAX_LEVELS;
@@ -2246,6 +2260,16 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 #pragma unroll
         for (int d = 0; d < MAX_LEVELS / 2; d++) l -= __popc(((g.lv_start[d] | 0x80008000u) - s1) & 0x80008000u);
     }
+#if DESC_SCALAR_PRE
+    int total = 0, lbase = 0, cnt_l = 0;
+#pragma unroll
+    for (int q = 0; q < MAX_LEVELS; q++) {
+        const int cq = q < nl ? cnt16[q] : 0;
+        total += cq;
+        lbase += q < l ? cq : 0;
+        cnt_l = q == l ? cq : cnt_l;
+    }
+#else
     int sc = cq;
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xf, 0xf, true);   // row_shr:1 (zero fill)
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);   // row_shr:2
@@ -2255,6 +2279,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const int total = __builtin_amdgcn_readlane(sc, 15);
     const int lbase = l > 0 ? __builtin_amdgcn_readlane(sc, l - 1) : 0;
     const int cnt_l = __builtin_amdgcn_readlane(cq, l);
+#endif
     const LevelDev& L = g.lv[l];
     if (s == 0 && lane == 0) counts[f] = total;
     const int i = s - L.out_base;
@@ -2908,7 +2933,8 @@ static int reserve_workspace(orbx_extractor* h, int frames) {
     if ((rc = h->d_P.reserve((size_t)frames * g.cand_frame * 4))) return rc;
     if ((rc = h->d_T.reserve((size_t)frames * g.cand_frame * 4))) return rc;
     if ((rc = h->d_sel.reserve((size_t)frames * g.out_frame * 4))) return rc;
-    if ((rc = h->d_selcnt.reserve((size_t)frames * g.nlevels * 4))) return rc;
+    // + 64 B: describe reads 16 counts from a frame's first (scalar loads, past the last frame too)
+    if ((rc = h->d_selcnt.reserve((size_t)frames * g.nlevels * 4 + 64))) return rc;
     if (!h->d_fault.ptr) {   // sticky until read (orbx_batch_status / the host Extract)
         if ((rc = h->d_fault.reserve(16))) return rc;
         ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));

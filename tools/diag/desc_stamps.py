@@ -33,8 +33,10 @@ assert lib().orbx_debug_qt_stamps(C.cast(buf, C.c_void_p)) == 0
 st = np.array(list(buf)[64:], dtype=np.int64).reshape(1024, 8)
 st = st[(st[:, 0] > 0) & (st[:, 6] > 0)]
 d = np.diff(st[:, :7], axis=1)
-names = ["patch load+stage", "IC angle+atan", "H blur", "sincos", "samples+ballots", "stores"]
+names = ["patch load+stage", "blur+angle+atan", "barrier", "sincos", "samples+ballots", "stores"]
 print(f"{len(st)} sampled wavefronts; median ticks per phase:")
+pre = st[:, 0] - st[:, 7]   # stamp 7: entry, before the keypoint-word / count load and the level lookup
+print(f"  {'preamble (kp load)':18s} {int(np.median(pre)):8d}  (p90 {int(np.percentile(pre, 90))})")
 for i, n in enumerate(names):
     print(f"  {n:18s} {int(np.median(d[:, i])):8d}  (p90 {int(np.percentile(d[:, i], 90))})")
-print("  total", int(np.median(st[:, 6] - st[:, 0])))
+print("  total", int(np.median(st[:, 6] - st[:, 7])))
