@@ -59,6 +59,22 @@ int orbx_destroy(orbx_extractor* h);
 int orbx_scale_tables(const orbx_extractor* h, float* scale, float* inv_scale, float* sigma2,
                       float* inv_sigma2, int32_t* features_per_level);
 
+/* OpenCV-build switches.  Two results of the reference depend on how its OpenCV / C++ headers were
+ * built, not on its own source; each is a switch here (default in brackets), restated identically by
+ * the CPU oracle (oracle_set_compat).  INTEGRATION.md §1 says how to pick them for a given build.
+ *   trig_mode   ComputeOrbDescriptor's `cos(angle)` / `sin(angle)` on a float (src/ORBextractor.cc:107):
+ *               [0] ::cos(double) / ::sin(double), the overload visible without `using namespace std`;
+ *               1 std::cos(float) / std::sin(float) = glibc cosf / sinf (a `using namespace std`, or a
+ *               libstdc++ <math.h> wrapper, before :107).
+ *   resize_simd the vector width V (bytes) of the OpenCV build's cv::resize INTER_LINEAR 8U vertical pass
+ *               (src/ORBextractor.cc:468; VResizeLinearVec_32s8u rounds via (S >> 4) * b >> 16, its
+ *               scalar tail via (S0*b0 + S1*b1 + 2^21) >> 22): [16] SSE2-SSE4 / NEON baseline builds,
+ *               32 AVX2 baseline, 64 AVX-512 baseline, 8 (half-width), 1 no SIMD (scalar everywhere),
+ *               0 the SIMD rounding on every column.
+ * -1 keeps a switch.  Environment defaults at orbx_create: ORBX_TRIG=double|float, ORBX_RESIZE_TAIL=V. */
+int orbx_set_opencv_compat(orbx_extractor* h, int trig_mode, int resize_simd);
+int orbx_get_opencv_compat(const orbx_extractor* h, int* trig_mode, int* resize_simd);
+
 /* Upper bound on keypoints Extract can return for an image of rows x cols (per-level
  * quadtree output <= max(quota, 4*roots) + 3). */
 int orbx_max_keypoints(const orbx_extractor* h, int rows, int cols, int32_t* cap);

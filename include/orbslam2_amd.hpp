@@ -62,6 +62,13 @@ public:
     ORBextractor(const ORBextractor&) = delete;
     ORBextractor& operator=(const ORBextractor&) = delete;
 
+    // The OpenCV-build switches (orbslam2_amd.h orbx_set_opencv_compat): trig_mode 0
+    // ::cos(double) / 1 cosf for src/ORBextractor.cc:107, resize_simd = the cv::resize SIMD width V.
+    // -1 keeps a switch.
+    void SetOpenCVCompat(int trig_mode, int resize_simd) {
+        check(orbx_set_opencv_compat(h_, trig_mode, resize_simd), "orbx_set_opencv_compat");
+    }
+
     // Extract on a raw CV_8U image.  Returns false (outputs untouched) when no keypoint exists —
     // the reference's early return (src/ORBextractor.cc:778-782).
     bool Extract(const uint8_t* img, int rows, int cols, size_t step, std::vector<orbx_keypoint>& keypoints,

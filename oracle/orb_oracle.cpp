@@ -39,11 +39,19 @@
  * therefore "parity unpinned" against a real OpenCV/g2o build; it is pinned only by the
  * known-answer values derivable from the reference text (umax, quotas, pyramid sizes, Gaussian
  * taps, pattern checksum — tests/test_oracle_kat.py) and by libstdc++ itself for the sort.
- * Documented choices where the reference is ambiguous:
- *   - cos/sin in ComputeOrbDescriptor (:107) resolve to ::cos(double) (no `using namespace std`
- *     in the refactor) => a = (float)cos((double)angle).
- *   - cv::resize vertical pass uses the universal-intrinsics rounding
- *     ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2 for every column (the SIMD loop's formula).
+ * Documented choices where the reference is ambiguous, each a switch (oracle_set_compat, the same
+ * modes as the product's orbx_set_opencv_compat):
+ *   - cos/sin in ComputeOrbDescriptor (:107).  trig 0 (default): ::cos(double) (no `using namespace
+ *     std` in the refactor) => a = (float)cos((double)angle).  trig 1: the float overloads
+ *     std::cos(float) / std::sin(float) = glibc cosf / sinf (visible when a `using namespace std` or
+ *     a libstdc++ <math.h> wrapper precedes :107).
+ *   - cv::resize vertical pass (VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>,
+ *     VResizeLinearVec_32s8u>).  The SIMD part rounds ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2;
+ *     the scalar tail after it (S0*b0 + S1*b1 + 2^21) >> 22.  resize_simd V = the build's vector
+ *     width in bytes: the SIMD loop covers x += V while x <= w - V, then x += V/2 while x < w - V/2;
+ *     the scalar formula takes the rest.  V = 16 (default: SSE2-SSE4 / NEON baseline builds), 32
+ *     (AVX2 baseline), 64 (AVX-512 baseline), 1 (no SIMD: scalar everywhere), 0 (the SIMD formula on
+ *     every column, rounds 1-4's only mode).
  *   - GaussianBlur taps are OpenCV 4.x's error-diffused Q8 [18,34,48,56,48,34,18].
  *   - Compiled -ffp-contract=off: the reference is ISO C++14 (CMakeLists.txt:10-11), under
  *     which GCC does not contract a*b+c.
@@ -116,6 +124,21 @@ struct Img {
     uint8_t at(int y, int x) const { return data[(size_t)y * step + x]; }
 };
 
+// OpenCV-build switches (oracle_set_compat); process-wide, set before any extraction
+static int g_trig_float = 0;    // 0: (float)::cos((double)angle); 1: cosf / sinf
+static int g_resize_simd = 16;  // vector width V of the resize's VResizeLinearVec_32s8u (see header)
+
+// First column VResizeLinear computes with its scalar loop ([ext] imgproc/src/resize.cpp: the vector
+// op returns x after `for (; x <= w - V; x += V)` and `for (; x < w - V/2; x += V/2)`).
+static int resize_tail_x(int w, int V) {
+    if (V <= 0) return w;
+    if (V == 1) return 0;
+    int x = 0;
+    for (; x <= w - V; x += V) {}
+    for (; x < w - V / 2; x += V / 2) {}
+    return x;
+}
+
 // cv::resize(src, dst, Size(dw, dh)) with INTER_LINEAR on CV_8UC1 [ext].
 static void resize_linear(const Img& src, Img& dst, int dw, int dh) {
     const int sw = src.cols, sh = src.rows;
@@ -154,11 +177,14 @@ static void resize_linear(const Img& src, Img& dst, int dw, int dh) {
         hrow(clip(sy), r0);
         hrow(clip(sy + 1), r1);
         uint8_t* D = dst.mut_row(dy);
-        for (int x = 0; x < dw; x++) {
+        const int xt = resize_tail_x(dw, g_resize_simd);
+        for (int x = 0; x < xt; x++) {   // VResizeLinearVec_32s8u: v_mul_hi of the packed S >> 4, v_rshr_pack_u<2>
             const int s0 = std::min(r0[x] >> 4, 32767), s1 = std::min(r1[x] >> 4, 32767);
             const int v = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
             D[x] = sat_u8((v + 2) >> 2);
         }
+        for (int x = xt; x < dw; x++)   // scalar tail: FixedPtCast<int, uchar, 22>
+            D[x] = sat_u8((r0[x] * b0 + r1[x] * b1 + (1 << 21)) >> 22);
     }
 }
 
@@ -530,7 +556,14 @@ struct Extractor {
     static void describe(const Kp& k, const Img& im, uint8_t* desc) {
         const float factorPI = (float)(M_PI / 180.f);
         const float angle = k.angle * factorPI;
-        const float a = (float)std::cos((double)angle), b = (float)std::sin((double)angle);
+        float a, b;
+        if (g_trig_float) {   // std::cos(float) / std::sin(float): glibc cosf / sinf
+            a = std::cos(angle);
+            b = std::sin(angle);
+        } else {              // ::cos(double) / ::sin(double)
+            a = (float)std::cos((double)angle);
+            b = (float)std::sin((double)angle);
+        }
         const uint8_t* c = im.row(cv_round(k.y)) + cv_round(k.x);
         const int step = (int)im.step;
         auto val = [&](int idx) {
@@ -1462,6 +1495,16 @@ void oracle_gaussian_taps(int32_t* taps7) {
 }
 
 float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+
+// OpenCV-build switches (see the header): trig 0 double / 1 float; resize_simd V in {0, 1, 16, 32, 64}.
+// Negative values leave a switch unchanged.  Returns the previous values as trig | V << 8.
+int oracle_set_compat(int trig, int resize_simd) {
+    const int prev = g_trig_float | (g_resize_simd << 8);
+    if (trig >= 0) g_trig_float = trig ? 1 : 0;
+    if (resize_simd >= 0) g_resize_simd = resize_simd;
+    return prev;
+}
+int oracle_resize_tail_x(int w, int resize_simd) { return resize_tail_x(w, resize_simd); }
 
 // Pyramid: level l written at out + offs[l] (tight rows); dims in w[l], h[l].
 int oracle_pyramid(const orbx_params* prm, const uint8_t* img, int rows, int cols, size_t step, uint8_t* out,

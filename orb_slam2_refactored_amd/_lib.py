@@ -133,6 +133,8 @@ SIGNATURES = {
     "orbx_destroy": (C.c_int, [VP]),
     "orbx_scale_tables": (C.c_int, [VP, VP, VP, VP, VP, VP]),
     "orbx_max_keypoints": (C.c_int, [VP, C.c_int, C.c_int, C.POINTER(I32)]),
+    "orbx_set_opencv_compat": (C.c_int, [VP, C.c_int, C.c_int]),
+    "orbx_get_opencv_compat": (C.c_int, [VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "orbx_extract": (C.c_int, [VP, VP, C.c_int, C.c_int, SZ, VP, VP, C.c_int, C.POINTER(C.c_int)]),
     "orbx_pyramid_level": (C.c_int, [VP, C.c_int, VP, SZ, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "orbx_extract_batch_device": (C.c_int, [VP, VP, C.c_int, C.c_int, C.c_int, SZ, SZ, VP, VP, VP, C.c_int, VP]),

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include <hip/hip_ext.h>
@@ -62,6 +63,7 @@ struct LevelDev {
     float scale, size;
     long long xtab_off, ytab_off;   // resize coefficient tables (l >= 1)
     double ssx, ssy;                // (double)w[l-1] / w[l], (double)h[l-1] / h[l] (l >= 1)
+    int tail_x;                     // first column of VResizeLinear's scalar tail (l >= 1; w: none)
 };
 
 struct Geom {
@@ -181,7 +183,9 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
 // 1. pyramid
 // ------------------------------------------------------------------------------------------
 // cv::resize INTER_LINEAR CV_8UC1 [ext]: horizontal 11-bit fixed point (exact int32), vertical
-// with the universal-intrinsics rounding ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2.
+// with the universal-intrinsics rounding ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2 up to the
+// level's tail_x and the scalar loop's (S0*b0 + S1*b1 + 2^21) >> 22 from there (the OpenCV build's
+// SIMD width decides where the vector loop stops: orbx_set_opencv_compat, oracle resize_tail_x).
 // xtab[dx] = {sx0 | sx1 << 16, a0 | a1 << 16}; ytab[dy] = {sy0 | sy1 << 16, b0 | b1 << 16}.
 // One workgroup = a 64 x 16 tile of level l (256 threads, 4 output pixels each).  The source
 // rectangle of level l-1 it needs is staged in LDS with dword loads; coefficients come from the
@@ -194,6 +198,17 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));   // packed u16 
 // quarter-rate v_mul_hi_u32).
 __device__ __forceinline__ uint32_t htap24(uint32_t h) { return h & 0xffff0u; }
 __device__ __forceinline__ uint32_t vcoef24(int b) { return ((uint32_t)b & 0xfffu) << 12; }
+// VResizeLinear's scalar loop, FixedPtCast<int, uchar, 22>: (S0*b0 + S1*b1 + 2^21) >> 22 on the full
+// horizontal sums (S < 2^20, b <= 2048: both products and the sum fit 32 bits); b24 = b << 12
+__device__ __forceinline__ uint32_t vtail(uint32_t h0, uint32_t h1, uint32_t b0_24, uint32_t b1_24) {
+    return (__umul24(h0, b0_24 >> 12) + __umul24(h1, b1_24 >> 12) + (1u << 21)) >> 22;
+}
+
+// two u8 taps of the 8-byte window (hi:lo) picked by a v_perm selector, as a packed u16 pair
+__device__ __forceinline__ us2 pyr_tap(uint32_t hi, uint32_t lo, uint32_t sel) {
+    const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
+    return *reinterpret_cast<const us2*>(&r);
+}
 
 constexpr int PYR_TW = 64, PYR_TH = 64;
 constexpr int PYR_SW = 144, PYR_SH = 128;   // LDS source tile capacity (scale factor <= ~1.9)
@@ -241,38 +256,46 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
         if (!__syncthreads_or(!fits)) {   // block-uniform: every thread's taps fit its 8-byte windows
             if (q0 >= tw) return;   // after the block-wide vote: no barrier follows
             const bool full = q0 + 3 < tw;
-            auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
-                const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
-                return *reinterpret_cast<const us2*>(&r);
-            };
             uint8_t* dst = pyr + (long long)f * g.pyr_frame_bytes + L.off + tx0 + q0 +
                            (long long)(ty0 + (int)(threadIdx.x >> 4)) * L.stride;
             const long long dstep = 16ll * L.stride;
-            for (int ty = threadIdx.x >> 4; ty < th; ty += 16, dst += dstep) {
-                const int4 yv = ys_t[ty];
-                // (the masks only tell the compiler b << 12 fits 24 bits: v_mul_hi_u32_u24, not v_mul_hi_u32)
-                const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;
-                uint32_t out = 0;
+            // this thread's first column in the scalar tail (<= 0: all four, >= 4: none); the tail
+            // loop is a separate instantiation, so columns left of tail_x run the plain loop
+            const int tcol = L.tail_x - (tx0 + q0);
+            auto rows = [&](auto tail_c) {
+                constexpr bool TAIL = decltype(tail_c)::value;
+                for (int ty = threadIdx.x >> 4; ty < th; ty += 16, dst += dstep) {
+                    const int4 yv = ys_t[ty];
+                    // (the masks only tell the compiler b << 12 fits 24 bits: v_mul_hi_u32_u24, not v_mul_hi_u32)
+                    const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;
+                    uint32_t out = 0;
 #pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    const uint32_t* s0 = reinterpret_cast<const uint32_t*>(S + yv.x + wdb[j]);
-                    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(S + yv.y + wdb[j]);
-                    const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
-                    const uint32_t h0a = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel0[j]), a0[j], 0u, false));
-                    const uint32_t h1a = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel0[j]), a0[j], 0u, false));
-                    const uint32_t h0b = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel1[j]), a1[j], 0u, false));
-                    const uint32_t h1b = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel1[j]), a1[j], 0u, false));
-                    const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
-                    const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
-                    out |= (va | (vb << 8)) << (16 * j);
+                    for (int j = 0; j < 2; j++) {
+                        const uint32_t* s0 = reinterpret_cast<const uint32_t*>(S + yv.x + wdb[j]);
+                        const uint32_t* s1 = reinterpret_cast<const uint32_t*>(S + yv.y + wdb[j]);
+                        const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
+                        const uint32_t r0a = __builtin_amdgcn_udot2(pyr_tap(w01, w00, sel0[j]), a0[j], 0u, false);
+                        const uint32_t r1a = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel0[j]), a0[j], 0u, false);
+                        const uint32_t r0b = __builtin_amdgcn_udot2(pyr_tap(w01, w00, sel1[j]), a1[j], 0u, false);
+                        const uint32_t r1b = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel1[j]), a1[j], 0u, false);
+                        uint32_t va = (__umulhi(htap24(r0a), b0) + __umulhi(htap24(r1a), b1) + 2) >> 2;
+                        uint32_t vb = (__umulhi(htap24(r0b), b0) + __umulhi(htap24(r1b), b1) + 2) >> 2;
+                        if (TAIL) {
+                            va = 2 * j >= tcol ? vtail(r0a, r1a, b0, b1) : va;
+                            vb = 2 * j + 1 >= tcol ? vtail(r0b, r1b, b0, b1) : vb;
+                        }
+                        out |= (va | (vb << 8)) << (16 * j);
+                    }
+                    if (full) {
+                        *reinterpret_cast<uint32_t*>(dst) = out;   // tx0 + q0 and the row stride: multiples of 4
+                    } else {
+                        for (int k = 0; k < 3; k++)
+                            if (q0 + k < tw) dst[k] = (uint8_t)(out >> (8 * k));
+                    }
                 }
-                if (full) {
-                    *reinterpret_cast<uint32_t*>(dst) = out;   // tx0 + q0 and the row stride: multiples of 4
-                } else {
-                    for (int k = 0; k < 3; k++)
-                        if (q0 + k < tw) dst[k] = (uint8_t)(out >> (8 * k));
-                }
-            }
+            };
+            if (tcol < 4) rows(std::true_type{});
+            else rows(std::false_type{});
             return;
         }
     }
@@ -295,7 +318,8 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
             const int h0 = S[r0 + sx0] * a0 + S[r0 + sx1] * a1;
             const int h1 = S[r1 + sx0] * a0 + S[r1 + sx1] * a1;
             const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
-            const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+            int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+            if (tx0 + q0 + k >= L.tail_x) v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
             packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
         }
         uint8_t* dst = dbase + (long long)(ty0 + ty) * L.stride;
@@ -476,14 +500,15 @@ __global__ __launch_bounds__(256) void pyramid_level_kernel(Geom g, int l, const
 constexpr int PP_MAXP = 8;   // level-l row passes per thread
 constexpr int PP_MAXC = 96, PP_MAXR = 96;   // level-l rectangle columns / rows the tables hold
 
-__device__ __forceinline__ uint32_t pyr_px_generic(const uint8_t* S, int2 xv, int4 yv, int xa) {
+__device__ __forceinline__ uint32_t pyr_px_generic(const uint8_t* S, int2 xv, int4 yv, int xa, bool tail) {
     const int r0 = yv.x, r1 = yv.y;
     const int sx0 = (xv.x & 0xffff) - xa, sx1 = (xv.x >> 16) - xa, a0 = xv.y & 0xffff, a1 = xv.y >> 16;
     const int b0 = yv.z >> 12, b1 = yv.w >> 12;
     const int h0 = S[r0 + sx0] * a0 + S[r0 + sx1] * a1;
     const int h1 = S[r1 + sx0] * a0 + S[r1 + sx1] * a1;
     const int s0 = min(h0 >> 4, 32767), s1 = min(h1 >> 4, 32767);
-    const int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+    int v = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2;
+    if (tail) v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
     return (uint32_t)(v > 255 ? 255 : v);
 }
 
@@ -562,36 +587,43 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
             a0[j] = *reinterpret_cast<const us2*>(&xv0.y);
             a1[j] = *reinterpret_cast<const us2*>(&xv1.y);
         }
-        auto tap = [](uint32_t hi, uint32_t lo, uint32_t sel) {
-            const uint32_t r = __builtin_amdgcn_perm(hi, lo, sel);
-            return *reinterpret_cast<const us2*>(&r);
-        };
+        // this thread's first level-l column in the scalar tail (<= 0: all four, >= 4: none)
+        const int tcol = L1.tail_x - (c0 + 4 * q);
+        auto rows = [&](auto tail_c) {
+            constexpr bool TAIL = decltype(tail_c)::value;
 #pragma unroll
-        for (int pp = 0; pp < PP_MAXP; pp++) {
-            const int r = r0 + pp * rpp;
-            out[pp] = 0;
-            if (r >= nrow) break;
-            const int4 yv = ys1[r];
-            if (fits) {
-                const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;   // 24-bit: see above
+            for (int pp = 0; pp < PP_MAXP; pp++) {
+                const int r = r0 + pp * rpp;
+                out[pp] = 0;
+                if (r >= nrow) break;
+                const int4 yv = ys1[r];
+                if (fits) {
+                    const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;   // 24-bit: see above
 #pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    const uint32_t* s0 = reinterpret_cast<const uint32_t*>(S + yv.x + 4 * (int)wdv[j]);
-                    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(S + yv.y + 4 * (int)wdv[j]);
-                    const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
-                    const uint32_t h0a = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel0[j]), a0[j], 0u, false));
-                    const uint32_t h1a = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel0[j]), a0[j], 0u, false));
-                    const uint32_t h0b = htap24(__builtin_amdgcn_udot2(tap(w01, w00, sel1[j]), a1[j], 0u, false));
-                    const uint32_t h1b = htap24(__builtin_amdgcn_udot2(tap(w11, w10, sel1[j]), a1[j], 0u, false));
-                    const uint32_t va = (__umulhi(h0a, b0) + __umulhi(h1a, b1) + 2) >> 2;
-                    const uint32_t vb = (__umulhi(h0b, b0) + __umulhi(h1b, b1) + 2) >> 2;
-                    out[pp] |= (va | (vb << 8)) << (16 * j);
+                    for (int j = 0; j < 2; j++) {
+                        const uint32_t* s0 = reinterpret_cast<const uint32_t*>(S + yv.x + 4 * (int)wdv[j]);
+                        const uint32_t* s1 = reinterpret_cast<const uint32_t*>(S + yv.y + 4 * (int)wdv[j]);
+                        const uint32_t w00 = s0[0], w01 = s0[1], w10 = s1[0], w11 = s1[1];
+                        const uint32_t r0a = __builtin_amdgcn_udot2(pyr_tap(w01, w00, sel0[j]), a0[j], 0u, false);
+                        const uint32_t r1a = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel0[j]), a0[j], 0u, false);
+                        const uint32_t r0b = __builtin_amdgcn_udot2(pyr_tap(w01, w00, sel1[j]), a1[j], 0u, false);
+                        const uint32_t r1b = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel1[j]), a1[j], 0u, false);
+                        uint32_t va = (__umulhi(htap24(r0a), b0) + __umulhi(htap24(r1a), b1) + 2) >> 2;
+                        uint32_t vb = (__umulhi(htap24(r0b), b0) + __umulhi(htap24(r1b), b1) + 2) >> 2;
+                        if (TAIL) {
+                            va = 2 * j >= tcol ? vtail(r0a, r1a, b0, b1) : va;
+                            vb = 2 * j + 1 >= tcol ? vtail(r0b, r1b, b0, b1) : vb;
+                        }
+                        out[pp] |= (va | (vb << 8)) << (16 * j);
+                    }
+                } else {   // taps outside the 8-byte windows (not at the supported scale factors)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) out[pp] |= pyr_px_generic(S, xv[k], yv, T.xa, k >= tcol) << (8 * k);
                 }
-            } else {   // taps outside the 8-byte windows (not at the supported scale factors)
-#pragma unroll
-                for (int k = 0; k < 4; k++) out[pp] |= pyr_px_generic(S, xv[k], yv, T.xa) << (8 * k);
             }
-        }
+        };
+        if (tcol < 4) rows(std::true_type{});
+        else rows(std::false_type{});
     }
     __syncthreads();   // every read of the level-(l-1) rectangle done: S now takes the level-l one
     if (act) {
@@ -2217,6 +2249,8 @@ static_assert(HCS % 4 == 0 && HCS >= 48, "8-byte aligned columns of 48 rows (the
 constexpr int HB_ELEMS = DESC_HBT ? 40 * HCS : 48 * HBS;
 
 // One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
+// TRIG: ComputeOrbDescriptor's cos / sin (:107): 0 = (float)::cos((double)angle), 1 = cosf / sinf.
+template <int TRIG>
 __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
                                                       int in_step, const uint8_t* __restrict__ pyr,
                                                       const uint32_t* __restrict__ sel,
@@ -2501,9 +2535,10 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 
     const float factorPI = (float)(M_PI / 180.f);
     const float ang = angle * factorPI;
-    float a, b;   // (float)::cos / ::sin((double)ang), sincos_f.h (checked on every float in range)
+    float a, b;   // (float)::cos / ::sin((double)ang) or cosf / sinf, sincos_f.h (each checked on every float in range)
     DESC_STAMP(3);
-    sincos_f2d(ang, &b, &a);
+    if (TRIG) sincosf_glibc(ang, &b, &a);
+    else sincos_f2d(ang, &b, &a);
     DESC_STAMP(4);
     auto sample = [&](float x, float y) -> int {
         // byte offset of blurred pixel (18 + dy, 18 + dx) from the rounded floats (exact integers)
@@ -2610,6 +2645,9 @@ struct orbx_extractor {
     int debug_nc = 0;
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
     int pyr_pair = 2;   // pyramid_pair_kernel for levels (1,2), (3,4), (5,6) (level 0 16-byte aligned); 1: (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
+    // OpenCV-build switches (orbx_set_opencv_compat; ORBX_TRIG / ORBX_RESIZE_TAIL)
+    int trig_float = 0;    // ComputeOrbDescriptor's cos / sin: 0 ::cos(double), 1 cosf / sinf
+    int resize_simd = 16;  // the resize's vector width V: scalar tail after the SIMD loop (0: none, 1: all scalar)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
     // level-split overlap (launch_chunk): level 0's FAST + quadtree on a side stream.  Off by
@@ -2638,6 +2676,19 @@ struct orbx_extractor {
     size_t last_step = 0;
     int last_frames = 0;
 };
+
+// First column VResizeLinear computes with its scalar loop in an OpenCV build whose universal
+// intrinsics are V bytes wide ([ext] imgproc/src/resize.cpp VResizeLinearVec_32s8u: `for (; x <= w -
+// V; x += V)` then `for (; x < w - V/2; x += V/2)`).  V = 0: the SIMD rounding everywhere; V = 1: a
+// build without SIMD, scalar everywhere.
+static int resize_tail_x(int w, int V) {
+    if (V <= 0) return w;
+    if (V == 1) return 0;
+    int x = 0;
+    for (; x <= w - V; x += V) {}
+    for (; x < w - V / 2; x += V / 2) {}
+    return x;
+}
 
 static int cv_round_d(double v) { return (int)std::lrint(v); }
 static int cv_round_f(float v) { return (int)std::lrintf(v); }
@@ -2682,7 +2733,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     for (int l = 0; l < Lc; l++) {
         LevelDev& L = g.lv[l];
         if (l == 0) {
-            L.w = cols; L.h = rows; L.stride = cols; L.off = -1;
+            L.w = cols; L.h = rows; L.stride = cols; L.off = -1; L.tail_x = cols;
         } else {
             L.h = cv_round_f(h->inv_scale[l] * rows);
             L.w = cv_round_f(h->inv_scale[l] * cols);
@@ -2700,6 +2751,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
             L.ytab_off = (long long)ytab.size();
             L.ssx = (double)sw / L.w;
             L.ssy = (double)sh / L.h;
+            L.tail_x = resize_tail_x(L.w, h->resize_simd);
             int xmax = dw;
             std::vector<int> sxs(dw), a0s(dw), a1s(dw);
             for (int dx = 0; dx < dw; dx++) {
@@ -3051,7 +3103,7 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         quadtree(0, g.nlevels, st);
     }
     {
-    launch_timed(h, 3, describe_kernel, dim3((unsigned)g.out_frame, (unsigned)F), dim3(64),
+    launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F), dim3(64),
                        0u, st, g,
                        d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
     }
@@ -3147,6 +3199,12 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     if (const char* e = getenv("ORBX_DEBUG_NC")) h->debug_nc = atoi(e);
+    // OpenCV-build switches (orbx_set_opencv_compat): ORBX_TRIG=double|float, ORBX_RESIZE_TAIL=V
+    if (const char* e = getenv("ORBX_TRIG")) h->trig_float = (e[0] == 'f' || e[0] == '1') ? 1 : 0;
+    if (const char* e = getenv("ORBX_RESIZE_TAIL")) {
+        const int v = atoi(e);
+        if (v == 0 || v == 1 || v == 8 || v == 16 || v == 32 || v == 64) h->resize_simd = v;
+    }
     compute_tables(h);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -3175,6 +3233,28 @@ int orbx_destroy(orbx_extractor* h) {
     if (h->lvl_fork) (void)hipEventDestroy(h->lvl_fork);
     if (h->lvl_join) (void)hipEventDestroy(h->lvl_join);
     delete h;
+    return ORB_OK;
+}
+
+int orbx_set_opencv_compat(orbx_extractor* h, int trig_mode, int resize_simd) {
+    ORB_CHECK_ARG(h, "null extractor");
+    ORB_CHECK_ARG(trig_mode >= -1 && trig_mode <= 1, "trig_mode must be -1 (keep), 0 (double) or 1 (float)");
+    ORB_CHECK_ARG(resize_simd == -1 || resize_simd == 0 || resize_simd == 1 || resize_simd == 8 || resize_simd == 16 ||
+                      resize_simd == 32 || resize_simd == 64,
+                  "resize_simd must be -1 (keep), 0, 1, 8, 16, 32 or 64");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (trig_mode >= 0) h->trig_float = trig_mode;
+    if (resize_simd >= 0 && resize_simd != h->resize_simd) {
+        h->resize_simd = resize_simd;
+        h->g_rows = h->g_cols = -1;   // the levels' tail columns change: rebuild the geometry
+    }
+    return ORB_OK;
+}
+
+int orbx_get_opencv_compat(const orbx_extractor* h, int* trig_mode, int* resize_simd) {
+    ORB_CHECK_ARG(h, "null extractor");
+    if (trig_mode) *trig_mode = h->trig_float;
+    if (resize_simd) *resize_simd = h->resize_simd;
     return ORB_OK;
 }
 

@@ -69,4 +69,60 @@ ORB_HD void sincos_f2d(float xf, float* s_out, float* c_out) {
     *c_out = (float)c;
 }
 
+// sinf / cosf of glibc >= 2.28 (the generic sysdeps/ieee754/flt-32 s_sinf.c / s_cosf.c, from ARM's
+// optimized-routines, and their FMA ifunc variants): what `cos(angle)` / `sin(angle)` compute when the
+// float overloads std::cos(float) / std::sin(float) are visible at ORBextractor.cc:107 (a `using
+// namespace std` or a libstdc++ <math.h> wrapper included anywhere before it).  For 0 <= x < 120:
+// n = round(x * 2/pi) via the 2^24-scaled integer path, r = x - n * pi/2 in double, then the
+// quadrant's double polynomial (sin: x + x^3 s1 + x^7 (s2 + x^2 s3); cos: c0 + x^2 c1 + x^4 c2 +
+// x^6 (c3 + x^2 c4)), negated cosine coefficients in quadrants 2 / 3.  Plain double ops: with or
+// without contraction the float results equal glibc's sinf / cosf on every float in [0, 6.2832]
+// (tests/native/sincos_check.cpp, mode f: 1,086,918,649 values, 0 mismatches either way).
+struct SincosfTab { double c0, c1, c2, c3, c4; };
+ORB_HD float sincosf_poly(double x, double x2, const SincosfTab& p, int n) {
+    const double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
+    if ((n & 1) == 0) {
+        const double x3 = x * x2;
+        const double t1 = s2 + x2 * s3;
+        const double x7 = x3 * x2;
+        const double s = x + x3 * s1;
+        return (float)(s + x7 * t1);
+    }
+    const double x4 = x2 * x2;
+    const double t2 = p.c3 + x2 * p.c4;
+    const double t1 = p.c0 + x2 * p.c1;
+    const double x6 = x4 * x2;
+    const double c = t1 + x4 * p.c2;
+    return (float)(c + x6 * t2);
+}
+
+ORB_HD void sincosf_glibc(float y, float* s_out, float* c_out) {
+    const SincosfTab pos = {0x1p0, -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10,
+                            0x1.99343027bf8c3p-16};
+    const SincosfTab neg = {-0x1p0, 0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10,
+                            -0x1.99343027bf8c3p-16};
+    double x = (double)y;
+    const unsigned top = (__builtin_bit_cast(unsigned, y) >> 20) & 0x7ffu;   // abstop12
+    if (top < 0x3f4u) {   // |y| < pi/4 (abstop12(0x1.921fb6p-1f))
+        if (top < 0x398u) {   // |y| < 2^-12
+            *s_out = y;
+            *c_out = 1.0f;
+            return;
+        }
+        const double x2 = x * x;
+        *s_out = sincosf_poly(x, x2, pos, 0);
+        *c_out = sincosf_poly(x, x2, pos, 1);
+        return;
+    }
+    // reduce_fast (!TOINT_INTRINSICS): r = x * (2/pi * 2^24), n = ((int)r + 2^23) >> 24
+    const double r = x * 0x1.45F306DC9C883p+23;
+    const int n = ((int)r + 0x800000) >> 24;
+    x = x - (double)n * 0x1.921FB54442D18p0;
+    const double sg = ((n + 1) & 2) ? -1.0 : 1.0;   // sign[n & 3] = {1, -1, -1, 1}
+    const SincosfTab& p = (n & 2) ? neg : pos;
+    const double xs = x * sg, x2 = x * x;
+    *s_out = sincosf_poly(xs, x2, p, n);
+    *c_out = sincosf_poly(xs, x2, p, n ^ 1);
+}
+
 }  // namespace orbamd

@@ -65,6 +65,22 @@ class ORBextractor:
     def FeaturesPerLevel(self):
         return self._quota.copy()
 
+    TRIG_MODES = {"double": 0, "float": 1}
+
+    def set_opencv_compat(self, trig=None, resize_simd=None):
+        """The OpenCV-build switches (include/orbslam2_amd.h orbx_set_opencv_compat): trig "double"
+        (::cos(double), default) or "float" (cosf / sinf) for ComputeOrbDescriptor's cos / sin
+        (src/ORBextractor.cc:107); resize_simd = the build's SIMD width V in bytes for cv::resize's
+        scalar tail (16 default; 0 = SIMD rounding everywhere, 1 = scalar everywhere).  None keeps."""
+        t = -1 if trig is None else self.TRIG_MODES[trig] if isinstance(trig, str) else int(trig)
+        v = -1 if resize_simd is None else int(resize_simd)
+        check(lib().orbx_set_opencv_compat(self._h, t, v), "orbx_set_opencv_compat")
+
+    def get_opencv_compat(self):
+        t, v = C.c_int(0), C.c_int(0)
+        check(lib().orbx_get_opencv_compat(self._h, C.byref(t), C.byref(v)), "orbx_get_opencv_compat")
+        return ("double", "float")[t.value], v.value
+
     def max_keypoints(self, rows, cols):
         cap = C.c_int32(0)
         check(lib().orbx_max_keypoints(self._h, rows, cols, C.byref(cap)), "orbx_max_keypoints")

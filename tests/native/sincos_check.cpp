@@ -1,5 +1,7 @@
-// Compares orbamd::sincos_f2d against glibc (float)sin / (float)cos of (double)x for every float x
-// in [lo, hi) (default [0, 6.2832]), split over threads.  Build: g++ -O2 -ffp-contract=off -pthread.
+// Compares orbamd::sincos_f2d against glibc (float)sin / (float)cos of (double)x (mode d, default) or
+// orbamd::sincosf_glibc against glibc sinf / cosf (mode f) for every float x in [lo, hi) (default
+// [0, 6.2832]), split over threads.  Build: g++ -O2 -ffp-contract=off -pthread.
+// Usage: sincos_check [threads] [step] [d|f]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -14,6 +16,7 @@ int main(int argc, char** argv) {
     float lo = 0.f, hi = 6.2832f;
     int nt = argc > 1 ? atoi(argv[1]) : 8;
     unsigned step = argc > 2 ? (unsigned)atoi(argv[2]) : 1;   // test every step-th float
+    const bool fmode = argc > 3 && argv[3][0] == 'f';
     unsigned a, b;
     memcpy(&a, &lo, 4);
     memcpy(&b, &hi, 4);
@@ -26,8 +29,16 @@ int main(int argc, char** argv) {
                 float x;
                 memcpy(&x, &u, 4);
                 float s, c;
-                orbamd::sincos_f2d(x, &s, &c);
-                const float rs = (float)::sin((double)x), rc = (float)::cos((double)x);
+                float rs, rc;
+                if (fmode) {
+                    orbamd::sincosf_glibc(x, &s, &c);
+                    rs = ::sinf(x);
+                    rc = ::cosf(x);
+                } else {
+                    orbamd::sincos_f2d(x, &s, &c);
+                    rs = (float)::sin((double)x);
+                    rc = (float)::cos((double)x);
+                }
                 if (memcmp(&s, &rs, 4) || memcmp(&c, &rc, 4)) {
                     if (nb < 5) printf("mismatch x=%.9g (0x%08x): s %.9g vs %.9g, c %.9g vs %.9g\n", x, u, s, rs, c, rc);
                     nb++;

@@ -65,6 +65,32 @@ def lib():
     return _lib
 
 
+def set_compat(trig=None, resize_simd=None):
+    """The oracle's OpenCV-build switches (process-wide; oracle_set_compat): trig "double" / "float",
+    resize_simd V.  None keeps a switch.  Returns the previous (trig, resize_simd)."""
+    t = -1 if trig is None else {"double": 0, "float": 1}[trig] if isinstance(trig, str) else int(trig)
+    v = -1 if resize_simd is None else int(resize_simd)
+    prev = lib().oracle_set_compat(t, v)
+    return ("double", "float")[prev & 0xff], prev >> 8
+
+
+class compat:
+    """Context manager: oracle switches set for the block, restored after."""
+    def __init__(self, trig=None, resize_simd=None):
+        self.args = (trig, resize_simd)
+
+    def __enter__(self):
+        self.prev = set_compat(*self.args)
+        return self
+
+    def __exit__(self, *exc):
+        set_compat(*self.prev)
+
+
+def resize_tail_x(w, resize_simd):
+    return lib().oracle_resize_tail_x(int(w), int(resize_simd))
+
+
 def ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 

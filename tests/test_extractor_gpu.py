@@ -177,7 +177,9 @@ def test_extract_c1_golden(seed):
     g = np.load(GOLDEN / f"extract_c1_seed{seed}.npz")
     img = synth_image(int(g["seed"]), int(g["width"]), int(g["height"]))
     assert np.array_equal(img, g["image"]), "synthetic generator changed"
-    kps, desc = make(int(g["nfeatures"])).Extract(img)
+    ex = make(int(g["nfeatures"]))
+    ex.set_opencv_compat(str(g["trig"]), int(g["resize_simd"]))   # the switches the fixture was made with
+    kps, desc = ex.Extract(img)
     okps = g["kps"].astype(np.int32).view(kps.dtype).reshape(-1)
     assert_same_kps(kps, okps, desc, g["desc"])
 

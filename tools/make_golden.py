@@ -37,11 +37,13 @@ def main(only=None):
         pose_opt()
         return
     pose_opt()
+    trig, simd = O.set_compat()   # the OpenCV-build switches the fixtures were made with (defaults)
     for seed in range(4):
         img = synth_image(seed, 640, 480)
         kps, desc, per = O.extract(O.params(1000), img)
         np.savez_compressed(OUT / f"extract_c1_seed{seed}.npz", seed=seed, width=640, height=480, nfeatures=1000,
-                            image=img, kps=kps.view(np.int32).reshape(-1, 7), desc=desc, per_level=per)
+                            image=img, kps=kps.view(np.int32).reshape(-1, 7), desc=desc, per_level=per,
+                            trig=trig, resize_simd=simd)
     # matcher: descriptors of two C1 frames
     d0 = np.load(OUT / "extract_c1_seed0.npz")["desc"]
     d1 = np.load(OUT / "extract_c1_seed1.npz")["desc"]
