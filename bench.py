@@ -318,7 +318,7 @@ def c2_textured_leg(dev, local, frames=1024, cpu=True, info=None):
     return r
 
 
-def c2_1000_leg(dev, local, frames=1024):
+def c2_1000_leg(dev, local, frames=1024, cpu=True, info=None):
     """The metric string's feature count: C2's pan sequence at 1000 features (the headline line runs
     configs[1] at 2000, the larger configuration)."""
     from orb_slam2_refactored_amd.synth import pan_sequence
@@ -326,6 +326,11 @@ def c2_1000_leg(dev, local, frames=1024):
     r = {"workload": "C2 pan sequence at 1000 features (the metric's feature count), 1280x720, 8 levels, "
                      "extract + match vs previous frame"}
     r.update(extract_match_gpu_leg(dev, local, seq, 1000, reps=frames))
+    if cpu:
+        r["cpu_baseline"] = cpu_baseline_block("frames/s", "1280x720 pan-sequence frames at 1000 features, "
+                                               "extract + match vs previous",
+                                               cpu_extract_match(seq[:4], 1000, 1, 4.0),
+                                               cpu_extract_match(seq[:8], 1000, info["threads_all"], 4.0), info)
     return r
 
 
@@ -853,17 +858,41 @@ class Ranks:
             dist.destroy_process_group()
 
 
+def count_gpus_kfd() -> int:
+    """GPUs visible to this process, counted from the KFD topology in sysfs (a node with SIMDs is a GPU),
+    restricted by HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set.  No HIP
+    or torch call: the launcher never initialises the GPU runtime before it starts the rank processes."""
+    n = 0
+    nodes = Path("/sys/class/kfd/kfd/topology/nodes")
+    try:
+        for d in nodes.iterdir():
+            try:
+                props = (d / "properties").read_text()
+            except OSError:
+                continue
+            for line in props.splitlines():
+                k, _, v = line.partition(" ")
+                if k == "simd_count" and int(v or 0) > 0:
+                    n += 1
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        vis = os.environ.get(var)
+        if vis is not None:
+            n = min(n, len([x for x in vis.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(args) -> int:
-    """`bench.py --gpus N` without a launcher: start N fresh rank processes (this process never touches
-    the GPU: it only counts devices, which does not initialise HIP, and starts children rather than
-    exec'ing), rank 0's stdout is the JSON line.  The driver's own form -- torch.distributed.run setting
-    WORLD_SIZE / RANK / LOCAL_RANK -- runs the same rank code directly."""
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes, rank 0's stdout is the JSON line.
+    This process never touches the GPU runtime: it counts GPUs from sysfs (count_gpus_kfd, no HIP / torch
+    call) and starts children rather than exec'ing.  The driver's own form -- torch.distributed.run
+    setting WORLD_SIZE / RANK / LOCAL_RANK -- runs the same rank code directly."""
     import socket
     import subprocess
     n = args.gpus
     if not args.stub:
-        import torch
-        have = torch.cuda.device_count()
+        have = count_gpus_kfd()
         if have < n:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
             return 2
@@ -1035,7 +1064,7 @@ class ShardedRun:
                 "cross_matches_run_all_ranks": int(self.ranks.sum(float(self.cross)))}
 
 
-def c5_leg(ranks, ex, m, base, total=1024, steps=20, warmup=3):
+def c5_leg(ranks, ex, m, base, total=1024, steps=20, warmup=3, nfeat=2000):
     """configs[4]: 1024 independent 1280x720 frames per step in total, sharded over the N ranks (1024/N per
     rank: the fixed-size job of C5, i.e. strong scaling), extract + match vs predecessor + the counts /
     descriptor all-gather and the cross-shard predecessor match.  Runs on every rank (collectives); at N = 1
@@ -1045,12 +1074,23 @@ def c5_leg(ranks, ex, m, base, total=1024, steps=20, warmup=3):
     B = total // ranks.world
     run = ShardedRun(ranks, ex, m, base, B, exchange=True)
     elapsed, _ = run.timed(steps, warmup)
-    out = {"workload": f"C5 (configs[4]): {total} 1280x720 frames per step in total, {B} per rank on "
+    H, W = base.shape[1:]
+    ms = 1e3 * elapsed / steps
+    # the extractor's algorithmic bytes (SURVEY §8d B_ext) of all ranks' frames over the whole step, against
+    # N x the per-GPU HBM peak: the north star's "fraction of HBM roofline" at this N
+    n_kp = ranks.sum(float(run.slots().counts.float().sum().item())) / total
+    bytes_frame, _ = algorithmic_bytes(W, H, n_kp)
+    gbs = bytes_frame * total / (ms * 1e-3) / 1e9
+    out = {"workload": f"C5 (configs[4]): {total} {W}x{H} frames per step in total, {B} per rank on "
                        f"{ranks.world} rank(s), extract + match vs predecessor, RCCL counts + descriptor "
                        "all-gather, cross-shard predecessor match",
            "frames_per_step": total, "frames_per_rank": B, "n_ranks": ranks.world, "scaling": "strong",
            "steps": steps, "warmup": warmup, "frames_per_s": total * steps / elapsed,
-           "ms_per_step": 1e3 * elapsed / steps}
+           "ms_per_step": ms, "keypoints_per_frame": n_kp, "keypoint_quota": nfeat,
+           "hbm_frac": gbs / (HBM_PEAK_GBS * ranks.world),
+           "hbm": {"algorithmic_bytes_per_frame": bytes_frame, "GBs_all_ranks": gbs,
+                   "peak_GBs_all_ranks": HBM_PEAK_GBS * ranks.world,
+                   "note": "extractor algorithmic bytes (SURVEY §8d B_ext) x frames / ms_per_step over N x peak"}}
     out.update(run.exchange_block(steps))
     return out
 
@@ -1195,6 +1235,8 @@ def main():
                            "ops": "512 FP4 flops per query x candidate pair, n_kp^2 pairs per matched frame (B - 1 per step)",
                            "match_ms_per_step": match_ms},
         "keypoints_per_frame": n_kp,
+        "keypoint_quota": args.nfeatures,
+        "keypoints_over_quota": n_kp / args.nfeatures if args.nfeatures else None,
         "matches_last_step": matches,
         "device_fault_mask": run.fault,
         "timed_region_s": elapsed,
@@ -1206,7 +1248,8 @@ def main():
                                   workload="the headline's exchange (weak scaling, frames_per_step_per_gpu per rank)")
     # C5 (configs[4]) on every rank: it has collectives, so it runs before the rank-0-only legs
     if not args.no_c5:
-        result["c5"] = c5_leg(ranks, ex, m, base, total=args.c5_frames)
+        result["c5"] = c5_leg(ranks, ex, m, base, total=args.c5_frames, steps=args.steps, warmup=args.warmup,
+                              nfeat=args.nfeatures)
 
     legs = rank == 0 and not args.no_legs and not args.stub
     cpu = world == 1 and not args.no_cpu_baseline and rank == 0 and not args.stub
@@ -1222,7 +1265,7 @@ def main():
     if legs and not args.no_textured:
         result["c2_textured"] = c2_textured_leg(dev, local, cpu=cpu, info=info)
     if legs and not args.no_c1:
-        result["c2_1000"] = c2_1000_leg(dev, local)
+        result["c2_1000"] = c2_1000_leg(dev, local, cpu=cpu, info=info)
     if legs and not args.no_c3:
         result["c3"] = c3_leg(dev, local, cpu=cpu, info=info)
     if legs and not args.no_stereo:
@@ -1240,6 +1283,14 @@ def main():
             "frames/s", f"{W}x{H} pan-sequence frames, extract + brute-force match vs previous",
             cpu_extract_match(base[:4], args.nfeatures, 1, 8.0),
             cpu_extract_match(base[:8], args.nfeatures, info["threads_all"], 8.0), info)
+    # the headline's actual load next to it (inside config, which the driver's record keeps whole): the pan
+    # frames fill ~70 % of the quota; the full-quota textured frames run at about half the rate
+    result["config"]["load"] = {
+        "keypoints_per_frame": n_kp, "keypoint_quota": args.nfeatures,
+        "keypoints_over_quota": n_kp / args.nfeatures if args.nfeatures else None,
+        "c2_textured_frames_per_s": (result.get("c2_textured") or {}).get("frames_per_s"),
+        "c2_textured_keypoints_per_frame": (result.get("c2_textured") or {}).get("keypoints_per_frame"),
+        "c2_1000_frames_per_s": (result.get("c2_1000") or {}).get("frames_per_s")}
     # the metric's other halves, flat and last on the line (a record that keeps only the tail of stdout
     # still holds them)
     result["summary"] = summary(result)
@@ -1257,16 +1308,20 @@ def summary(r):
             v = v[p]
         return round(v, 4) if isinstance(v, float) else v
     return {"c2_frames_per_s": g("value"), "c2_ms_per_step": g("ms_per_step"), "n_gpus": g("n_gpus"),
+            "c2_keypoints_per_frame": g("keypoints_per_frame"), "c2_keypoint_quota": g("keypoint_quota"),
+            "c2_textured_keypoints_per_frame": g("c2_textured", "keypoints_per_frame"),
             "fast_cells_frac": g("roofline", "frac"), "fast_cells_ms": g("roofline", "avg_launch_ms"),
             "pipeline_traffic_over_algorithmic": g("roofline", "pipeline_traffic_over_algorithmic"),
             "localba_iters_per_s": g("localba", "iters_per_s"), "localba_ms_per_call": g("localba", "ms_per_call"),
             "localba_cpu_iters_per_s": g("localba", "cpu_baseline", "value"),
             "c1_frames_per_s": g("c1", "frames_per_s"), "c1_cpu_median_ms": g("c1", "cpu_baseline", "median_ms"),
             "c2_1000_frames_per_s": g("c2_1000", "frames_per_s"),
+            "c2_1000_cpu_frames_per_s": g("c2_1000", "cpu_baseline", "value"),
             "c2_textured_frames_per_s": g("c2_textured", "frames_per_s"),
             "c3_pairs_per_s": g("c3", "pairs_per_s"),
             "c5_frames_per_s": g("c5", "frames_per_s"), "c5_n_ranks": g("c5", "n_ranks"),
-            "c5_gather_ms": g("c5", "gather_ms_max_over_ranks"), "cpu_frames_per_s": g("cpu_baseline", "value")}
+            "c5_gather_ms": g("c5", "gather_ms_max_over_ranks"), "c5_hbm_frac": g("c5", "hbm_frac"),
+            "cpu_frames_per_s": g("cpu_baseline", "value")}
 
 
 if __name__ == "__main__":

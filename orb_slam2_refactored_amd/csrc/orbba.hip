@@ -1342,10 +1342,14 @@ __device__ bool ba_decide_step(const BADev& b, BACtl* host_snap, int seq, double
 }
 
 // The control snapshot into pinned host memory: the body as relaxed system-scope stores (write-through
-// to the host, no L2 writeback of the device's other data), then the sequence id the host polls for as a
-// system-scope RELEASE store, so the host's acquire load of `seq` (the host ring poll in orbba_local_ba) orders every
-// body word before it by the memory model, not by the gfx9 rule that vmcnt(0) retires earlier stores
-// (What's weak 8).  ORBBA_SNAP_RELEASE=0 builds the round-3 form for A/B only.
+// to the host), then the sequence id the host polls for as a system-scope RELEASE store, so the host's
+// acquire load of `seq` (the host ring poll in orbba_local_ba) orders every body word before it by the
+// memory model, not by the gfx9 rule that vmcnt(0) retires earlier stores (What's weak 8).
+// Cost: on gfx950 the release compiles to `buffer_wbl2 sc0 sc1; s_waitcnt vmcnt(0)` before the seq store,
+// i.e. a write-back of the whole L2 on every snapshot (once per LM trial, from one thread).  Measured
+// against the relaxed form (ORBBA_SNAP_RELEASE=0, tools/ab_build.sh), alternating on one box, 40 calls
+// each: 9.27-9.33k vs 8.98-9.31k LM iterations/s -- no cost above the noise, since the L2 holds little
+// dirty data between the solve kernels.  ORBBA_SNAP_RELEASE=0 builds the round-3 form for A/B only.
 #ifndef ORBBA_SNAP_RELEASE
 #define ORBBA_SNAP_RELEASE 1
 #endif

@@ -46,8 +46,12 @@ def test_launcher_starts_n_ranks_stub():
     assert x["gather_bytes_per_step"] > 0
     c5 = r["c5"]
     assert c5["n_ranks"] == 2 and c5["frames_per_rank"] == 8 and c5["frames_per_step"] == 16
-    # each of warmup + steps matched exactly once on rank 1 (no duplicate match of the warm-up's last step)
-    assert c5["cross_matches_run_all_ranks"] == 3 + 20
+    # each of warmup + steps (C5 takes --steps / --warmup) matched exactly once on rank 1 (no duplicate match
+    # of the warm-up's last step)
+    assert c5["cross_matches_run_all_ranks"] == 1 + 3
+    assert c5["steps"] == 3 and c5["warmup"] == 1
+    assert 0 < c5["hbm_frac"] < 1 and c5["keypoint_quota"] == 2000
+    assert r["config"]["load"]["keypoint_quota"] == 2000
     assert r["summary"]["n_gpus"] == 2 and r["summary"]["c5_n_ranks"] == 2
 
 
@@ -59,9 +63,20 @@ def test_launcher_single_rank_stub_has_c5():
     assert r["c5"]["n_ranks"] == 1 and r["c5"]["frames_per_rank"] == 8 and r["c5"]["cross_matches_run"] == 0
 
 
+def test_count_gpus_kfd_without_hip(monkeypatch):
+    """The launcher counts GPUs from sysfs, never through torch / HIP (a parent that initialised HIP and then
+    started the ranks is what this pool forbids); visibility variables cap the count."""
+    n = bench.count_gpus_kfd()
+    assert n >= 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.count_gpus_kfd() == 0
+    src = (ROOT / "bench.py").read_text()
+    body = src[src.index("def launch_ranks"):src.index("# ----", src.index("def launch_ranks"))]
+    assert "import torch" not in body and "device_count(" not in body and "hipGetDeviceCount" not in body
+
+
 def test_gpus_without_devices_fails_loudly():
-    import torch
-    if torch.cuda.device_count() >= 2:
+    if bench.count_gpus_kfd() >= 2:
         pytest.skip("GPUs present")
     p = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"], _env(), timeout=120)
     assert p.returncode == 2

@@ -73,3 +73,38 @@ def test_pack_descriptors_clamps_counts_and_output():
     assert (got[6:11] == 0xA5).all()                        # the rows frame 1 claimed beyond cap: untouched
     assert torch.equal(got[11:12], desc[2, :1])             # frame 2 clipped at out_rows
     assert (got[12] == 0xA5).all()                          # the guard row after out_rows: untouched
+
+
+@pytest.mark.parametrize("frames,cap,seed", [(1, 1, 0), (5, 3, 1), (33, 64, 2), (128, 2024, 3)])
+def test_pack_descriptors_kernel_matches_gloo_pack(frames, cap, seed):
+    """the device kernel behind orbx_pack_descriptors against the gloo (CPU) path's own pack
+    (shard.CompactExchange's repeat_interleave / index_select block) on ragged layouts, counts of 0 and of
+    the full slot capacity included."""
+    from orb_slam2_refactored_amd.shard import CompactExchange
+    g = torch.Generator().manual_seed(seed)
+    counts = torch.randint(0, cap + 1, (frames,), generator=g, dtype=torch.int32)
+    counts[0] = 0
+    counts[-1] = cap
+    if frames > 2:
+        counts[1] = cap
+        counts[2] = 0
+    desc = torch.randint(0, 256, (frames, cap, 32), generator=g, dtype=torch.uint8)
+    cpu = CompactExchange(frames, cap, "cpu")   # world 1, no process group: the gloo path's pack, run locally
+    loc = cpu.local(0)
+    loc.desc.copy_(desc)
+    loc.counts.copy_(counts)
+    cpu.publish(0)
+    cpu.drain()
+    want = cpu.block(0, 0)
+    assert torch.equal(want, torch.cat([desc[f, :int(counts[f])] for f in range(frames)]))
+    total = int(counts.sum())
+    incl = torch.cumsum(counts, 0, dtype=torch.int32)
+    out = torch.full((total + 1, 32), 0x5A, dtype=torch.uint8, device="cuda")
+    d_desc, d_counts, d_incl = desc.cuda(), counts.cuda(), incl.cuda()
+    _lib.check(_lib.lib().orbx_pack_descriptors(_lib.tptr(d_desc), cap, _lib.tptr(d_counts), _lib.tptr(d_incl),
+                                                frames, _lib.tptr(out), total, _lib.stream_ptr()),
+               "orbx_pack_descriptors")
+    torch.cuda.synchronize()
+    got = out.cpu()
+    assert torch.equal(got[:total], want)
+    assert (got[total] == 0x5A).all()
