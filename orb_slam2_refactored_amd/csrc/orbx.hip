@@ -2248,78 +2248,16 @@ constexpr int HCS = 52;
 static_assert(HCS % 4 == 0 && HCS >= 48, "8-byte aligned columns of 48 rows (the tiles' slack rows)");
 constexpr int HB_ELEMS = DESC_HBT ? 40 * HCS : 48 * HBS;
 
-// One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
-// TRIG: ComputeOrbDescriptor's cos / sin (:107): 0 = (float)::cos((double)angle), 1 = cosf / sinf.
+// One kept keypoint (level l, selection word k, output row o of the frame's slots): the raw 43x43 patch,
+// IC_Angle, the 7x7 Q8 blur and the rBRIEF samples, written to kps / desc at row o.  One wavefront.
 template <int TRIG>
-__global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
-                                                      int in_step, const uint8_t* __restrict__ pyr,
-                                                      const uint32_t* __restrict__ sel,
-                                                      const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
-                                                      uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                      int cap) {
-    // the raw patch R is dead once every lane holds its row for the horizontal blur (one
-    // wavefront: its LDS reads complete before its later writes), so the blurred rows Hb reuse it
-    __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];   // 43 blurred rows + 5 rows of blur slack
-    uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
-    static_assert(47 * RS + 64 <= HB_ELEMS * 2, "R (and the blur's reads of rows 43..47) must fit in Hb");
+__device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, uint32_t k, long long o,
+                                                  const uint8_t* __restrict__ in, long long in_fstride, int in_step,
+                                                  const uint8_t* __restrict__ pyr, orbx_keypoint* __restrict__ kps,
+                                                  uint8_t* __restrict__ desc, uint16_t* Hb, int lb) {
     const int lane = threadIdx.x;
-    const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
-    DESC_STAMP(7);   // entry (diagnostic build): the preamble's loads are timed from here
-    const int f = divmod_of(g, lb);
-    const int s = lb - f * g.out_frame;   // selection slot (level-major, out_cap slots per level)
-    // The slot's level and the frame's per-level counts without a dependent chain of loads: the
-    // level is the number of level starts (kernarg) <= s; one vector load brings level q's kept
-    // count to lane q < nlevels and the slot's keypoint word to lane 63, and the level's output base
-    // is an inclusive row scan of the counts (nlevels <= 16: lanes 0-15).
-    const int nl = g.nlevels;
-#if DESC_SCALAR_PRE
-    // every address here is wave-uniform: scalar loads (the scalar cache path, not queued behind the
-    // other wavefronts' patch loads); 16 counts read unconditionally (the count buffer has 64 B of slack)
-    const uint32_t k = sel[(long long)f * g.out_frame + s];
-    const int* cf = sel_cnt + f * nl;
-    int cnt16[MAX_LEVELS];
-#pragma unroll
-    for (int q = 0; q < MAX_LEVELS; q++) cnt16[q] = cf[q];
-#else
-    const int* lp = lane < nl ? sel_cnt + f * nl + lane
-                              : reinterpret_cast<const int*>(sel + (long long)f * g.out_frame + s);
-    const int cw = (lane < nl || lane == 63) ? *lp : 0;
-    const int cq = lane < nl ? cw : 0;
-#endif
-    // levels >= nlevels carry 0x7fff (host; out_frame < 0x7fff checked there): a field x <= s iff bit
-    // 15 of (x | 0x8000) - (s + 1) is clear, and no field borrows from the next
-    int l = MAX_LEVELS;
-    {
-        const unsigned s1 = (unsigned)(s + 1) * 0x00010001u;
-#pragma unroll
-        for (int d = 0; d < MAX_LEVELS / 2; d++) l -= __popc(((g.lv_start[d] | 0x80008000u) - s1) & 0x80008000u);
-    }
-#if DESC_SCALAR_PRE
-    int total = 0, lbase = 0, cnt_l = 0;
-#pragma unroll
-    for (int q = 0; q < MAX_LEVELS; q++) {
-        const int cq = q < nl ? cnt16[q] : 0;
-        total += cq;
-        lbase += q < l ? cq : 0;
-        cnt_l = q == l ? cq : cnt_l;
-    }
-#else
-    int sc = cq;
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xf, 0xf, true);   // row_shr:1 (zero fill)
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);   // row_shr:2
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xf, 0xf, true);   // row_shr:4
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x118, 0xf, 0xf, true);   // row_shr:8
-    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane(cw, 63);
-    const int total = __builtin_amdgcn_readlane(sc, 15);
-    const int lbase = l > 0 ? __builtin_amdgcn_readlane(sc, l - 1) : 0;
-    const int cnt_l = __builtin_amdgcn_readlane(cq, l);
-#endif
+    uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
     const LevelDev& L = g.lv[l];
-    if (s == 0 && lane == 0) counts[f] = total;
-    const int i = s - L.out_base;
-    if (i >= cnt_l) return;   // slot past the level's kept count
-    const int oidx = lbase + i;   // output order: level-major list order
-    if (oidx >= cap) return;
     DESC_STAMP(0);
     // the blur's constant A fragments, in flight under the patch load
     i4v afr[3];
@@ -2586,7 +2524,6 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     DESC_STAMP(5);
     // The 32 descriptor bytes and the 7-word keypoint record are wave-uniform: v_writelane places
     // them in lanes 0..7 / 0..6 of one register each (no per-lane selects or branches), one store each.
-    const long long o = (long long)f * cap + oidx;
     uint32_t dv = 0, kv = 0;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -2604,6 +2541,80 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     if (lane < 8) reinterpret_cast<uint32_t*>(desc + o * 32)[lane] = dv;
     if (lane < 7) reinterpret_cast<uint32_t*>(kps + o)[lane] = kv;
     DESC_STAMP(6);
+}
+
+// One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
+// TRIG: ComputeOrbDescriptor's cos / sin (:107): 0 = (float)::cos((double)angle), 1 = cosf / sinf.
+template <int TRIG>
+__global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ in, long long in_fstride,
+                                                      int in_step, const uint8_t* __restrict__ pyr,
+                                                      const uint32_t* __restrict__ sel,
+                                                      const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
+                                                      uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
+                                                      int cap) {
+    // the raw patch R is dead once every lane holds its row for the horizontal blur (one
+    // wavefront: its LDS reads complete before its later writes), so the blurred rows Hb reuse it
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];   // 43 blurred rows + 5 rows of blur slack
+    static_assert(47 * RS + 64 <= HB_ELEMS * 2, "R (and the blur's reads of rows 43..47) must fit in Hb");
+    const int lane = threadIdx.x;
+    const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    DESC_STAMP(7);   // entry (diagnostic build): the preamble's loads are timed from here
+    const int f = divmod_of(g, lb);
+    const int s = lb - f * g.out_frame;   // selection slot (level-major, out_cap slots per level)
+    // The slot's level and the frame's per-level counts without a dependent chain of loads: the
+    // level is the number of level starts (kernarg) <= s; one vector load brings level q's kept
+    // count to lane q < nlevels and the slot's keypoint word to lane 63, and the level's output base
+    // is an inclusive row scan of the counts (nlevels <= 16: lanes 0-15).
+    const int nl = g.nlevels;
+#if DESC_SCALAR_PRE
+    // every address here is wave-uniform: scalar loads (the scalar cache path, not queued behind the
+    // other wavefronts' patch loads); 16 counts read unconditionally (the count buffer has 64 B of slack)
+    const uint32_t k = sel[(long long)f * g.out_frame + s];
+    const int* cf = sel_cnt + f * nl;
+    int cnt16[MAX_LEVELS];
+#pragma unroll
+    for (int q = 0; q < MAX_LEVELS; q++) cnt16[q] = cf[q];
+#else
+    const int* lp = lane < nl ? sel_cnt + f * nl + lane
+                              : reinterpret_cast<const int*>(sel + (long long)f * g.out_frame + s);
+    const int cw = (lane < nl || lane == 63) ? *lp : 0;
+    const int cq = lane < nl ? cw : 0;
+#endif
+    // levels >= nlevels carry 0x7fff (host; out_frame < 0x7fff checked there): a field x <= s iff bit
+    // 15 of (x | 0x8000) - (s + 1) is clear, and no field borrows from the next
+    int l = MAX_LEVELS;
+    {
+        const unsigned s1 = (unsigned)(s + 1) * 0x00010001u;
+#pragma unroll
+        for (int d = 0; d < MAX_LEVELS / 2; d++) l -= __popc(((g.lv_start[d] | 0x80008000u) - s1) & 0x80008000u);
+    }
+#if DESC_SCALAR_PRE
+    int total = 0, lbase = 0, cnt_l = 0;
+#pragma unroll
+    for (int q = 0; q < MAX_LEVELS; q++) {
+        const int cq = q < nl ? cnt16[q] : 0;
+        total += cq;
+        lbase += q < l ? cq : 0;
+        cnt_l = q == l ? cq : cnt_l;
+    }
+#else
+    int sc = cq;
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xf, 0xf, true);   // row_shr:1 (zero fill)
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);   // row_shr:2
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xf, 0xf, true);   // row_shr:4
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x118, 0xf, 0xf, true);   // row_shr:8
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane(cw, 63);
+    const int total = __builtin_amdgcn_readlane(sc, 15);
+    const int lbase = l > 0 ? __builtin_amdgcn_readlane(sc, l - 1) : 0;
+    const int cnt_l = __builtin_amdgcn_readlane(cq, l);
+#endif
+    const LevelDev& L = g.lv[l];
+    if (s == 0 && lane == 0) counts[f] = total;
+    const int i = s - L.out_base;
+    if (i >= cnt_l) return;   // slot past the level's kept count
+    const int oidx = lbase + i;   // output order: level-major list order
+    if (oidx >= cap) return;
+    describe_keypoint<TRIG>(g, l, f, k, (long long)f * cap + oidx, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
 }
 
 __global__ __launch_bounds__(256) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
