@@ -2250,19 +2250,34 @@ constexpr int HB_ELEMS = DESC_HBT ? 40 * HCS : 48 * HBS;
 
 // One kept keypoint (level l, selection word k, output row o of the frame's slots): the raw 43x43 patch,
 // IC_Angle, the 7x7 Q8 blur and the rBRIEF samples, written to kps / desc at row o.  One wavefront.
-template <int TRIG>
+// A pointer the compiler cannot see through (an empty asm on its SGPR pair): inside the persistent
+// kernel's loop the constant-table loads stay per keypoint instead of being hoisted out of the loop as
+// ~52 VGPRs of loop-invariant fragments (127 VGPRs, 4 wavefronts per SIMD).
+template <typename T>
+__device__ __forceinline__ const T* opaque_ptr(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+template <int TRIG, bool LOOP>
 __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, uint32_t k, long long o,
                                                   const uint8_t* __restrict__ in, long long in_fstride, int in_step,
                                                   const uint8_t* __restrict__ pyr, orbx_keypoint* __restrict__ kps,
                                                   uint8_t* __restrict__ desc, uint16_t* Hb, int lb) {
-    const int lane = threadIdx.x;
+    int lane = threadIdx.x;
+    // (in the loop, the lane id is opaque too: every lane-derived offset is rebuilt per keypoint, not held
+    // across the loop by LICM)
+    if (LOOP) asm volatile("" : "+v"(lane));
     uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
     const LevelDev& L = g.lv[l];
+    const HBlurA* hblur_a = LOOP ? opaque_ptr(&c_hblur_a) : &c_hblur_a;
+    const AngleA* angle_a = LOOP ? opaque_ptr(&c_angle_a) : &c_angle_a;
+    const float* pattern = LOOP ? opaque_ptr(c_pattern) : c_pattern;
     DESC_STAMP(0);
     // the blur's constant A fragments, in flight under the patch load
     i4v afr[3];
 #pragma unroll
-    for (int mt = 0; mt < 3; mt++) afr[mt] = *reinterpret_cast<const i4v*>(c_hblur_a.v[mt][lane]);
+    for (int mt = 0; mt < 3; mt++) afr[mt] = *reinterpret_cast<const i4v*>(hblur_a->v[mt][lane]);
 
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
     int step;
@@ -2399,8 +2414,8 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
         i4v au[3], av[3];
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-            au[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
-            av[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
+            au[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][0][lane]);
+            av[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][1][lane]);
         }
         angle_products(au, av);
     }
@@ -2454,15 +2469,15 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     // the lane's four pattern pairs, loaded before the angle / atan / sincos chain hides their latency
     float4 pat[4];
 #pragma unroll
-    for (int r = 0; r < 4; r++) pat[r] = reinterpret_cast<const float4*>(c_pattern)[r * 64 + lane];
+    for (int r = 0; r < 4; r++) pat[r] = reinterpret_cast<const float4*>(pattern)[r * 64 + lane];
 #endif
 #if DESC_ANGLE_MFMA && !DESC_ANGLE_FIRST
     {
         i4v au[3], av[3];
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-            au[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][0][lane]);
-            av[nt] = *reinterpret_cast<const i4v*>(c_angle_a.v[nt][1][lane]);
+            au[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][0][lane]);
+            av[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][1][lane]);
         }
         angle_products(au, av);
     }
@@ -2517,7 +2532,7 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
 #if DESC_PAT_EARLY
         const float4 q = pat[r];
 #else
-        const float4 q = reinterpret_cast<const float4*>(c_pattern)[r * 64 + lane];   // pairs 2p, 2p + 1
+        const float4 q = reinterpret_cast<const float4*>(pattern)[r * 64 + lane];   // pairs 2p, 2p + 1
 #endif
         words[r] = __ballot(sample(q.x, q.y) < sample(q.z, q.w));
     }
@@ -2614,7 +2629,73 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     if (i >= cnt_l) return;   // slot past the level's kept count
     const int oidx = lbase + i;   // output order: level-major list order
     if (oidx >= cap) return;
-    describe_keypoint<TRIG>(g, l, f, k, (long long)f * cap + oidx, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
+    describe_keypoint<TRIG, false>(g, l, f, k, (long long)f * cap + oidx, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
+}
+
+// Persistent describe (round 5).  One launch of G one-wavefront workgroups sized to the machine (the
+// occupancy limit x CUs) instead of one workgroup per selection slot: 16.6M slot workgroups per 8192-frame
+// C2 step ran into the workgroup launch rate (~2 per ns, MI355X_MICROARCH "a 1024-block grid starts
+// first->last within 0.34-0.69 us"), and a third of them exited at once (empty slots).  Work items are
+// (frame, chunk of kpi consecutive output rows); each wavefront strides over the items of its XCD group:
+// workgroup w runs on the XCD group w % 8 (round-robin dealing), and group x owns the contiguous frames
+// [F x / 8, F (x + 1) / 8), so a frame's patches are read through one XCD's L2.  Row j of frame f is
+// keypoint i = j - lbase[l] of the level l whose output range holds it (the reference's level-major order,
+// :818), selection slot L.out_base + i.  The frame's count is written by the wavefront that takes chunk 0.
+template <int TRIG>
+__global__ __launch_bounds__(64) void describe_persist_kernel(Geom g, const uint8_t* __restrict__ in,
+                                                              long long in_fstride, int in_step,
+                                                              const uint8_t* __restrict__ pyr,
+                                                              const uint32_t* __restrict__ sel,
+                                                              const int* __restrict__ sel_cnt,
+                                                              orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                              int32_t* __restrict__ counts, int cap, int F, int nchunk,
+                                                              int kpi) {
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];
+    const int lane = threadIdx.x;
+    const int G = (int)gridDim.x, w = (int)blockIdx.x;
+    const int x = w & 7;
+    const int gx = (G - x + 7) >> 3;              // wavefronts of group x
+    const int f0 = (int)(((long long)F * x) >> 3), f1 = (int)(((long long)F * (x + 1)) >> 3);
+    const int nitems = (f1 - f0) * nchunk;
+    const int nl = g.nlevels;
+    for (int it = w >> 3; it < nitems; it += gx) {
+        const int fr = it / nchunk;
+        const int c = it - fr * nchunk;
+        const int f = f0 + fr;
+        // the frame's kept counts per level (wave-uniform: one s_load_dwordx16 from the scalar cache, re-read
+        // per keypoint rather than held across the loop; the count buffer has 64 B of slack)
+        const int* cf = sel_cnt + f * nl;
+        int total = 0;
+        {
+            int c16[MAX_LEVELS];   // unconditional loads: one s_load_dwordx16
+#pragma unroll
+            for (int q = 0; q < MAX_LEVELS; q++) c16[q] = cf[q];
+#pragma unroll
+            for (int q = 0; q < MAX_LEVELS; q++) total += q < nl ? c16[q] : 0;
+        }
+        if (c == 0 && lane == 0) counts[f] = total;
+        const int j0 = c * kpi, j1 = min(min(total, j0 + kpi), cap);
+        for (int j = j0; j < j1; j++) {
+            int c16[MAX_LEVELS];
+            const int* cfj = cf;
+            asm volatile("" : "+s"(cfj));   // re-read per keypoint (scalar cache) instead of held across the loop
+#pragma unroll
+            for (int q = 0; q < MAX_LEVELS; q++) c16[q] = cfj[q];
+            int l = 0, lbase = 0, run = 0;
+#pragma unroll
+            for (int q = 0; q < MAX_LEVELS - 1; q++) {
+                run += q < nl ? c16[q] : 0;
+                if (run <= j) { l = q + 1; lbase = run; }
+            }
+            // l opaque: the level's fields come by one dynamic kernarg load each, not as select chains over
+            // all 16 levels' preloaded fields (SGPR spills)
+            l = __builtin_amdgcn_readfirstlane(l);
+            asm volatile("" : "+s"(l));
+            const uint32_t k = sel[(long long)f * g.out_frame + g.lv[l].out_base + (j - lbase)];
+            describe_keypoint<TRIG, true>(g, l, f, k, (long long)f * cap + j, in, in_fstride, in_step, pyr, kps, desc, Hb,
+                                          it);
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
@@ -2657,6 +2738,10 @@ struct orbx_extractor {
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
     int pyr_pair = 2;   // pyramid_pair_kernel for levels (1,2), (3,4), (5,6) (level 0 16-byte aligned); 1: (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
     // OpenCV-build switches (orbx_set_opencv_compat; ORBX_TRIG / ORBX_RESIZE_TAIL)
+    int desc_persist = 1;  // describe_persist_kernel (0: one workgroup per selection slot; ORBX_DESC_PERSIST)
+    int desc_kpi = 8;      // output rows per persistent work item (ORBX_DESC_KPI)
+    int desc_waves = 0;    // persistent grid (0: occupancy x CUs; ORBX_DESC_WAVES)
+    int desc_grid = 0;     // resolved grid
     int trig_float = 0;    // ComputeOrbDescriptor's cos / sin: 0 ::cos(double), 1 cosf / sinf
     int resize_simd = 16;  // the resize's vector width V: scalar tail after the SIMD loop (0: none, 1: all scalar)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
@@ -3113,10 +3198,14 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         fast(0, g.nlevels, st);
         quadtree(0, g.nlevels, st);
     }
-    {
-    launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F), dim3(64),
-                       0u, st, g,
-                       d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
+    if (h->desc_persist) {
+        const int nchunk = (g.out_frame + h->desc_kpi - 1) / h->desc_kpi;
+        launch_timed(h, 3, h->trig_float ? describe_persist_kernel<1> : describe_persist_kernel<0>,
+                     dim3((unsigned)h->desc_grid), dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps,
+                     d_desc, d_counts, cap, F, nchunk, h->desc_kpi);
+    } else {
+        launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F),
+                     dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
     }
 }
 
@@ -3210,6 +3299,9 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     if (const char* e = getenv("ORBX_DEBUG_NC")) h->debug_nc = atoi(e);
+    if (const char* e = getenv("ORBX_DESC_PERSIST")) h->desc_persist = atoi(e) != 0;
+    if (const char* e = getenv("ORBX_DESC_KPI")) h->desc_kpi = std::max(1, std::min(256, atoi(e)));
+    if (const char* e = getenv("ORBX_DESC_WAVES")) h->desc_waves = std::max(0, atoi(e)) & ~7;
     // OpenCV-build switches (orbx_set_opencv_compat): ORBX_TRIG=double|float, ORBX_RESIZE_TAIL=V
     if (const char* e = getenv("ORBX_TRIG")) h->trig_float = (e[0] == 'f' || e[0] == '1') ? 1 : 0;
     if (const char* e = getenv("ORBX_RESIZE_TAIL")) {
@@ -3217,6 +3309,14 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
         if (v == 0 || v == 1 || v == 8 || v == 16 || v == 32 || v == 64) h->resize_simd = v;
     }
     compute_tables(h);
+    {   // persistent describe grid: every wavefront resident at once (occupancy x CUs), a multiple of 8
+        int ncu = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)describe_persist_kernel<0>, 64, 0) !=
+            hipSuccess)
+            per_cu = 8;
+        h->desc_grid = h->desc_waves > 0 ? h->desc_waves : std::max(8, (ncu * std::max(per_cu, 1)) & ~7);
+    }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
