@@ -20,4 +20,6 @@ for kind in pan textured; do
     done
   done
 done
+timeout -k 10 60 tools/probe/hazard_probe 200 > gpurun_out/hazard_probe.log 2>&1 || { tail gpurun_out/hazard_probe.log; exit 9; }
+cat gpurun_out/hazard_probe.log
 echo "session done"

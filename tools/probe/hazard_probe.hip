@@ -1,0 +1,164 @@
+// Hazard probe (gfx950): instruction pairs the compiler's hazard recognizer does not see when they sit in
+// inline asm, each run many times over the whole chip and checked against the host, to learn which ones
+// the hardware does NOT order by itself (VERDICT r04 "Next round" 3: the round-4 describe builds whose
+// descriptors differed between identical runs).
+//   T0  control: the same VALU ops with 4 s_nop wait states between writer and reader;
+//   T1  v_mov_b32 x2 writing a VGPR pair, v_fmac_f64 reading it as the accumulator, 0 wait states
+//       (DESIGN §4 describe round 4: the fma-sincos build's v_fmac_f64_e32 read a pair written by two
+//       v_mov_b32 one or two instructions earlier);
+//   T2  the same with the pair as src0 instead of the accumulator;
+//   T3  v_mfma_i32_16x16x64_i8 with D exactly over A (the pattern tools/mfma_overlap.py reports in
+//       describe_kernel), result read after 18 wait states, vs a D elsewhere;
+//   T4  positive control: VALU write -> DPP read of the same VGPR with 0 wait states (a documented
+//       hazard: 2 wait states required) -- shows the probe can see a hazard at all.
+// Every lane computes a known answer; the kernel counts lanes whose result differs.  No scalar stores.
+// Build: hipcc --offload-arch=gfx950 -O2 hazard_probe.hip -o hazard_probe ; run: ./hazard_probe [iters]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <vector>
+
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double fmac_pair_acc(double a, double b, unsigned clo, unsigned chi, int nop) {
+    double r;
+    if (nop)
+        asm volatile(
+            "v_mov_b32 v40, %1\n\tv_mov_b32 v41, %2\n\ts_nop 4\n\t"
+            "v_fmac_f64_e32 v[40:41], %3, %4\n\ts_nop 4\n\tv_mov_b64 %0, v[40:41]\n\ts_nop 4"
+            : "=v"(r) : "v"(clo), "v"(chi), "v"(a), "v"(b) : "v40", "v41");
+    else
+        asm volatile(
+            "v_mov_b32 v40, %1\n\tv_mov_b32 v41, %2\n\t"
+            "v_fmac_f64_e32 v[40:41], %3, %4\n\ts_nop 4\n\tv_mov_b64 %0, v[40:41]\n\ts_nop 4"
+            : "=v"(r) : "v"(clo), "v"(chi), "v"(a), "v"(b) : "v40", "v41");
+    return r;
+}
+
+__device__ __forceinline__ double fmac_pair_src(double c, double b, unsigned alo, unsigned ahi, int nop) {
+    double r = c;
+    if (nop)
+        asm volatile(
+            "v_mov_b32 v42, %1\n\tv_mov_b32 v43, %2\n\ts_nop 4\n\t"
+            "v_fmac_f64_e32 %0, v[42:43], %3\n\ts_nop 4"
+            : "+v"(r) : "v"(alo), "v"(ahi), "v"(b) : "v42", "v43");
+    else
+        asm volatile(
+            "v_mov_b32 v42, %1\n\tv_mov_b32 v43, %2\n\t"
+            "v_fmac_f64_e32 %0, v[42:43], %3\n\ts_nop 4"
+            : "+v"(r) : "v"(alo), "v"(ahi), "v"(b) : "v42", "v43");
+    return r;
+}
+
+// D over A exactly (overlap 1) or D elsewhere (overlap 0); C = 0.  The result is read 18+ wait states later.
+__device__ __forceinline__ i4v mfma_da(i4v a, i4v b, int overlap) {
+    i4v r;
+    if (overlap)
+        asm volatile(
+            "v_mov_b32 v44, %1\n\tv_mov_b32 v45, %2\n\tv_mov_b32 v46, %3\n\tv_mov_b32 v47, %4\n\t"
+            "v_mov_b32 v48, %5\n\tv_mov_b32 v49, %6\n\tv_mov_b32 v50, %7\n\tv_mov_b32 v51, %8\n\ts_nop 4\n\t"
+            "v_mfma_i32_16x16x64_i8 v[44:47], v[44:47], v[48:51], 0\n\t"
+            "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"
+            "v_mov_b32 %0, v44\n\ts_nop 4"
+            : "=v"(r.x) : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)
+            : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51");
+    else
+        asm volatile(
+            "v_mov_b32 v44, %1\n\tv_mov_b32 v45, %2\n\tv_mov_b32 v46, %3\n\tv_mov_b32 v47, %4\n\t"
+            "v_mov_b32 v48, %5\n\tv_mov_b32 v49, %6\n\tv_mov_b32 v50, %7\n\tv_mov_b32 v51, %8\n\ts_nop 4\n\t"
+            "v_mfma_i32_16x16x64_i8 v[52:55], v[44:47], v[48:51], 0\n\t"
+            "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"
+            "v_mov_b32 %0, v52\n\ts_nop 4"
+            : "=v"(r.x) : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)
+            : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55");
+    r.y = r.z = r.w = 0;
+    return r;
+}
+
+// VALU write then DPP read of the written VGPR (quad_perm [1,0,3,2]), 0 or 4 wait states
+__device__ __forceinline__ unsigned dpp_after_write(unsigned v, int nop) {
+    unsigned r;
+    if (nop)
+        asm volatile("v_add_u32 v56, %1, 1\n\ts_nop 4\n\tv_mov_b32_dpp %0, v56 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\ts_nop 4"
+                     : "=v"(r) : "v"(v) : "v56");
+    else
+        asm volatile("v_add_u32 v56, %1, 1\n\tv_mov_b32_dpp %0, v56 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\ts_nop 4"
+                     : "=v"(r) : "v"(v) : "v56");
+    return r;
+}
+
+__global__ __launch_bounds__(256) void probe(int test, int nop, int iters, const double* __restrict__ da,
+                                            const double* __restrict__ db, const double* __restrict__ dc,
+                                            unsigned long long* __restrict__ bad, unsigned long long* __restrict__ sink) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    unsigned long long nb = 0, acc = 0;
+    for (int it = 0; it < iters; it++) {
+        const int i = (t * 7 + it * 131) & 4095;
+        const double a = da[i], b = db[i], c = dc[i];
+        if (test == 1) {
+            const unsigned long long cb = __double_as_longlong(c);
+            const double r = fmac_pair_acc(a, b, (unsigned)cb, (unsigned)(cb >> 32), nop);
+            const double e = fma(a, b, c);
+            nb += __double_as_longlong(r) != __double_as_longlong(e);
+            acc += __double_as_longlong(r);
+        } else if (test == 2) {
+            const unsigned long long ab = __double_as_longlong(a);
+            const double r = fmac_pair_src(c, b, (unsigned)ab, (unsigned)(ab >> 32), nop);
+            const double e = fma(a, b, c);
+            nb += __double_as_longlong(r) != __double_as_longlong(e);
+            acc += __double_as_longlong(r);
+        } else if (test == 3) {
+            const unsigned long long ab = __double_as_longlong(a), bb = __double_as_longlong(b);
+            const i4v A = {(int)ab, (int)(ab >> 32), (int)(ab * 3), (int)(bb ^ ab)};
+            const i4v B = {(int)bb, (int)(bb >> 32), (int)(bb * 5), (int)(ab + bb)};
+            const i4v r1 = mfma_da(A, B, nop ? 0 : 1);   // nop != 0: the non-overlapping reference form
+            const i4v r0 = mfma_da(A, B, 0);
+            nb += r1.x != r0.x;
+            acc += (unsigned)r1.x;
+        } else if (test == 4) {
+            const unsigned v = (unsigned)__double_as_longlong(a) + (unsigned)it;
+            const unsigned r = dpp_after_write(v, nop);
+            const unsigned e = __shfl_xor(v + 1u, 1);
+            nb += r != e;
+            acc += r;
+        }
+    }
+    if (nb) atomicAdd(bad, nb);
+    sink[t & 1023] = acc;   // keep the work
+    (void)lane;
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 200;
+    std::vector<double> a(4096), b(4096), c(4096);
+    srand(1);
+    for (int i = 0; i < 4096; i++) {
+        a[i] = (rand() / (double)RAND_MAX - 0.5) * 1e3;
+        b[i] = (rand() / (double)RAND_MAX - 0.5) * 1e-2;
+        c[i] = (rand() / (double)RAND_MAX - 0.5) * 7;
+    }
+    double *da, *db, *dc;
+    unsigned long long *bad, *sink;
+    hipMalloc(&da, 4096 * 8); hipMalloc(&db, 4096 * 8); hipMalloc(&dc, 4096 * 8);
+    hipMalloc(&bad, 8); hipMalloc(&sink, 1024 * 8);
+    hipMemcpy(da, a.data(), 4096 * 8, hipMemcpyHostToDevice);
+    hipMemcpy(db, b.data(), 4096 * 8, hipMemcpyHostToDevice);
+    hipMemcpy(dc, c.data(), 4096 * 8, hipMemcpyHostToDevice);
+    const char* names[] = {"", "T1 v_mov x2 -> v_fmac_f64 acc", "T2 v_mov x2 -> v_fmac_f64 src0",
+                           "T3 mfma i8 D==A (vs D elsewhere)", "T4 VALU -> DPP read (positive control)"};
+    const int blocks = 256 * 8;   // 8 workgroups of 4 waves per CU
+    for (int test = 1; test <= 4; test++)
+        for (int nop = 0; nop <= 1; nop++) {
+            hipMemset(bad, 0, 8);
+            hipLaunchKernelGGL(probe, dim3(blocks), dim3(256), 0, 0, test, nop, iters, da, db, dc, bad, sink);
+            if (hipDeviceSynchronize() != hipSuccess) { printf("kernel error\n"); return 2; }
+            unsigned long long nb = 0;
+            hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+            printf("%-42s %s: %llu mismatches of %llu\n", names[test], nop ? (test == 3 ? "reference" : "4 nops ") : "0 nops ",
+                   nb, (unsigned long long)blocks * 256 * iters);
+        }
+    return 0;
+}
