@@ -2632,69 +2632,86 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     describe_keypoint<TRIG, false>(g, l, f, k, (long long)f * cap + oidx, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
 }
 
-// Persistent describe (round 5).  One launch of G one-wavefront workgroups sized to the machine (the
-// occupancy limit x CUs) instead of one workgroup per selection slot: 16.6M slot workgroups per 8192-frame
-// C2 step ran into the workgroup launch rate (~2 per ns, MI355X_MICROARCH "a 1024-block grid starts
-// first->last within 0.34-0.69 us"), and a third of them exited at once (empty slots).  Work items are
-// (frame, chunk of kpi consecutive output rows); each wavefront strides over the items of its XCD group:
-// workgroup w runs on the XCD group w % 8 (round-robin dealing), and group x owns the contiguous frames
-// [F x / 8, F (x + 1) / 8), so a frame's patches are read through one XCD's L2.  Row j of frame f is
-// keypoint i = j - lbase[l] of the level l whose output range holds it (the reference's level-major order,
-// :818), selection slot L.out_base + i.  The frame's count is written by the wavefront that takes chunk 0.
+// Persistent describe (round 5).  One launch of G one-wavefront workgroups sized to the machine instead of
+// one workgroup per selection slot (16.6M per 8192-frame C2 step, a third of them empty slots that exit at
+// once).  Work items are (frame, chunk of kpi consecutive output rows); the items of the contiguous
+// frames [F x / 8, F (x + 1) / 8) belong to XCD group x = w % 8 (workgroups are dealt round-robin over the
+// XCDs, so a frame's patches go through one XCD's L2), and the group's wavefronts take them from the
+// group's work counter (one agent-scope atomic per item, the next item's taken before the current one is
+// processed).  Dynamic: a wavefront admitted late (the grid is sized from the occupancy API, which can
+// promise one more wavefront per SIMD than the SGPR count admits) or a group with denser frames only
+// shifts items between wavefronts, never adds a round.  Row j of frame f is keypoint i = j - lbase[l] of
+// the level whose output range holds it (the reference's level-major order, :818), selection slot
+// L.out_base + i.  The frame's count is written by the wavefront that takes chunk 0.
+struct DescArgs {
+    Geom g;
+    const uint8_t* in;
+    long long in_fstride;
+    const uint8_t* pyr;
+    const uint32_t* sel;
+    const int* sel_cnt;
+    orbx_keypoint* kps;
+    uint8_t* desc;
+    int32_t* counts;
+    int* work;        // 8 group counters, 128 B apart, zeroed before the launch
+    int in_step, cap, F, nchunk, kpi;
+};
+typedef __attribute__((address_space(4))) const DescArgs KDescArgs;
+
+#ifndef DESC_PERSIST_WAVES
+#define DESC_PERSIST_WAVES 8   // waves per SIMD the register allocation targets (8: 64 VGPRs, 2 spilled; 7: 71, none)
+#endif
 template <int TRIG>
-__global__ __launch_bounds__(64) void describe_persist_kernel(Geom g, const uint8_t* __restrict__ in,
-                                                              long long in_fstride, int in_step,
-                                                              const uint8_t* __restrict__ pyr,
-                                                              const uint32_t* __restrict__ sel,
-                                                              const int* __restrict__ sel_cnt,
-                                                              orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                              int32_t* __restrict__ counts, int cap, int F, int nchunk,
-                                                              int kpi) {
+__global__ __launch_bounds__(64, DESC_PERSIST_WAVES) void describe_persist_kernel(DescArgs args) {
     __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];
     const int lane = threadIdx.x;
-    const int G = (int)gridDim.x, w = (int)blockIdx.x;
+    const int w = (int)blockIdx.x;
     const int x = w & 7;
-    const int gx = (G - x + 7) >> 3;              // wavefronts of group x
+    const int F = args.F, nchunk = args.nchunk;
     const int f0 = (int)(((long long)F * x) >> 3), f1 = (int)(((long long)F * (x + 1)) >> 3);
     const int nitems = (f1 - f0) * nchunk;
-    const int nl = g.nlevels;
-    for (int it = w >> 3; it < nitems; it += gx) {
+    int* ctr = args.work + 32 * x;
+    auto take = [&]() {
+        int v = 0;
+        if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    int it = take();
+    while (it < nitems) {
+        const int nxt = take();   // in flight under this item's keypoints
+        // every argument re-read from the kernarg segment per item through an opaque pointer (scalar
+        // loads): nothing but the loop state is held in SGPRs across the loop
+        KDescArgs* ap = (KDescArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ap));
+        const DescArgs& a = *(const DescArgs*)ap;
+        const Geom& g = a.g;
         const int fr = it / nchunk;
         const int c = it - fr * nchunk;
         const int f = f0 + fr;
-        // the frame's kept counts per level (wave-uniform: one s_load_dwordx16 from the scalar cache, re-read
-        // per keypoint rather than held across the loop; the count buffer has 64 B of slack)
-        const int* cf = sel_cnt + f * nl;
+        const int nl = g.nlevels;
+        // the frame's kept counts per level (wave-uniform: one s_load_dwordx16; the count buffer has 64 B
+        // of slack)
+        const int* cf = a.sel_cnt + f * nl;
+        int c16[MAX_LEVELS];
+#pragma unroll
+        for (int q = 0; q < MAX_LEVELS; q++) c16[q] = cf[q];
         int total = 0;
-        {
-            int c16[MAX_LEVELS];   // unconditional loads: one s_load_dwordx16
 #pragma unroll
-            for (int q = 0; q < MAX_LEVELS; q++) c16[q] = cf[q];
-#pragma unroll
-            for (int q = 0; q < MAX_LEVELS; q++) total += q < nl ? c16[q] : 0;
-        }
-        if (c == 0 && lane == 0) counts[f] = total;
-        const int j0 = c * kpi, j1 = min(min(total, j0 + kpi), cap);
+        for (int q = 0; q < MAX_LEVELS; q++) total += q < nl ? c16[q] : 0;
+        if (c == 0 && lane == 0) a.counts[f] = total;
+        const int j0 = c * a.kpi, j1 = min(min(total, j0 + a.kpi), a.cap);
         for (int j = j0; j < j1; j++) {
-            int c16[MAX_LEVELS];
-            const int* cfj = cf;
-            asm volatile("" : "+s"(cfj));   // re-read per keypoint (scalar cache) instead of held across the loop
-#pragma unroll
-            for (int q = 0; q < MAX_LEVELS; q++) c16[q] = cfj[q];
             int l = 0, lbase = 0, run = 0;
 #pragma unroll
             for (int q = 0; q < MAX_LEVELS - 1; q++) {
                 run += q < nl ? c16[q] : 0;
                 if (run <= j) { l = q + 1; lbase = run; }
             }
-            // l opaque: the level's fields come by one dynamic kernarg load each, not as select chains over
-            // all 16 levels' preloaded fields (SGPR spills)
-            l = __builtin_amdgcn_readfirstlane(l);
-            asm volatile("" : "+s"(l));
-            const uint32_t k = sel[(long long)f * g.out_frame + g.lv[l].out_base + (j - lbase)];
-            describe_keypoint<TRIG, true>(g, l, f, k, (long long)f * cap + j, in, in_fstride, in_step, pyr, kps, desc, Hb,
-                                          it);
+            const uint32_t k = a.sel[(long long)f * g.out_frame + g.lv[l].out_base + (j - lbase)];
+            describe_keypoint<TRIG, true>(g, l, f, k, (long long)f * a.cap + j, a.in, a.in_fstride, a.in_step, a.pyr,
+                                          a.kps, a.desc, Hb, it);
         }
+        it = nxt;
     }
 }
 
@@ -2759,6 +2776,7 @@ struct orbx_extractor {
     // workspace for up to ws_frames frames
     int ws_frames = 0;
     DevBuf d_pyr, d_slots, d_cellcnt, d_P, d_T, d_sel, d_selcnt, d_fault;
+    DevBuf d_work;   // describe_persist_kernel's 8 group counters (128 B apart)
     // single-frame host API buffers
     DevBuf d_img, d_kps, d_desc, d_counts;
     DevBuf d_stereo_sad;   // stereo scratch (orbx_stereo_matches_batch_device)
@@ -3083,6 +3101,7 @@ static int reserve_workspace(orbx_extractor* h, int frames) {
     if ((rc = h->d_sel.reserve((size_t)frames * g.out_frame * 4))) return rc;
     // + 64 B: describe reads 16 counts from a frame's first (scalar loads, past the last frame too)
     if ((rc = h->d_selcnt.reserve((size_t)frames * g.nlevels * 4 + 64))) return rc;
+    if ((rc = h->d_work.reserve(8 * 128))) return rc;
     if (!h->d_fault.ptr) {   // sticky until read (orbx_batch_status / the host Extract)
         if ((rc = h->d_fault.reserve(16))) return rc;
         ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));
@@ -3199,10 +3218,25 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         quadtree(0, g.nlevels, st);
     }
     if (h->desc_persist) {
-        const int nchunk = (g.out_frame + h->desc_kpi - 1) / h->desc_kpi;
+        DescArgs a;
+        a.g = g;
+        a.in = d_imgs;
+        a.in_fstride = fstride;
+        a.pyr = pyr;
+        a.sel = sel;
+        a.sel_cnt = selcnt;
+        a.kps = d_kps;
+        a.desc = d_desc;
+        a.counts = d_counts;
+        a.work = h->d_work.as<int>();
+        a.in_step = step;
+        a.cap = cap;
+        a.F = F;
+        a.kpi = h->desc_kpi;
+        a.nchunk = (g.out_frame + h->desc_kpi - 1) / h->desc_kpi;
+        (void)hipMemsetAsync(a.work, 0, 8 * 128, st);
         launch_timed(h, 3, h->trig_float ? describe_persist_kernel<1> : describe_persist_kernel<0>,
-                     dim3((unsigned)h->desc_grid), dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps,
-                     d_desc, d_counts, cap, F, nchunk, h->desc_kpi);
+                     dim3((unsigned)h->desc_grid), dim3(64), 0u, st, a);
     } else {
         launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F),
                      dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
@@ -3330,7 +3364,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
 int orbx_destroy(orbx_extractor* h) {
     if (!h) return ORB_OK;
     (void)hipSetDevice(h->device);
-    DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
+    DevBuf* bufs[] = {&h->d_work, &h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
                       &h->d_counts, &h->d_stereo_sad};
     for (DevBuf* b : bufs) b->release();

@@ -9,6 +9,7 @@
 //   T2  the same with the pair as src0 instead of the accumulator;
 //   T3  v_mfma_i32_16x16x64_i8 with D exactly over A (the pattern tools/mfma_overlap.py reports in
 //       describe_kernel), result read after 18 wait states, vs a D elsewhere;
+//   T5  v_mfma_i32_16x16x64_i8 result read by a VALU K wait states after issue: the hardware's window;
 //   T4  positive control: VALU write -> DPP read of the same VGPR with 0 wait states (a documented
 //       hazard: 2 wait states required) -- shows the probe can see a hazard at all.
 // Every lane computes a known answer; the kernel counts lanes whose result differs.  No scalar stores.
@@ -77,6 +78,49 @@ __device__ __forceinline__ i4v mfma_da(i4v a, i4v b, int overlap) {
     return r;
 }
 
+// MFMA result read by a VALU K wait states after the MFMA issue (the MFMA's inputs settled 5 wait states
+// before it).  K = 0 .. 18: the window the hardware needs for v_mfma_i32_16x16x64_i8 (D in VGPRs).
+#define MFMA_RAW(K, NOPS)                                                                                   \
+    __device__ __noinline__ int mfma_raw_##K(i4v a, i4v b) {                                               \
+        int r;                                                                                              \
+        asm volatile("v_mov_b32 v44, %1\n\tv_mov_b32 v45, %2\n\tv_mov_b32 v46, %3\n\tv_mov_b32 v47, %4\n\t"  \
+                     "v_mov_b32 v48, %5\n\tv_mov_b32 v49, %6\n\tv_mov_b32 v50, %7\n\tv_mov_b32 v51, %8\n\t"  \
+                     "v_mov_b32 v52, 0\n\tv_mov_b32 v53, 0\n\tv_mov_b32 v54, 0\n\tv_mov_b32 v55, 0\n\ts_nop 4\n\t" \
+                     "v_mfma_i32_16x16x64_i8 v[52:55], v[44:47], v[48:51], v[52:55]\n\t" NOPS                 \
+                     "v_mov_b32 %0, v52\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"                                   \
+                     : "=v"(r) : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w) \
+                     : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55");     \
+        return r;                                                                                           \
+    }
+MFMA_RAW(0, "")
+MFMA_RAW(2, "s_nop 1\n\t")
+MFMA_RAW(4, "s_nop 3\n\t")
+MFMA_RAW(6, "s_nop 5\n\t")
+MFMA_RAW(8, "s_nop 7\n\t")
+MFMA_RAW(9, "s_nop 7\n\ts_nop 0\n\t")
+MFMA_RAW(10, "s_nop 7\n\ts_nop 1\n\t")
+MFMA_RAW(11, "s_nop 7\n\ts_nop 2\n\t")
+MFMA_RAW(12, "s_nop 7\n\ts_nop 3\n\t")
+MFMA_RAW(14, "s_nop 7\n\ts_nop 5\n\t")
+MFMA_RAW(16, "s_nop 7\n\ts_nop 7\n\t")
+MFMA_RAW(20, "s_nop 7\n\ts_nop 7\n\ts_nop 3\n\t")
+__device__ __forceinline__ int mfma_raw(int k, i4v a, i4v b) {
+    switch (k) {
+        case 0: return mfma_raw_0(a, b);
+        case 2: return mfma_raw_2(a, b);
+        case 4: return mfma_raw_4(a, b);
+        case 6: return mfma_raw_6(a, b);
+        case 8: return mfma_raw_8(a, b);
+        case 9: return mfma_raw_9(a, b);
+        case 10: return mfma_raw_10(a, b);
+        case 11: return mfma_raw_11(a, b);
+        case 12: return mfma_raw_12(a, b);
+        case 14: return mfma_raw_14(a, b);
+        case 16: return mfma_raw_16(a, b);
+        default: return mfma_raw_20(a, b);
+    }
+}
+
 // VALU write then DPP read of the written VGPR (quad_perm [1,0,3,2]), 0 or 4 wait states
 __device__ __forceinline__ unsigned dpp_after_write(unsigned v, int nop) {
     unsigned r;
@@ -118,6 +162,13 @@ __global__ __launch_bounds__(256) void probe(int test, int nop, int iters, const
             const i4v r0 = mfma_da(A, B, 0);
             nb += r1.x != r0.x;
             acc += (unsigned)r1.x;
+        } else if (test == 5) {
+            const unsigned long long ab = __double_as_longlong(a), bb = __double_as_longlong(b);
+            const i4v A = {(int)ab, (int)(ab >> 32), (int)(ab * 3), (int)(bb ^ ab)};
+            const i4v B = {(int)bb, (int)(bb >> 32), (int)(bb * 5), (int)(ab + bb)};
+            const int r = mfma_raw(nop, A, B), e = mfma_raw(20, A, B);
+            nb += r != e;
+            acc += (unsigned)r;
         } else if (test == 4) {
             const unsigned v = (unsigned)__double_as_longlong(a) + (unsigned)it;
             const unsigned r = dpp_after_write(v, nop);
@@ -160,5 +211,15 @@ int main(int argc, char** argv) {
             printf("%-42s %s: %llu mismatches of %llu\n", names[test], nop ? (test == 3 ? "reference" : "4 nops ") : "0 nops ",
                    nb, (unsigned long long)blocks * 256 * iters);
         }
+    const int ks[] = {0, 2, 4, 6, 8, 9, 10, 11, 12, 14, 16};
+    for (int k : ks) {
+        hipMemset(bad, 0, 8);
+        hipLaunchKernelGGL(probe, dim3(blocks), dim3(256), 0, 0, 5, k, iters / 4, da, db, dc, bad, sink);
+        if (hipDeviceSynchronize() != hipSuccess) { printf("kernel error\n"); return 2; }
+        unsigned long long nb = 0;
+        hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+        printf("T5 mfma i8 16x16x64 -> VALU read after %2d wait states: %llu mismatches of %llu\n", k, nb,
+               (unsigned long long)blocks * 256 * (iters / 4));
+    }
     return 0;
 }
