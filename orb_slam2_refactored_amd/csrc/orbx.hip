@@ -2250,29 +2250,17 @@ constexpr int HB_ELEMS = DESC_HBT ? 40 * HCS : 48 * HBS;
 
 // One kept keypoint (level l, selection word k, output row o of the frame's slots): the raw 43x43 patch,
 // IC_Angle, the 7x7 Q8 blur and the rBRIEF samples, written to kps / desc at row o.  One wavefront.
-// A pointer the compiler cannot see through (an empty asm on its SGPR pair): inside the persistent
-// kernel's loop the constant-table loads stay per keypoint instead of being hoisted out of the loop as
-// ~52 VGPRs of loop-invariant fragments (127 VGPRs, 4 wavefronts per SIMD).
-template <typename T>
-__device__ __forceinline__ const T* opaque_ptr(const T* p) {
-    asm volatile("" : "+s"(p));
-    return p;
-}
-
-template <int TRIG, bool LOOP>
+template <int TRIG>
 __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, uint32_t k, long long o,
                                                   const uint8_t* __restrict__ in, long long in_fstride, int in_step,
                                                   const uint8_t* __restrict__ pyr, orbx_keypoint* __restrict__ kps,
                                                   uint8_t* __restrict__ desc, uint16_t* Hb, int lb) {
-    int lane = threadIdx.x;
-    // (in the loop, the lane id is opaque too: every lane-derived offset is rebuilt per keypoint, not held
-    // across the loop by LICM)
-    if (LOOP) asm volatile("" : "+v"(lane));
+    const int lane = threadIdx.x;
     uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
     const LevelDev& L = g.lv[l];
-    const HBlurA* hblur_a = LOOP ? opaque_ptr(&c_hblur_a) : &c_hblur_a;
-    const AngleA* angle_a = LOOP ? opaque_ptr(&c_angle_a) : &c_angle_a;
-    const float* pattern = LOOP ? opaque_ptr(c_pattern) : c_pattern;
+    const HBlurA* hblur_a = &c_hblur_a;
+    [[maybe_unused]] const AngleA* angle_a = &c_angle_a;
+    const float* pattern = c_pattern;
     DESC_STAMP(0);
     // the blur's constant A fragments, in flight under the patch load
     i4v afr[3];
@@ -2439,6 +2427,12 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
                 acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bfr[nt], afr[mt], cinit, 0, 0, 0);
 #else
                 acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+#endif
+#ifdef DESC_KEEPALIVE_DIAG
+        // diagnostic only (tests/test_dpp_hazards.py): round 4's empty-asm keep-alives of the products'
+        // operands, the build whose descriptors differed between identical runs
+        asm volatile("" ::"v"(bfr[0]), "v"(bfr[1]), "v"(bfr[2]));
+        asm volatile("" ::"v"(afr[0]), "v"(afr[1]), "v"(afr[2]));
 #endif
         auto put = [&](int nt, int mt) {
             uint2 pk;
@@ -2629,90 +2623,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     if (i >= cnt_l) return;   // slot past the level's kept count
     const int oidx = lbase + i;   // output order: level-major list order
     if (oidx >= cap) return;
-    describe_keypoint<TRIG, false>(g, l, f, k, (long long)f * cap + oidx, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
-}
-
-// Persistent describe (round 5).  One launch of G one-wavefront workgroups sized to the machine instead of
-// one workgroup per selection slot (16.6M per 8192-frame C2 step, a third of them empty slots that exit at
-// once).  Work items are (frame, chunk of kpi consecutive output rows); the items of the contiguous
-// frames [F x / 8, F (x + 1) / 8) belong to XCD group x = w % 8 (workgroups are dealt round-robin over the
-// XCDs, so a frame's patches go through one XCD's L2), and the group's wavefronts take them from the
-// group's work counter (one agent-scope atomic per item, the next item's taken before the current one is
-// processed).  Dynamic: a wavefront admitted late (the grid is sized from the occupancy API, which can
-// promise one more wavefront per SIMD than the SGPR count admits) or a group with denser frames only
-// shifts items between wavefronts, never adds a round.  Row j of frame f is keypoint i = j - lbase[l] of
-// the level whose output range holds it (the reference's level-major order, :818), selection slot
-// L.out_base + i.  The frame's count is written by the wavefront that takes chunk 0.
-struct DescArgs {
-    Geom g;
-    const uint8_t* in;
-    long long in_fstride;
-    const uint8_t* pyr;
-    const uint32_t* sel;
-    const int* sel_cnt;
-    orbx_keypoint* kps;
-    uint8_t* desc;
-    int32_t* counts;
-    int* work;        // 8 group counters, 128 B apart, zeroed before the launch
-    int in_step, cap, F, nchunk, kpi;
-};
-typedef __attribute__((address_space(4))) const DescArgs KDescArgs;
-
-#ifndef DESC_PERSIST_WAVES
-#define DESC_PERSIST_WAVES 8   // waves per SIMD the register allocation targets (8: 64 VGPRs, 2 spilled; 7: 71, none)
-#endif
-template <int TRIG>
-__global__ __launch_bounds__(64, DESC_PERSIST_WAVES) void describe_persist_kernel(DescArgs args) {
-    __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];
-    const int lane = threadIdx.x;
-    const int w = (int)blockIdx.x;
-    const int x = w & 7;
-    const int F = args.F, nchunk = args.nchunk;
-    const int f0 = (int)(((long long)F * x) >> 3), f1 = (int)(((long long)F * (x + 1)) >> 3);
-    const int nitems = (f1 - f0) * nchunk;
-    int* ctr = args.work + 32 * x;
-    auto take = [&]() {
-        int v = 0;
-        if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return __builtin_amdgcn_readfirstlane(v);
-    };
-    int it = take();
-    while (it < nitems) {
-        const int nxt = take();   // in flight under this item's keypoints
-        // every argument re-read from the kernarg segment per item through an opaque pointer (scalar
-        // loads): nothing but the loop state is held in SGPRs across the loop
-        KDescArgs* ap = (KDescArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ap));
-        const DescArgs& a = *(const DescArgs*)ap;
-        const Geom& g = a.g;
-        const int fr = it / nchunk;
-        const int c = it - fr * nchunk;
-        const int f = f0 + fr;
-        const int nl = g.nlevels;
-        // the frame's kept counts per level (wave-uniform: one s_load_dwordx16; the count buffer has 64 B
-        // of slack)
-        const int* cf = a.sel_cnt + f * nl;
-        int c16[MAX_LEVELS];
-#pragma unroll
-        for (int q = 0; q < MAX_LEVELS; q++) c16[q] = cf[q];
-        int total = 0;
-#pragma unroll
-        for (int q = 0; q < MAX_LEVELS; q++) total += q < nl ? c16[q] : 0;
-        if (c == 0 && lane == 0) a.counts[f] = total;
-        const int j0 = c * a.kpi, j1 = min(min(total, j0 + a.kpi), a.cap);
-        for (int j = j0; j < j1; j++) {
-            int l = 0, lbase = 0, run = 0;
-#pragma unroll
-            for (int q = 0; q < MAX_LEVELS - 1; q++) {
-                run += q < nl ? c16[q] : 0;
-                if (run <= j) { l = q + 1; lbase = run; }
-            }
-            const uint32_t k = a.sel[(long long)f * g.out_frame + g.lv[l].out_base + (j - lbase)];
-            describe_keypoint<TRIG, true>(g, l, f, k, (long long)f * a.cap + j, a.in, a.in_fstride, a.in_step, a.pyr,
-                                          a.kps, a.desc, Hb, it);
-        }
-        it = nxt;
-    }
+    describe_keypoint<TRIG>(g, l, f, k, (long long)f * cap + oidx, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
 }
 
 __global__ __launch_bounds__(256) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
@@ -2755,10 +2666,6 @@ struct orbx_extractor {
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
     int pyr_pair = 2;   // pyramid_pair_kernel for levels (1,2), (3,4), (5,6) (level 0 16-byte aligned); 1: (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
     // OpenCV-build switches (orbx_set_opencv_compat; ORBX_TRIG / ORBX_RESIZE_TAIL)
-    int desc_persist = 1;  // describe_persist_kernel (0: one workgroup per selection slot; ORBX_DESC_PERSIST)
-    int desc_kpi = 8;      // output rows per persistent work item (ORBX_DESC_KPI)
-    int desc_waves = 0;    // persistent grid (0: occupancy x CUs; ORBX_DESC_WAVES)
-    int desc_grid = 0;     // resolved grid
     int trig_float = 0;    // ComputeOrbDescriptor's cos / sin: 0 ::cos(double), 1 cosf / sinf
     int resize_simd = 16;  // the resize's vector width V: scalar tail after the SIMD loop (0: none, 1: all scalar)
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
@@ -2776,7 +2683,6 @@ struct orbx_extractor {
     // workspace for up to ws_frames frames
     int ws_frames = 0;
     DevBuf d_pyr, d_slots, d_cellcnt, d_P, d_T, d_sel, d_selcnt, d_fault;
-    DevBuf d_work;   // describe_persist_kernel's 8 group counters (128 B apart)
     // single-frame host API buffers
     DevBuf d_img, d_kps, d_desc, d_counts;
     DevBuf d_stereo_sad;   // stereo scratch (orbx_stereo_matches_batch_device)
@@ -3101,7 +3007,6 @@ static int reserve_workspace(orbx_extractor* h, int frames) {
     if ((rc = h->d_sel.reserve((size_t)frames * g.out_frame * 4))) return rc;
     // + 64 B: describe reads 16 counts from a frame's first (scalar loads, past the last frame too)
     if ((rc = h->d_selcnt.reserve((size_t)frames * g.nlevels * 4 + 64))) return rc;
-    if ((rc = h->d_work.reserve(8 * 128))) return rc;
     if (!h->d_fault.ptr) {   // sticky until read (orbx_batch_status / the host Extract)
         if ((rc = h->d_fault.reserve(16))) return rc;
         ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));
@@ -3217,30 +3122,8 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         fast(0, g.nlevels, st);
         quadtree(0, g.nlevels, st);
     }
-    if (h->desc_persist) {
-        DescArgs a;
-        a.g = g;
-        a.in = d_imgs;
-        a.in_fstride = fstride;
-        a.pyr = pyr;
-        a.sel = sel;
-        a.sel_cnt = selcnt;
-        a.kps = d_kps;
-        a.desc = d_desc;
-        a.counts = d_counts;
-        a.work = h->d_work.as<int>();
-        a.in_step = step;
-        a.cap = cap;
-        a.F = F;
-        a.kpi = h->desc_kpi;
-        a.nchunk = (g.out_frame + h->desc_kpi - 1) / h->desc_kpi;
-        (void)hipMemsetAsync(a.work, 0, 8 * 128, st);
-        launch_timed(h, 3, h->trig_float ? describe_persist_kernel<1> : describe_persist_kernel<0>,
-                     dim3((unsigned)h->desc_grid), dim3(64), 0u, st, a);
-    } else {
-        launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F),
-                     dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
-    }
+    launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F),
+                 dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
 }
 
 // Frames are split into sub-batches on the handle's side streams (fork/join with events on st) so
@@ -3333,9 +3216,6 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     if (const char* e = getenv("ORBX_DEBUG_NC")) h->debug_nc = atoi(e);
-    if (const char* e = getenv("ORBX_DESC_PERSIST")) h->desc_persist = atoi(e) != 0;
-    if (const char* e = getenv("ORBX_DESC_KPI")) h->desc_kpi = std::max(1, std::min(256, atoi(e)));
-    if (const char* e = getenv("ORBX_DESC_WAVES")) h->desc_waves = std::max(0, atoi(e)) & ~7;
     // OpenCV-build switches (orbx_set_opencv_compat): ORBX_TRIG=double|float, ORBX_RESIZE_TAIL=V
     if (const char* e = getenv("ORBX_TRIG")) h->trig_float = (e[0] == 'f' || e[0] == '1') ? 1 : 0;
     if (const char* e = getenv("ORBX_RESIZE_TAIL")) {
@@ -3343,14 +3223,6 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
         if (v == 0 || v == 1 || v == 8 || v == 16 || v == 32 || v == 64) h->resize_simd = v;
     }
     compute_tables(h);
-    {   // persistent describe grid: every wavefront resident at once (occupancy x CUs), a multiple of 8
-        int ncu = 0, per_cu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)describe_persist_kernel<0>, 64, 0) !=
-            hipSuccess)
-            per_cu = 8;
-        h->desc_grid = h->desc_waves > 0 ? h->desc_waves : std::max(8, (ncu * std::max(per_cu, 1)) & ~7);
-    }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -3364,7 +3236,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
 int orbx_destroy(orbx_extractor* h) {
     if (!h) return ORB_OK;
     (void)hipSetDevice(h->device);
-    DevBuf* bufs[] = {&h->d_work, &h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
+    DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
                       &h->d_counts, &h->d_stereo_sad};
     for (DevBuf* b : bufs) b->release();

@@ -19,6 +19,9 @@
 namespace orbamd {
 
 ORB_HD void sincos_f2d(float xf, float* s_out, float* c_out) {
+#ifdef SINCOS_FMA_DIAG   // diagnostic A/B only (round 4's fused sincos; DESIGN §4 describe round 4)
+#pragma clang fp contract(fast)
+#endif
     const double x = (double)xf;
     const double invpio2 = 6.36619772367581382433e-01;
     const double pio2_1 = 1.57079632673412561417e+00;    // first 33 bits of pi/2

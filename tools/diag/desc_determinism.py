@@ -8,7 +8,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 from test_extractor_gpu import _patchwork as patchwork, make
 
 
-frames = np.stack([patchwork(40 + i, 320, 240) for i in range(24)])
+NF, W, H = (int(os.environ.get(k, d)) for k, d in (("DET_FRAMES", 24), ("DET_W", 320), ("DET_H", 240)))
+frames = np.stack([patchwork(40 + i, W, H) for i in range(NF)])
 t = torch.from_numpy(frames).cuda()
 outs = []
 for spec in (0, 0, 0, 1, 8):

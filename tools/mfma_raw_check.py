@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Static check of a gfx950 listing: is every read of an MFMA's destination far enough behind the MFMA?
+
+An XDL MFMA writes its D registers several cycles after issue; a VALU / memory / DPP / readlane read of
+D inside that window returns the OLD register contents (tools/probe/hazard_probe.hip, T5, measures the
+window on the hardware).  The compiler inserts the wait states itself -- except that it counts an inline
+asm statement as wait states even when the asm is empty (a `asm volatile("" :: "v"(x))` keep-alive, or
+an opaque-pointer `asm volatile("" : "+s"(p))`), so an empty asm between an MFMA and the read of its
+result can leave the read inside the window.  That is the round-4 describe nondeterminism (DESIGN §4,
+describe round 4; VERDICT r04 "Next round" 3): results that depend on the read racing the write.
+
+Wait states: 1 per instruction, N+1 per `s_nop N`; the empty-asm markers (`;;#ASMSTART` / `;;#ASMEND`
+with nothing between) count 0.  Control flow: straight-line order plus every branch edge (writes pending
+at a branch stay pending at its target, one wait state later), as tools/dpp_hazard_check.py does.
+Required wait states per MFMA shape: REQUIRED below (from the probe; an MFMA reading the D of an earlier
+one as SrcC is ordered by the hardware and not checked).
+
+usage: mfma_raw_check.py listing.s [kernel-substring]   (exit 1 when a read falls inside a window)"""
+import re
+import sys
+
+# wait states between an MFMA's issue and the first safe read of its D by (a VALU / DPP / readlane, a
+# memory instruction).  The compiler's own spacing in this repository's listings, where no inline asm sits
+# between (the smallest value for which its code has no violation): i8 and FP4 16x16 8, f64 16x16x4 19 / 18.
+# hazard_probe T5 measures the hardware's window for the i8 shape.
+REQUIRED = {
+    "v_mfma_i32_16x16x64_i8": (8, 8),
+    "v_mfma_scale_f32_16x16x128_f8f6f4": (8, 8),
+    "v_mfma_f64_16x16x4_f64": (19, 18),
+}
+DEFAULT_REQUIRED = (19, 19)
+MEM_OPS = ("ds_", "buffer_", "global_", "flat_", "scratch_")
+
+reg_re = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b")
+label_re = re.compile(r"^([.\w$]+):")
+func_re = re.compile(r"^[A-Za-z_][\w.$]*:")
+
+
+def regs(op):
+    out = []
+    for m in reg_re.finditer(op):
+        if m.group(1):
+            out += list(range(int(m.group(1)), int(m.group(2)) + 1))
+        else:
+            out.append(int(m.group(3)))
+    return out
+
+
+def functions(lines):
+    fns, cur = [], None
+    for line in lines:
+        s = line.rstrip("\n")
+        t = s.strip()
+        if func_re.match(t) and not t.startswith("."):
+            cur = (t[:-1], [])
+            fns.append(cur)
+            continue
+        if cur is not None:
+            cur[1].append(t)
+    return fns
+
+
+def ws_of(t):
+    m = re.match(r"s_nop\s+(\d+)", t)
+    return int(m.group(1)) + 1 if m else 1
+
+
+def walk(body, incoming, report):
+    """pending: vgpr -> (VALU wait states still required, mfma text, how many fewer a memory read needs).
+    Returns the branch edges."""
+    edges = {}
+    pending = {}
+    bad = 0
+    in_asm, asm_count = False, 0
+    for t in body:
+        if t.startswith(";;#ASMSTART"):
+            in_asm, asm_count = True, 0
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if not t or t.startswith(";") or t.startswith("."):
+            continue
+        m = label_re.match(t)
+        if m:
+            for r, (need, src, d) in incoming.get(m.group(1), {}).items():
+                if need > pending.get(r, (0, "", 0))[0]:
+                    pending[r] = (need, src, d)
+            continue
+        code = t.split(";")[0].strip()
+        if not code:
+            continue
+        op = code.split()[0]
+        args = code[len(op):]
+        parts = [p.strip() for p in args.split(",")] if args.strip() else []
+        if op.startswith("v_mfma"):
+            # an MFMA reading an in-flight D as A/B is a hazard too; as SrcC (same shape, chained) it is not
+            srcs = parts[1:3]
+            for p in srcs:
+                for r in regs(p):
+                    if r in pending:
+                        if report:
+                            print(f"  {code}  reads v{r} of `{pending[r][1]}` with {pending[r][0]} wait states left")
+                        bad += 1
+            step = ws_of(code)
+            pending = {r: (n - step, s, d) for r, (n, s, d) in pending.items() if n - step > 0}
+            need_valu, need_mem = REQUIRED.get(op, DEFAULT_REQUIRED)
+            for r in regs(parts[0]) if parts else []:
+                pending[r] = (need_valu, code, need_valu - need_mem)
+            continue
+        if pending and not op.startswith("s_"):
+            # the first operand of a VALU op or a load is its destination; every operand of a store is read
+            srcs = parts[1:] if op.startswith(("v_", "ds_read", "ds_load", "global_load", "buffer_load",
+                                                "flat_load", "scratch_load")) else parts
+            if op.startswith(("buffer_store", "global_store", "flat_store", "ds_write", "ds_store", "scratch_store")):
+                srcs = parts
+            mem = op.startswith(MEM_OPS)
+            for p in srcs:
+                for r in regs(p):
+                    if r in pending:
+                        left = pending[r][0] - (pending[r][2] if mem else 0)
+                        if left <= 0:
+                            continue
+                        if report:
+                            print(f"  {code}  reads v{r} of `{pending[r][1]}` with {left} wait states left")
+                        bad += 1
+        step = ws_of(code)
+        pending = {r: (n - step, s, d) for r, (n, s, d) in pending.items() if n - step > 0}
+        if op.startswith(("s_branch", "s_cbranch")) and parts:
+            tgt = parts[-1]
+            e = edges.setdefault(tgt, {})
+            for r, (n, s, d) in pending.items():
+                if n - 1 > e.get(r, (0, "", 0))[0]:
+                    e[r] = (n - 1, s, d)
+    return edges, bad
+
+
+def check(path, want=""):
+    total = 0
+    for name, body in functions(open(path).read().splitlines()):
+        if want and want not in name:
+            continue
+        incoming = {}
+        for _ in range(4):   # propagate branch edges to a fixed point (loops)
+            edges, _ = walk(body, incoming, False)
+            if edges == incoming:
+                break
+            incoming = edges
+        _, bad = walk(body, incoming, False)
+        if bad:
+            print(f"{name}: {bad} read(s) of an MFMA result inside its window")
+            walk(body, incoming, True)
+        total += bad
+    return total
+
+
+if __name__ == "__main__":
+    n = check(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")
+    print(f"{n} MFMA-result read hazard(s)")
+    sys.exit(1 if n else 0)

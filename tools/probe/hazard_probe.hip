@@ -10,6 +10,7 @@
 //   T3  v_mfma_i32_16x16x64_i8 with D exactly over A (the pattern tools/mfma_overlap.py reports in
 //       describe_kernel), result read after 18 wait states, vs a D elsewhere;
 //   T5  v_mfma_i32_16x16x64_i8 result read by a VALU K wait states after issue: the hardware's window;
+//   T6/T7  WAR: a VALU overwrites the MFMA's SrcA / SrcC K wait states after its issue;
 //   T4  positive control: VALU write -> DPP read of the same VGPR with 0 wait states (a documented
 //       hazard: 2 wait states required) -- shows the probe can see a hazard at all.
 // Every lane computes a known answer; the kernel counts lanes whose result differs.  No scalar stores.
@@ -121,6 +122,50 @@ __device__ __forceinline__ int mfma_raw(int k, i4v a, i4v b) {
     }
 }
 
+// WAR: a VALU overwrites an MFMA source K wait states after the MFMA issue -- SrcA (v44) for T6, SrcC (v52,
+// D elsewhere) for T7; the product is read 24+ wait states later and compared with the undisturbed one.
+#define MFMA_WAR(K, NOPS)                                                                                   \
+    __device__ __noinline__ int mfma_war_a_##K(i4v a, i4v b) {                                             \
+        int r;                                                                                              \
+        asm volatile("v_mov_b32 v44, %1\n\tv_mov_b32 v45, %2\n\tv_mov_b32 v46, %3\n\tv_mov_b32 v47, %4\n\t"  \
+                     "v_mov_b32 v48, %5\n\tv_mov_b32 v49, %6\n\tv_mov_b32 v50, %7\n\tv_mov_b32 v51, %8\n\ts_nop 4\n\t" \
+                     "v_mfma_i32_16x16x64_i8 v[56:59], v[44:47], v[48:51], 0\n\t" NOPS                        \
+                     "v_mov_b32 v44, 0x5a5a5a5a\n\tv_mov_b32 v47, 0x12345678\n\t"                            \
+                     "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tv_mov_b32 %0, v56\n\ts_nop 4"                        \
+                     : "=v"(r) : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w) \
+                     : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v56", "v57", "v58", "v59");     \
+        return r;                                                                                           \
+    }                                                                                                       \
+    __device__ __noinline__ int mfma_war_c_##K(i4v a, i4v b) {                                             \
+        int r;                                                                                              \
+        asm volatile("v_mov_b32 v44, %1\n\tv_mov_b32 v45, %2\n\tv_mov_b32 v46, %3\n\tv_mov_b32 v47, %4\n\t"  \
+                     "v_mov_b32 v48, %5\n\tv_mov_b32 v49, %6\n\tv_mov_b32 v50, %7\n\tv_mov_b32 v51, %8\n\t"  \
+                     "v_mov_b32 v52, 0x8000\n\tv_mov_b32 v53, 0x8000\n\tv_mov_b32 v54, 0x8000\n\tv_mov_b32 v55, 0x8000\n\ts_nop 4\n\t" \
+                     "v_mfma_i32_16x16x64_i8 v[56:59], v[44:47], v[48:51], v[52:55]\n\t" NOPS                 \
+                     "v_mov_b32 v52, 0x77777\n\tv_mov_b32 v55, 0x33333\n\t"                                    \
+                     "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tv_mov_b32 %0, v56\n\ts_nop 4"                        \
+                     : "=v"(r) : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w) \
+                     : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", \
+                       "v57", "v58", "v59");                                                                    \
+        return r;                                                                                           \
+    }
+MFMA_WAR(0, "")
+MFMA_WAR(2, "s_nop 1\n\t")
+MFMA_WAR(4, "s_nop 3\n\t")
+MFMA_WAR(8, "s_nop 7\n\t")
+MFMA_WAR(12, "s_nop 7\n\ts_nop 3\n\t")
+MFMA_WAR(20, "s_nop 7\n\ts_nop 7\n\ts_nop 3\n\t")
+__device__ __forceinline__ int mfma_war(int c, int k, i4v a, i4v b) {
+    switch (k) {
+        case 0: return c ? mfma_war_c_0(a, b) : mfma_war_a_0(a, b);
+        case 2: return c ? mfma_war_c_2(a, b) : mfma_war_a_2(a, b);
+        case 4: return c ? mfma_war_c_4(a, b) : mfma_war_a_4(a, b);
+        case 8: return c ? mfma_war_c_8(a, b) : mfma_war_a_8(a, b);
+        case 12: return c ? mfma_war_c_12(a, b) : mfma_war_a_12(a, b);
+        default: return c ? mfma_war_c_20(a, b) : mfma_war_a_20(a, b);
+    }
+}
+
 // VALU write then DPP read of the written VGPR (quad_perm [1,0,3,2]), 0 or 4 wait states
 __device__ __forceinline__ unsigned dpp_after_write(unsigned v, int nop) {
     unsigned r;
@@ -167,6 +212,13 @@ __global__ __launch_bounds__(256) void probe(int test, int nop, int iters, const
             const i4v A = {(int)ab, (int)(ab >> 32), (int)(ab * 3), (int)(bb ^ ab)};
             const i4v B = {(int)bb, (int)(bb >> 32), (int)(bb * 5), (int)(ab + bb)};
             const int r = mfma_raw(nop, A, B), e = mfma_raw(20, A, B);
+            nb += r != e;
+            acc += (unsigned)r;
+        } else if (test == 6 || test == 7) {
+            const unsigned long long ab = __double_as_longlong(a), bb = __double_as_longlong(b);
+            const i4v A = {(int)ab, (int)(ab >> 32), (int)(ab * 3), (int)(bb ^ ab)};
+            const i4v B = {(int)bb, (int)(bb >> 32), (int)(bb * 5), (int)(ab + bb)};
+            const int r = mfma_war(test == 7, nop, A, B), e = mfma_war(test == 7, 20, A, B);
             nb += r != e;
             acc += (unsigned)r;
         } else if (test == 4) {
@@ -221,5 +273,16 @@ int main(int argc, char** argv) {
         printf("T5 mfma i8 16x16x64 -> VALU read after %2d wait states: %llu mismatches of %llu\n", k, nb,
                (unsigned long long)blocks * 256 * (iters / 4));
     }
+    const int kw[] = {0, 2, 4, 8, 12};
+    for (int test = 6; test <= 7; test++)
+        for (int k : kw) {
+            hipMemset(bad, 0, 8);
+            hipLaunchKernelGGL(probe, dim3(blocks), dim3(256), 0, 0, test, k, iters / 4, da, db, dc, bad, sink);
+            if (hipDeviceSynchronize() != hipSuccess) { printf("kernel error\n"); return 2; }
+            unsigned long long nb = 0;
+            hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+            printf("T%d mfma i8 16x16x64, VALU overwrites Src%s after %2d wait states: %llu mismatches of %llu\n", test,
+                   test == 6 ? "A" : "C", k, nb, (unsigned long long)blocks * 256 * (iters / 4));
+        }
     return 0;
 }
