@@ -11,6 +11,7 @@
 //       describe_kernel), result read after 18 wait states, vs a D elsewhere;
 //   T5  v_mfma_i32_16x16x64_i8 result read by a VALU K wait states after issue: the hardware's window;
 //   T6/T7  WAR: a VALU overwrites the MFMA's SrcA / SrcC K wait states after its issue;
+//   T8/T9  D partially over SrcA / SrcB (the DESC_ANGLE_MFMA=0 build's allocation);
 //   T4  positive control: VALU write -> DPP read of the same VGPR with 0 wait states (a documented
 //       hazard: 2 wait states required) -- shows the probe can see a hazard at all.
 // Every lane computes a known answer; the kernel counts lanes whose result differs.  No scalar stores.
@@ -166,6 +167,27 @@ __device__ __forceinline__ int mfma_war(int c, int k, i4v a, i4v b) {
     }
 }
 
+// D partially over a source: D = v[46:49] over SrcA v[44:47] (T8), D = v[50:53] over SrcB v[48:51] (T9),
+// vs D = v[52:55] (no overlap); C = 0.  The allocation of the DESC_ANGLE_MFMA=0 describe build
+// (`v_mfma_i32_16x16x64_i8 v[14:17], v[16:19], v[6:9], ...`), the one build that reproduces the
+// round-4 nondeterminism.  Every D element compared.
+#define MFMA_PART(NAME, D, D0, D1, D2, D3, ...)                                                           \
+    __device__ __noinline__ i4v NAME(i4v a, i4v b) {                                                       \
+        i4v r;                                                                                              \
+        asm volatile("v_mov_b32 v44, %4\n\tv_mov_b32 v45, %5\n\tv_mov_b32 v46, %6\n\tv_mov_b32 v47, %7\n\t"  \
+                     "v_mov_b32 v48, %8\n\tv_mov_b32 v49, %9\n\tv_mov_b32 v50, %10\n\tv_mov_b32 v51, %11\n\ts_nop 4\n\t" \
+                     "v_mfma_i32_16x16x64_i8 " D ", v[44:47], v[48:51], 0\n\t"                                \
+                     "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"                                                      \
+                     "v_mov_b32 %0, " D0 "\n\tv_mov_b32 %1, " D1 "\n\tv_mov_b32 %2, " D2 "\n\tv_mov_b32 %3, " D3 "\n\ts_nop 4" \
+                     : "=v"(r.x), "=v"(r.y), "=v"(r.z), "=v"(r.w)                                           \
+                     : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)       \
+                     : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", __VA_ARGS__);                  \
+        return r;                                                                                           \
+    }
+MFMA_PART(mfma_part_a, "v[46:49]", "v46", "v47", "v48", "v49", "v52")
+MFMA_PART(mfma_part_b, "v[50:53]", "v50", "v51", "v52", "v53", "v54")
+MFMA_PART(mfma_part_none, "v[52:55]", "v52", "v53", "v54", "v55", "v56")
+
 // VALU write then DPP read of the written VGPR (quad_perm [1,0,3,2]), 0 or 4 wait states
 __device__ __forceinline__ unsigned dpp_after_write(unsigned v, int nop) {
     unsigned r;
@@ -221,6 +243,14 @@ __global__ __launch_bounds__(256) void probe(int test, int nop, int iters, const
             const int r = mfma_war(test == 7, nop, A, B), e = mfma_war(test == 7, 20, A, B);
             nb += r != e;
             acc += (unsigned)r;
+        } else if (test == 8 || test == 9) {
+            const unsigned long long ab = __double_as_longlong(a), bb = __double_as_longlong(b);
+            const i4v A = {(int)ab, (int)(ab >> 32), (int)(ab * 3), (int)(bb ^ ab)};
+            const i4v B = {(int)bb, (int)(bb >> 32), (int)(bb * 5), (int)(ab + bb)};
+            const i4v r = test == 8 ? mfma_part_a(A, B) : mfma_part_b(A, B);
+            const i4v e = mfma_part_none(A, B);
+            nb += (r.x != e.x) + (r.y != e.y) + (r.z != e.z) + (r.w != e.w);
+            acc += (unsigned)r.x;
         } else if (test == 4) {
             const unsigned v = (unsigned)__double_as_longlong(a) + (unsigned)it;
             const unsigned r = dpp_after_write(v, nop);
@@ -272,6 +302,15 @@ int main(int argc, char** argv) {
         hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
         printf("T5 mfma i8 16x16x64 -> VALU read after %2d wait states: %llu mismatches of %llu\n", k, nb,
                (unsigned long long)blocks * 256 * (iters / 4));
+    }
+    for (int test = 8; test <= 9; test++) {
+        hipMemset(bad, 0, 8);
+        hipLaunchKernelGGL(probe, dim3(blocks), dim3(256), 0, 0, test, 0, iters, da, db, dc, bad, sink);
+        if (hipDeviceSynchronize() != hipSuccess) { printf("kernel error\n"); return 2; }
+        unsigned long long nb = 0;
+        hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+        printf("T%d mfma i8 16x16x64, D partially over Src%s: %llu element mismatches of %llu\n", test, test == 8 ? "A" : "B",
+               nb, 4ull * blocks * 256 * iters);
     }
     const int kw[] = {0, 2, 4, 8, 12};
     for (int test = 6; test <= 7; test++)
