@@ -12,6 +12,7 @@
 //   T5  v_mfma_i32_16x16x64_i8 result read by a VALU K wait states after issue: the hardware's window;
 //   T6/T7  WAR: a VALU overwrites the MFMA's SrcA / SrcC K wait states after its issue;
 //   T8/T9  D partially over SrcA / SrcB (the DESC_ANGLE_MFMA=0 build's allocation);
+//   T10/T11  an LDS load (VALU write) over SrcA of an MFMA queued behind 0-3 others (the angold build);
 //   T4  positive control: VALU write -> DPP read of the same VGPR with 0 wait states (a documented
 //       hazard: 2 wait states required) -- shows the probe can see a hazard at all.
 // Every lane computes a known answer; the kernel counts lanes whose result differs.  No scalar stores.
@@ -188,6 +189,46 @@ MFMA_PART(mfma_part_a, "v[46:49]", "v46", "v47", "v48", "v49", "v52")
 MFMA_PART(mfma_part_b, "v[50:53]", "v50", "v51", "v52", "v53", "v54")
 MFMA_PART(mfma_part_none, "v[52:55]", "v52", "v53", "v54", "v55", "v56")
 
+// The DESC_ANGLE_MFMA=0 describe build (the reproducible nondeterministic one) issues three MFMAs back to
+// back and then a `ds_read_b128` whose destination overlaps the third MFMA's SrcA:
+//     v_mfma v[32:35], v[16:19], ... ; v_mfma v[36:39], v[16:19], ... ; v_mfma v[14:17], v[16:19], ...
+//     ds_read_b128 v[18:21], v40 offset:1536
+// T10: NPRE MFMAs (0-3) on other registers, then the victim MFMA reading SrcA v[44:47], then an LDS load
+// (or a VALU write for T11) into v[46:49] K wait states later; the victim's D vs the undisturbed product.
+#define MFMA_LDS_WAR(NAME, PRE, OVW)                                                                         \
+    __device__ __noinline__ int NAME(i4v a, i4v b, unsigned lds_addr) {                                    \
+        int r;                                                                                               \
+        asm volatile("v_mov_b32 v44, %1\n\tv_mov_b32 v45, %2\n\tv_mov_b32 v46, %3\n\tv_mov_b32 v47, %4\n\t"   \
+                     "v_mov_b32 v48, %5\n\tv_mov_b32 v49, %6\n\tv_mov_b32 v50, %7\n\tv_mov_b32 v51, %8\n\t"   \
+                     "v_mov_b32 v60, %5\n\tv_mov_b32 v61, %6\n\tv_mov_b32 v62, %7\n\tv_mov_b32 v63, %8\n\ts_nop 4\n\t" \
+                     PRE                                                                                      \
+                     "v_mfma_i32_16x16x64_i8 v[52:55], v[44:47], v[60:63], 0\n\t"                              \
+                     OVW                                                                                      \
+                     "s_waitcnt lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"               \
+                     "v_mov_b32 %0, v52\n\ts_nop 4"                                                           \
+                     : "=v"(r)                                                                                \
+                     : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(lds_addr) \
+                     : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56",  \
+                       "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69",  \
+                       "v70", "v71", "memory");                                                               \
+        return r;                                                                                            \
+    }
+#define PRE0 ""
+#define PRE1 "v_mfma_i32_16x16x64_i8 v[64:67], v[48:51], v[60:63], 0\n\t"
+#define PRE3 "v_mfma_i32_16x16x64_i8 v[64:67], v[48:51], v[60:63], 0\n\tv_mfma_i32_16x16x64_i8 v[68:71], v[48:51], v[60:63], 0\n\tv_mfma_i32_16x16x64_i8 v[56:59], v[48:51], v[60:63], 0\n\t"
+#define OVW_LDS "ds_read_b128 v[46:49], %9\n\t"
+#define OVW_LDS4 "s_nop 3\n\tds_read_b128 v[46:49], %9\n\t"
+#define OVW_LDS16 "s_nop 7\n\ts_nop 7\n\tds_read_b128 v[46:49], %9\n\t"
+#define OVW_VALU "v_mov_b32 v46, 0x5a5a5a5a\n\tv_mov_b32 v47, 0x12345678\n\t"
+#define OVW_NONE ""
+MFMA_LDS_WAR(war_lds_p0, PRE0, OVW_LDS)
+MFMA_LDS_WAR(war_lds_p1, PRE1, OVW_LDS)
+MFMA_LDS_WAR(war_lds_p3, PRE3, OVW_LDS)
+MFMA_LDS_WAR(war_lds_p3k4, PRE3, OVW_LDS4)
+MFMA_LDS_WAR(war_lds_p3k16, PRE3, OVW_LDS16)
+MFMA_LDS_WAR(war_valu_p3, PRE3, OVW_VALU)
+MFMA_LDS_WAR(war_none_p3, PRE3, OVW_NONE)
+
 // VALU write then DPP read of the written VGPR (quad_perm [1,0,3,2]), 0 or 4 wait states
 __device__ __forceinline__ unsigned dpp_after_write(unsigned v, int nop) {
     unsigned r;
@@ -198,6 +239,37 @@ __device__ __forceinline__ unsigned dpp_after_write(unsigned v, int nop) {
         asm volatile("v_add_u32 v56, %1, 1\n\tv_mov_b32_dpp %0, v56 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\ts_nop 4"
                      : "=v"(r) : "v"(v) : "v56");
     return r;
+}
+
+__global__ __launch_bounds__(256) void probe_war(int variant, int iters, const double* __restrict__ da,
+                                                const double* __restrict__ db, unsigned long long* __restrict__ bad,
+                                                unsigned long long* __restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) unsigned lds[256 * 4];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = 0; k < 4; k++) lds[threadIdx.x * 4 + k] = 0xdeadbeefu ^ (threadIdx.x * 4 + k) * 0x9e3779b9u;
+    __syncthreads();
+    const unsigned addr = (unsigned)(threadIdx.x * 16);
+    unsigned long long nb = 0, acc = 0;
+    for (int it = 0; it < iters; it++) {
+        const int i = (t * 7 + it * 131) & 4095;
+        const unsigned long long ab = __double_as_longlong(da[i]), bb = __double_as_longlong(db[i]);
+        const i4v A = {(int)ab, (int)(ab >> 32), (int)(ab * 3), (int)(bb ^ ab)};
+        const i4v B = {(int)bb, (int)(bb >> 32), (int)(bb * 5), (int)(ab + bb)};
+        int r;
+        switch (variant) {
+            case 0: r = war_lds_p0(A, B, addr); break;
+            case 1: r = war_lds_p1(A, B, addr); break;
+            case 2: r = war_lds_p3(A, B, addr); break;
+            case 3: r = war_lds_p3k4(A, B, addr); break;
+            case 4: r = war_lds_p3k16(A, B, addr); break;
+            default: r = war_valu_p3(A, B, addr); break;
+        }
+        const int e = war_none_p3(A, B, addr);
+        nb += r != e;
+        acc += (unsigned)r;
+    }
+    if (nb) atomicAdd(bad, nb);
+    sink[t & 1023] = acc;
 }
 
 __global__ __launch_bounds__(256) void probe(int test, int nop, int iters, const double* __restrict__ da,
@@ -311,6 +383,20 @@ int main(int argc, char** argv) {
         hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
         printf("T%d mfma i8 16x16x64, D partially over Src%s: %llu element mismatches of %llu\n", test, test == 8 ? "A" : "B",
                nb, 4ull * blocks * 256 * iters);
+    }
+    const char* wn[] = {"T10 LDS load over SrcA right after the MFMA, no MFMA ahead",
+                        "T10 LDS load over SrcA right after the MFMA, 1 MFMA ahead",
+                        "T10 LDS load over SrcA right after the MFMA, 3 MFMAs ahead",
+                        "T10 LDS load over SrcA 4 wait states after, 3 MFMAs ahead",
+                        "T10 LDS load over SrcA 16 wait states after, 3 MFMAs ahead",
+                        "T11 VALU write over SrcA right after the MFMA, 3 MFMAs ahead"};
+    for (int v = 0; v < 6; v++) {
+        hipMemset(bad, 0, 8);
+        hipLaunchKernelGGL(probe_war, dim3(blocks), dim3(256), 0, 0, v, iters, da, db, bad, sink);
+        if (hipDeviceSynchronize() != hipSuccess) { printf("kernel error\n"); return 2; }
+        unsigned long long nb = 0;
+        hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+        printf("%-64s: %llu mismatches of %llu\n", wn[v], nb, (unsigned long long)blocks * 256 * iters);
     }
     const int kw[] = {0, 2, 4, 8, 12};
     for (int test = 6; test <= 7; test++)
