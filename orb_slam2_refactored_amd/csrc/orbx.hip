@@ -1699,11 +1699,109 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
 #endif
     // ---- gather candidates in cell raster order (DetectFAST push_back order).  Pass 1: total count;
     //      the arrays live in LDS when they fit.  Pass 2: one lane per cell copies its points.
+    // Root id of a keypoint (:562-569): (int)(((float)x - roi.x) / hx) in double; monotone in x.
+    const int R = L.nroots;
+    auto root_x = [&](int x) -> int {
+        const float dx = (float)x - (float)L.rx;   // keypoint.pt.x - roi.x (float)
+        return (int)((double)dx / L.hx);
+    };
+    if (threadIdx.x < MAX_ROOTS) rc[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_fail = 0;
     int n_total = 0, carry = 0;
-    if (L.ncells <= 4 * (int)blockDim.x) {
+    bool parted = false;   // the gather below writes the root-partitioned order itself (round 5)
+    if (L.ncells <= 4 * (int)blockDim.x && R <= 4) {
         // thread t owns cells 4t .. 4t+3 (raster order): their counts and slot offsets are loaded
-        // together, one block reduction picks LDS or global candidate arrays, one block scan places
-        // the threads' runs, and every thread's first 8 points per cell are loaded in one batch
+        // together and the points go straight to their root's segment.  A cell whose zone lies inside
+        // one root (all but the cells on a root boundary) sends all its points there, a boundary cell
+        // splits them by x; one block scan per root (R <= 4) of the threads' counts places the threads'
+        // runs, so each segment keeps the gather order: the stable partition of :547-579 without the
+        // round trip through T.  Every thread's first 8 points per cell are loaded in one batch.
+        const int i0 = 4 * threadIdx.x;
+        int cv[4], cs[4], rl[4], rh[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int i = i0 + k;
+            cv[k] = 0; cs[k] = 0; rl[k] = 0; rh[k] = 0;
+            if (i < L.ncells) {
+                const CellDev cd = cells[L.cell_base + i];
+                cv[k] = ccell[i];
+                cs[k] = cd.slot;
+                const int zx = (cd.x0y0 & 0xffff) + 3;            // the zone's first column
+                rl[k] = root_x(zx);
+                rh[k] = root_x(zx + (cd.zwzh & 0xffff) - 1);     // and its last
+            }
+        }
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) bad |= cv[k] > 0 && (rl[k] < 0 || rh[k] >= R);
+        if (bad) atomicOr(fault, FAULT_QT_ROOT);
+        int cnt[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (rl[k] == rh[k]) {
+#pragma unroll
+                for (int rt = 0; rt < 4; rt++) cnt[rt] += rl[k] == rt ? cv[k] : 0;
+            } else {   // a boundary cell (rare): its points' roots
+                for (int q = 0; q < cv[k]; q++) {
+                    const int rt = root_x(kp_x(fslots[cs[k] + q]));
+#pragma unroll
+                    for (int u = 0; u < 4; u++) cnt[u] += rt == u;
+                }
+            }
+        }
+        int run[4];
+        int base = 0;
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++) {
+            if (rt >= R) { run[rt] = 0; continue; }   // block-uniform
+            int tot;
+            run[rt] = base + block_excl_scan(cnt[rt], tmp, &tot);
+            if (threadIdx.x == 0) rc[rt] = tot;
+            base += tot;
+        }
+        n_total = base;
+        if (n_total <= PTC) { P = lds_P; T = lds_T; }
+        uint32_t r[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[k][q] = q < cv[k] ? fslots[cs[k] + q] : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (rl[k] == rh[k]) {
+                int o = run[0];
+#pragma unroll
+                for (int rt = 1; rt < 4; rt++) o = rl[k] == rt ? run[rt] : o;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (q < cv[k]) P[o + q] = r[k][q];
+                for (int q0 = 8; q0 < cv[k]; q0 += 8) {   // > 8 points in a cell: batches of 8 loads
+                    uint32_t r2[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) r2[q] = q0 + q < cv[k] ? fslots[cs[k] + q0 + q] : 0u;
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (q0 + q < cv[k]) P[o + q0 + q] = r2[q];
+                }
+#pragma unroll
+                for (int rt = 0; rt < 4; rt++) run[rt] += rl[k] == rt ? cv[k] : 0;
+            } else {
+                for (int q = 0; q < cv[k]; q++) {
+                    const uint32_t kk = fslots[cs[k] + q];
+                    const int rt = root_x(kp_x(kk));
+                    int o = run[0];
+#pragma unroll
+                    for (int u = 1; u < 4; u++) o = rt == u ? run[u] : o;
+                    P[o] = kk;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) run[u] += rt == u;
+                }
+            }
+        }
+        carry = n_total;
+        parted = true;
+    } else if (L.ncells <= 4 * (int)blockDim.x) {
+        // (more than 4 roots: an aspect ratio above 4.5) the gather in raster order, partitioned below
         const int i0 = 4 * threadIdx.x;
         int cv[4], cs[4];
 #pragma unroll
@@ -1715,18 +1813,10 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
         const int sum = cv[0] + cv[1] + cv[2] + cv[3];
         const int ex = block_excl_scan(sum, tmp, &n_total);
         if (n_total <= PTC) { P = lds_P; T = lds_T; }
-        uint32_t r[4][8];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int q = 0; q < 8; q++) r[k][q] = q < cv[k] ? fslots[cs[k] + q] : 0u;
         int o = ex;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-                if (q < cv[k]) P[o + q] = r[k][q];
-            for (int q0 = 8; q0 < cv[k]; q0 += 8) {   // > 8 points in a cell: batches of 8 loads
+            for (int q0 = 0; q0 < cv[k]; q0 += 8) {
                 uint32_t r2[8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) r2[q] = q0 + q < cv[k] ? fslots[cs[k] + q0 + q] : 0u;
@@ -1777,15 +1867,10 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
     }
     __syncthreads();
 
-    // ---- root nodes (:547-579): stable partition by root id
-    const int R = L.nroots;
-    if (threadIdx.x < MAX_ROOTS) rc[threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_fail = 0;
-    __syncthreads();
-    auto root_of = [&](uint32_t k) -> int {
-        const float dx = (float)kp_x(k) - (float)L.rx;   // keypoint.pt.x - roi.x (float)
-        return (int)((double)dx / L.hx);
-    };
+    // ---- root nodes (:547-579): stable partition by root id (the large-grid gather's order; the
+    //      small-grid gather above wrote the partitioned order itself)
+    if (!parted) {   // block-uniform
+    auto root_of = [&](uint32_t k) -> int { return root_x(kp_x(k)); };
     // every wave partitions a contiguous quarter (root ids kept in registers between the passes);
     // quarter q's base offset per root = that root's count over quarters < q -> stable overall
     __shared__ int s_rcnt[4][MAX_ROOTS];
@@ -1877,6 +1962,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
         P = T;
         T = t;
     }
+    }   // !parted
     if (threadIdx.x == 0) {
         int n = 0, acc = 0;
         for (int q = 0; q < R; q++) {

@@ -30,6 +30,8 @@ REQUIRED = {
 }
 DEFAULT_REQUIRED = (19, 19)
 MEM_OPS = ("ds_", "buffer_", "global_", "flat_", "scratch_")
+# a load issued within this many wait states of an MFMA must not write that MFMA's sources
+WAR_WINDOW = 16
 
 reg_re = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b")
 label_re = re.compile(r"^([.\w$]+):")
@@ -135,6 +137,47 @@ def walk(body, incoming, report):
     return edges, bad
 
 
+LOAD_OPS = ("ds_read", "ds_load", "buffer_load", "global_load", "flat_load", "scratch_load")
+
+
+def war_loads(body, window, report):
+    """Loads (asynchronous VGPR writes) whose destination overlaps a SrcA / SrcB / SrcC register of an
+    MFMA issued within the previous `window` wait states (straight-line order; a label or branch ends
+    the window).  Returns the count."""
+    recent = []   # (wait states since issue, set of source vgprs, mfma text)
+    bad = 0
+    for t in body:
+        if not t or t.startswith(";") or t.startswith("."):
+            continue
+        if label_re.match(t):
+            recent = []
+            continue
+        code = t.split(";")[0].strip()
+        if not code:
+            continue
+        op = code.split()[0]
+        args = code[len(op):]
+        parts = [p.strip() for p in args.split(",")] if args.strip() else []
+        if op.startswith(LOAD_OPS) and parts:
+            dst = set(regs(parts[0]))
+            for age, srcs, txt in recent:
+                hit = dst & srcs
+                if hit:
+                    bad += 1
+                    if report:
+                        print(f"  {code}  overwrites v{min(hit)} read by `{txt}` {age} wait states after its issue")
+        step = ws_of(code)
+        recent = [(a + step, s_, x) for a, s_, x in recent if a + step < window]
+        if op.startswith("v_mfma") and len(parts) >= 4:
+            srcs = set()
+            for p in parts[1:4]:
+                srcs |= set(regs(p))
+            recent.append((0, srcs, code))
+        if op.startswith(("s_branch", "s_cbranch", "s_setpc", "s_swappc")):
+            recent = []
+    return bad
+
+
 def check(path, want=""):
     total = 0
     for name, body in functions(open(path).read().splitlines()):
@@ -150,7 +193,11 @@ def check(path, want=""):
         if bad:
             print(f"{name}: {bad} read(s) of an MFMA result inside its window")
             walk(body, incoming, True)
-        total += bad
+        wb = war_loads(body, WAR_WINDOW, False)
+        if wb:
+            print(f"{name}: {wb} load(s) over the source of an MFMA in flight")
+            war_loads(body, WAR_WINDOW, True)
+        total += bad + wb
     return total
 
 
