@@ -2570,8 +2570,13 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     const float ang = angle * factorPI;
     float a, b;   // (float)::cos / ::sin((double)ang) or cosf / sinf, sincos_f.h (each checked on every float in range)
     DESC_STAMP(3);
+#ifdef DESC_SINCOS_COST_DIAG   // diagnostic A/B only: hardware sin / cos (inexact) to price the exact path
+    a = __cosf(ang);
+    b = __sinf(ang);
+#else
     if (TRIG) sincosf_glibc(ang, &b, &a);
     else sincos_f2d(ang, &b, &a);
+#endif
     DESC_STAMP(4);
     auto sample = [&](float x, float y) -> int {
         // byte offset of blurred pixel (18 + dy, 18 + dx) from the rounded floats (exact integers)

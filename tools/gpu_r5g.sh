@@ -22,4 +22,11 @@ for kind in pan textured; do
     done
   done
 done
+for i in 1 2; do
+  for v in new cheapsc; do
+    if [ $v = cheapsc ]; then export ORBSLAM2_AMD_LIB=$PWD/tools/ab/lib_cheapsc.so; else unset ORBSLAM2_AMD_LIB; fi
+    timeout -k 10 120 python tools/kbench.py --frames 2048 --iters 5 --pan > gpurun_out/kb.log 2>&1 || { tail gpurun_out/kb.log; exit 8; }
+    sed "s/^/sincos-cost pan $v: /" gpurun_out/kb.log | tail -1
+  done
+done
 echo "session done"
