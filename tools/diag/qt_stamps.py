@@ -37,7 +37,9 @@ while 3 + 2 * i < 63 and v[3 + 2 * i] > 0 and 4 + 2 * i < 64:
     i += 1
 print("end", v[63] - t0, "(+", v[63] - prev, ")   [s_memtime ticks]")
 
-wg = np.array(list(buf)[64:64 + 2 * F * 8], dtype=np.int64).reshape(F, 8, 2)
+# g_qt_wg holds 4096 (frame, level) workgroups: frames past 4096 / 8 = 512 are not recorded
+Fw = min(F, 4096 // 8)
+wg = np.array(list(buf)[64:64 + 2 * Fw * 8], dtype=np.int64).reshape(Fw, 8, 2)
 dur = wg[:, :, 1] - wg[:, :, 0]
 for l in range(8):
     print(f"level {l}: WG ticks mean {dur[:, l].mean():8.0f} max {dur[:, l].max():8.0f}")
