@@ -2575,7 +2575,7 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     b = __sinf(ang);
 #else
     if (TRIG) sincosf_glibc(ang, &b, &a);
-    else sincos_f2d(ang, &b, &a);
+    else sincos_f2d_t<true>(ang, &b, &a);   // ang is wave-uniform (one keypoint per wavefront)
 #endif
     DESC_STAMP(4);
     auto sample = [&](float x, float y) -> int {

@@ -1,7 +1,8 @@
 // Compares orbamd::sincos_f2d against glibc (float)sin / (float)cos of (double)x (mode d, default) or
 // orbamd::sincosf_glibc against glibc sinf / cosf (mode f) for every float x in [lo, hi) (default
 // [0, 6.2832]), split over threads.  Build: g++ -O2 -ffp-contract=off -pthread.
-// Usage: sincos_check [threads] [step] [d|f]
+// Usage: sincos_check [threads] [step] [d|f|l]   (d: the table form sincos_f2d, l: the fdlibm form
+// sincos_f2d_fdlibm, both against (float)sin / cos((double)x); f: sincosf_glibc against sinf / cosf)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +18,7 @@ int main(int argc, char** argv) {
     int nt = argc > 1 ? atoi(argv[1]) : 8;
     unsigned step = argc > 2 ? (unsigned)atoi(argv[2]) : 1;   // test every step-th float
     const bool fmode = argc > 3 && argv[3][0] == 'f';
+    const bool lmode = argc > 3 && argv[3][0] == 'l';
     unsigned a, b;
     memcpy(&a, &lo, 4);
     memcpy(&b, &hi, 4);
@@ -35,7 +37,8 @@ int main(int argc, char** argv) {
                     rs = ::sinf(x);
                     rc = ::cosf(x);
                 } else {
-                    orbamd::sincos_f2d(x, &s, &c);
+                    if (lmode) orbamd::sincos_f2d_fdlibm(x, &s, &c);
+                    else orbamd::sincos_f2d(x, &s, &c);
                     rs = (float)::sin((double)x);
                     rc = (float)::cos((double)x);
                 }
