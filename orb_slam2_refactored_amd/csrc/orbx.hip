@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         crop_stage_rows<CST>(src, lane, crop, CSd);
     }
     const int tlo = min(th_ini, th_min);
-    bool spec = spec_min > 0 && th_ini > tlo && prev_ini >= spec_min;
+    bool spec = spec_min != 0 && th_ini > tlo && prev_ini >= spec_min;   // spec_min < 0: every cell
     uint8_t* Mc = Mz + ZSd + 1;   // zone (0, 0); the zero border makes out-of-zone neighbours read 0
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
     const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
@@ -3302,7 +3302,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->p = *params;
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
-    if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(0, atoi(e));
+    if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(-1, atoi(e));   // -1: every cell
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;

@@ -29,4 +29,14 @@ for i in 1 2; do
     sed "s/^/sincos-cost pan $v: /" gpurun_out/kb.log | tail -1
   done
 done
+unset ORBSLAM2_AMD_LIB
+for kind in pan textured; do
+  args="--frames 2048 --iters 5 --pan"; [ $kind = textured ] && args="--frames 1024 --iters 5 --textured"
+  for i in 1 2; do
+    for sp in 8 1 -1; do
+      ORBX_FAST_SPEC=$sp timeout -k 10 120 python tools/kbench.py $args > gpurun_out/kb.log 2>&1 || { tail gpurun_out/kb.log; exit 8; }
+      sed "s/^/fast-spec $kind $sp: /" gpurun_out/kb.log | tail -1
+    done
+  done
+done
 echo "session done"
