@@ -2501,6 +2501,9 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     // 42 (stored into slack rows) and columns past 36 are computed from neighbouring bytes and never
     // read; columns past 39 are not stored.
     {
+#if defined(DESC_DIAG_NOPS) && DESC_DIAG_NOPS == 1   // diagnostic bisection only: drain before the products
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
         const i4v cinit = {128 * 256, 128 * 256, 128 * 256, 128 * 256};
         i4v acc[3][3];   // all nine products first: their results are not waited on one at a time
 #pragma unroll
@@ -2513,6 +2516,9 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
                 acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bfr[nt], afr[mt], cinit, 0, 0, 0);
 #else
                 acc[nt][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[mt], bfr[nt], cinit, 0, 0, 0);
+#endif
+#if defined(DESC_DIAG_NOPS) && DESC_DIAG_NOPS == 2   // diagnostic bisection only: drain after the products
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #endif
 #ifdef DESC_KEEPALIVE_DIAG
         // diagnostic only (tests/test_dpp_hazards.py): round 4's empty-asm keep-alives of the products'
@@ -2575,7 +2581,7 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     b = __sinf(ang);
 #else
     if (TRIG) sincosf_glibc(ang, &b, &a);
-    else sincos_f2d_t<true>(ang, &b, &a);   // ang is wave-uniform (one keypoint per wavefront)
+    else sincos_f2d_fdlibm(ang, &b, &a);
 #endif
     DESC_STAMP(4);
     auto sample = [&](float x, float y) -> int {

@@ -10,6 +10,7 @@ make -s
 mkdir -p _build/ab ../../tools/ab
 extra=""
 case $src in orbx|orbm) extra="-mllvm -amdgpu-mfma-vgpr-form";; esac
+[ -n "$NO_VGPR_FORM" ] && extra=""   # MFMA results in AGPRs (the compiler's default form)
 file=$src.hip
 if [ -n "$REV" ]; then file=_build/ab/${src}_$name.hip; git show "$REV:orb_slam2_refactored_amd/csrc/$src.hip" > $file; fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result \

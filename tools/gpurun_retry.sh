@@ -5,7 +5,7 @@
 # usage: tools/gpurun_retry.sh <timeout-seconds> <script> [args...]
 t=$1; shift
 log=$(mktemp /tmp/gpurun_retry.XXXXXX)
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 ${GPURUN_ATTEMPTS:-20}); do
   /usr/local/graft/bin/gpurun --timeout "$t" -- bash "$@" 2>&1 | tee "$log"
   rc=${PIPESTATUS[0]}
   if [ $rc -eq 3 ] && grep -q "status=transient" "$log"; then
