@@ -64,6 +64,7 @@ struct LevelDev {
     long long xtab_off, ytab_off;   // resize coefficient tables (l >= 1)
     double ssx, ssy;                // (double)w[l-1] / w[l], (double)h[l-1] / h[l] (l >= 1)
     int tail_x;                     // first column of VResizeLinear's scalar tail (l >= 1; w: none)
+    int mt_off;                     // first 16-column block in the matrix-core resize tables (-1: none)
 };
 
 struct Geom {
@@ -659,6 +660,346 @@ static bool pyr_pair_fits(const Geom& g, int l) {
     return ncol + 8 <= PYR_SW && nrow <= PYR_SH && ncol <= PP_MAXC && nrow <= PP_MAXR && (nrow + rpp - 1) / rpp <= PP_MAXP &&
            bw <= PYR_SW && bh <= PYR_SH &&
            bh * ((bw + 15) / 16) <= PYR_PF * 256;
+}
+
+// ---- the level pair with the horizontal pass on the matrix cores (round 5) ----
+// VResizeLinear's horizontal sums for a block of 16 output columns (M) and 16 source rows (N) are
+// one v_mfma_f32_16x16x32_f16 over K = 32 source columns from kb (the block's first tap rounded
+// down to a dword):
+//   A[m][k] = a0 at k = sx0 - kb, a1 at k = sx1 - kb (integers <= 2049: exact in f16),
+//   B[k][n] = 1024 + pixel (the byte under an f16 0x64 high byte: one v_perm per two pixels),
+//   C[m]    = 2^23 - 1024 (a0 + a1).
+// Every partial sum is an integer below 2^24, so D = 2^23 + (S0 a0 + S1 a1) exactly and its float
+// bits carry the horizontal sum in bits 0..19 (h < 2^19).  A source row's sums are computed once
+// (the VALU form computes them for each of the ~1.7 output rows that read the row) into a
+// per-wavefront ring of 48 rows; the vertical taps stay on the VALU (their per-term truncation is
+// not a product).  A and C come from a per-level table built on the host (one 2 KiB entry per
+// 16-column block); a wavefront owns one block at a time, so the ring needs no workgroup barrier.
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float pf4v __attribute__((ext_vector_type(4)));
+struct PyrMfmaLane { uint32_t a[4]; float c[4]; };   // one lane's A fragment (8 f16) and C (4 f32)
+constexpr int PM_GROUPS = 4;                 // source-row groups of 16 per unit (and per ring)
+constexpr int PM_RING = 16 * PM_GROUPS;      // horizontal-sum rows per wavefront ring
+constexpr int PM_HQ = PM_RING * 4 + 4;       // dwords per column quad of a ring (+4: quads on distinct banks)
+constexpr int PM_MAXB1 = 6;                  // level-l rectangle blocks (96 columns)
+constexpr int PM_UROWS = 48;                 // output rows per unit (three steps of 16)
+
+// v_mul_hi_u32_u24 on operands the compiler cannot see are < 2^24 (ring values, table coefficients)
+__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// One unit: output rows y0 .. y0 + 47 (< nrow) of a 16-column block.  The four source-row groups from
+// glo (a unit reads at most 4 x 16 source rows at the supported scale factors; host check) are read
+// together (one address per unit, the groups at immediate offsets), multiplied back to back and
+// written to ring slots 0..3; then each step's ring rows are read (lane = output row n of the step,
+// column quad g).  sl: this lane's S byte offset of group 0 (kbrel + 8 g + n * PYR_SW, kb and the S
+// origin 8-byte aligned); ys[y] = {sy0 * 16, sy1 * 16 (S rows), b0 << 12, b1 << 12}, r0s[y] / rr[y] =
+// sy0 / sy1.  tcol: the block's first column in VResizeLinear's scalar tail (>= 16: none).
+template <bool TAIL>
+__device__ __forceinline__ void pyr_mfma_unit(const uint8_t* S, int sl, const h8v& A, const pf4v& C, uint32_t* ring,
+                                              const int4* ys, const int* r0s, const int* rr, int y0, int nrow,
+                                              int tcol, uint32_t (&o)[PM_UROWS / 16]) {
+    const int lane = lane_id(), n = lane & 15, g = lane >> 4;
+    constexpr uint32_t hmask = TAIL ? 0xfffffu : 0xffff0u;   // the tail's formula needs the full sum
+    const int glo = __builtin_amdgcn_readfirstlane(r0s[y0]) >> 4;
+    const uint8_t* sp = S + (sl + glo * (16 * PYR_SW));
+    uint2 w[PM_GROUPS];
+#pragma unroll
+    for (int k = 0; k < PM_GROUPS; k++) w[k] = *reinterpret_cast<const uint2*>(sp + k * (16 * PYR_SW));
+    int4 yv[PM_UROWS / 16];
+#pragma unroll
+    for (int st = 0; st < PM_UROWS / 16; st++) yv[st] = ys[min(y0 + 16 * st + n, nrow - 1)];
+    pf4v d[PM_GROUPS];   // the four products issued back to back, then read
+#pragma unroll
+    for (int k = 0; k < PM_GROUPS; k++) {
+        const uint4 bu = make_uint4(__builtin_amdgcn_perm(0x64646464u, w[k].x, 0x04010400u),
+                                    __builtin_amdgcn_perm(0x64646464u, w[k].x, 0x04030402u),
+                                    __builtin_amdgcn_perm(0x64646464u, w[k].y, 0x04010400u),
+                                    __builtin_amdgcn_perm(0x64646464u, w[k].y, 0x04030402u));
+        d[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(h8v, bu), C, 0, 0, 0);
+    }
+    uint32_t* rw = ring + g * PM_HQ + 4 * n;
+#pragma unroll
+    for (int k = 0; k < PM_GROUPS; k++)
+        *reinterpret_cast<uint4*>(rw + 64 * k) =
+            make_uint4(__float_as_uint(d[k][0]) & hmask, __float_as_uint(d[k][1]) & hmask,
+                       __float_as_uint(d[k][2]) & hmask, __float_as_uint(d[k][3]) & hmask);
+    // ring row r (S row) sits at byte (r - 16 glo) * 16 of the lane's column-quad area
+    const uint8_t* rq = reinterpret_cast<const uint8_t*>(ring + g * PM_HQ) - glo * 256;
+#pragma unroll
+    for (int st = 0; st < PM_UROWS / 16; st++) {
+        const uint4 h0 = *reinterpret_cast<const uint4*>(rq + yv[st].x);
+        const uint4 h1 = *reinterpret_cast<const uint4*>(rq + yv[st].y);
+        const uint32_t b0 = (uint32_t)yv[st].z, b1 = (uint32_t)yv[st].w;
+        auto px = [&](uint32_t a, uint32_t c, int k) -> uint32_t {
+            if (!TAIL) return (mulhi24(a, b0) + mulhi24(c, b1) + 2) >> 2;
+            const uint32_t v = (mulhi24(a & 0xffff0u, b0) + mulhi24(c & 0xffff0u, b1) + 2) >> 2;
+            return 4 * g + k >= tcol ? vtail(a, c, b0, b1) : v;
+        };
+        o[st] = px(h0.x, h1.x, 0) | (px(h0.y, h1.y, 1) << 8) | (px(h0.z, h1.z, 2) << 16) | (px(h0.w, h1.w, 3) << 24);
+    }
+    (void)rr;
+}
+
+// A block's A / C fragments from the host table
+__device__ __forceinline__ void pyr_mfma_frag(const PyrMfmaLane* tab, h8v& A, pf4v& C) {
+    const PyrMfmaLane t = tab[lane_id()];
+    A = __builtin_bit_cast(h8v, make_uint4(t.a[0], t.a[1], t.a[2], t.a[3]));
+    C = pf4v{t.c[0], t.c[1], t.c[2], t.c[3]};
+}
+
+// The per-output-row tables of pyr_mfma_unit for output rows [r0, r0 + nrow) of a level, source
+// rows from sy_lo (threads 0..nrow-1 write one row each).
+__device__ __forceinline__ void pyr_mfma_rows(const int2* ytab, int r0, int nrow, int sy_lo, int4* ys, int* r0s, int* rr) {
+    const int y = threadIdx.x;
+    if (y < nrow) {
+        const int2 v = ytab[r0 + y];
+        const int s0 = (v.x & 0xffff) - sy_lo, s1 = (v.x >> 16) - sy_lo;
+        ys[y] = make_int4(s0 * 16, s1 * 16, (int)vcoef24(v.y), (int)vcoef24(v.y >> 16));
+        r0s[y] = s0;
+        rr[y] = s1;
+    }
+}
+
+// 4 output pixels (one dword) at byte column col of a row; partial at the right edge (last: the
+// last column that may be written)
+__device__ __forceinline__ void pyr_store4(uint8_t* dst, uint32_t o, int col, int last) {
+    if (col + 3 <= last) *reinterpret_cast<uint32_t*>(dst) = o;
+    else
+        for (int k = 0; k < 3; k++)
+            if (col + k <= last) dst[k] = (uint8_t)(o >> (8 * k));
+}
+
+__global__ __launch_bounds__(256) void pyramid_pair_mfma_kernel(Geom g, int l, const uint8_t* __restrict__ in,
+                                                                long long in_fstride, int in_step, uint8_t* pyr,
+                                                                const int2* __restrict__ ytab,
+                                                                const PyrMfmaLane* __restrict__ mt,
+                                                                const int* __restrict__ mkb) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW + 16];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 4 * PM_HQ];
+    __shared__ int4 ys1[PP_MAXR], ys2[PYR_TH];
+    __shared__ int r0s1[PP_MAXR], r0s2[PYR_TH], rr1[PP_MAXR], rr2[PYR_TH];
+    const LevelDev& L0 = g.lv[l - 1];
+    const LevelDev& L1 = g.lv[l];
+    const LevelDev& L2 = g.lv[l + 1];
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gx = gridDim.x, gxy = gridDim.x * gridDim.y;
+    const int lb = xcd_swizzle(blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z, gxy * gridDim.z);
+    const int f = lb / gxy;
+    const int tx0 = (lb % gx) * PYR_TW, ty0 = ((lb % gxy) / gx) * PYR_TH;
+    const int tw = min(PYR_TW, L2.w - tx0), th = min(PYR_TH, L2.h - ty0);
+    auto u = [](int x) { return __builtin_amdgcn_readfirstlane(x); };
+    // level-l rectangle [c0, c1] x [ay0, ay1], c0 on a 16-column block boundary
+    const int ax0 = max(0, (int)floor((tx0 + 0.5) * L2.ssx - 0.5) - 2);
+    const int c1 = u(min(L1.w - 1, (int)floor((tx0 + tw - 0.5) * L2.ssx - 0.5) + 2));
+    const int ay0 = u(max(0, (int)floor((ty0 + 0.5) * L2.ssy - 0.5) - 2));
+    const int ay1 = u(min(L1.h - 1, (int)floor((ty0 + th - 0.5) * L2.ssy - 0.5) + 2));
+    const int c0 = u(ax0 & ~15);
+    const int ncol = c1 - c0 + 1, nrow = ay1 - ay0 + 1;
+    PyrTile T;
+    const int bx0 = max(0, (int)floor((c0 + 0.5) * L1.ssx - 0.5) - 2);
+    const int bx1 = min(L0.w - 1, (int)floor((c1 + 0.5) * L1.ssx - 0.5) + 2);
+    T.sy_lo = u(max(0, (int)floor((ay0 + 0.5) * L1.ssy - 0.5) - 2));
+    const int by1 = min(L0.h - 1, (int)floor((ay1 + 0.5) * L1.ssy - 0.5) + 2);
+    T.xa = u(bx0 & ~15);
+    T.nc = u(((bx1 - T.xa) >> 4) + 1);
+    T.items = u((by1 - T.sy_lo + 1) * T.nc);
+    T.mul = u(((1 << 20) + T.nc - 1) / T.nc);
+    T.src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &T.sstep);   // 16-byte aligned (host)
+    {
+        uint4 v0, v1, v2, v3, v4;
+        pyr_fetch(T, tid, v0, v1, v2, v3, v4);
+        pyr_mfma_rows(ytab + L1.ytab_off, ay0, nrow, T.sy_lo, ys1, r0s1, rr1);
+        pyr_mfma_rows(ytab + L2.ytab_off, ty0, th, ay0, ys2, r0s2, rr2);
+        pyr_stage(T, tid, S, v0, 0);
+        pyr_stage(T, tid, S, v1, 1);
+        pyr_stage(T, tid, S, v2, 2);
+        pyr_stage(T, tid, S, v3, 3);
+        pyr_stage(T, tid, S, v4, 4);
+    }
+    __syncthreads();
+    uint32_t* myring = ring + w * 4 * PM_HQ;
+    const int n = tid & 15, q = (tid >> 4) & 3;
+    constexpr int NST = PM_UROWS / 16;
+    // level l: units (block b, 48-row part p) dealt round robin to the wavefronts; the rows stay in
+    // registers until every wavefront is done reading the level-(l-1) rectangle
+    const int nb1 = (ncol + 15) >> 4, np1 = (nrow + PM_UROWS - 1) / PM_UROWS;
+    const int nu1 = nb1 * np1;
+    constexpr int MAXU1 = (PM_MAXB1 * ((PP_MAXR + PM_UROWS - 1) / PM_UROWS) + 3) / 4;
+    uint32_t o1[MAXU1][NST];
+    const long long lstride = u(L1.stride);
+    uint8_t* lrow = pyr + (long long)f * g.pyr_frame_bytes + L1.off + (long long)(ay0 + n) * lstride + c0 + 4 * q;
+#pragma unroll
+    for (int ui = 0; ui < MAXU1; ui++) {
+        const int un = w + 4 * ui;
+        if (un >= nu1) break;
+        const int b = un / np1, p = un - b * np1;
+        const int bc = c0 + 16 * b;   // the block's first column
+        const int blk = L1.mt_off + (bc >> 4);
+        h8v A;
+        pf4v C;
+        pyr_mfma_frag(mt + (long long)blk * 64, A, C);
+        const int sl = mkb[blk] - T.xa + 8 * q + n * PYR_SW;
+        const int tcol = L1.tail_x - bc;
+        const int y0 = PM_UROWS * p;
+        if (tcol < 16) pyr_mfma_unit<true>(S, sl, A, C, myring, ys1, r0s1, rr1, y0, nrow, tcol, o1[ui]);
+        else pyr_mfma_unit<false>(S, sl, A, C, myring, ys1, r0s1, rr1, y0, nrow, tcol, o1[ui]);
+        const int col = bc + 4 * q;
+        if (col <= c1) {
+            uint8_t* dst = lrow + (long long)y0 * lstride + 16 * b;
+#pragma unroll
+            for (int st = 0; st < NST; st++)
+                if (y0 + 16 * st + n < nrow) pyr_store4(dst + (long long)(16 * st) * lstride, o1[ui][st], col, c1);
+        }
+    }
+    __syncthreads();   // every read of the level-(l-1) rectangle done: S now takes the level-l one
+#pragma unroll
+    for (int ui = 0; ui < MAXU1; ui++) {
+        const int un = w + 4 * ui;
+        if (un >= nu1) break;
+        const int b = un / np1, p = un - b * np1;
+#pragma unroll
+        for (int st = 0; st < NST; st++) {
+            const int y = PM_UROWS * p + 16 * st + n;
+            if (y < nrow) *reinterpret_cast<uint32_t*>(&S[y * PYR_SW + 16 * b + 4 * q]) = o1[ui][st];
+        }
+    }
+    __syncthreads();
+    // level l+1: wavefront w takes block w of the 64-column tile, rows in 48-row parts
+    if (16 * w < tw) {
+        const int bc = tx0 + 16 * w;
+        const int blk = L2.mt_off + (bc >> 4);
+        h8v A;
+        pf4v C;
+        pyr_mfma_frag(mt + (long long)blk * 64, A, C);
+        const int sl = mkb[blk] - c0 + 8 * q + n * PYR_SW;
+        const int col = bc + 4 * q;
+        const int tcol = L2.tail_x - bc;
+        const long long dstride = u(L2.stride);
+        uint8_t* drow = pyr + (long long)f * g.pyr_frame_bytes + L2.off + col + (long long)(ty0 + n) * dstride;
+#pragma unroll
+        for (int p = 0; p < (PYR_TH + PM_UROWS - 1) / PM_UROWS; p++) {
+            const int y0 = PM_UROWS * p;
+            if (y0 >= th) break;
+            uint32_t o[NST];
+            if (tcol < 16) pyr_mfma_unit<true>(S, sl, A, C, myring, ys2, r0s2, rr2, y0, th, tcol, o);
+            else pyr_mfma_unit<false>(S, sl, A, C, myring, ys2, r0s2, rr2, y0, th, tcol, o);
+            if (col < tx0 + tw) {
+#pragma unroll
+                for (int st = 0; st < NST; st++)
+                    if (y0 + 16 * st + n < th)
+                        pyr_store4(drow + (long long)(y0 + 16 * st) * dstride, o[st], col, tx0 + tw - 1);
+            }
+        }
+    }
+}
+
+// f16 bits of an integer 0 <= v <= 2048 (exact: at most 11 significant bits)
+static uint16_t f16_of_int(int v) {
+    if (v <= 0) return 0;
+    int e = 0;
+    while ((2 << e) <= v) e++;   // v in [2^e, 2^(e+1))
+    const int m = e >= 10 ? (v - (1 << e)) >> (e - 10) : (v - (1 << e)) << (10 - e);
+    return (uint16_t)(((e + 15) << 10) | m);
+}
+
+// A / C fragments of pyramid_pair_mfma_kernel for one level's columns (xt: its xtab entries, dw
+// columns), appended to mt / mkb; returns the level's first block, or -1 when a block's taps do
+// not fit K = 32 from its dword-aligned first tap (scale factors above ~1.7).
+static int pyr_mfma_tables(const int2* xt, int dw, std::vector<PyrMfmaLane>& mt, std::vector<int>& mkb) {
+    const int nb = (dw + 15) / 16;
+    std::vector<PyrMfmaLane> lanes((size_t)nb * 64);
+    std::vector<int> kbs(nb);
+    for (int j = 0; j < nb; j++) {
+        const int kb = (xt[16 * j].x & 0xffff) & ~7;   // 8-byte aligned: the B fragments are ds_read_b64
+        kbs[j] = kb;
+        for (int ln = 0; ln < 64; ln++) {
+            PyrMfmaLane& t = lanes[(size_t)j * 64 + ln];
+            const int c = 16 * j + (ln & 15), gq = ln >> 4;
+            uint16_t hv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (c < dw) {
+                const int sx0 = xt[c].x & 0xffff, sx1 = xt[c].x >> 16, a0 = xt[c].y & 0xffff, a1 = xt[c].y >> 16;
+                const int e0 = sx0 - kb, e1 = sx1 - kb;
+                if (e0 < 0 || e1 < e0 || e1 > 31 || a0 < 0 || a1 < 0 || a0 + a1 > 4096) return -1;
+                for (int k = 0; k < 8; k++) {
+                    const int kk = 8 * gq + k;
+                    const int wv = (kk == e0 ? a0 : 0) + (kk == e1 ? a1 : 0);
+                    if (wv > 2048) return -1;
+                    hv[k] = f16_of_int(wv);
+                }
+            }
+            for (int k = 0; k < 4; k++) t.a[k] = (uint32_t)hv[2 * k] | ((uint32_t)hv[2 * k + 1] << 16);
+            for (int r = 0; r < 4; r++) {
+                const int cm = 16 * j + 4 * gq + r;
+                const int sum = cm < dw ? (xt[cm].y & 0xffff) + (xt[cm].y >> 16) : 0;
+                t.c[r] = (float)(8388608 - 1024 * sum);
+            }
+        }
+    }
+    const int off = (int)mkb.size();
+    mt.insert(mt.end(), lanes.begin(), lanes.end());
+    mkb.insert(mkb.end(), kbs.begin(), kbs.end());
+    return off;
+}
+
+// pyramid_pair_mfma_kernel's geometry replayed for every tile of the pair (l, l+1): the staged
+// rectangles fit S, every block's K window lies inside S's rows, and a unit's source rows lie in
+// at most PM_GROUPS groups of 16.
+static bool pyr_mfma_pair_fits(const Geom& g, int l, const std::vector<int>& mkb, const std::vector<int2>& ytab) {
+    const LevelDev &L0 = g.lv[l - 1], &L1 = g.lv[l], &L2 = g.lv[l + 1];
+    if (L1.mt_off < 0 || L2.mt_off < 0) return false;
+    auto fl = [](double v) { return (int)std::floor(v); };
+    int max_rows = 0, max_nc = 0;
+    for (int ty0 = 0; ty0 < L2.h; ty0 += PYR_TH) {
+        const int th = std::min(PYR_TH, L2.h - ty0);
+        const int ay0 = std::max(0, fl((ty0 + 0.5) * L2.ssy - 0.5) - 2);
+        const int ay1 = std::min(L1.h - 1, fl((ty0 + th - 0.5) * L2.ssy - 0.5) + 2);
+        const int nrow = ay1 - ay0 + 1;
+        const int sy_lo = std::max(0, fl((ay0 + 0.5) * L1.ssy - 0.5) - 2);
+        const int by1 = std::min(L0.h - 1, fl((ay1 + 0.5) * L1.ssy - 0.5) + 2);
+        if (nrow > PP_MAXR || by1 - sy_lo + 1 > PYR_SH) return false;
+        max_rows = std::max(max_rows, by1 - sy_lo + 1);
+        // the rows' taps inside the staged rows, and each 16-row step within 33 source rows
+        auto rows_ok = [&](const LevelDev& L, int r0, int nr, int lo, int cap) {
+            for (int y = 0; y < nr; y++) {
+                const int2 v = ytab[L.ytab_off + r0 + y];
+                const int s0 = (v.x & 0xffff) - lo, s1 = (v.x >> 16) - lo;
+                if (s0 < 0 || s1 >= cap || s1 < s0) return false;
+                // a unit's (PM_UROWS output rows') source rows within PM_GROUPS groups of 16 inside S
+                const int2 vl = ytab[L.ytab_off + r0 + std::min(nr - 1, (y / PM_UROWS) * PM_UROWS + PM_UROWS - 1)];
+                const int2 vf = ytab[L.ytab_off + r0 + (y / PM_UROWS) * PM_UROWS];
+                const int glo = ((vf.x & 0xffff) - lo) >> 4;
+                if ((((vl.x >> 16) - lo) >> 4) - glo >= PM_GROUPS || 16 * (glo + PM_GROUPS) > PYR_SH) return false;
+            }
+            return true;
+        };
+        if (!rows_ok(L1, ay0, nrow, sy_lo, by1 - sy_lo + 1) || !rows_ok(L2, ty0, th, ay0, nrow)) return false;
+    }
+    for (int tx0 = 0; tx0 < L2.w; tx0 += PYR_TW) {
+        const int tw = std::min(PYR_TW, L2.w - tx0);
+        const int ax0 = std::max(0, fl((tx0 + 0.5) * L2.ssx - 0.5) - 2);
+        const int c1 = std::min(L1.w - 1, fl((tx0 + tw - 0.5) * L2.ssx - 0.5) + 2);
+        const int c0 = ax0 & ~15;
+        const int ncol = c1 - c0 + 1;
+        const int bx0 = std::max(0, fl((c0 + 0.5) * L1.ssx - 0.5) - 2);
+        const int bx1 = std::min(L0.w - 1, fl((c1 + 0.5) * L1.ssx - 0.5) + 2);
+        const int xa = bx0 & ~15, nc = ((bx1 - xa) >> 4) + 1;
+        if (ncol > 16 * PM_MAXB1 || 16 * nc > PYR_SW) return false;
+        max_nc = std::max(max_nc, nc);
+        for (int b = 0; b < (ncol + 15) / 16; b++) {
+            const int kbrel = mkb[L1.mt_off + (c0 >> 4) + b] - xa;
+            if (kbrel < 0 || kbrel + 32 > PYR_SW) return false;
+        }
+        for (int b = 0; 16 * b < tw; b++) {   // (c0 is a multiple of 16: kb - c0 stays 8-byte aligned)
+            const int kbrel = mkb[L2.mt_off + (tx0 >> 4) + b] - c0;
+            if (kbrel < 0 || kbrel + 32 > PYR_SW) return false;
+        }
+    }
+    return max_rows * max_nc <= PYR_PF * 256;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2761,6 +3102,9 @@ struct orbx_extractor {
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     int debug_nc = 0;
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
+    int pyr_mfma = 0;   // ORBX_PYR_MFMA=1: pyramid_pair_mfma_kernel where the level pair's tables fit (measured slower: DESIGN §4)
+    std::vector<char> pyr_mfma_ok;   // per level l: the pair (l, l+1) fits pyramid_pair_mfma_kernel
+    DevBuf d_pyrmt, d_pyrkb;         // its A / C fragments per 16-column block, and the blocks' first tap column
     int pyr_pair = 2;   // pyramid_pair_kernel for levels (1,2), (3,4), (5,6) (level 0 16-byte aligned); 1: (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
     // OpenCV-build switches (orbx_set_opencv_compat; ORBX_TRIG / ORBX_RESIZE_TAIL)
     int trig_float = 0;    // ComputeOrbDescriptor's cos / sin: 0 ::cos(double), 1 cosf / sinf
@@ -2843,6 +3187,8 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     g.nlevels = Lc;
     for (int l = Lc; l < MAX_LEVELS; l++) g.lv[l].out_base = INT_MAX;   // describe's level count
     std::vector<int2> xtab, ytab;
+    std::vector<PyrMfmaLane> mt;
+    std::vector<int> mkb;
     std::vector<CellDev> cells;
     long long pyr_off = 0, slot = 0, cand = 0;
     int out = 0, NC = 64;
@@ -2850,7 +3196,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     for (int l = 0; l < Lc; l++) {
         LevelDev& L = g.lv[l];
         if (l == 0) {
-            L.w = cols; L.h = rows; L.stride = cols; L.off = -1; L.tail_x = cols;
+            L.w = cols; L.h = rows; L.stride = cols; L.off = -1; L.tail_x = cols; L.mt_off = -1;
         } else {
             L.h = cv_round_f(h->inv_scale[l] * rows);
             L.w = cv_round_f(h->inv_scale[l] * cols);
@@ -2889,6 +3235,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
                 if (dx >= xmax) { sx1 = sx0; a0 = 2048; a1 = 0; }
                 xtab.push_back(make_int2(sx0 | (sx1 << 16), (a0 & 0xffff) | (a1 << 16)));
             }
+            L.mt_off = pyr_mfma_tables(xtab.data() + L.xtab_off, dw, mt, mkb);
             for (int dy = 0; dy < dh; dy++) {
                 float fy = (float)((dy + 0.5) * scale_y - 0.5);
                 int sy = (int)std::floor(fy);
@@ -3023,6 +3370,14 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         ORB_HIP_TRY(hipMemcpy(h->d_xtab.ptr, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice));
     if (!ytab.empty())
         ORB_HIP_TRY(hipMemcpy(h->d_ytab.ptr, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice));
+    if ((rc = h->d_pyrmt.reserve(std::max<size_t>(1, mt.size()) * sizeof(PyrMfmaLane)))) return rc;
+    if ((rc = h->d_pyrkb.reserve(std::max<size_t>(1, mkb.size()) * sizeof(int)))) return rc;
+    if (!mt.empty())
+        ORB_HIP_TRY(hipMemcpy(h->d_pyrmt.ptr, mt.data(), mt.size() * sizeof(PyrMfmaLane), hipMemcpyHostToDevice));
+    if (!mkb.empty())
+        ORB_HIP_TRY(hipMemcpy(h->d_pyrkb.ptr, mkb.data(), mkb.size() * sizeof(int), hipMemcpyHostToDevice));
+    h->pyr_mfma_ok.assign(Lc, 0);
+    for (int l = 1; l + 1 < Lc; l++) h->pyr_mfma_ok[l] = pyr_mfma_pair_fits(g, l, mkb, ytab);
     h->geom = g;
     h->cells = cells;
     {   // FAST column strips: up to fast_cpw vertically consecutive cells of one column per wavefront
@@ -3186,6 +3541,14 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     auto pyramid = [&](int l) -> int {
         const int first = h->pyr_pair == 2 ? 1 : 2;   // pairs (1,2), (3,4), (5,6) or (2,3), (4,5), (6,7)
         const bool a16 = l > 1 || (((uintptr_t)d_imgs | (uintptr_t)fstride | (uintptr_t)step) & 15) == 0;
+        if (h->pyr_pair && l >= first && (l - first) % 2 == 0 && l + 1 < g.nlevels && a16 && h->pyr_mfma &&
+            h->pyr_mfma_ok[l]) {
+            const int ntx = (g.lv[l + 1].w + PYR_TW - 1) / PYR_TW, nty = (g.lv[l + 1].h + PYR_TH - 1) / PYR_TH;
+            launch_timed(h, 0, pyramid_pair_mfma_kernel, dim3((unsigned)ntx, (unsigned)nty, (unsigned)F), dim3(256), 0u,
+                         st, g, l, d_imgs, fstride, step, pyr, h->d_ytab.as<int2>(), h->d_pyrmt.as<PyrMfmaLane>(),
+                         h->d_pyrkb.as<int>());
+            return 1;
+        }
         if (h->pyr_pair && l >= first && (l - first) % 2 == 0 && l + 1 < g.nlevels && a16 && pyr_pair_fits(g, l)) {
             const int ntx = (g.lv[l + 1].w + PYR_TW - 1) / PYR_TW, nty = (g.lv[l + 1].h + PYR_TH - 1) / PYR_TH;
             launch_timed(h, 0, pyramid_pair_kernel, dim3((unsigned)ntx, (unsigned)nty, (unsigned)F), dim3(256), 0u, st,
@@ -3311,6 +3674,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(-1, atoi(e));   // -1: every cell
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
+    if (const char* e = getenv("ORBX_PYR_MFMA")) h->pyr_mfma = atoi(e) != 0;
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     if (const char* e = getenv("ORBX_DEBUG_NC")) h->debug_nc = atoi(e);
     // OpenCV-build switches (orbx_set_opencv_compat): ORBX_TRIG=double|float, ORBX_RESIZE_TAIL=V

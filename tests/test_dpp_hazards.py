@@ -20,12 +20,18 @@ VARIANTS = [("orbba.hip", []), ("orbba.hip", ["-DSB_SPLIT_DEF=8"]), ("orbba.hip"
 VGPR_FORM = ("orbx.hip", "orbm.hip")   # built with -amdgpu-mfma-vgpr-form, as the Makefile does
 
 
-@pytest.mark.parametrize("src,flags", VARIANTS, ids=["orbba", "orbba-sb8", "orbba-newton0", "orbx", "orbm"])
-def test_no_dpp_hazards(tmp_path, src, flags):
-    listing = tmp_path / (src + ".s")
+_LISTINGS = {}
+
+
+def listing_of(tmp_dir, src, flags):
+    """The device listing of src built as the Makefile builds it (plus flags), compiled once per session."""
+    key = (src, tuple(flags))
+    if key in _LISTINGS:
+        return _LISTINGS[key]
+    listing = tmp_dir / (src + "_".join(f.strip("-").replace("=", "") for f in flags) + ".s")
     extra = list(flags)
     if "newton0" in extra:
-        inc = tmp_path / "orbba_diag_n0.inc"
+        inc = tmp_dir / "orbba_diag_n0.inc"
         subprocess.run([sys.executable, str(ROOT / "tools" / "gen_ba_diag.py"), "0", str(inc)], check=True,
                        capture_output=True, timeout=120)
         extra = [f'-DORBBA_DIAG_INC="{inc}"']
@@ -36,9 +42,51 @@ def test_no_dpp_hazards(tmp_path, src, flags):
     if not Path(cmd[0]).exists():
         pytest.skip("hipcc not available")
     subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    _LISTINGS[key] = listing
+    return listing
+
+
+@pytest.fixture(scope="module")
+def lst_dir(tmp_path_factory):
+    return tmp_path_factory.mktemp("listings")
+
+
+@pytest.mark.parametrize("src,flags", VARIANTS, ids=["orbba", "orbba-sb8", "orbba-newton0", "orbx", "orbm"])
+def test_no_dpp_hazards(lst_dir, src, flags):
+    listing = listing_of(lst_dir, src, flags)
     out = subprocess.run([sys.executable, str(ROOT / "tools" / "dpp_hazard_check.py"), str(listing)],
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("src,flags", [("orbx.hip", []), ("orbm.hip", []), ("orbba.hip", [])],
+                         ids=["orbx", "orbm", "orbba"])
+def test_no_mfma_hazards(lst_dir, src, flags):
+    """Every shipped MFMA kernel: no read of an MFMA result inside its window (tools/mfma_raw_check.py)."""
+    listing = listing_of(lst_dir, src, flags)
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "mfma_raw_check.py"), str(listing)],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_describe_free_of_nondeterministic_pattern(lst_dir):
+    """describe_kernel has no LDS load into a source register of an MFMA issued within 16 wait states:
+    the schedule of both describe builds whose descriptors differed between identical runs on MI355X
+    (DESC_ANGLE_MFMA=0 and DESC_ANGLE_FIRST=1: 1018-1024 differing rows per 64 frames; the shipped,
+    keep-alive and fused-sincos builds: 0 and no such load).  A correlate, not a proven hazard (the i8
+    matcher has it and is exact): DESIGN §4, describe round 5."""
+    listing = listing_of(lst_dir, "orbx.hip", [])
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "mfma_raw_check.py"), str(listing), "describe_kernel",
+                          "--war"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_mfma_checker_rejects_nondeterministic_describe(lst_dir):
+    """The rule flags the build the determinism probe found nondeterministic (the LDS IC_Angle)."""
+    listing = listing_of(lst_dir, "orbx.hip", ["-DDESC_ANGLE_MFMA=0"])
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "mfma_raw_check.py"), str(listing), "describe_kernel",
+                          "--war"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 1 and "load(s) over the source of an MFMA in flight" in out.stdout, out.stdout
 
 
 def test_mfma_overlap_checker(tmp_path):

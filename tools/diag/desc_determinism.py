@@ -38,4 +38,14 @@ for r, o in enumerate(outs[1:], 1):
             print(f"run {r} frame {i} row {j}/{n}: kp_diff={bool(kd[j])} kp={kp.tolist()} "
                   f"bits_diff={int(np.unpackbits(outs[0][1][i, j] ^ o[1][i, j]).sum())}")
 print("differences:", bad)
+if os.environ.get("DET_DUMP"):
+    # every differing row of run 1 against run 0: frame, row, keypoint record, differing bit indices
+    import json
+    rows = []
+    for i, n in enumerate(cnt):
+        d0, d1 = outs[0][1][i, :n], outs[1][1][i, :n]
+        for j in np.nonzero(~np.all(d0 == d1, axis=1))[0]:
+            bits = np.nonzero(np.unpackbits(d0[j] ^ d1[j], bitorder="little"))[0]
+            rows.append({"frame": i, "row": int(j), "kp": outs[0][0][i, j].tolist(), "bits": bits.tolist()})
+    json.dump(rows, open(os.environ["DET_DUMP"], "w"))
 sys.exit(1 if bad else 0)

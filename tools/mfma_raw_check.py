@@ -1,21 +1,37 @@
 #!/usr/bin/env python3
-"""Static check of a gfx950 listing: is every read of an MFMA's destination far enough behind the MFMA?
+"""Static checks of a gfx950 listing around the MFMAs.
 
-An XDL MFMA writes its D registers several cycles after issue; a VALU / memory / DPP / readlane read of
-D inside that window returns the OLD register contents (tools/probe/hazard_probe.hip, T5, measures the
-window on the hardware).  The compiler inserts the wait states itself -- except that it counts an inline
-asm statement as wait states even when the asm is empty (a `asm volatile("" :: "v"(x))` keep-alive, or
-an opaque-pointer `asm volatile("" : "+s"(p))`), so an empty asm between an MFMA and the read of its
-result can leave the read inside the window.  That is the round-4 describe nondeterminism (DESIGN §4,
-describe round 4; VERDICT r04 "Next round" 3): results that depend on the read racing the write.
+1. RAW: is every read of an MFMA's destination far enough behind the MFMA?  An XDL MFMA writes its D
+   registers several cycles after issue; a VALU / memory / DPP / readlane read of D inside that window
+   returns the OLD register contents (tools/probe/hazard_probe.hip, T5, measures the window on the
+   hardware).  The compiler inserts the wait states itself -- except that it counts an inline asm
+   statement as wait states even when the asm is empty, so an empty asm between an MFMA and the read
+   of its result can leave the read inside the window.
+   Wait states: 1 per instruction, N+1 per `s_nop N`; the empty-asm markers (`;;#ASMSTART` /
+   `;;#ASMEND` with nothing between) count 0.  Control flow: straight-line order plus every branch edge
+   (writes pending at a branch stay pending at its target, one wait state later), as
+   tools/dpp_hazard_check.py does.  A VALU write of a pending register ends its window (later reads
+   see the VALU's value).  Required wait states per MFMA shape: REQUIRED below.
 
-Wait states: 1 per instruction, N+1 per `s_nop N`; the empty-asm markers (`;;#ASMSTART` / `;;#ASMEND`
-with nothing between) count 0.  Control flow: straight-line order plus every branch edge (writes pending
-at a branch stay pending at its target, one wait state later), as tools/dpp_hazard_check.py does.
-Required wait states per MFMA shape: REQUIRED below (from the probe; an MFMA reading the D of an earlier
-one as SrcC is ordered by the hardware and not checked).
+2. LDS-load WAR (--war): an LDS load (ds_read / ds_load) whose destination overlaps a SrcA / SrcB /
+   SrcC register of an MFMA issued within the previous WAR_WINDOW wait states.  This is the pattern of
+   every describe build that gave different descriptor bits between identical runs (round 5,
+   tools/diag/desc_determinism.py on 64 frames of 640 x 480, today's describe source):
+     DESC_ANGLE_MFMA=0 (the LDS IC_Angle)   1022-1024 differing rows   3 loads at 0 / 5 / 10 wait states
+     DESC_ANGLE_FIRST=1                     1018                        1 load at 0 wait states
+     shipped, DESC_KEEPALIVE_DIAG, SINCOS_FMA_DIAG       0              none
+   The register allocator reuses a source register of an MFMA it has just issued as the destination
+   of the next fragment's LDS load (`v_mfma ... v[16:19] ...` then `ds_read_b128 v[18:21]`); the
+   compiler's hazard recognizer inserts nothing, and the outcome depends on whether the load returns
+   before the MFMA has read its operands.  The isolated hardware probe (hazard_probe T10 / T12, the
+   exact angold sequence) did not reproduce it, and the i8 matcher (hamming_top2_mfma_kernel, the
+   same pattern at 0-5 wait states) and the LocalBA solve (f64 MFMAs, 0-12) give exact, repeatable
+   results (tools/diag/matcher_i8_war.py: 0 differences in 12 runs of 65536 x 2048 / 16384 x 4500).
+   So the pattern is not by itself a hazard; it is a correlate of the two describe schedules that are,
+   and describe is kept free of it as a precaution (tests/test_dpp_hazards.py).  Global loads
+   (hundreds of cycles) are not counted.
 
-usage: mfma_raw_check.py listing.s [kernel-substring]   (exit 1 when a read falls inside a window)"""
+usage: mfma_raw_check.py listing.s [kernel-substring] [--war]   (exit 1 on any finding)"""
 import re
 import sys
 
@@ -26,11 +42,13 @@ import sys
 REQUIRED = {
     "v_mfma_i32_16x16x64_i8": (8, 8),
     "v_mfma_scale_f32_16x16x128_f8f6f4": (8, 8),
+    "v_mfma_f32_16x16x32_f16": (8, 8),
     "v_mfma_f64_16x16x4_f64": (19, 18),
 }
 DEFAULT_REQUIRED = (19, 19)
 MEM_OPS = ("ds_", "buffer_", "global_", "flat_", "scratch_")
-# a load issued within this many wait states of an MFMA must not write that MFMA's sources
+# an LDS load issued within this many wait states of an MFMA must not write that MFMA's sources
+# (the nondeterministic builds have them at 0-10; the shipped kernels have none within 64)
 WAR_WINDOW = 16
 
 reg_re = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b")
@@ -126,6 +144,9 @@ def walk(body, incoming, report):
                         if report:
                             print(f"  {code}  reads v{r} of `{pending[r][1]}` with {left} wait states left")
                         bad += 1
+        if pending and op.startswith("v_") and parts and not op.startswith(("v_cmp", "v_readlane", "v_readfirstlane")):
+            for r in regs(parts[0]):   # a VALU result replaces the MFMA's value: later reads see it
+                pending.pop(r, None)
         step = ws_of(code)
         pending = {r: (n - step, s, d) for r, (n, s, d) in pending.items() if n - step > 0}
         if op.startswith(("s_branch", "s_cbranch")) and parts:
@@ -137,12 +158,12 @@ def walk(body, incoming, report):
     return edges, bad
 
 
-LOAD_OPS = ("ds_read", "ds_load", "buffer_load", "global_load", "flat_load", "scratch_load")
+LOAD_OPS = ("ds_read", "ds_load")   # LDS loads: tens of cycles, inside an MFMA queue's operand reads
 
 
 def war_loads(body, window, report):
-    """Loads (asynchronous VGPR writes) whose destination overlaps a SrcA / SrcB / SrcC register of an
-    MFMA issued within the previous `window` wait states (straight-line order; a label or branch ends
+    """LDS loads (asynchronous VGPR writes) whose destination overlaps a SrcA / SrcB / SrcC register of
+    an MFMA issued within the previous `window` wait states (straight-line order; a label or branch ends
     the window).  Returns the count."""
     recent = []   # (wait states since issue, set of source vgprs, mfma text)
     bad = 0
@@ -178,7 +199,7 @@ def war_loads(body, window, report):
     return bad
 
 
-def check(path, want=""):
+def check(path, want="", war=False):
     total = 0
     for name, body in functions(open(path).read().splitlines()):
         if want and want not in name:
@@ -193,7 +214,7 @@ def check(path, want=""):
         if bad:
             print(f"{name}: {bad} read(s) of an MFMA result inside its window")
             walk(body, incoming, True)
-        wb = war_loads(body, WAR_WINDOW, False)
+        wb = war_loads(body, WAR_WINDOW, False) if war else 0
         if wb:
             print(f"{name}: {wb} load(s) over the source of an MFMA in flight")
             war_loads(body, WAR_WINDOW, True)
@@ -202,6 +223,7 @@ def check(path, want=""):
 
 
 if __name__ == "__main__":
-    n = check(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")
+    args = [a for a in sys.argv[1:] if a != "--war"]
+    n = check(args[0], args[1] if len(args) > 1 else "", "--war" in sys.argv)
     print(f"{n} MFMA-result read hazard(s)")
     sys.exit(1 if n else 0)

@@ -229,6 +229,66 @@ MFMA_LDS_WAR(war_lds_p3k16, PRE3, OVW_LDS16)
 MFMA_LDS_WAR(war_valu_p3, PRE3, OVW_VALU)
 MFMA_LDS_WAR(war_none_p3, PRE3, OVW_NONE)
 
+// T12: the DESC_ANGLE_MFMA=0 describe sequence (tools/ab lib_angold): three MFMAs reading the same SrcA,
+// the third writing D partly over that SrcA, then an LDS load over the rest of SrcA.  Returns the 12
+// result elements (three D's) folded into 4 sums of distinct weights.
+#define MFMA3_LDS(NAME, D3, OVW)                                                                              \
+    __device__ __noinline__ i4v NAME(i4v a, i4v b, unsigned lds_addr) {                                     \
+        i4v r;                                                                                               \
+        asm volatile("v_mov_b32 v44, %4\n\tv_mov_b32 v45, %5\n\tv_mov_b32 v46, %6\n\tv_mov_b32 v47, %7\n\t"   \
+                     "v_mov_b32 v72, %8\n\tv_mov_b32 v73, %9\n\tv_mov_b32 v74, %10\n\tv_mov_b32 v75, %11\n\t" \
+                     "v_mov_b32 v60, %9\n\tv_mov_b32 v61, %8\n\tv_mov_b32 v62, %11\n\tv_mov_b32 v63, %10\n\t" \
+                     "v_mov_b32 v56, %11\n\tv_mov_b32 v57, %10\n\tv_mov_b32 v58, %9\n\tv_mov_b32 v59, %8\n\ts_nop 4\n\t" \
+                     "v_mfma_i32_16x16x64_i8 v[64:67], v[44:47], v[72:75], 0\n\t"                              \
+                     "v_mov_b32 v76, 1\n\tv_mov_b32 v77, 2\n\tv_mov_b32 v78, 3\n\tv_mov_b32 v79, 4\n\t"     \
+                     "v_mfma_i32_16x16x64_i8 v[68:71], v[44:47], v[60:63], 0\n\t"                              \
+                     "v_mov_b32 v76, 5\n\tv_mov_b32 v77, 6\n\tv_mov_b32 v78, 7\n\tv_mov_b32 v79, 8\n\t"     \
+                     "v_mfma_i32_16x16x64_i8 " D3 ", v[44:47], v[56:59], 0\n\t"                                \
+                     OVW                                                                                      \
+                     "s_waitcnt lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"               \
+                     "v_add3_u32 %0, v64, v68, v42\n\tv_add3_u32 %1, v65, v69, v43\n\t"                         \
+                     "v_add3_u32 %2, v66, v70, v44\n\tv_add3_u32 %3, v67, v71, v45\n\ts_nop 4"                  \
+                     : "=v"(r.x), "=v"(r.y), "=v"(r.z), "=v"(r.w)                                             \
+                     : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(lds_addr) \
+                     : "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v56", "v57", "v58", "v59", "v60",  \
+                       "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73",  \
+                       "v74", "v75", "v76", "v77", "v78", "v79", "memory");                                   \
+        return r;                                                                                            \
+    }
+// (the D elsewhere forms copy their D into v[42:45] so the folds compare the same elements)
+#define D3_OVER "v[42:45]"
+#define D3_ELSE "v[42:45]"
+#define OVW12 "ds_read_b128 v[46:49], %12\n\t"
+#define OVW12_16 "s_nop 7\n\ts_nop 7\n\tds_read_b128 v[46:49], %12\n\t"
+#define OVW12_OFF "ds_read_b128 v[48:51], %12\n\t"
+MFMA3_LDS(m3_lds, D3_OVER, OVW12)
+MFMA3_LDS(m3_lds16, D3_OVER, OVW12_16)
+MFMA3_LDS(m3_lds_off, D3_OVER, OVW12_OFF)
+MFMA3_LDS(m3_none, D3_OVER, "")
+
+__global__ __launch_bounds__(256) void probe_war12(int variant, int iters, const double* __restrict__ da,
+                                                  const double* __restrict__ db, unsigned long long* __restrict__ bad,
+                                                  unsigned long long* __restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) unsigned lds[256 * 4];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = 0; k < 4; k++) lds[threadIdx.x * 4 + k] = 0xdeadbeefu ^ (threadIdx.x * 4 + k) * 0x9e3779b9u;
+    __syncthreads();
+    const unsigned addr = (unsigned)(threadIdx.x * 16);
+    unsigned long long nb = 0, acc = 0;
+    for (int it = 0; it < iters; it++) {
+        const int i = (t * 7 + it * 131) & 4095;
+        const unsigned long long ab = __double_as_longlong(da[i]), bb = __double_as_longlong(db[i]);
+        const i4v A = {(int)ab, (int)(ab >> 32), (int)(ab * 3), (int)(bb ^ ab)};
+        const i4v B = {(int)bb, (int)(bb >> 32), (int)(bb * 5), (int)(ab + bb)};
+        const i4v r = variant == 0 ? m3_lds(A, B, addr) : variant == 1 ? m3_lds16(A, B, addr) : m3_lds_off(A, B, addr);
+        const i4v e = m3_none(A, B, addr);
+        nb += (r.x != e.x) + (r.y != e.y) + (r.z != e.z) + (r.w != e.w);
+        acc += (unsigned)r.x;
+    }
+    if (nb) atomicAdd(bad, nb);
+    sink[t & 1023] = acc;
+}
+
 // VALU write then DPP read of the written VGPR (quad_perm [1,0,3,2]), 0 or 4 wait states
 __device__ __forceinline__ unsigned dpp_after_write(unsigned v, int nop) {
     unsigned r;
@@ -397,6 +457,17 @@ int main(int argc, char** argv) {
         unsigned long long nb = 0;
         hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
         printf("%-64s: %llu mismatches of %llu\n", wn[v], nb, (unsigned long long)blocks * 256 * iters);
+    }
+    const char* wn12[] = {"T12 angold: 3 MFMAs on one SrcA, D3 over its first half, LDS load over the rest",
+                          "T12 the same, the LDS load 16 wait states later",
+                          "T12 the same, the LDS load into registers no MFMA reads"};
+    for (int v = 0; v < 3; v++) {
+        hipMemset(bad, 0, 8);
+        hipLaunchKernelGGL(probe_war12, dim3(blocks), dim3(256), 0, 0, v, iters, da, db, bad, sink);
+        if (hipDeviceSynchronize() != hipSuccess) { printf("kernel error\n"); return 2; }
+        unsigned long long nb = 0;
+        hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+        printf("%-84s: %llu element mismatches of %llu\n", wn12[v], nb, 4ull * blocks * 256 * iters);
     }
     const int kw[] = {0, 2, 4, 8, 12};
     for (int test = 6; test <= 7; test++)
