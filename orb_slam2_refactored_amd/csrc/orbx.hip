@@ -678,11 +678,9 @@ static bool pyr_pair_fits(const Geom& g, int l) {
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float pf4v __attribute__((ext_vector_type(4)));
 struct PyrMfmaLane { uint32_t a[4]; float c[4]; };   // one lane's A fragment (8 f16) and C (4 f32)
-constexpr int PM_GROUPS = 4;                 // source-row groups of 16 per unit (and per ring)
-constexpr int PM_RING = 16 * PM_GROUPS;      // horizontal-sum rows per wavefront ring
-constexpr int PM_HQ = PM_RING * 4 + 4;       // dwords per column quad of a ring (+4: quads on distinct banks)
-constexpr int PM_MAXB1 = 6;                  // level-l rectangle blocks (96 columns)
-constexpr int PM_UROWS = 48;                 // output rows per unit (three steps of 16)
+constexpr int PM_MAXB1 = 6;      // level-l rectangle blocks (96 columns)
+constexpr int PM_TAB = PYR_SH;   // per-source-row table entries (rows of S)
+constexpr int PM_MAXU1 = 12;     // level-l units (block, 15-row group) per wavefront
 
 // v_mul_hi_u32_u24 on operands the compiler cannot see are < 2^24 (ring values, table coefficients)
 __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
@@ -691,57 +689,41 @@ __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
     return r;
 }
 
-// One unit: output rows y0 .. y0 + 47 (< nrow) of a 16-column block.  The four source-row groups from
-// glo (a unit reads at most 4 x 16 source rows at the supported scale factors; host check) are read
-// together (one address per unit, the groups at immediate offsets), multiplied back to back and
-// written to ring slots 0..3; then each step's ring rows are read (lane = output row n of the step,
-// column quad g).  sl: this lane's S byte offset of group 0 (kbrel + 8 g + n * PYR_SW, kb and the S
-// origin 8-byte aligned); ys[y] = {sy0 * 16, sy1 * 16 (S rows), b0 << 12, b1 << 12}, r0s[y] / rr[y] =
-// sy0 / sy1.  tcol: the block's first column in VResizeLinear's scalar tail (>= 16: none).
+// One unit: source rows 15 k .. 15 k + 15 of S (16 rows, the last shared with the next group) x a
+// 16-column block.  The product leaves lane (n, g) with the horizontal sums of source row 15 k + n,
+// columns 4 g .. 4 g + 3; at scale factors >= 1 a source row is the upper tap sy0 of at most one
+// output row, so lane n (n < 15) computes that output row from its own sums and lane n + 1's (DPP
+// row_shl:1) -- the vertical pass needs no exchange through LDS.  sp: this lane's S address of
+// group 0 (kb - S's first column + 8 g + n * PYR_SW); tab[r] = {byte offset of r's output row in the
+// output level (-1: none), b0 << 12, b1 << 12, the row in the rectangle}.  Returns the lane's 4 pixels
+// (meaningful when tab[15 k + n].x >= 0 and n < 15).
 template <bool TAIL>
-__device__ __forceinline__ void pyr_mfma_unit(const uint8_t* S, int sl, const h8v& A, const pf4v& C, uint32_t* ring,
-                                              const int4* ys, const int* r0s, const int* rr, int y0, int nrow,
-                                              int tcol, uint32_t (&o)[PM_UROWS / 16]) {
-    const int lane = lane_id(), n = lane & 15, g = lane >> 4;
+__device__ __forceinline__ uint32_t pyr_mfma_unit(const uint8_t* sp, int k, const h8v& A, const pf4v& C, const int4& t,
+                                                  int tcol) {
+    const int g = lane_id() >> 4;
     constexpr uint32_t hmask = TAIL ? 0xfffffu : 0xffff0u;   // the tail's formula needs the full sum
-    const int glo = __builtin_amdgcn_readfirstlane(r0s[y0]) >> 4;
-    const uint8_t* sp = S + (sl + glo * (16 * PYR_SW));
-    uint2 w[PM_GROUPS];
+    const uint2 w = *reinterpret_cast<const uint2*>(sp + k * (15 * PYR_SW));
+    const uint4 bu = make_uint4(__builtin_amdgcn_perm(0x64646464u, w.x, 0x04010400u),
+                                __builtin_amdgcn_perm(0x64646464u, w.x, 0x04030402u),
+                                __builtin_amdgcn_perm(0x64646464u, w.y, 0x04010400u),
+                                __builtin_amdgcn_perm(0x64646464u, w.y, 0x04030402u));
+    const pf4v d = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(h8v, bu), C, 0, 0, 0);
+    const uint32_t b0 = (uint32_t)t.y, b1 = (uint32_t)t.z;
+    uint32_t out = 0;
 #pragma unroll
-    for (int k = 0; k < PM_GROUPS; k++) w[k] = *reinterpret_cast<const uint2*>(sp + k * (16 * PYR_SW));
-    int4 yv[PM_UROWS / 16];
-#pragma unroll
-    for (int st = 0; st < PM_UROWS / 16; st++) yv[st] = ys[min(y0 + 16 * st + n, nrow - 1)];
-    pf4v d[PM_GROUPS];   // the four products issued back to back, then read
-#pragma unroll
-    for (int k = 0; k < PM_GROUPS; k++) {
-        const uint4 bu = make_uint4(__builtin_amdgcn_perm(0x64646464u, w[k].x, 0x04010400u),
-                                    __builtin_amdgcn_perm(0x64646464u, w[k].x, 0x04030402u),
-                                    __builtin_amdgcn_perm(0x64646464u, w[k].y, 0x04010400u),
-                                    __builtin_amdgcn_perm(0x64646464u, w[k].y, 0x04030402u));
-        d[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(h8v, bu), C, 0, 0, 0);
+    for (int j = 0; j < 4; j++) {
+        const uint32_t h0 = __float_as_uint(d[j]) & hmask;
+        const uint32_t h1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)h0, 0x101, 0xf, 0xf, true);   // row_shl:1 (lane 15: 0)
+        uint32_t v;
+        if (!TAIL) {
+            v = (mulhi24(h0, b0) + mulhi24(h1, b1) + 2) >> 2;
+        } else {
+            v = (mulhi24(h0 & 0xffff0u, b0) + mulhi24(h1 & 0xffff0u, b1) + 2) >> 2;
+            v = 4 * g + j >= tcol ? vtail(h0, h1, b0, b1) : v;
+        }
+        out |= v << (8 * j);
     }
-    uint32_t* rw = ring + g * PM_HQ + 4 * n;
-#pragma unroll
-    for (int k = 0; k < PM_GROUPS; k++)
-        *reinterpret_cast<uint4*>(rw + 64 * k) =
-            make_uint4(__float_as_uint(d[k][0]) & hmask, __float_as_uint(d[k][1]) & hmask,
-                       __float_as_uint(d[k][2]) & hmask, __float_as_uint(d[k][3]) & hmask);
-    // ring row r (S row) sits at byte (r - 16 glo) * 16 of the lane's column-quad area
-    const uint8_t* rq = reinterpret_cast<const uint8_t*>(ring + g * PM_HQ) - glo * 256;
-#pragma unroll
-    for (int st = 0; st < PM_UROWS / 16; st++) {
-        const uint4 h0 = *reinterpret_cast<const uint4*>(rq + yv[st].x);
-        const uint4 h1 = *reinterpret_cast<const uint4*>(rq + yv[st].y);
-        const uint32_t b0 = (uint32_t)yv[st].z, b1 = (uint32_t)yv[st].w;
-        auto px = [&](uint32_t a, uint32_t c, int k) -> uint32_t {
-            if (!TAIL) return (mulhi24(a, b0) + mulhi24(c, b1) + 2) >> 2;
-            const uint32_t v = (mulhi24(a & 0xffff0u, b0) + mulhi24(c & 0xffff0u, b1) + 2) >> 2;
-            return 4 * g + k >= tcol ? vtail(a, c, b0, b1) : v;
-        };
-        o[st] = px(h0.x, h1.x, 0) | (px(h0.y, h1.y, 1) << 8) | (px(h0.z, h1.z, 2) << 16) | (px(h0.w, h1.w, 3) << 24);
-    }
-    (void)rr;
+    return out;
 }
 
 // A block's A / C fragments from the host table
@@ -751,16 +733,19 @@ __device__ __forceinline__ void pyr_mfma_frag(const PyrMfmaLane* tab, h8v& A, pf
     C = pf4v{t.c[0], t.c[1], t.c[2], t.c[3]};
 }
 
-// The per-output-row tables of pyr_mfma_unit for output rows [r0, r0 + nrow) of a level, source
-// rows from sy_lo (threads 0..nrow-1 write one row each).
-__device__ __forceinline__ void pyr_mfma_rows(const int2* ytab, int r0, int nrow, int sy_lo, int4* ys, int* r0s, int* rr) {
+// The per-source-row table of pyr_mfma_unit: output rows [r0, r0 + nrow) of a level (row stride
+// ostride) whose source rows start at S row 0 = sy_lo.  Thread y fills source rows sy0(y) ..
+// sy0(y + 1) - 1 (thread 0 also the rows above sy0(0), the last thread the rows to PM_TAB).
+__device__ __forceinline__ void pyr_mfma_tab(const int2* ytab, int r0, int nrow, int sy_lo, int ostride, int4* tab) {
     const int y = threadIdx.x;
     if (y < nrow) {
         const int2 v = ytab[r0 + y];
-        const int s0 = (v.x & 0xffff) - sy_lo, s1 = (v.x >> 16) - sy_lo;
-        ys[y] = make_int4(s0 * 16, s1 * 16, (int)vcoef24(v.y), (int)vcoef24(v.y >> 16));
-        r0s[y] = s0;
-        rr[y] = s1;
+        const int s0 = (v.x & 0xffff) - sy_lo;
+        const int s0n = y + 1 < nrow ? (ytab[r0 + y + 1].x & 0xffff) - sy_lo : PM_TAB;
+        if (y == 0)
+            for (int r = 0; r < s0; r++) tab[r] = make_int4(-1, 0, 0, -1);
+        tab[s0] = make_int4((r0 + y) * ostride, (int)vcoef24(v.y), (int)vcoef24(v.y >> 16), y);
+        for (int r = s0 + 1; r < min(s0n, PM_TAB); r++) tab[r] = make_int4(-1, 0, 0, -1);
     }
 }
 
@@ -779,9 +764,7 @@ __global__ __launch_bounds__(256) void pyramid_pair_mfma_kernel(Geom g, int l, c
                                                                 const PyrMfmaLane* __restrict__ mt,
                                                                 const int* __restrict__ mkb) {
     __shared__ __attribute__((aligned(16))) uint8_t S[PYR_SH * PYR_SW + 16];
-    __shared__ __attribute__((aligned(16))) uint32_t ring[4 * 4 * PM_HQ];
-    __shared__ int4 ys1[PP_MAXR], ys2[PYR_TH];
-    __shared__ int r0s1[PP_MAXR], r0s2[PYR_TH], rr1[PP_MAXR], rr2[PYR_TH];
+    __shared__ int4 tab1[PM_TAB], tab2[PM_TAB];
     const LevelDev& L0 = g.lv[l - 1];
     const LevelDev& L1 = g.lv[l];
     const LevelDev& L2 = g.lv[l + 1];
@@ -804,97 +787,105 @@ __global__ __launch_bounds__(256) void pyramid_pair_mfma_kernel(Geom g, int l, c
     const int bx0 = max(0, (int)floor((c0 + 0.5) * L1.ssx - 0.5) - 2);
     const int bx1 = min(L0.w - 1, (int)floor((c1 + 0.5) * L1.ssx - 0.5) + 2);
     T.sy_lo = u(max(0, (int)floor((ay0 + 0.5) * L1.ssy - 0.5) - 2));
-    const int by1 = min(L0.h - 1, (int)floor((ay1 + 0.5) * L1.ssy - 0.5) + 2);
+    const int by1 = u(min(L0.h - 1, (int)floor((ay1 + 0.5) * L1.ssy - 0.5) + 2));
     T.xa = u(bx0 & ~15);
     T.nc = u(((bx1 - T.xa) >> 4) + 1);
     T.items = u((by1 - T.sy_lo + 1) * T.nc);
     T.mul = u(((1 << 20) + T.nc - 1) / T.nc);
     T.src = level_base(g, l - 1, f, in, in_fstride, in_step, pyr, &T.sstep);   // 16-byte aligned (host)
+    // at the level's last row the lower tap is clipped to the upper one (sy1 = sy0): S row sy0 + 1
+    // then holds a copy of the last row, so the lane below always supplies the lower tap
+    const int rep1 = by1 == L0.h - 1 ? by1 - T.sy_lo : -1;
     {
         uint4 v0, v1, v2, v3, v4;
         pyr_fetch(T, tid, v0, v1, v2, v3, v4);
-        pyr_mfma_rows(ytab + L1.ytab_off, ay0, nrow, T.sy_lo, ys1, r0s1, rr1);
-        pyr_mfma_rows(ytab + L2.ytab_off, ty0, th, ay0, ys2, r0s2, rr2);
-        pyr_stage(T, tid, S, v0, 0);
-        pyr_stage(T, tid, S, v1, 1);
-        pyr_stage(T, tid, S, v2, 2);
-        pyr_stage(T, tid, S, v3, 3);
-        pyr_stage(T, tid, S, v4, 4);
+        pyr_mfma_tab(ytab + L1.ytab_off, ay0, nrow, T.sy_lo, (int)L1.stride, tab1);
+        pyr_mfma_tab(ytab + L2.ytab_off, ty0, th, ay0, (int)L2.stride, tab2);
+        auto stage = [&](const uint4& v, int k) {
+            const int i = tid + 256 * k;
+            if (i < T.items) {
+                const int rr = pyr_piece_row(T, i), c = i - mul12(rr, T.nc);
+                *reinterpret_cast<uint4*>(&S[mul12(rr, PYR_SW) + 16 * c]) = v;
+                if (rr == rep1) *reinterpret_cast<uint4*>(&S[mul12(rr + 1, PYR_SW) + 16 * c]) = v;
+            }
+        };
+        stage(v0, 0);
+        stage(v1, 1);
+        stage(v2, 2);
+        stage(v3, 3);
+        stage(v4, 4);
     }
     __syncthreads();
-    uint32_t* myring = ring + w * 4 * PM_HQ;
     const int n = tid & 15, q = (tid >> 4) & 3;
-    constexpr int NST = PM_UROWS / 16;
-    // level l: units (block b, 48-row part p) dealt round robin to the wavefronts; the rows stay in
-    // registers until every wavefront is done reading the level-(l-1) rectangle
-    const int nb1 = (ncol + 15) >> 4, np1 = (nrow + PM_UROWS - 1) / PM_UROWS;
-    const int nu1 = nb1 * np1;
-    constexpr int MAXU1 = (PM_MAXB1 * ((PP_MAXR + PM_UROWS - 1) / PM_UROWS) + 3) / 4;
-    uint32_t o1[MAXU1][NST];
-    const long long lstride = u(L1.stride);
-    uint8_t* lrow = pyr + (long long)f * g.pyr_frame_bytes + L1.off + (long long)(ay0 + n) * lstride + c0 + 4 * q;
-#pragma unroll
-    for (int ui = 0; ui < MAXU1; ui++) {
-        const int un = w + 4 * ui;
-        if (un >= nu1) break;
-        const int b = un / np1, p = un - b * np1;
-        const int bc = c0 + 16 * b;   // the block's first column
-        const int blk = L1.mt_off + (bc >> 4);
+    // level l: units (block b, group k) block-major, a contiguous range per wavefront; the rows
+    // stay in registers until every wavefront is done reading the level-(l-1) rectangle
+    const int nb1 = (ncol + 15) >> 4;
+    const int g1 = u(((ytab[L1.ytab_off + ay1].x & 0xffff) - T.sy_lo) / 15 + 1);   // groups to the last output's sy0
+    const int nu1 = nb1 * g1;
+    const int ub = (nu1 * w) >> 2, ue = (nu1 * (w + 1)) >> 2;
+    uint32_t o1[PM_MAXU1];
+    uint8_t* lbase = pyr + (long long)f * g.pyr_frame_bytes + L1.off + c0 + 4 * q;
+    {
+        int cur = -1;
         h8v A;
         pf4v C;
-        pyr_mfma_frag(mt + (long long)blk * 64, A, C);
-        const int sl = mkb[blk] - T.xa + 8 * q + n * PYR_SW;
-        const int tcol = L1.tail_x - bc;
-        const int y0 = PM_UROWS * p;
-        if (tcol < 16) pyr_mfma_unit<true>(S, sl, A, C, myring, ys1, r0s1, rr1, y0, nrow, tcol, o1[ui]);
-        else pyr_mfma_unit<false>(S, sl, A, C, myring, ys1, r0s1, rr1, y0, nrow, tcol, o1[ui]);
-        const int col = bc + 4 * q;
-        if (col <= c1) {
-            uint8_t* dst = lrow + (long long)y0 * lstride + 16 * b;
+        const uint8_t* sp = S;
+        int tcol = 16;
 #pragma unroll
-            for (int st = 0; st < NST; st++)
-                if (y0 + 16 * st + n < nrow) pyr_store4(dst + (long long)(16 * st) * lstride, o1[ui][st], col, c1);
+        for (int i = 0; i < PM_MAXU1; i++) {
+            const int un = ub + i;
+            if (un >= ue) break;
+            const int b = un / g1, k = un - b * g1;
+            if (b != cur) {   // wavefront-uniform
+                cur = b;
+                const int blk = L1.mt_off + ((c0 >> 4) + b);
+                pyr_mfma_frag(mt + (long long)blk * 64, A, C);
+                sp = S + (mkb[blk] - T.xa + 8 * q + n * PYR_SW);
+                tcol = L1.tail_x - (c0 + 16 * b);
+            }
+            const int4 t = tab1[15 * k + n];   // < PM_TAB (host check)
+            o1[i] = tcol < 16 ? pyr_mfma_unit<true>(sp, k, A, C, t, tcol) : pyr_mfma_unit<false>(sp, k, A, C, t, tcol);
+            const int col = c0 + 16 * b + 4 * q;
+            if (t.x >= 0 && n < 15 && col <= c1) pyr_store4(lbase + 16 * b + t.x, o1[i], col, c1);
         }
     }
     __syncthreads();   // every read of the level-(l-1) rectangle done: S now takes the level-l one
+    const int rep2 = ay1 == L1.h - 1 ? nrow - 1 : -1;
 #pragma unroll
-    for (int ui = 0; ui < MAXU1; ui++) {
-        const int un = w + 4 * ui;
-        if (un >= nu1) break;
-        const int b = un / np1, p = un - b * np1;
-#pragma unroll
-        for (int st = 0; st < NST; st++) {
-            const int y = PM_UROWS * p + 16 * st + n;
-            if (y < nrow) *reinterpret_cast<uint32_t*>(&S[y * PYR_SW + 16 * b + 4 * q]) = o1[ui][st];
+    for (int i = 0; i < PM_MAXU1; i++) {
+        const int un = ub + i;
+        if (un >= ue) break;
+        const int b = un / g1, k = un - b * g1;
+        const int4 t = tab1[15 * k + n];
+        if (t.x >= 0 && n < 15) {
+            *reinterpret_cast<uint32_t*>(&S[t.w * PYR_SW + 16 * b + 4 * q]) = o1[i];
+            if (t.w == rep2) *reinterpret_cast<uint32_t*>(&S[(t.w + 1) * PYR_SW + 16 * b + 4 * q]) = o1[i];
         }
     }
     __syncthreads();
-    // level l+1: wavefront w takes block w of the 64-column tile, rows in 48-row parts
+    // level l+1: wavefront w takes block w of the 64-column tile, all its groups
     if (16 * w < tw) {
         const int bc = tx0 + 16 * w;
         const int blk = L2.mt_off + (bc >> 4);
         h8v A;
         pf4v C;
         pyr_mfma_frag(mt + (long long)blk * 64, A, C);
-        const int sl = mkb[blk] - c0 + 8 * q + n * PYR_SW;
+        const uint8_t* sp = S + (mkb[blk] - c0 + 8 * q + n * PYR_SW);
         const int col = bc + 4 * q;
         const int tcol = L2.tail_x - bc;
-        const long long dstride = u(L2.stride);
-        uint8_t* drow = pyr + (long long)f * g.pyr_frame_bytes + L2.off + col + (long long)(ty0 + n) * dstride;
-#pragma unroll
-        for (int p = 0; p < (PYR_TH + PM_UROWS - 1) / PM_UROWS; p++) {
-            const int y0 = PM_UROWS * p;
-            if (y0 >= th) break;
-            uint32_t o[NST];
-            if (tcol < 16) pyr_mfma_unit<true>(S, sl, A, C, myring, ys2, r0s2, rr2, y0, th, tcol, o);
-            else pyr_mfma_unit<false>(S, sl, A, C, myring, ys2, r0s2, rr2, y0, th, tcol, o);
-            if (col < tx0 + tw) {
-#pragma unroll
-                for (int st = 0; st < NST; st++)
-                    if (y0 + 16 * st + n < th)
-                        pyr_store4(drow + (long long)(y0 + 16 * st) * dstride, o[st], col, tx0 + tw - 1);
+        const int g2 = u(((ytab[L2.ytab_off + ty0 + th - 1].x & 0xffff) - ay0) / 15 + 1);
+        uint8_t* dbase = pyr + (long long)f * g.pyr_frame_bytes + L2.off + col;
+        const int last = tx0 + tw - 1;
+        auto run = [&](auto tail_c) {
+            constexpr bool TAIL = decltype(tail_c)::value;
+            for (int k = 0; k < g2; k++) {
+                const int4 t = tab2[15 * k + n];
+                const uint32_t o = pyr_mfma_unit<TAIL>(sp, k, A, C, t, tcol);
+                if (t.x >= 0 && n < 15 && col <= last) pyr_store4(dbase + t.x, o, col, last);
             }
-        }
+        };
+        if (tcol < 16) run(std::true_type{});
+        else run(std::false_type{});
     }
 }
 
@@ -947,13 +938,13 @@ static int pyr_mfma_tables(const int2* xt, int dw, std::vector<PyrMfmaLane>& mt,
 }
 
 // pyramid_pair_mfma_kernel's geometry replayed for every tile of the pair (l, l+1): the staged
-// rectangles fit S, every block's K window lies inside S's rows, and a unit's source rows lie in
-// at most PM_GROUPS groups of 16.
+// rectangles fit S, every block's K window lies inside S's rows, one output row per source row, and
+// the 15-row groups (and their tables) inside S.
 static bool pyr_mfma_pair_fits(const Geom& g, int l, const std::vector<int>& mkb, const std::vector<int2>& ytab) {
     const LevelDev &L0 = g.lv[l - 1], &L1 = g.lv[l], &L2 = g.lv[l + 1];
     if (L1.mt_off < 0 || L2.mt_off < 0) return false;
     auto fl = [](double v) { return (int)std::floor(v); };
-    int max_rows = 0, max_nc = 0;
+    int max_rows = 0, max_nc = 0, max_nb1 = 0, max_g1 = 0;
     for (int ty0 = 0; ty0 < L2.h; ty0 += PYR_TH) {
         const int th = std::min(PYR_TH, L2.h - ty0);
         const int ay0 = std::max(0, fl((ty0 + 0.5) * L2.ssy - 0.5) - 2);
@@ -963,21 +954,22 @@ static bool pyr_mfma_pair_fits(const Geom& g, int l, const std::vector<int>& mkb
         const int by1 = std::min(L0.h - 1, fl((ay1 + 0.5) * L1.ssy - 0.5) + 2);
         if (nrow > PP_MAXR || by1 - sy_lo + 1 > PYR_SH) return false;
         max_rows = std::max(max_rows, by1 - sy_lo + 1);
-        // the rows' taps inside the staged rows, and each 16-row step within 33 source rows
-        auto rows_ok = [&](const LevelDev& L, int r0, int nr, int lo, int cap) {
+        max_g1 = std::max(max_g1, ((ytab[L1.ytab_off + ay1].x & 0xffff) - sy_lo) / 15 + 1);
+        // per output row: sy0 strictly increasing (one output row per source row), sy1 = sy0 + 1 except
+        // at the level's last row (clipped: S holds a copy there); the groups' rows and the copy in S
+        auto rows_ok = [&](const LevelDev& L, const LevelDev& Ls, int r0, int nr, int lo, int staged) {
+            int prev = -1;
             for (int y = 0; y < nr; y++) {
                 const int2 v = ytab[L.ytab_off + r0 + y];
                 const int s0 = (v.x & 0xffff) - lo, s1 = (v.x >> 16) - lo;
-                if (s0 < 0 || s1 >= cap || s1 < s0) return false;
-                // a unit's (PM_UROWS output rows') source rows within PM_GROUPS groups of 16 inside S
-                const int2 vl = ytab[L.ytab_off + r0 + std::min(nr - 1, (y / PM_UROWS) * PM_UROWS + PM_UROWS - 1)];
-                const int2 vf = ytab[L.ytab_off + r0 + (y / PM_UROWS) * PM_UROWS];
-                const int glo = ((vf.x & 0xffff) - lo) >> 4;
-                if ((((vl.x >> 16) - lo) >> 4) - glo >= PM_GROUPS || 16 * (glo + PM_GROUPS) > PYR_SH) return false;
+                if (s0 <= prev || s0 < 0 || !(s1 == s0 + 1 || (s1 == s0 && (v.x >> 16) == Ls.h - 1))) return false;
+                if (s1 >= staged) return false;
+                prev = s0;
             }
-            return true;
+            const int groups = prev / 15 + 1;
+            return 15 * groups < PM_TAB && 15 * groups < PYR_SH && staged + 1 <= PYR_SH;
         };
-        if (!rows_ok(L1, ay0, nrow, sy_lo, by1 - sy_lo + 1) || !rows_ok(L2, ty0, th, ay0, nrow)) return false;
+        if (!rows_ok(L1, L0, ay0, nrow, sy_lo, by1 - sy_lo + 1) || !rows_ok(L2, L1, ty0, th, ay0, nrow)) return false;
     }
     for (int tx0 = 0; tx0 < L2.w; tx0 += PYR_TW) {
         const int tw = std::min(PYR_TW, L2.w - tx0);
@@ -989,6 +981,7 @@ static bool pyr_mfma_pair_fits(const Geom& g, int l, const std::vector<int>& mkb
         const int bx1 = std::min(L0.w - 1, fl((c1 + 0.5) * L1.ssx - 0.5) + 2);
         const int xa = bx0 & ~15, nc = ((bx1 - xa) >> 4) + 1;
         if (ncol > 16 * PM_MAXB1 || 16 * nc > PYR_SW) return false;
+        max_nb1 = std::max(max_nb1, (ncol + 15) / 16);
         max_nc = std::max(max_nc, nc);
         for (int b = 0; b < (ncol + 15) / 16; b++) {
             const int kbrel = mkb[L1.mt_off + (c0 >> 4) + b] - xa;
@@ -999,7 +992,7 @@ static bool pyr_mfma_pair_fits(const Geom& g, int l, const std::vector<int>& mkb
             if (kbrel < 0 || kbrel + 32 > PYR_SW) return false;
         }
     }
-    return max_rows * max_nc <= PYR_PF * 256;
+    return max_rows * max_nc <= PYR_PF * 256 && max_nb1 * max_g1 <= 4 * PM_MAXU1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1316,7 +1309,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
-                                                        int strip_beg, int nstrips, int spec_min) {
+                                                        int strip_beg, int nstrips, int spec_min, int spec_first) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -1359,7 +1352,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // the diagonal filter and the corner list at iniThFAST only.  When the NMS keeps one of them
     // that is DetectFAST's answer (:527); otherwise the cell is re-run at min(ini, min).  On
     // texture-rich frames most pixels pass at minThFAST but few at iniThFAST.
-    int prev_ini = 0;
+    int prev_ini = spec_first ? spec_min : 0;   // spec_first: a strip's first cell speculates too
     for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
     int ci;
@@ -3099,6 +3092,7 @@ struct orbx_extractor {
     // a cell runs the speculative iniThFAST pass when the wavefront's previous cell kept at least
     // fast_spec corners at iniThFAST (texture-rich regions); 0 = never (ORBX_FAST_SPEC)
     int fast_spec = 8;
+    int fast_spec_first = 0;   // a strip's first cell (no predecessor) speculates too (ORBX_FAST_SPEC_FIRST)
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     int debug_nc = 0;
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
@@ -3523,7 +3517,7 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
                                                  : fast_cells_kernel<0, 0>;
         launch_timed(h, 1, kern, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
-                           h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec);
+                           h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec, h->fast_spec_first);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
@@ -3672,6 +3666,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(-1, atoi(e));   // -1: every cell
+    if (const char* e = getenv("ORBX_FAST_SPEC_FIRST")) h->fast_spec_first = atoi(e) != 0;
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_MFMA")) h->pyr_mfma = atoi(e) != 0;
