@@ -198,6 +198,13 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));   // packed u16 
 // masks tell the compiler both operands fit in 24 bits (v_mul_hi_u32_u24 instead of the
 // quarter-rate v_mul_hi_u32).
 __device__ __forceinline__ uint32_t htap24(uint32_t h) { return h & 0xffff0u; }
+// v_mul_hi_u32_u24 on operands the compiler cannot see are < 2^24 (table coefficients b << 12, the
+// matrix-core pass's sums): no mask instruction to prove it
+__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ uint32_t vcoef24(int b) { return ((uint32_t)b & 0xfffu) << 12; }
 // VResizeLinear's scalar loop, FixedPtCast<int, uchar, 22>: (S0*b0 + S1*b1 + 2^21) >> 22 on the full
 // horizontal sums (S < 2^20, b <= 2048: both products and the sum fit 32 bits); b24 = b << 12
@@ -267,8 +274,7 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
                 constexpr bool TAIL = decltype(tail_c)::value;
                 for (int ty = threadIdx.x >> 4; ty < th; ty += 16, dst += dstep) {
                     const int4 yv = ys_t[ty];
-                    // (the masks only tell the compiler b << 12 fits 24 bits: v_mul_hi_u32_u24, not v_mul_hi_u32)
-                    const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;
+                    const uint32_t b0 = (uint32_t)yv.z, b1 = (uint32_t)yv.w;   // b << 12 (pyr_row_taps)
                     uint32_t out = 0;
 #pragma unroll
                     for (int j = 0; j < 2; j++) {
@@ -279,8 +285,8 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
                         const uint32_t r1a = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel0[j]), a0[j], 0u, false);
                         const uint32_t r0b = __builtin_amdgcn_udot2(pyr_tap(w01, w00, sel1[j]), a1[j], 0u, false);
                         const uint32_t r1b = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel1[j]), a1[j], 0u, false);
-                        uint32_t va = (__umulhi(htap24(r0a), b0) + __umulhi(htap24(r1a), b1) + 2) >> 2;
-                        uint32_t vb = (__umulhi(htap24(r0b), b0) + __umulhi(htap24(r1b), b1) + 2) >> 2;
+                        uint32_t va = (mulhi24(htap24(r0a), b0) + mulhi24(htap24(r1a), b1) + 2) >> 2;
+                        uint32_t vb = (mulhi24(htap24(r0b), b0) + mulhi24(htap24(r1b), b1) + 2) >> 2;
                         if (TAIL) {
                             va = 2 * j >= tcol ? vtail(r0a, r1a, b0, b1) : va;
                             vb = 2 * j + 1 >= tcol ? vtail(r0b, r1b, b0, b1) : vb;
@@ -599,7 +605,7 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
                 if (r >= nrow) break;
                 const int4 yv = ys1[r];
                 if (fits) {
-                    const uint32_t b0 = (uint32_t)yv.z & 0xfff000u, b1 = (uint32_t)yv.w & 0xfff000u;   // 24-bit: see above
+                    const uint32_t b0 = (uint32_t)yv.z, b1 = (uint32_t)yv.w;   // b << 12 (pyr_row_taps)
 #pragma unroll
                     for (int j = 0; j < 2; j++) {
                         const uint32_t* s0 = reinterpret_cast<const uint32_t*>(S + yv.x + 4 * (int)wdv[j]);
@@ -609,8 +615,8 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
                         const uint32_t r1a = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel0[j]), a0[j], 0u, false);
                         const uint32_t r0b = __builtin_amdgcn_udot2(pyr_tap(w01, w00, sel1[j]), a1[j], 0u, false);
                         const uint32_t r1b = __builtin_amdgcn_udot2(pyr_tap(w11, w10, sel1[j]), a1[j], 0u, false);
-                        uint32_t va = (__umulhi(htap24(r0a), b0) + __umulhi(htap24(r1a), b1) + 2) >> 2;
-                        uint32_t vb = (__umulhi(htap24(r0b), b0) + __umulhi(htap24(r1b), b1) + 2) >> 2;
+                        uint32_t va = (mulhi24(htap24(r0a), b0) + mulhi24(htap24(r1a), b1) + 2) >> 2;
+                        uint32_t vb = (mulhi24(htap24(r0b), b0) + mulhi24(htap24(r1b), b1) + 2) >> 2;
                         if (TAIL) {
                             va = 2 * j >= tcol ? vtail(r0a, r1a, b0, b1) : va;
                             vb = 2 * j + 1 >= tcol ? vtail(r0b, r1b, b0, b1) : vb;
@@ -682,12 +688,6 @@ constexpr int PM_MAXB1 = 6;      // level-l rectangle blocks (96 columns)
 constexpr int PM_TAB = PYR_SH;   // per-source-row table entries (rows of S)
 constexpr int PM_MAXU1 = 12;     // level-l units (block, 15-row group) per wavefront
 
-// v_mul_hi_u32_u24 on operands the compiler cannot see are < 2^24 (ring values, table coefficients)
-__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
 
 // One unit: source rows 15 k .. 15 k + 15 of S (16 rows, the last shared with the next group) x a
 // 16-column block.  The product leaves lane (n, g) with the horizontal sums of source row 15 k + n,
@@ -3092,7 +3092,9 @@ struct orbx_extractor {
     // a cell runs the speculative iniThFAST pass when the wavefront's previous cell kept at least
     // fast_spec corners at iniThFAST (texture-rich regions); 0 = never (ORBX_FAST_SPEC)
     int fast_spec = 8;
-    int fast_spec_first = 0;   // a strip's first cell (no predecessor) speculates too (ORBX_FAST_SPEC_FIRST)
+    // a strip's first cell (no predecessor) speculates too (ORBX_FAST_SPEC_FIRST=0: never): fast_cells
+    // 5.00 -> 4.38 ms per 1024 textured frames, 4.68 -> 4.74 per 2048 pan frames (round 5)
+    int fast_spec_first = 1;
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     int debug_nc = 0;
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
