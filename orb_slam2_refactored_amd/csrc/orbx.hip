@@ -1309,7 +1309,8 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
-                                                        int strip_beg, int nstrips, int spec_min, int spec_first) {
+                                                        int strip_beg, int nstrips, int spec_min,
+                                                        int* __restrict__ cell_hint) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -1352,11 +1353,15 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // the diagonal filter and the corner list at iniThFAST only.  When the NMS keeps one of them
     // that is DetectFAST's answer (:527); otherwise the cell is re-run at min(ini, min).  On
     // texture-rich frames most pixels pass at minThFAST but few at iniThFAST.
-    int prev_ini = spec_first ? spec_min : 0;   // spec_first: a strip's first cell speculates too
+    // A strip's first cell has no predecessor: with cell_hint it takes the iniThFAST count its cell had
+    // in frame 0 of the previous launch (consecutive batches of a sequence see the same texture there).
+    // The hint only decides whether to speculate, never the result.
+    int prev_ini = 0;
     for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
     int ci;
     const CropSrc src = source(item, cell, ci);
+    if (item == i_beg && cell_hint) prev_ini = __builtin_amdgcn_readfirstlane(cell_hint[ci]);
     const int x0 = src.x0, y0 = src.y0;
     const int zh = cell.zwzh >> 16;
     {
@@ -1593,6 +1598,7 @@ full_pass:   // the speculative pass kept no corner at iniThFAST: the full pass 
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
         cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap);
+        if (f == 0 && cell_hint) cell_hint[ci] = n_ini;   // one writer per cell: frame 0
     }
     if (item == i_beg) {
         FAST_STAMP(2, __builtin_amdgcn_s_memtime());
@@ -3092,9 +3098,10 @@ struct orbx_extractor {
     // a cell runs the speculative iniThFAST pass when the wavefront's previous cell kept at least
     // fast_spec corners at iniThFAST (texture-rich regions); 0 = never (ORBX_FAST_SPEC)
     int fast_spec = 8;
-    // a strip's first cell (no predecessor) speculates too (ORBX_FAST_SPEC_FIRST=0: never): fast_cells
-    // 5.00 -> 4.38 ms per 1024 textured frames, 4.68 -> 4.74 per 2048 pan frames (round 5)
+    // a strip's first cell (no predecessor) speculates when its cell kept >= fast_spec iniThFAST corners
+    // in frame 0 of the previous launch (d_cellhint; ORBX_FAST_SPEC_FIRST=0: never)
     int fast_spec_first = 1;
+    DevBuf d_cellhint;
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     int debug_nc = 0;
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
@@ -3407,6 +3414,8 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
                 }
         }
         h->strip_beg[g.nlevels] = (int)strips.size();
+        if ((rc = h->d_cellhint.reserve(std::max<size_t>(1, cells.size()) * sizeof(int)))) return rc;
+        ORB_HIP_TRY(hipMemset(h->d_cellhint.ptr, 0, std::max<size_t>(1, cells.size()) * sizeof(int)));
         if ((rc = h->d_strips.reserve(std::max<size_t>(1, strips.size()) * sizeof(int2)))) return rc;
         if (!strips.empty())
             ORB_HIP_TRY(hipMemcpy(h->d_strips.ptr, strips.data(), strips.size() * sizeof(int2), hipMemcpyHostToDevice));
@@ -3519,7 +3528,8 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
                                                  : fast_cells_kernel<0, 0>;
         launch_timed(h, 1, kern, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
-                           h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec, h->fast_spec_first);
+                           h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec,
+                           h->fast_spec_first ? h->d_cellhint.as<int>() : (int*)nullptr);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
@@ -3696,7 +3706,7 @@ int orbx_destroy(orbx_extractor* h) {
     (void)hipSetDevice(h->device);
     DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
-                      &h->d_counts, &h->d_stereo_sad};
+                      &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb, &h->d_cellhint};
     for (DevBuf* b : bufs) b->release();
     for (auto& v : h->prof_ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
