@@ -1310,7 +1310,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
                                                         int th_min, uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
                                                         int strip_beg, int nstrips, int spec_min,
-                                                        int* __restrict__ cell_hint) {
+                                                        int* __restrict__ cell_hint, int hint_all) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -1361,7 +1361,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     CellDev cell;
     int ci;
     const CropSrc src = source(item, cell, ci);
-    if (item == i_beg && cell_hint) prev_ini = __builtin_amdgcn_readfirstlane(cell_hint[ci]);
+    if ((item == i_beg || hint_all) && cell_hint) prev_ini = __builtin_amdgcn_readfirstlane(cell_hint[ci]);
     const int x0 = src.x0, y0 = src.y0;
     const int zh = cell.zwzh >> 16;
     {
@@ -3529,7 +3529,7 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         launch_timed(h, 1, kern, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
                            h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec,
-                           h->fast_spec_first ? h->d_cellhint.as<int>() : (int*)nullptr);
+                           h->fast_spec_first ? h->d_cellhint.as<int>() : (int*)nullptr, h->fast_spec_first == 2);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
@@ -3678,7 +3678,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(-1, atoi(e));   // -1: every cell
-    if (const char* e = getenv("ORBX_FAST_SPEC_FIRST")) h->fast_spec_first = atoi(e) != 0;
+    if (const char* e = getenv("ORBX_FAST_SPEC_FIRST")) h->fast_spec_first = std::max(0, std::min(2, atoi(e)));   // 2: every cell by its hint
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_MFMA")) h->pyr_mfma = atoi(e) != 0;
