@@ -301,7 +301,9 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
                     }
                 }
             };
-            if (tcol < 4) rows(std::true_type{});
+            // block-uniform: only the tiles that reach the tail run the selecting loop (a per-thread choice
+            // made the waves holding both kinds of lane run both loops)
+            if (tx0 + tw > L.tail_x) rows(std::true_type{});
             else rows(std::false_type{});
             return;
         }
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
                 }
             }
         };
-        if (tcol < 4) rows(std::true_type{});
+        if (c1 >= L1.tail_x) rows(std::true_type{});   // block-uniform, as in pyr_tile_compute
         else rows(std::false_type{});
     }
     __syncthreads();   // every read of the level-(l-1) rectangle done: S now takes the level-l one
@@ -1309,8 +1311,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
                                                         int in_step, const uint8_t* __restrict__ pyr, int th_ini,
                                                         int th_min, uint32_t* __restrict__ slots,
                                                         int* __restrict__ cell_cnt, uint32_t* fault, FastLds fl,
-                                                        int strip_beg, int nstrips, int spec_min,
-                                                        int* __restrict__ cell_hint, int hint_all) {
+                                                        int strip_beg, int nstrips, int spec_arg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fsm[];
     uint8_t* crop = fsm;                                   // crop col c at byte 1 + c
     uint8_t* Mz = fsm + fl.crop_bytes;
@@ -1353,20 +1354,26 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // the diagonal filter and the corner list at iniThFAST only.  When the NMS keeps one of them
     // that is DetectFAST's answer (:527); otherwise the cell is re-run at min(ini, min).  On
     // texture-rich frames most pixels pass at minThFAST but few at iniThFAST.
-    // A strip's first cell has no predecessor: with cell_hint it takes the iniThFAST count its cell had
-    // in frame 0 of the previous launch (consecutive batches of a sequence see the same texture there).
-    // The hint only decides whether to speculate, never the result.
+    // spec_arg: the threshold (-1: every cell), bit 29 (threshold > 0 only): a strip's first cell, which has
+    // no predecessor, takes as its hint the corner count its cell kept in frame 0 -- cell_cnt's frame-0
+    // slot, from this launch or the previous one (consecutive batches of a sequence see the same texture
+    // there).  No extra pointer: the kernel is at its SGPR limit.  The hint only decides whether to
+    // speculate, never the result.
+    const int spec_min = spec_arg < 0 ? spec_arg : spec_arg & 0x1fffffff;
+    const bool hint_first = spec_arg > 0 && ((spec_arg >> 29) & 1);
     int prev_ini = 0;
     for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
     int ci;
     const CropSrc src = source(item, cell, ci);
-    if ((item == i_beg || hint_all) && cell_hint) prev_ini = __builtin_amdgcn_readfirstlane(cell_hint[ci]);
+    const bool use_hint = hint_first && item == i_beg;
+    const int hint = use_hint ? cell_cnt[ci] : 0;   // issued ahead of the crop loads, read after them
     const int x0 = src.x0, y0 = src.y0;
     const int zh = cell.zwzh >> 16;
     {
         crop_stage_rows<CST>(src, lane, crop, CSd);
     }
+    if (use_hint) prev_ini = __builtin_amdgcn_readfirstlane(hint);
     const int tlo = min(th_ini, th_min);
     bool spec = spec_min != 0 && th_ini > tlo && prev_ini >= spec_min;   // spec_min < 0: every cell
     uint8_t* Mc = Mz + ZSd + 1;   // zone (0, 0); the zero border makes out-of-zone neighbours read 0
@@ -1598,7 +1605,6 @@ full_pass:   // the speculative pass kept no corner at iniThFAST: the full pass 
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
         cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap);
-        if (f == 0 && cell_hint) cell_hint[ci] = n_ini;   // one writer per cell: frame 0
     }
     if (item == i_beg) {
         FAST_STAMP(2, __builtin_amdgcn_s_memtime());
@@ -3098,10 +3104,9 @@ struct orbx_extractor {
     // a cell runs the speculative iniThFAST pass when the wavefront's previous cell kept at least
     // fast_spec corners at iniThFAST (texture-rich regions); 0 = never (ORBX_FAST_SPEC)
     int fast_spec = 8;
-    // a strip's first cell (no predecessor) speculates when its cell kept >= fast_spec iniThFAST corners
-    // in frame 0 of the previous launch (d_cellhint; ORBX_FAST_SPEC_FIRST=0: never)
+    // a strip's first cell (no predecessor) speculates when its cell kept >= fast_spec corners in frame 0
+    // (cell_cnt's frame-0 slot; ORBX_FAST_SPEC_FIRST=0: never)
     int fast_spec_first = 1;
-    DevBuf d_cellhint;
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     int debug_nc = 0;
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
@@ -3238,7 +3243,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
                 if (dx >= xmax) { sx1 = sx0; a0 = 2048; a1 = 0; }
                 xtab.push_back(make_int2(sx0 | (sx1 << 16), (a0 & 0xffff) | (a1 << 16)));
             }
-            L.mt_off = pyr_mfma_tables(xtab.data() + L.xtab_off, dw, mt, mkb);
+            L.mt_off = h->pyr_mfma ? pyr_mfma_tables(xtab.data() + L.xtab_off, dw, mt, mkb) : -1;
             for (int dy = 0; dy < dh; dy++) {
                 float fy = (float)((dy + 0.5) * scale_y - 0.5);
                 int sy = (int)std::floor(fy);
@@ -3373,14 +3378,15 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         ORB_HIP_TRY(hipMemcpy(h->d_xtab.ptr, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice));
     if (!ytab.empty())
         ORB_HIP_TRY(hipMemcpy(h->d_ytab.ptr, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice));
-    if ((rc = h->d_pyrmt.reserve(std::max<size_t>(1, mt.size()) * sizeof(PyrMfmaLane)))) return rc;
-    if ((rc = h->d_pyrkb.reserve(std::max<size_t>(1, mkb.size()) * sizeof(int)))) return rc;
+    // (only with ORBX_PYR_MFMA=1: the default path allocates nothing for it)
+    if (!mt.empty() && (rc = h->d_pyrmt.reserve(mt.size() * sizeof(PyrMfmaLane)))) return rc;
+    if (!mkb.empty() && (rc = h->d_pyrkb.reserve(mkb.size() * sizeof(int)))) return rc;
     if (!mt.empty())
         ORB_HIP_TRY(hipMemcpy(h->d_pyrmt.ptr, mt.data(), mt.size() * sizeof(PyrMfmaLane), hipMemcpyHostToDevice));
     if (!mkb.empty())
         ORB_HIP_TRY(hipMemcpy(h->d_pyrkb.ptr, mkb.data(), mkb.size() * sizeof(int), hipMemcpyHostToDevice));
     h->pyr_mfma_ok.assign(Lc, 0);
-    for (int l = 1; l + 1 < Lc; l++) h->pyr_mfma_ok[l] = pyr_mfma_pair_fits(g, l, mkb, ytab);
+    for (int l = 1; l + 1 < Lc; l++) h->pyr_mfma_ok[l] = h->pyr_mfma && pyr_mfma_pair_fits(g, l, mkb, ytab);
     h->geom = g;
     h->cells = cells;
     {   // FAST column strips: up to fast_cpw vertically consecutive cells of one column per wavefront
@@ -3414,8 +3420,6 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
                 }
         }
         h->strip_beg[g.nlevels] = (int)strips.size();
-        if ((rc = h->d_cellhint.reserve(std::max<size_t>(1, cells.size()) * sizeof(int)))) return rc;
-        ORB_HIP_TRY(hipMemset(h->d_cellhint.ptr, 0, std::max<size_t>(1, cells.size()) * sizeof(int)));
         if ((rc = h->d_strips.reserve(std::max<size_t>(1, strips.size()) * sizeof(int2)))) return rc;
         if (!strips.empty())
             ORB_HIP_TRY(hipMemcpy(h->d_strips.ptr, strips.data(), strips.size() * sizeof(int2), hipMemcpyHostToDevice));
@@ -3528,8 +3532,8 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
                                                  : fast_cells_kernel<0, 0>;
         launch_timed(h, 1, kern, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
-                           h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns, h->fast_spec,
-                           h->fast_spec_first ? h->d_cellhint.as<int>() : (int*)nullptr, h->fast_spec_first == 2);
+                           h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns,
+                           h->fast_spec > 0 && h->fast_spec_first ? h->fast_spec | (1 << 29) : h->fast_spec);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
@@ -3678,7 +3682,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(-1, atoi(e));   // -1: every cell
-    if (const char* e = getenv("ORBX_FAST_SPEC_FIRST")) h->fast_spec_first = std::max(0, std::min(2, atoi(e)));   // 2: every cell by its hint
+    if (const char* e = getenv("ORBX_FAST_SPEC_FIRST")) h->fast_spec_first = atoi(e) != 0;
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_PAIR")) h->pyr_pair = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("ORBX_PYR_MFMA")) h->pyr_mfma = atoi(e) != 0;
@@ -3706,7 +3710,7 @@ int orbx_destroy(orbx_extractor* h) {
     (void)hipSetDevice(h->device);
     DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
-                      &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb, &h->d_cellhint};
+                      &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb};
     for (DevBuf* b : bufs) b->release();
     for (auto& v : h->prof_ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
