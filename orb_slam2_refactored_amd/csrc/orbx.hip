@@ -61,11 +61,14 @@ struct LevelDev {
     int nroots;
     double hx;
     float scale, size;
-    long long xtab_off, ytab_off;   // resize coefficient tables (l >= 1)
-    double ssx, ssy;                // (double)w[l-1] / w[l], (double)h[l-1] / h[l] (l >= 1)
+    int xtab_off, ytab_off;         // resize coefficient tables (l >= 1)
     int tail_x;                     // first column of VResizeLinear's scalar tail (l >= 1; w: none)
     int mt_off;                     // first 16-column block in the matrix-core resize tables (-1: none)
+    double ssx, ssy;                // (double)w[l-1] / w[l], (double)h[l-1] / h[l] (l >= 1)
 };
+// 128 bytes: g.lv[l] is a shift, and the kernels' scalar registers stay where round 4 had them (a
+// 136-byte LevelDev made fast_cells' level indexing a multiply and moved its SGPR spills: +3.7 %)
+static_assert(sizeof(LevelDev) == 128, "LevelDev stays 128 bytes");
 
 struct Geom {
     int nlevels;
@@ -88,6 +91,9 @@ __device__ __forceinline__ int divmod_of(const Geom& g, int n) {
     const unsigned t = __umulhi((unsigned)n, g.of_m);
     return (int)((t + (((unsigned)n - t) >> g.of_s1)) >> g.of_s2);
 }
+
+// cell_cnt entries: the cell's kept corner count, plus a hint bit for fast_cells' next launch
+constexpr int CELL_CNT_MASK = 0xffff, CELL_CNT_INI = 1 << 30;
 
 struct CellDev {
     int level;
@@ -891,6 +897,16 @@ __global__ __launch_bounds__(256) void pyramid_pair_mfma_kernel(Geom g, int l, c
     }
 }
 
+// FAST's first-cell hint for the next launch: bit 31 of every strip descriptor = the CELL_CNT_INI bit of
+// its first cell in frame 0 (cell_cnt's frame-0 slots).  One thread per strip, after fast_cells.
+__global__ void fast_hint_kernel(int2* __restrict__ strips, const int* __restrict__ cell_cnt, int nstrips) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nstrips) return;
+    const int2 sd = strips[s];
+    const unsigned bit = (cell_cnt[sd.x] & CELL_CNT_INI) ? 0x80000000u : 0u;
+    strips[s].y = (int)(((unsigned)sd.y & 0x7fffffffu) | bit);
+}
+
 // f16 bits of an integer 0 <= v <= 2048 (exact: at most 11 significant bits)
 static uint16_t f16_of_int(int v) {
     if (v <= 0) return 0;
@@ -1326,7 +1342,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // wavefront = (frame, column strip): up to fast_cpw vertically consecutive cells of one column
     const int f = lb / nstrips;
     const int2 sd = strips[strip_beg + lb - f * nstrips];
-    const int i_beg = 0, i_end = sd.y & 255, cstride = sd.y >> 8;
+    const int i_beg = 0, i_end = sd.y & 255, cstride = (sd.y >> 8) & 0x7fffff;   // bit 31: the first-cell hint
     // every cell of a strip has the same level and zone width (host-checked): the crop's level
     // base, step and row-dword count and every per-lane quantity that depends on the zone width are
     // loop-invariant over the strip
@@ -1355,25 +1371,22 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // that is DetectFAST's answer (:527); otherwise the cell is re-run at min(ini, min).  On
     // texture-rich frames most pixels pass at minThFAST but few at iniThFAST.
     // spec_arg: the threshold (-1: every cell), bit 29 (threshold > 0 only): a strip's first cell, which has
-    // no predecessor, takes as its hint the corner count its cell kept in frame 0 -- cell_cnt's frame-0
-    // slot, from this launch or the previous one (consecutive batches of a sequence see the same texture
-    // there).  No extra pointer: the kernel is at its SGPR limit.  The hint only decides whether to
-    // speculate, never the result.
+    // no predecessor, speculates when the strip's hint bit (bit 31 of its descriptor, set by
+    // fast_hint_kernel from the CELL_CNT_INI bit its cell got in frame 0 of the previous launch) is set.
+    // Consecutive batches of a sequence see the same texture there.  The hint costs the cell loop
+    // nothing (the descriptor is already in SGPRs; the kernel is at its SGPR limit), and it only decides
+    // whether to speculate, never the result.
     const int spec_min = spec_arg < 0 ? spec_arg : spec_arg & 0x1fffffff;
-    const bool hint_first = spec_arg > 0 && ((spec_arg >> 29) & 1);
-    int prev_ini = 0;
+    int prev_ini = (spec_arg > 0 && ((spec_arg >> 29) & 1) && sd.y < 0) ? spec_min : 0;
     for (int item = i_beg; item < i_end; item++) {
     CellDev cell;
     int ci;
     const CropSrc src = source(item, cell, ci);
-    const bool use_hint = hint_first && item == i_beg;
-    const int hint = use_hint ? cell_cnt[ci] : 0;   // issued ahead of the crop loads, read after them
     const int x0 = src.x0, y0 = src.y0;
     const int zh = cell.zwzh >> 16;
     {
         crop_stage_rows<CST>(src, lane, crop, CSd);
     }
-    if (use_hint) prev_ini = __builtin_amdgcn_readfirstlane(hint);
     const int tlo = min(th_ini, th_min);
     bool spec = spec_min != 0 && th_ini > tlo && prev_ini >= spec_min;   // spec_min < 0: every cell
     uint8_t* Mc = Mz + ZSd + 1;   // zone (0, 0); the zero border makes out-of-zone neighbours read 0
@@ -1604,7 +1617,9 @@ full_pass:   // the speculative pass kept no corner at iniThFAST: the full pass 
     if (item == i_beg) FAST_STAMP(4, __builtin_amdgcn_s_memtime());
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
-        cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap);
+        // bit 30: this cell kept >= spec_min corners at iniThFAST (the next strips' first-cell hint;
+        // the quadtree masks the count with CELL_CNT_MASK)
+        cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap) | (n_ini >= spec_min ? CELL_CNT_INI : 0);
     }
     if (item == i_beg) {
         FAST_STAMP(2, __builtin_amdgcn_s_memtime());
@@ -2070,7 +2085,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
             cv[k] = 0; cs[k] = 0; rl[k] = 0; rh[k] = 0;
             if (i < L.ncells) {
                 const CellDev cd = cells[L.cell_base + i];
-                cv[k] = ccell[i];
+                cv[k] = ccell[i] & CELL_CNT_MASK;
                 cs[k] = cd.slot;
                 const int zx = (cd.x0y0 & 0xffff) + 3;            // the zone's first column
                 rl[k] = root_x(zx);
@@ -2153,7 +2168,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int i = i0 + k;
-            cv[k] = i < L.ncells ? ccell[i] : 0;
+            cv[k] = i < L.ncells ? ccell[i] & CELL_CNT_MASK : 0;
             cs[k] = i < L.ncells ? cells[L.cell_base + i].slot : 0;
         }
         const int sum = cv[0] + cv[1] + cv[2] + cv[3];
@@ -2176,7 +2191,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
     } else {
         {
             int part = 0;
-            for (int i = threadIdx.x; i < L.ncells; i += blockDim.x) part += ccell[i];
+            for (int i = threadIdx.x; i < L.ncells; i += blockDim.x) part += ccell[i] & CELL_CNT_MASK;
             part = wave_sum_i32(part);
             if (lane_id() == 0) tmp[8 + w] = part;
             __syncthreads();
@@ -2186,7 +2201,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
         if (n_total <= PTC) { P = lds_P; T = lds_T; }
         for (int b = 0; b < L.ncells; b += blockDim.x) {
             const int i = b + threadIdx.x;
-            const int v = i < L.ncells ? ccell[i] : 0;
+            const int v = i < L.ncells ? ccell[i] & CELL_CNT_MASK : 0;
             int tot;
             const int ex = block_excl_scan(v, tmp, &tot);
             if (v > 0) {
@@ -3218,8 +3233,8 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
             // cv::resize tables (same arithmetic as the oracle / OpenCV)
             const int sw = prev_w, sh = prev_h, dw = L.w, dh = L.h;
             const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
-            L.xtab_off = (long long)xtab.size();
-            L.ytab_off = (long long)ytab.size();
+            L.xtab_off = (int)xtab.size();
+            L.ytab_off = (int)ytab.size();
             L.ssx = (double)sw / L.w;
             L.ssy = (double)sh / L.h;
             L.tail_x = resize_tail_x(L.w, h->resize_simd);
@@ -3534,6 +3549,9 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
                            h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns,
                            h->fast_spec > 0 && h->fast_spec_first ? h->fast_spec | (1 << 29) : h->fast_spec);
+        if (h->fast_spec > 0 && h->fast_spec_first)   // the hint bits for the next launch (this one has read them)
+            hipLaunchKernelGGL(fast_hint_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s,
+                               h->d_strips.as<int2>() + sb, h->d_cellcnt.as<int>(), ns);
     };
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
@@ -3920,7 +3938,7 @@ int orbx_debug_level_candidates(const orbx_extractor* h, int frame, int level, u
     int m = 0;
     for (int c = 0; c < L.ncells; c++) {
         const CellDev& cd = h->cells[L.cell_base + c];
-        for (int j = 0; j < cnt[c]; j++) {
+        for (int j = 0; j < (cnt[c] & CELL_CNT_MASK); j++) {
             if (out && m < cap) out[m] = slots[cd.slot + j];
             m++;
         }
