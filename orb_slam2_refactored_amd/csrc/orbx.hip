@@ -207,9 +207,13 @@ __device__ __forceinline__ uint32_t htap24(uint32_t h) { return h & 0xffff0u; }
 // v_mul_hi_u32_u24 on operands the compiler cannot see are < 2^24 (table coefficients b << 12, the
 // matrix-core pass's sums): no mask instruction to prove it
 __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+#ifdef PYR_MULHI_MASK_DIAG   // diagnostic A/B only: the masked compiler form
+    return __umulhi(a & 0xffffffu, b & 0xffffffu);
+#else
     uint32_t r;
     asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
+#endif
 }
 __device__ __forceinline__ uint32_t vcoef24(int b) { return ((uint32_t)b & 0xfffu) << 12; }
 // VResizeLinear's scalar loop, FixedPtCast<int, uchar, 22>: (S0*b0 + S1*b1 + 2^21) >> 22 on the full
@@ -309,8 +313,11 @@ __device__ __forceinline__ void pyr_tile_compute(const Geom& g, const LevelDev& 
             };
             // block-uniform: only the tiles that reach the tail run the selecting loop (a per-thread choice
             // made the waves holding both kinds of lane run both loops)
+#ifndef PYR_NO_TAIL_DIAG
             if (tx0 + tw > L.tail_x) rows(std::true_type{});
-            else rows(std::false_type{});
+            else
+#endif
+                rows(std::false_type{});
             return;
         }
     }
@@ -637,8 +644,11 @@ __global__ __launch_bounds__(256) void pyramid_pair_kernel(Geom g, int l, const 
                 }
             }
         };
+#ifndef PYR_NO_TAIL_DIAG   // diagnostic A/B only (drops the tail's formula): the price of its instantiation
         if (c1 >= L1.tail_x) rows(std::true_type{});   // block-uniform, as in pyr_tile_compute
-        else rows(std::false_type{});
+        else
+#endif
+            rows(std::false_type{});
     }
     __syncthreads();   // every read of the level-(l-1) rectangle done: S now takes the level-l one
     if (act) {
