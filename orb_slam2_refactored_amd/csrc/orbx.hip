@@ -1889,12 +1889,15 @@ __device__ __forceinline__ void qt_emit_children(const QtNode& parent, int4 cc, 
     }
 }
 
+#ifndef QT_STAMP_LEVEL
+#define QT_STAMP_LEVEL 0   // the level whose frame-0 workgroup records the phase stamps (ORB_QT_STAMPS)
+#endif
 #ifdef ORB_QT_STAMPS
 __device__ unsigned long long g_qt_stamps[64];
 __device__ unsigned long long g_qt_wg[4096 * 2];   // per (frame, level) WG: start, end
 #define QT_STAMP(k)                                                                                \
     do {                                                                                           \
-        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && (k) < 64)                    \
+        if (blockIdx.x == 0 && lev0 + (int)blockIdx.y == QT_STAMP_LEVEL && threadIdx.x == 0 && (k) < 64)\
             g_qt_stamps[(k)] = __builtin_amdgcn_s_memtime();                                       \
     } while (0)
 #else
@@ -2106,17 +2109,35 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
 #pragma unroll
         for (int k = 0; k < 4; k++) bad |= cv[k] > 0 && (rl[k] < 0 || rh[k] >= R);
         if (bad) atomicOr(fault, FAULT_QT_ROOT);
+        uint32_t r[4][8];   // every cell's first 8 points, one batch of loads for the counts and the copy
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[k][q] = q < cv[k] ? fslots[cs[k] + q] : 0u;
         int cnt[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (rl[k] == rh[k]) {
 #pragma unroll
                 for (int rt = 0; rt < 4; rt++) cnt[rt] += rl[k] == rt ? cv[k] : 0;
-            } else {   // a boundary cell (rare): its points' roots
-                for (int q = 0; q < cv[k]; q++) {
-                    const int rt = root_x(kp_x(fslots[cs[k] + q]));
+            } else {   // a boundary cell: its points' roots, loads in batches of 8 (a textured frame's
+                       // boundary cells hold tens of points: one dependent load per point made this
+                       // thread the gather's critical path, round 5)
+                auto count = [&](uint32_t kk) {
+                    const int rt = root_x(kp_x(kk));
 #pragma unroll
                     for (int u = 0; u < 4; u++) cnt[u] += rt == u;
+                };
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (q < cv[k]) count(r[k][q]);
+                for (int q0 = 8; q0 < cv[k]; q0 += 8) {
+                    uint32_t r2[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) r2[q] = q0 + q < cv[k] ? fslots[cs[k] + q0 + q] : 0u;
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (q0 + q < cv[k]) count(r2[q]);
                 }
             }
         }
@@ -2132,11 +2153,6 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
         }
         n_total = base;
         if (n_total <= PTC) { P = lds_P; T = lds_T; }
-        uint32_t r[4][8];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int q = 0; q < 8; q++) r[k][q] = q < cv[k] ? fslots[cs[k] + q] : 0u;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (rl[k] == rh[k]) {
@@ -2157,8 +2173,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
 #pragma unroll
                 for (int rt = 0; rt < 4; rt++) run[rt] += rl[k] == rt ? cv[k] : 0;
             } else {
-                for (int q = 0; q < cv[k]; q++) {
-                    const uint32_t kk = fslots[cs[k] + q];
+                auto put = [&](uint32_t kk) {
                     const int rt = root_x(kp_x(kk));
                     int o = run[0];
 #pragma unroll
@@ -2166,6 +2181,17 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                     P[o] = kk;
 #pragma unroll
                     for (int u = 0; u < 4; u++) run[u] += rt == u;
+                };
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (q < cv[k]) put(r[k][q]);
+                for (int q0 = 8; q0 < cv[k]; q0 += 8) {
+                    uint32_t r2[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) r2[q] = q0 + q < cv[k] ? fslots[cs[k] + q0 + q] : 0u;
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (q0 + q < cv[k]) put(r2[q]);
                 }
             }
         }
@@ -2366,7 +2392,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
         const int n = s_n;
         const int state = s_state;
         QT_STAMP(3 + 2 * iter_no);
-        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+        if (threadIdx.x == 0 && blockIdx.x == 0 && l == QT_STAMP_LEVEL) {
 #ifdef ORB_QT_STAMPS
             if (4 + 2 * iter_no < 60) g_qt_stamps[4 + 2 * iter_no] = ((unsigned long long)state << 32) | (unsigned)n;
 #endif
@@ -2417,10 +2443,12 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                 }
             }
             __syncthreads();
-            // group positions: reverse processing order; divisibles: forward order
+            // group positions: reverse processing order; divisibles: forward order.  The ne and dv counts
+            // share one block scan (16-bit halves: a chunk's totals are <= 4 blockDim); with one chunk
+            // (kdiv <= blockDim, every small level) the scan's total is the grand total the reverse
+            // order needs, so the separate total pass and its two barriers are skipped (round 5)
             int ne_carry = 0, dv_carry = 0, ne_total = 0;
-            // total ne first
-            {
+            if (kdiv > (int)blockDim.x) {   // block-uniform
                 int part = 0;
                 for (int j = threadIdx.x; j < kdiv; j += blockDim.x) part += ne4(cc[j]);
                 part = wave_sum_i32(part);
@@ -2432,9 +2460,10 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
             for (int b = 0; b < kdiv; b += blockDim.x) {
                 const int j = b + threadIdx.x;
                 const int4 c = j < kdiv ? cc[j] : make_int4(0, 0, 0, 0);
-                int t1, t2;
-                const int ex_ne = block_excl_scan(ne4(c), tmp, &t1);
-                const int ex_dv = block_excl_scan(dv4(c), tmp, &t2);
+                int tt;
+                const int ex = block_excl_scan(ne4(c) | (dv4(c) << 16), tmp, &tt);
+                const int t1 = tt & 0xffff, t2 = tt >> 16, ex_ne = ex & 0xffff, ex_dv = ex >> 16;
+                if (kdiv <= (int)blockDim.x) ne_total = t1;
                 if (j < kdiv) {
                     const int incl = ne_carry + ex_ne + ne4(c);
                     const int gpos = ne_total - incl;   // sum of ne over items after j
@@ -2512,8 +2541,8 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
             for (int j = w; j < proc; j += nw)
                 if (na[prev[j].node].cnt > 16) (void)qt_wave_split(na[prev[j].node], P, T);
             __syncthreads();
-            int ne_total = 0;
-            {
+            int ne_total = 0;   // (one packed scan; the total pass only for more than one chunk, as phase 1)
+            if (proc > (int)blockDim.x) {   // block-uniform
                 int part = 0;
                 for (int j = threadIdx.x; j < proc; j += blockDim.x) part += ne4(cc[j]);
                 part = wave_sum_i32(part);
@@ -2526,9 +2555,10 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
             for (int b = 0; b < proc; b += blockDim.x) {
                 const int j = b + threadIdx.x;
                 const int4 c = j < proc ? cc[j] : make_int4(0, 0, 0, 0);
-                int t1, t2;
-                const int ex_ne = block_excl_scan(ne4(c), tmp, &t1);
-                const int ex_dv = block_excl_scan(dv4(c), tmp, &t2);
+                int tt;
+                const int ex = block_excl_scan(ne4(c) | (dv4(c) << 16), tmp, &tt);
+                const int t1 = tt & 0xffff, t2 = tt >> 16, ex_ne = ex & 0xffff, ex_dv = ex >> 16;
+                if (proc <= (int)blockDim.x) ne_total = t1;
                 if (j < proc) {
                     const int gpos = ne_total - (ne_carry + ex_ne + ne4(c));
                     qt_emit_children(na[prev[j].node], c, gpos, dv_carry + ex_dv, nb, divs, NC);

@@ -5,7 +5,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[2]
-os.environ["ORBSLAM2_AMD_LIB"] = str(ROOT / "tools" / "diag" / "liborbslam2_amd_stamps.so")
+# QT_STAMPS_LIB: a build with -DQT_STAMP_LEVEL=<l> stamps level l's frame-0 workgroup instead of level 0's
+os.environ["ORBSLAM2_AMD_LIB"] = os.environ.get("QT_STAMPS_LIB", str(ROOT / "tools" / "diag" / "liborbslam2_amd_stamps.so"))
 sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
