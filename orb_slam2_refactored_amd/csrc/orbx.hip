@@ -2109,35 +2109,17 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
 #pragma unroll
         for (int k = 0; k < 4; k++) bad |= cv[k] > 0 && (rl[k] < 0 || rh[k] >= R);
         if (bad) atomicOr(fault, FAULT_QT_ROOT);
-        uint32_t r[4][8];   // every cell's first 8 points, one batch of loads for the counts and the copy
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int q = 0; q < 8; q++) r[k][q] = q < cv[k] ? fslots[cs[k] + q] : 0u;
         int cnt[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (rl[k] == rh[k]) {
 #pragma unroll
                 for (int rt = 0; rt < 4; rt++) cnt[rt] += rl[k] == rt ? cv[k] : 0;
-            } else {   // a boundary cell: its points' roots, loads in batches of 8 (a textured frame's
-                       // boundary cells hold tens of points: one dependent load per point made this
-                       // thread the gather's critical path, round 5)
-                auto count = [&](uint32_t kk) {
-                    const int rt = root_x(kp_x(kk));
+            } else {   // a boundary cell (rare): its points' roots
+                for (int q = 0; q < cv[k]; q++) {
+                    const int rt = root_x(kp_x(fslots[cs[k] + q]));
 #pragma unroll
                     for (int u = 0; u < 4; u++) cnt[u] += rt == u;
-                };
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (q < cv[k]) count(r[k][q]);
-                for (int q0 = 8; q0 < cv[k]; q0 += 8) {
-                    uint32_t r2[8];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) r2[q] = q0 + q < cv[k] ? fslots[cs[k] + q0 + q] : 0u;
-#pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        if (q0 + q < cv[k]) count(r2[q]);
                 }
             }
         }
@@ -2153,6 +2135,11 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
         }
         n_total = base;
         if (n_total <= PTC) { P = lds_P; T = lds_T; }
+        uint32_t r[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[k][q] = q < cv[k] ? fslots[cs[k] + q] : 0u;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (rl[k] == rh[k]) {
@@ -2173,7 +2160,8 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
 #pragma unroll
                 for (int rt = 0; rt < 4; rt++) run[rt] += rl[k] == rt ? cv[k] : 0;
             } else {
-                auto put = [&](uint32_t kk) {
+                for (int q = 0; q < cv[k]; q++) {
+                    const uint32_t kk = fslots[cs[k] + q];
                     const int rt = root_x(kp_x(kk));
                     int o = run[0];
 #pragma unroll
@@ -2181,17 +2169,6 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                     P[o] = kk;
 #pragma unroll
                     for (int u = 0; u < 4; u++) run[u] += rt == u;
-                };
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (q < cv[k]) put(r[k][q]);
-                for (int q0 = 8; q0 < cv[k]; q0 += 8) {
-                    uint32_t r2[8];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) r2[q] = q0 + q < cv[k] ? fslots[cs[k] + q0 + q] : 0u;
-#pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        if (q0 + q < cv[k]) put(r2[q]);
                 }
             }
         }
