@@ -2084,19 +2084,27 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
     int n_total = 0, carry = 0;
     bool parted = false;   // the gather below writes the root-partitioned order itself (round 5)
     if (L.ncells <= 4 * (int)blockDim.x && R <= 4) {
-        // thread t owns cells 4t .. 4t+3 (raster order): their counts and slot offsets are loaded
+        // thread t owns cells cpt t .. cpt t + cpt - 1 (raster order): their counts and slot offsets are loaded
         // together and the points go straight to their root's segment.  A cell whose zone lies inside
         // one root (all but the cells on a root boundary) sends all its points there, a boundary cell
         // splits them by x; one block scan per root (R <= 4) of the threads' counts places the threads'
         // runs, so each segment keeps the gather order: the stable partition of :547-579 without the
         // round trip through T.  Every thread's first 8 points per cell are loaded in one batch.
-        const int i0 = 4 * threadIdx.x;
+        // Cells per thread: as few as the grid allows (a small level's 100-500 cells over 1-2 per
+        // thread instead of 4), so a thread's chain of dependent slot loads is shorter (round 5);
+        // thread order is still cell order.
+#ifndef QT_GATHER_CPT4
+        const int cpt = L.ncells <= (int)blockDim.x ? 1 : L.ncells <= 2 * (int)blockDim.x ? 2 : 4;
+#else
+        const int cpt = 4;
+#endif
+        const int i0 = cpt * threadIdx.x;
         int cv[4], cs[4], rl[4], rh[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int i = i0 + k;
             cv[k] = 0; cs[k] = 0; rl[k] = 0; rh[k] = 0;
-            if (i < L.ncells) {
+            if (k < cpt && i < L.ncells) {
                 const CellDev cd = cells[L.cell_base + i];
                 cv[k] = ccell[i] & CELL_CNT_MASK;
                 cs[k] = cd.slot;
