@@ -2100,25 +2100,6 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
 #endif
         const int i0 = cpt * threadIdx.x;
         int cv[4], cs[4], rl[4], rh[4];
-#ifdef QT_GATHER_VCELLS
-        // the thread's four slots k hold its cells' points as runs of 8 (the last run of a cell takes
-        // the rest): a cell of <= 32 points at one cell per thread is one batch of loads
-        const int vpc = 4 / cpt;   // runs per cell
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int i = i0 + k / vpc, beg = 8 * (k % vpc);
-            cv[k] = 0; cs[k] = 0; rl[k] = 0; rh[k] = 0;
-            if (i < L.ncells) {
-                const CellDev cd = cells[L.cell_base + i];
-                const int c = (ccell[i] & CELL_CNT_MASK) - beg;
-                cv[k] = k % vpc == vpc - 1 ? max(c, 0) : min(max(c, 0), 8);
-                cs[k] = cd.slot + beg;
-                const int zx = (cd.x0y0 & 0xffff) + 3;
-                rl[k] = root_x(zx);
-                rh[k] = root_x(zx + (cd.zwzh & 0xffff) - 1);
-            }
-        }
-#else
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int i = i0 + k;
@@ -2132,7 +2113,6 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                 rh[k] = root_x(zx + (cd.zwzh & 0xffff) - 1);     // and its last
             }
         }
-#endif
         bool bad = false;
 #pragma unroll
         for (int k = 0; k < 4; k++) bad |= cv[k] > 0 && (rl[k] < 0 || rh[k] >= R);
