@@ -1757,7 +1757,13 @@ __device__ int4 qt_group16_split(const QtNode& n, int cnt, const uint32_t* __res
 // then the stable scatter in tiles of 1024 points, point u*256 + tid of a tile in thread tid, its
 // position from the per-(u, child, wave) ballot counts of the tile.  sc: 64 ints of LDS scratch.
 // Every thread must call it; the counts are block-uniform.
-constexpr int QT_BIG = 2048;   // phase-1 nodes above this size are split by the whole block
+// Phase-1 nodes above this size are split by the whole block (round 5: 2048 -> 512, quadtree
+// -3 % on pan frames, +0.7 % textured: a level's first pass has a few root nodes of 500-2000
+// points, and a wavefront per node left the other wavefronts idle)
+#ifndef QT_BIG_DEF
+#define QT_BIG_DEF 512
+#endif
+constexpr int QT_BIG = QT_BIG_DEF;
 __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, uint32_t* __restrict__ T, int* sc) {
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const int xm = n.tlx + (n.brx - n.tlx + 1) / 2;
@@ -2094,7 +2100,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
         // thread instead of 4), so a thread's chain of dependent slot loads is shorter (round 5);
         // thread order is still cell order.
 #ifndef QT_GATHER_CPT4
-        const int cpt = L.ncells <= (int)blockDim.x ? 1 : L.ncells <= 2 * (int)blockDim.x ? 2 : 4;
+        const int cpt = (L.ncells + (int)blockDim.x - 1) / (int)blockDim.x;   // 1..4
 #else
         const int cpt = 4;
 #endif
