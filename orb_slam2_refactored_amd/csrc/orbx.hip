@@ -1906,7 +1906,17 @@ __device__ unsigned long long g_qt_wg[4096 * 2];   // per (frame, level) WG: sta
         if (blockIdx.x == 0 && lev0 + (int)blockIdx.y == QT_STAMP_LEVEL && threadIdx.x == 0 && (k) < 64)\
             g_qt_stamps[(k)] = __builtin_amdgcn_s_memtime();                                       \
     } while (0)
+#ifndef QT_SUB_ITER
+#define QT_SUB_ITER 5   // the phase-1 pass whose sub-phases are stamped (56-59)
+#endif
+#define QT_SUBSTAMP(k)                                                                             \
+    do {                                                                                           \
+        if (iter_no == QT_SUB_ITER + 1) QT_STAMP(k);                                               \
+    } while (0)
 #else
+#define QT_SUBSTAMP(k) \
+    do {               \
+    } while (0)
 #define QT_STAMP(k) \
     do {            \
     } while (0)
@@ -2408,6 +2418,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                 kdiv += tot;
             }
             __syncthreads();
+            QT_SUBSTAMP(56);
             // nodes of <= 16 points: four per wavefront (16-lane groups); larger: one wavefront each
             for (int b = 4 * w; b < kdiv; b += 4 * nw) {   // wave-uniform trip count
                 const int j = b + (lane_id() >> 4);
@@ -2434,6 +2445,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                 }
             }
             __syncthreads();
+            QT_SUBSTAMP(57);
             // group positions: reverse processing order; divisibles: forward order.  The ne and dv counts
             // share one block scan (16-bit halves: a chunk's totals are <= 4 blockDim); with one chunk
             // (kdiv <= blockDim, every small level) the scan's total is the grand total the reverse
@@ -2464,6 +2476,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                 dv_carry += t2;
             }
             const int n_new = ne_total + nnd;
+            QT_SUBSTAMP(55);   // (thread 0: its emit done)
             for (int i = threadIdx.x; i < n; i += blockDim.x)
                 if (na[i].cnt <= 1 && ne_total + ib[i] < NC) nb[ne_total + ib[i]] = na[i];
             // commit: the single points of the non-divisible nodes join the split nodes' points in
@@ -2476,6 +2489,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                 T = t;
             }
             __syncthreads();
+            QT_SUBSTAMP(58);
             if (threadIdx.x == 0) {
                 if (n_new > NC) { s_fail = 1; atomicOr(fault, FAULT_QT_NODES); }
                 s_n = min(n_new, NC);
@@ -2485,6 +2499,7 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
                 else if (n_new + 3 * dv_carry > nfeat) s_state = 1;
             }
             __syncthreads();
+            QT_SUBSTAMP(59);
             QtNode* t = na; na = nb; nb = t;
         } else {
             // Phase 2 round (:632-672): split the previous round's divisible nodes, largest

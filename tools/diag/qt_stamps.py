@@ -49,3 +49,9 @@ for r in range(3):
     a = list(buf)[40 + 4 * r:44 + 4 * r]
     if a[0] and a[3] > a[0]:
         print(f"phase-2 round {r}: sort {a[1] - a[0]} counts+stop {a[2] - a[1]} split+emit {a[3] - a[2]}")
+
+SUB = int(os.environ.get("QT_SUB_ITER", "5"))   # the build's -DQT_SUB_ITER (sub-phase stamps 55-59)
+if v[56] and v[59] > v[3 + 2 * SUB]:
+    b = v[3 + 2 * SUB]
+    print(f"phase-1 pass {SUB} sub-phases: compaction {v[56] - b} split {v[57] - v[56]} "
+          f"emit (thread 0) {v[55] - v[57]} copy+commit {v[58] - v[55]} state {v[59] - v[58]}")
