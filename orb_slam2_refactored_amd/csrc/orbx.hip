@@ -1770,15 +1770,18 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
     const int ym = n.tly + (n.bry - n.tly + 1) / 2;
     auto quad = [&](uint32_t k) { return kp_x(k) < xm ? (kp_y(k) < ym ? 0 : 2) : (kp_y(k) < ym ? 1 : 3); };
     int c[4] = {0, 0, 0, 0};
-    for (int b = 0; b < n.cnt; b += 1024) {
-        uint32_t k[4];
+#ifndef QT_BS_CNT
+#define QT_BS_CNT 4
+#endif
+    for (int b = 0; b < n.cnt; b += 256 * QT_BS_CNT) {   // (the counts: QT_BS_CNT points per thread per round)
+        uint32_t k[QT_BS_CNT];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < QT_BS_CNT; u++) {
             const int j = b + 256 * u + tid;
             k[u] = j < n.cnt ? P[n.beg + j] : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < QT_BS_CNT; u++) {
             const int q = b + 256 * u + tid < n.cnt ? quad(k[u]) : -1;
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) c[qq] += q == qq;
@@ -1798,6 +1801,44 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
     o[2] = o[1] + tot[1];
     o[3] = o[2] + tot[2];
     __syncthreads();
+#ifdef QT_BS_PF
+    // the next tile's points are loaded before this tile's barrier (ranks kept as ints, so the
+    // prefetch costs no registers over the 64-bit ballot masks)
+    uint32_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) k[u] = 256 * u + tid < n.cnt ? P[n.beg + 256 * u + tid] : 0u;
+    for (int b = 0; b < n.cnt; b += 1024) {
+        int q[4], rk[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            q[u] = b + 256 * u + tid < n.cnt ? quad(k[u]) : -1;
+            rk[u] = 0;
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const unsigned long long bm = __ballot(q[u] == qq);
+                if (q[u] == qq) rk[u] = rank64(bm);
+                if (lane == 0) sc[16 * u + 4 * qq + w] = popc64(bm);   // (u, child, wave)
+            }
+        }
+        uint32_t kn[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int j = b + 1024 + 256 * u + tid;
+            kn[u] = j < n.cnt ? P[n.beg + j] : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (q[u] < 0) continue;
+            const int* cq = sc + 4 * q[u];
+            int off = o[q[u]];
+            for (int uu = 0; uu < u; uu++) off += cq[16 * uu] + cq[16 * uu + 1] + cq[16 * uu + 2] + cq[16 * uu + 3];
+            for (int ww = 0; ww < w; ww++) off += cq[16 * u + ww];
+            T[off + rk[u]] = k[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) k[u] = kn[u];
+#else
     for (int b = 0; b < n.cnt; b += 1024) {
         uint32_t k[4];
         int q[4];
@@ -1828,6 +1869,7 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
             for (int ww = 0; ww < w; ww++) off += cq[16 * u + ww];
             T[off + rank64(m[u])] = k[u];
         }
+#endif
 #pragma unroll
         for (int qq = 0; qq < 4; qq++)
 #pragma unroll
