@@ -66,11 +66,12 @@ int orbx_scale_tables(const orbx_extractor* h, float* scale, float* inv_scale, f
  *               [0] ::cos(double) / ::sin(double), the overload visible without `using namespace std`;
  *               1 std::cos(float) / std::sin(float) = glibc cosf / sinf (a `using namespace std`, or a
  *               libstdc++ <math.h> wrapper, before :107).
- *   resize_simd the vector width V (bytes) of the OpenCV build's cv::resize INTER_LINEAR 8U vertical pass
- *               (src/ORBextractor.cc:468; VResizeLinearVec_32s8u rounds via (S >> 4) * b >> 16, its
- *               scalar tail via (S0*b0 + S1*b1 + 2^21) >> 22): [16] SSE2-SSE4 / NEON baseline builds,
- *               32 AVX2 baseline, 64 AVX-512 baseline, 8 (half-width), 1 no SIMD (scalar everywhere),
- *               0 the SIMD rounding on every column.
+ *   resize_simd tail mode V of cv::resize INTER_LINEAR 8U's vertical pass (src/ORBextractor.cc:468).
+ *               VResizeLinearVec_32s8u rounds via ((S >> 4) * b) >> 16, and OpenCV's uchar
+ *               specialisation of VResizeLinear repeats that rounding in its unrolled and scalar tails
+ *               [ext, recalled], so [0] (the vector rounding on every column) is every build's result.
+ *               8 / 16 / 32 / 64: a FixedPtCast tail (S0*b0 + S1*b1 + 2^21) >> 22 after a V-byte vector
+ *               loop; 1: FixedPtCast everywhere.  These are sensitivity switches (parity unpinned).
  * -1 keeps a switch.  Environment defaults at orbx_create: ORBX_TRIG=double|float, ORBX_RESIZE_TAIL=V. */
 int orbx_set_opencv_compat(orbx_extractor* h, int trig_mode, int resize_simd);
 int orbx_get_opencv_compat(const orbx_extractor* h, int* trig_mode, int* resize_simd);

@@ -46,12 +46,13 @@
  *     std::cos(float) / std::sin(float) = glibc cosf / sinf (visible when a `using namespace std` or
  *     a libstdc++ <math.h> wrapper precedes :107).
  *   - cv::resize vertical pass (VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>,
- *     VResizeLinearVec_32s8u>).  The SIMD part rounds ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2;
- *     the scalar tail after it (S0*b0 + S1*b1 + 2^21) >> 22.  resize_simd V = the build's vector
- *     width in bytes: the SIMD loop covers x += V while x <= w - V, then x += V/2 while x < w - V/2;
- *     the scalar formula takes the rest.  V = 16 (default: SSE2-SSE4 / NEON baseline builds), 32
- *     (AVX2 baseline), 64 (AVX-512 baseline), 1 (no SIMD: scalar everywhere), 0 (the SIMD formula on
- *     every column, rounds 1-4's only mode).
+ *     VResizeLinearVec_32s8u>).  The vector op rounds ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2,
+ *     and OpenCV's explicit uchar specialisation of VResizeLinear repeats that formula in its unrolled
+ *     and scalar tail loops [ext, recalled], so the result does not depend on the build's SIMD width:
+ *     resize_simd V = 0 (default) applies it to every column.  The other modes model a tail with
+ *     FixedPtCast rounding (S0*b0 + S1*b1 + 2^21) >> 22 after a V-byte vector loop (x += V while
+ *     x <= w - V, then x += V/2 while x < w - V/2): V = 8 / 16 / 32 / 64, or 1 (FixedPtCast
+ *     everywhere).  They are sensitivity switches, not claimed to match a real build.
  *   - GaussianBlur taps are OpenCV 4.x's error-diffused Q8 [18,34,48,56,48,34,18].
  *   - Compiled -ffp-contract=off: the reference is ISO C++14 (CMakeLists.txt:10-11), under
  *     which GCC does not contract a*b+c.
@@ -126,7 +127,7 @@ struct Img {
 
 // OpenCV-build switches (oracle_set_compat); process-wide, set before any extraction
 static int g_trig_float = 0;    // 0: (float)::cos((double)angle); 1: cosf / sinf
-static int g_resize_simd = 16;  // vector width V of the resize's VResizeLinearVec_32s8u (see header)
+static int g_resize_simd = 0;   // tail mode V of the resize's vertical pass (see header; 0 = SIMD rounding everywhere)
 
 // First column VResizeLinear computes with its scalar loop ([ext] imgproc/src/resize.cpp: the vector
 // op returns x after `for (; x <= w - V; x += V)` and `for (; x < w - V/2; x += V/2)`).

@@ -191,8 +191,9 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
 // ------------------------------------------------------------------------------------------
 // cv::resize INTER_LINEAR CV_8UC1 [ext]: horizontal 11-bit fixed point (exact int32), vertical
 // with the universal-intrinsics rounding ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2 up to the
-// level's tail_x and the scalar loop's (S0*b0 + S1*b1 + 2^21) >> 22 from there (the OpenCV build's
-// SIMD width decides where the vector loop stops: orbx_set_opencv_compat, oracle resize_tail_x).
+// level's tail_x and (S0*b0 + S1*b1 + 2^21) >> 22 from there.  Default tail mode 0: tail_x = w, the
+// vector rounding on every column (OpenCV's uchar VResizeLinear specialisation uses it in its scalar
+// tail too); the other modes are sensitivity switches (orbx_set_opencv_compat, oracle resize_tail_x).
 // xtab[dx] = {sx0 | sx1 << 16, a0 | a1 << 16}; ytab[dy] = {sy0 | sy1 << 16, b0 | b1 << 16}.
 // One workgroup = a 64 x 16 tile of level l (256 threads, 4 output pixels each).  The source
 // rectangle of level l-1 it needs is staged in LDS with dword loads; coefficients come from the
@@ -3219,7 +3220,10 @@ struct orbx_extractor {
     int pyr_pair = 2;   // pyramid_pair_kernel for levels (1,2), (3,4), (5,6) (level 0 16-byte aligned); 1: (2,3), (4,5), (6,7) (ORBX_PYR_PAIR)
     // OpenCV-build switches (orbx_set_opencv_compat; ORBX_TRIG / ORBX_RESIZE_TAIL)
     int trig_float = 0;    // ComputeOrbDescriptor's cos / sin: 0 ::cos(double), 1 cosf / sinf
-    int resize_simd = 16;  // the resize's vector width V: scalar tail after the SIMD loop (0: none, 1: all scalar)
+    // the resize's tail mode V (0, default: the SIMD rounding on every column, as OpenCV's uchar
+    // specialisation of VResizeLinear does in its unrolled and scalar tails too; 8-64: a tail with
+    // FixedPtCast rounding after a V-byte vector loop; 1: FixedPtCast everywhere).  Parity unpinned.
+    int resize_simd = 0;
     std::vector<std::pair<hipStream_t, hipEvent_t>> sub;
     hipEvent_t fork_ev = nullptr;
     // level-split overlap (launch_chunk): level 0's FAST + quadtree on a side stream.  Off by
@@ -3249,10 +3253,12 @@ struct orbx_extractor {
     int last_frames = 0;
 };
 
-// First column VResizeLinear computes with its scalar loop in an OpenCV build whose universal
-// intrinsics are V bytes wide ([ext] imgproc/src/resize.cpp VResizeLinearVec_32s8u: `for (; x <= w -
-// V; x += V)` then `for (; x < w - V/2; x += V/2)`).  V = 0: the SIMD rounding everywhere; V = 1: a
-// build without SIMD, scalar everywhere.
+// First column that takes FixedPtCast<int, uchar, 22> rounding under tail mode V: after a V-byte
+// vector loop ([ext] imgproc/src/resize.cpp VResizeLinearVec_32s8u: `for (; x <= w - V; x += V)` then
+// `for (; x < w - V/2; x += V/2)`).  V = 0 (default): none -- the recalled uchar specialisation of
+// VResizeLinear rounds its unrolled and scalar tails like the vector op, so every column takes the SIMD
+// formula whatever the build's SIMD width.  V = 1: FixedPtCast everywhere.  Modes other than 0 model
+// builds whose tail rounds differently; they are kept as sensitivity switches (parity unpinned).
 static int resize_tail_x(int w, int V) {
     if (V <= 0) return w;
     if (V == 1) return 0;

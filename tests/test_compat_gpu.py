@@ -1,9 +1,11 @@
 """The OpenCV-build switches (orbx_set_opencv_compat): every mode is bit-exact GPU vs oracle.
 
 trig: ComputeOrbDescriptor's cos / sin (src/ORBextractor.cc:107) as ::cos(double) or cosf.
-resize_simd V: where cv::resize's vertical SIMD loop stops and the scalar tail's rounding starts
-(src/ORBextractor.cc:466-468).  The default (double, 16) is covered by every other extractor test;
-here each other mode on the C1 / C2 / C3 shapes and on widths whose tails differ per level."""
+resize_simd V: tail mode of cv::resize's vertical pass (src/ORBextractor.cc:466-468): 0 (default) the
+vector rounding on every column, as OpenCV's uchar VResizeLinear specialisation does in its tails too;
+8-64 / 1 model a FixedPtCast-rounded tail (sensitivity switches).  The default (double, 0) is covered by
+every other extractor test; here each other mode on the C1 / C2 / C3 shapes and on widths whose tails
+differ per level."""
 import numpy as np
 import pytest
 
@@ -12,7 +14,7 @@ from orb_slam2_refactored_amd.synth import textured_image
 
 pytestmark = pytest.mark.gpu
 FIELDS = ("x", "y", "size", "angle", "response", "octave", "class_id")
-MODES = [("double", 0), ("double", 1), ("double", 8), ("double", 32), ("double", 64), ("float", 16), ("float", 0)]
+MODES = [("double", 16), ("double", 1), ("double", 8), ("double", 32), ("double", 64), ("float", 16), ("float", 0)]
 
 
 def same(kps, okps, desc, odesc, what):
@@ -60,11 +62,11 @@ def test_mode_switch_and_env_defaults(oracle, monkeypatch):
     defaults a new handle starts with."""
     img = synth_image(7, 1280, 720)
     ex = ORBextractor(ORBextractor.Parameters(2000))
-    assert ex.get_opencv_compat() == ("double", 16)
+    assert ex.get_opencv_compat() == ("double", 0)
     a = ex.Extract(img)
     ex.set_opencv_compat(resize_simd=1)
     b = ex.Extract(img)
-    ex.set_opencv_compat(resize_simd=16)
+    ex.set_opencv_compat(resize_simd=0)
     c = ex.Extract(img)
     assert not np.array_equal(a[1][:100], b[1][:100]) or len(a[0]) != len(b[0])
     same(a[0], c[0], a[1], c[1], "back to the default")

@@ -106,9 +106,9 @@ def test_trig_modes_identical_on_golden_frames(oracle):
     p = oracle.params(1000)
     for seed in range(4):
         img = synth_image(seed, 640, 480)
-        with oracle.compat("double", 16):
+        with oracle.compat("double", 0):
             k0, d0, _ = oracle.extract(p, img)
-        with oracle.compat("float", 16):
+        with oracle.compat("float", 0):
             k1, d1, _ = oracle.extract(p, img)
         assert np.array_equal(k0, k1) and np.array_equal(d0, d1)
 
@@ -117,4 +117,4 @@ def test_compat_restores(oracle):
     prev = oracle.set_compat()
     with oracle.compat("float", 1):
         assert oracle.set_compat() == ("float", 1)
-    assert oracle.set_compat() == prev == ("double", 16)
+    assert oracle.set_compat() == prev == ("double", 0)
