@@ -1,6 +1,6 @@
 """pyramid_pair_mfma_kernel (ORBX_PYR_MFMA=1: the horizontal pass of cv::resize on v_mfma_f32_16x16x32_f16,
 the vertical taps in source-row space through DPP; DESIGN §4 "Pyramid, round 5") against the oracle's
-ComputePyramid (src/ORBextractor.cc:1080-1090), at the bench / config shapes, odd widths and heights,
+ComputePyramid (src/ORBextractor.cc:455-470), at the bench / config shapes, odd widths and heights,
 both OpenCV resize-tail modes and the batched device path.  Off by default (slower than the VALU pair
 kernel); these tests keep the kept code exact."""
 import numpy as np
