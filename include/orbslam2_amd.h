@@ -106,7 +106,8 @@ int orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int n_fr
 
 /* Device-side capacity checks of the batched path.  Every kernel of an extraction ORs a fault bit
  * into the handle's fault word when a capacity bound is violated (1 quadtree node array, 2 keypoint
- * outside the root nodes = the reference's CV_Assert :569, 4 FAST cell slot, 8 per-level output);
+ * outside the root nodes = the reference's CV_Assert :569, 4 FAST cell slot, 8 per-level output,
+ * 16 a kernel launched with a block size it is not written for: it exits before touching memory);
  * the batch is then truncated, never written out of bounds.  The word is sticky across batches
  * until read.  orbx_batch_status waits for `stream`, returns the mask in *fault_mask, clears it and
  * returns ORB_EINTERNAL when it was non-zero (the single-frame orbx_extract checks it itself).

@@ -38,6 +38,7 @@ enum DeviceFault : uint32_t {
     FAULT_QT_ROOT = 1u << 1,      // keypoint mapped outside the root nodes (CV_Assert :569)
     FAULT_CELL_CAP = 1u << 2,     // FAST cell slot overflow (cannot happen: strict NMS bound)
     FAULT_OUT_CAP = 1u << 3,      // per-level output capacity exceeded
+    FAULT_BLOCK_SIZE = 1u << 4,   // a kernel launched with a block size other than the one it is written for
 };
 
 // Grow-only device buffer.

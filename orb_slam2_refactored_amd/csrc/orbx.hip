@@ -169,7 +169,7 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
-// Block-wide exclusive scan for blockDim.x == 256 (4 waves). `tmp` >= 8 ints of LDS.
+// Block-wide exclusive scan for any blockDim.x that is a multiple of 64 (<= 8 waves). `tmp` >= 8 ints of LDS.
 __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
     const int w = threadIdx.x >> 6, l = lane_id();
     const int inc = wave_incl_scan(v);
@@ -909,7 +909,8 @@ __global__ __launch_bounds__(256) void pyramid_pair_mfma_kernel(Geom g, int l, c
 }
 
 // FAST's first-cell hint for the next launch: bit 31 of every strip descriptor = the CELL_CNT_INI bit of
-// its first cell in frame 0 (cell_cnt's frame-0 slots).  One thread per strip, after fast_cells.
+// its first cell in frame 0 (cell_cnt's frame-0 slots).  One thread per strip, once per batch after every
+// stage of it (launch_fast_hint).
 __global__ void fast_hint_kernel(int2* __restrict__ strips, const int* __restrict__ cell_cnt, int nstrips) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nstrips) return;
@@ -1754,10 +1755,19 @@ __device__ int4 qt_group16_split(const QtNode& n, int cnt, const uint32_t* __res
     return make_int4(c0, c1, c2, c3);
 }
 
-// All threads of the (256-thread) block split one large node: child counts by a block reduction,
-// then the stable scatter in tiles of 1024 points, point u*256 + tid of a tile in thread tid, its
-// position from the per-(u, child, wave) ballot counts of the tile.  sc: 64 ints of LDS scratch.
-// Every thread must call it; the counts are block-uniform.
+// quadtree_kernel's block size.  qt_block_split is written for exactly QT_THREADS threads (QT_WAVES
+// wavefronts): its child counts are summed from QT_WAVES per-wave partials and its scatter tiles are
+// 4 x QT_THREADS points with (u, child, wave) ballot counts.  Round 5's 64-thread experiment
+// (ORBX_QT_SMALL=64) broke exactly this: with one wavefront the totals read three stale wave slots,
+// the child offsets went wild and T was written out of bounds (the illegal access in
+// test_fast_candidates_dense_cells[noise], whose dense root nodes take this split).  The kernel now
+// checks its block size on entry and sets FAULT_BLOCK_SIZE instead of running (quadtree_kernel).
+constexpr int QT_THREADS = 256, QT_WAVES = QT_THREADS / 64;
+static_assert(QT_WAVES == 4, "qt_block_split's scratch layout (sc[16 u + 4 child + wave]) holds 4 wavefronts");
+// All threads of the QT_THREADS block split one large node: child counts by a block reduction,
+// then the stable scatter in tiles of 4 QT_THREADS points, point u*QT_THREADS + tid of a tile in
+// thread tid, its position from the per-(u, child, wave) ballot counts of the tile.  sc: 64 ints of
+// LDS scratch.  Every thread must call it; the counts are block-uniform.
 // Phase-1 nodes above this size are split by the whole block (round 5: 2048 -> 512, quadtree
 // -3 % on pan frames, +0.7 % textured: a level's first pass has a few root nodes of 500-2000
 // points, and a wavefront per node left the other wavefronts idle)
@@ -1774,16 +1784,16 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
 #ifndef QT_BS_CNT
 #define QT_BS_CNT 4
 #endif
-    for (int b = 0; b < n.cnt; b += 256 * QT_BS_CNT) {   // (the counts: QT_BS_CNT points per thread per round)
+    for (int b = 0; b < n.cnt; b += QT_THREADS * QT_BS_CNT) {   // (the counts: QT_BS_CNT points per thread per round)
         uint32_t k[QT_BS_CNT];
 #pragma unroll
         for (int u = 0; u < QT_BS_CNT; u++) {
-            const int j = b + 256 * u + tid;
+            const int j = b + QT_THREADS * u + tid;
             k[u] = j < n.cnt ? P[n.beg + j] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < QT_BS_CNT; u++) {
-            const int q = b + 256 * u + tid < n.cnt ? quad(k[u]) : -1;
+            const int q = b + QT_THREADS * u + tid < n.cnt ? quad(k[u]) : -1;
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) c[qq] += q == qq;
         }
@@ -1796,7 +1806,7 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
     __syncthreads();
     int tot[4], o[4];
 #pragma unroll
-    for (int qq = 0; qq < 4; qq++) tot[qq] = sc[qq] + sc[4 + qq] + sc[8 + qq] + sc[12 + qq];
+    for (int qq = 0; qq < 4; qq++) tot[qq] = sc[qq] + sc[4 + qq] + sc[8 + qq] + sc[12 + qq];   // QT_WAVES = 4 partials
     o[0] = n.beg;
     o[1] = o[0] + tot[0];
     o[2] = o[1] + tot[1];
@@ -1807,12 +1817,12 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
     // prefetch costs no registers over the 64-bit ballot masks)
     uint32_t k[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) k[u] = 256 * u + tid < n.cnt ? P[n.beg + 256 * u + tid] : 0u;
-    for (int b = 0; b < n.cnt; b += 1024) {
+    for (int u = 0; u < 4; u++) k[u] = QT_THREADS * u + tid < n.cnt ? P[n.beg + QT_THREADS * u + tid] : 0u;
+    for (int b = 0; b < n.cnt; b += 4 * QT_THREADS) {
         int q[4], rk[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            q[u] = b + 256 * u + tid < n.cnt ? quad(k[u]) : -1;
+            q[u] = b + QT_THREADS * u + tid < n.cnt ? quad(k[u]) : -1;
             rk[u] = 0;
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
@@ -1824,7 +1834,7 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
         uint32_t kn[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int j = b + 1024 + 256 * u + tid;
+            const int j = b + 4 * QT_THREADS + QT_THREADS * u + tid;
             kn[u] = j < n.cnt ? P[n.beg + j] : 0u;
         }
         __syncthreads();
@@ -1840,18 +1850,18 @@ __device__ int4 qt_block_split(const QtNode& n, const uint32_t* __restrict__ P, 
 #pragma unroll
         for (int u = 0; u < 4; u++) k[u] = kn[u];
 #else
-    for (int b = 0; b < n.cnt; b += 1024) {
+    for (int b = 0; b < n.cnt; b += 4 * QT_THREADS) {
         uint32_t k[4];
         int q[4];
         unsigned long long m[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int j = b + 256 * u + tid;
+            const int j = b + QT_THREADS * u + tid;
             k[u] = j < n.cnt ? P[n.beg + j] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            q[u] = b + 256 * u + tid < n.cnt ? quad(k[u]) : -1;
+            q[u] = b + QT_THREADS * u + tid < n.cnt ? quad(k[u]) : -1;
             m[u] = 0;
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
@@ -2088,7 +2098,7 @@ __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, i
 #ifndef QT_WAVES_DEF
 #define QT_WAVES_DEF 4   // wavefronts per SIMD = workgroups per CU (4 wavefronts each)
 #endif
-__global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
+__global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
                                                        const uint32_t* __restrict__ slots, const CellDev* cells,
                                                        uint32_t* __restrict__ Pbuf, uint32_t* __restrict__ Tbuf,
                                                        uint32_t* __restrict__ sel, int* __restrict__ sel_cnt, int NC,
@@ -2111,9 +2121,16 @@ __global__ __launch_bounds__(256, QT_WAVES_DEF) void quadtree_kernel(Geom g, con
     __shared__ int rc[MAX_ROOTS];
 
     const int f = blockIdx.x, l = lev0 + (int)blockIdx.y;   // levels lev0 .. lev0 + gridDim.y - 1
+    int* scnt = sel_cnt + f * g.nlevels + l;
+    if (blockDim.x != QT_THREADS) {   // block-uniform: a launch this kernel is not written for fails loudly
+        if (threadIdx.x == 0) {
+            atomicOr(fault, FAULT_BLOCK_SIZE);
+            *scnt = 0;   // describe then sees an empty level, never stale selections
+        }
+        return;
+    }
     const LevelDev& L = g.lv[l];
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    int* scnt = sel_cnt + f * g.nlevels + l;
     if (L.rw <= 0 || L.rh <= 0 || L.ncells == 0) {
         if (threadIdx.x == 0) *scnt = 0;
         return;
@@ -3031,7 +3048,7 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     b = __sinf(ang);
 #else
     if (TRIG) sincosf_glibc(ang, &b, &a);
-    else sincos_f2d_fdlibm(ang, &b, &a);
+    else sincos_f2d(ang, &b, &a);
 #endif
     DESC_STAMP(4);
     auto sample = [&](float x, float y) -> int {
@@ -3213,6 +3230,7 @@ struct orbx_extractor {
     int fast_spec_first = 1;
     int nsub = 1;       // sub-batches on side streams (launch_batch; ORBX_NSUB)
     int debug_nc = 0;
+    int debug_qt_block = 0;   // test hook (ORBX_DEBUG_QT_BLOCK): launch quadtree_kernel with this block size (FAULT_BLOCK_SIZE)
     uint32_t fault_host = 0;   // test hook (ORBX_DEBUG_NC): shrink the quadtree node capacity to induce FAULT_QT_NODES
     int pyr_mfma = 0;   // ORBX_PYR_MFMA=1: pyramid_pair_mfma_kernel where the level pair's tables fit (measured slower: DESIGN §4)
     std::vector<char> pyr_mfma_ok;   // per level l: the pair (l, l+1) fits pyramid_pair_mfma_kernel
@@ -3643,19 +3661,17 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
                            h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns,
                            h->fast_spec > 0 && h->fast_spec_first ? h->fast_spec | (1 << 29) : h->fast_spec);
-        if (h->fast_spec > 0 && h->fast_spec_first)   // the hint bits for the next launch (this one has read them)
-            hipLaunchKernelGGL(fast_hint_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s,
-                               h->d_strips.as<int2>() + sb, h->d_cellcnt.as<int>(), ns);
     };
+    const unsigned qt_block = h->debug_qt_block ? (unsigned)h->debug_qt_block : (unsigned)QT_THREADS;
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
         if (h->qt_ptc0 > 0 && l0 == 0) {   // tuning knob: level 0 alone, with its own LDS point capacity
-            launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, 1u), dim3(256), (uint32_t)h->qt_lds0, s, g, cellcnt,
+            launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, 1u), dim3(qt_block), (uint32_t)h->qt_lds0, s, g, cellcnt,
                          slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->qt_ptc0, fault, 0);
             l0 = 1;
             if (--nl <= 0) return;
         }
-        launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(256), (uint32_t)h->qt_lds, s, g,
+        launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(qt_block), (uint32_t)h->qt_lds, s, g,
                            cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0);
     };
     // levels l and l+1 in one pyramid_pair_kernel launch where the shapes fit its LDS rectangles
@@ -3708,6 +3724,19 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
                  dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
 }
 
+// The first-cell hint bits for the next launch (fast_hint_kernel): once per batch, on st after every
+// sub-batch and side stream has joined, so no fast_cells launch of this batch is still reading the strip
+// descriptors it rewrites, and frame 0's cell counts (the first chunk's) are final.
+static int launch_fast_hint(orbx_extractor* h, hipStream_t st) {
+    if (!(h->fast_spec > 0 && h->fast_spec_first)) return ORB_OK;
+    const int ns = h->strip_beg[h->geom.nlevels];
+    if (ns <= 0) return ORB_OK;
+    hipLaunchKernelGGL(fast_hint_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, h->d_strips.as<int2>(),
+                       h->d_cellcnt.as<int>(), ns);
+    ORB_HIP_TRY(hipGetLastError());
+    return ORB_OK;
+}
+
 // Frames are split into sub-batches on the handle's side streams (fork/join with events on st) so
 // that one sub-batch's latency-bound stages (the short pyramid levels, the quadtree's level-0 tail)
 // overlap another's FAST / describe work.
@@ -3727,7 +3756,7 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
         }
         launch_chunk(h, 0, d_imgs, F, fstride, step, d_kps, d_desc, d_counts, cap, st, side);
         ORB_HIP_TRY(hipGetLastError());
-        return ORB_OK;
+        return launch_fast_hint(h, st);
     }
     while ((int)h->sub.size() < nsub) {
         hipStream_t s2;
@@ -3748,7 +3777,7 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
         f0 += Fi;
     }
     ORB_HIP_TRY(hipGetLastError());
-    return ORB_OK;
+    return launch_fast_hint(h, st);
 }
 
 static int check_fault(orbx_extractor* h) {
@@ -3801,6 +3830,10 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_PYR_MFMA")) h->pyr_mfma = atoi(e) != 0;
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     if (const char* e = getenv("ORBX_DEBUG_NC")) h->debug_nc = atoi(e);
+    if (const char* e = getenv("ORBX_DEBUG_QT_BLOCK")) {
+        const int b = atoi(e);
+        if (b >= 64 && b <= QT_THREADS && b % 64 == 0) h->debug_qt_block = b;
+    }
     // OpenCV-build switches (orbx_set_opencv_compat): ORBX_TRIG=double|float, ORBX_RESIZE_TAIL=V
     if (const char* e = getenv("ORBX_TRIG")) h->trig_float = (e[0] == 'f' || e[0] == '1') ? 1 : 0;
     if (const char* e = getenv("ORBX_RESIZE_TAIL")) {

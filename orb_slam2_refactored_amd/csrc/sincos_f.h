@@ -20,43 +20,8 @@
 
 namespace orbamd {
 
-// Round 5: the same function by a table reduction, about half the double operations of the fdlibm form
-// below (which it replaces in describe_kernel; the fdlibm form stays as the reference of the checks).
-// theta = k C + d with k = rint(theta / C), C = 2 pi / 256 in two parts (k C_HI exact), |d| <= pi / 256;
-// sin theta = S_k cos d + C_k sin d, cos theta = C_k cos d - S_k sin d with S_k, C_k = sin / cos (k C)
-// from a 257-entry table of doubles (tools/gen_sincos_tab.cpp, x87 long double rounded to double) and
-// sin d = d + d^3 (-1/6 + d^2 / 120), cos d = 1 + d^2 (-1/2 + d^2 (1/24 - d^2 / 720)) (truncation
-// < 1e-17).  Its float results equal glibc's (float)sin / cos((double)x) on EVERY float in [0, 6.2832]
-// (tests/native/sincos_check.cpp, mode t: 1,086,918,649 values, 0 mismatches) -- the domain is finite, so
-// that is the proof; a sine or cosine polynomial one term shorter gives 3 mismatches.  In describe the
-// table index is wave-uniform: the two table entries come by scalar loads.
-struct SincosTabEntry {
-    double s, c;
-};
-static constexpr SincosTabEntry kSincosTab[ORB_SINCOS_TAB_N + 1] = {ORB_SINCOS_TAB_VALUES};
-
-// UNIFORM (device): the caller guarantees xf is the same on every lane of the wavefront (describe: one
-// keypoint per wavefront), so the table index is read from lane 0 and the entry comes by scalar loads.
-template <bool UNIFORM>
-ORB_HD void sincos_f2d_t(float xf, float* s_out, float* c_out) {
-    const double x = (double)xf;
-    const double kd = __builtin_rint(x * (ORB_SINCOS_TAB_N / 6.283185307179586476925286766559));
-    int k = (int)kd;
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (UNIFORM) k = __builtin_amdgcn_readfirstlane(k);
-#endif
-    const double d = (x - kd * ORB_SINCOS_C_HI) - kd * ORB_SINCOS_C_LO;
-    const double z = d * d;
-    const double sd = d + d * z * (-1.0 / 6 + z * (1.0 / 120));
-    const double cd = 1.0 + z * (-0.5 + z * (1.0 / 24 + z * (-1.0 / 720)));
-    const SincosTabEntry t = kSincosTab[k];
-    *s_out = (float)(t.s * cd + t.c * sd);
-    *c_out = (float)(t.c * cd - t.s * sd);
-}
-ORB_HD void sincos_f2d(float xf, float* s_out, float* c_out) { sincos_f2d_t<false>(xf, s_out, c_out); }
-
-// The fdlibm form (rounds 1-4): kept as the second restatement the checks compare with.
-ORB_HD void sincos_f2d_fdlibm(float xf, float* s_out, float* c_out) {
+// sincos_f2d: the fdlibm form, the one describe_kernel evaluates (rounds 1-6).
+ORB_HD void sincos_f2d(float xf, float* s_out, float* c_out) {
 #ifdef SINCOS_FMA_DIAG   // diagnostic A/B only (round 4's fused sincos; DESIGN §4 describe round 4)
 #pragma clang fp contract(fast)
 #endif
@@ -109,6 +74,45 @@ ORB_HD void sincos_f2d_fdlibm(float xf, float* s_out, float* c_out) {
     *s_out = (float)s;
     *c_out = (float)c;
 }
+
+// sincos_f2d_tab (round 5): the same function by a table reduction, about half the double operations of
+// the fdlibm form above.  Measured slower in describe (its table entry arrives by a scalar load on the
+// wave's one dependent chain; DESIGN §4 describe round 5), so describe keeps sincos_f2d; this form is
+// kept, tested, for callers without that chain.  Domain: [0, 2 pi] (the angle ComputeOrbDescriptor
+// takes); the table index is clamped to the table, so any other input reads inside it (inexactly).
+// theta = k C + d with k = rint(theta / C), C = 2 pi / 256 in two parts (k C_HI exact), |d| <= pi / 256;
+// sin theta = S_k cos d + C_k sin d, cos theta = C_k cos d - S_k sin d with S_k, C_k = sin / cos (k C)
+// from a 257-entry table of doubles (tools/gen_sincos_tab.cpp, x87 long double rounded to double) and
+// sin d = d + d^3 (-1/6 + d^2 / 120), cos d = 1 + d^2 (-1/2 + d^2 (1/24 - d^2 / 720)) (truncation
+// < 1e-17).  Its float results equal glibc's (float)sin / cos((double)x) on EVERY float in [0, 6.2832]
+// (tests/native/sincos_check.cpp, mode t: 1,086,918,649 values, 0 mismatches) -- the domain is finite, so
+// that is the proof; a sine or cosine polynomial one term shorter gives 3 mismatches.  In describe the
+// table index is wave-uniform: the two table entries come by scalar loads.
+struct SincosTabEntry {
+    double s, c;
+};
+static constexpr SincosTabEntry kSincosTab[ORB_SINCOS_TAB_N + 1] = {ORB_SINCOS_TAB_VALUES};
+
+// UNIFORM (device): the caller guarantees xf is the same on every lane of the wavefront (describe: one
+// keypoint per wavefront), so the table index is read from lane 0 and the entry comes by scalar loads.
+template <bool UNIFORM>
+ORB_HD void sincos_f2d_tab_t(float xf, float* s_out, float* c_out) {
+    const double x = (double)xf;
+    const double kd = __builtin_rint(x * (ORB_SINCOS_TAB_N / 6.283185307179586476925286766559));
+    int k = (int)kd;
+    k = k < 0 ? 0 : (k > ORB_SINCOS_TAB_N ? ORB_SINCOS_TAB_N : k);   // [0, 2 pi] maps to 0..N; outside: clamped
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (UNIFORM) k = __builtin_amdgcn_readfirstlane(k);
+#endif
+    const double d = (x - kd * ORB_SINCOS_C_HI) - kd * ORB_SINCOS_C_LO;
+    const double z = d * d;
+    const double sd = d + d * z * (-1.0 / 6 + z * (1.0 / 120));
+    const double cd = 1.0 + z * (-0.5 + z * (1.0 / 24 + z * (-1.0 / 720)));
+    const SincosTabEntry t = kSincosTab[k];
+    *s_out = (float)(t.s * cd + t.c * sd);
+    *c_out = (float)(t.c * cd - t.s * sd);
+}
+ORB_HD void sincos_f2d_tab(float xf, float* s_out, float* c_out) { sincos_f2d_tab_t<false>(xf, s_out, c_out); }
 
 // sinf / cosf of glibc >= 2.28 (the generic sysdeps/ieee754/flt-32 s_sinf.c / s_cosf.c, from ARM's
 // optimized-routines, and their FMA ifunc variants): what `cos(angle)` / `sin(angle)` compute when the

@@ -71,7 +71,8 @@ class ORBextractor:
         """The OpenCV-build switches (include/orbslam2_amd.h orbx_set_opencv_compat): trig "double"
         (::cos(double), default) or "float" (cosf / sinf) for ComputeOrbDescriptor's cos / sin
         (src/ORBextractor.cc:107); resize_simd = the build's SIMD width V in bytes for cv::resize's
-        scalar tail (16 default; 0 = SIMD rounding everywhere, 1 = scalar everywhere).  None keeps."""
+        scalar tail (0 default = SIMD rounding everywhere, as OpenCV's uchar VResizeLinear; 8-64 = a
+        FixedPtCast tail after a V-byte loop, 1 = FixedPtCast everywhere: sensitivity switches).  None keeps."""
         t = -1 if trig is None else self.TRIG_MODES[trig] if isinstance(trig, str) else int(trig)
         v = -1 if resize_simd is None else int(resize_simd)
         check(lib().orbx_set_opencv_compat(self._h, t, v), "orbx_set_opencv_compat")

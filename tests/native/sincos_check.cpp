@@ -1,8 +1,8 @@
 // Compares orbamd::sincos_f2d against glibc (float)sin / (float)cos of (double)x (mode d, default) or
 // orbamd::sincosf_glibc against glibc sinf / cosf (mode f) for every float x in [lo, hi) (default
 // [0, 6.2832]), split over threads.  Build: g++ -O2 -ffp-contract=off -pthread.
-// Usage: sincos_check [threads] [step] [d|f|l]   (d: the table form sincos_f2d, l: the fdlibm form
-// sincos_f2d_fdlibm, both against (float)sin / cos((double)x); f: sincosf_glibc against sinf / cosf)
+// Usage: sincos_check [threads] [step] [d|f|t]   (d: the fdlibm form sincos_f2d that describe uses, t: the
+// table form sincos_f2d_tab, both against (float)sin / cos((double)x); f: sincosf_glibc against sinf / cosf)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -18,7 +18,7 @@ int main(int argc, char** argv) {
     int nt = argc > 1 ? atoi(argv[1]) : 8;
     unsigned step = argc > 2 ? (unsigned)atoi(argv[2]) : 1;   // test every step-th float
     const bool fmode = argc > 3 && argv[3][0] == 'f';
-    const bool lmode = argc > 3 && argv[3][0] == 'l';
+    const bool tmode = argc > 3 && argv[3][0] == 't';
     unsigned a, b;
     memcpy(&a, &lo, 4);
     memcpy(&b, &hi, 4);
@@ -37,7 +37,7 @@ int main(int argc, char** argv) {
                     rs = ::sinf(x);
                     rc = ::cosf(x);
                 } else {
-                    if (lmode) orbamd::sincos_f2d_fdlibm(x, &s, &c);
+                    if (tmode) orbamd::sincos_f2d_tab(x, &s, &c);
                     else orbamd::sincos_f2d(x, &s, &c);
                     rs = (float)::sin((double)x);
                     rc = (float)::cos((double)x);

@@ -344,6 +344,30 @@ def test_batch_status_clean_and_induced_fault():
     assert (cnt.cpu().numpy() <= ex.max_keypoints(720, 1280)).all()
 
 
+def test_quadtree_block_size_guard():
+    """quadtree_kernel is written for 256-thread blocks (qt_block_split sums 4 per-wave partials and
+    scatters 4 x 256-point tiles); round 5's 64-thread experiment wrote out of bounds on dense levels.
+    A launch with another block size (ORBX_DEBUG_QT_BLOCK test hook) must set FAULT_BLOCK_SIZE (16),
+    write empty levels and touch nothing else -- on the pure-noise frames that faulted."""
+    import os
+    import torch
+    from orb_slam2_refactored_amd._lib import OrbError
+    rng = np.random.default_rng(40)
+    frames = torch.from_numpy(rng.integers(0, 256, (2, 480, 640)).astype(np.uint8)).cuda()
+    os.environ["ORBX_DEBUG_QT_BLOCK"] = "64"
+    try:
+        bad = ORBextractor(ORBextractor.Parameters(1000))
+    finally:
+        del os.environ["ORBX_DEBUG_QT_BLOCK"]
+    _, _, cnt = bad.extract_batch_device(frames)
+    with pytest.raises(OrbError, match="fault mask 16"):
+        bad.batch_status()
+    assert (cnt.cpu().numpy() == 0).all()
+    ok = ORBextractor(ORBextractor.Parameters(1000))
+    _, _, cnt = ok.extract_batch_device(frames)
+    assert ok.batch_status() == 0 and (cnt.cpu().numpy() > 0).all()
+
+
 def test_batch_device_rejects_bad_output_buffers():
     import torch
     frames = torch.from_numpy(np.stack([synth_image(1, 640, 480)] * 2)).cuda()

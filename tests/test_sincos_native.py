@@ -1,5 +1,5 @@
 """describe_kernel's double sincos of the float angle (orb_slam2_refactored_amd/csrc/sincos_f.h; mode d the
-round-5 table form sincos_f2d, mode l the fdlibm form of rounds 1-4)
+fdlibm form sincos_f2d that describe uses, mode t the round-5 table form sincos_f2d_tab)
 against glibc's (float)::sin / ::cos((double)x), the functions ComputeOrbDescriptor calls
 (ORBextractor.cc:105-107).  The header is plain IEEE double arithmetic built with
 -ffp-contract=off, as in the library, so host and device compute the same bits.  Here every 97th
@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parents[1]
 import pytest
 
 
-@pytest.mark.parametrize("mode", ["d", "l", "f"])
+@pytest.mark.parametrize("mode", ["d", "t", "f"])
 def test_sincos_matches_glibc(tmp_path, mode):
     exe = tmp_path / "sincos_check"
     subprocess.run(["g++", "-O2", "-ffp-contract=off", "-pthread", str(ROOT / "tests" / "native" / "sincos_check.cpp"),
