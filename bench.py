@@ -138,6 +138,72 @@ def measured_traffic_step(frames, W, H, nfeat, nlevels=8, profile=None):
     return tot
 
 
+# Issue roofline (VERDICT r05 "Next round" 5): the extractor kernels are bound by instruction issue, not
+# HBM, so each stage's committed PMC instruction counts (profiles/rNN_pmc_inst_summary_{pan,textured}.txt,
+# tools/gpu_pmc_round.sh: SQ_INSTS_VALU / SQ_INSTS_SALU per dispatch at 1024 frames, scaled to this
+# launch's frames) are priced against the chip's issue slots over the stage's live time:
+#   VALU: 1024 SIMDs x CLK_GHZ; a wave64 vector instruction holds its SIMD 4 cycles for the packed u16,
+#         permute, compare and 64-bit forms the extractor is built from (tools/probe/issue_probe3; it is also
+#         the rate rocprof's VALUBusy assumes) and 2 cycles for plain 32-bit ALU forms (SIMD-32 dual pass,
+#         MI355X_MICROARCH constants table), so valu_frac_4cyc is the upper and valu_frac_2cyc the lower
+#         bound of the VALU pipe's occupancy;
+#   SALU: one scalar instruction per cycle per CU (256 CUs x CLK_GHZ; the rate SALUBusy assumes).
+CLK_GHZ = 2.4
+ISSUE_MODEL = ("VALU: 4 cycles (upper) / 2 cycles (lower) per wave64 instruction per SIMD, 1024 SIMDs; SALU: 1 "
+               "instruction per cycle per CU, 256 CUs; clock 2.4 GHz; instruction counts from the committed PMC "
+               "pass at 1024 frames scaled to the launch")
+
+
+def pmc_inst_profile(kind):
+    """The newest committed PMC instruction summary of the pan or textured C2 workload: (file, {kernel:
+    {counter: per-dispatch value}}), or (None, None)."""
+    for f in sorted(ROOT.glob(f"profiles/*_pmc_inst_summary_{kind}.txt"), reverse=True):
+        d, cur = {}, None
+        for line in f.read_text().splitlines():
+            if not line.strip():
+                continue
+            if not line.startswith(" "):
+                cur = line.strip()
+                d[cur] = {}
+            elif cur is not None:
+                parts = line.split()
+                try:
+                    d[cur][parts[0]] = float(parts[-1])
+                except ValueError:
+                    pass
+        return f.name, d
+    return None, None
+
+
+def issue_roofline(kind, stage_ms, frames, nlevels=8, pmc_frames=1024):
+    """Per-stage VALU / SALU issue fractions (see ISSUE_MODEL) from `stage_ms` (ms per step of each stage)."""
+    src, d = pmc_inst_profile(kind)
+    if d is None:
+        return None
+    out = {}
+    for stage, ks in stage_kernels(nlevels).items():
+        t = (stage_ms.get(stage) or 0.0) * 1e-3
+        valu = salu = 0.0
+        ok = t > 0
+        for kernel, launches in ks:
+            c = d.get(kernel)
+            if launches and (not c or "SQ_INSTS_VALU" not in c or "SQ_INSTS_SALU" not in c):
+                ok = False
+                break
+            if launches:
+                valu += c["SQ_INSTS_VALU"] * launches
+                salu += c["SQ_INSTS_SALU"] * launches
+        if not ok:
+            continue
+        valu *= frames / pmc_frames
+        salu *= frames / pmc_frames
+        simd_slots = 1024 * CLK_GHZ * 1e9 * t
+        out[stage] = {"ms_per_step": 1e3 * t, "valu_insts": valu, "salu_insts": salu,
+                      "valu_frac_4cyc": 4 * valu / simd_slots, "valu_frac_2cyc": 2 * valu / simd_slots,
+                      "salu_frac": salu / (256 * CLK_GHZ * 1e9 * t)}
+    return {"source": f"profiles/{src}", "workload": kind, "model": ISSUE_MODEL, "stages": out}
+
+
 def cpu_info():
     model = None
     try:
@@ -215,7 +281,7 @@ def event_ms(fn, steps, stream):
     return e0.elapsed_time(e1) / steps
 
 
-def extract_match_gpu_leg(dev, local, frames_np, nfeat, steps=10, reps=None):
+def extract_match_gpu_leg(dev, local, frames_np, nfeat, steps=10, reps=None, issue_kind=None):
     """Batched extract + match-vs-predecessor on `frames_np` tiled to `reps` frames; returns the rate,
     per-stage times and the fast_cells roofline."""
     import torch
@@ -257,7 +323,8 @@ def extract_match_gpu_leg(dev, local, frames_np, nfeat, steps=10, reps=None):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (fb / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS) if fms else 0.0,
                          "algorithmic_bytes_per_launch": fb, "avg_launch_ms": fms,
-                         "pipeline_algorithmic_GBs": bytes_frame * F / (sum(stg.values()) * 1e-3) / 1e9}}
+                         "pipeline_algorithmic_GBs": bytes_frame * F / (sum(stg.values()) * 1e-3) / 1e9,
+                         "issue": issue_roofline(issue_kind, stg, F) if issue_kind else None}}
 
 
 # ------------------------------------------------------------------------------------------ legs
@@ -310,7 +377,7 @@ def c2_textured_leg(dev, local, frames=1024, cpu=True, info=None):
     seq = np.stack([textured_image(4000 + i, 1280, 720) for i in range(16)])
     r = {"workload": "C2 on textured 1280x720 frames (value noise + sigma-12 pixel noise), 2000 features, "
                      "extract + match vs previous frame"}
-    r.update(extract_match_gpu_leg(dev, local, seq, 2000, reps=frames))
+    r.update(extract_match_gpu_leg(dev, local, seq, 2000, reps=frames, issue_kind="textured"))
     if cpu:
         r["cpu_baseline"] = cpu_baseline_block("frames/s", "textured 1280x720 frames, extract + match vs previous",
                                                cpu_extract_match(seq[:4], 2000, 1, 4.0),
@@ -501,6 +568,92 @@ def stereo_leg(dev, local, pairs=64, steps=5):
     return {"workload": "ComputeStereoMatches on 1242x375 stereo pairs (extracted on the device), 2000 features",
             "pairs_per_step": pairs, "pairs_per_s": pairs / (ms * 1e-3), "stereo_match_ms_per_step": ms,
             "matched_per_pair": matched}
+
+
+def latency_leg(dev, local, cpu=True, calls=100):
+    """Single-call latency at the reference's own call shape (VERDICT r05 "Next round" 5):
+    * C2: one 1280x720 frame through the host API `orbx_extract` (ORBextractor::Extract, H2D + extract +
+      D2H, synchronous), as Tracking::GrabImageMonocular calls it (System.cc:449-452 for the stereo
+      case; one frame per call);
+    * C3: one 1242x375 stereo pair as Frame's stereo constructor does it (Frame.cc: the two Extract calls
+      on two threads, then ComputeStereoMatches, System.cc:449-461): two handles, two host threads, then
+      the host-pyramid `orbm_compute_stereo_matches` on the handles' GetImagePyramid() levels;
+    each with the single-thread oracle doing the same work beside it (median of the calls)."""
+    import threading
+    import torch
+    from orb_slam2_refactored_amd import ComputeStereoMatches, ORBextractor
+    from orb_slam2_refactored_amd.synth import KITTI, pan_sequence, stereo_pair
+    torch.cuda.synchronize()
+    seq = pan_sequence(0, 1280, 720, 16)
+    ex = ORBextractor(ORBextractor.Parameters(2000), device=local)
+    for i in range(10):
+        ex.Extract(seq[i % 16])
+    lat = []
+    for i in range(calls):
+        t0 = time.perf_counter()
+        ex.Extract(seq[i % 16])
+        lat.append(time.perf_counter() - t0)
+    r = {"c2_extract": {"workload": "C2 single frame through orbx_extract (host image in, keypoints + descriptors out)",
+                        "calls": calls, "median_ms": 1e3 * float(np.median(lat)), "p90_ms": 1e3 * float(np.percentile(lat, 90))}}
+    pairs = [stereo_pair(7000 + i) for i in range(8)]
+    bf, base = KITTI["bf"], KITTI["bf"] / KITTI["fx"]
+    exl = ORBextractor(ORBextractor.Parameters(2000), device=local)
+    exr = ORBextractor(ORBextractor.Parameters(2000), device=local)
+    scale = np.asarray(exl.GetScaleFactors(), np.float32)
+    inv = np.asarray(exl.GetInverseScaleFactors(), np.float32)
+    res = {}
+
+    def side(name, e, img):
+        res[name] = e.Extract(img)
+
+    def pair_call(L, R):
+        ta = threading.Thread(target=side, args=("L", exl, L))
+        tb = threading.Thread(target=side, args=("R", exr, R))
+        t0 = time.perf_counter()
+        ta.start(); tb.start(); ta.join(); tb.join()
+        t1 = time.perf_counter()
+        (kl, dl), (kr, dr) = res["L"], res["R"]
+        pl, pr = exl.GetImagePyramid(), exr.GetImagePyramid()
+        t2 = time.perf_counter()
+        ur, dp = ComputeStereoMatches(kl, dl, pl, kr, dr, pr, scale, inv, bf, base)
+        t3 = time.perf_counter()
+        return t1 - t0, t2 - t1, t3 - t2, t3 - t0, float((dp > 0).sum())
+    for i in range(5):
+        pair_call(pairs[i % 8][0], pairs[i % 8][1])
+    rows = [pair_call(pairs[i % 8][0], pairs[i % 8][1]) for i in range(calls // 2)]
+    a = np.array(rows)
+    r["c3_stereo_pair"] = {
+        "workload": "C3 stereo pair 1242x375, 2000 features: Extract L and R on two host threads (two handles), "
+                    "GetImagePyramid of both, orbm_compute_stereo_matches on the host pyramids",
+        "calls": len(rows), "median_ms": 1e3 * float(np.median(a[:, 3])),
+        "extract_two_threads_median_ms": 1e3 * float(np.median(a[:, 0])),
+        "get_pyramids_median_ms": 1e3 * float(np.median(a[:, 1])),
+        "stereo_match_median_ms": 1e3 * float(np.median(a[:, 2])), "matched_per_pair": float(np.mean(a[:, 4]))}
+    if cpu:
+        O = oracle()
+        p = O.params(2000)
+        t = []
+        for i in range(12):
+            t0 = time.perf_counter()
+            O.extract(p, seq[i % 16])
+            t.append(time.perf_counter() - t0)
+        r["c2_extract"]["cpu_baseline"] = {"median_ms": 1e3 * float(np.median(t[2:])), "cores": 1, "kind": "port",
+                                           "sample": "10 single-frame oracle Extract calls after 2 warm-ups, 1 thread"}
+        tt = O.scale_tables(p)
+        t = []
+        for i in range(8):
+            L, R = pairs[i % 8][0], pairs[i % 8][1]
+            t0 = time.perf_counter()
+            kl, dl, _ = O.extract(p, L)
+            kr, dr, _ = O.extract(p, R)
+            pl, pr = O.pyramid(p, L), O.pyramid(p, R)
+            O.compute_stereo_matches(kl, dl, pl, kr, dr, pr, tt["scale"], tt["inv_scale"], bf, base)
+            t.append(time.perf_counter() - t0)
+        r["c3_stereo_pair"]["cpu_baseline"] = {
+            "median_ms": 1e3 * float(np.median(t[2:])), "cores": 1, "kind": "port",
+            "sample": "6 stereo pairs after 2 warm-ups, oracle Extract L then R + ComputeStereoMatches on one thread "
+                      "(the pyramid recomputed for the matcher is included)"}
+    return r
 
 
 def pose_leg(dev, frames=1024, edges=1000, steps=10, cpu=True):
@@ -1095,6 +1248,35 @@ def c5_leg(ranks, ex, m, base, total=1024, steps=20, warmup=3, nfeat=2000):
     return out
 
 
+def c5_per_rank_leg(ranks, ex, m, base, per_rank=128, n_project=8, steps=20, warmup=3):
+    """C5 (configs[4]) as ONE rank of the N = 8 job sees it, measured on this one GPU (VERDICT r05 "Next
+    round" 5): 1024 / 8 = 128 frames per step through the exchange path (pack, counts / payload gather,
+    cross-shard match; the same code as N > 1, with a world of 1), next to the xGMI time of the gather the
+    eight ranks would do: each rank receives 7/8 of 8 x this rank's measured payload.  The projection
+    assumes the gather overlaps the next step's kernels (it runs on the process group's stream) or, as a
+    bound, that it serialises behind one link."""
+    run = ShardedRun(ranks, ex, m, base, per_rank, exchange=True)
+    elapsed, _ = run.timed(steps, warmup)
+    ms = 1e3 * elapsed / steps
+    blk = run.exchange_block(steps)
+    payload_rank = blk["gather_bytes_per_step"] - ranks.world * per_rank * 4   # this rank's descriptor block
+    gathered = n_project * (payload_rank + per_rank * 4)
+    recv = gathered * (n_project - 1) / n_project
+    x7, x1 = recv / (7 * 153e9) * 1e3, recv / 153e9 * 1e3
+    return {"workload": f"C5 per-rank share at N = {n_project}: {per_rank} 1280x720 frames per step on this GPU, "
+                        "extract + match vs predecessor + the exchange path (world of 1)",
+            "frames_per_rank": per_rank, "steps": steps, "warmup": warmup, "ms_per_step": ms,
+            "frames_per_s_this_rank": per_rank * steps / elapsed,
+            "payload_bytes_per_rank_per_step": payload_rank,
+            "projected_n": n_project, "projected_gather_bytes_per_step": gathered,
+            "projected_received_bytes_per_rank": recv,
+            "xgmi_bound_ms": {"all_7_links": x7, "single_link": x1},
+            "projected_job_frames_per_s": {
+                "gather_overlapped": n_project * per_rank / (max(ms, x7) * 1e-3),
+                "gather_serial_single_link": n_project * per_rank / ((ms + x1) * 1e-3)},
+            "gather_ms_local": blk["gather_ms_per_step"]}
+
+
 # ------------------------------------------------------------------------------------------ main
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
@@ -1113,7 +1295,7 @@ def parse_args(argv=None):
     ap.add_argument("--c5-frames", type=int, default=1024, help="C5's total frames per step (configs[4]: 1024)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test of the launcher / exchange only: gloo, stub extraction, no GPU, no measurement")
-    for leg in ("c1", "textured", "c3", "ba", "stereo", "pose", "projection", "bow", "c5"):
+    for leg in ("c1", "textured", "c3", "ba", "stereo", "pose", "projection", "bow", "c5", "latency", "c5n8"):
         ap.add_argument(f"--no-{leg}", action="store_true")
     return ap.parse_args(argv)
 
@@ -1228,7 +1410,12 @@ def main():
                      "pipeline_GBs_from_ms_per_step": bytes_frame * B / (ms_per_step * 1e-3) / 1e9,
                      "pipeline_frac": bytes_frame * B / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "pipeline_traffic_per_step": pipe_traffic,
-                     "pipeline_traffic_over_algorithmic": pipe_traffic / (bytes_frame * B) if pipe_traffic else None},
+                     "pipeline_traffic_over_algorithmic": pipe_traffic / (bytes_frame * B) if pipe_traffic else None,
+                     # what actually binds the extractor kernels: instruction issue (ISSUE_MODEL); the
+                     # dominant kernel's fractions use its live timed-region launch time
+                     "issue": issue_roofline("pan", dict({k: v[0] / brk_steps for k, v in breakdown.items()},
+                                                         **({"fast_cells": per_launch_ms * launches_per_step}
+                                                            if dom == "fast_cells" else {})), B)},
         # the brute-force matcher's FP4 MFMA path: every query x candidate pair is a 256-bit dot product
         "match_roofline": {"bound": "mfma", "kernel": "match (FP4 tiles)", "achieved": match_tflops,
                            "peak": FP4_PEAK_TFLOPS, "unit": "TFLOP/s (FP4)", "frac": match_tflops / FP4_PEAK_TFLOPS,
@@ -1251,6 +1438,9 @@ def main():
         result["c5"] = c5_leg(ranks, ex, m, base, total=args.c5_frames, steps=args.steps, warmup=args.warmup,
                               nfeat=args.nfeatures)
 
+    if world == 1 and not args.stub and not args.no_c5n8 and not args.no_legs:
+        result["c5_n8_per_rank"] = c5_per_rank_leg(ranks, ex, m, base, per_rank=max(1, args.c5_frames // 8),
+                                                   steps=args.steps, warmup=args.warmup)
     legs = rank == 0 and not args.no_legs and not args.stub
     cpu = world == 1 and not args.no_cpu_baseline and rank == 0 and not args.stub
     info = cpu_info()
@@ -1270,6 +1460,8 @@ def main():
         result["c3"] = c3_leg(dev, local, cpu=cpu, info=info)
     if legs and not args.no_stereo:
         result["stereo"] = stereo_leg(dev, local)
+    if legs and not args.no_latency:
+        result["latency"] = latency_leg(dev, local, cpu=cpu)
     if legs and not args.no_projection:
         result["search_by_projection"] = projection_leg(dev, cpu=cpu)
         result["search_by_projection"]["relocalisation"] = reloc_leg(dev, cpu=cpu)

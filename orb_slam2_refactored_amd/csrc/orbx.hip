@@ -40,9 +40,6 @@ constexpr int HBLUR_W = 37;             // horizontally blurred columns: +-18
 constexpr int HBS = 40;                 // LDS row stride of the blurred rows (u16): 20 dwords, 8-byte aligned rows
 static_assert(HBLUR_W + 3 <= HBS, "the blur's fourth-column tiles store up to column 39");
 
-__constant__ __attribute__((aligned(16))) float c_pattern[1024] = {   // bit_pattern_31_ (:142-400) as floats (the samples' operands)
-#include "orb_pattern31.inc"
-};
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 constexpr int c_umax_h[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};   // compile-time copy
 __constant__ int c_gauss[7] = {18, 34, 48, 56, 48, 34, 18};   // OpenCV 4.x bit-exact Q8 taps
@@ -2742,7 +2739,6 @@ constexpr HBlurA make_hblur_a() {
             }
     return t;
 }
-__constant__ HBlurA c_hblur_a = make_hblur_a();
 
 // IC_Angle (:74-101) as the same i8 products on the blur's B fragments: D_t = A_t B_nt chained over
 // the three row tiles, with A_t[m][k] = the disk weight of patch pixel (row m + 16 nt, column k) —
@@ -2764,7 +2760,21 @@ constexpr AngleA make_angle_a() {
                 }
     return t;
 }
-__constant__ AngleA c_angle_a = make_angle_a();
+// describe's constant tables in ONE symbol, read through one buffer resource (a lane's 16 bytes at
+// lane * 16 + a compile-time offset): one address materialisation instead of one s_getpc + 64-bit add per
+// table load (13 loads, ~39 SALU instructions per keypoint wave, in a kernel bound by SALU issue; round 6)
+struct DescTabs {
+    HBlurA hb;                              // 3 KiB
+    AngleA an;                              // 6 KiB
+    float pat[1024];                        // bit_pattern_31_ (:142-400) as floats (the samples' operands), 4 KiB
+};
+__constant__ __attribute__((aligned(16))) DescTabs c_desc_tabs = {make_hblur_a(), make_angle_a(), {
+#include "orb_pattern31.inc"
+}};
+constexpr int DT_HB = 0, DT_AN = 3 * 1024, DT_PAT = 9 * 1024;
+// the fdlibm sincos constants as a __constant__ copy: scalar loads instead of two s_mov_b32 per double
+__constant__ __attribute__((aligned(16))) SincosK c_sincos_k = kSincosK;
+static_assert(sizeof(HBlurA) == 3 * 1024 && sizeof(AngleA) == 6 * 1024, "table offsets");
 typedef int i4v __attribute__((ext_vector_type(4)));
 
 #ifdef ORB_DESC_STAMPS
@@ -2811,14 +2821,17 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     const int lane = threadIdx.x;
     uint8_t* R = reinterpret_cast<uint8_t*>(Hb);
     const LevelDev& L = g.lv[l];
-    const HBlurA* hblur_a = &c_hblur_a;
-    [[maybe_unused]] const AngleA* angle_a = &c_angle_a;
-    const float* pattern = c_pattern;
+    const __amdgpu_buffer_rsrc_t trs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<DescTabs*>(&c_desc_tabs), 0, (int)sizeof(DescTabs), 0x00020000);
+    // a lane's 16 bytes of 1 KiB table row `row` (hb: mt; an: 2 nt + moment; pat: r), constant offsets
+    auto tab16 = [&](int off) -> i4v {
+        return __builtin_bit_cast(i4v, __builtin_amdgcn_raw_buffer_load_b128(trs, off + 16 * lane, 0, 0));
+    };
     DESC_STAMP(0);
     // the blur's constant A fragments, in flight under the patch load
     i4v afr[3];
 #pragma unroll
-    for (int mt = 0; mt < 3; mt++) afr[mt] = *reinterpret_cast<const i4v*>(hblur_a->v[mt][lane]);
+    for (int mt = 0; mt < 3; mt++) afr[mt] = tab16(DT_HB + 1024 * mt);
 
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
     int step;
@@ -2955,8 +2968,8 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
         i4v au[3], av[3];
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-            au[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][0][lane]);
-            av[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][1][lane]);
+            au[nt] = tab16(DT_AN + 1024 * (2 * nt));
+            av[nt] = tab16(DT_AN + 1024 * (2 * nt + 1));
         }
         angle_products(au, av);
     }
@@ -3022,15 +3035,15 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     // the lane's four pattern pairs, loaded before the angle / atan / sincos chain hides their latency
     float4 pat[4];
 #pragma unroll
-    for (int r = 0; r < 4; r++) pat[r] = reinterpret_cast<const float4*>(pattern)[r * 64 + lane];
+    for (int r = 0; r < 4; r++) pat[r] = __builtin_bit_cast(float4, tab16(DT_PAT + 1024 * r));
 #endif
 #if DESC_ANGLE_MFMA && !DESC_ANGLE_FIRST
     {
         i4v au[3], av[3];
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-            au[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][0][lane]);
-            av[nt] = *reinterpret_cast<const i4v*>(angle_a->v[nt][1][lane]);
+            au[nt] = tab16(DT_AN + 1024 * (2 * nt));
+            av[nt] = tab16(DT_AN + 1024 * (2 * nt + 1));
         }
         angle_products(au, av);
     }
@@ -3048,7 +3061,7 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     b = __sinf(ang);
 #else
     if (TRIG) sincosf_glibc(ang, &b, &a);
-    else sincos_f2d(ang, &b, &a);
+    else sincos_f2d_k(ang, &b, &a, c_sincos_k);
 #endif
     DESC_STAMP(4);
     auto sample = [&](float x, float y) -> int {
@@ -3090,7 +3103,7 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
 #if DESC_PAT_EARLY
         const float4 q = pat[r];
 #else
-        const float4 q = reinterpret_cast<const float4*>(pattern)[r * 64 + lane];   // pairs 2p, 2p + 1
+        const float4 q = __builtin_bit_cast(float4, tab16(DT_PAT + 1024 * r));   // pairs 2p, 2p + 1
 #endif
         words[r] = __ballot(sample(q.x, q.y) < sample(q.z, q.w));
     }
@@ -3116,6 +3129,30 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     DESC_STAMP(6);
 }
 
+#ifndef DESC_SLOT_TAB
+#define DESC_SLOT_TAB 1   // the slot's level from a host table and the level's output range from a per-frame prefix (0: SWAR + 16 counts)
+#endif
+constexpr int LVP = 32;   // per-frame stride (ints) of describe's level prefix (nlevels + 1 <= 17 used; 128 B rows)
+
+// Per frame: the exclusive prefix of the kept counts over levels (lvl_pre[f][l] = first output row of level
+// l, lvl_pre[f][nl] = the frame's total) and counts[f].  One thread per frame, between the quadtree and
+// describe; it takes the per-level sums out of every describe wavefront's scalar preamble (round 6: the
+// 16-count load, the level compare chain and the prefix sum were ~150 of a wave's ~330 SALU instructions,
+// and describe was SALU-issue-bound, SALUBusy 83 %).
+__global__ __launch_bounds__(256) void describe_prefix_kernel(const int* __restrict__ sel_cnt, int nl, int F,
+                                                              int* __restrict__ lvl_pre, int32_t* __restrict__ counts) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    int acc = 0;
+    int* pre = lvl_pre + (long long)f * LVP;
+    for (int q = 0; q < nl; q++) {
+        pre[q] = acc;
+        acc += sel_cnt[f * nl + q];
+    }
+    pre[nl] = acc;
+    counts[f] = acc;
+}
+
 // One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
 // TRIG: ComputeOrbDescriptor's cos / sin (:107): 0 = (float)::cos((double)angle), 1 = cosf / sinf.
 template <int TRIG>
@@ -3124,7 +3161,8 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                                                       const uint32_t* __restrict__ sel,
                                                       const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
                                                       uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                      int cap) {
+                                                      int cap, const uint32_t* __restrict__ slot_tab,
+                                                      const int* __restrict__ lvl_pre) {
     // the raw patch R is dead once every lane holds its row for the horizontal blur (one
     // wavefront: its LDS reads complete before its later writes), so the blurred rows Hb reuse it
     __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];   // 43 blurred rows + 5 rows of blur slack
@@ -3134,12 +3172,26 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     DESC_STAMP(7);   // entry (diagnostic build): the preamble's loads are timed from here
     const int f = divmod_of(g, lb);
     const int s = lb - f * g.out_frame;   // selection slot (level-major, out_cap slots per level)
+#if DESC_SLOT_TAB
+    // slot -> (level, rank in the level) from the host's table, the level's output rows from the frame's
+    // prefix (describe_prefix_kernel, which also wrote counts[f]): three scalar loads, no sums
+    (void)sel_cnt;
+    (void)counts;
+    (void)lane;
+    const uint32_t e = slot_tab[s];
+    const uint32_t k = sel[(long long)f * g.out_frame + s];
+    const int l = (int)(e & 255u), i = (int)(e >> 8);
+    const int2 pr = *reinterpret_cast<const int2*>(lvl_pre + (long long)f * LVP + l);
+    if (i >= pr.y - pr.x) return;   // slot past the level's kept count
+    const int oidx = pr.x + i;      // output order: level-major list order
+    if (oidx >= cap) return;
+#else
+    (void)slot_tab;
+    (void)lvl_pre;
     // The slot's level and the frame's per-level counts without a dependent chain of loads: the
-    // level is the number of level starts (kernarg) <= s; one vector load brings level q's kept
-    // count to lane q < nlevels and the slot's keypoint word to lane 63, and the level's output base
-    // is an inclusive row scan of the counts (nlevels <= 16: lanes 0-15).
+    // level is the number of level starts (kernarg) <= s, and the level's output base is the sum of
+    // the counts of the levels before it.
     const int nl = g.nlevels;
-#if DESC_SCALAR_PRE
     // every address here is wave-uniform: scalar loads (the scalar cache path, not queued behind the
     // other wavefronts' patch loads); 16 counts read unconditionally (the count buffer has 64 B of slack)
     const uint32_t k = sel[(long long)f * g.out_frame + s];
@@ -3147,12 +3199,6 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     int cnt16[MAX_LEVELS];
 #pragma unroll
     for (int q = 0; q < MAX_LEVELS; q++) cnt16[q] = cf[q];
-#else
-    const int* lp = lane < nl ? sel_cnt + f * nl + lane
-                              : reinterpret_cast<const int*>(sel + (long long)f * g.out_frame + s);
-    const int cw = (lane < nl || lane == 63) ? *lp : 0;
-    const int cq = lane < nl ? cw : 0;
-#endif
     // levels >= nlevels carry 0x7fff (host; out_frame < 0x7fff checked there): a field x <= s iff bit
     // 15 of (x | 0x8000) - (s + 1) is clear, and no field borrows from the next
     int l = MAX_LEVELS;
@@ -3161,7 +3207,6 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 #pragma unroll
         for (int d = 0; d < MAX_LEVELS / 2; d++) l -= __popc(((g.lv_start[d] | 0x80008000u) - s1) & 0x80008000u);
     }
-#if DESC_SCALAR_PRE
     int total = 0, lbase = 0, cnt_l = 0;
 #pragma unroll
     for (int q = 0; q < MAX_LEVELS; q++) {
@@ -3170,23 +3215,12 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         lbase += q < l ? cq : 0;
         cnt_l = q == l ? cq : cnt_l;
     }
-#else
-    int sc = cq;
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xf, 0xf, true);   // row_shr:1 (zero fill)
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xf, 0xf, true);   // row_shr:2
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xf, 0xf, true);   // row_shr:4
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x118, 0xf, 0xf, true);   // row_shr:8
-    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane(cw, 63);
-    const int total = __builtin_amdgcn_readlane(sc, 15);
-    const int lbase = l > 0 ? __builtin_amdgcn_readlane(sc, l - 1) : 0;
-    const int cnt_l = __builtin_amdgcn_readlane(cq, l);
-#endif
-    const LevelDev& L = g.lv[l];
     if (s == 0 && lane == 0) counts[f] = total;
-    const int i = s - L.out_base;
+    const int i = s - g.lv[l].out_base;
     if (i >= cnt_l) return;   // slot past the level's kept count
     const int oidx = lbase + i;   // output order: level-major list order
     if (oidx >= cap) return;
+#endif
     describe_keypoint<TRIG>(g, l, f, k, (long long)f * cap + oidx, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
 }
 
@@ -3252,6 +3286,8 @@ struct orbx_extractor {
     hipEvent_t lvl_fork = nullptr, lvl_join = nullptr;
     DevBuf d_cells, d_xtab, d_ytab;
     DevBuf d_strips;                 // FAST work items: column strips of cells (fast_cells_kernel)
+    DevBuf d_slottab;                // describe: selection slot -> level | rank << 8 (out_frame entries)
+    DevBuf d_lvlpre;                 // describe: per-frame level prefix of the kept counts (LVP ints per frame)
     std::vector<int> strip_beg;      // first strip of each level (nlevels + 1 entries)
 
     // workspace for up to ws_frames frames
@@ -3505,6 +3541,13 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         ORB_HIP_TRY(hipMemcpy(h->d_xtab.ptr, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice));
     if (!ytab.empty())
         ORB_HIP_TRY(hipMemcpy(h->d_ytab.ptr, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice));
+    {   // describe's slot table: slot s of level l's [out_base, out_base + out_cap) -> l | (s - out_base) << 8
+        std::vector<uint32_t> st((size_t)g.out_frame, 0u);
+        for (int l = 0; l < Lc; l++)
+            for (int i = 0; i < g.lv[l].out_cap; i++) st[(size_t)g.lv[l].out_base + i] = (uint32_t)l | ((uint32_t)i << 8);
+        if ((rc = h->d_slottab.reserve(st.size() * sizeof(uint32_t)))) return rc;
+        ORB_HIP_TRY(hipMemcpy(h->d_slottab.ptr, st.data(), st.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     // (only with ORBX_PYR_MFMA=1: the default path allocates nothing for it)
     if (!mt.empty() && (rc = h->d_pyrmt.reserve(mt.size() * sizeof(PyrMfmaLane)))) return rc;
     if (!mkb.empty() && (rc = h->d_pyrkb.reserve(mkb.size() * sizeof(int)))) return rc;
@@ -3595,6 +3638,7 @@ static int reserve_workspace(orbx_extractor* h, int frames) {
     if ((rc = h->d_sel.reserve((size_t)frames * g.out_frame * 4))) return rc;
     // + 64 B: describe reads 16 counts from a frame's first (scalar loads, past the last frame too)
     if ((rc = h->d_selcnt.reserve((size_t)frames * g.nlevels * 4 + 64))) return rc;
+    if ((rc = h->d_lvlpre.reserve((size_t)frames * LVP * 4))) return rc;
     if (!h->d_fault.ptr) {   // sticky until read (orbx_batch_status / the host Extract)
         if ((rc = h->d_fault.reserve(16))) return rc;
         ORB_HIP_TRY(hipMemset(h->d_fault.ptr, 0, 16));
@@ -3720,8 +3764,13 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         fast(0, g.nlevels, st);
         quadtree(0, g.nlevels, st);
     }
+    int* lvlpre = h->d_lvlpre.as<int>() + (long long)f0 * LVP;
+    if (DESC_SLOT_TAB)
+        hipLaunchKernelGGL(describe_prefix_kernel, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, st, (const int*)selcnt,
+                           g.nlevels, F, lvlpre, d_counts);
     launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F),
-                 dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap);
+                 dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap,
+                 h->d_slottab.as<uint32_t>(), lvlpre);
 }
 
 // The first-cell hint bits for the next launch (fast_hint_kernel): once per batch, on st after every
@@ -3856,7 +3905,7 @@ int orbx_destroy(orbx_extractor* h) {
     (void)hipSetDevice(h->device);
     DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
-                      &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb};
+                      &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb, &h->d_slottab, &h->d_lvlpre};
     for (DevBuf* b : bufs) b->release();
     for (auto& v : h->prof_ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }

@@ -20,42 +20,54 @@
 
 namespace orbamd {
 
+// The fdlibm form's double constants.  sincos_f2d_k reads them through K: from a constexpr table they
+// fold to literals (the host checks and sincos_f2d), from a __constant__ copy they arrive by scalar
+// loads (describe_kernel, round 6: a literal double costs two s_mov_b32 of a wave's SALU issue, and
+// describe was bound by SALU issue).  The operations and their order are the same either way.
+struct SincosK {
+    double invpio2, pio2_1, pio2_1t;
+    double S1, S2, S3, S4, S5, S6;
+    double C1, C2, C3, C4, C5, C6;
+    double t_030, t_078125, t_028125;
+};
+static constexpr SincosK kSincosK = {
+    6.36619772367581382433e-01,   // 2 / pi
+    1.57079632673412561417e+00,   // first 33 bits of pi/2
+    6.07710050650619224932e-11,   // pi/2 - pio2_1
+    -1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
+    2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10,
+    4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,
+    -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11,
+    0.3, 0.78125, 0.28125};
+
 // sincos_f2d: the fdlibm form, the one describe_kernel evaluates (rounds 1-6).
-ORB_HD void sincos_f2d(float xf, float* s_out, float* c_out) {
+template <class KT>
+ORB_HD void sincos_f2d_k(float xf, float* s_out, float* c_out, const KT& K) {
 #ifdef SINCOS_FMA_DIAG   // diagnostic A/B only (round 4's fused sincos; DESIGN §4 describe round 4)
 #pragma clang fp contract(fast)
 #endif
     const double x = (double)xf;
-    const double invpio2 = 6.36619772367581382433e-01;
-    const double pio2_1 = 1.57079632673412561417e+00;    // first 33 bits of pi/2
-    const double pio2_1t = 6.07710050650619224932e-11;   // pi/2 - pio2_1
-    const double n_d = __builtin_rint(x * invpio2);
+    const double n_d = __builtin_rint(x * K.invpio2);
     const int n = (int)n_d;
-    const double r0 = x - n_d * pio2_1;                  // exact
-    const double w = n_d * pio2_1t;
+    const double r0 = x - n_d * K.pio2_1;                // exact
+    const double w = n_d * K.pio2_1t;
     const double r = r0 - w;
     const double y = (r0 - r) - w;                       // tail of the reduced argument
     const double z = r * r;
     // __kernel_sin(r, y, 1)
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
     const double v = z * r;
-    const double rs = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
-    const double sn = r - ((z * (0.5 * y - v * rs) - y) - v * S1);
+    const double rs = K.S2 + z * (K.S3 + z * (K.S4 + z * (K.S5 + z * K.S6)));
+    const double sn = r - ((z * (0.5 * y - v * rs) - y) - v * K.S1);
     // __kernel_cos(r, y)
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    const double rc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double rc = z * (K.C1 + z * (K.C2 + z * (K.C3 + z * (K.C4 + z * (K.C5 + z * K.C6)))));
     double cs;
     const double ar = r < 0 ? -r : r;
-    if (ar < 0.3) {
+    if (ar < K.t_030) {
         cs = 1.0 - (0.5 * z - (z * rc - r * y));
     } else {
         double qx;
-        if (ar > 0.78125) {
-            qx = 0.28125;
+        if (ar > K.t_078125) {
+            qx = K.t_028125;
         } else {   // |r| / 4 with the low word cleared
             const unsigned long long bits = __builtin_bit_cast(unsigned long long, ar);
             qx = __builtin_bit_cast(double, (bits - (0x00200000ull << 32)) & 0xffffffff00000000ull);
@@ -74,6 +86,7 @@ ORB_HD void sincos_f2d(float xf, float* s_out, float* c_out) {
     *s_out = (float)s;
     *c_out = (float)c;
 }
+ORB_HD void sincos_f2d(float xf, float* s_out, float* c_out) { sincos_f2d_k(xf, s_out, c_out, kSincosK); }
 
 // sincos_f2d_tab (round 5): the same function by a table reduction, about half the double operations of
 // the fdlibm form above.  Measured slower in describe (its table entry arrives by a scalar load on the

@@ -10,6 +10,8 @@
 #   kb_env   tools/kbench.py once per environment setting in $KB_ENVS ("A=1 B=2;A=0", ';'-separated),
 #            on $KB_ARGS (default: 2048 pan frames), two rounds
 #   ba       tools/babench.py 40 on the in-tree library, three runs
+#   pmc_pan | pmc_tex   instruction counters (tools/pmc_groups_inst.txt) on 1024 pan / textured frames, and the
+#            per-cell / per-wavefront counts (tools/pmc_percell.py) -> gpurun_out/pmci_{pan,textured}/
 #
 # Example: gpurun -- 'bash tools/gpu_round.sh tests smoke bench'
 #          gpurun -- 'KB_ENVS="ORBX_FAST_SPEC=8;ORBX_FAST_SPEC=-1" bash tools/gpu_round.sh kb_env'
@@ -68,6 +70,10 @@ for step in "$@"; do
         sed "s/^/[$e] /" gpurun_out/kb.log | tail -1
       done
     done ;;
+  pmc_pan|pmc_tex)
+    w=pan; [ $step = pmc_tex ] && w=textured
+    PMC_GROUPS=tools/pmc_groups_inst.txt bash tools/gpu_pmc.sh pmci_$w --$w --frames 1024 > gpurun_out/pmci_$w.log 2>&1 || { tail gpurun_out/pmci_$w.log; exit 10; }
+    python3 tools/pmc_percell.py gpurun_out/pmci_$w 1024 | tee gpurun_out/pmci_$w/percell.txt ;;
   *) echo "unknown step $step"; exit 1 ;;
   esac
 done
