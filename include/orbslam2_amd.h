@@ -317,6 +317,15 @@ int orbx_stereo_matches_batch_device(orbx_extractor* left, orbx_extractor* right
                                      float bf, float baseline, float* d_uright, float* d_depth,
                                      void* stream);
 
+/* ComputeStereoMatches for the reference's own call shape (System.cc:449-461, Frame's stereo
+ * constructor: two Extract calls, then ComputeStereoMatches on mvKeys / mvKeysRight and the two
+ * extractors' mvImagePyramid): `left` / `right` are the handles whose last call was orbx_extract on
+ * the pair's images; their keypoints, descriptors and pyramids are still on the device, so nothing but
+ * uright / depth (n_left floats each, -1 = no match) crosses PCIe.  n_left must equal the left
+ * Extract's keypoint count.  Synchronous; call after both Extract calls have returned. */
+int orbx_stereo_matches_last(orbx_extractor* left, orbx_extractor* right, float bf, float baseline, float* uright,
+                             float* depth, int n_left);
+
 /* ------------------------------------------------------------------------------------------
  * Local-map search.  Replaces ORBmatcher::SearchByProjection(Frame&, const std::vector<MapPoint*>&,
  * float th) (include/ORBmatcher.h:58, src/ORBmatcher.cc:315-382) together with the frame's

@@ -275,6 +275,17 @@ inline void ComputeStereoMatches(const std::vector<orbx_keypoint>& keypointsL, c
           "orbm_compute_stereo_matches");
 }
 
+// The same on the two extractors' last Extract (System.cc:449-461): keypoints, descriptors and pyramids stay
+// on the device; only uright / depth come back.  nLeft = keypointsLeft.size() of that Extract.
+inline void ComputeStereoMatches(ORBextractor& left, ORBextractor& right, size_t nLeft, float bf, float baseline,
+                                 std::vector<float>& uright, std::vector<float>& depth) {
+    uright.assign(nLeft, -1.f);
+    depth.assign(nLeft, -1.f);
+    check(orbx_stereo_matches_last(left.handle(), right.handle(), bf, baseline, uright.data(), depth.data(),
+                                   (int)nLeft),
+          "orbx_stereo_matches_last");
+}
+
 // Optimizer::LocalBundleAdjustment from the flattened graph (Optimizer.cc:540-631): the caller
 // gathers local / fixed keyframes and local map points exactly as :493-537, calls this, then
 // erases the outlier observations and writes poses / points back under the map mutex (:677-735).

@@ -159,6 +159,7 @@ SIGNATURES = {
                                               C.c_float, VP, VP]),
     "orbx_stereo_matches_batch_device": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, VP, VP, VP, C.c_int, C.c_float,
                                                    C.c_float, VP, VP, VP]),
+    "orbx_stereo_matches_last": (C.c_int, [VP, VP, C.c_float, C.c_float, VP, VP, C.c_int]),
     "orbm_search_by_projection": (C.c_int, [C.POINTER(ProjBatch), VP, VP, C.c_int]),
     "orbm_search_by_projection_device": (C.c_int, [C.POINTER(ProjBatch), VP, VP, VP]),
     "orbm_search_by_projection_motion_device": (C.c_int, [C.POINTER(MotionBatch), VP, VP, VP]),

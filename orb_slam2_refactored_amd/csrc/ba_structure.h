@@ -13,6 +13,7 @@ struct int2h {
 
 struct HostStructure {
     std::vector<int> act, hp, hl, pt_beg, pt_slot, pt_id, ps_beg, ps_slot, ps_id, blk_i1, blk_i2, blk_beg;
+    std::vector<int> last_pt, blk_cur;   // point-sorted path scratch: last point per pose, block cursors
     std::vector<int2h> blk_pair;
     std::vector<int> blk_index, fs_beg, fs_slot, fs_hp, sl, sp, cur;   // scratch (capacity kept across calls)
     std::vector<uint8_t> pa, la;
@@ -22,6 +23,147 @@ struct HostStructure {
     int np = 0, nl = 0;
 };
 
+inline void build_structure_generic(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
+                                    const int* ek, HostStructure& s);
+
+// The same arrays when every edge is active (the first optimize()) and the edges come grouped by point
+// (point ids non-decreasing): Optimizer.cc:580-627 adds them so, map point by map point, each with its
+// observations.  Then the point lists are runs (pt_slot = identity), the pose lists one counting sort,
+// and the pose-pair blocks come from each point's free slots directly: pass 1 counts the pairs of
+// every block (np x np counters), pass 2 appends each point's pairs to their blocks, points ascending --
+// the order the bitset path produces (block (i1, i2): points of col[i1] & col[i2] ascending, pair
+// (slot of i1, slot of i2)) without the per-pose bitsets and the (pose, point) slot table.  A point
+// that sees a free pose twice (the bitset path's `dup`) or unsorted edges take the generic build.
+// Returns false (nothing built) when the preconditions do not hold.
+inline bool build_structure_point_sorted(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed,
+                                         const int* ep, const int* ek, HostStructure& s) {
+    const int E = (int)level.size();
+    {
+        const uint8_t* lv = level.data();
+        int bad = 0;
+        for (int e = 0; e < E; e++) bad |= lv[e] | (e > 0 && ep[e] < ep[e - 1]);
+        if (bad) return false;
+    }
+    // (raw pointers throughout: a store through a vector's int* may alias another vector's members, so
+    // the compiler would reload every data pointer per element)
+    s.pa.assign(P, 0);
+    s.hp.resize(P);
+    s.ps_id.resize(P);
+    int np = 0;
+    {
+        uint8_t* pa = s.pa.data();
+        for (int e = 0; e < E; e++) pa[ek[e]] = 1;
+        int* hp = s.hp.data();
+        int* pid = s.ps_id.data();
+        for (int i = 0; i < P; i++) {
+            hp[i] = (pa[i] && !fixed[i]) ? np : -1;
+            if (hp[i] >= 0) pid[np++] = i;
+        }
+    }
+    s.ps_id.resize(np);
+    // per edge its Hessian pose index (sp); a point seeing a free pose twice takes the generic build
+    s.sp.resize(E);
+    s.last_pt.assign(std::max(np, 1), -1);
+    {
+        const int* hp = s.hp.data();
+        int* sp = s.sp.data();
+        int* last = s.last_pt.data();
+        for (int e = 0; e < E; e++) {
+            const int h = hp[ek[e]];
+            sp[e] = h;
+            if (h < 0) continue;
+            if (last[h] == ep[e]) return false;
+            last[h] = ep[e];
+        }
+    }
+    s.act.resize(E);
+    s.pt_slot.resize(E);
+    s.hl.assign(N, -1);
+    s.pt_id.resize(N);
+    s.pt_beg.resize((size_t)N + 1);
+    int nl = 0;
+    {
+        int* act = s.act.data();
+        int* pts = s.pt_slot.data();
+        int* hl = s.hl.data();
+        int* pid = s.pt_id.data();
+        int* pb = s.pt_beg.data();
+        for (int e = 0; e < E; e++) {
+            act[e] = e;
+            pts[e] = e;
+            if (e == 0 || ep[e] != ep[e - 1]) {   // points: runs of the sorted edges
+                hl[ep[e]] = nl;
+                pid[nl] = ep[e];
+                pb[nl++] = e;
+            }
+        }
+        pb[nl] = E;
+    }
+    s.pt_beg.resize((size_t)nl + 1);
+    s.pt_id.resize(nl);
+    s.np = np; s.nl = nl;
+    // poses: counting sort of the free edges by Hessian pose index (stable: e ascending)
+    s.ps_beg.assign((size_t)np + 1, 0);
+    {
+        const int* sp = s.sp.data();
+        int* qb = s.ps_beg.data();
+        for (int e = 0; e < E; e++)
+            if (sp[e] >= 0) qb[sp[e] + 1]++;
+        for (int i = 0; i < np; i++) qb[i + 1] += qb[i];
+        s.ps_slot.resize(qb[np]);
+        s.cur.assign(s.ps_beg.begin(), s.ps_beg.end() - 1);
+        int* cur = s.cur.data();
+        int* pss = s.ps_slot.data();
+        for (int e = 0; e < E; e++)
+            if (sp[e] >= 0) pss[cur[sp[e]]++] = e;
+    }
+    // pose-pair blocks: pass 1 counts, the block list, pass 2 fills (points ascending)
+    s.blk_index.assign((size_t)np * np, 0);
+    int* cnt = s.blk_index.data();
+    const int* sp = s.sp.data();
+    const int* pb = s.pt_beg.data();
+    for (int l = 0; l < nl; l++) {
+        const int b0 = pb[l], b1 = pb[l + 1];
+        for (int a = b0; a < b1; a++) {
+            const int ia = sp[a];
+            if (ia < 0) continue;
+            for (int c = a; c < b1; c++) {
+                const int ic = sp[c];
+                if (ic >= 0) cnt[ia < ic ? ia * np + ic : ic * np + ia]++;
+            }
+        }
+    }
+    s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0);
+    int total = 0;
+    for (int i1 = 0; i1 < np; i1++)
+        for (int i2 = i1; i2 < np; i2++) {
+            int& c = cnt[(size_t)i1 * np + i2];
+            if (c == 0 && i1 != i2) { c = -1; continue; }
+            s.blk_i1.push_back(i1);
+            s.blk_i2.push_back(i2);
+            const int beg = total;
+            total += c;
+            c = beg;   // now the block's fill cursor
+            s.blk_beg.push_back(total);
+        }
+    s.blk_pair.resize(total);
+    int2h* out = s.blk_pair.data();
+    for (int l = 0; l < nl; l++) {
+        const int b0 = pb[l], b1 = pb[l + 1];
+        for (int a = b0; a < b1; a++) {
+            const int ia = sp[a];
+            if (ia < 0) continue;
+            for (int c = a; c < b1; c++) {
+                const int ic = sp[c];
+                if (ic < 0) continue;
+                if (ia <= ic) out[cnt[ia * np + ic]++] = int2h{a, c};
+                else out[cnt[ic * np + ia]++] = int2h{c, a};
+            }
+        }
+    }
+    return true;
+}
+
 // SparseOptimizer::initializeOptimization(level) (sparse_optimizer.cpp:206-264) and the
 // BlockSolver structure (block_solver.hpp:142-295): active edges / vertices, Hessian indices, and
 // the Schur fill pattern (pose pairs that share a point).  Flat two-pass build (count, then fill)
@@ -30,6 +172,11 @@ struct HostStructure {
 // Pair order inside a block: points ascending, then (slot a, slot c) in the point's slot order.
 inline void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
                      const int* ek, HostStructure& s) {
+    if (build_structure_point_sorted(P, N, level, fixed, ep, ek, s)) return;
+    build_structure_generic(P, N, level, fixed, ep, ek, s);
+}
+inline void build_structure_generic(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
+                                    const int* ek, HostStructure& s) {
     const int E = (int)level.size();
     s.pa.assign(P, 0);
     s.la.assign(N, 0);

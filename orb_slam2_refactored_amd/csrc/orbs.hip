@@ -348,18 +348,30 @@ extern "C" int orbm_compute_stereo_matches(const orbm_stereo_view* left, const o
     int rc;
     if ((rc = g_st.buf.reserve(off))) return rc;
     char* base = g_st.buf.as<char>();
-    ORB_HIP_TRY(hipMemcpy(base + o_kL, left->kps, (size_t)nL * 28, hipMemcpyHostToDevice));
-    if (nR) ORB_HIP_TRY(hipMemcpy(base + o_kR, right->kps, (size_t)nR * 28, hipMemcpyHostToDevice));
-    ORB_HIP_TRY(hipMemcpy(base + o_dL, left->desc, (size_t)nL * 32, hipMemcpyHostToDevice));
-    if (nR) ORB_HIP_TRY(hipMemcpy(base + o_dR, right->desc, (size_t)nR * 32, hipMemcpyHostToDevice));
+    // everything the device reads goes up in two 1D copies from one host staging image of the slab
+    // (keypoints + descriptors, then the 2 x nl levels): pitched or per-array copies from pageable
+    // memory cost a staging round trip each (a row each, for a pitched level)
+    thread_local std::vector<char> stage;
+    stage.resize(off);
+    std::memcpy(stage.data() + o_kL, left->kps, (size_t)nL * 28);
+    if (nR) std::memcpy(stage.data() + o_kR, right->kps, (size_t)nR * 28);
+    std::memcpy(stage.data() + o_dL, left->desc, (size_t)nL * 32);
+    if (nR) std::memcpy(stage.data() + o_dR, right->desc, (size_t)nR * 32);
+    for (int v = 0; v < 2; v++)
+        for (int l = 0; l < nl; l++) {
+            const int rows = views[v]->level_rows[l], cols = views[v]->level_cols[l];
+            const size_t stp = (size_t)views[v]->level_step[l];
+            for (int y = 0; y < rows; y++)
+                std::memcpy(stage.data() + o_lv[v][l] + (size_t)y * cols, views[v]->level[l] + y * stp, (size_t)cols);
+        }
+    ORB_HIP_TRY(hipMemcpy(base, stage.data(), o_u, hipMemcpyHostToDevice));
+    ORB_HIP_TRY(hipMemcpy(base + o_lv[0][0], stage.data() + o_lv[0][0], off - o_lv[0][0], hipMemcpyHostToDevice));
     StereoSide S[2];
     for (int v = 0; v < 2; v++) {
         std::memset(&S[v], 0, sizeof(StereoSide));
         S[v].nlevels = nl;
         for (int l = 0; l < nl; l++) {
             const int rows = views[v]->level_rows[l], cols = views[v]->level_cols[l];
-            ORB_HIP_TRY(hipMemcpy2D(base + o_lv[v][l], cols, views[v]->level[l], views[v]->level_step[l], cols, rows,
-                                    hipMemcpyHostToDevice));
             S[v].off[l] = (long long)o_lv[v][l];
             S[v].stride[l] = cols;
             S[v].rows[l] = rows;

@@ -2834,8 +2834,12 @@ __device__ __forceinline__ void describe_keypoint(const Geom& g, int l, int f, u
     for (int mt = 0; mt < 3; mt++) afr[mt] = tab16(DT_HB + 1024 * mt);
 
     const int kx = kp_x(k), ky = kp_y(k), score = kp_s(k);
-    int step;
-    const uint8_t* img = level_base(g, l, f, in, in_fstride, in_step, pyr, &step);
+    // the level's base and row step: both candidates' operands come with the kernel arguments' first
+    // scalar round trip, and the selection is an s_cselect (no branch to a second round trip)
+    const uint8_t* img0 = in + (long long)f * in_fstride;
+    const uint8_t* imgl = pyr + (long long)f * g.pyr_frame_bytes + L.off;
+    const uint8_t* img = l == 0 ? img0 : imgl;
+    const int step = l == 0 ? in_step : L.stride;
     // 43x43 neighbourhood (reflect-101 outside the level, as the blur's BORDER_REFLECT_101)
     if (kx >= 21 && ky >= 21 && kx + 21 + 8 < L.w && ky + 21 < L.h) {
         // interior: 16 lanes per row (dword d of row 4k + lane/16), 11 row groups; all loads in
@@ -3180,8 +3184,15 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     (void)lane;
     const uint32_t e = slot_tab[s];
     const uint32_t k = sel[(long long)f * g.out_frame + s];
+    // both words in one scalar round trip (the compiler would sink k's load past the exits below, into a
+    // third dependent round trip on every kept keypoint's chain)
+    asm volatile("" ::"s"(e), "s"(k), "s"(cap), "s"(in), "s"(in_fstride), "s"(in_step), "s"(pyr), "s"(g.pyr_frame_bytes));
     const int l = (int)(e & 255u), i = (int)(e >> 8);
     const int2 pr = *reinterpret_cast<const int2*>(lvl_pre + (long long)f * LVP + l);
+    {   // the level's fields describe_keypoint reads, in the same round trip as the prefix (kernarg, CSE'd)
+        const LevelDev& L = g.lv[l];
+        asm volatile("" ::"s"(pr.x), "s"(pr.y), "s"(L.w), "s"(L.h), "s"(L.stride), "s"(L.off));
+    }
     if (i >= pr.y - pr.x) return;   // slot past the level's kept count
     const int oidx = pr.x + i;      // output order: level-major list order
     if (oidx >= cap) return;
@@ -3305,6 +3316,10 @@ struct orbx_extractor {
     long long last_fstride = 0;
     size_t last_step = 0;
     int last_frames = 0;
+    bool last_single = false;   // the last extraction was orbx_extract (outputs in d_kps / d_desc / d_counts)
+    int last_kcap = 0;          // its output capacity (row stride of d_kps / d_desc)
+    DevBuf d_stereo_out;        // orbx_stereo_matches_last: uright | depth on the device
+    std::vector<uint8_t> h_stage;   // host staging of the pageable copies (one copy per level / call)
 };
 
 // First column that takes FixedPtCast<int, uchar, 22> rounding under tail mode V: after a V-byte
@@ -3905,7 +3920,8 @@ int orbx_destroy(orbx_extractor* h) {
     (void)hipSetDevice(h->device);
     DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
-                      &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb, &h->d_slottab, &h->d_lvlpre};
+                      &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb, &h->d_slottab, &h->d_lvlpre,
+                      &h->d_stereo_out};
     for (DevBuf* b : bufs) b->release();
     for (auto& v : h->prof_ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -3987,6 +4003,7 @@ int orbx_extract_batch_device(orbx_extractor* h, const uint8_t* d_imgs, int n_fr
     if ((rc = reserve_workspace(h, n_frames))) return rc;
     hipStream_t st = (hipStream_t)stream;   // NULL = the default stream, like every HIP API
     h->last_in = d_imgs;
+    h->last_single = false;
     h->last_fstride = (long long)frame_stride;
     h->last_step = step;
     h->last_frames = n_frames;
@@ -4009,11 +4026,18 @@ int orbx_extract(orbx_extractor* h, const uint8_t* img, int rows, int cols, size
     if ((rc = h->d_desc.reserve((size_t)kcap * 32))) return rc;
     if ((rc = h->d_counts.reserve(16))) return rc;
     hipStream_t st = h->stream;
-    ORB_HIP_TRY(hipMemcpy2DAsync(h->d_img.ptr, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
+    // a contiguous image (the usual cv::Mat) goes up in one 1D copy: a pitched copy from pageable memory
+    // may be staged row by row
+    if (step == (size_t)cols)
+        ORB_HIP_TRY(hipMemcpyAsync(h->d_img.ptr, img, (size_t)rows * cols, hipMemcpyHostToDevice, st));
+    else
+        ORB_HIP_TRY(hipMemcpy2DAsync(h->d_img.ptr, cols, img, step, cols, rows, hipMemcpyHostToDevice, st));
     h->last_in = h->d_img.as<uint8_t>();
     h->last_fstride = (long long)rows * cols;
     h->last_step = cols;
     h->last_frames = 1;
+    h->last_single = true;
+    h->last_kcap = kcap;
     rc = launch_batch(h, h->d_img.as<uint8_t>(), 1, (long long)rows * cols, cols, h->d_kps.as<orbx_keypoint>(),
                       h->d_desc.as<uint8_t>(), h->d_counts.as<int32_t>(), kcap, st);
     if (rc) return rc;
@@ -4094,7 +4118,15 @@ int orbx_pyramid_level(const orbx_extractor* h, int level, uint8_t* dst, size_t 
     ORB_CHECK_ARG(dst_step >= (size_t)c, "dst_step too small");
     ORB_HIP_TRY(hipSetDevice(h->device));
     ORB_HIP_TRY(hipStreamSynchronize(h->stream));
-    ORB_HIP_TRY(hipMemcpy2D(dst, dst_step, p, st, c, r, hipMemcpyDeviceToHost));
+    if (dst_step == st) {
+        ORB_HIP_TRY(hipMemcpy(dst, p, (size_t)(r - 1) * st + c, hipMemcpyDeviceToHost));
+    } else {   // one 1D copy of the level's rows into host staging, then the row repack on the host: a
+               // pitched copy into pageable memory may be staged row by row (ms per level)
+        std::vector<uint8_t>& tmp = const_cast<orbx_extractor*>(h)->h_stage;
+        tmp.resize((size_t)(r - 1) * st + c);
+        ORB_HIP_TRY(hipMemcpy(tmp.data(), p, tmp.size(), hipMemcpyDeviceToHost));
+        for (int y = 0; y < r; y++) std::memcpy(dst + (size_t)y * dst_step, tmp.data() + (size_t)y * st, (size_t)c);
+    }
     return ORB_OK;
 }
 
@@ -4251,6 +4283,51 @@ int orbx_stereo_matches_batch_device(orbx_extractor* left, orbx_extractor* right
     if ((rc = left->d_stereo_sad.reserve(ints * sizeof(int32_t)))) return rc;
     return launch_stereo(L, R, sp, n_frames, d_kps_l, d_desc_l, d_counts_l, 0, d_kps_r, d_desc_r, d_counts_r, 0, cap,
                          d_uright, d_depth, left->d_stereo_sad.as<int32_t>(), (hipStream_t)stream);
+}
+
+int orbx_stereo_matches_last(orbx_extractor* left, orbx_extractor* right, float bf, float baseline, float* uright,
+                             float* depth, int n_left) {
+    ORB_CHECK_ARG(left && right && left != right && uright && depth, "null argument");
+    ORB_CHECK_ARG(left->last_single && right->last_single, "both extractors need a single-frame orbx_extract first");
+    ORB_CHECK_ARG(left->g_rows == right->g_rows && left->g_cols == right->g_cols &&
+                      left->p.nlevels == right->p.nlevels && left->p.scaleFactor == right->p.scaleFactor &&
+                      left->last_kcap == right->last_kcap,
+                  "left / right extractors differ in image size or pyramid parameters");
+    ORB_CHECK_ARG(left->p.nlevels <= ST_MAX_LEVELS, "too many levels");
+    std::unique_lock<std::mutex> la(left->mu, std::defer_lock), lb(right->mu, std::defer_lock);
+    std::lock(la, lb);
+    ORB_HIP_TRY(hipSetDevice(left->device));
+    const int cap = left->last_kcap;
+    int32_t nl = 0;
+    ORB_HIP_TRY(hipMemcpy(&nl, left->d_counts.ptr, 4, hipMemcpyDeviceToHost));
+    ORB_CHECK_ARG(n_left == nl, "n_left differs from the left extractor's keypoint count");
+    if (nl == 0) return ORB_OK;
+    int rc;
+    StereoSide L, R;
+    stereo_side(left, L);
+    stereo_side(right, R);
+    StereoParams sp;
+    std::memset(&sp, 0, sizeof(sp));
+    for (int l = 0; l < left->p.nlevels; l++) {
+        sp.scale[l] = left->scale[l];
+        sp.inv_scale[l] = left->inv_scale[l];
+    }
+    sp.bf = bf;
+    sp.baseline = baseline;
+    const size_t ints = stereo_scratch_ints(1, cap, L.rows[0], stereo_row_span(sp, left->p.nlevels));
+    if ((rc = left->d_stereo_sad.reserve(ints * sizeof(int32_t)))) return rc;
+    if ((rc = left->d_stereo_out.reserve(2 * (size_t)cap * sizeof(float)))) return rc;
+    float* d_u = left->d_stereo_out.as<float>();
+    float* d_d = d_u + cap;
+    hipStream_t st = left->stream;
+    if ((rc = launch_stereo(L, R, sp, 1, left->d_kps.as<orbx_keypoint>(), left->d_desc.as<uint8_t>(),
+                            left->d_counts.as<int32_t>(), 0, right->d_kps.as<orbx_keypoint>(), right->d_desc.as<uint8_t>(),
+                            right->d_counts.as<int32_t>(), 0, cap, d_u, d_d, left->d_stereo_sad.as<int32_t>(), st)))
+        return rc;
+    ORB_HIP_TRY(hipMemcpyAsync(uright, d_u, (size_t)nl * sizeof(float), hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipMemcpyAsync(depth, d_d, (size_t)nl * sizeof(float), hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipStreamSynchronize(st));
+    return ORB_OK;
 }
 
 int orbx_debug_fast_stamps(unsigned long long* out, int n_words) {

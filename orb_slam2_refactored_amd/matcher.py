@@ -301,6 +301,18 @@ def ComputeStereoMatches(keypointsL, descriptorsL, pyramidL, keypointsR, descrip
     return ur, dp
 
 
+def ComputeStereoMatchesLast(extractor_l, extractor_r, n_left: int, bf: float, baseline: float):
+    """ComputeStereoMatches at the reference's call shape (System.cc:449-461: Extract L and R, then
+    ComputeStereoMatches on mvKeys / mvKeysRight and both mvImagePyramid): on the two extractors' last
+    single-frame Extract, whose keypoints, descriptors and pyramids are still on the device.  n_left =
+    the left Extract's keypoint count.  Returns (uright, depth), float32 [n_left], -1 = no match."""
+    ur = np.full(n_left, -1, np.float32)
+    dp = np.full(n_left, -1, np.float32)
+    check(lib().orbx_stereo_matches_last(extractor_l._h, extractor_r._h, C.c_float(bf), C.c_float(baseline), ptr(ur),
+                                         ptr(dp), int(n_left)), "orbx_stereo_matches_last")
+    return ur, dp
+
+
 def stereo_matches_batch_device(extractor_l, extractor_r, outs_l, outs_r, bf: float, baseline: float, out=None,
                                 stream=None):
     """Batched ComputeStereoMatches on the frames of two extractors' last batches.  outs_l / outs_r are

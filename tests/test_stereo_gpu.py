@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from orb_slam2_refactored_amd import ComputeStereoMatches, ORBextractor
-from orb_slam2_refactored_amd.matcher import stereo_matches_batch_device
+from orb_slam2_refactored_amd.matcher import ComputeStereoMatchesLast, stereo_matches_batch_device
 from orb_slam2_refactored_amd.synth import KITTI, stereo_pair
 
 pytestmark = pytest.mark.gpu
@@ -30,6 +30,50 @@ def test_stereo_host_api_bit_exact(oracle, seed, W, H, nf):
     assert (exp_d > 0).sum() > 0.3 * len(kl)
     assert np.array_equal(got_u.view(np.int32), exp_u.view(np.int32))
     assert np.array_equal(got_d.view(np.int32), exp_d.view(np.int32))
+
+
+@pytest.mark.parametrize("seed,W,H,nf", [(0, 1242, 375, 2000), (3, 640, 480, 1000)])
+def test_stereo_last_extract_bit_exact(oracle, seed, W, H, nf):
+    """orbx_stereo_matches_last: the reference's call shape (Extract L, Extract R, ComputeStereoMatches on
+    the extractors' own keypoints / descriptors / pyramids, System.cc:449-461), nothing copied back
+    but uright / depth; bit-identical to the oracle, and to the host-pyramid entry point."""
+    import threading
+    L, R, _ = stereo_pair(seed, W, H)
+    exl = ORBextractor(ORBextractor.Parameters(nf))
+    exr = ORBextractor(ORBextractor.Parameters(nf))
+    out = {}
+    ta = threading.Thread(target=lambda: out.__setitem__("L", exl.Extract(L)))
+    tb = threading.Thread(target=lambda: out.__setitem__("R", exr.Extract(R)))
+    ta.start(); tb.start(); ta.join(); tb.join()
+    (kl, dl), (kr, dr) = out["L"], out["R"]
+    got_u, got_d = ComputeStereoMatchesLast(exl, exr, len(kl), BF, BASELINE)
+    p = oracle.params(nf)
+    t = oracle.scale_tables(p)
+    okl, odl, opl = oracle_side(oracle, p, L)
+    okr, odr, opr = oracle_side(oracle, p, R)
+    exp_u, exp_d = oracle.compute_stereo_matches(okl, odl, opl, okr, odr, opr, t["scale"], t["inv_scale"], BF, BASELINE)
+    assert (exp_d > 0).sum() > 0.3 * len(okl)
+    assert np.array_equal(got_u.view(np.int32), exp_u.view(np.int32))
+    assert np.array_equal(got_d.view(np.int32), exp_d.view(np.int32))
+    h_u, h_d = ComputeStereoMatches(kl, dl, exl.GetImagePyramid(), kr, dr, exr.GetImagePyramid(), t["scale"],
+                                    t["inv_scale"], BF, BASELINE)
+    assert np.array_equal(h_u.view(np.int32), exp_u.view(np.int32)) and np.array_equal(h_d.view(np.int32), exp_d.view(np.int32))
+
+
+def test_stereo_last_extract_rejects_batch_handles():
+    import torch
+    from orb_slam2_refactored_amd._lib import OrbError
+    L, R, _ = stereo_pair(4, 640, 480)
+    exl = ORBextractor(ORBextractor.Parameters(1000))
+    exr = ORBextractor(ORBextractor.Parameters(1000))
+    kl, _ = exl.Extract(L)
+    exr.extract_batch_device(torch.from_numpy(R[None]).cuda())   # right: a batch, not a single Extract
+    torch.cuda.synchronize()
+    with pytest.raises(OrbError):
+        ComputeStereoMatchesLast(exl, exr, len(kl), BF, BASELINE)
+    exr.Extract(R)
+    with pytest.raises(OrbError):
+        ComputeStereoMatchesLast(exl, exr, len(kl) + 1, BF, BASELINE)   # wrong n_left
 
 
 def test_stereo_empty_sides(oracle):
