@@ -170,9 +170,10 @@ inline bool build_structure_point_sorted(int P, int N, const std::vector<uint8_t
 // over per-slot (point, pose) Hessian ids, into vectors that keep their capacity across calls: no
 // allocation per point or per block.
 // Pair order inside a block: points ascending, then (slot a, slot c) in the point's slot order.
+// sorted: try the point-sorted path first (ORBBA_STRUCT=sorted; measured, see DESIGN §4 LocalBA round 6)
 inline void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
-                     const int* ek, HostStructure& s) {
-    if (build_structure_point_sorted(P, N, level, fixed, ep, ek, s)) return;
+                     const int* ek, HostStructure& s, bool sorted = false) {
+    if (sorted && build_structure_point_sorted(P, N, level, fixed, ep, ek, s)) return;
     build_structure_generic(P, N, level, fixed, ep, ek, s);
 }
 inline void build_structure_generic(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,

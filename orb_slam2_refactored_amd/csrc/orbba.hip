@@ -1654,7 +1654,11 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     bool have_classified = false;   // the outlier classification ran (second optimize())
     auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
         if (!have_structure) {
-            build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs);
+            static const bool sorted_build = [] {
+                const char* e = getenv("ORBBA_STRUCT");
+                return e && std::string(e) == "sorted";
+            }();
+            build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs, sorted_build);
             mark("build_structure");
         }
         const int Ea = (int)hs.act.size(), np = hs.np, nl = hs.nl, D = 6 * np;

@@ -10,6 +10,9 @@
 #   kb_env   tools/kbench.py once per environment setting in $KB_ENVS ("A=1 B=2;A=0", ';'-separated),
 #            on $KB_ARGS (default: 2048 pan frames), two rounds
 #   ba       tools/babench.py 40 on the in-tree library, three runs
+#   ba_env   tools/babench.py 40 once per setting in $BA_ENVS (as kb_env), two rounds; ba_timing: one
+#            call's host-side phase times (ORBBA_DEBUG_TIMING=1)
+#   stereo   tests/test_stereo_gpu.py
 #   pmc_pan | pmc_tex   instruction counters (tools/pmc_groups_inst.txt) on 1024 pan / textured frames, and the
 #            per-cell / per-wavefront counts (tools/pmc_percell.py) -> gpurun_out/pmci_{pan,textured}/
 #
@@ -47,6 +50,20 @@ for step in "$@"; do
       timeout -k 10 60 python tools/babench.py 40 > gpurun_out/babench.log 2>&1 || { tail gpurun_out/babench.log; exit 5; }
       grep LocalBA gpurun_out/babench.log
     done ;;
+  ba_env)
+    IFS=';' read -ra envs <<< "${BA_ENVS:-}"
+    for i in 1 2; do
+      for e in "${envs[@]}"; do
+        env $e timeout -k 10 60 python tools/babench.py 40 > gpurun_out/babench.log 2>&1 || { tail gpurun_out/babench.log; exit 5; }
+        grep LocalBA gpurun_out/babench.log | sed "s/^/[$e] /"
+      done
+    done ;;
+  ba_timing)
+    ORBBA_DEBUG_TIMING=1 timeout -k 10 60 python tools/babench.py 2 > gpurun_out/ba_timing.log 2>&1 || { tail gpurun_out/ba_timing.log; exit 5; }
+    tail -14 gpurun_out/ba_timing.log ;;
+  stereo)
+    timeout -k 10 300 $PYT tests/test_stereo_gpu.py -q > gpurun_out/pytest_stereo.log 2>&1 || { tail -30 gpurun_out/pytest_stereo.log; exit 2; }
+    tail -2 gpurun_out/pytest_stereo.log ;;
   ba_ab)
     for i in 1 2 3; do
       ORBSLAM2_AMD_LIB=$PWD/tools/ab/lib_${BASE:-head}.so timeout -k 10 60 python tools/babench.py 40 > gpurun_out/babench.log 2>&1 || exit 5
