@@ -72,6 +72,7 @@ struct BADev {
     const int* ep;
     const int* ek;
     const uint8_t* stereo;
+    int cam_step;         // 5: a camera per edge; 0: one camera for every edge (uploaded once)
     const double* obs;    // E x 3
     const double* info;   // E
     const double* cam;    // E x 5
@@ -133,7 +134,7 @@ __device__ __forceinline__ void robustify(const BADev& b, int e, double chi, dou
 // EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::computeError (types_six_dof_expmap.h:90-95,122-127)
 // for edge e with camera-frame point Xc; stores g2o's _error and returns the robust chi2 term.
 __device__ __forceinline__ double edge_error(const BADev& b, int e, const double* Xc) {
-    const double* c = b.cam + 5 * e;
+    const double* c = b.cam + b.cam_step * e;
     const double* z = b.obs + 3 * e;
     if (!b.stereo[e]) {
         b.err[3 * e + 0] = z[0] - (Xc[0] / Xc[2] * c[0] + c[2]);
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
             // difference is rounding-level, within the LocalBA tolerance)
             const double x = Xc[0], y = Xc[1], z = Xc[2];
             const double iz = 1.0 / z, iz2 = iz * iz;
-            const double* c = b.cam + 5 * e;
+            const double* c = b.cam + b.cam_step * e;
             const double fx = c[0], fy = c[1], bf = c[4];
             const bool st = b.stereo[e];
             const int d = st ? 3 : 2;
@@ -1577,9 +1578,14 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
 
     // ---- device problem + state.  Everything the host provides is laid out in one region, built
     // in pinned staging with the same offsets and uploaded with a single copy.
+    // One camera for the whole window (every keyframe of a map shares the calibration: the usual case)
+    // goes up once instead of 40 B per edge: half the staging copy and the upload (round 6)
+    bool one_cam = E > 0;
+    for (int e = 1; e < E && one_cam; e++) one_cam = std::memcmp(pr->edge_cam + 5 * (size_t)e, pr->edge_cam, 40) == 0;
+    const size_t ncam = one_cam ? 5 : 5 * (size_t)E;
     const size_t up_bytes = carve_size<uint8_t>(P) + carve_size<int>(E) * 2 + carve_size<uint8_t>(E) +
                             carve_size<double>(3 * (size_t)E) + carve_size<double>(E) +
-                            carve_size<double>(5 * (size_t)E) + carve_size<double>(4 * (size_t)P) +
+                            carve_size<double>(ncam) + carve_size<double>(4 * (size_t)P) +
                             carve_size<double>(3 * (size_t)P) + carve_size<double>(3 * (size_t)N);
     const size_t state_bytes = carve_size<double>(4 * (size_t)P) + carve_size<double>(3 * (size_t)P) +
                                carve_size<double>(3 * (size_t)N) + carve_size<uint8_t>(E) * 2 +
@@ -1602,7 +1608,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     uint8_t* d_st = cp.take<uint8_t>(E);
     double* d_obs = cp.take<double>(3 * (size_t)E);
     double* d_info = cp.take<double>(E);
-    double* d_cam = cp.take<double>(5 * (size_t)E);
+    double* d_cam = cp.take<double>(ncam);
     b.q = cp.take<double>(4 * (size_t)P);
     b.t = cp.take<double>(3 * (size_t)P);
     b.X = cp.take<double>(3 * (size_t)N);
@@ -1614,7 +1620,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         for (int e = 0; e < E; e++) hst[e] = pr->edge_obs[3 * e + 2] < 0 ? 0 : 1;   // ur < 0 => mono (:595)
         std::memcpy(hp.take<double>(3 * (size_t)E), pr->edge_obs, 24 * (size_t)E);
         std::memcpy(hp.take<double>(E), pr->edge_inv_sigma2, 8 * (size_t)E);
-        std::memcpy(hp.take<double>(5 * (size_t)E), pr->edge_cam, 40 * (size_t)E);
+        std::memcpy(hp.take<double>(ncam), pr->edge_cam, 8 * ncam);
         std::memcpy(hp.take<double>(4 * (size_t)P), q0.data(), 32 * (size_t)P);
         std::memcpy(hp.take<double>(3 * (size_t)P), pr->pose_t, 24 * (size_t)P);
         std::memcpy(hp.take<double>(3 * (size_t)N), pr->points, 24 * (size_t)N);
@@ -1626,6 +1632,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     uint8_t* d_level = cs.take<uint8_t>(E);
     b.err = cs.take<double>(3 * (size_t)E);
     b.fixed = d_fixed; b.ep = d_ep; b.ek = d_ek; b.stereo = d_st; b.obs = d_obs; b.info = d_info; b.cam = d_cam;
+    b.cam_step = one_cam ? 0 : 5;
     b.level = d_level;
     b.ctl = C.ctlbuf.as<BACtl>();
     b.stop = stop_flag ? C.d_stop : nullptr;

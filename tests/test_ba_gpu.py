@@ -34,6 +34,18 @@ def test_local_ba_matches_oracle(oracle, seed, kf, pts, fixed):
     assert g["chi2"][1] < g["chi2"][0]
 
 
+def test_local_ba_per_edge_cameras(oracle):
+    """Edges with different cameras (a second calibration on every third keyframe) take the per-edge camera
+    upload; one shared camera (every other test) is uploaded once (cam_step 0).  Both match the oracle."""
+    pr = make_ba_problem(7, n_kf=10, n_pts=900, n_fixed=1)
+    cam = pr["edge_cam"].copy()
+    sel = (pr["edge_pose"] % 3) == 1
+    cam[sel, 0] *= 1.01   # fx
+    cam[sel, 2] += 2.0    # cx
+    pr = dict(pr, edge_cam=cam)
+    compare(LocalBundleAdjustment(pr), oracle.local_ba(pr))
+
+
 def test_local_ba_golden():
     z = np.load(GOLDEN / "local_ba_small.npz")
     pr = {k: z[k] for k in z.files if not k.startswith("out_")}
