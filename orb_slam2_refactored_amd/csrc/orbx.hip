@@ -3143,8 +3143,11 @@ constexpr int LVP = 32;   // per-frame stride (ints) of describe's level prefix 
 // describe; it takes the per-level sums out of every describe wavefront's scalar preamble (round 6: the
 // 16-count load, the level compare chain and the prefix sum were ~150 of a wave's ~330 SALU instructions,
 // and describe was SALU-issue-bound, SALUBusy 83 %).
+// stat[0]: the batch's largest frame total (atomicMax; the host sizes the next batch's dense describe grid
+// from it).
 __global__ __launch_bounds__(256) void describe_prefix_kernel(const int* __restrict__ sel_cnt, int nl, int F,
-                                                              int* __restrict__ lvl_pre, int32_t* __restrict__ counts) {
+                                                              int* __restrict__ lvl_pre, int32_t* __restrict__ counts,
+                                                              int* __restrict__ stat) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= F) return;
     int acc = 0;
@@ -3155,6 +3158,56 @@ __global__ __launch_bounds__(256) void describe_prefix_kernel(const int* __restr
     }
     pre[nl] = acc;
     counts[f] = acc;
+    atomicMax(stat, acc);
+}
+
+// The dense describe grid (round 6): launch slot s of frame f IS output row s.  Its level is the number of
+// levels 1..nl whose first row is <= s (one vector load of the frame's prefix, one ballot), its rank in the
+// level s - pre[l], its selection word sel[f][out_base_l + rank].  A launch of C slots per frame covers the
+// frames with at most C keypoints; C comes from the previous batch's largest total (stat[0]), so the grid
+// no longer carries every level's out_cap slack (2024 slots for ~1395 keypoints per C2 pan frame, 31 % of
+// the wavefronts empty), and describe_overflow_kernel covers rows >= C of any frame that has more.
+struct DescGrid {
+    int C;                 // slots per frame in this launch
+    unsigned m;            // lb / C by the round-up magic (as divmod_of)
+    int s1, s2;
+};
+template <int TRIG>
+__device__ __forceinline__ void describe_dense_slot(const Geom& g, int f, int s, const uint8_t* __restrict__ in,
+                                                    long long in_fstride, int in_step, const uint8_t* __restrict__ pyr,
+                                                    const uint32_t* __restrict__ sel, orbx_keypoint* __restrict__ kps,
+                                                    uint8_t* __restrict__ desc, int cap, const int* __restrict__ lvl_pre,
+                                                    uint16_t* Hb, int lb) {
+    const int lane = threadIdx.x, nl = g.nlevels;
+    const int pq = lane <= nl ? lvl_pre[(long long)f * LVP + lane] : 0x7fffffff;
+    const int T = __builtin_amdgcn_readlane(pq, nl);
+    if (s >= T || s >= cap) return;   // wave-uniform
+    const int l = popc64(__ballot(lane >= 1 && lane <= nl && pq <= s));
+    const int pre_l = __builtin_amdgcn_readlane(pq, l);
+    const uint32_t k = sel[(long long)f * g.out_frame + g.lv[l].out_base + (s - pre_l)];
+    describe_keypoint<TRIG>(g, l, f, k, (long long)f * cap + s, in, in_fstride, in_step, pyr, kps, desc, Hb, lb);
+}
+
+// Rows >= C of the frames whose total exceeds the dense launch's C: a fixed grid of one-wave workgroups
+// loops over the frames (wave w: frames w, w + grid, ...) and their extra rows.  Exits at once when no
+// frame overflows.
+template <int TRIG>
+__global__ __launch_bounds__(64) void describe_overflow_kernel(Geom g, const uint8_t* __restrict__ in,
+                                                               long long in_fstride, int in_step,
+                                                               const uint8_t* __restrict__ pyr,
+                                                               const uint32_t* __restrict__ sel,
+                                                               orbx_keypoint* __restrict__ kps,
+                                                               uint8_t* __restrict__ desc, int cap,
+                                                               const int* __restrict__ lvl_pre, int F, int C) {
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];
+    for (int f = blockIdx.x; f < F; f += gridDim.x) {
+        const int T = min(lvl_pre[(long long)f * LVP + g.nlevels], cap);
+        for (int s = C; s < T; s++) {
+            describe_dense_slot<TRIG>(g, f, s, in, in_fstride, in_step, pyr, sel, kps, desc, cap, lvl_pre, Hb,
+                                      (int)blockIdx.x);
+            __syncthreads();   // Hb is reused by the next row
+        }
+    }
 }
 
 // One wavefront per selection slot of a frame; slots past their level's kept count exit at once.
@@ -3166,7 +3219,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                                                       const int* __restrict__ sel_cnt, orbx_keypoint* __restrict__ kps,
                                                       uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
                                                       int cap, const uint32_t* __restrict__ slot_tab,
-                                                      const int* __restrict__ lvl_pre) {
+                                                      const int* __restrict__ lvl_pre, DescGrid dg) {
     // the raw patch R is dead once every lane holds its row for the horizontal blur (one
     // wavefront: its LDS reads complete before its later writes), so the blurred rows Hb reuse it
     __shared__ __attribute__((aligned(16))) uint16_t Hb[HB_ELEMS];   // 43 blurred rows + 5 rows of blur slack
@@ -3174,6 +3227,14 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const int lane = threadIdx.x;
     const int lb = xcd_swizzle(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     DESC_STAMP(7);   // entry (diagnostic build): the preamble's loads are timed from here
+    if (dg.C > 0) {   // the dense grid (DescGrid): slot = output row
+        const unsigned t = __umulhi((unsigned)lb, dg.m);
+        const int fd = (int)((t + (((unsigned)lb - t) >> dg.s1)) >> dg.s2);
+        (void)sel_cnt; (void)counts; (void)slot_tab;
+        describe_dense_slot<TRIG>(g, fd, lb - fd * dg.C, in, in_fstride, in_step, pyr, sel, kps, desc, cap, lvl_pre, Hb,
+                                  lb);
+        return;
+    }
     const int f = divmod_of(g, lb);
     const int s = lb - f * g.out_frame;   // selection slot (level-major, out_cap slots per level)
 #if DESC_SLOT_TAB
@@ -3316,6 +3377,14 @@ struct orbx_extractor {
     long long last_fstride = 0;
     size_t last_step = 0;
     int last_frames = 0;
+    // dense describe grid (DescGrid): slots per frame from the previous batch's largest total
+    int desc_dense = 1;         // ORBX_DESC_DENSE=0: the slot-table grid (out_frame slots per frame)
+    int desc_force_c = 0;       // test hook (ORBX_DESC_C): this C for every batch (exercises the overflow kernel)
+    int desc_c = 0;             // C of the next batch (0: unknown, out_frame)
+    DevBuf d_dstat;             // stat[0] = the batch's largest frame total (describe_prefix_kernel)
+    int32_t* h_dstat = nullptr; // pinned copy of it
+    hipEvent_t dstat_ev = nullptr;
+    bool dstat_pending = false;
     bool last_single = false;   // the last extraction was orbx_extract (outputs in d_kps / d_desc / d_counts)
     int last_kcap = 0;          // its output capacity (row stride of d_kps / d_desc)
     DevBuf d_stereo_out;        // orbx_stereo_matches_last: uright | depth on the device
@@ -3782,10 +3851,28 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     int* lvlpre = h->d_lvlpre.as<int>() + (long long)f0 * LVP;
     if (DESC_SLOT_TAB)
         hipLaunchKernelGGL(describe_prefix_kernel, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, st, (const int*)selcnt,
-                           g.nlevels, F, lvlpre, d_counts);
-    launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>, dim3((unsigned)g.out_frame, (unsigned)F),
-                 dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, selcnt, d_kps, d_desc, d_counts, cap,
-                 h->d_slottab.as<uint32_t>(), lvlpre);
+                           g.nlevels, F, lvlpre, d_counts, h->d_dstat.as<int>());
+    // the dense grid: C slots per frame (from the previous batch's largest total), the overflow kernel for
+    // rows >= C of any frame with more (DescGrid); or the slot-table grid (out_frame slots)
+    const int rows_max = std::min(g.out_frame, cap);
+    const int C = (DESC_SLOT_TAB && h->desc_dense) ? std::max(1, std::min(h->desc_c > 0 ? h->desc_c : rows_max, rows_max)) : 0;
+    DescGrid dg{};
+    if (C > 0) {
+        dg.C = C;
+        const unsigned d = (unsigned)C;
+        int lg = 0;
+        while ((1ull << lg) < d) lg++;
+        dg.m = (unsigned)((((1ull << lg) - d) << 32) / d + 1);
+        dg.s1 = lg > 0 ? 1 : 0;
+        dg.s2 = lg > 0 ? lg - 1 : 0;
+    }
+    launch_timed(h, 3, h->trig_float ? describe_kernel<1> : describe_kernel<0>,
+                 dim3((unsigned)(C > 0 ? C : g.out_frame), (unsigned)F), dim3(64), 0u, st, g, d_imgs, fstride, step, pyr,
+                 sel, selcnt, d_kps, d_desc, d_counts, cap, h->d_slottab.as<uint32_t>(), lvlpre, dg);
+    if (C > 0 && C < rows_max)
+        launch_timed(h, 3, h->trig_float ? describe_overflow_kernel<1> : describe_overflow_kernel<0>,
+                     dim3((unsigned)std::min(F, 2048)), dim3(64), 0u, st, g, d_imgs, fstride, step, pyr, sel, d_kps, d_desc,
+                     cap, (const int*)lvlpre, F, C);
 }
 
 // The first-cell hint bits for the next launch (fast_hint_kernel): once per batch, on st after every
@@ -3804,8 +3891,38 @@ static int launch_fast_hint(orbx_extractor* h, hipStream_t st) {
 // Frames are split into sub-batches on the handle's side streams (fork/join with events on st) so
 // that one sub-batch's latency-bound stages (the short pyramid levels, the quadtree's level-0 tail)
 // overlap another's FAST / describe work.
+// The dense describe grid's C for this batch: the previous batch's largest frame total (read back
+// asynchronously; a copy not yet landed keeps the last C) plus a margin, rounded up to 64.
+static int describe_grid_begin(orbx_extractor* h, hipStream_t st) {
+    if (!h->dstat_ev) {
+        ORB_HIP_TRY(hipEventCreateWithFlags(&h->dstat_ev, hipEventDisableTiming));
+        ORB_HIP_TRY(hipHostMalloc((void**)&h->h_dstat, 64, hipHostMallocDefault));
+        int rc;
+        if ((rc = h->d_dstat.reserve(64))) return rc;
+    }
+    if (h->dstat_pending && hipEventQuery(h->dstat_ev) == hipSuccess) {
+        const int mx = *h->h_dstat;
+        h->desc_c = (int)align_up((size_t)std::max(mx + 32, 64), 64);
+        h->dstat_pending = false;
+    }
+    if (h->desc_force_c > 0) h->desc_c = h->desc_force_c;
+    ORB_HIP_TRY(hipMemsetAsync(h->d_dstat.ptr, 0, 4, st));
+    return ORB_OK;
+}
+static int describe_grid_end(orbx_extractor* h, hipStream_t st) {
+    if (h->dstat_pending) return ORB_OK;   // the previous read-back has not landed: keep its slot
+    ORB_HIP_TRY(hipMemcpyAsync(h->h_dstat, h->d_dstat.ptr, 4, hipMemcpyDeviceToHost, st));
+    ORB_HIP_TRY(hipEventRecord(h->dstat_ev, st));
+    h->dstat_pending = true;
+    return ORB_OK;
+}
+
 static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long long fstride, int step,
                         orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, hipStream_t st) {
+    {
+        const int rc = describe_grid_begin(h, st);
+        if (rc) return rc;
+    }
     int nsub = std::min(h->nsub, F / ORBX_MIN_SUB_FRAMES);
     if (nsub <= 1) {
         hipStream_t side = nullptr;
@@ -3820,7 +3937,8 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
         }
         launch_chunk(h, 0, d_imgs, F, fstride, step, d_kps, d_desc, d_counts, cap, st, side);
         ORB_HIP_TRY(hipGetLastError());
-        return launch_fast_hint(h, st);
+        const int rc = describe_grid_end(h, st);
+        return rc ? rc : launch_fast_hint(h, st);
     }
     while ((int)h->sub.size() < nsub) {
         hipStream_t s2;
@@ -3841,7 +3959,8 @@ static int launch_batch(orbx_extractor* h, const uint8_t* d_imgs, int F, long lo
         f0 += Fi;
     }
     ORB_HIP_TRY(hipGetLastError());
-    return launch_fast_hint(h, st);
+    const int rc = describe_grid_end(h, st);
+    return rc ? rc : launch_fast_hint(h, st);
 }
 
 static int check_fault(orbx_extractor* h) {
@@ -3894,6 +4013,8 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_PYR_MFMA")) h->pyr_mfma = atoi(e) != 0;
     if (const char* e = getenv("ORBX_LEVEL_OVERLAP")) h->lvl_overlap = atoi(e) != 0;
     if (const char* e = getenv("ORBX_DEBUG_NC")) h->debug_nc = atoi(e);
+    if (const char* e = getenv("ORBX_DESC_DENSE")) h->desc_dense = atoi(e) != 0;
+    if (const char* e = getenv("ORBX_DESC_C")) h->desc_force_c = std::max(0, atoi(e));
     if (const char* e = getenv("ORBX_DEBUG_QT_BLOCK")) {
         const int b = atoi(e);
         if (b >= 64 && b <= QT_THREADS && b % 64 == 0) h->debug_qt_block = b;
@@ -3921,7 +4042,7 @@ int orbx_destroy(orbx_extractor* h) {
     DevBuf* bufs[] = {&h->d_cells, &h->d_strips, &h->d_xtab, &h->d_ytab, &h->d_pyr, &h->d_slots, &h->d_cellcnt, &h->d_P,
                       &h->d_T, &h->d_sel, &h->d_selcnt, &h->d_fault, &h->d_img, &h->d_kps, &h->d_desc,
                       &h->d_counts, &h->d_stereo_sad, &h->d_pyrmt, &h->d_pyrkb, &h->d_slottab, &h->d_lvlpre,
-                      &h->d_stereo_out};
+                      &h->d_stereo_out, &h->d_dstat};
     for (DevBuf* b : bufs) b->release();
     for (auto& v : h->prof_ev)
         for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -3932,6 +4053,8 @@ int orbx_destroy(orbx_extractor* h) {
     if (h->lvl_side) (void)hipStreamDestroy(h->lvl_side);
     if (h->lvl_fork) (void)hipEventDestroy(h->lvl_fork);
     if (h->lvl_join) (void)hipEventDestroy(h->lvl_join);
+    if (h->dstat_ev) (void)hipEventDestroy(h->dstat_ev);
+    if (h->h_dstat) (void)hipHostFree(h->h_dstat);
     delete h;
     return ORB_OK;
 }
