@@ -12,6 +12,7 @@
 #   ba       tools/babench.py 40 on the in-tree library, three runs
 #   ba_env   tools/babench.py 40 once per setting in $BA_ENVS (as kb_env), two rounds; ba_timing: one
 #            call's host-side phase times (ORBBA_DEBUG_TIMING=1)
+#   kb_sweep tools/kbench.py on pan frames at 64 .. 2048 frames per launch (per-frame stage times)
 #   stereo   tests/test_stereo_gpu.py      batests  tests/test_ba_gpu.py + tests/test_cpp_dropin_gpu.py
 #   pmc_pan | pmc_tex   instruction counters (tools/pmc_groups_inst.txt) on 1024 pan / textured frames, and the
 #            per-cell / per-wavefront counts (tools/pmc_percell.py) -> gpurun_out/pmci_{pan,textured}/
@@ -61,6 +62,11 @@ for step in "$@"; do
   ba_timing)
     ORBBA_DEBUG_TIMING=1 timeout -k 10 60 python tools/babench.py 2 > gpurun_out/ba_timing.log 2>&1 || { tail gpurun_out/ba_timing.log; exit 5; }
     tail -14 gpurun_out/ba_timing.log ;;
+  kb_sweep)
+    for n in 64 128 256 512 2048; do
+      timeout -k 10 120 python tools/kbench.py --frames $n --iters 10 --pan > gpurun_out/kb.log 2>&1 || { tail gpurun_out/kb.log; exit 8; }
+      sed "s/^/[$n frames] /" gpurun_out/kb.log | tail -1
+    done ;;
   batests)
     timeout -k 10 300 $PYT tests/test_ba_gpu.py tests/test_cpp_dropin_gpu.py -q > gpurun_out/pytest_ba.log 2>&1 || { tail -30 gpurun_out/pytest_ba.log; exit 2; }
     tail -2 gpurun_out/pytest_ba.log ;;
