@@ -21,7 +21,97 @@ struct HostStructure {
     std::vector<int> slot_of;              // [pose][point] -> free slot (pair blocks; a block's fill reads
                                            // two rows in point order)
     int np = 0, nl = 0;
+    int n_act = 0, n_ps = 0, n_pairs = 0;   // sizes of act / ps_slot / blk_pair (also when the device fills them)
 };
+
+// The host half of the device-side build (round 6; orbba.hip ba_struct_slots_kernel +
+// ba_struct_pairs_kernel fill act, pt_slot, ps_slot and blk_pair on the GPU).  Under the
+// point-sorted preconditions (every edge active, point ids non-decreasing, no point seeing a free
+// pose twice -- Optimizer.cc:580-627 adds the edges map point by map point) it computes everything
+// but those four arrays: the vertex indices, the point runs, the per-pose counts and the pose-pair
+// block list with each block's pair count (popcounts of per-pose point bitsets).  O(E) plus
+// np^2/2 x nl/64 popcounts; the arrays the device fills equal build_structure's (the fill walks
+// the points of each block in ascending order, as the bitset path does).  Returns false (the
+// caller then runs build_structure) when a precondition fails.
+inline bool build_structure_counts(int P, int N, const uint8_t* fixed, const int* ep, const int* ek, int E,
+                                   HostStructure& s) {
+    for (int e = 1; e < E; e++)
+        if (ep[e] < ep[e - 1]) return false;
+    s.pa.assign(P, 0);
+    s.hp.resize(P);
+    s.ps_id.resize(P);
+    int np = 0;
+    {
+        uint8_t* pa = s.pa.data();
+        for (int e = 0; e < E; e++) pa[ek[e]] = 1;
+        int* hp = s.hp.data();
+        int* pid = s.ps_id.data();
+        for (int i = 0; i < P; i++) {
+            hp[i] = (pa[i] && !fixed[i]) ? np : -1;
+            if (hp[i] >= 0) pid[np++] = i;
+        }
+    }
+    s.ps_id.resize(np);
+    s.hl.assign(N, -1);
+    s.pt_id.resize(N);
+    s.pt_beg.resize((size_t)N + 1);
+    int nl = 0;
+    {
+        int* hl = s.hl.data();
+        int* pid = s.pt_id.data();
+        int* pb = s.pt_beg.data();
+        for (int e = 0; e < E; e++)
+            if (e == 0 || ep[e] != ep[e - 1]) {
+                hl[ep[e]] = nl;
+                pid[nl] = ep[e];
+                pb[nl++] = e;
+            }
+        pb[nl] = E;
+    }
+    s.pt_beg.resize((size_t)nl + 1);
+    s.pt_id.resize(nl);
+    const int W = (nl + 63) >> 6;
+    s.col.assign((size_t)np * W, 0ull);
+    s.ps_beg.assign((size_t)np + 1, 0);
+    {
+        const int* hp = s.hp.data();
+        const int* pb = s.pt_beg.data();
+        unsigned long long* col = s.col.data();
+        int* qb = s.ps_beg.data();
+        for (int l = 0; l < nl; l++) {
+            const unsigned long long bit = 1ull << (l & 63);
+            for (int e = pb[l]; e < pb[l + 1]; e++) {
+                const int h = hp[ek[e]];
+                if (h < 0) continue;
+                unsigned long long& w = col[(size_t)h * W + (l >> 6)];
+                if (w & bit) return false;   // the point sees this free pose twice
+                w |= bit;
+                qb[h + 1]++;
+            }
+        }
+        for (int i = 0; i < np; i++) qb[i + 1] += qb[i];
+    }
+    s.blk_i1.clear(); s.blk_i2.clear(); s.blk_beg.assign(1, 0);
+    int total = 0;
+    {
+        const unsigned long long* col = s.col.data();
+        for (int i1 = 0; i1 < np; i1++)
+            for (int i2 = i1; i2 < np; i2++) {
+                const unsigned long long* c1 = col + (size_t)i1 * W;
+                const unsigned long long* c2 = col + (size_t)i2 * W;
+                int cnt = 0;
+                for (int w = 0; w < W; w++) cnt += __builtin_popcountll(c1[w] & c2[w]);
+                if (cnt == 0 && i1 != i2) continue;
+                s.blk_i1.push_back(i1);
+                s.blk_i2.push_back(i2);
+                total += cnt;
+                s.blk_beg.push_back(total);
+            }
+    }
+    s.np = np; s.nl = nl;
+    s.n_act = E; s.n_ps = s.ps_beg[np]; s.n_pairs = total;
+    return true;
+}
 
 inline void build_structure_generic(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
                                     const int* ek, HostStructure& s);
@@ -173,8 +263,11 @@ inline bool build_structure_point_sorted(int P, int N, const std::vector<uint8_t
 // sorted: try the point-sorted path first (ORBBA_STRUCT=sorted; measured, see DESIGN §4 LocalBA round 6)
 inline void build_structure(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
                      const int* ek, HostStructure& s, bool sorted = false) {
-    if (sorted && build_structure_point_sorted(P, N, level, fixed, ep, ek, s)) return;
-    build_structure_generic(P, N, level, fixed, ep, ek, s);
+    if (!(sorted && build_structure_point_sorted(P, N, level, fixed, ep, ek, s)))
+        build_structure_generic(P, N, level, fixed, ep, ek, s);
+    s.n_act = (int)s.act.size();
+    s.n_ps = (int)s.ps_slot.size();
+    s.n_pairs = (int)s.blk_pair.size();
 }
 inline void build_structure_generic(int P, int N, const std::vector<uint8_t>& level, const uint8_t* fixed, const int* ep,
                                     const int* ek, HostStructure& s) {

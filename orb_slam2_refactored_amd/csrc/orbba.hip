@@ -1017,6 +1017,259 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
     BA_STAMP(42);
 }
 
+// ---- Device half of the structure build (round 6; host half: ba_structure.h build_structure_counts).
+// The (free pose, point) slot table, pose-major (row i: the edge of pose i at each point, -1 where
+// none; memset to -1 first), and the identity lists of the point-sorted case.
+__global__ void ba_struct_slots_kernel(const int* __restrict__ ep, const int* __restrict__ ek,
+                                       const int* __restrict__ hp, const int* __restrict__ hl, int E, int nl,
+                                       int* __restrict__ act, int* __restrict__ pt_slot, int* __restrict__ slot_of) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    act[e] = e;
+    pt_slot[e] = e;
+    const int h = hp[ek[e]];
+    if (h >= 0) slot_of[(long long)h * nl + hl[ep[e]]] = e;
+}
+// One workgroup per pose-pair block (i1, i2): the points with an edge to both, ascending, as (edge of
+// i1, edge of i2) pairs -- build_structure's order; a diagonal block's first members are also the
+// pose's edge list (ps_slot).  Ordered compaction 1024 points at a time (wave ballots + an LDS scan).
+__global__ __launch_bounds__(1024) void ba_struct_pairs_kernel(const int* __restrict__ blk_i1,
+                                                                const int* __restrict__ blk_i2,
+                                                                const int* __restrict__ blk_beg,
+                                                                const int* __restrict__ ps_beg,
+                                                                const int* __restrict__ slot_of, int nl,
+                                                                int2* __restrict__ blk_pair, int* __restrict__ ps_slot) {
+    __shared__ int wsum[16];
+    const int blk = blockIdx.x, i1 = blk_i1[blk], i2 = blk_i2[blk];
+    const int* r1 = slot_of + (long long)i1 * nl;
+    const int* r2 = slot_of + (long long)i2 * nl;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int psd = i1 == i2 ? ps_beg[i1] - blk_beg[blk] : 0;   // ps_slot index - pair index
+    int base = blk_beg[blk];
+    for (int l0 = 0; l0 < nl; l0 += 1024) {
+        const int l = l0 + threadIdx.x;
+        int a = -1, c = -1;
+        if (l < nl) {
+            a = r1[l];
+            c = r2[l];
+        }
+        const bool keep = a >= 0 && c >= 0;
+        const unsigned long long bm = __ballot(keep);
+        if (lane == 0) wsum[wv] = __popcll(bm);
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            const int v = wsum[w];
+            off += w < wv ? v : 0;
+            tot += v;
+        }
+        if (keep) {
+            const int pos = base + off + __popcll(bm & below);
+            blk_pair[pos] = make_int2(a, c);
+            if (i1 == i2) ps_slot[pos + psd] = a;
+        }
+        base += tot;
+        __syncthreads();
+    }
+}
+
+// ---- The same solve, pivot by pivot (round 6; ORBBA_SOLVE=block selects the blocked kernel above).
+// The blocked kernel's critical path is wavefront 0's 16-pivot diagonal factorisation of every block
+// (≈6.6k of ≈11k ticks per block, the other three wavefronts mostly waiting).  Here the whole
+// workgroup takes every pivot: 256 threads as a 16 x 16 grid, thread (ty, tx) holding the
+// lower-triangle entries A(ty + 16a, tx + 16c), c <= a < 8, in registers (the cyclic layout keeps the
+// shrinking trailing matrix spread evenly), one workgroup barrier per pivot:
+//   * column j (published in LDS by its owners at the previous step) is read by every thread: the
+//     multipliers of its rows (ty + 16a) and columns (tx + 16c), the pivot d_j and y_j;
+//   * while those reads are in flight, the previous pivot's rank-1 update runs (deferred);
+//   * then the owners of column j+1 (tx = (j+1) mod 16) apply pivot j to it and publish it, and the
+//     owner of y_{j+1} does the same for the right-hand side (forward substitution folded in):
+//     only this lookahead is on the per-pivot critical path.
+// U (LDS, column-major, stride ld odd) keeps every published column U_{ij} = L_{ij} d_j, so the back
+// substitution x_c = d_c^-1 (z_c - sum_{j>c} U_{jc} x_j) runs on wavefront 0 alone, one pivot per step
+// from the last, x_j broadcast by v_readlane: no barriers.  Block and pivot forms give the same
+// solution up to rounding (tests/test_ba_gpu.py: identical iterations and outliers either way).
+constexpr int SP_NB = 8;   // 16-row blocks: D <= 128
+__host__ __device__ constexpr int sp_ld(int D) { return 16 * ((D + 15) / 16) + 1; }
+__host__ __device__ constexpr size_t sp_lds_doubles(int D) { return (size_t)D * sp_ld(D) + 3 * 128; }
+#define SP_TRI(a, c) ((a) * ((a) + 1) / 2 + (c))
+
+// pivot j-1's update of column K (owners) and of y row K (its owner), ahead of the deferred update
+template <int K>
+__device__ __forceinline__ void sp_col_prev(double (&R)[36], double (&yv)[SP_NB], const double (&crp)[SP_NB],
+                                            const double (&ccp)[SP_NB], double yfp, bool own_col, bool own_y,
+                                            int nb) {
+    if (own_col) {
+#pragma unroll
+        for (int a = K; a < SP_NB; a++)
+            if (a < nb) R[SP_TRI(a, K)] = fma(-crp[a], ccp[K], R[SP_TRI(a, K)]);
+    }
+    if (own_y) yv[K] = fma(-crp[K], yfp, yv[K]);
+}
+// pivot j's update of column K = j+1 and its publication; the same for y_{j+1}
+template <int K>
+__device__ __forceinline__ void sp_col_next(double (&R)[36], double (&yv)[SP_NB], const double (&cr)[SP_NB],
+                                            double ccK, double yf, bool own_col, bool own_y, int nb, int ty,
+                                            double* Ucol, double* yout) {
+    if (own_col) {
+#pragma unroll
+        for (int a = K; a < SP_NB; a++)
+            if (a < nb) {
+                const double v = fma(-cr[a], ccK, R[SP_TRI(a, K)]);
+                R[SP_TRI(a, K)] = v;
+                Ucol[ty + 16 * a] = v;
+            }
+    }
+    if (own_y) {
+        yv[K] = fma(-cr[K], yf, yv[K]);
+        *yout = yv[K];
+    }
+}
+#define SP_SWITCH(cn, CALL)                 \
+    switch (cn) {                           \
+        case 0: CALL(0); break;             \
+        case 1: CALL(1); break;             \
+        case 2: CALL(2); break;             \
+        case 3: CALL(3); break;             \
+        case 4: CALL(4); break;             \
+        case 5: CALL(5); break;             \
+        case 6: CALL(6); break;             \
+        default: CALL(7); break;            \
+    }
+
+__global__ __launch_bounds__(256) void ba_solve_pivot_kernel(BADev b, int D) {
+    BA_RETURN_IF_DONE(b);
+    extern __shared__ __attribute__((aligned(16))) double U[];   // column j at U + j * ld
+    const int nb = (D + 15) >> 4, ld = sp_ld(D);
+    double* ybuf = U + (size_t)D * ld;   // z_j as published (final after pivot j-1)
+    double* dv = ybuf + 128;             // 1 / d_j
+    double* xbuf = dv + 128;             // the solution
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    double q_pre[4] = {0, 0, 0, 0}, t_pre[3] = {0, 0, 0}, bp_pre[6] = {0, 0, 0, 0, 0, 0};
+    if (tid < b.np) {
+        const int id = b.ps_id[tid];
+        for (int j = 0; j < 4; j++) q_pre[j] = b.q[4 * id + j];
+        for (int j = 0; j < 3; j++) t_pre[j] = b.t[3 * id + j];
+        for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
+    }
+    // S's lower triangle straight into registers (36 independent loads per thread)
+    double R[36], yv[SP_NB];
+#pragma unroll
+    for (int a = 0; a < SP_NB; a++) {
+        const int i = ty + 16 * a;
+#pragma unroll
+        for (int c = 0; c <= a; c++) {
+            const int k = tx + 16 * c;
+            R[SP_TRI(a, c)] = (a < nb && i < D && k <= i) ? b.S[i * D + k] : 0.0;
+        }
+        yv[a] = (tx == 0 && a < nb && i < D) ? b.bs[i] : 0.0;
+    }
+    if (tx == 0) {   // column 0 and y_0
+#pragma unroll
+        for (int a = 0; a < SP_NB; a++)
+            if (a < nb) U[ty + 16 * a] = R[SP_TRI(a, 0)];
+        if (ty == 0) ybuf[0] = yv[0];
+    }
+    __syncthreads();
+    double crp[SP_NB], ccp[SP_NB], yfp = 0;   // pivot j-1's multipliers (its deferred update)
+#pragma unroll
+    for (int a = 0; a < SP_NB; a++) crp[a] = ccp[a] = 0;
+    int jbp = 0;   // block of pivot j-1
+    bool ok = true;
+    for (int j = 0; j < D; j++) {
+        const int jb = j >> 4;
+        const double* Uj = U + j * ld;
+        double cr[SP_NB], cc[SP_NB];
+#pragma unroll
+        for (int a = 0; a < SP_NB; a++) {
+            const bool live = a >= jb && a < nb;   // wave-uniform
+            cr[a] = live ? Uj[ty + 16 * a] : 0.0;
+            cc[a] = live ? Uj[tx + 16 * a] : 0.0;
+        }
+        const double dj = Uj[j], yj = ybuf[j];
+        const int jn = j + 1, cn = jn >> 4, tn = jn & 15;
+        const bool own_col = jn < D && tx == tn, own_y = jn < D && tx == 0 && ty == tn;
+        // pivot j-1 on column j+1 and y_{j+1} (their owners), then everywhere else: column j and
+        // y_j already have it (the previous lookahead), columns / rows below the pivot are final
+        if (jn < D) {
+#define SP_PREV(K) sp_col_prev<K>(R, yv, crp, ccp, yfp, own_col, own_y, nb)
+            SP_SWITCH(cn, SP_PREV)
+#undef SP_PREV
+        }
+#pragma unroll
+        for (int c = 0; c < SP_NB; c++) {
+            if ((c == cn && tx == tn) || (c == jb && tx == (j & 15))) ccp[c] = 0.0;
+            if ((c == cn && ty == tn) || (c == jb && ty == (j & 15))) crp[c] = 0.0;
+        }
+#pragma unroll
+        for (int a = 0; a < SP_NB; a++) {
+            if (a >= jbp && a < nb) {   // wave-uniform
+#pragma unroll
+                for (int c = 0; c <= a; c++)
+                    if (c >= jbp) R[SP_TRI(a, c)] = fma(-crp[a], ccp[c], R[SP_TRI(a, c)]);
+                yv[a] = fma(-crp[a], yfp, yv[a]);
+            }
+        }
+        // pivot j
+        ok = ok && dj != 0 && isfinite(dj);
+        const double inv = rcp_d(dj), yf = inv * yj;
+        if (jn < D) {
+            double ccn = 0;
+#pragma unroll
+            for (int c = 0; c < SP_NB; c++) ccn = c == cn ? cc[c] : ccn;
+            ccn *= inv;
+#define SP_NEXT(K) sp_col_next<K>(R, yv, cr, ccn, yf, own_col, own_y, nb, ty, U + jn * ld, ybuf + jn)
+            SP_SWITCH(cn, SP_NEXT)
+#undef SP_NEXT
+        }
+        if (tid == 0) dv[j] = inv;
+#pragma unroll
+        for (int a = 0; a < SP_NB; a++) {
+            crp[a] = cr[a];
+            ccp[a] = cc[a] * inv;
+        }
+        yfp = yf;
+        jbp = jb;
+        __syncthreads();
+    }
+    // back substitution on wavefront 0: lane l holds columns l and l + 64
+    if (tid < 64) {
+        const int l = tid, l0 = min(l, D - 1), l1 = min(l + 64, D - 1);   // (clamped: reads stay inside U)
+        double acc0 = 0, acc1 = 0, x0 = 0, x1 = 0;
+        for (int j = D - 1; j >= 0; j--) {
+            const double accj = j >= 64 ? readlane_d(acc1, j - 64) : readlane_d(acc0, j);
+            const double xj = dv[j] * (ybuf[j] - accj);
+            if (j >= 64) x1 = l == j - 64 ? xj : x1;
+            else x0 = l == j ? xj : x0;
+            acc0 = fma(U[l0 * ld + j], xj, acc0);   // U_{j,l} (garbage for l >= j: those x are final)
+            acc1 = fma(U[l1 * ld + j], xj, acc1);
+        }
+        if (l < D) xbuf[l] = x0;
+        if (l + 64 < D) xbuf[l + 64] = x1;
+    }
+    __syncthreads();
+    for (int i = tid; i < D; i += blockDim.x) b.x[i] = ok ? xbuf[i] : 0.0;
+    if (tid == 0) b.ctl->ok2 = ok;
+    const double lam = b.ctl->lambda;
+    if (tid < b.np) {   // push() + oplus for the free poses, scale terms x.(lambda x + b)
+        const int i = tid;
+        const int id = b.ps_id[i];
+        double xi[6], part = 0;
+        for (int j = 0; j < 6; j++) {
+            xi[j] = ok ? xbuf[6 * i + j] : 0.0;
+            part += xi[j] * (lam * xi[j] + bp_pre[j]);
+        }
+        b.part[b.nl + i] = part;
+        for (int j = 0; j < 4; j++) b.q_sv[4 * id + j] = q_pre[j];
+        for (int j = 0; j < 3; j++) b.t_sv[3 * id + j] = t_pre[j];
+        se3_exp_update(xi, q_pre, t_pre);
+        for (int j = 0; j < 4; j++) b.q[4 * id + j] = q_pre[j];
+        for (int j = 0; j < 3; j++) b.t[3 * id + j] = t_pre[j];
+    }
+}
+
 // The same blocked LDL^T for reduced systems too large for LDS (more than 21 free keyframes, D > 128;
 // the reference's window is every covisible keyframe, Optimizer.cc:494-504, with no upper bound).
 // The padded system lives in HBM / L2 (b.Sg, row stride Dp+1); y, D^-1 and the forward-substitution
@@ -1660,15 +1913,20 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     bool have_structure = false;
     bool have_classified = false;   // the outlier classification ran (second optimize())
     auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
+        bool dev_build = false;   // act / pt_slot / ps_slot / blk_pair filled on the device
         if (!have_structure) {
-            static const bool sorted_build = [] {
-                const char* e = getenv("ORBBA_STRUCT");
-                return e && std::string(e) == "sorted";
-            }();
-            build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs, sorted_build);
-            mark("build_structure");
+            // ORBBA_STRUCT: "host" = the whole build on the host (generic), "sorted" = the host's
+            // point-sorted variant; default: counts on the host, lists on the device when the edges
+            // are point-sorted (read per call: tests compare the forms in one process)
+            const char* sm = getenv("ORBBA_STRUCT");
+            const std::string mode = sm ? sm : "";
+            dev_build = mode != "host" && mode != "sorted" && mode != "generic" &&
+                        build_structure_counts(P, N, pr->pose_fixed, pr->edge_point, pr->edge_pose, E, hs);
+            if (!dev_build)
+                build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs, mode == "sorted");
+            mark(dev_build ? "build_structure (counts)" : "build_structure");
         }
-        const int Ea = (int)hs.act.size(), np = hs.np, nl = hs.nl, D = 6 * np;
+        const int Ea = hs.n_act, np = hs.np, nl = hs.nl, D = 6 * np;
         const int nblk = (int)hs.blk_i1.size();
         *iters_out = 0;
         *chi_out = 0;
@@ -1677,16 +1935,24 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (Ea == 0 || np + nl == 0) return ORB_OK;
         // reduced system: in LDS up to 21 free keyframes (D <= 128), else in HBM (ba_solve_global_kernel)
         const bool glob = D > 128 || solve_lds_doubles(D) * 8 + 4096 > 160 * 1024;
+        // the pivot-wise solve (default) or the blocked one (ORBBA_SOLVE=block), both in LDS
+        // (read per call: tests compare the forms in one process)
+        const bool pivot_solve = [] {
+            const char* e = getenv("ORBBA_SOLVE");
+            return !(e && std::string(e) == "block");
+        }();
         if (glob && np > ORBBA_MAX_FREE_KEYFRAMES) {
             set_error("LocalBA: more than ORBBA_MAX_FREE_KEYFRAMES free keyframes in the local window");
             return ORB_EINVAL;
         }
         const int Dp = solve_dp(D);
         // structure upload
-        const size_t sbytes = carve_size<int>(Ea) + carve_size<int>(P) + carve_size<int>(N) + carve_size<int>(nl + 1) +
-                              carve_size<int>(Ea) + carve_size<int>(nl) + carve_size<int>(np + 1) +
-                              carve_size<int>(hs.ps_slot.size()) + carve_size<int>(np) + carve_size<int>(nblk) * 2 +
-                              carve_size<int>(nblk + 1) + carve_size<int2>(hs.blk_pair.size()) + carve_size<int>(np);
+        const size_t nps = (size_t)hs.n_ps, npairs = (size_t)hs.n_pairs;
+        const size_t sbytes = carve_size<int>(P) + carve_size<int>(N) + carve_size<int>(nl + 1) + carve_size<int>(nl) +
+                              carve_size<int>(np + 1) + carve_size<int>(np) + carve_size<int>(nblk) * 2 +
+                              carve_size<int>(nblk + 1) + carve_size<int>(np) + carve_size<int>(Ea) * 2 +
+                              carve_size<int>(nps) + carve_size<int2>(npairs) +
+                              (dev_build ? carve_size<int>((size_t)np * nl) : 0);
         int rc2;
         if (!have_structure) {
         if ((rc2 = C.structure.reserve(sbytes))) return rc2;
@@ -1695,39 +1961,54 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         auto put = [&](const void* src, size_t n, char* hdst) {
             if (n) std::memcpy(hdst, src, n);
         };
-        int* d_act = cr.take<int>(Ea);
+        // the host-built arrays first (the device build uploads only these), then the four lists
         int* d_hp = cr.take<int>(P);
         int* d_hl = cr.take<int>(N);
         int* d_ptb = cr.take<int>(nl + 1);
-        int* d_pts = cr.take<int>(Ea);
         int* d_pti = cr.take<int>(nl);
         int* d_psb = cr.take<int>(np + 1);
-        int* d_pss = cr.take<int>(hs.ps_slot.size());
         int* d_psi = cr.take<int>(np);
         int* d_b1 = cr.take<int>(nblk);
         int* d_b2 = cr.take<int>(nblk);
         int* d_bb = cr.take<int>(nblk + 1);
-        int2* d_bp = cr.take<int2>(hs.blk_pair.size());
         int* d_bd = cr.take<int>(np);
-        put(hs.act.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
+        const size_t small_bytes = cr.off;
+        int* d_act = cr.take<int>(Ea);
+        int* d_pts = cr.take<int>(Ea);
+        int* d_pss = cr.take<int>(nps);
+        int2* d_bp = cr.take<int2>(npairs);
         put(hs.hp.data(), 4 * (size_t)P, (char*)hr.take<int>(P));
         put(hs.hl.data(), 4 * (size_t)N, (char*)hr.take<int>(N));
         put(hs.pt_beg.data(), 4 * (size_t)(nl + 1), (char*)hr.take<int>(nl + 1));
-        put(hs.pt_slot.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
         put(hs.pt_id.data(), 4 * (size_t)nl, (char*)hr.take<int>(nl));
         put(hs.ps_beg.data(), 4 * (size_t)(np + 1), (char*)hr.take<int>(np + 1));
-        put(hs.ps_slot.data(), 4 * hs.ps_slot.size(), (char*)hr.take<int>(hs.ps_slot.size()));
         put(hs.ps_id.data(), 4 * (size_t)np, (char*)hr.take<int>(np));
         put(hs.blk_i1.data(), 4 * (size_t)nblk, (char*)hr.take<int>(nblk));
         put(hs.blk_i2.data(), 4 * (size_t)nblk, (char*)hr.take<int>(nblk));
         put(hs.blk_beg.data(), 4 * (size_t)(nblk + 1), (char*)hr.take<int>(nblk + 1));
-        put(hs.blk_pair.data(), 8 * hs.blk_pair.size(), (char*)hr.take<int2>(hs.blk_pair.size()));
         {
             int* bd = hr.take<int>(np);
             for (int k = 0; k < nblk; k++)
                 if (hs.blk_i1[k] == hs.blk_i2[k]) bd[hs.blk_i1[k]] = k;
         }
-        ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, cr.off, hipMemcpyHostToDevice, st));
+        if (dev_build) {
+            int* d_slot = cr.take<int>((size_t)np * nl);
+            ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, small_bytes, hipMemcpyHostToDevice, st));
+            if (np && nl) ORB_HIP_TRY(hipMemsetAsync(d_slot, 0xff, 4 * (size_t)np * nl, st));
+            if (Ea)
+                hipLaunchKernelGGL(ba_struct_slots_kernel, dim3((Ea + 255) / 256), dim3(256), 0, st, d_ep, d_ek, d_hp, d_hl,
+                                   Ea, nl, d_act, d_pts, d_slot);
+            if (nblk && nl)
+                hipLaunchKernelGGL(ba_struct_pairs_kernel, dim3(nblk), dim3(1024), 0, st, d_b1, d_b2, d_bb, d_psb, d_slot, nl,
+                                   d_bp, d_pss);
+            ORB_HIP_TRY(hipGetLastError());
+        } else {
+            put(hs.act.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
+            put(hs.pt_slot.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
+            put(hs.ps_slot.data(), 4 * nps, (char*)hr.take<int>(nps));
+            put(hs.blk_pair.data(), 8 * npairs, (char*)hr.take<int2>(npairs));
+            ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, cr.off, hipMemcpyHostToDevice, st));
+        }
         b.Ea = Ea; b.np = np; b.nl = nl; b.nblk = nblk;
         b.act = d_act; b.hp = d_hp; b.hl = d_hl; b.pt_beg = d_ptb; b.pt_slot = d_pts; b.pt_id = d_pti;
         b.ps_beg = d_psb; b.ps_slot = d_pss; b.ps_id = d_psi; b.blk_i1 = d_b1; b.blk_i2 = d_b2; b.blk_beg = d_bb;
@@ -1766,16 +2047,21 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
         if (nblk) ORB_HIP_TRY(hipMemsetAsync(b.blk_done, 0, (size_t)nblk * 4, st));
-        const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
+        const size_t ldlt_lds = glob          ? (size_t)3 * Dp * 8
+                                : pivot_solve ? std::max<size_t>(sp_lds_doubles(D) * 8, 16)
+                                              : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
         {   // the dynamic LDS limit is a process-wide attribute of the kernel: raised (a host call) only
             // when a call needs more than any call before it on this device, never lowered
             static std::mutex mu;
-            static size_t lim[64][2] = {};
+            static size_t lim[64][3] = {};
             const size_t need = std::max<size_t>(ldlt_lds, 1024);
             std::lock_guard<std::mutex> lk(mu);
-            size_t& cur = lim[device & 63][glob ? 1 : 0];
+            const int kind = glob ? 1 : pivot_solve ? 2 : 0;
+            size_t& cur = lim[device & 63][kind];
             if (need > cur) {
-                ORB_HIP_TRY(hipFuncSetAttribute(glob ? (const void*)ba_solve_global_kernel : (const void*)ba_solve_kernel,
+                ORB_HIP_TRY(hipFuncSetAttribute(glob ? (const void*)ba_solve_global_kernel
+                                                : pivot_solve ? (const void*)ba_solve_pivot_kernel
+                                                              : (const void*)ba_solve_kernel,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
                 cur = need;
             }
@@ -1803,6 +2089,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 }
                 hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1 + np, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
                 if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
+                else if (pivot_solve) hipLaunchKernelGGL(ba_solve_pivot_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
                 else hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
                 const int slot = enq % LOOKAHEAD;
                 C.step_seq = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;

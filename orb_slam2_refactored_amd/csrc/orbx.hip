@@ -1329,7 +1329,13 @@ __device__ __forceinline__ void crop_stage_rows(const CropSrc& c, int lane, uint
 // CST / ZST: the crop and zone-map row strides when known at compile time (the C1-C3 geometries:
 // 48 / 36 and 52 / 40), so every LDS address off a row base folds into the instruction's offset
 // field; 0 = read them from FastLds (any other geometry).
-template <int CST, int ZST>
+// PAIR (round 6, ORBX_FAST_PAIR=1): two vertically consecutive cells of the strip per pass, as one
+// merged zone (one crop of zhA + zhB + 6 rows, one zone map with a zero separator row between the
+// cells so the 3x3 NMS stays cell-local, one set of rings): the end-of-cell partial drains, partial
+// strength batches, NMS chunks and emission loops happen once per pair instead of once per cell.
+// Counts, the iniThFAST / minThFAST choice (:527-530), the slot capacity and the output stay per cell;
+// a speculative pass is kept only when both cells keep an iniThFAST corner.
+template <int CST, int ZST, bool PAIR>
 __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, const CellDev* __restrict__ cells,
                                                         const int2* __restrict__ strips,
                                                         const uint8_t* __restrict__ in, long long in_fstride,
@@ -1387,12 +1393,25 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // whether to speculate, never the result.
     const int spec_min = spec_arg < 0 ? spec_arg : spec_arg & 0x1fffffff;
     int prev_ini = (spec_arg > 0 && ((spec_arg >> 29) & 1) && sd.y < 0) ? spec_min : 0;
-    for (int item = i_beg; item < i_end; item++) {
+    for (int item = i_beg; item < i_end; item += PAIR ? 2 : 1) {
     CellDev cell;
     int ci;
-    const CropSrc src = source(item, cell, ci);
+    CropSrc src = source(item, cell, ci);
     const int x0 = src.x0, y0 = src.y0;
-    const int zh = cell.zwzh >> 16;
+    const int zhA = cell.zwzh >> 16;
+    // PAIR: the second cell (the one below; zhB = 0 when the strip has an odd count) extends the zone
+    const bool hasB = PAIR && item + 1 < i_end;
+    CellDev cellB = cell;
+    int ciB = ci, zhB = 0;
+    if (hasB) {
+        ciB = ci + cstride;
+        cellB = cells[ciB];
+        zhB = cellB.zwzh >> 16;
+        src.ch += zhB;
+    }
+    const int zh = zhA + zhB;
+    // zone-map row of zone row y: PAIR inserts a zero row between the cells
+    auto mrow = [&](int y) { return PAIR ? y + (y >= zhA ? 1 : 0) : y; };
     {
         crop_stage_rows<CST>(src, lane, crop, CSd);
     }
@@ -1400,10 +1419,11 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     bool spec = spec_min != 0 && th_ini > tlo && prev_ini >= spec_min;   // spec_min < 0: every cell
     uint8_t* Mc = Mz + ZSd + 1;   // zone (0, 0); the zero border makes out-of-zone neighbours read 0
     uint32_t* out = slots + (long long)f * g.slot_frame + cell.slot;
-    const int cap = ((zw + 1) / 2) * ((zh + 1) / 2);
+    const int cap = ((zw + 1) / 2) * ((zhA + 1) / 2);
     int n_ini = 0, n_min = 0, total = 0;
+    int n_iniB = 0, totalB = 0;   // PAIR: the second cell
     for (;;) {   // passes: speculative (iniThFAST) and / or full (min(ini, min))
-    for (int i = lane; i < ((zh + 2) * ZSd + 15) >> 4; i += 64) reinterpret_cast<uint4*>(Mz)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = lane; i < ((zh + 2 + (PAIR ? 1 : 0)) * ZSd + 15) >> 4; i += 64) reinterpret_cast<uint4*>(Mz)[i] = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
     if (item == i_beg) FAST_STAMP(1, __builtin_amdgcn_s_memtime());
 
@@ -1440,14 +1460,16 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         if (c) {
             const int pos = nc + rank64(bm);
             if (pos < fl.ccap) clist[pos] = (short)i;   // past ccap: the cell takes the zone-scan NMS below
-            Mc[__mul24(i >> 8, ZSd) + (i & 255)] = (uint8_t)min(M, 255);
+            Mc[__mul24(mrow(i >> 8), ZSd) + (i & 255)] = (uint8_t)min(M, 255);
         }
         nc += popc64(bm);
         h2 += n;
     };
     auto drain = [&](int n) {
         const uint32_t e = lane < n ? gring[(head + lane) & (GR_RING - 1)] : 0u;   // 0: no pass bits
-        const int i0 = (int)((e >> 2) & 0x3fffu);
+        // zone index (y << 8) | x; PAIR: stored as (y << 6) | x at bits 18-30 (merged zones are taller
+        // than the 64 rows bits 2-15 hold)
+        const int i0 = PAIR ? (int)(((e >> 24) << 8) | ((e >> 18) & 63u)) : (int)((e >> 2) & 0x3fffu);
         const uint8_t* c = crop + __mul24((i0 >> 8) + 3, CSd) + 4 + (i0 & 255);   // zone (y, x): dword aligned
         const uint32_t* cp = reinterpret_cast<const uint32_t*>(c + 2 * CSd);
         const uint32_t* cm = reinterpret_cast<const uint32_t*>(c - 2 * CSd);
@@ -1482,7 +1504,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
     // per-lane LDS address of zone (qy, qx) = crop (qy+3, qx+3) at byte qx+4 and the group's zone index
     // (qy << 8) | qx at bits 2-15, both stepped by a wave-uniform amount per chunk of RPC rows
     const uint8_t* rowq = crop + __mul24(qy + 3, CSd) + 4 + qx;
-    const uint32_t e0s = (uint32_t)((qy << 8) | qx) << 2;
+    const uint32_t e0s = PAIR ? (uint32_t)((qy << 6) | qx) << 18 : (uint32_t)((qy << 8) | qx) << 2;
     const bool qxin = qx < zw;
     for (int yb = 0, yoff = 0; yb < zh; yb += RPC, yoff += RPC * CSd) {
         const int y = yb + qy;
@@ -1513,7 +1535,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
         if (any) {
             // ring slot = qn + the passers of the lower lanes (mbcnt accumulates qn)
             const unsigned pos = __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, (unsigned)qn));
-            gring[pos & (GR_RING - 1)] = bt3<BT_OR3>(us2u(pe), us2u(po) + us2u(po), e0s + ((uint32_t)yb << 10));
+            gring[pos & (GR_RING - 1)] = bt3<BT_OR3>(us2u(pe), us2u(po) + us2u(po), e0s + ((uint32_t)yb << (PAIR ? 24 : 10)));
         }
         qn += popc64(bm);
         wave_lds_sync();
@@ -1526,7 +1548,72 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
 
     n_ini = 0;
     n_min = 0;
-    if (nc > fl.ccap) {
+    if constexpr (PAIR) {
+        // Both cells' NMS in one walk (the list, or the zone map row by row for dense pairs), with a
+        // third ballot per chunk marking the first cell's entries (row-major: a prefix), then each
+        // cell's emission from its own threshold's ballots.  Ballots: 3 words per chunk / pass.
+        const bool dense = nc > fl.ccap;
+        const int rsh = zw <= 32 ? 5 : 6, RP = 64 >> rsh;
+        const int zx = lane & ((1 << rsh) - 1), zr = lane >> rsh;
+        unsigned long long* pb = dense ? reinterpret_cast<unsigned long long*>(queue) : bal;
+        int nm_b = 0, nch = 0;
+        const int nsteps = dense ? (zh + RP - 1) / RP : (nc + 63) >> 6;
+        for (; nch < nsteps; nch++) {
+            bool ki = false, km = false, inA = false;
+            int y = -1, x = 0;
+            if (dense) {
+                if (zx < zw && zr + nch * RP < zh) { y = zr + nch * RP; x = zx; }
+            } else if (nch * 64 + lane < nc) {
+                const int i = clist[nch * 64 + lane];
+                y = i >> 8;
+                x = i & 255;
+            }
+            if (y >= 0) {
+                inA = y < zhA;
+                const uint8_t* c0 = Mc + __mul24(mrow(y), ZSd) + x;
+                const int m = c0[0];
+                if (m) {
+                    const int n0 = max(max((int)c0[-ZSd - 1], (int)c0[-ZSd]), (int)c0[-ZSd + 1]);
+                    const int n1 = max((int)c0[-1], (int)c0[1]);
+                    const int n2 = max(max((int)c0[ZSd - 1], (int)c0[ZSd]), (int)c0[ZSd + 1]);
+                    const bool top = max(max(n0, n1), n2) < m;
+                    ki = top && m > th_ini;
+                    km = top && m > th_min;
+                }
+            }
+            const unsigned long long bi = __ballot(ki), bmn = __ballot(km), ba = __ballot(inA);
+            if (lane == 0) { pb[3 * nch] = bi; pb[3 * nch + 1] = bmn; pb[3 * nch + 2] = ba; }
+            n_ini += popc64(bi & ba);
+            n_min += popc64(bmn & ba);
+            n_iniB += popc64(bi & ~ba);
+            nm_b += popc64(bmn & ~ba);
+        }
+        wave_lds_sync();
+        if (spec && (n_ini == 0 || (hasB && n_iniB == 0))) goto full_pass;
+        const int wA = n_ini > 0 ? 0 : 1, wB = n_iniB > 0 ? 0 : 1;
+        total = wA == 0 ? n_ini : n_min;
+        totalB = wB == 0 ? n_iniB : nm_b;
+        uint32_t* outB = slots + (long long)f * g.slot_frame + cellB.slot;
+        const int capB = ((zw + 1) / 2) * ((zhB + 1) / 2);
+        const unsigned long long below = lanemask_lt();
+        int runA = 0, runB = 0;
+        for (int p = 0; p < nch; p++) {
+            const unsigned long long ba = pb[3 * p + 2];
+            const unsigned long long kA = pb[3 * p + wA] & ba, kB = pb[3 * p + wB] & ~ba;
+            if (((kA | kB) >> lane) & 1) {
+                const bool a = (kA >> lane) & 1;
+                const int r = a ? runA + popc64(kA & below) : runB + popc64(kB & below);
+                int y, x;
+                if (dense) { y = zr + p * RP; x = zx; }
+                else { const int i = clist[p * 64 + lane]; y = i >> 8; x = i & 255; }
+                if (r < (a ? cap : capB))
+                    (a ? out : outB)[r] = (uint32_t)(x0 + 3 + x) | ((uint32_t)(y0 + 3 + y) << 12) |
+                                          ((uint32_t)(Mc[__mul24(mrow(y), ZSd) + x] - 1) << 24);
+            }
+            runA += popc64(kA);
+            runB += popc64(kB);
+        }
+    } else if (nc > fl.ccap) {
         // Dense cell (more corners than the list holds, e.g. pure noise): NMS over the zone map in
         // row-major order, one zone row per pass (zw <= 64), the same keep rule: a corner is kept
         // at threshold t iff M > t and every neighbour is < M (for M > t, a neighbour q >= M is
@@ -1622,13 +1709,18 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
 full_pass:   // the speculative pass kept no corner at iniThFAST: the full pass decides
     spec = false;
     }   // passes
-    prev_ini = n_ini;
+    prev_ini = hasB ? n_iniB : n_ini;
     if (item == i_beg) FAST_STAMP(4, __builtin_amdgcn_s_memtime());
     if (lane == 0) {
         if (total > cap) atomicOr(fault, FAULT_CELL_CAP);
         // bit 30: this cell kept >= spec_min corners at iniThFAST (the next strips' first-cell hint;
         // the quadtree masks the count with CELL_CNT_MASK)
         cell_cnt[(long long)f * g.ncells_total + ci] = min(total, cap) | (n_ini >= spec_min ? CELL_CNT_INI : 0);
+        if (hasB) {
+            const int capB = ((zw + 1) / 2) * ((zhB + 1) / 2);
+            if (totalB > capB) atomicOr(fault, FAULT_CELL_CAP);
+            cell_cnt[(long long)f * g.ncells_total + ciB] = min(totalB, capB) | (n_iniB >= spec_min ? CELL_CNT_INI : 0);
+        }
     }
     if (item == i_beg) {
         FAST_STAMP(2, __builtin_amdgcn_s_memtime());
@@ -3331,6 +3423,8 @@ struct orbx_extractor {
     // a cell runs the speculative iniThFAST pass when the wavefront's previous cell kept at least
     // fast_spec corners at iniThFAST (texture-rich regions); 0 = never (ORBX_FAST_SPEC)
     int fast_spec = 8;
+    int fast_pair = 0;      // ORBX_FAST_PAIR=1: fast_cells_kernel<..., PAIR> (two cells per pass; round 6)
+    bool fast_pair_on = false;   // requested and the geometry allows it (consecutive strip cells adjacent)
     // a strip's first cell (no predecessor) speculates when its cell kept >= fast_spec corners in frame 0
     // (cell_cnt's frame-0 slot; ORBX_FAST_SPEC_FIRST=0: never)
     int fast_spec_first = 1;
@@ -3378,7 +3472,7 @@ struct orbx_extractor {
     size_t last_step = 0;
     int last_frames = 0;
     // dense describe grid (DescGrid): slots per frame from the previous batch's largest total
-    int desc_dense = 1;         // ORBX_DESC_DENSE=0: the slot-table grid (out_frame slots per frame)
+    int desc_dense = 0;         // ORBX_DESC_DENSE=1: the dense grid (measured no faster, DESIGN §4 describe round 6)
     int desc_force_c = 0;       // test hook (ORBX_DESC_C): this C for every batch (exercises the overflow kernel)
     int desc_c = 0;             // C of the next batch (0: unknown, out_frame)
     DevBuf d_dstat;             // stat[0] = the batch's largest frame total (describe_prefix_kernel)
@@ -3685,18 +3779,38 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
             set_error("FAST cell larger than the kernel supports");
             return ORB_EINTERNAL;
         }
+        // PAIR: every strip's consecutive cells adjacent (zone B starts where zone A ends, same x0), the
+        // merged zone's rows within the 7 bits of the pair encoding, and a dense pair's 3 ballot words
+        // per pass within the drained ring
+        h->fast_pair_on = false;
+        if (h->fast_pair) {
+            bool ok = 2 * mzh < 128 && 24 * ((2 * mzh + 1) / (mzw <= 32 ? 2 : 1) + 1) <= 2 * (2 * GR_RING + FQ2_RING);
+            for (int l = 0; l < g.nlevels && ok; l++) {
+                const LevelDev& L = g.lv[l];
+                if (L.ncells <= 0) continue;
+                int ncx = 0;   // cells per grid row (the strips' cell stride)
+                while (ncx < L.ncells && (cells[L.cell_base + ncx].x0y0 >> 16) == (cells[L.cell_base].x0y0 >> 16)) ncx++;
+                for (int c = L.cell_base; c + ncx < L.cell_base + L.ncells && ok; c++) {
+                    const CellDev &A = cells[c], &B = cells[c + ncx];
+                    ok = (A.x0y0 & 0xffff) == (B.x0y0 & 0xffff) && (B.x0y0 >> 16) == (A.x0y0 >> 16) + (A.zwzh >> 16);
+                }
+            }
+            h->fast_pair_on = ok;
+        }
+        const int zrows = h->fast_pair_on ? 2 * mzh + 1 : mzh;   // zone rows per pass (+ the separator)
         FastLds fl;
         fl.CS = (int)align_up(mzw + 6 + 8, 4);         // +1 shift, +4 dword over-read each side
         if (fl.CS < 4 * ((mzw + 6 + 1 + 3) / 4)) fl.CS = 4 * ((mzw + 6 + 1 + 3) / 4);
         fl.ZS = (int)align_up(mzw + 2, 4);             // zone map with a zero border of 1
         // rows: the tallest crop + slack, and at least the CROP_NG row groups of 4 rows the staging's first
         // batch always stores
-        fl.crop_bytes = (int)align_up((size_t)fl.CS * std::max(mzh + 6 + FAST_CROP_SLACK, 4 * CROP_NG), 16);
-        fl.mz_bytes = (int)align_up((size_t)fl.ZS * (mzh + 2), 16);
+        fl.crop_bytes = (int)align_up((size_t)fl.CS * std::max(zrows + 6 + FAST_CROP_SLACK, 4 * CROP_NG), 16);
+        fl.mz_bytes = (int)align_up((size_t)fl.ZS * (zrows + 2), 16);
         fl.qcap = 2 * GR_RING + FQ2_RING;   // in u16 entries
         fl.ccap = std::min(FAST_CLIST_CAP, (int)align_up((size_t)mzw * mzh, 8));
         const int nbal = (fl.ccap + 63) / 64;
-        h->fast_lds = (size_t)fl.crop_bytes + fl.mz_bytes + 2 * (size_t)(fl.qcap + fl.ccap) + 16 * (size_t)nbal;
+        h->fast_lds = (size_t)fl.crop_bytes + fl.mz_bytes + 2 * (size_t)(fl.qcap + fl.ccap) +
+                      (h->fast_pair_on ? 24 : 16) * (size_t)nbal;
         h->fl = fl;
     }
     h->NC = NC;
@@ -3782,9 +3896,12 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
         const int sb = h->strip_beg[l0], ns = h->strip_beg[l1] - sb;
         if (ns <= 0) return;
         const FastLds& fl = h->fl;
-        auto kern = fl.CS == 48 && fl.ZS == 36   ? fast_cells_kernel<48, 36>
-                    : fl.CS == 52 && fl.ZS == 40 ? fast_cells_kernel<52, 40>
-                                                 : fast_cells_kernel<0, 0>;
+        auto kern = h->fast_pair_on ? (fl.CS == 48 && fl.ZS == 36   ? fast_cells_kernel<48, 36, true>
+                                       : fl.CS == 52 && fl.ZS == 40 ? fast_cells_kernel<52, 40, true>
+                                                                    : fast_cells_kernel<0, 0, true>)
+                                    : (fl.CS == 48 && fl.ZS == 36   ? fast_cells_kernel<48, 36, false>
+                                       : fl.CS == 52 && fl.ZS == 40 ? fast_cells_kernel<52, 40, false>
+                                                                    : fast_cells_kernel<0, 0, false>);
         launch_timed(h, 1, kern, dim3((unsigned)(ns * F)), dim3(64), (uint32_t)h->fast_lds, s,
                            g, h->d_cells.as<CellDev>(), h->d_strips.as<int2>(), d_imgs, fstride, step, pyr, h->p.iniThFAST,
                            h->p.minThFAST, slots, cellcnt, fault, h->fl, sb, ns,
@@ -4006,6 +4123,7 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     h->device = device;
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(-1, atoi(e));   // -1: every cell
+    if (const char* e = getenv("ORBX_FAST_PAIR")) h->fast_pair = atoi(e) != 0;
     if (const char* e = getenv("ORBX_FAST_SPEC_FIRST")) h->fast_spec_first = atoi(e) != 0;
 
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));

@@ -344,22 +344,24 @@ def test_batch_status_clean_and_induced_fault():
     assert (cnt.cpu().numpy() <= ex.max_keypoints(720, 1280)).all()
 
 
-@pytest.mark.parametrize("env", [("ORBX_DESC_DENSE", "0"), ("ORBX_DESC_C", "64"), ("ORBX_DESC_C", "1000")])
+@pytest.mark.parametrize("env", [{"ORBX_DESC_DENSE": "1"}, {"ORBX_DESC_DENSE": "1", "ORBX_DESC_C": "64"},
+                                 {"ORBX_DESC_DENSE": "1", "ORBX_DESC_C": "1000"}])
 def test_describe_grids_equal(env):
-    """describe's grids give identical output: the dense grid (slot = output row, C from the previous
-    batch's largest total) against the slot-table grid (ORBX_DESC_DENSE=0), and a forced small C
+    """describe's grids give identical output: the dense grid (ORBX_DESC_DENSE=1: slot = output row, C
+    from the previous batch's largest total) against the default slot-table grid, and a forced small C
     (ORBX_DESC_C) that sends most rows through describe_overflow_kernel."""
     import os
     import torch
     frames = torch.from_numpy(np.stack([synth_image(60 + i, 1280, 720) for i in range(6)])).cuda()
     ref = ORBextractor(ORBextractor.Parameters(2000))
-    for _ in range(2):   # the second batch runs the dense grid sized from the first
+    for _ in range(2):
         r = [t.cpu().numpy() for t in ref.extract_batch_device(frames)]
-    os.environ[env[0]] = env[1]
+    os.environ.update(env)
     try:
         alt = ORBextractor(ORBextractor.Parameters(2000))
     finally:
-        del os.environ[env[0]]
+        for k in env:
+            del os.environ[k]
     for _ in range(2):
         a = [t.cpu().numpy() for t in alt.extract_batch_device(frames)]
     assert ref.batch_status() == 0 and alt.batch_status() == 0

@@ -14,6 +14,7 @@
 #            call's host-side phase times (ORBBA_DEBUG_TIMING=1)
 #   kb_sweep tools/kbench.py on pan frames at 64 .. 2048 frames per launch (per-frame stage times)
 #   stereo   tests/test_stereo_gpu.py      batests  tests/test_ba_gpu.py + tests/test_cpp_dropin_gpu.py
+#   pyt      pytest on $PYT_FILES (-m gpu -x -q)
 #   pmc_pan | pmc_tex   instruction counters (tools/pmc_groups_inst.txt) on 1024 pan / textured frames, and the
 #            per-cell / per-wavefront counts (tools/pmc_percell.py) -> gpurun_out/pmci_{pan,textured}/
 #
@@ -70,6 +71,9 @@ for step in "$@"; do
   batests)
     timeout -k 10 300 $PYT tests/test_ba_gpu.py tests/test_cpp_dropin_gpu.py -q > gpurun_out/pytest_ba.log 2>&1 || { tail -30 gpurun_out/pytest_ba.log; exit 2; }
     tail -2 gpurun_out/pytest_ba.log ;;
+  pyt)
+    timeout -k 10 600 $PYT $PYT_FILES -m gpu -x -q > gpurun_out/pytest_pyt.log 2>&1 || { tail -30 gpurun_out/pytest_pyt.log; exit 2; }
+    tail -2 gpurun_out/pytest_pyt.log ;;
   stereo)
     timeout -k 10 300 $PYT tests/test_stereo_gpu.py -q > gpurun_out/pytest_stereo.log 2>&1 || { tail -30 gpurun_out/pytest_stereo.log; exit 2; }
     tail -2 gpurun_out/pytest_stereo.log ;;
