@@ -822,8 +822,16 @@ __device__ __forceinline__ void solve_trailing_tile_g(double* A, int ld, int J0,
 //   (lookahead), while wavefronts 1-3 update every other trailing tile.
 // Back substitution runs on wavefront 0 alone: x_J = Linv_JJ^T t_J, then t_c -= sum_i L_ic x_i for
 // all earlier columns c (right-looking), block by block from the last.
-__global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
+// NT threads (round 6: 1024 by default, ORBBA_SOLVE_THREADS=256 the round-5 form): wavefront 0 as
+// above; the other NT/64 - 1 wavefronts load S, take the panels and the trailing tiles -- with 15 of
+// them instead of 3, the lookahead phase of an early block (up to 28 trailing tiles) no longer
+// outlasts wavefront 0's diagonal factorisation.  The trailing tiles go to the wavefronts that do
+// not share wavefront 0's SIMD first (waves w with w % 4 != 0; a workgroup's waves are dealt to the
+// SIMDs in turn), so the diagonal chain keeps its SIMD's issue slots.
+template <int NT>
+__global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D) {
     BA_RETURN_IF_DONE(b);
+    constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) double A[];   // Dp x ld
     const int Dp = solve_dp(D), ld = Dp + 1;
     double* y = A + (size_t)Dp * ld;   // rhs -> z -> D^-1 z -> x
@@ -871,18 +879,18 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
         BA_STAMPW(0);
         if (!solve_diag_block(A, y, dinv, vz, ld, 0, lane, D) && lane == 0) s_ok = 0;
     } else {
-        constexpr int RQ = 38;   // rows per wavefront: 3 x 38 >= 128 - 16
+        constexpr int RQ = (128 - SB + NW - 2) / (NW - 1);   // rows per wavefront: (NW-1) x RQ >= 128 - 16
         const int r0 = SB + wv - 1;
         double2 v[RQ];
 #pragma unroll
         for (int q = 0; q < RQ; q++) {
-            const int r = min(r0 + 3 * q, D - 1);
+            const int r = min(r0 + (NW - 1) * q, D - 1);
             const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;   // pieces up to the block's end
-            v[q] = r0 + 3 * q < D && lane < npr ? S2[r * npc + lane] : make_double2(0.0, 0.0);
+            v[q] = r0 + (NW - 1) * q < D && lane < npr ? S2[r * npc + lane] : make_double2(0.0, 0.0);
         }
 #pragma unroll
         for (int q = 0; q < RQ; q++) {
-            const int r = r0 + 3 * q;
+            const int r = r0 + (NW - 1) * q;
             const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;
             if (r < D && lane < npr) {
                 A[r * ld + 2 * lane] = v[q].x;
@@ -892,9 +900,9 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
         // identity padding of rows 16.. (no divisions): columns D..Dp-1 of every row, then rows
         // D..Dp-1; a thread per (row group, column) of each
         const int t = tid - 64, npad = Dp - D;
-        for (int r = SB + t / 16; r < Dp; r += 192 / 16)
+        for (int r = SB + t / 16; r < Dp; r += (NT - 64) / 16)
             if ((t & 15) < npad) A[r * ld + D + (t & 15)] = r == D + (t & 15) ? 1.0 : 0.0;
-        for (int r = max(D, SB) + t / 64; r < Dp; r += 3)
+        for (int r = max(D, SB) + t / 64; r < Dp; r += NW - 1)
             for (int c = lane; c < D; c += 64) A[r * ld + c] = 0.0;
         if (tid < Dp) y[tid] = bs_v;
     }
@@ -915,7 +923,7 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
             }
 #pragma unroll
             for (int s2 = 0; s2 < 4; s2++) bvz[s2] = col == 0 ? vz[J0 + 4 * s2 + kq] : 0.0;   // B = [v | 0]
-            for (int t = wv; t < nbk; t += 4) {
+            for (int t = wv; t < nbk; t += NW) {
                 const int i0 = R0 + SB * t;
                 double av[4];
 #pragma unroll
@@ -951,7 +959,10 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BADev b, int D) {
                 if (J0 == 32) BA_STAMPW(45);
             } else {
                 const int ntile = nbk * (nbk + 1) / 2;
-                for (int t = wv; t < ntile; t += 3) {   // tile 0 = (J+1, J+1) belongs to wavefront 0
+                // helper h: the waves off wavefront 0's SIMD first (w % 4 != 0), then its SIMD-mates
+                constexpr int NH = NW - 1, NOFF = NW - NW / 4;   // helpers; helpers off SIMD 0
+                const int h = (wv & 3) ? (wv >> 2) * 3 + (wv & 3) - 1 : NOFF + (wv >> 2) - 1;
+                for (int t = 1 + h; t < ntile; t += NH) {   // tile 0 = (J+1, J+1) belongs to wavefront 0
                     int I = 0;
                     while ((I + 1) * (I + 2) / 2 <= t) I++;
                     const int K = t - I * (I + 1) / 2;
@@ -1072,201 +1083,6 @@ __global__ __launch_bounds__(1024) void ba_struct_pairs_kernel(const int* __rest
         }
         base += tot;
         __syncthreads();
-    }
-}
-
-// ---- The same solve, pivot by pivot (round 6; ORBBA_SOLVE=block selects the blocked kernel above).
-// The blocked kernel's critical path is wavefront 0's 16-pivot diagonal factorisation of every block
-// (≈6.6k of ≈11k ticks per block, the other three wavefronts mostly waiting).  Here the whole
-// workgroup takes every pivot: 256 threads as a 16 x 16 grid, thread (ty, tx) holding the
-// lower-triangle entries A(ty + 16a, tx + 16c), c <= a < 8, in registers (the cyclic layout keeps the
-// shrinking trailing matrix spread evenly), one workgroup barrier per pivot:
-//   * column j (published in LDS by its owners at the previous step) is read by every thread: the
-//     multipliers of its rows (ty + 16a) and columns (tx + 16c), the pivot d_j and y_j;
-//   * while those reads are in flight, the previous pivot's rank-1 update runs (deferred);
-//   * then the owners of column j+1 (tx = (j+1) mod 16) apply pivot j to it and publish it, and the
-//     owner of y_{j+1} does the same for the right-hand side (forward substitution folded in):
-//     only this lookahead is on the per-pivot critical path.
-// U (LDS, column-major, stride ld odd) keeps every published column U_{ij} = L_{ij} d_j, so the back
-// substitution x_c = d_c^-1 (z_c - sum_{j>c} U_{jc} x_j) runs on wavefront 0 alone, one pivot per step
-// from the last, x_j broadcast by v_readlane: no barriers.  Block and pivot forms give the same
-// solution up to rounding (tests/test_ba_gpu.py: identical iterations and outliers either way).
-constexpr int SP_NB = 8;   // 16-row blocks: D <= 128
-__host__ __device__ constexpr int sp_ld(int D) { return 16 * ((D + 15) / 16) + 1; }
-__host__ __device__ constexpr size_t sp_lds_doubles(int D) { return (size_t)D * sp_ld(D) + 3 * 128; }
-#define SP_TRI(a, c) ((a) * ((a) + 1) / 2 + (c))
-
-// pivot j-1's update of column K (owners) and of y row K (its owner), ahead of the deferred update
-template <int K>
-__device__ __forceinline__ void sp_col_prev(double (&R)[36], double (&yv)[SP_NB], const double (&crp)[SP_NB],
-                                            const double (&ccp)[SP_NB], double yfp, bool own_col, bool own_y,
-                                            int nb) {
-    if (own_col) {
-#pragma unroll
-        for (int a = K; a < SP_NB; a++)
-            if (a < nb) R[SP_TRI(a, K)] = fma(-crp[a], ccp[K], R[SP_TRI(a, K)]);
-    }
-    if (own_y) yv[K] = fma(-crp[K], yfp, yv[K]);
-}
-// pivot j's update of column K = j+1 and its publication; the same for y_{j+1}
-template <int K>
-__device__ __forceinline__ void sp_col_next(double (&R)[36], double (&yv)[SP_NB], const double (&cr)[SP_NB],
-                                            double ccK, double yf, bool own_col, bool own_y, int nb, int ty,
-                                            double* Ucol, double* yout) {
-    if (own_col) {
-#pragma unroll
-        for (int a = K; a < SP_NB; a++)
-            if (a < nb) {
-                const double v = fma(-cr[a], ccK, R[SP_TRI(a, K)]);
-                R[SP_TRI(a, K)] = v;
-                Ucol[ty + 16 * a] = v;
-            }
-    }
-    if (own_y) {
-        yv[K] = fma(-cr[K], yf, yv[K]);
-        *yout = yv[K];
-    }
-}
-#define SP_SWITCH(cn, CALL)                 \
-    switch (cn) {                           \
-        case 0: CALL(0); break;             \
-        case 1: CALL(1); break;             \
-        case 2: CALL(2); break;             \
-        case 3: CALL(3); break;             \
-        case 4: CALL(4); break;             \
-        case 5: CALL(5); break;             \
-        case 6: CALL(6); break;             \
-        default: CALL(7); break;            \
-    }
-
-__global__ __launch_bounds__(256) void ba_solve_pivot_kernel(BADev b, int D) {
-    BA_RETURN_IF_DONE(b);
-    extern __shared__ __attribute__((aligned(16))) double U[];   // column j at U + j * ld
-    const int nb = (D + 15) >> 4, ld = sp_ld(D);
-    double* ybuf = U + (size_t)D * ld;   // z_j as published (final after pivot j-1)
-    double* dv = ybuf + 128;             // 1 / d_j
-    double* xbuf = dv + 128;             // the solution
-    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
-    double q_pre[4] = {0, 0, 0, 0}, t_pre[3] = {0, 0, 0}, bp_pre[6] = {0, 0, 0, 0, 0, 0};
-    if (tid < b.np) {
-        const int id = b.ps_id[tid];
-        for (int j = 0; j < 4; j++) q_pre[j] = b.q[4 * id + j];
-        for (int j = 0; j < 3; j++) t_pre[j] = b.t[3 * id + j];
-        for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
-    }
-    // S's lower triangle straight into registers (36 independent loads per thread)
-    double R[36], yv[SP_NB];
-#pragma unroll
-    for (int a = 0; a < SP_NB; a++) {
-        const int i = ty + 16 * a;
-#pragma unroll
-        for (int c = 0; c <= a; c++) {
-            const int k = tx + 16 * c;
-            R[SP_TRI(a, c)] = (a < nb && i < D && k <= i) ? b.S[i * D + k] : 0.0;
-        }
-        yv[a] = (tx == 0 && a < nb && i < D) ? b.bs[i] : 0.0;
-    }
-    if (tx == 0) {   // column 0 and y_0
-#pragma unroll
-        for (int a = 0; a < SP_NB; a++)
-            if (a < nb) U[ty + 16 * a] = R[SP_TRI(a, 0)];
-        if (ty == 0) ybuf[0] = yv[0];
-    }
-    __syncthreads();
-    double crp[SP_NB], ccp[SP_NB], yfp = 0;   // pivot j-1's multipliers (its deferred update)
-#pragma unroll
-    for (int a = 0; a < SP_NB; a++) crp[a] = ccp[a] = 0;
-    int jbp = 0;   // block of pivot j-1
-    bool ok = true;
-    for (int j = 0; j < D; j++) {
-        const int jb = j >> 4;
-        const double* Uj = U + j * ld;
-        double cr[SP_NB], cc[SP_NB];
-#pragma unroll
-        for (int a = 0; a < SP_NB; a++) {
-            const bool live = a >= jb && a < nb;   // wave-uniform
-            cr[a] = live ? Uj[ty + 16 * a] : 0.0;
-            cc[a] = live ? Uj[tx + 16 * a] : 0.0;
-        }
-        const double dj = Uj[j], yj = ybuf[j];
-        const int jn = j + 1, cn = jn >> 4, tn = jn & 15;
-        const bool own_col = jn < D && tx == tn, own_y = jn < D && tx == 0 && ty == tn;
-        // pivot j-1 on column j+1 and y_{j+1} (their owners), then everywhere else: column j and
-        // y_j already have it (the previous lookahead), columns / rows below the pivot are final
-        if (jn < D) {
-#define SP_PREV(K) sp_col_prev<K>(R, yv, crp, ccp, yfp, own_col, own_y, nb)
-            SP_SWITCH(cn, SP_PREV)
-#undef SP_PREV
-        }
-#pragma unroll
-        for (int c = 0; c < SP_NB; c++) {
-            if ((c == cn && tx == tn) || (c == jb && tx == (j & 15))) ccp[c] = 0.0;
-            if ((c == cn && ty == tn) || (c == jb && ty == (j & 15))) crp[c] = 0.0;
-        }
-#pragma unroll
-        for (int a = 0; a < SP_NB; a++) {
-            if (a >= jbp && a < nb) {   // wave-uniform
-#pragma unroll
-                for (int c = 0; c <= a; c++)
-                    if (c >= jbp) R[SP_TRI(a, c)] = fma(-crp[a], ccp[c], R[SP_TRI(a, c)]);
-                yv[a] = fma(-crp[a], yfp, yv[a]);
-            }
-        }
-        // pivot j
-        ok = ok && dj != 0 && isfinite(dj);
-        const double inv = rcp_d(dj), yf = inv * yj;
-        if (jn < D) {
-            double ccn = 0;
-#pragma unroll
-            for (int c = 0; c < SP_NB; c++) ccn = c == cn ? cc[c] : ccn;
-            ccn *= inv;
-#define SP_NEXT(K) sp_col_next<K>(R, yv, cr, ccn, yf, own_col, own_y, nb, ty, U + jn * ld, ybuf + jn)
-            SP_SWITCH(cn, SP_NEXT)
-#undef SP_NEXT
-        }
-        if (tid == 0) dv[j] = inv;
-#pragma unroll
-        for (int a = 0; a < SP_NB; a++) {
-            crp[a] = cr[a];
-            ccp[a] = cc[a] * inv;
-        }
-        yfp = yf;
-        jbp = jb;
-        __syncthreads();
-    }
-    // back substitution on wavefront 0: lane l holds columns l and l + 64
-    if (tid < 64) {
-        const int l = tid, l0 = min(l, D - 1), l1 = min(l + 64, D - 1);   // (clamped: reads stay inside U)
-        double acc0 = 0, acc1 = 0, x0 = 0, x1 = 0;
-        for (int j = D - 1; j >= 0; j--) {
-            const double accj = j >= 64 ? readlane_d(acc1, j - 64) : readlane_d(acc0, j);
-            const double xj = dv[j] * (ybuf[j] - accj);
-            if (j >= 64) x1 = l == j - 64 ? xj : x1;
-            else x0 = l == j ? xj : x0;
-            acc0 = fma(U[l0 * ld + j], xj, acc0);   // U_{j,l} (garbage for l >= j: those x are final)
-            acc1 = fma(U[l1 * ld + j], xj, acc1);
-        }
-        if (l < D) xbuf[l] = x0;
-        if (l + 64 < D) xbuf[l + 64] = x1;
-    }
-    __syncthreads();
-    for (int i = tid; i < D; i += blockDim.x) b.x[i] = ok ? xbuf[i] : 0.0;
-    if (tid == 0) b.ctl->ok2 = ok;
-    const double lam = b.ctl->lambda;
-    if (tid < b.np) {   // push() + oplus for the free poses, scale terms x.(lambda x + b)
-        const int i = tid;
-        const int id = b.ps_id[i];
-        double xi[6], part = 0;
-        for (int j = 0; j < 6; j++) {
-            xi[j] = ok ? xbuf[6 * i + j] : 0.0;
-            part += xi[j] * (lam * xi[j] + bp_pre[j]);
-        }
-        b.part[b.nl + i] = part;
-        for (int j = 0; j < 4; j++) b.q_sv[4 * id + j] = q_pre[j];
-        for (int j = 0; j < 3; j++) b.t_sv[3 * id + j] = t_pre[j];
-        se3_exp_update(xi, q_pre, t_pre);
-        for (int j = 0; j < 4; j++) b.q[4 * id + j] = q_pre[j];
-        for (int j = 0; j < 3; j++) b.t[3 * id + j] = t_pre[j];
     }
 }
 
@@ -1935,12 +1751,14 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (Ea == 0 || np + nl == 0) return ORB_OK;
         // reduced system: in LDS up to 21 free keyframes (D <= 128), else in HBM (ba_solve_global_kernel)
         const bool glob = D > 128 || solve_lds_doubles(D) * 8 + 4096 > 160 * 1024;
-        // the pivot-wise solve (default) or the blocked one (ORBBA_SOLVE=block), both in LDS
-        // (read per call: tests compare the forms in one process)
-        const bool pivot_solve = [] {
-            const char* e = getenv("ORBBA_SOLVE");
-            return !(e && std::string(e) == "block");
+        // the LDS solve's workgroup: 1024 threads, or the round-5 256 (ORBBA_SOLVE_THREADS=256; read per call)
+        const bool solve256 = [] {
+            const char* e = getenv("ORBBA_SOLVE_THREADS");
+            return e && atoi(e) == 256;
         }();
+        const void* solve_fn = glob ? (const void*)ba_solve_global_kernel
+                               : solve256 ? (const void*)ba_solve_kernel<256> : (const void*)ba_solve_kernel<1024>;
+
         if (glob && np > ORBBA_MAX_FREE_KEYFRAMES) {
             set_error("LocalBA: more than ORBBA_MAX_FREE_KEYFRAMES free keyframes in the local window");
             return ORB_EINVAL;
@@ -2047,22 +1865,16 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
         if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
         if (nblk) ORB_HIP_TRY(hipMemsetAsync(b.blk_done, 0, (size_t)nblk * 4, st));
-        const size_t ldlt_lds = glob          ? (size_t)3 * Dp * 8
-                                : pivot_solve ? std::max<size_t>(sp_lds_doubles(D) * 8, 16)
-                                              : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
+        const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
         {   // the dynamic LDS limit is a process-wide attribute of the kernel: raised (a host call) only
             // when a call needs more than any call before it on this device, never lowered
             static std::mutex mu;
             static size_t lim[64][3] = {};
             const size_t need = std::max<size_t>(ldlt_lds, 1024);
             std::lock_guard<std::mutex> lk(mu);
-            const int kind = glob ? 1 : pivot_solve ? 2 : 0;
-            size_t& cur = lim[device & 63][kind];
+            size_t& cur = lim[device & 63][glob ? 1 : solve256 ? 2 : 0];
             if (need > cur) {
-                ORB_HIP_TRY(hipFuncSetAttribute(glob ? (const void*)ba_solve_global_kernel
-                                                : pivot_solve ? (const void*)ba_solve_pivot_kernel
-                                                              : (const void*)ba_solve_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+                ORB_HIP_TRY(hipFuncSetAttribute(solve_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
                 cur = need;
             }
         }
@@ -2089,8 +1901,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 }
                 hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1 + np, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
                 if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
-                else if (pivot_solve) hipLaunchKernelGGL(ba_solve_pivot_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
-                else hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), ldlt_lds, st, b, D);
+                else if (solve256) hipLaunchKernelGGL(ba_solve_kernel<256>, dim3(1), dim3(256), ldlt_lds, st, b, D);
+                else hipLaunchKernelGGL(ba_solve_kernel<1024>, dim3(1), dim3(1024), ldlt_lds, st, b, D);
                 const int slot = enq % LOOKAHEAD;
                 C.step_seq = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;
                 ids[slot] = C.step_seq;

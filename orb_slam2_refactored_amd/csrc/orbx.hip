@@ -1548,6 +1548,7 @@ __global__ __launch_bounds__(64, FAST_WAVES_DEF) void fast_cells_kernel(Geom g, 
 
     n_ini = 0;
     n_min = 0;
+    n_iniB = 0;   // (a speculative pass that fell through left its counts)
     if constexpr (PAIR) {
         // Both cells' NMS in one walk (the list, or the zone map row by row for dense pairs), with a
         // third ballot per chunk marking the first cell's entries (row-major: a prefix), then each
