@@ -829,7 +829,7 @@ __device__ __forceinline__ void solve_trailing_tile_g(double* A, int ld, int J0,
 // not share wavefront 0's SIMD first (waves w with w % 4 != 0; a workgroup's waves are dealt to the
 // SIMDs in turn), so the diagonal chain keeps its SIMD's issue slots.
 template <int NT>
-__global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D) {
+__global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_helpers) {
     BA_RETURN_IF_DONE(b);
     constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) double A[];   // Dp x ld
@@ -960,9 +960,12 @@ __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D) {
             } else {
                 const int ntile = nbk * (nbk + 1) / 2;
                 // helper h: the waves off wavefront 0's SIMD first (w % 4 != 0), then its SIMD-mates
-                constexpr int NH = NW - 1, NOFF = NW - NW / 4;   // helpers; helpers off SIMD 0
+                // (simd0_helpers = 0: wavefront 0's SIMD-mates take no tiles at all when there are enough
+                // other helpers, so the diagonal chain has its SIMD to itself)
+                constexpr int NOFF = NW - NW / 4;   // helpers off SIMD 0
+                const int NH = (simd0_helpers || NOFF == 0) ? NW - 1 : NOFF;
                 const int h = (wv & 3) ? (wv >> 2) * 3 + (wv & 3) - 1 : NOFF + (wv >> 2) - 1;
-                for (int t = 1 + h; t < ntile; t += NH) {   // tile 0 = (J+1, J+1) belongs to wavefront 0
+                for (int t = 1 + h; h < NH && t < ntile; t += NH) {   // tile 0 = (J+1, J+1) belongs to wavefront 0
                     int I = 0;
                     while ((I + 1) * (I + 2) / 2 <= t) I++;
                     const int K = t - I * (I + 1) / 2;
@@ -1557,6 +1560,53 @@ struct BAContext {
 };
 thread_local BAContext g_ba;
 
+// The call's buffer initialisations as ONE launch per batch instead of a hipMemsetAsync each (round 6:
+// 11 memsets per call ran as 16 fill kernels of ~4.4 us, ~70 us of the call's GPU time in rocprofv3).
+// Segments start 16-byte aligned (carve offsets are multiples of 256); a byte value replicated.
+constexpr int BA_FILL_MAX = 8;
+struct BAFill {
+    void* p[BA_FILL_MAX];
+    unsigned long long n[BA_FILL_MAX];
+    unsigned v[BA_FILL_MAX];
+    int cnt;
+};
+__global__ __launch_bounds__(256) void ba_fill_kernel(BAFill f) {
+    const unsigned long long gt = blockIdx.x * 256ull + threadIdx.x, gs = gridDim.x * 256ull;
+    for (int s = 0; s < f.cnt; s++) {
+        uint8_t* p = static_cast<uint8_t*>(f.p[s]);
+        const unsigned b = f.v[s] & 0xffu, w = b * 0x01010101u;
+        const uint4 v4 = make_uint4(w, w, w, w);
+        const unsigned long long nv = f.n[s] >> 4;
+        for (unsigned long long i = gt; i < nv; i += gs) reinterpret_cast<uint4*>(p)[i] = v4;
+        for (unsigned long long i = (nv << 4) + gt; i < f.n[s]; i += gs) p[i] = (uint8_t)b;
+    }
+}
+struct FillQueue {
+    BAFill f{};
+    unsigned long long bytes = 0;
+    int add(void* p, size_t n, int v, hipStream_t st) {
+        if (!n) return ORB_OK;
+        if (f.cnt == BA_FILL_MAX) {
+            if (int rc = flush(st)) return rc;
+        }
+        f.p[f.cnt] = p;
+        f.n[f.cnt] = n;
+        f.v[f.cnt] = (unsigned)v;
+        f.cnt++;
+        bytes += n;
+        return ORB_OK;
+    }
+    int flush(hipStream_t st) {
+        if (!f.cnt) return ORB_OK;
+        const unsigned nb = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(1024, bytes / (16 * 256 * 2)));
+        hipLaunchKernelGGL(ba_fill_kernel, dim3(nb), dim3(256), 0, st, f);
+        f.cnt = 0;
+        bytes = 0;
+        ORB_HIP_TRY(hipGetLastError());
+        return ORB_OK;
+    }
+};
+
 struct Carve {
     char* base;
     size_t off = 0;
@@ -1706,13 +1756,12 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     b.ctl = C.ctlbuf.as<BACtl>();
     b.stop = stop_flag ? C.d_stop : nullptr;
     b.stop_after = stop_after;
-    ORB_HIP_TRY(hipMemsetAsync(b.ctl, 0, sizeof(BACtl), st));   // trials / stopped count over the whole call
+    FillQueue fills;   // flushed (one launch) before the first kernel that reads them
+    if ((rc = fills.add(b.ctl, sizeof(BACtl), 0, st))) return rc;   // trials / stopped count over the whole call
     ORB_HIP_TRY(hipMemcpyAsync(C.prob.ptr, C.h_prob.ptr, cp.off, hipMemcpyHostToDevice, st));
-    if (E) {
-        ORB_HIP_TRY(hipMemsetAsync(b.robust, 1, E, st));
-        ORB_HIP_TRY(hipMemsetAsync(d_level, 0, E, st));
-        ORB_HIP_TRY(hipMemsetAsync(b.err, 0, 24 * (size_t)E, st));
-    }
+    if ((rc = fills.add(b.robust, E, 1, st)) || (rc = fills.add(d_level, E, 0, st)) ||
+        (rc = fills.add(b.err, 24 * (size_t)E, 0, st)))
+        return rc;
     res->iterations[0] = res->iterations[1] = 0;
     res->chi2[0] = res->chi2[1] = 0;
 
@@ -1755,6 +1804,10 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         const bool solve256 = [] {
             const char* e = getenv("ORBBA_SOLVE_THREADS");
             return e && atoi(e) == 256;
+        }();
+        const int simd0_helpers = [] {   // ORBBA_SOLVE_SIMD0=1: wavefront 0's SIMD-mates take trailing tiles too
+            const char* e = getenv("ORBBA_SOLVE_SIMD0");
+            return e && atoi(e) != 0 ? 1 : 0;
         }();
         const void* solve_fn = glob ? (const void*)ba_solve_global_kernel
                                : solve256 ? (const void*)ba_solve_kernel<256> : (const void*)ba_solve_kernel<1024>;
@@ -1812,7 +1865,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         if (dev_build) {
             int* d_slot = cr.take<int>((size_t)np * nl);
             ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, small_bytes, hipMemcpyHostToDevice, st));
-            if (np && nl) ORB_HIP_TRY(hipMemsetAsync(d_slot, 0xff, 4 * (size_t)np * nl, st));
+            if ((rc2 = fills.add(d_slot, 4 * (size_t)np * nl, 0xff, st)) || (rc2 = fills.flush(st))) return rc2;
             if (Ea)
                 hipLaunchKernelGGL(ba_struct_slots_kernel, dim3((Ea + 255) / 256), dim3(256), 0, st, d_ep, d_ek, d_hp, d_hl,
                                    Ea, nl, d_act, d_pts, d_slot);
@@ -1862,9 +1915,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.part = cy.take<double>(nl + np);
         b.Sg = glob ? cy.take<double>((size_t)Dp * (Dp + 1)) : nullptr;
         double* d_wgpart = cy.take<double>(2 * (size_t)((nl * 8 + 63) / 64));   // point-update workgroup partials
-        ORB_HIP_TRY(hipMemsetAsync(b.J, 0, 72 * 8 * (size_t)Ea, st));
-        if (D) ORB_HIP_TRY(hipMemsetAsync(b.S, 0, (size_t)D * D * 8, st));
-        if (nblk) ORB_HIP_TRY(hipMemsetAsync(b.blk_done, 0, (size_t)nblk * 4, st));
+        if ((rc2 = fills.add(b.J, 72 * 8 * (size_t)Ea, 0, st)) || (rc2 = fills.add(b.S, (size_t)D * D * 8, 0, st)) ||
+            (rc2 = fills.add(b.blk_done, (size_t)nblk * 4, 0, st)) || (rc2 = fills.flush(st)))
+            return rc2;
         const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
         {   // the dynamic LDS limit is a process-wide attribute of the kernel: raised (a host call) only
             // when a call needs more than any call before it on this device, never lowered
@@ -1901,8 +1954,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 }
                 hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1 + np, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
                 if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
-                else if (solve256) hipLaunchKernelGGL(ba_solve_kernel<256>, dim3(1), dim3(256), ldlt_lds, st, b, D);
-                else hipLaunchKernelGGL(ba_solve_kernel<1024>, dim3(1), dim3(1024), ldlt_lds, st, b, D);
+                else if (solve256) hipLaunchKernelGGL(ba_solve_kernel<256>, dim3(1), dim3(256), ldlt_lds, st, b, D, 1);
+                else hipLaunchKernelGGL(ba_solve_kernel<1024>, dim3(1), dim3(1024), ldlt_lds, st, b, D, simd0_helpers);
                 const int slot = enq % LOOKAHEAD;
                 C.step_seq = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;
                 ids[slot] = C.step_seq;
@@ -1983,6 +2036,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     double* hX = hres.take<double>(3 * (size_t)N);
     uint8_t* ho = hres.take<uint8_t>(E);
     double* hc = hres.take<double>(E);
+    if ((rc = fills.flush(st))) return rc;   // (a call that optimised nothing still classifies)
     if (const int nt = std::max(E, std::max(N, P))) {
         hipLaunchKernelGGL(ba_classify_kernel, dim3((nt + 255) / 256), dim3(256), 0, st, b, ro, rch, (uint8_t*)nullptr, 0,
                            rq, rt, rX);

@@ -15,6 +15,7 @@
 #   kb_sweep tools/kbench.py on pan frames at 64 .. 2048 frames per launch (per-frame stage times)
 #   stereo   tests/test_stereo_gpu.py      batests  tests/test_ba_gpu.py + tests/test_cpp_dropin_gpu.py
 #   pyt      pytest on $PYT_FILES (-m gpu -x -q)
+#   ba_prof  rocprofv3 kernel stats of tools/babench.py 20, once per setting in $BA_ENVS (per-kernel averages)
 #   pmc_pan | pmc_tex   instruction counters (tools/pmc_groups_inst.txt) on 1024 pan / textured frames, and the
 #            per-cell / per-wavefront counts (tools/pmc_percell.py) -> gpurun_out/pmci_{pan,textured}/
 #
@@ -71,6 +72,16 @@ for step in "$@"; do
   batests)
     timeout -k 10 300 $PYT tests/test_ba_gpu.py tests/test_cpp_dropin_gpu.py -q > gpurun_out/pytest_ba.log 2>&1 || { tail -30 gpurun_out/pytest_ba.log; exit 2; }
     tail -2 gpurun_out/pytest_ba.log ;;
+  ba_prof)
+    IFS=';' read -ra envs <<< "${BA_ENVS:-X=0}"
+    k=0
+    for e in "${envs[@]}"; do
+      k=$((k + 1))
+      env $e timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ba_prof$k -o ba -- \
+        python3 tools/babench.py 20 > gpurun_out/ba_prof$k.log 2>&1 || { tail gpurun_out/ba_prof$k.log; exit 5; }
+      echo "[$e] $(grep LocalBA gpurun_out/ba_prof$k.log)"
+      python3 -c "import csv; [print('   %-40s %5s %8.2f us' % (x['Name'].split('(')[0][-40:], x['Calls'], float(x['AverageNs']) / 1e3)) for x in list(csv.DictReader(open('gpurun_out/ba_prof$k/ba_kernel_stats.csv')))[:6]]"
+    done ;;
   pyt)
     timeout -k 10 600 $PYT $PYT_FILES -m gpu -x -q > gpurun_out/pytest_pyt.log 2>&1 || { tail -30 gpurun_out/pytest_pyt.log; exit 2; }
     tail -2 gpurun_out/pytest_pyt.log ;;
