@@ -183,6 +183,32 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
     return base + inc - v;
 }
 
+// The quadtree's group primitives for its two forms: WV = false, the whole workgroup on one tree
+// (workgroup barrier, block scan); WV = true (round 6), one wavefront per tree (no barrier: a wavefront
+// runs in lockstep, so an LDS / global write is visible to the wavefront's next read once issued and
+// the compiler is kept from reordering across the point; the fence orders global memory as the
+// workgroup barrier's does).
+template <bool WV>
+__device__ __forceinline__ void qt_sync() {
+    if constexpr (WV) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+        __syncthreads();
+    }
+}
+template <bool WV>
+__device__ __forceinline__ int grp_excl_scan(int v, int* tmp, int* total) {
+    if constexpr (WV) {
+        const int inc = wave_incl_scan(v);
+        *total = __builtin_amdgcn_readlane(inc, 63);
+        return inc - v;
+    } else {
+        return block_excl_scan(v, tmp, total);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // 1. pyramid
 // ------------------------------------------------------------------------------------------
@@ -2073,13 +2099,15 @@ __device__ unsigned long long g_qt_wg[4096 * 2];   // per (frame, level) WG: sta
 // result is identical to the sequential order.  All threads of the block must call it.
 // Scratch: Ls, Rs, seg_lo, seg_len (n ints each), tmp (n items), lists (6 * list_cap ints),
 // s_cnt (2 shared ints).  list_cap >= n / 17 + 1.
+template <bool WV>
 __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, int* seg_len, QtItem* tmp,
                               int* lists, int list_cap, int* s_cnt) {
-    const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int lane = lane_id(), w = WV ? 0 : (int)(threadIdx.x >> 6), nw = WV ? 1 : (int)(blockDim.x >> 6);
+    const int gtid = WV ? lane : (int)threadIdx.x, gbd = WV ? 64 : (int)blockDim.x;
     if (n <= 0) return;
     int* cur = lists;
     int* nxt = lists + 3 * list_cap;
-    if (threadIdx.x == 0) {
+    if (gtid == 0) {
         s_cnt[0] = 0;
         s_cnt[1] = 0;
         if (n > 16) {
@@ -2088,8 +2116,8 @@ __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, i
         }
     }
     if (n <= 16)
-        for (int i = threadIdx.x; i < n; i += blockDim.x) { seg_lo[i] = 0; seg_len[i] = n; }
-    __syncthreads();
+        for (int i = gtid; i < n; i += gbd) { seg_lo[i] = 0; seg_len[i] = n; }
+    qt_sync<WV>();
     while (true) {
         const int nc = s_cnt[0];
         if (nc == 0) break;
@@ -2160,16 +2188,16 @@ __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, i
             }
             wave_lds_sync();
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
+        qt_sync<WV>();
+        if (gtid == 0) {
             s_cnt[0] = s_cnt[1];
             s_cnt[1] = 0;
         }
         int* t = cur; cur = nxt; nxt = t;
-        __syncthreads();
+        qt_sync<WV>();
     }
     // final insertion pass == stable sort inside each final segment
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    for (int i = gtid; i < n; i += gbd) {
         const QtItem v = a[i];
         if (seg_len[i] < 0) { tmp[i] = v; continue; }
         const int lo = seg_lo[i], hi = lo + seg_len[i];
@@ -2180,20 +2208,27 @@ __device__ void qt_sort_block(QtItem* a, int n, int* Ls, int* Rs, int* seg_lo, i
         }
         tmp[lo + r] = v;
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = tmp[i];
-    __syncthreads();
+    qt_sync<WV>();
+    for (int i = gtid; i < n; i += gbd) a[i] = tmp[i];
+    qt_sync<WV>();
 }
 
 #ifndef QT_WAVES_DEF
 #define QT_WAVES_DEF 4   // wavefronts per SIMD = workgroups per CU (4 wavefronts each)
 #endif
+// per node: na, nb (QtNode), cc (int4), divs, prev (QtItem), ia, ib (int) -- the host sizes the LDS with it
+constexpr int QT_NODE_BYTES = 2 * (int)sizeof(QtNode) + (int)sizeof(int4) + 2 * (int)sizeof(QtItem) + 2 * (int)sizeof(int);
+template <bool WV>
 __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom g, const int* __restrict__ cell_cnt,
                                                        const uint32_t* __restrict__ slots, const CellDev* cells,
                                                        uint32_t* __restrict__ Pbuf, uint32_t* __restrict__ Tbuf,
                                                        uint32_t* __restrict__ sel, int* __restrict__ sel_cnt, int NC,
-                                                       int PTC, uint32_t* fault, int lev0) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+                                                       int PTC, uint32_t* fault, int lev0, int nlev) {
+    extern __shared__ __attribute__((aligned(16))) char smem_all[];
+    // WV: wavefront q of the workgroup runs level lev0 + 4 blockIdx.y + q on its own LDS slice and its
+    // own copy of the shared scalars; otherwise the workgroup runs level lev0 + blockIdx.y
+    const int wslot = WV ? (int)(threadIdx.x >> 6) : 0;
+    char* smem = smem_all + (WV ? (size_t)wslot * ((size_t)NC * QT_NODE_BYTES + (size_t)PTC * 8) : 0);
     QtNode* na = reinterpret_cast<QtNode*>(smem);
     QtNode* nb = na + NC;
     int4* cc = reinterpret_cast<int4*>(nb + NC);
@@ -2203,26 +2238,42 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
     int* ib = ia + NC;
     uint32_t* lds_P = reinterpret_cast<uint32_t*>(ib + NC);   // candidate arrays when they fit
     uint32_t* lds_T = lds_P + PTC;
-    __shared__ int tmp[16];
-    __shared__ int s_n, s_ndiv, s_state, s_proc, s_fail;
-    __shared__ int s_sortcnt[2];
-    __shared__ int s_anybig;
+    constexpr int NSC = WV ? QT_WAVES : 1;
+    __shared__ int tmp_a[NSC][16];
+    __shared__ int s_sc[NSC][8];
+    __shared__ int s_sortcnt_a[NSC][2];
     __shared__ int s_split[64];
-    __shared__ int rc[MAX_ROOTS];
+    __shared__ int rc_a[NSC][MAX_ROOTS];
+    int* tmp = tmp_a[wslot];
+    int& s_n = s_sc[wslot][0];
+    int& s_ndiv = s_sc[wslot][1];
+    int& s_state = s_sc[wslot][2];
+    int& s_proc = s_sc[wslot][3];
+    int& s_fail = s_sc[wslot][4];
+    int& s_anybig = s_sc[wslot][5];
+    int* s_sortcnt = s_sortcnt_a[wslot];
+    int* rc = rc_a[wslot];
 
-    const int f = blockIdx.x, l = lev0 + (int)blockIdx.y;   // levels lev0 .. lev0 + gridDim.y - 1
-    int* scnt = sel_cnt + f * g.nlevels + l;
+    const int f = blockIdx.x, l = WV ? lev0 + 4 * (int)blockIdx.y + wslot : lev0 + (int)blockIdx.y;
     if (blockDim.x != QT_THREADS) {   // block-uniform: a launch this kernel is not written for fails loudly
         if (threadIdx.x == 0) {
             atomicOr(fault, FAULT_BLOCK_SIZE);
-            *scnt = 0;   // describe then sees an empty level, never stale selections
+            // describe then sees empty levels, never stale selections (WV: all four of the group)
+            for (int q = 0; q < (WV ? 4 : 1); q++) {
+                const int lq = WV ? lev0 + 4 * (int)blockIdx.y + q : l;
+                if (!WV || lq < lev0 + nlev) sel_cnt[f * g.nlevels + lq] = 0;
+            }
         }
         return;
     }
+    if (WV && l >= lev0 + nlev) return;   // (wave-uniform; no workgroup barrier in this form)
+    int* scnt = sel_cnt + f * g.nlevels + l;
     const LevelDev& L = g.lv[l];
-    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int qtid = WV ? lane_id() : (int)threadIdx.x;   // thread index within the tree's group
+    constexpr int QBD = WV ? 64 : QT_THREADS;               // the group's size
+    const int w = WV ? 0 : (int)(threadIdx.x >> 6), nw = WV ? 1 : QT_WAVES;
     if (L.rw <= 0 || L.rh <= 0 || L.ncells == 0) {
-        if (threadIdx.x == 0) *scnt = 0;
+        if (qtid == 0) *scnt = 0;
         return;
     }
     uint32_t* P = Pbuf + (long long)f * g.cand_frame + L.cand_base;
@@ -2245,11 +2296,11 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         const float dx = (float)x - (float)L.rx;   // keypoint.pt.x - roi.x (float)
         return (int)((double)dx / L.hx);
     };
-    if (threadIdx.x < MAX_ROOTS) rc[threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_fail = 0;
+    if (qtid < MAX_ROOTS) rc[qtid] = 0;
+    if (qtid == 0) s_fail = 0;
     int n_total = 0, carry = 0;
     bool parted = false;   // the gather below writes the root-partitioned order itself (round 5)
-    if (L.ncells <= 4 * (int)blockDim.x && R <= 4) {
+    if (L.ncells <= 4 * QBD && R <= 4) {
         // thread t owns cells cpt t .. cpt t + cpt - 1 (raster order): their counts and slot offsets are loaded
         // together and the points go straight to their root's segment.  A cell whose zone lies inside
         // one root (all but the cells on a root boundary) sends all its points there, a boundary cell
@@ -2260,11 +2311,11 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         // thread instead of 4), so a thread's chain of dependent slot loads is shorter (round 5);
         // thread order is still cell order.
 #ifndef QT_GATHER_CPT4
-        const int cpt = (L.ncells + (int)blockDim.x - 1) / (int)blockDim.x;   // 1..4
+        const int cpt = (L.ncells + QBD - 1) / QBD;   // 1..4
 #else
         const int cpt = 4;
 #endif
-        const int i0 = cpt * threadIdx.x;
+        const int i0 = cpt * qtid;
         int cv[4], cs[4], rl[4], rh[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -2303,8 +2354,8 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         for (int rt = 0; rt < 4; rt++) {
             if (rt >= R) { run[rt] = 0; continue; }   // block-uniform
             int tot;
-            run[rt] = base + block_excl_scan(cnt[rt], tmp, &tot);
-            if (threadIdx.x == 0) rc[rt] = tot;
+            run[rt] = base + grp_excl_scan<WV>(cnt[rt], tmp, &tot);
+            if (qtid == 0) rc[rt] = tot;
             base += tot;
         }
         n_total = base;
@@ -2348,9 +2399,9 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         }
         carry = n_total;
         parted = true;
-    } else if (L.ncells <= 4 * (int)blockDim.x) {
+    } else if (L.ncells <= 4 * QBD) {
         // (more than 4 roots: an aspect ratio above 4.5) the gather in raster order, partitioned below
-        const int i0 = 4 * threadIdx.x;
+        const int i0 = 4 * qtid;
         int cv[4], cs[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -2359,7 +2410,7 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             cs[k] = i < L.ncells ? cells[L.cell_base + i].slot : 0;
         }
         const int sum = cv[0] + cv[1] + cv[2] + cv[3];
-        const int ex = block_excl_scan(sum, tmp, &n_total);
+        const int ex = grp_excl_scan<WV>(sum, tmp, &n_total);
         if (n_total <= PTC) { P = lds_P; T = lds_T; }
         int o = ex;
 #pragma unroll
@@ -2378,19 +2429,19 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
     } else {
         {
             int part = 0;
-            for (int i = threadIdx.x; i < L.ncells; i += blockDim.x) part += ccell[i] & CELL_CNT_MASK;
+            for (int i = qtid; i < L.ncells; i += QBD) part += ccell[i] & CELL_CNT_MASK;
             part = wave_sum_i32(part);
             if (lane_id() == 0) tmp[8 + w] = part;
-            __syncthreads();
+            qt_sync<WV>();
             for (int q = 0; q < nw; q++) n_total += tmp[8 + q];
-            __syncthreads();
+            qt_sync<WV>();
         }
         if (n_total <= PTC) { P = lds_P; T = lds_T; }
-        for (int b = 0; b < L.ncells; b += blockDim.x) {
-            const int i = b + threadIdx.x;
+        for (int b = 0; b < L.ncells; b += QBD) {
+            const int i = b + qtid;
             const int v = i < L.ncells ? ccell[i] & CELL_CNT_MASK : 0;
             int tot;
-            const int ex = block_excl_scan(v, tmp, &tot);
+            const int ex = grp_excl_scan<WV>(v, tmp, &tot);
             if (v > 0) {
                 const uint32_t* __restrict__ src = fslots + cells[L.cell_base + i].slot;
                 uint32_t* dst = P + carry + ex;
@@ -2406,14 +2457,21 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             carry += tot;
         }
     }
-    __syncthreads();
+    qt_sync<WV>();
     const int n_src = carry;
-    QT_STAMP(1);
-    if (n_src == 0) {
-        if (threadIdx.x == 0) *scnt = 0;
+    if (WV && !parted) {   // the host sends only levels the partitioned gather takes (<= 256 cells, <= 4 roots)
+        if (qtid == 0) {
+            atomicOr(fault, FAULT_BLOCK_SIZE);
+            *scnt = 0;
+        }
         return;
     }
-    __syncthreads();
+    QT_STAMP(1);
+    if (n_src == 0) {
+        if (qtid == 0) *scnt = 0;
+        return;
+    }
+    qt_sync<WV>();
 
     // ---- root nodes (:547-579): stable partition by root id (the large-grid gather's order; the
     //      small-grid gather above wrote the partitioned order itself)
@@ -2458,7 +2516,7 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         if (lane_id() == 0)
             for (int q = 0; q < R; q++) s_rcnt[w][q] = counts[q];
     }
-    __syncthreads();
+    qt_sync<WV>();
     {
         int o[MAX_ROOTS];
         int acc = 0;
@@ -2470,7 +2528,7 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             }
             o[q] = acc + before;
             acc += tot;
-            if (threadIdx.x == 0) rc[q] = tot;
+            if (qtid == 0) rc[q] = tot;
         }
 #pragma unroll
         for (int t = 0; t < QT_RPL; t++) {
@@ -2504,14 +2562,14 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             }
         }
     }
-    __syncthreads();
+    qt_sync<WV>();
     {   // the partitioned copy becomes P (every thread swaps the same pointers)
         uint32_t* t = P;
         P = T;
         T = t;
     }
     }   // !parted
-    if (threadIdx.x == 0) {
+    if (qtid == 0) {
         int n = 0, acc = 0;
         for (int q = 0; q < R; q++) {
             if (rc[q] > 0) {
@@ -2531,7 +2589,7 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         s_ndiv = 0;
         s_anybig = 0;
     }
-    __syncthreads();
+    qt_sync<WV>();
 
     const int nfeat = L.quota;
     QT_STAMP(2);
@@ -2543,7 +2601,7 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         const int n = s_n;
         const int state = s_state;
         QT_STAMP(3 + 2 * iter_no);
-        if (threadIdx.x == 0 && blockIdx.x == 0 && l == QT_STAMP_LEVEL) {
+        if (qtid == 0 && blockIdx.x == 0 && l == QT_STAMP_LEVEL) {
 #ifdef ORB_QT_STAMPS
             if (4 + 2 * iter_no < 60) g_qt_stamps[4 + 2 * iter_no] = ((unsigned long long)state << 32) | (unsigned)n;
 #endif
@@ -2554,20 +2612,20 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             // Phase 1 pass (:588-630): split every divisible node in list order.
             // D positions via compaction
             int kdiv = 0, nnd = 0;   // (s_anybig was cleared before the last barrier)
-            for (int b = 0; b < n; b += blockDim.x) {
-                const int i = b + threadIdx.x;
+            for (int b = 0; b < n; b += QBD) {
+                const int i = b + qtid;
                 const int dvf = (i < n && na[i].cnt > 1) ? 1 : 0;
-                if (i < n && na[i].cnt > QT_BIG) s_anybig = 1;
+                if (!WV && i < n && na[i].cnt > QT_BIG) s_anybig = 1;   // (WV: one wavefront per tree, no block split)
                 int tot;
-                const int ex = block_excl_scan(dvf, tmp, &tot);
+                const int ex = grp_excl_scan<WV>(dvf, tmp, &tot);
                 if (i < n) {
                     if (dvf) ia[kdiv + ex] = i;               // D: divisible, processing order
                     else ib[i] = nnd + (i - b - ex);          // rank among non-divisible
                 }
-                nnd += min((int)blockDim.x, n - b) - tot;
+                nnd += min(QBD, n - b) - tot;
                 kdiv += tot;
             }
-            __syncthreads();
+            qt_sync<WV>();
             QT_SUBSTAMP(56);
             // nodes of <= 16 points: four per wavefront (16-lane groups); larger: one wavefront each
             for (int b = 4 * w; b < kdiv; b += 4 * nw) {   // wave-uniform trip count
@@ -2583,40 +2641,40 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             }
             for (int j = w; j < kdiv; j += nw) {
                 const int cn = na[ia[j]].cnt;
-                if (cn <= 16 || cn > QT_BIG) continue;   // wave-uniform
+                if (cn <= 16 || (!WV && cn > QT_BIG)) continue;   // wave-uniform
                 const int4 c = qt_wave_split(na[ia[j]], P, T);
                 if (lane_id() == 0) cc[j] = c;
             }
-            if (s_anybig) {   // block-uniform (set before the scans' barriers)
+            if (!WV && s_anybig) {   // block-uniform (set before the scans' barriers)
                 for (int j = 0; j < kdiv; j++) {
                     if (na[ia[j]].cnt <= QT_BIG) continue;   // block-uniform
                     const int4 c = qt_block_split(na[ia[j]], P, T, s_split);
-                    if (threadIdx.x == 0) cc[j] = c;
+                    if (qtid == 0) cc[j] = c;
                 }
             }
-            __syncthreads();
+            qt_sync<WV>();
             QT_SUBSTAMP(57);
             // group positions: reverse processing order; divisibles: forward order.  The ne and dv counts
             // share one block scan (16-bit halves: a chunk's totals are <= 4 blockDim); with one chunk
             // (kdiv <= blockDim, every small level) the scan's total is the grand total the reverse
             // order needs, so the separate total pass and its two barriers are skipped (round 5)
             int ne_carry = 0, dv_carry = 0, ne_total = 0;
-            if (kdiv > (int)blockDim.x) {   // block-uniform
+            if (kdiv > QBD) {   // block-uniform
                 int part = 0;
-                for (int j = threadIdx.x; j < kdiv; j += blockDim.x) part += ne4(cc[j]);
+                for (int j = qtid; j < kdiv; j += QBD) part += ne4(cc[j]);
                 part = wave_sum_i32(part);
                 if (lane_id() == 0) tmp[8 + w] = part;
-                __syncthreads();
+                qt_sync<WV>();
                 for (int q = 0; q < nw; q++) ne_total += tmp[8 + q];
-                __syncthreads();
+                qt_sync<WV>();
             }
-            for (int b = 0; b < kdiv; b += blockDim.x) {
-                const int j = b + threadIdx.x;
+            for (int b = 0; b < kdiv; b += QBD) {
+                const int j = b + qtid;
                 const int4 c = j < kdiv ? cc[j] : make_int4(0, 0, 0, 0);
                 int tt;
-                const int ex = block_excl_scan(ne4(c) | (dv4(c) << 16), tmp, &tt);
+                const int ex = grp_excl_scan<WV>(ne4(c) | (dv4(c) << 16), tmp, &tt);
                 const int t1 = tt & 0xffff, t2 = tt >> 16, ex_ne = ex & 0xffff, ex_dv = ex >> 16;
-                if (kdiv <= (int)blockDim.x) ne_total = t1;
+                if (kdiv <= QBD) ne_total = t1;
                 if (j < kdiv) {
                     const int incl = ne_carry + ex_ne + ne4(c);
                     const int gpos = ne_total - incl;   // sum of ne over items after j
@@ -2627,20 +2685,20 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             }
             const int n_new = ne_total + nnd;
             QT_SUBSTAMP(55);   // (thread 0: its emit done)
-            for (int i = threadIdx.x; i < n; i += blockDim.x)
+            for (int i = qtid; i < n; i += QBD)
                 if (na[i].cnt <= 1 && ne_total + ib[i] < NC) nb[ne_total + ib[i]] = na[i];
             // commit: the single points of the non-divisible nodes join the split nodes' points in
             // T, which becomes P (every thread swaps the same pointers)
-            for (int i = threadIdx.x; i < n; i += blockDim.x)
+            for (int i = qtid; i < n; i += QBD)
                 if (na[i].cnt == 1) T[na[i].beg] = P[na[i].beg];
             {
                 uint32_t* t = P;
                 P = T;
                 T = t;
             }
-            __syncthreads();
+            qt_sync<WV>();
             QT_SUBSTAMP(58);
-            if (threadIdx.x == 0) {
+            if (qtid == 0) {
                 if (n_new > NC) { s_fail = 1; atomicOr(fault, FAULT_QT_NODES); }
                 s_n = min(n_new, NC);
                 s_ndiv = dv_carry;
@@ -2648,41 +2706,41 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
                 if (n_new >= nfeat || n_new == n || s_fail) s_state = 2;
                 else if (n_new + 3 * dv_carry > nfeat) s_state = 1;
             }
-            __syncthreads();
+            qt_sync<WV>();
             QT_SUBSTAMP(59);
             QtNode* t = na; na = nb; nb = t;
         } else {
             // Phase 2 round (:632-672): split the previous round's divisible nodes, largest
             // first (std::sort, emulated), stopping as soon as the list reaches nfeat.
             const int m = s_ndiv;
-            for (int j = threadIdx.x; j < m; j += blockDim.x) prev[j] = divs[j];
-            __syncthreads();
+            for (int j = qtid; j < m; j += QBD) prev[j] = divs[j];
+            qt_sync<WV>();
             QT_STAMP(40 + 4 * min(p2_round, 5));
             {
                 int* seg = reinterpret_cast<int*>(cc);   // cc (4 NC ints) is free until the splits below
-                qt_sort_block(prev, m, ia, ib, seg, seg + NC, divs, seg + 2 * NC, NC / 3, s_sortcnt);
+                qt_sort_block<WV>(prev, m, ia, ib, seg, seg + NC, divs, seg + 2 * NC, NC / 3, s_sortcnt);
             }
             QT_STAMP(41 + 4 * min(p2_round, 5));
-            for (int j = threadIdx.x; j < m; j += blockDim.x) cc[j] = qt_thread_count(na[prev[j].node], P);
-            for (int i = threadIdx.x; i < n; i += blockDim.x) ia[i] = 0;   // erased flags
-            if (threadIdx.x == 0) s_proc = m;
-            __syncthreads();
+            for (int j = qtid; j < m; j += QBD) cc[j] = qt_thread_count(na[prev[j].node], P);
+            for (int i = qtid; i < n; i += QBD) ia[i] = 0;   // erased flags
+            if (qtid == 0) s_proc = m;
+            qt_sync<WV>();
             // first sorted item whose split brings the list to nfeat (:666-667), by prefix sums
             {
                 int carry2 = 0;
-                for (int b = 0; b < m; b += blockDim.x) {
-                    const int j = b + threadIdx.x;
+                for (int b = 0; b < m; b += QBD) {
+                    const int j = b + qtid;
                     const int d = j < m ? ne4(cc[j]) - 1 : 0;
                     int tot;
-                    const int ex = block_excl_scan(d, tmp, &tot);
+                    const int ex = grp_excl_scan<WV>(d, tmp, &tot);
                     if (j < m && n + carry2 + ex + d >= nfeat) atomicMin(&s_proc, j + 1);
                     carry2 += tot;
                 }
             }
-            __syncthreads();
+            qt_sync<WV>();
             const int proc = s_proc;
             QT_STAMP(42 + 4 * min(p2_round, 5));
-            for (int j = threadIdx.x; j < proc; j += blockDim.x) ia[prev[j].node] = 1;
+            for (int j = qtid; j < proc; j += QBD) ia[prev[j].node] = 1;
             // split the processed prefix only: small nodes one thread each, large ones one wave each
             for (int b = 4 * w; b < proc; b += 4 * nw) {   // <= 16 points: 16-lane groups
                 const int j = b + (lane_id() >> 4);
@@ -2696,25 +2754,25 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             }
             for (int j = w; j < proc; j += nw)
                 if (na[prev[j].node].cnt > 16) (void)qt_wave_split(na[prev[j].node], P, T);
-            __syncthreads();
+            qt_sync<WV>();
             int ne_total = 0;   // (one packed scan; the total pass only for more than one chunk, as phase 1)
-            if (proc > (int)blockDim.x) {   // block-uniform
+            if (proc > QBD) {   // block-uniform
                 int part = 0;
-                for (int j = threadIdx.x; j < proc; j += blockDim.x) part += ne4(cc[j]);
+                for (int j = qtid; j < proc; j += QBD) part += ne4(cc[j]);
                 part = wave_sum_i32(part);
                 if (lane_id() == 0) tmp[8 + w] = part;
-                __syncthreads();
+                qt_sync<WV>();
                 for (int q = 0; q < nw; q++) ne_total += tmp[8 + q];
-                __syncthreads();
+                qt_sync<WV>();
             }
             int ne_carry = 0, dv_carry = 0;
-            for (int b = 0; b < proc; b += blockDim.x) {
-                const int j = b + threadIdx.x;
+            for (int b = 0; b < proc; b += QBD) {
+                const int j = b + qtid;
                 const int4 c = j < proc ? cc[j] : make_int4(0, 0, 0, 0);
                 int tt;
-                const int ex = block_excl_scan(ne4(c) | (dv4(c) << 16), tmp, &tt);
+                const int ex = grp_excl_scan<WV>(ne4(c) | (dv4(c) << 16), tmp, &tt);
                 const int t1 = tt & 0xffff, t2 = tt >> 16, ex_ne = ex & 0xffff, ex_dv = ex >> 16;
-                if (proc <= (int)blockDim.x) ne_total = t1;
+                if (proc <= QBD) ne_total = t1;
                 if (j < proc) {
                     const int gpos = ne_total - (ne_carry + ex_ne + ne4(c));
                     qt_emit_children(na[prev[j].node], c, gpos, dv_carry + ex_dv, nb, divs, NC);
@@ -2724,11 +2782,11 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
             }
             // survivors keep their order after the new groups
             int surv = 0;
-            for (int b = 0; b < n; b += blockDim.x) {
-                const int i = b + threadIdx.x;
+            for (int b = 0; b < n; b += QBD) {
+                const int i = b + qtid;
                 const int keep = (i < n && !ia[i]) ? 1 : 0;
                 int tot;
-                const int ex = block_excl_scan(keep, tmp, &tot);
+                const int ex = grp_excl_scan<WV>(keep, tmp, &tot);
                 if (keep && ne_total + surv + ex < NC) nb[ne_total + surv + ex] = na[i];
                 surv += tot;
             }
@@ -2736,15 +2794,15 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
                 const QtNode& p = na[prev[j].node];
                 for (int q = lane_id(); q < p.cnt; q += 64) P[p.beg + q] = T[p.beg + q];
             }
-            __syncthreads();
-            if (threadIdx.x == 0) {
+            qt_sync<WV>();
+            if (qtid == 0) {
                 const int n_new = ne_total + surv;
                 if (n_new > NC) { s_fail = 1; atomicOr(fault, FAULT_QT_NODES); }
                 s_n = min(n_new, NC);
                 s_ndiv = dv_carry;
                 if (n_new >= nfeat || n_new == n || s_fail) s_state = 2;
             }
-            __syncthreads();
+            qt_sync<WV>();
             QT_STAMP(43 + 4 * min(p2_round, 5));
             p2_round++;
             QtNode* t = na; na = nb; nb = t;
@@ -2755,8 +2813,8 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
     //      per node (nodes are small at this point).
     const int n = s_n;
     uint32_t* out = sel + (long long)f * g.out_frame + L.out_base;
-    if (n > L.out_cap && threadIdx.x == 0) atomicOr(fault, FAULT_OUT_CAP);
-    for (int i = threadIdx.x; i < n && i < L.out_cap; i += blockDim.x) {
+    if (n > L.out_cap && qtid == 0) atomicOr(fault, FAULT_OUT_CAP);
+    for (int i = qtid; i < n && i < L.out_cap; i += QBD) {
         const QtNode nd = na[i];
         int bs = -1;
         uint32_t best = 0;
@@ -2770,10 +2828,10 @@ __global__ __launch_bounds__(QT_THREADS, QT_WAVES_DEF) void quadtree_kernel(Geom
         }
         out[i] = best;
     }
-    if (threadIdx.x == 0) *scnt = min(n, L.out_cap);
+    if (qtid == 0) *scnt = min(n, L.out_cap);
     QT_STAMP(63);
 #ifdef ORB_QT_STAMPS
-    if (threadIdx.x == 0 && f * g.nlevels + l < 4096) {
+    if (qtid == 0 && f * g.nlevels + l < 4096) {
         g_qt_wg[2 * (f * g.nlevels + l)] = qt_t0;
         g_qt_wg[2 * (f * g.nlevels + l) + 1] = __builtin_amdgcn_s_memtime();
     }
@@ -3391,7 +3449,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 
 __global__ __launch_bounds__(256) void qt_sort_test_kernel(QtItem* items, int n, int* scratch) {
     __shared__ int s_cnt[2];
-    qt_sort_block(items, n, scratch, scratch + n, scratch + 2 * n, scratch + 3 * n,
+    qt_sort_block<false>(items, n, scratch, scratch + n, scratch + 2 * n, scratch + 3 * n,
                   reinterpret_cast<QtItem*>(scratch + 4 * n), scratch + 6 * n, n / 3 + 2, s_cnt);
 }
 
@@ -3418,6 +3476,11 @@ struct orbx_extractor {
     size_t qt_lds = 0;
     int qt_ptc0 = 0;        // ORBX_QT_PTC0 (tuning knob): level 0 in its own launch with this LDS point capacity
     size_t qt_lds0 = 0;
+    // round 6: the small levels [qtw_l0, nlevels) as one tree per wavefront (quadtree_kernel<true>),
+    // four per workgroup, each with its own node capacity / LDS point capacity (ORBX_QT_WAVE=1; exact,
+    // measured: pan quadtree -2 %, textured +13 % -- off by default, DESIGN §4 quadtree round 6)
+    int qt_wave = 0, qt_wave_wg = 2, qtw_l0 = 0, qtw_nc = 0, qtw_ptc = 0;
+    size_t qtw_lds = 0;
     FastLds fl;
     size_t fast_lds = 0;
     int fast_cpw = 16;  // FAST cells per wavefront (4 -> 16: -2 % pan, -17 % textured: fewer first cells without a speculation hint; ORBX_FAST_CPW)
@@ -3687,7 +3750,7 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
     int PTC = 2048;
     {
         hipFuncAttributes fa{};
-        const size_t stat = hipFuncGetAttributes(&fa, (const void*)quadtree_kernel) == hipSuccess ? fa.sharedSizeBytes : 1024;
+        const size_t stat = hipFuncGetAttributes(&fa, (const void*)quadtree_kernel<false>) == hipSuccess ? fa.sharedSizeBytes : 1024;
         for (int t = QT_WAVES_DEF; t >= 2; t--) {
             const long long room = (long long)(160 * 1024 / t) - (long long)stat - (long long)node_lds;
             const int p = (int)std::min<long long>(2048, room / 8) & ~63;
@@ -3708,8 +3771,32 @@ static int setup_geometry(orbx_extractor* h, int rows, int cols) {
         if (lds0 > 156 * 1024) { PTC0 = 0; lds0 = 0; }
     }
     if (std::max(lds, lds0) > 48 * 1024)
-        ORB_HIP_TRY(hipFuncSetAttribute((const void*)quadtree_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        ORB_HIP_TRY(hipFuncSetAttribute((const void*)quadtree_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)std::max(lds, lds0)));
+    // Wave-per-tree levels: the trailing levels whose cells the partitioned gather of one wavefront takes
+    // (<= 4 x 64 cells, <= 4 roots); node capacity from their own quotas; LDS points so that
+    // qt_wave_wg workgroups of four trees fit a CU (a level with more points keeps them in HBM).
+    h->qtw_l0 = g.nlevels;
+    if (h->qt_wave) {
+        int l0w = g.nlevels;
+        while (l0w > 0 && g.lv[l0w - 1].ncells <= 4 * 64 && g.lv[l0w - 1].nroots <= 4) l0w--;
+        int ncw = 64;
+        for (int l = l0w; l < g.nlevels; l++) ncw = std::max(ncw, g.lv[l].out_cap + 8);
+        ncw = (int)align_up(ncw, 64);
+        hipFuncAttributes fa{};
+        const size_t stat = hipFuncGetAttributes(&fa, (const void*)quadtree_kernel<true>) == hipSuccess ? fa.sharedSizeBytes : 2048;
+        const long long per_wave = ((long long)(160 * 1024 / std::max(1, h->qt_wave_wg)) - (long long)stat) / 4;
+        const int ptcw = (int)std::min<long long>(2048, (per_wave - (long long)ncw * QT_NODE_BYTES) / 8) & ~63;
+        if (l0w < g.nlevels && ptcw >= 64) {
+            h->qtw_l0 = l0w;
+            h->qtw_nc = ncw;
+            h->qtw_ptc = ptcw;
+            h->qtw_lds = 4 * ((size_t)ncw * QT_NODE_BYTES + (size_t)ptcw * 8);
+            if (h->qtw_lds > 48 * 1024)
+                ORB_HIP_TRY(hipFuncSetAttribute((const void*)quadtree_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)h->qtw_lds));
+        }
+    }
     int rc;
     if ((rc = h->d_cells.reserve(std::max<size_t>(1, cells.size()) * sizeof(CellDev)))) return rc;
     if ((rc = h->d_xtab.reserve(std::max<size_t>(1, xtab.size()) * sizeof(int2)))) return rc;
@@ -3911,14 +3998,23 @@ static void launch_chunk(orbx_extractor* h, int f0, const uint8_t* d_imgs, int F
     const unsigned qt_block = h->debug_qt_block ? (unsigned)h->debug_qt_block : (unsigned)QT_THREADS;
     auto quadtree = [&](int l0, int nl, hipStream_t s) {
         if (nl <= 0) return;
+        // levels from qtw_l0 on: one tree per wavefront, four per workgroup (quadtree_kernel<true>)
+        const int lw = std::max(l0, h->qtw_l0), nw_lv = l0 + nl - lw;
+        if (nw_lv > 0) {
+            launch_timed(h, 2, quadtree_kernel<true>, dim3((unsigned)F, (unsigned)((nw_lv + 3) / 4)), dim3(qt_block),
+                         (uint32_t)h->qtw_lds, s, g, cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->qtw_nc,
+                         h->qtw_ptc, fault, lw, nw_lv);
+            nl -= nw_lv;
+            if (nl <= 0) return;
+        }
         if (h->qt_ptc0 > 0 && l0 == 0) {   // tuning knob: level 0 alone, with its own LDS point capacity
-            launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, 1u), dim3(qt_block), (uint32_t)h->qt_lds0, s, g, cellcnt,
-                         slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->qt_ptc0, fault, 0);
+            launch_timed(h, 2, quadtree_kernel<false>, dim3((unsigned)F, 1u), dim3(qt_block), (uint32_t)h->qt_lds0, s, g,
+                         cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->qt_ptc0, fault, 0, 1);
             l0 = 1;
             if (--nl <= 0) return;
         }
-        launch_timed(h, 2, quadtree_kernel, dim3((unsigned)F, (unsigned)nl), dim3(qt_block), (uint32_t)h->qt_lds, s, g,
-                           cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0);
+        launch_timed(h, 2, quadtree_kernel<false>, dim3((unsigned)F, (unsigned)nl), dim3(qt_block), (uint32_t)h->qt_lds, s,
+                     g, cellcnt, slots, h->d_cells.as<CellDev>(), Pb, Tb, sel, selcnt, h->NC, h->PTC, fault, l0, nl);
     };
     // levels l and l+1 in one pyramid_pair_kernel launch where the shapes fit its LDS rectangles
     // (returns the number of extra levels built)
@@ -4125,6 +4221,8 @@ int orbx_create(const orbx_params* params, int device, orbx_extractor** out) {
     if (const char* e = getenv("ORBX_FAST_CPW")) h->fast_cpw = std::max(1, std::min(64, atoi(e)));   // tuning knobs
     if (const char* e = getenv("ORBX_FAST_SPEC")) h->fast_spec = std::max(-1, atoi(e));   // -1: every cell
     if (const char* e = getenv("ORBX_FAST_PAIR")) h->fast_pair = atoi(e) != 0;
+    if (const char* e = getenv("ORBX_QT_WAVE")) h->qt_wave = atoi(e) != 0;
+    if (const char* e = getenv("ORBX_QT_WAVE_WG")) h->qt_wave_wg = std::max(1, std::min(4, atoi(e)));
     if (const char* e = getenv("ORBX_FAST_SPEC_FIRST")) h->fast_spec_first = atoi(e) != 0;
 
     if (const char* e = getenv("ORBX_NSUB")) h->nsub = std::max(1, std::min(8, atoi(e)));

@@ -370,7 +370,8 @@ def test_describe_grids_equal(env):
         assert np.array_equal(r[0][i, :n], a[0][i, :n]) and np.array_equal(r[1][i, :n], a[1][i, :n]), i
 
 
-def test_quadtree_block_size_guard():
+@pytest.mark.parametrize("wave", ["0", "1"])
+def test_quadtree_block_size_guard(wave, monkeypatch):
     """quadtree_kernel is written for 256-thread blocks (qt_block_split sums 4 per-wave partials and
     scatters 4 x 256-point tiles); round 5's 64-thread experiment wrote out of bounds on dense levels.
     A launch with another block size (ORBX_DEBUG_QT_BLOCK test hook) must set FAULT_BLOCK_SIZE (16),
@@ -380,6 +381,7 @@ def test_quadtree_block_size_guard():
     from orb_slam2_refactored_amd._lib import OrbError
     rng = np.random.default_rng(40)
     frames = torch.from_numpy(rng.integers(0, 256, (2, 480, 640)).astype(np.uint8)).cuda()
+    monkeypatch.setenv("ORBX_QT_WAVE", wave)   # (1: the wave-per-tree launch clears its four levels too)
     os.environ["ORBX_DEBUG_QT_BLOCK"] = "64"
     try:
         bad = ORBextractor(ORBextractor.Parameters(1000))
