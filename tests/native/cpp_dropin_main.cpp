@@ -10,7 +10,11 @@
 //                               -> out_pose_R.f64, out_pose_t.f64, out_points.f64, out_outlier.u8,
 //                                  out_iterations.i32 (2), out_ran.i32
 //   cpp_dropin localba_twice <dir>  as localba, twice on the same thread (context reuse)
+//   cpp_dropin stereo   <dir>   left.u8, right.u8 (rows x cols), meta.i32 {rows, cols, nfeatures}, cam.f32 {bf, baseline}
+//                               -> uright.f32, depth.f32 (nL each), nL.i32: Extract L and R on two std::threads
+//                               and ComputeStereoMatches on the two extractors (System.cc:449-461)
 #include <cstdio>
+#include <thread>
 #include <fstream>
 #include <iostream>
 #include <string>
@@ -110,9 +114,31 @@ static int run_localba(const std::string& d, int reps) {
     return 0;
 }
 
+static int run_stereo(const std::string& d) {
+    const auto meta = load<int32_t>(d + "/meta.i32");
+    const auto L = load<uint8_t>(d + "/left.u8");
+    const auto R = load<uint8_t>(d + "/right.u8");
+    const auto cam = load<float>(d + "/cam.f32");
+    ORB_SLAM2_AMD::ORBextractor exL{ORB_SLAM2_AMD::ORBextractor::Parameters{meta[2]}};
+    ORB_SLAM2_AMD::ORBextractor exR{ORB_SLAM2_AMD::ORBextractor::Parameters{meta[2]}};
+    std::vector<orbx_keypoint> kL, kR;
+    std::vector<uint8_t> dL, dR;
+    std::thread tL([&] { exL.Extract(L.data(), meta[0], meta[1], (size_t)meta[1], kL, dL); });
+    std::thread tR([&] { exR.Extract(R.data(), meta[0], meta[1], (size_t)meta[1], kR, dR); });
+    tL.join();
+    tR.join();
+    std::vector<float> uright, depth;
+    ORB_SLAM2_AMD::ComputeStereoMatches(exL, exR, kL.size(), cam[0], cam[1], uright, depth);
+    const int32_t n = (int32_t)kL.size();
+    save(d + "/uright.f32", uright.data(), uright.size());
+    save(d + "/depth.f32", depth.data(), depth.size());
+    save(d + "/nL.i32", &n, 1);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc != 3) {
-        std::cerr << "usage: cpp_dropin extract|match|localba|localba_twice <dir>\n";
+        std::cerr << "usage: cpp_dropin extract|match|localba|localba_twice|stereo <dir>\n";
         return 2;
     }
     const std::string mode = argv[1], dir = argv[2];
@@ -121,6 +147,7 @@ int main(int argc, char** argv) {
         if (mode == "match") return run_match(dir);
         if (mode == "localba") return run_localba(dir, 1);
         if (mode == "localba_twice") return run_localba(dir, 2);
+        if (mode == "stereo") return run_stereo(dir);
     } catch (const std::exception& e) {
         std::cerr << "error: " << e.what() << "\n";
         return 1;

@@ -1,5 +1,5 @@
 """Runs the C++ drop-in classes (include/orbslam2_amd.hpp: ORBextractor::Extract, ORBmatcher with
-checkOri, LocalBundleAdjustment) — the boundary the reference would link — on the GPU through
+checkOri, LocalBundleAdjustment, ComputeStereoMatches on two extractors) — the boundary the reference would link — on the GPU through
 tests/native/cpp_dropin_main.cpp (built by __graft_entry__.build()), and compares their outputs with
 the committed golden fixtures and the oracle."""
 import subprocess
@@ -79,6 +79,32 @@ def test_cpp_local_ba_matches_golden(tmp_path, mode):
     assert np.array_equal(outl, z["out_outlier"])
     assert tuple(it) == tuple(z["out_iterations"])
     assert int(np.fromfile(tmp_path / "out_ran.i32", np.int32)[0]) == 1
+
+
+def test_cpp_stereo_two_threads(tmp_path, oracle):
+    """The reference's stereo call shape in C++ (System.cc:449-461): Extract L and R on two std::threads,
+    then ComputeStereoMatches on the two extractors (orbx_stereo_matches_last); uright / depth bit-identical
+    to the oracle's ComputeStereoMatches on its own extraction and pyramids."""
+    from orb_slam2_refactored_amd.synth import KITTI, stereo_pair
+    L, R, _ = stereo_pair(0, 1242, 375)
+    bf, baseline = np.float32(KITTI["bf"]), np.float32(KITTI["bf"] / KITTI["fx"])
+    L.tofile(tmp_path / "left.u8")
+    R.tofile(tmp_path / "right.u8")
+    np.array([L.shape[0], L.shape[1], 2000], np.int32).tofile(tmp_path / "meta.i32")
+    np.array([bf, baseline], np.float32).tofile(tmp_path / "cam.f32")
+    run("stereo", tmp_path)
+    got_u = np.fromfile(tmp_path / "uright.f32", np.float32)
+    got_d = np.fromfile(tmp_path / "depth.f32", np.float32)
+    p = oracle.params(2000)
+    t = oracle.scale_tables(p)
+    kl, dl, _ = oracle.extract(p, L)
+    kr, dr, _ = oracle.extract(p, R)
+    exp_u, exp_d = oracle.compute_stereo_matches(kl, dl, oracle.pyramid(p, L), kr, dr, oracle.pyramid(p, R), t["scale"],
+                                                 t["inv_scale"], float(bf), float(baseline))
+    assert int(np.fromfile(tmp_path / "nL.i32", np.int32)[0]) == len(kl)
+    assert (exp_d > 0).sum() > 0.3 * len(kl)
+    assert np.array_equal(got_u.view(np.int32), exp_u.view(np.int32))
+    assert np.array_equal(got_d.view(np.int32), exp_d.view(np.int32))
 
 
 def test_cpp_local_ba_stop_on_entry(tmp_path):
