@@ -68,6 +68,19 @@ def test_local_ba_unsorted_edges(oracle):
     compare(LocalBundleAdjustment(pr), oracle.local_ba(pr))
 
 
+def test_local_ba_repeated_observation(oracle):
+    """A point observed twice by the same free keyframe (two edges with the same (point, pose)) breaks
+    the device structure build's precondition: the call takes the host build (generic path with
+    nested pair loops) and still matches the oracle."""
+    pr = make_ba_problem(10, n_kf=8, n_pts=600, n_fixed=1)
+    ep, ek = np.asarray(pr["edge_point"]), np.asarray(pr["edge_pose"])
+    fixed = np.asarray(pr["pose_fixed"]).astype(bool)
+    dup = [e for e in range(0, len(ep), 37) if not fixed[ek[e]]][:10]
+    order = np.sort(np.concatenate([np.arange(len(ep)), np.asarray(dup)]))   # duplicates next to their originals
+    pr = {k: (np.asarray(v)[order] if k.startswith("edge_") else v) for k, v in pr.items()}
+    compare(LocalBundleAdjustment(pr), oracle.local_ba(pr))
+
+
 def test_local_ba_golden():
     z = np.load(GOLDEN / "local_ba_small.npz")
     pr = {k: z[k] for k in z.files if not k.startswith("out_")}
