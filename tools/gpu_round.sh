@@ -58,7 +58,7 @@ for step in "$@"; do
     for i in 1 2; do
       for e in "${envs[@]}"; do
         env $e timeout -k 10 60 python tools/babench.py 40 > gpurun_out/babench.log 2>&1 || { tail gpurun_out/babench.log; exit 5; }
-        grep LocalBA gpurun_out/babench.log | sed "s/^/[$e] /"
+        grep LocalBA gpurun_out/babench.log | sed "s|^|[$e] |"
       done
     done ;;
   ba_timing)
@@ -108,7 +108,7 @@ for step in "$@"; do
     for i in 1 2; do
       for e in "${envs[@]}"; do
         env $e timeout -k 10 120 python tools/kbench.py ${KB_ARGS:---frames 2048 --iters 5 --pan} > gpurun_out/kb.log 2>&1 || { tail gpurun_out/kb.log; exit 8; }
-        sed "s/^/[$e] /" gpurun_out/kb.log | tail -1
+        sed "s|^|[$e] |" gpurun_out/kb.log | tail -1
       done
     done ;;
   pmc_pan|pmc_tex)
