@@ -1946,7 +1946,12 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         bool fin = false, stop_sent = false;
         BACtl last{};
         while (!fin) {
-            while (enq < max_steps && enq - seen < LOOKAHEAD) {
+            // no trial past the ones that can still be needed: each completes at most one iteration, so
+            // with as many in flight as iterations remain (the latest snapshot's), the next is enqueued
+            // only if one of those turns out a retry (round 6: the call used to end behind up to
+            // LOOKAHEAD no-op trials of 5 launches each)
+            const int remaining = seen ? last.iters_max - last.it : iters;
+            while (enq < max_steps && enq - seen < LOOKAHEAD && enq - seen < remaining) {
                 hipLaunchKernelGGL(ba_iter_kernel, gg, dim3(64), 0, st, b);
                 if (enq == 0) {   // first trial: computeLambdaInit needs Hpp before the Schur step
                     hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b);
