@@ -10,7 +10,7 @@
 #   kb_env   tools/kbench.py once per environment setting in $KB_ENVS ("A=1 B=2;A=0", ';'-separated),
 #            on $KB_ARGS (default: 2048 pan frames), two rounds
 #   ba       tools/babench.py 40 on the in-tree library, three runs
-#   ba_env   tools/babench.py 40 once per setting in $BA_ENVS (as kb_env), two rounds; ba_timing: one
+#   ba_env   tools/babench.py 40 once per setting in $BA_ENVS (as kb_env), $BA_ROUNDS rounds (2); ba_timing: one
 #            call's host-side phase times (ORBBA_DEBUG_TIMING=1)
 #   kb_sweep tools/kbench.py on pan frames at 64 .. 2048 frames per launch (per-frame stage times)
 #   stereo   tests/test_stereo_gpu.py      batests  tests/test_ba_gpu.py + tests/test_cpp_dropin_gpu.py
@@ -55,7 +55,7 @@ for step in "$@"; do
     done ;;
   ba_env)
     IFS=';' read -ra envs <<< "${BA_ENVS:-}"
-    for i in 1 2; do
+    for i in $(seq 1 ${BA_ROUNDS:-2}); do
       for e in "${envs[@]}"; do
         env $e timeout -k 10 60 python tools/babench.py 40 > gpurun_out/babench.log 2>&1 || { tail gpurun_out/babench.log; exit 5; }
         grep LocalBA gpurun_out/babench.log | sed "s|^|[$e] |"
