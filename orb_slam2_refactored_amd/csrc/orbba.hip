@@ -109,7 +109,8 @@ struct BADev {
     double* x;            // D + 3 nl
     double* rchi;         // Ea: robust chi2 per active slot
     double* part;         // scale partials: nl + np
-    double* Spart;         // (SB_SPLIT + 1) x nblk x 36: the Schur-block parts' partial blocks (+ Hpp)
+    double* Spart;         // the Schur-block parts' partial blocks (+ Hpp): (SB_SPLIT + 1) x nblk x 36 for the
+                           // global solve, (SB_SPLIT + 1) row-major D x D matrices (both orientations) for the LDS solve
     unsigned* blk_done;    // nblk: parts of the block finished (the last one forms S)
     const int* blk_diag;   // np: block index of the diagonal block (i, i)
     BACtl* ctl;
@@ -474,8 +475,12 @@ __device__ __forceinline__ void schur_block_count_in(const BADev& b, int blk, in
     // wavefront 0 only (the wavefront of the counting thread).
     __syncthreads();
     if (threadIdx.x == 0) {
+#ifndef ORBBA_DIAG_RELAXED_COUNTIN
         s_last = __hip_atomic_fetch_add(&b.blk_done[blk], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)expect - 1;
         if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else   // timing diagnostic only (no hand-off ordering; results may be wrong): the cost of the release
+        s_last = __hip_atomic_fetch_add(&b.blk_done[blk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)expect - 1;
+#endif
     }
     __syncthreads();
     if (s_last && threadIdx.x < 36) {
@@ -496,7 +501,7 @@ __device__ __forceinline__ void schur_block_count_in(const BADev& b, int blk, in
     }
 }
 
-__global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, int accum) {
+__global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, int accum, int direct) {
     BA_RETURN_IF_DONE(b);
     __shared__ double sh[1024];
     __shared__ int sslot[PA_SLOTS];
@@ -548,6 +553,12 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
         }
         // Hpp (this trial's or the kept one) as the diagonal block's extra part, republished by
         // wavefront 0 so that the counting wavefront's own release orders it
+        if (direct) {   // the LDS solve sums the parts itself (no count-in)
+            if (threadIdx.x < 36)
+                b.Spart[((long long)SB_SPLIT * D + 6 * i1 + threadIdx.x / 6) * D + 6 * i1 + threadIdx.x % 6] =
+                    b.Hpp[36 * i1 + threadIdx.x];
+            return;
+        }
         const int dblk = b.blk_diag[i1];
         if (threadIdx.x < 36) b.Spart[((long long)SB_SPLIT * b.nblk + dblk) * 36 + threadIdx.x] = b.Hpp[36 * i1 + threadIdx.x];
         schur_block_count_in(b, dblk, D, SB_SPLIT + 1);
@@ -582,9 +593,15 @@ __global__ __launch_bounds__(1024) void ba_schur_block_kernel(BADev b, int D, in
     if (threadIdx.x < 36) {
         double s = 0;
         for (int q = 0; q < SB_G; q++) s += sh[q * 36 + threadIdx.x];
-        b.Spart[((long long)part * b.nblk + blk) * 36 + threadIdx.x] = -s;
+        if (direct) {   // part matrix `part`, both orientations (as S itself)
+            double* Sp = b.Spart + (long long)part * D * D;
+            Sp[(long long)(6 * i1 + r) * D + 6 * i2 + cc] = -s;
+            if (i1 != i2) Sp[(long long)(6 * i2 + cc) * D + 6 * i1 + r] = -s;
+        } else {
+            b.Spart[((long long)part * b.nblk + blk) * 36 + threadIdx.x] = -s;
+        }
     }
-    schur_block_count_in(b, blk, D, i1 == i2 ? SB_SPLIT + 1 : SB_SPLIT);
+    if (!direct) schur_block_count_in(b, blk, D, i1 == i2 ? SB_SPLIT + 1 : SB_SPLIT);
 }
 
 
@@ -828,6 +845,33 @@ __device__ __forceinline__ void solve_trailing_tile_g(double* A, int ld, int J0,
 // outlasts wavefront 0's diagonal factorisation.  The trailing tiles go to the wavefronts that do
 // not share wavefront 0's SIMD first (waves w with w % 4 != 0; a workgroup's waves are dealt to the
 // SIMDs in turn), so the diagonal chain keeps its SIMD's issue slots.
+// S's entries (r, c), (r, c + 1) (c even: one pose block) from the Schur-block part matrices, summed
+// as schur_block_count_in forms them for the global solve: part 0 (+ the pose's Hpp part + lambda I on a
+// diagonal block), then parts 1 .. (round 6: S is no longer assembled in HBM by a last-arriving
+// workgroup, whose agent-scope release cost ba_schur_block_kernel ~4.5 us per trial).
+__device__ __forceinline__ double2 s_piece(const BADev& b, int D, int r, int c, double lam) {
+    const int i1 = r / 6, rr = r - 6 * i1, i2 = c / 6, cc = c - 6 * i2;
+    const long long pstride = (long long)D * D;
+    const double* p = b.Spart + (long long)r * D + c;
+    // Branch-free, so every piece's loads are in flight together: the Hpp matrix is zero off the
+    // diagonal pose blocks, and adding +0 there changes nothing (at most -0 -> +0 in pk, which v = 0 + pk
+    // turns into +0 anyway).
+    const bool dg = i1 == i2;
+    const double2 h = *reinterpret_cast<const double2*>(p + SB_SPLIT * pstride);
+    double2 v = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int k = 0; k < SB_SPLIT; k++) {
+        double2 pk = *reinterpret_cast<const double2*>(p + k * pstride);
+        if (k == 0) {
+            pk.x = (pk.x + h.x) + (dg && rr == cc ? lam : 0.0);
+            pk.y = (pk.y + h.y) + (dg && rr == cc + 1 ? lam : 0.0);
+        }
+        v.x += pk.x;
+        v.y += pk.y;
+    }
+    return v;
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_helpers) {
     BA_RETURN_IF_DONE(b);
@@ -841,16 +885,9 @@ __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int col = lane & 15, kq = lane >> 4;
     BA_STAMP(41);
-    // pose state for the update at the end, loaded now so its latency hides behind the solve
-    double q_pre[4] = {0, 0, 0, 0}, t_pre[3] = {0, 0, 0}, bp_pre[6] = {0, 0, 0, 0, 0, 0};
-    if (tid < b.np) {
-        const int id = b.ps_id[tid];
-        for (int j = 0; j < 4; j++) q_pre[j] = b.q[4 * id + j];
-        for (int j = 0; j < 3; j++) t_pre[j] = b.t[3 * id + j];
-        for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
-    }
     // the rhs first: its load is in flight with S's
     const double bs_v = tid < D ? b.bs[tid] : 0.0;   // D <= 128 < blockDim
+    const double lam = b.ctl->lambda;
     // S -> LDS, only its lower block triangle (row r: columns up to the end of its 16-column block):
     // the factorisation, the panels, the trailing updates and the back substitution read nothing
     // above the diagonal blocks, and the diagonal blocks' upper triangles receive Linv before they are
@@ -858,14 +895,14 @@ __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_
     // than one block) and factors it while wavefronts 1-3 load rows 16.. (the load is latency-bound:
     // 38 rows of 16-byte pieces in flight per lane, lane c = piece c of the row).  D = 6 np is even,
     // so every row of S starts 16-byte aligned.
-    const int npc = D / 2;
-    const double2* S2 = reinterpret_cast<const double2*>(b.S);
     if (wv == 0) {
         double2 v[2];
 #pragma unroll
         for (int k = 0; k < 2; k++) {   // 16 rows x 8 pieces over 64 lanes
             const int p = lane + 64 * k, r = p >> 3, c = 2 * (p & 7);
-            v[k] = r < D && c < D ? S2[r * npc + (c >> 1)] : make_double2(r == c ? 1.0 : 0.0, r == c + 1 ? 1.0 : 0.0);
+            // loads from a clamped (in-bounds) position, unconditionally: no branch around them
+            const double2 sv = s_piece(b, D, min(r, D - 1), min(c, D - 2), lam);
+            v[k] = r < D && c < D ? sv : make_double2(r == c ? 1.0 : 0.0, r == c + 1 ? 1.0 : 0.0);
         }
 #pragma unroll
         for (int k = 0; k < 2; k++) {
@@ -886,7 +923,8 @@ __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_
         for (int q = 0; q < RQ; q++) {
             const int r = min(r0 + (NW - 1) * q, D - 1);
             const int npr = min(D, (r & ~(SB - 1)) + SB) >> 1;   // pieces up to the block's end
-            v[q] = r0 + (NW - 1) * q < D && lane < npr ? S2[r * npc + lane] : make_double2(0.0, 0.0);
+            const double2 sv = s_piece(b, D, r, min(2 * lane, D - 2), lam);   // r is clamped above
+            v[q] = r0 + (NW - 1) * q < D && lane < npr ? sv : make_double2(0.0, 0.0);
         }
 #pragma unroll
         for (int q = 0; q < RQ; q++) {
@@ -978,6 +1016,16 @@ __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_
         BA_STAMP(3 + 3 * (J0 / SB));
     }
     const int ok = s_ok;
+    // pose state for the update at the end, loaded now so its latency hides behind the back
+    // substitution (loaded at the kernel start, it was live across the factorisation: with S staged
+    // from the part matrices that spilled it to scratch, each load then waited for in turn)
+    double q_pre[4] = {0, 0, 0, 0}, t_pre[3] = {0, 0, 0}, bp_pre[6] = {0, 0, 0, 0, 0, 0};
+    if (tid < b.np) {
+        const int id = b.ps_id[tid];
+        for (int j = 0; j < 4; j++) q_pre[j] = b.q[4 * id + j];
+        for (int j = 0; j < 3; j++) t_pre[j] = b.t[3 * id + j];
+        for (int j = 0; j < 6; j++) bp_pre[j] = b.bp[6 * tid + j];
+    }
     if (ok) {   // back substitution, block by block from the last: x_J on wavefront 0, then every
                 // earlier column's update (one thread per column) on the whole workgroup
         for (int i = tid; i < Dp; i += blockDim.x) y[i] *= dinv[i];   // t = D^-1 z
@@ -1011,8 +1059,7 @@ __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_
     for (int i = tid; i < D; i += blockDim.x) b.x[i] = ok ? y[i] : 0.0;
     if (tid == 0) b.ctl->ok2 = ok;
     __syncthreads();
-    // push() + oplus for the free poses, scale terms x.(lambda x + b)
-    const double lam = b.ctl->lambda;
+    // push() + oplus for the free poses, scale terms x.(lambda x + b) (lam: read at the start)
     if (tid < b.np) {   // np <= 21 < blockDim
         const int i = tid;
         const int id = b.ps_id[i];
@@ -1888,10 +1935,11 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         have_structure = true;
         }
         // system buffers
+        const size_t spart_n = (size_t)(SB_SPLIT + 1) * (glob ? 36 * (size_t)nblk : (size_t)D * D);   // + Hpp part
         const size_t ybytes = carve_size<double>(72 * (size_t)Ea) + carve_size<double>(24 * (size_t)Ea) +
                               carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +
                               carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
-                              carve_size<double>((size_t)D * D) + carve_size<double>((size_t)(SB_SPLIT + 1) * nblk * 36) +
+                              carve_size<double>((size_t)D * D) + carve_size<double>(spart_n) +
                               carve_size<unsigned>((size_t)nblk) + carve_size<double>(D) +
                               carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
                               carve_size<double>(nl + np) + (glob ? carve_size<double>((size_t)Dp * (Dp + 1)) : 0) +
@@ -1907,7 +1955,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.Hpp = cy.take<double>(36 * (size_t)np);
         b.bp = cy.take<double>(6 * (size_t)np);
         b.S = cy.take<double>((size_t)D * D);
-        b.Spart = cy.take<double>((size_t)(SB_SPLIT + 1) * nblk * 36);   // + the diagonal blocks' Hpp part
+        b.Spart = cy.take<double>(spart_n);
         b.blk_done = cy.take<unsigned>((size_t)nblk);
         b.bs = cy.take<double>(D);
         b.x = cy.take<double>(D + 3 * (size_t)nl);
@@ -1915,7 +1963,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.part = cy.take<double>(nl + np);
         b.Sg = glob ? cy.take<double>((size_t)Dp * (Dp + 1)) : nullptr;
         double* d_wgpart = cy.take<double>(2 * (size_t)((nl * 8 + 63) / 64));   // point-update workgroup partials
-        if ((rc2 = fills.add(b.J, 72 * 8 * (size_t)Ea, 0, st)) || (rc2 = fills.add(b.S, (size_t)D * D * 8, 0, st)) ||
+        if ((rc2 = fills.add(b.J, 72 * 8 * (size_t)Ea, 0, st)) || (rc2 = glob ? fills.add(b.S, (size_t)D * D * 8, 0, st)
+                         : fills.add(b.Spart, spart_n * 8, 0, st)) ||
             (rc2 = fills.add(b.blk_done, (size_t)nblk * 4, 0, st)) || (rc2 = fills.flush(st)))
             return rc2;
         const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
@@ -1957,7 +2006,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                     hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b);
                     hipLaunchKernelGGL(ba_schur_point_kernel, gg, dim3(64), 0, st, b);
                 }
-                hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1 + np, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1);
+                hipLaunchKernelGGL(ba_schur_block_kernel, dim3(nblk + 1 + np, SB_SPLIT), dim3(1024), 0, st, b, D, enq == 0 ? 0 : 1,
+                                   glob ? 0 : 1);
                 if (glob) hipLaunchKernelGGL(ba_solve_global_kernel, dim3(1), dim3(1024), ldlt_lds, st, b, D);
                 else if (solve256) hipLaunchKernelGGL(ba_solve_kernel<256>, dim3(1), dim3(256), ldlt_lds, st, b, D, 1);
                 else hipLaunchKernelGGL(ba_solve_kernel<1024>, dim3(1), dim3(1024), ldlt_lds, st, b, D, simd0_helpers);
