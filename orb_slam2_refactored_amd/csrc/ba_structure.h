@@ -35,15 +35,38 @@ struct HostStructure {
 // caller then runs build_structure) when a precondition fails.
 inline bool build_structure_counts(int P, int N, const uint8_t* fixed, const int* ep, const int* ek, int E,
                                    HostStructure& s) {
-    for (int e = 1; e < E; e++)
-        if (ep[e] < ep[e - 1]) return false;
+    // one pass over the edges: the sort check, the point runs and the poses that have edges
     s.pa.assign(P, 0);
+    s.hl.assign(N, -1);
+    s.pt_id.resize(N);
+    s.pt_beg.resize((size_t)N + 1);
+    int nl = 0;
+    {
+        uint8_t* pa = s.pa.data();
+        int* hl = s.hl.data();
+        int* pid = s.pt_id.data();
+        int* pb = s.pt_beg.data();
+        int prev = -1;
+        for (int e = 0; e < E; e++) {
+            const int x = ep[e];
+            if (x != prev) {
+                if (x < prev) return false;   // not point-sorted
+                hl[x] = nl;
+                pid[nl] = x;
+                pb[nl++] = e;
+                prev = x;
+            }
+            pa[ek[e]] = 1;
+        }
+        pb[nl] = E;
+    }
+    s.pt_beg.resize((size_t)nl + 1);
+    s.pt_id.resize(nl);
     s.hp.resize(P);
     s.ps_id.resize(P);
     int np = 0;
     {
-        uint8_t* pa = s.pa.data();
-        for (int e = 0; e < E; e++) pa[ek[e]] = 1;
+        const uint8_t* pa = s.pa.data();
         int* hp = s.hp.data();
         int* pid = s.ps_id.data();
         for (int i = 0; i < P; i++) {
@@ -52,24 +75,6 @@ inline bool build_structure_counts(int P, int N, const uint8_t* fixed, const int
         }
     }
     s.ps_id.resize(np);
-    s.hl.assign(N, -1);
-    s.pt_id.resize(N);
-    s.pt_beg.resize((size_t)N + 1);
-    int nl = 0;
-    {
-        int* hl = s.hl.data();
-        int* pid = s.pt_id.data();
-        int* pb = s.pt_beg.data();
-        for (int e = 0; e < E; e++)
-            if (e == 0 || ep[e] != ep[e - 1]) {
-                hl[ep[e]] = nl;
-                pid[nl] = ep[e];
-                pb[nl++] = e;
-            }
-        pb[nl] = E;
-    }
-    s.pt_beg.resize((size_t)nl + 1);
-    s.pt_id.resize(nl);
     const int W = (nl + 63) >> 6;
     s.col.assign((size_t)np * W, 0ull);
     s.ps_beg.assign((size_t)np + 1, 0);

@@ -21,9 +21,14 @@
 // Every reduction runs in a fixed order, so results are bit-reproducible run to run.  The LM
 // control scalars live on the device; the host reads one small status block per trial to decide
 // whether to run another (the reference's loop condition), and polls the stop flag like g2o.
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <vector>
 
@@ -86,6 +91,7 @@ struct BADev {
     const int* hl;        // N: point index or -1
     const int* pt_beg;    // nl+1: CSR of active slots per active point (slot order)
     const int* pt_slot;
+    int4* pt_rec;         // Ea, per point-list entry u: {k = pt_slot[u], e = act[k], pose ek[e], hp[ek[e]]}
     const int* pt_id;     // nl: point id of point index
     const int* ps_beg;    // np+1: CSR of active slots per free pose
     const int* ps_slot;
@@ -183,8 +189,9 @@ __device__ __forceinline__ void schur_point_terms(const BADev& b, int l, int sub
 #pragma unroll
     for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1] + Di[3 * i + 2] * bl[2];
     for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
-        const int k = b.pt_slot[u];
-        if (b.hp[b.ek[b.act[k]]] < 0) continue;
+        const int4 rc = b.pt_rec[u];
+        if (rc.w < 0) continue;
+        const int k = rc.x;
         const double* Hpl = b.J + (long long)k * 72 + 54;
         double* W = b.W + (long long)k * 24;
         for (int r = 0; r < 6; r++) {
@@ -220,14 +227,23 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
         return;
     }
     if (live) {
+        const double* Xl = b.X + 3 * b.pt_id[l];   // = X + 3 ep[e] for every edge of the point
         for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
-            const int k = b.pt_slot[u];
-            const int e = b.act[k];
-            if (b.level[e]) continue;   // a level-1 edge (second optimize()): no error, no terms (J stays 0)
-            const int pi = b.ek[e];
+            const int4 rc = b.pt_rec[u];
+            const int k = rc.x, e = rc.y;
+            if (b.level[e]) {   // a level-1 edge (second optimize()): no error, no terms -- its pose-side
+                                // terms are zeros (written here: the call no longer clears J per optimize())
+                if (rc.w >= 0) {
+                    double* J = b.J + (long long)k * 72;
+#pragma unroll
+                    for (int i = 12; i < 72; i++) J[i] = 0.0;
+                }
+                continue;
+            }
+            const int pi = rc.z;
             const double* q4 = b.q + 4 * pi;
             double Xc[3], R[9];
-            se3_map(q4, b.t + 3 * pi, b.X + 3 * b.ep[e], Xc);
+            se3_map(q4, b.t + 3 * pi, Xl, Xc);
             chi += edge_error(b, e, Xc);
             q_to_R(q4, R);
             // Jacobians with one reciprocal of z (g2o divides by z / z^2 in every term; the
@@ -287,7 +303,7 @@ __global__ __launch_bounds__(64) void ba_iter_kernel(BADev b) {
                     H[3 * i + j] += h;
                 }
             }
-            if (b.hp[pi] >= 0) {
+            if (rc.w >= 0) {   // free pose
                 double* J = b.J + (long long)k * 72;
 #pragma unroll
                 for (int i = 0; i < 6; i++) {
@@ -1078,17 +1094,29 @@ __global__ __launch_bounds__(NT) void ba_solve_kernel(BADev b, int D, int simd0_
     BA_STAMP(42);
 }
 
+// The point lists' entry records (once per call, after the structure): one 16-byte load per entry in
+// the per-trial point kernels instead of the pt_slot -> act -> ek -> hp chain of dependent loads.  The
+// host-built structure only; the device build writes them in ba_struct_slots_kernel.
+__global__ __launch_bounds__(256) void ba_rec_kernel(BADev b) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= b.Ea) return;
+    const int k = b.pt_slot[u], e = b.act[k], pi = b.ek[e];
+    b.pt_rec[u] = make_int4(k, e, pi, b.hp[pi]);
+}
+
 // ---- Device half of the structure build (round 6; host half: ba_structure.h build_structure_counts).
 // The (free pose, point) slot table, pose-major (row i: the edge of pose i at each point, -1 where
-// none; memset to -1 first), and the identity lists of the point-sorted case.
+// none; memset to -1 first), the identity lists of the point-sorted case and their entry records.
 __global__ void ba_struct_slots_kernel(const int* __restrict__ ep, const int* __restrict__ ek,
                                        const int* __restrict__ hp, const int* __restrict__ hl, int E, int nl,
-                                       int* __restrict__ act, int* __restrict__ pt_slot, int* __restrict__ slot_of) {
+                                       int* __restrict__ act, int* __restrict__ pt_slot, int* __restrict__ slot_of,
+                                       int4* __restrict__ rec) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     act[e] = e;
     pt_slot[e] = e;
-    const int h = hp[ek[e]];
+    const int pi = ek[e], h = hp[pi];
+    rec[e] = make_int4(e, e, pi, h);
     if (h >= 0) slot_of[(long long)h * nl + hl[ep[e]]] = e;
 }
 // One workgroup per pose-pair block (i1, i2): the points with an edge to both, ascending, as (edge of
@@ -1303,8 +1331,8 @@ __global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D, dou
     double cl[3] = {0, 0, 0};
     if (live)
         for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
-            const int k = b.pt_slot[u];
-            const int ip = b.hp[b.ek[b.act[k]]];
+            const int4 rc = b.pt_rec[u];
+            const int k = rc.x, ip = rc.w;
             if (ip < 0) continue;
             const double* Hpl = b.J + (long long)k * 72 + 54;
             for (int c = 0; c < 3; c++) {
@@ -1339,9 +1367,10 @@ __global__ __launch_bounds__(64) void ba_point_update_kernel(BADev b, int D, dou
             b.part[l] = part;
         }
         for (int u = b.pt_beg[l] + sub; u < b.pt_beg[l + 1]; u += GRP) {
-            const int e = b.act[b.pt_slot[u]];
+            const int4 rc = b.pt_rec[u];
+            const int e = rc.y;
             if (b.level[e]) continue;   // g2o computes active errors only: a level-1 edge keeps its _error
-            const int pi = b.ek[e];
+            const int pi = rc.z;
             double Xc[3];
             se3_map(b.q + 4 * pi, b.t + 3 * pi, Xn, Xc);
             chi += edge_error(b, e, Xc);
@@ -1557,14 +1586,16 @@ namespace {
 // Grow-only pinned host buffer.  Only grown when no copy from it is in flight.
 struct PinnedBuf {
     char* ptr = nullptr;
+    char* dptr = nullptr;   // the device's view (mapped buffers)
     size_t cap = 0;
-    int ensure(size_t bytes) {
+    int ensure(size_t bytes, bool mapped = false) {
         if (bytes <= cap) return ORB_OK;
         if (ptr) (void)hipHostFree(ptr);
-        ptr = nullptr;
+        ptr = dptr = nullptr;
         cap = 0;
         const size_t c = align_up(bytes + bytes / 4, 1 << 16);
-        ORB_HIP_TRY(hipHostMalloc((void**)&ptr, c, hipHostMallocDefault));
+        ORB_HIP_TRY(hipHostMalloc((void**)&ptr, c, mapped ? hipHostMallocMapped : hipHostMallocDefault));
+        if (mapped) ORB_HIP_TRY(hipHostGetDevicePointer((void**)&dptr, ptr, 0));
         cap = c;
         return ORB_OK;
     }
@@ -1573,11 +1604,79 @@ struct PinnedBuf {
     }
 };
 
+// A helper thread per calling thread (round 6): it runs the host half of the structure build (the
+// counts, ~50 us at C4) while the calling thread stages and enqueues the problem upload, instead of
+// after it.  Started on first use; a process that forked after that (the thread does not exist in the
+// child) runs the job on the calling thread.
+class HostHelper {
+public:
+    void post(std::function<void()> f) {
+        if (!start()) {   // no helper in this process: run it here
+            f();
+            done_.store(true, std::memory_order_release);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = std::move(f);
+            has_ = true;
+            done_.store(false, std::memory_order_relaxed);
+        }
+        cv_.notify_one();
+    }
+    void wait() const {   // the job is short: spin (yielding) rather than sleep
+        while (!done_.load(std::memory_order_acquire)) std::this_thread::yield();
+    }
+    ~HostHelper() {
+        if (th_.joinable()) {
+            if (pid_ != getpid()) {   // forked child: the thread object has no thread behind it
+                th_.detach();
+                return;
+            }
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                quit_ = true;
+            }
+            cv_.notify_one();
+            th_.join();
+        }
+    }
+
+private:
+    bool start() {
+        if (th_.joinable()) return pid_ == getpid();
+        pid_ = getpid();
+        th_ = std::thread([this] { run(); });
+        return true;
+    }
+    void run() {
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            cv_.wait(lk, [&] { return has_ || quit_; });
+            if (quit_) return;
+            std::function<void()> f = std::move(job_);
+            has_ = false;
+            lk.unlock();
+            f();
+            done_.store(true, std::memory_order_release);
+            lk.lock();
+        }
+    }
+    std::thread th_;
+    pid_t pid_ = 0;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::function<void()> job_;
+    bool has_ = false, quit_ = false;
+    std::atomic<bool> done_{true};
+};
+
 // Device-resident LocalBA workspace (one per thread: LocalMapping runs one LocalBA at a time).
 struct BAContext {
+    HostHelper helper;   // destroyed last (declared first): no job is in flight after a call returns
     int device = -1;
     hipStream_t st = nullptr;
-    DevBuf prob, state, structure, sys, ctlbuf, resbuf;
+    DevBuf prob, state, structure, sys, ctlbuf;
     BACtl* h_ctl = nullptr;   // pinned
     BACtl* h_ring = nullptr;  // pinned, device-mapped control snapshots, one per step in flight
     BACtl* d_ring = nullptr;
@@ -1590,7 +1689,7 @@ struct BAContext {
     void reset_device() {
         if (device >= 0) (void)hipSetDevice(device);
         if (st) (void)hipStreamSynchronize(st);
-        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release(); resbuf.release();
+        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
         if (st) { (void)hipStreamDestroy(st); st = nullptr; }
         if (h_ring) { (void)hipHostFree(h_ring); h_ring = nullptr; d_ring = nullptr; }
         if (h_stop) { (void)hipHostFree(h_stop); h_stop = nullptr; d_stop = nullptr; }
@@ -1600,7 +1699,7 @@ struct BAContext {
     ~BAContext() {
         if (h_stop) (void)hipHostFree(h_stop);
         if (h_ring) (void)hipHostFree(h_ring);
-        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release(); resbuf.release();
+        prob.release(); state.release(); structure.release(); sys.release(); ctlbuf.release();
         if (h_ctl) (void)hipHostFree(h_ctl);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -1713,6 +1812,29 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     *C.h_stop = stopped() ? 1 : 0;
 
     mark("context");
+    // The host half of the structure build: on the helper thread, in parallel with the staging below
+    // (default path).  ORBBA_STRUCT: "host" = the whole build on the host (generic), "sorted" = the
+    // host's point-sorted variant; default: counts on the host, lists on the device when the edges are
+    // point-sorted (read per call: tests compare the forms in one process).
+    thread_local HostStructure hs;   // capacity kept across calls
+    const char* smode_env = getenv("ORBBA_STRUCT");
+    const std::string smode = smode_env ? smode_env : "";
+    const bool try_counts = smode != "host" && smode != "sorted" && smode != "generic";
+    bool counts_ok = false;
+    struct HelperWait {   // every return path waits for a posted job (it writes hs and counts_ok)
+        HostHelper& h;
+        bool on;
+        ~HelperWait() {
+            if (on) h.wait();
+        }
+    } helper_wait{C.helper, false};
+    if (try_counts && E >= 1024) {
+        HostStructure* hsp = &hs;   // (the helper's own thread_local hs is another object)
+        C.helper.post([hsp, &counts_ok, P, N, E, pr] {
+            counts_ok = build_structure_counts(P, N, pr->pose_fixed, pr->edge_point, pr->edge_pose, E, *hsp);
+        });
+        helper_wait.on = true;
+    }
     // initial estimates: SE3Quat(R, t) -> Quaterniond(R) normalised (Optimizer.cc:145-150)
     std::vector<double> q0(4 * (size_t)P);
     for (int i = 0; i < P; i++) {
@@ -1763,7 +1885,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     if ((rc = C.state.reserve(state_bytes))) return rc;
     if ((rc = C.ctlbuf.reserve(sizeof(BACtl) + 64))) return rc;
     if ((rc = C.h_prob.ensure(up_bytes))) return rc;
-    if ((rc = C.h_res.ensure(res_bytes))) return rc;
+    if ((rc = C.h_res.ensure(res_bytes, true))) return rc;   // mapped: the final gather writes it directly
     Carve cp{C.prob.as<char>()}, hp{C.h_prob.ptr}, cs{C.state.as<char>()};
     BADev b;
     std::memset(&b, 0, sizeof(b));
@@ -1814,7 +1936,6 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
 
     mark("staging + upload enqueued");
     std::vector<uint8_t> level(E, 0);
-    thread_local HostStructure hs;   // capacity kept across calls
     bool hook_stopped = false;   // the device ended a loop on the stop flag (or the test hook)
     // ------------------------------------------------------------------ one optimize(iters)
     // The structure is built once, for the first optimize() (every edge at level 0).  The second
@@ -1826,16 +1947,17 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     bool have_classified = false;   // the outlier classification ran (second optimize())
     auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
         bool dev_build = false;   // act / pt_slot / ps_slot / blk_pair filled on the device
+        const bool fresh = !have_structure;   // the first optimize() of the call
         if (!have_structure) {
-            // ORBBA_STRUCT: "host" = the whole build on the host (generic), "sorted" = the host's
-            // point-sorted variant; default: counts on the host, lists on the device when the edges
-            // are point-sorted (read per call: tests compare the forms in one process)
-            const char* sm = getenv("ORBBA_STRUCT");
-            const std::string mode = sm ? sm : "";
-            dev_build = mode != "host" && mode != "sorted" && mode != "generic" &&
-                        build_structure_counts(P, N, pr->pose_fixed, pr->edge_point, pr->edge_pose, E, hs);
+            if (helper_wait.on) {   // the counts posted at entry
+                C.helper.wait();
+                helper_wait.on = false;
+                dev_build = counts_ok;
+            } else {
+                dev_build = try_counts && build_structure_counts(P, N, pr->pose_fixed, pr->edge_point, pr->edge_pose, E, hs);
+            }
             if (!dev_build)
-                build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs, mode == "sorted");
+                build_structure(P, N, level, pr->pose_fixed, pr->edge_point, pr->edge_pose, hs, smode == "sorted");
             mark(dev_build ? "build_structure (counts)" : "build_structure");
         }
         const int Ea = hs.n_act, np = hs.np, nl = hs.nl, D = 6 * np;
@@ -1869,7 +1991,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         const size_t sbytes = carve_size<int>(P) + carve_size<int>(N) + carve_size<int>(nl + 1) + carve_size<int>(nl) +
                               carve_size<int>(np + 1) + carve_size<int>(np) + carve_size<int>(nblk) * 2 +
                               carve_size<int>(nblk + 1) + carve_size<int>(np) + carve_size<int>(Ea) * 2 +
-                              carve_size<int>(nps) + carve_size<int2>(npairs) +
+                              carve_size<int>(nps) + carve_size<int2>(npairs) + carve_size<int4>(Ea) +
                               (dev_build ? carve_size<int>((size_t)np * nl) : 0);
         int rc2;
         if (!have_structure) {
@@ -1895,6 +2017,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         int* d_pts = cr.take<int>(Ea);
         int* d_pss = cr.take<int>(nps);
         int2* d_bp = cr.take<int2>(npairs);
+        const size_t list_bytes = cr.off;   // the host build uploads up to here
+        int4* d_rec = cr.take<int4>(Ea);
         put(hs.hp.data(), 4 * (size_t)P, (char*)hr.take<int>(P));
         put(hs.hl.data(), 4 * (size_t)N, (char*)hr.take<int>(N));
         put(hs.pt_beg.data(), 4 * (size_t)(nl + 1), (char*)hr.take<int>(nl + 1));
@@ -1915,7 +2039,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             if ((rc2 = fills.add(d_slot, 4 * (size_t)np * nl, 0xff, st)) || (rc2 = fills.flush(st))) return rc2;
             if (Ea)
                 hipLaunchKernelGGL(ba_struct_slots_kernel, dim3((Ea + 255) / 256), dim3(256), 0, st, d_ep, d_ek, d_hp, d_hl,
-                                   Ea, nl, d_act, d_pts, d_slot);
+                                   Ea, nl, d_act, d_pts, d_slot, d_rec);
             if (nblk && nl)
                 hipLaunchKernelGGL(ba_struct_pairs_kernel, dim3(nblk), dim3(1024), 0, st, d_b1, d_b2, d_bb, d_psb, d_slot, nl,
                                    d_bp, d_pss);
@@ -1925,13 +2049,16 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             put(hs.pt_slot.data(), 4 * (size_t)Ea, (char*)hr.take<int>(Ea));
             put(hs.ps_slot.data(), 4 * nps, (char*)hr.take<int>(nps));
             put(hs.blk_pair.data(), 8 * npairs, (char*)hr.take<int2>(npairs));
-            ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, cr.off, hipMemcpyHostToDevice, st));
+            ORB_HIP_TRY(hipMemcpyAsync(C.structure.ptr, C.h_struct.ptr, list_bytes, hipMemcpyHostToDevice, st));
         }
         b.Ea = Ea; b.np = np; b.nl = nl; b.nblk = nblk;
         b.act = d_act; b.hp = d_hp; b.hl = d_hl; b.pt_beg = d_ptb; b.pt_slot = d_pts; b.pt_id = d_pti;
         b.ps_beg = d_psb; b.ps_slot = d_pss; b.ps_id = d_psi; b.blk_i1 = d_b1; b.blk_i2 = d_b2; b.blk_beg = d_bb;
         b.blk_pair = d_bp;
         b.blk_diag = d_bd;
+        b.pt_rec = d_rec;
+        if (Ea && !dev_build) hipLaunchKernelGGL(ba_rec_kernel, dim3((Ea + 255) / 256), dim3(256), 0, st, b);
+        ORB_HIP_TRY(hipGetLastError());
         have_structure = true;
         }
         // system buffers
@@ -1963,10 +2090,13 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         b.part = cy.take<double>(nl + np);
         b.Sg = glob ? cy.take<double>((size_t)Dp * (Dp + 1)) : nullptr;
         double* d_wgpart = cy.take<double>(2 * (size_t)((nl * 8 + 63) / 64));   // point-update workgroup partials
-        if ((rc2 = fills.add(b.J, 72 * 8 * (size_t)Ea, 0, st)) || (rc2 = glob ? fills.add(b.S, (size_t)D * D * 8, 0, st)
-                         : fills.add(b.Spart, spart_n * 8, 0, st)) ||
-            (rc2 = fills.add(b.blk_done, (size_t)nblk * 4, 0, st)) || (rc2 = fills.flush(st)))
+        // (J needs no clearing: every linearising trial writes the entries that are read -- those of the
+        // edges to free poses, zeros for a level-1 edge.  S / the part matrices are zero where no pose
+        // pair block is, and the second optimize() keeps the structure, so they are cleared once.)
+        if (fresh && ((rc2 = glob ? fills.add(b.S, (size_t)D * D * 8, 0, st) : fills.add(b.Spart, spart_n * 8, 0, st)) ||
+                      (rc2 = fills.add(b.blk_done, (size_t)nblk * 4, 0, st))))
             return rc2;
+        if ((rc2 = fills.flush(st))) return rc2;
         const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
         {   // the dynamic LDS limit is a process-wide attribute of the kernel: raised (a host call) only
             // when a call needs more than any call before it on this device, never lowered
@@ -2078,9 +2208,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             if ((rc = optimize(10, &res->iterations[1], &res->chi2[1]))) return rc;
         }
     }
-    // final classification + poses / points gathered into one result region (h_res's layout), one copy
-    if ((rc = C.resbuf.reserve(res_bytes))) return rc;
-    Carve dres{C.resbuf.as<char>()}, hres{C.h_res.ptr};
+    // final classification + poses / points gathered straight into the mapped pinned result region
+    // (round 6: no device-to-host copy behind the kernel)
+    Carve dres{C.h_res.dptr}, hres{C.h_res.ptr};
     double* rq = dres.take<double>(4 * (size_t)P);
     double* rt = dres.take<double>(3 * (size_t)P);
     double* rX = dres.take<double>(3 * (size_t)N);
@@ -2093,11 +2223,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     double* hc = hres.take<double>(E);
     if ((rc = fills.flush(st))) return rc;   // (a call that optimised nothing still classifies)
     if (const int nt = std::max(E, std::max(N, P))) {
-        hipLaunchKernelGGL(ba_classify_kernel, dim3((nt + 255) / 256), dim3(256), 0, st, b, ro, rch, (uint8_t*)nullptr, 0,
-                           rq, rt, rX);
+        hipLaunchKernelGGL(ba_classify_kernel, dim3((nt + 255) / 256), dim3(256), 0, st, b, ro,
+                           res->edge_chi2 ? rch : (double*)nullptr, (uint8_t*)nullptr, 0, rq, rt, rX);
         ORB_HIP_TRY(hipGetLastError());
-        ORB_HIP_TRY(hipMemcpyAsync(C.h_res.ptr, C.resbuf.ptr, res->edge_chi2 ? dres.off : (size_t)(reinterpret_cast<char*>(rch) - C.resbuf.as<char>()),
-                                   hipMemcpyDeviceToHost, st));
     }
     ORB_HIP_TRY(hipStreamSynchronize(st));
     mark("results copied");
@@ -2109,6 +2237,10 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     for (int i = 0; i < P; i++) {
         q_to_R(&hq[4 * i], res->pose_R + 9 * i);
         if (res->pose_q) std::memcpy(res->pose_q + 4 * i, &hq[4 * i], 32);
+    }
+    if (helper_wait.on) {   // (a call that optimised nothing never waited for the counts)
+        C.helper.wait();
+        helper_wait.on = false;
     }
     // the dense pair-block scratch (slot_of: nl x np ints, col: np x nl/64 words) of a very large window
     // is released rather than kept with the thread (C4 keeps its 0.3 MB)

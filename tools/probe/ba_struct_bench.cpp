@@ -33,5 +33,16 @@ int main(int argc, char** argv) {
     printf("build_structure %.1f us (P %d N %d E %d np %d nl %d blocks %zu pairs %zu) checksum %016llx\n",
            std::chrono::duration<double, std::micro>(t1 - t0).count() / reps, P, N, E, hs.np, hs.nl, hs.blk_i1.size(),
            hs.blk_pair.size(), h);
+    // the host half of the device build (the default path)
+    orbamd_host::HostStructure hc;
+    if (!orbamd_host::build_structure_counts(P, N, fixed.data(), ep.data(), ek.data(), E, hc)) return 2;
+    t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; r++) orbamd_host::build_structure_counts(P, N, fixed.data(), ep.data(), ek.data(), E, hc);
+    t1 = std::chrono::steady_clock::now();
+    h = 1469598103934665603ull;
+    mix(hc.hp); mix(hc.hl); mix(hc.pt_beg); mix(hc.pt_id); mix(hc.ps_beg); mix(hc.ps_id); mix(hc.blk_i1); mix(hc.blk_i2);
+    mix(hc.blk_beg);
+    printf("build_structure_counts %.1f us (blocks %zu pairs %d) checksum %016llx\n",
+           std::chrono::duration<double, std::micro>(t1 - t0).count() / reps, hc.blk_i1.size(), hc.n_pairs, h);
     return 0;
 }
