@@ -1715,9 +1715,13 @@ struct BAFill {
     unsigned long long n[BA_FILL_MAX];
     unsigned v[BA_FILL_MAX];
     int cnt;
+    BACtl* ctl;       // when set: the first optimize()'s control block, written whole (ba_ctl_start_kernel's
+    BACtl ctl_init;   // job for that call, one launch earlier)
 };
 __global__ __launch_bounds__(256) void ba_fill_kernel(BAFill f) {
     const unsigned long long gt = blockIdx.x * 256ull + threadIdx.x, gs = gridDim.x * 256ull;
+    if (f.ctl && gt < sizeof(BACtl) / 8)
+        reinterpret_cast<unsigned long long*>(f.ctl)[gt] = reinterpret_cast<const unsigned long long*>(&f.ctl_init)[gt];
     for (int s = 0; s < f.cnt; s++) {
         uint8_t* p = static_cast<uint8_t*>(f.p[s]);
         const unsigned b = f.v[s] & 0xffu, w = b * 0x01010101u;
@@ -1742,11 +1746,16 @@ struct FillQueue {
         bytes += n;
         return ORB_OK;
     }
+    void set_ctl(BACtl* c, const BACtl& init) {
+        f.ctl = c;
+        f.ctl_init = init;
+    }
     int flush(hipStream_t st) {
-        if (!f.cnt) return ORB_OK;
+        if (!f.cnt && !f.ctl) return ORB_OK;
         const unsigned nb = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(1024, bytes / (16 * 256 * 2)));
         hipLaunchKernelGGL(ba_fill_kernel, dim3(nb), dim3(256), 0, st, f);
         f.cnt = 0;
+        f.ctl = nullptr;
         bytes = 0;
         ORB_HIP_TRY(hipGetLastError());
         return ORB_OK;
@@ -1926,7 +1935,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     b.stop = stop_flag ? C.d_stop : nullptr;
     b.stop_after = stop_after;
     FillQueue fills;   // flushed (one launch) before the first kernel that reads them
-    if ((rc = fills.add(b.ctl, sizeof(BACtl), 0, st))) return rc;   // trials / stopped count over the whole call
+    // (the control block is written whole by the first optimize()'s fill: trials / stopped count from 0
+    // over the whole call)
     ORB_HIP_TRY(hipMemcpyAsync(C.prob.ptr, C.h_prob.ptr, cp.off, hipMemcpyHostToDevice, st));
     if ((rc = fills.add(b.robust, E, 1, st)) || (rc = fills.add(d_level, E, 0, st)) ||
         (rc = fills.add(b.err, 24 * (size_t)E, 0, st)))
@@ -1994,6 +2004,49 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                               carve_size<int>(nps) + carve_size<int2>(npairs) + carve_size<int4>(Ea) +
                               (dev_build ? carve_size<int>((size_t)np * nl) : 0);
         int rc2;
+        // system buffers (carved before the structure upload, so that their clears and the control
+        // block ride on the structure's fill launch)
+        const size_t spart_n = (size_t)(SB_SPLIT + 1) * (glob ? 36 * (size_t)nblk : (size_t)D * D);   // + Hpp part
+        const size_t ybytes = carve_size<double>(72 * (size_t)Ea) + carve_size<double>(24 * (size_t)Ea) +
+                              carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +
+                              carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
+                              carve_size<double>((size_t)D * D) + carve_size<double>(spart_n) +
+                              carve_size<unsigned>((size_t)nblk) + carve_size<double>(D) +
+                              carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
+                              carve_size<double>(nl + np) + (glob ? carve_size<double>((size_t)Dp * (Dp + 1)) : 0) +
+                              carve_size<double>(2 * (size_t)((nl * 8 + 63) / 64)) +
+                              64;
+        if ((rc2 = C.sys.reserve(ybytes))) return rc2;
+        Carve cy{C.sys.as<char>()};
+        b.J = cy.take<double>(72 * (size_t)Ea);
+        b.W = cy.take<double>(24 * (size_t)Ea);
+        b.Hll = cy.take<double>(9 * (size_t)nl);
+        b.Dinv = cy.take<double>(9 * (size_t)nl);
+        b.bl = cy.take<double>(3 * (size_t)nl);
+        b.Hpp = cy.take<double>(36 * (size_t)np);
+        b.bp = cy.take<double>(6 * (size_t)np);
+        b.S = cy.take<double>((size_t)D * D);
+        b.Spart = cy.take<double>(spart_n);
+        b.blk_done = cy.take<unsigned>((size_t)nblk);
+        b.bs = cy.take<double>(D);
+        b.x = cy.take<double>(D + 3 * (size_t)nl);
+        b.rchi = cy.take<double>(std::max(Ea, nl));
+        b.part = cy.take<double>(nl + np);
+        b.Sg = glob ? cy.take<double>((size_t)Dp * (Dp + 1)) : nullptr;
+        double* d_wgpart = cy.take<double>(2 * (size_t)((nl * 8 + 63) / 64));   // point-update workgroup partials
+        // (J needs no clearing: every linearising trial writes the entries that are read -- those of the
+        // edges to free poses, zeros for a level-1 edge.  S / the part matrices are zero where no pose
+        // pair block is, and the second optimize() keeps the structure, so they are cleared once.)
+        if (fresh && ((rc2 = glob ? fills.add(b.S, (size_t)D * D * 8, 0, st) : fills.add(b.Spart, spart_n * 8, 0, st)) ||
+                      (rc2 = fills.add(b.blk_done, (size_t)nblk * 4, 0, st))))
+            return rc2;
+        if (fresh) {   // the first optimize()'s control block (ba_ctl_start_kernel(iters, 0) on a zeroed block)
+            BACtl init{};
+            init.done = iters <= 0 ? 1 : 0;
+            init.need_lin = 1;
+            init.iters_max = iters;
+            fills.set_ctl(b.ctl, init);
+        }
         if (!have_structure) {
         if ((rc2 = C.structure.reserve(sbytes))) return rc2;
         if ((rc2 = C.h_struct.ensure(sbytes))) return rc2;
@@ -2061,41 +2114,6 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         ORB_HIP_TRY(hipGetLastError());
         have_structure = true;
         }
-        // system buffers
-        const size_t spart_n = (size_t)(SB_SPLIT + 1) * (glob ? 36 * (size_t)nblk : (size_t)D * D);   // + Hpp part
-        const size_t ybytes = carve_size<double>(72 * (size_t)Ea) + carve_size<double>(24 * (size_t)Ea) +
-                              carve_size<double>(9 * (size_t)nl) * 2 + carve_size<double>(3 * (size_t)nl) +
-                              carve_size<double>(36 * (size_t)np) + carve_size<double>(6 * (size_t)np) +
-                              carve_size<double>((size_t)D * D) + carve_size<double>(spart_n) +
-                              carve_size<unsigned>((size_t)nblk) + carve_size<double>(D) +
-                              carve_size<double>(D + 3 * (size_t)nl) + carve_size<double>(std::max(Ea, nl)) +
-                              carve_size<double>(nl + np) + (glob ? carve_size<double>((size_t)Dp * (Dp + 1)) : 0) +
-                              carve_size<double>(2 * (size_t)((nl * 8 + 63) / 64)) +
-                              64;
-        if ((rc2 = C.sys.reserve(ybytes))) return rc2;
-        Carve cy{C.sys.as<char>()};
-        b.J = cy.take<double>(72 * (size_t)Ea);
-        b.W = cy.take<double>(24 * (size_t)Ea);
-        b.Hll = cy.take<double>(9 * (size_t)nl);
-        b.Dinv = cy.take<double>(9 * (size_t)nl);
-        b.bl = cy.take<double>(3 * (size_t)nl);
-        b.Hpp = cy.take<double>(36 * (size_t)np);
-        b.bp = cy.take<double>(6 * (size_t)np);
-        b.S = cy.take<double>((size_t)D * D);
-        b.Spart = cy.take<double>(spart_n);
-        b.blk_done = cy.take<unsigned>((size_t)nblk);
-        b.bs = cy.take<double>(D);
-        b.x = cy.take<double>(D + 3 * (size_t)nl);
-        b.rchi = cy.take<double>(std::max(Ea, nl));
-        b.part = cy.take<double>(nl + np);
-        b.Sg = glob ? cy.take<double>((size_t)Dp * (Dp + 1)) : nullptr;
-        double* d_wgpart = cy.take<double>(2 * (size_t)((nl * 8 + 63) / 64));   // point-update workgroup partials
-        // (J needs no clearing: every linearising trial writes the entries that are read -- those of the
-        // edges to free poses, zeros for a level-1 edge.  S / the part matrices are zero where no pose
-        // pair block is, and the second optimize() keeps the structure, so they are cleared once.)
-        if (fresh && ((rc2 = glob ? fills.add(b.S, (size_t)D * D * 8, 0, st) : fills.add(b.Spart, spart_n * 8, 0, st)) ||
-                      (rc2 = fills.add(b.blk_done, (size_t)nblk * 4, 0, st))))
-            return rc2;
         if ((rc2 = fills.flush(st))) return rc2;
         const size_t ldlt_lds = glob ? (size_t)3 * Dp * 8 : std::max<size_t>(solve_lds_doubles(D) * 8, 16);
         {   // the dynamic LDS limit is a process-wide attribute of the kernel: raised (a host call) only
@@ -2117,8 +2135,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         mark("structure upload enqueued");
         constexpr int LOOKAHEAD = 2;
         const int first_seq = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;   // step 0's id (slot 0)
-        hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, iters, have_classified ? 1 : 0,
-                           C.d_ring + 0, first_seq);
+        if (!fresh)   // (the first optimize()'s control block came with the fill launch)
+            hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, iters, have_classified ? 1 : 0,
+                               C.d_ring + 0, first_seq);
         const int max_steps = iters * 10;
         int enq = 0, seen = 0;
         int ids[LOOKAHEAD] = {0, 0};

@@ -17,7 +17,7 @@ def _need(arrays: dict, counts: dict, what: str):
     """Refuse arrays with fewer elements than the C-ABI reads from them (it has no bound of its own)."""
     for name, want in counts.items():
         a = arrays[name]
-        n = int(a.numel()) if hasattr(a, "numel") else int(np.size(a))
+        n = a.size if isinstance(a, np.ndarray) else int(a.numel()) if hasattr(a, "numel") else int(np.size(a))
         if n < want:
             raise ValueError(f"{what}: {name} has {n} elements, needs {want}")
 
@@ -39,8 +39,9 @@ def LocalBundleAdjustment(problem: dict, stop_flag=None, device: int = 0) -> dic
                    k(problem["edge_obs"], np.float64), k(problem["edge_inv_sigma2"], np.float64),
                    k(problem["edge_cam"], np.float64))
     P, N, E = pr.n_poses, pr.n_points, pr.n_edges
-    out = dict(pose_R=np.zeros((P, 9)), pose_t=np.zeros((P, 3)), pose_q=np.zeros((P, 4)), points=np.zeros((N, 3)),
-               edge_outlier=np.zeros(E, np.uint8), edge_chi2=np.zeros(E))
+    # (np.empty: orbba_local_ba writes every element of each, also when it optimises nothing)
+    out = dict(pose_R=np.empty((P, 9)), pose_t=np.empty((P, 3)), pose_q=np.empty((P, 4)), points=np.empty((N, 3)),
+               edge_outlier=np.empty(E, np.uint8), edge_chi2=np.empty(E))
     res = BAResult(ptr(out["pose_R"]), ptr(out["pose_t"]), ptr(out["pose_q"]), ptr(out["points"]),
                    ptr(out["edge_outlier"]), ptr(out["edge_chi2"]))
     sf = None
