@@ -1547,8 +1547,11 @@ __global__ void ba_ctl_stop_kernel(BADev b) { b.ctl->done = 1; }
 
 // With rq / rt / rX (the final call) it also gathers the poses and points into the result region,
 // so the results come back in one copy.
+// only_if_done: the final gather enqueued speculatively behind the LM step the host expects to be the
+// last; it does nothing unless the loop has ended by then (the host then enqueues another).
 __global__ void ba_classify_kernel(BADev b, uint8_t* outlier, double* chi2o, uint8_t* level, int set_level,
-                                   double* rq, double* rt, double* rX) {
+                                   double* rq, double* rt, double* rX, int only_if_done) {
+    if (only_if_done && !b.ctl->done) return;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (rq && e < b.P) {
         for (int j = 0; j < 4; j++) rq[4 * e + j] = b.q[4 * e + j];
@@ -1947,6 +1950,27 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     mark("staging + upload enqueued");
     std::vector<uint8_t> level(E, 0);
     bool hook_stopped = false;   // the device ended a loop on the stop flag (or the test hook)
+    // the final classification + poses / points, gathered straight into the mapped pinned result region
+    // (round 6: no device-to-host copy behind the kernel); `gather` enqueues it
+    Carve dres{C.h_res.dptr};
+    double* rq = dres.take<double>(4 * (size_t)P);
+    double* rt = dres.take<double>(3 * (size_t)P);
+    double* rX = dres.take<double>(3 * (size_t)N);
+    uint8_t* ro = dres.take<uint8_t>(E);
+    double* rch = dres.take<double>(E);
+    const int n_gather = std::max(E, std::max(N, P));
+    auto gather = [&](int only_if_done) {
+        hipLaunchKernelGGL(ba_classify_kernel, dim3((n_gather + 255) / 256), dim3(256), 0, st, b, ro,
+                           res->edge_chi2 ? rch : (double*)nullptr, (uint8_t*)nullptr, 0, rq, rt, rX, only_if_done);
+    };
+    bool gathered = false;   // a speculative gather ran behind the step that ended the last loop
+    // the outlier classification between the loops (Optimizer.cc:644-670): levels + robust kernels off
+    auto classify_levels = [&](int only_if_done) {
+        hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, (uint8_t*)nullptr,
+                           (double*)nullptr, d_level, 1, (double*)nullptr, (double*)nullptr, (double*)nullptr,
+                           only_if_done);
+    };
+    bool leveled = false;   // likewise for the classification after the first loop
     // ------------------------------------------------------------------ one optimize(iters)
     // The structure is built once, for the first optimize() (every edge at level 0).  The second
     // optimize() (initializeOptimization(0) after the outliers went to level 1) reuses it: its active
@@ -1955,7 +1979,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     // keeps a zero Hessian block (+ lambda), i.e. a zero update, as if it were not in the problem.
     bool have_structure = false;
     bool have_classified = false;   // the outlier classification ran (second optimize())
-    auto optimize = [&](int iters, int32_t* iters_out, double* chi_out) -> int {
+    auto optimize = [&](int iters, int32_t* iters_out, double* chi_out, bool last_loop) -> int {
         bool dev_build = false;   // act / pt_slot / ps_slot / blk_pair filled on the device
         const bool fresh = !have_structure;   // the first optimize() of the call
         if (!have_structure) {
@@ -2140,6 +2164,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                                C.d_ring + 0, first_seq);
         const int max_steps = iters * 10;
         int enq = 0, seen = 0;
+        int spec_at = 0;   // steps enqueued ahead of the latest speculative gather
         int ids[LOOKAHEAD] = {0, 0};
         bool fin = false, stop_sent = false;
         BACtl last{};
@@ -2168,6 +2193,17 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                                    (const double*)d_wgpart, (int)gg.x);
                 ORB_HIP_TRY(hipGetLastError());
                 enq++;
+            }
+            // the call's last loop: once the steps in flight are all that can be needed (no retry),
+            // the final gather goes right behind them, guarded on `done` -- the GPU need not wait for
+            // the host to see the last snapshot (round 6: ~15 us per call)
+            // (the first loop: the classification, which leaves the control block as it is, so steps
+            // enqueued after it still run as the first loop's; loop 2's ctl_start stays host-driven)
+            if ((last_loop ? n_gather : E) && enq > spec_at && !stop_sent &&
+                enq - seen >= (seen ? last.iters_max - last.it : iters)) {
+                if (last_loop) gather(1);
+                else classify_levels(1);
+                spec_at = enq;
             }
             if (seen == enq || stop_sent) break;
             const int slot = seen % LOOKAHEAD;
@@ -2202,7 +2238,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             ORB_HIP_TRY(hipMemcpy(&last, b.ctl, sizeof(BACtl), hipMemcpyDeviceToHost));
         }
         // else: `last` is the final snapshot; the steps still queued return at once, stream-ordered
-        // before anything the caller enqueues next
+        // before anything the caller enqueues next.  The step that ended the loop is step `seen` - 1:
+        // a speculative gather enqueued after it ran on the final state.
+        if (fin && seen <= spec_at) (last_loop ? gathered : leveled) = true;
         *iters_out = last.iters_done;
         *chi_out = last.chi_out;
         hook_stopped = hook_stopped || last.stopped;
@@ -2212,38 +2250,29 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     const bool run = !stopped() && stop_after != 0;   // Optimizer.cc:633-634: stop before optimising => nothing done
     res->ran = run ? 1 : 0;
     if (run) {
-        if ((rc = optimize(5, &res->iterations[0], &res->chi2[0]))) return rc;
+        if ((rc = optimize(5, &res->iterations[0], &res->chi2[0], false))) return rc;
         if (!stopped() && !hook_stopped) {   // doMore (:639-642)
             // tag outliers (level 1) and drop the robust kernels (:644-670)
             // (no host copy of the levels: the structure is not rebuilt and the device counts the
             // level-0 edges for ba_ctl_start_kernel)
             if (E) {
-                hipLaunchKernelGGL(ba_classify_kernel, dim3((E + 255) / 256), dim3(256), 0, st, b, (uint8_t*)nullptr,
-                                   (double*)nullptr, d_level, 1, (double*)nullptr, (double*)nullptr, (double*)nullptr);
+                if (!leveled) classify_levels(0);
                 ORB_HIP_TRY(hipGetLastError());
                 have_classified = true;
             }
             mark("classify enqueued");
-            if ((rc = optimize(10, &res->iterations[1], &res->chi2[1]))) return rc;
+            if ((rc = optimize(10, &res->iterations[1], &res->chi2[1], true))) return rc;
         }
     }
-    // final classification + poses / points gathered straight into the mapped pinned result region
-    // (round 6: no device-to-host copy behind the kernel)
-    Carve dres{C.h_res.dptr}, hres{C.h_res.ptr};
-    double* rq = dres.take<double>(4 * (size_t)P);
-    double* rt = dres.take<double>(3 * (size_t)P);
-    double* rX = dres.take<double>(3 * (size_t)N);
-    uint8_t* ro = dres.take<uint8_t>(E);
-    double* rch = dres.take<double>(E);
+    Carve hres{C.h_res.ptr};
     double* hq = hres.take<double>(4 * (size_t)P);
     double* ht = hres.take<double>(3 * (size_t)P);
     double* hX = hres.take<double>(3 * (size_t)N);
     uint8_t* ho = hres.take<uint8_t>(E);
     double* hc = hres.take<double>(E);
     if ((rc = fills.flush(st))) return rc;   // (a call that optimised nothing still classifies)
-    if (const int nt = std::max(E, std::max(N, P))) {
-        hipLaunchKernelGGL(ba_classify_kernel, dim3((nt + 255) / 256), dim3(256), 0, st, b, ro,
-                           res->edge_chi2 ? rch : (double*)nullptr, (uint8_t*)nullptr, 0, rq, rt, rX);
+    if (n_gather && !gathered) {
+        gather(0);
         ORB_HIP_TRY(hipGetLastError());
     }
     ORB_HIP_TRY(hipStreamSynchronize(st));
