@@ -1523,8 +1523,11 @@ __device__ __forceinline__ void snapshot_to_host(const BACtl& snap, int seq, BAC
 // (initializeOptimization(0) finds no active edge); the loop ends here and the snapshot the host waits
 // for as step 0's (`seq` in ring slot `host_snap`) is written by this kernel, so the host never needs the
 // classification on its side.
-__global__ void ba_ctl_start_kernel(BADev b, int iters, int check_active, BACtl* host_snap, int seq) {
+// only_if_done: enqueued speculatively behind the first loop (after its guarded classification); it
+// starts the second loop only if the first has ended by then.
+__global__ void ba_ctl_start_kernel(BADev b, int iters, int check_active, BACtl* host_snap, int seq, int only_if_done) {
     BACtl* c = b.ctl;
+    if (only_if_done && !c->done) return;
     c->it = 0;
     c->q = 0;
     c->nbad = 0;
@@ -1971,6 +1974,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                            only_if_done);
     };
     bool leveled = false;   // likewise for the classification after the first loop
+    bool started_ahead = false;   // ... and the second loop's ctl_start
+    constexpr int next_iters = 10;   // the second optimize()'s iterations (Optimizer.cc:672)
     // ------------------------------------------------------------------ one optimize(iters)
     // The structure is built once, for the first optimize() (every edge at level 0).  The second
     // optimize() (initializeOptimization(0) after the outliers went to level 1) reuses it: its active
@@ -2159,12 +2164,14 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         mark("structure upload enqueued");
         constexpr int LOOKAHEAD = 2;
         const int first_seq = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;   // step 0's id (slot 0)
-        if (!fresh)   // (the first optimize()'s control block came with the fill launch)
+        if (!fresh && !started_ahead)   // (the first optimize()'s control block came with the fill launch; the
+                                         // second's ctl_start may have been enqueued behind the first loop)
             hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, iters, have_classified ? 1 : 0,
-                               C.d_ring + 0, first_seq);
+                               C.d_ring + 0, first_seq, 0);
         const int max_steps = iters * 10;
         int enq = 0, seen = 0;
-        int spec_at = 0;   // steps enqueued ahead of the latest speculative gather
+        int spec_at = 0;   // steps enqueued ahead of the latest speculative gather / classification
+        bool trans_spec = false;   // the second loop's ctl_start is enqueued behind the first loop's steps
         int ids[LOOKAHEAD] = {0, 0};
         bool fin = false, stop_sent = false;
         BACtl last{};
@@ -2174,7 +2181,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             // only if one of those turns out a retry (round 6: the call used to end behind up to
             // LOOKAHEAD no-op trials of 5 launches each)
             const int remaining = seen ? last.iters_max - last.it : iters;
-            while (enq < max_steps && enq - seen < LOOKAHEAD && enq - seen < remaining) {
+            while (enq < max_steps && enq - seen < LOOKAHEAD && enq - seen < remaining && !(trans_spec && seen < spec_at)) {
                 hipLaunchKernelGGL(ba_iter_kernel, gg, dim3(64), 0, st, b);
                 if (enq == 0) {   // first trial: computeLambdaInit needs Hpp before the Schur step
                     hipLaunchKernelGGL(ba_pose_accum_kernel, dim3(np + 1), dim3(1024), 0, st, b);
@@ -2199,10 +2206,23 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             // the host to see the last snapshot (round 6: ~15 us per call)
             // (the first loop: the classification, which leaves the control block as it is, so steps
             // enqueued after it still run as the first loop's; loop 2's ctl_start stays host-driven)
+            // Without a stop flag or test hook, the first loop also gets the second's ctl_start behind
+            // its classification: then no step of the first loop is enqueued after them until every
+            // step before them has reported (trans_spec), since a step run after a ctl_start that did
+            // start the second loop would be taken for the second loop's.
             if ((last_loop ? n_gather : E) && enq > spec_at && !stop_sent &&
                 enq - seen >= (seen ? last.iters_max - last.it : iters)) {
-                if (last_loop) gather(1);
-                else classify_levels(1);
+                if (last_loop) {
+                    gather(1);
+                } else {
+                    classify_levels(1);
+                    if (!stop_flag && stop_after < 0) {
+                        const int seq2 = C.step_seq == 0x7fffffff ? 1 : C.step_seq + 1;   // the second loop's step 0
+                        hipLaunchKernelGGL(ba_ctl_start_kernel, dim3(1), dim3(1), 0, st, b, next_iters, 1, C.d_ring + 0,
+                                           seq2, 1);
+                        trans_spec = true;
+                    }
+                }
                 spec_at = enq;
             }
             if (seen == enq || stop_sent) break;
@@ -2227,6 +2247,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             last = C.h_ring[slot];
             seen++;
             fin = last.done != 0;
+            if (trans_spec && !fin && seen == spec_at) trans_spec = false;   // it did nothing: go on
             if (!fin && stopped() && !stop_sent) {   // force stop: end the loop after the steps in flight
                 hipLaunchKernelGGL(ba_ctl_stop_kernel, dim3(1), dim3(1), 0, st, b);
                 stop_sent = true;
@@ -2240,7 +2261,10 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         // else: `last` is the final snapshot; the steps still queued return at once, stream-ordered
         // before anything the caller enqueues next.  The step that ended the loop is step `seen` - 1:
         // a speculative gather enqueued after it ran on the final state.
-        if (fin && seen <= spec_at) (last_loop ? gathered : leveled) = true;
+        if (fin && seen <= spec_at) {
+            (last_loop ? gathered : leveled) = true;
+            if (trans_spec) started_ahead = true;
+        }
         *iters_out = last.iters_done;
         *chi_out = last.chi_out;
         hook_stopped = hook_stopped || last.stopped;
@@ -2261,7 +2285,7 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
                 have_classified = true;
             }
             mark("classify enqueued");
-            if ((rc = optimize(10, &res->iterations[1], &res->chi2[1], true))) return rc;
+            if ((rc = optimize(next_iters, &res->iterations[1], &res->chi2[1], true))) return rc;
         }
     }
     Carve hres{C.h_res.ptr};
