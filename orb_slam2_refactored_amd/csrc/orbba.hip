@@ -1846,7 +1846,11 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     if (try_counts && E >= 1024) {
         HostStructure* hsp = &hs;   // (the helper's own thread_local hs is another object)
         C.helper.post([hsp, &counts_ok, P, N, E, pr] {
-            counts_ok = build_structure_counts(P, N, pr->pose_fixed, pr->edge_point, pr->edge_pose, E, *hsp);
+            try {   // (an exception must not leave the helper thread: the calling thread's build takes over)
+                counts_ok = build_structure_counts(P, N, pr->pose_fixed, pr->edge_point, pr->edge_pose, E, *hsp);
+            } catch (...) {
+                counts_ok = false;
+            }
         });
         helper_wait.on = true;
     }
