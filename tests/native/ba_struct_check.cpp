@@ -66,7 +66,20 @@ int main(int argc, char** argv) {
             for (int i : poses) { ep.push_back(l); ek.push_back(i); }
         }
         if (ep.size() < 2) continue;
-        if (mode == 8) std::swap(ep[0], ep[ep.size() - 1]), std::swap(ek[0], ek[ek.size() - 1]);
+        if (mode == 8) {
+            if (t % 20 == 8) {   // the ends swapped
+                std::swap(ep[0], ep[ep.size() - 1]), std::swap(ek[0], ek[ek.size() - 1]);
+            } else {   // the whole edge list shuffled: far more point runs than points (the build's
+                       // scratch slots must hold them; the test is also built with ASan)
+                std::vector<size_t> ord(ep.size());
+                for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
+                std::shuffle(ord.begin(), ord.end(), rng);
+                std::vector<int> ep2(ep.size()), ek2(ek.size());
+                for (size_t i = 0; i < ord.size(); i++) ep2[i] = ep[ord[i]], ek2[i] = ek[ord[i]];
+                ep.swap(ep2);
+                ek.swap(ek2);
+            }
+        }
         if (mode == 9) { ep.insert(ep.begin() + 1, ep[0]); ek.insert(ek.begin() + 1, ek[0]); }
         const int E = (int)ep.size();
         HostStructure d;
