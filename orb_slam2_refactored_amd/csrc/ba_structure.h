@@ -35,10 +35,13 @@ struct HostStructure {
 // caller then runs build_structure) when a precondition fails.
 inline bool build_structure_counts(int P, int N, const uint8_t* fixed, const int* ep, const int* ek, int E,
                                    HostStructure& s) {
-    // one pass over the edges: the sort check, the point runs and the poses that have edges
+    // One pass over the edges: the sort check, the point runs and the poses that have edges.  Branch-
+    // free: every edge stores its index and point into the slot of the run after the current one,
+    // which the next run's first edge (or the final pb[nl] = E) overwrites, so only a run's first
+    // edge leaves its values (points start every ~4 edges: a branch there mispredicted often).
     s.pa.assign(P, 0);
     s.hl.assign(N, -1);
-    s.pt_id.resize(N);
+    s.pt_id.resize((size_t)N + 1);
     s.pt_beg.resize((size_t)N + 1);
     int nl = 0;
     {
@@ -47,17 +50,19 @@ inline bool build_structure_counts(int P, int N, const uint8_t* fixed, const int
         int* pid = s.pt_id.data();
         int* pb = s.pt_beg.data();
         int prev = -1;
+        bool unsorted = false;
         for (int e = 0; e < E; e++) {
             const int x = ep[e];
-            if (x != prev) {
-                if (x < prev) return false;   // not point-sorted
-                hl[x] = nl;
-                pid[nl] = x;
-                pb[nl++] = e;
-                prev = x;
-            }
+            unsorted |= x < prev;
+            const int j = nl < N ? nl : N;   // unsorted input can start more than N runs (then refused
+            pb[j] = e;                       // below): slot N is scratch, so no store leaves the arrays
+            pid[j] = x;
+            nl += x != prev;
+            hl[x] = (nl < N ? nl : N) - 1;
+            prev = x;
             pa[ek[e]] = 1;
         }
+        if (unsorted) return false;   // not point-sorted
         pb[nl] = E;
     }
     s.pt_beg.resize((size_t)nl + 1);
@@ -83,16 +88,21 @@ inline bool build_structure_counts(int P, int N, const uint8_t* fixed, const int
         const int* pb = s.pt_beg.data();
         unsigned long long* col = s.col.data();
         int* qb = s.ps_beg.data();
-        for (int l = 0; l < nl; l++) {
+        // one flat pass over the edges (the point index follows the runs; no per-point inner loop)
+        (void)pb;
+        const int* epp = ep;
+        int l = -1, prev = -1;
+        for (int e = 0; e < E; e++) {
+            const int x = epp[e];
+            l += x != prev;
+            prev = x;
+            const int h = hp[ek[e]];
+            if (h < 0) continue;
+            unsigned long long& w = col[(size_t)h * W + (l >> 6)];
             const unsigned long long bit = 1ull << (l & 63);
-            for (int e = pb[l]; e < pb[l + 1]; e++) {
-                const int h = hp[ek[e]];
-                if (h < 0) continue;
-                unsigned long long& w = col[(size_t)h * W + (l >> 6)];
-                if (w & bit) return false;   // the point sees this free pose twice
-                w |= bit;
-                qb[h + 1]++;
-            }
+            if (w & bit) return false;   // the point sees this free pose twice
+            w |= bit;
+            qb[h + 1]++;
         }
         for (int i = 0; i < np; i++) qb[i + 1] += qb[i];
     }
