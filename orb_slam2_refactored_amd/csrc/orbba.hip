@@ -1979,6 +1979,13 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
     };
     bool leveled = false;   // likewise for the classification after the first loop
     bool started_ahead = false;   // ... and the second loop's ctl_start
+    int spec_launched[2] = {0, 0};   // speculative loop ends enqueued per loop (ORBBA_DEBUG_TIMING report)
+    // test hook (ORBBA_DEBUG_SPEC_EARLY=1, tests/test_ba_gpu.py): enqueue the loop ends one step too
+    // early, so that each loop's first guesses miss and the fallback paths run
+    const int spec_slack = [] {
+        const char* e = getenv("ORBBA_DEBUG_SPEC_EARLY");
+        return e && atoi(e) != 0 ? 1 : 0;
+    }();
     constexpr int next_iters = 10;   // the second optimize()'s iterations (Optimizer.cc:672)
     // ------------------------------------------------------------------ one optimize(iters)
     // The structure is built once, for the first optimize() (every edge at level 0).  The second
@@ -2215,7 +2222,8 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
             // step before them has reported (trans_spec), since a step run after a ctl_start that did
             // start the second loop would be taken for the second loop's.
             if ((last_loop ? n_gather : E) && enq > spec_at && !stop_sent &&
-                enq - seen >= (seen ? last.iters_max - last.it : iters)) {
+                enq - seen >= (seen ? last.iters_max - last.it : iters) - spec_slack) {
+                spec_launched[last_loop ? 1 : 0]++;
                 if (last_loop) {
                     gather(1);
                 } else {
@@ -2325,6 +2333,9 @@ extern "C" int orbba_local_ba(const orbba_problem* pr, orbba_result* res, const 
         std::vector<unsigned long long>().swap(hs.col);
     }
     mark("end");
+    if (tdbg)
+        fprintf(stderr, "orbba loop ends enqueued ahead: first loop %d (used %d, ctl_start %d), second %d (used %d)\n",
+                spec_launched[0], leveled ? 1 : 0, started_ahead ? 1 : 0, spec_launched[1], gathered ? 1 : 0);
     if (tdbg)
         for (size_t i = 1; i < marks.size(); i++)
             fprintf(stderr, "orbba %-28s %8.1f us\n", marks[i].first,

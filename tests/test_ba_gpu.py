@@ -168,3 +168,47 @@ def test_local_ba_all_outliers_then_normal(oracle):
     assert tuple(g["iterations"]) == tuple(o["iterations"]) and g["iterations"][1] == 0
     pr2 = make_ba_problem(3, n_kf=5, n_pts=200, n_fixed=1)
     compare(LocalBundleAdjustment(pr2), oracle.local_ba(pr2))
+
+
+# Problems whose loops run differently: heavy outlier fractions (more rejected LM trials, so retries
+# after the host's guess of the last step) and problems started at their ground truth.  Round 6
+# enqueues each loop's end (the outlier classification, the second loop's ctl_start, the final gather)
+# behind the step the host expects to be the last, guarded on `done`; a retry after that guess takes the
+# host-driven path (ORBBA_DEBUG_TIMING=1 prints the hits and misses).  Every case must match the oracle.
+# (These generators always run the full (5, 10) iterations: an early end needs residuals at rounding
+# level, where the GPU's and the oracle's accept/reject decisions would no longer be comparable.)
+_LOOP_END_CASES = [(20, 20, 3000, 2, 0.15, False), (21, 20, 3000, 2, 0.30, False), (22, 12, 1500, 0, 0.25, False),
+                   (23, 8, 600, 1, 0.20, False), (24, 20, 3000, 2, 0.03, True), (25, 6, 300, 0, 0.10, True),
+                   (26, 12, 1500, 1, 0.30, True), (27, 5, 120, 1, 0.0, True)]
+
+
+def _loop_end_problem(seed, kf, pts, fixed, outl, at_gt):
+    pr = make_ba_problem(seed, n_kf=kf, n_pts=pts, n_fixed=fixed, outlier_frac=outl)
+    if at_gt:   # start at the ground truth: only the measurement noise is left to fit
+        pr = dict(pr, pose_R=pr["gt_R"].copy(), pose_t=pr["gt_t"].copy(), points=pr["gt_points"].copy())
+    return pr
+
+
+@pytest.mark.parametrize("seed,kf,pts,fixed,outl,at_gt", _LOOP_END_CASES)
+def test_local_ba_loop_end_variants(oracle, seed, kf, pts, fixed, outl, at_gt):
+    pr = _loop_end_problem(seed, kf, pts, fixed, outl, at_gt)
+    g = LocalBundleAdjustment(pr)
+    o = oracle.local_ba(pr)
+    compare(g, o)
+
+
+@pytest.mark.parametrize("case", [_LOOP_END_CASES[0], _LOOP_END_CASES[1], _LOOP_END_CASES[3], _LOOP_END_CASES[5]])
+def test_local_ba_loop_end_guess_misses(oracle, case, monkeypatch):
+    """The loop ends enqueued one step too early (ORBBA_DEBUG_SPEC_EARLY): each loop's first guarded
+    classification / ctl_start / gather does nothing, the host holds back further first-loop steps until
+    the steps before them have reported, then goes on and enqueues the loop end again.  Same results."""
+    monkeypatch.setenv("ORBBA_DEBUG_SPEC_EARLY", "1")
+    pr = _loop_end_problem(*case)
+    g = LocalBundleAdjustment(pr)
+    o = oracle.local_ba(pr)
+    compare(g, o)
+    monkeypatch.delenv("ORBBA_DEBUG_SPEC_EARLY")
+    g2 = LocalBundleAdjustment(pr)
+    for k in ("pose_R", "pose_t", "points", "edge_outlier", "edge_chi2"):
+        assert np.array_equal(g[k], g2[k]), k
+
